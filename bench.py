@@ -1,0 +1,219 @@
+"""Headline benchmark: edges/s of the bipartite SpMM in GCN_FC (hid=1024,
+depth=3) training steps on MI355X, with the HBM-roofline fraction of the
+SpMM kernel and the oracle CPU path timed beside it.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A step = one GCN_FC(8, 8, hids=1024, depth=3) training iteration of
+train.py:117-129 on the synthetic c2 graph (100K cons x 200K vars, nnz 2M,
+BASELINE.json configs[1]): forward (2 SpMM at F=8 + 2 at F=1024, FC stacks,
+heads, add_knowledge), balanced loss, backward (2 SpMM at F=1024 + FC
+grads), Adam step.  value = (hid-width SpMM edge traversals in the step) /
+step time, whole job.  N>1: one process per GPU (torchrun), each owning a
+c2-sized constraint-row partition of an N-times larger graph (see
+lpgnn.partition); boundary-variable rows are all-reduced over RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "lp-gnn_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--m", type=int, default=100_000)
+    ap.add_argument("--n", type=int, default=200_000)
+    ap.add_argument("--nnz", type=int, default=2_000_000)
+    ap.add_argument("--hids", type=int, default=1024)
+    ap.add_argument("--depth", type=int, default=3)
+    ap.add_argument("--rho", type=float, default=0.02, help="boundary edge fraction for N>1 partitions")
+    ap.add_argument("--cpu-steps", type=int, default=1, help="oracle CPU steps for cpu_baseline (0 = skip)")
+    ap.add_argument("--profile-only", action="store_true", help="no CPU baseline, no JSON extras (rocprof runs)")
+    return ap.parse_args()
+
+
+def spmm_bytes(n_rows: int, nnz: int, F: int, s: int = 4) -> int:
+    """Edge-gather algorithmic bytes of one SpMM launch:
+    every edge gathers one F-wide source row, col (int32) + val (f32) read
+    once, rowptr (int64) once, output row written once."""
+    return nnz * F * s + nnz * 8 + (n_rows + 1) * 8 + n_rows * F * s
+
+
+def load_pmc_traffic(workload: str):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
+    PMC summary (profiles/*pmc*.json, produced by tools/pmc_summary.py)."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            return d["hbm_bytes_per_launch"], os.path.basename(path)
+    return None, None
+
+
+def cpu_baseline(g, hids, depth, steps):
+    """The oracle (C restatement of torch_sparse spmm_cpu + torch CPU GEMMs)
+    timed on this host for `steps` full fwd+bwd steps of the same workload."""
+    from oracle import model_ref as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = min(threads, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
+    AT = O.csr_transpose(*A, g.m, g.n)
+    sd = {k: v.clone().requires_grad_(True) for k, v in O.init_state_dict(8, 8, hids, depth).items()}
+    x_s, x_t = torch.from_numpy(g.x_s), torch.from_numpy(g.x_t)
+    y_s, y_t = torch.from_numpy(g.y_s), torch.from_numpy(g.y_t)
+    opt = torch.optim.Adam(list(sd.values()), lr=1e-3, weight_decay=5e-4)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        lc, lv = O.gcn_fc_forward(sd, x_s, x_t, A, AT, depth)
+        loss = O.balanced(lc, lv, y_s, y_t)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    dt = (time.perf_counter() - t0) / steps
+    return dt, threads
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    import lpgnn
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.timing import TIMER
+    from lpgnn.train import make_optimizer, train_step
+
+    if world == 1:
+        g = synth.uniform_lp(args.m, args.n, args.nnz, seed=0)
+        adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
+        batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(dev), x_t=torch.from_numpy(g.x_t).to(dev),
+                               y_s=torch.from_numpy(g.y_s).to(dev), y_t=torch.from_numpy(g.y_t).to(dev),
+                               edge_index=adj, s_bs=g.m, t_bs=g.n)
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=args.hids, depth=args.depth).to(dev)
+        opt, _ = make_optimizer(model)
+        step = lambda: train_step(model, batch, opt)
+        local_nnz = g.nnz
+        workload = f"c2: synthetic LP {args.m}x{args.n} nnz={args.nnz}, GCN_FC(8,8,hids={args.hids},depth={args.depth}) fwd+bwd+Adam"
+        parallelism = "single"
+    else:
+        from lpgnn import partition
+
+        job = partition.build_bench_job(args, rank, world, dev)
+        step, local_nnz, g = job.step, job.local_nnz, None
+        workload = job.workload
+        parallelism = f"rowpart{world}"
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    TIMER.reset()
+    TIMER.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    dt = time.perf_counter() - t0
+    TIMER.enabled = False
+    kern = TIMER.summary()
+
+    # hid-width SpMM launches (the metric's kernel) measured on their stream
+    hid_keys = [k for k in kern if k[0] == "spmm" and k[3] == args.hids]
+    launches = sum(kern[k][0] for k in hid_keys)
+    spmm_ms = sum(kern[k][1] for k in hid_keys)
+    nnz_of = lambda k: local_nnz  # every launch traverses the local graph's edges once
+    bytes_total = sum(kern[k][0] * spmm_bytes(k[1], nnz_of(k), k[3]) for k in hid_keys)
+    edges_local = launches * local_nnz / args.steps  # per step
+    t = torch.tensor([dt], device=dev)
+    e = torch.tensor([edges_local], device=dev, dtype=torch.float64)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+    dt_max = t.item()
+    value = e.item() * args.steps / dt_max
+
+    achieved = bytes_total / (spmm_ms / 1e3) / 1e9 if spmm_ms > 0 else 0.0
+    per_launch_bytes = bytes_total / max(launches, 1)
+    traffic, traffic_src = load_pmc_traffic(workload)
+    out = {
+        "metric": "edges/sec bipartite SpMM (hid=1024, depth=3) at 1/2/4/8 MI355X; % HBM roofline",
+        "value": value,
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded uniform LP graph, LP feature layout; random-init GCN_FC weights)",
+        "config": {"workload": workload, "n_cons": args.m * world, "n_vars": args.n * world,
+                   "nnz": args.nnz * world, "hid": args.hids, "depth": args.depth, "parallelism": parallelism},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "lpg spmm_f32_rowwave (F=hid, both directions, fwd+bwd)",
+                     "bytes_per_launch": per_launch_bytes,
+                     "avg_launch_ms": spmm_ms / max(launches, 1), "launches": launches,
+                     "traffic_source": traffic_src},
+        "spmm_edges_per_s_kernel": launches * local_nnz / (spmm_ms / 1e3) if spmm_ms > 0 else None,
+        "spmm_ms_per_step": spmm_ms / args.steps,
+        "kernels": {f"{k[0]}[{k[1]}x{k[2]},F={k[3]},{k[4]}]": {"launches": v[0], "ms": v[1]}
+                    for k, v in sorted(kern.items())},
+        "library": lpgnn.library_path(),
+    }
+    if rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None:
+        cdt, threads = cpu_baseline(g, args.hids, args.depth, args.cpu_steps)
+        out["cpu_baseline"] = {"value": edges_local / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
+                               "sample": f"{args.cpu_steps} full fwd+bwd+Adam step(s) of the same c2 workload: "
+                                         f"oracle C spmm_cpu loop (OpenMP) + torch CPU GEMMs, "
+                                         f"{cdt:.2f} s/step",
+                               "s_per_step": cdt}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,113 @@
+/*
+ * lpgnn.h — C ABI of liblpgnn_hip.so, the MI355X (gfx950) hot path of the
+ * LP basis-prediction GNN (vbdai/lp-gnn, GCN_FC).
+ *
+ * The library replaces the native op the reference reaches through PyG:
+ *
+ *   arch.py:75-80  GraphConv(...)(x, adj_t)            (PyG 2.1 GraphConv, aggr='add')
+ *     -> torch_sparse.matmul(adj_t, x[0], reduce='add')  (torch_sparse 0.6.12 matmul.py)
+ *     -> torch.ops.torch_sparse.spmm_sum(row, rowptr, col, value, colptr, csr2csc, mat)
+ *        (torch_sparse 0.6.12 csrc/spmm.cpp SPMMSum; CPU csrc/cpu/spmm_cpu.cpp)
+ *
+ * and the COO->CSR / CSR->CSC conversions of the batch boundary:
+ *
+ *   dataset.py:301-304  SparseTensor.from_edge_index(edge_index_l2r, edge_attr, (ncons, nvars))
+ *   arch.py:71          edge_index.t()   (csr2csc permutation, every layer)
+ *
+ * Conventions (all entry points):
+ *   - plain C types only; every buffer is caller-owned; device pointers are
+ *     hipMalloc'd (or torch) memory on the current device; the library never
+ *     allocates on the hot path.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream); all
+ *     device work is stream-ordered and the calls are re-entrant.
+ *   - return value: LPG_OK or an error code; lpg_last_error() gives a
+ *     thread-local message (the C analogue of TORCH_CHECK's RuntimeError).
+ *   - determinism: no atomics on any floating-point path; results are
+ *     bitwise identical run to run and equal to the sequential CPU loop of
+ *     torch_sparse spmm_cpu (per-row edge order, product rounded then added).
+ */
+#ifndef LPGNN_H
+#define LPGNN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t lpg_status;
+#define LPG_OK 0
+#define LPG_ERR_INVALID 1     /* bad argument / shape / alignment            */
+#define LPG_ERR_HIP 2         /* a HIP runtime call failed                     */
+#define LPG_ERR_UNSUPPORTED 3 /* valid request this build does not implement   */
+
+/* One orientation of the bipartite adjacency, CSR with sorted columns.
+ * Row i of the destination side gathers rows col[rowptr[i]..rowptr[i+1]) of
+ * the source feature matrix, weighted by val[].  (torch_sparse SparseStorage:
+ * rowptr/col/value; rows = destination nodes of the message direction.) */
+typedef struct lpg_csr {
+  int64_t n_rows;         /* destination nodes                               */
+  int64_t n_cols;         /* source nodes (rows of X)                        */
+  int64_t nnz;            /* edges                                           */
+  const int64_t *rowptr;  /* [n_rows+1]                                      */
+  const int32_t *col;     /* [nnz], ascending within each row                */
+  const float *val;       /* [nnz], scaled A_ij (dataset.py:235-236)         */
+} lpg_csr;
+
+/* ---- errors / build info ------------------------------------------------ */
+const char *lpg_last_error(void);
+/* "gfx950" + build flags; never NULL. */
+const char *lpg_build_info(void);
+
+/* ---- dual-CSR pack (replaces from_edge_index + .t()) --------------------- */
+
+/* Host pack.  Input: COO edges of A (rows = constraints, cols = variables)
+ * as produced by MyToBipartite (dataset.py:296-304): int64 row/col, f32 val,
+ * any order, no duplicate (row, col) pairs.  Output (caller-allocated host
+ * buffers): CSR(A) [m rows] and CSR(A^T) [n rows], columns ascending within
+ * each row, i.e. torch_sparse's from_edge_index order and its csr2csc order
+ * (SparseTensor.t()).  Duplicates -> LPG_ERR_INVALID. */
+lpg_status lpg_csr_pack_host(const int64_t *row, const int64_t *col, const float *val,
+                             int64_t nnz, int64_t m, int64_t n,
+                             int64_t *a_rowptr, int32_t *a_col, float *a_val,
+                             int64_t *at_rowptr, int32_t *at_col, float *at_val);
+
+/* Device pack: same contract and bit-identical output, all pointers device
+ * memory, stream-ordered (no host sync).  `workspace` (16-byte aligned) must
+ * hold lpg_csr_pack_workspace_bytes(nnz, m, n) bytes.  Because validation
+ * cannot return through the status without a sync, the first 16 bytes of the
+ * workspace receive two int64 counters after the pack: [0] edges with an
+ * out-of-range index, [1] duplicate (row, col) pairs.  Non-zero => the
+ * output is undefined and the caller must report LPG_ERR_INVALID itself. */
+int64_t lpg_csr_pack_workspace_bytes(int64_t nnz, int64_t m, int64_t n);
+lpg_status lpg_csr_pack_f32(const int64_t *row, const int64_t *col, const float *val,
+                            int64_t nnz, int64_t m, int64_t n,
+                            int64_t *a_rowptr, int32_t *a_col, float *a_val,
+                            int64_t *at_rowptr, int32_t *at_col, float *at_val,
+                            void *workspace, void *stream);
+
+/* ---- SpMM (replaces torch_sparse spmm_sum, forward and backward) --------- */
+
+/* Y[i, 0:F] = sum_{e in row i} val[e] * X[col[e], 0:F]   (Y overwritten).
+ * X: [A->n_cols, >= F] row stride ldx floats; Y: [A->n_rows, >= F] stride ldy.
+ * fp32 storage and accumulation, sequential edge order per row.
+ * The backward of spmm(A, X) w.r.t. X is spmm(A^T, dY): call this entry on
+ * the other orientation (torch_sparse SPMMSum::backward). */
+lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx,
+                        float *Y, int64_t ldy, int64_t F, void *stream);
+
+/* Same, bf16 storage (uint16 bit patterns) with fp32 accumulation; the
+ * accumulated row is rounded to bf16 once (round-to-nearest-even). */
+lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
+                         uint16_t *Y, int64_t ldy, int64_t F, void *stream);
+
+/* Tuning knob for lpg_spmm_f32 (process-global, default 0 = auto):
+ * columns per slice of F processed by one wave (multiple of 256, or 0).
+ * Smaller slices keep the gathered source slice resident in the 256 MiB
+ * Infinity Cache; see DESIGN.md. */
+lpg_status lpg_spmm_set_slice(int64_t cols_per_slice);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LPGNN_H */

@@ -1,0 +1,385 @@
+// CSR SpMM for the bipartite cons<->var message passing of GCN_FC on gfx950.
+//
+// Replaces torch_sparse 0.6.12 `spmm_sum` (csrc/spmm.cpp SPMMSum, CPU loop in
+// csrc/cpu/spmm_cpu.cpp, CUDA spmm_kernel in csrc/cuda/spmm_cuda.cu), reached
+// from the reference through PyG GraphConv.message_and_aggregate at
+// arch.py:75-80 (both directions) and from SPMMSum::backward during
+// loss.backward() (train.py:128).
+//
+// Numerics: per output element the sum runs over the row's edges in CSR
+// order, acc = acc + (val * x) with the product rounded before the add
+// (this file is compiled with -ffp-contract=off and the pragma below), which
+// is exactly torch_sparse's CPU loop; the results are bitwise equal to it and
+// to oracle/spmm_ref.c.  No atomics anywhere.
+//
+// Mapping (CDNA4, wave64): one wave owns one destination row and a slice of
+// its columns.  In the fp32 wide kernel lane l holds columns
+// c0 + q*256 + 4l .. +3 for q < NV, so each source-row gather is NV fully
+// coalesced 1 KiB wave-instructions (global_load_dwordx4).  The row's
+// (col, val) pairs are fetched 64 at a time, one per lane, and broadcast with
+// v_readlane (wave-uniform -> the gather base is a scalar).  U edges are
+// gathered before any of them is accumulated, so U*NV 16-byte loads per lane
+// are in flight (4 rows in flight per wave at F = 1024).
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace lpg {
+namespace {
+
+constexpr int kBlock = 256;            // 4 waves
+constexpr int kWavesPerBlock = kBlock / 64;
+
+__device__ __forceinline__ int bcast_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ float bcast_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+__device__ __forceinline__ void axpy4(float4 &acc, float v, const float4 &x) {
+  acc.x = acc.x + v * x.x;
+  acc.y = acc.y + v * x.y;
+  acc.z = acc.z + v * x.z;
+  acc.w = acc.w + v * x.w;
+}
+
+// ---------------------------------------------------------------- fp32 wide
+template <int NV, int U, bool FULL>
+__global__ __launch_bounds__(kBlock) void spmm_f32_rowwave(
+    int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
+    float *__restrict__ Y, int64_t ldy, int64_t F) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (row >= n_rows) return;
+  const int64_t c0 = (int64_t)blockIdx.y * (NV * 256);
+
+  bool ok[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) ok[q] = FULL || (c0 + q * 256 + lane * 4 < F);
+
+  float4 acc[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  const float *Xs = X + c0 + lane * 4;
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  while (e < end) {
+    const int n = (int)(end - e < 64 ? end - e : 64);
+    int cl = 0;
+    float vl = 0.f;
+    if (lane < n) {
+      cl = col[e + lane];
+      vl = val[e + lane];
+    }
+    int j = 0;
+    for (; j + U <= n; j += U) {
+      float4 xv[U][NV];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const float *xr = Xs + (int64_t)bcast_i(cl, j + k) * ldx;
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+          xv[k][q] = ok[q] ? *reinterpret_cast<const float4 *>(xr + q * 256) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const float v = bcast_f(vl, j + k);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) axpy4(acc[q], v, xv[k][q]);
+      }
+    }
+    for (; j < n; ++j) {
+      const float *xr = Xs + (int64_t)bcast_i(cl, j) * ldx;
+      const float v = bcast_f(vl, j);
+      float4 xv[NV];
+#pragma unroll
+      for (int q = 0; q < NV; ++q)
+        xv[q] = ok[q] ? *reinterpret_cast<const float4 *>(xr + q * 256) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < NV; ++q) axpy4(acc[q], v, xv[q]);
+    }
+    e += n;
+  }
+
+  float *yr = Y + row * ldy + c0 + lane * 4;
+#pragma unroll
+  for (int q = 0; q < NV; ++q)
+    if (ok[q]) *reinterpret_cast<float4 *>(yr + q * 256) = acc[q];
+}
+
+// -------------------------------------------------------------- fp32 narrow
+// F <= FW <= 64: FW lanes per row, 256/FW rows per block (conv1, F = 8).
+template <int FW, int U>
+__global__ __launch_bounds__(kBlock) void spmm_f32_narrow(
+    int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
+    float *__restrict__ Y, int64_t ldy, int64_t F) {
+  constexpr int RPB = kBlock / FW;
+  const int sub = threadIdx.x % FW;
+  const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / FW;
+  if (row >= n_rows) return;
+  const bool active = sub < F;
+  const float *Xs = X + sub;
+  float acc = 0.f;
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  for (; e + U <= end; e += U) {
+    int c[U];
+    float v[U], x[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      c[k] = col[e + k];
+      v[k] = val[e + k];
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) x[k] = active ? Xs[(int64_t)c[k] * ldx] : 0.f;
+#pragma unroll
+    for (int k = 0; k < U; ++k) acc = acc + v[k] * x[k];
+  }
+  for (; e < end; ++e) {
+    const float x = active ? Xs[(int64_t)col[e] * ldx] : 0.f;
+    acc = acc + val[e] * x;
+  }
+  if (active) Y[row * ldy + sub] = acc;
+}
+
+// ------------------------------------------------------------- fp32 generic
+// Any F / stride / alignment: one wave per row, lane strides the columns.
+__global__ __launch_bounds__(kBlock) void spmm_f32_generic(
+    int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
+    float *__restrict__ Y, int64_t ldy, int64_t F) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  const int64_t beg = rowptr[row], end = rowptr[row + 1];
+  for (int64_t c = lane; c < F; c += 64) {
+    float acc = 0.f;
+    for (int64_t e = beg; e < end; ++e) acc = acc + val[e] * X[(int64_t)col[e] * ldx + c];
+    Y[row * ldy + c] = acc;
+  }
+}
+
+// ------------------------------------------------------------------ bf16
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+
+__device__ __forceinline__ uint32_t f32_to_bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x0040u;  // keep NaN a NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+__device__ __forceinline__ void axpy8_bf16(float (&acc)[8], float v, const uint4 &x) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    acc[2 * i] = acc[2 * i] + v * bf16_to_f32(w[i] & 0xffffu);
+    acc[2 * i + 1] = acc[2 * i + 1] + v * bf16_to_f32(w[i] >> 16);
+  }
+}
+
+// Lane l holds columns c0 + q*512 + 8l .. +7 (16 bytes) for q < NV.
+template <int NV, int U, bool FULL>
+__global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
+    int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
+    uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (row >= n_rows) return;
+  const int64_t c0 = (int64_t)blockIdx.y * (NV * 512);
+  bool ok[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) ok[q] = FULL || (c0 + q * 512 + lane * 8 < F);
+  float acc[NV][8];
+#pragma unroll
+  for (int q = 0; q < NV; ++q)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[q][i] = 0.f;
+
+  const uint16_t *Xs = X + c0 + lane * 8;
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  while (e < end) {
+    const int n = (int)(end - e < 64 ? end - e : 64);
+    int cl = 0;
+    float vl = 0.f;
+    if (lane < n) {
+      cl = col[e + lane];
+      vl = val[e + lane];
+    }
+    int j = 0;
+    for (; j + U <= n; j += U) {
+      uint4 xv[U][NV];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint16_t *xr = Xs + (int64_t)bcast_i(cl, j + k) * ldx;
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+          xv[k][q] = ok[q] ? *reinterpret_cast<const uint4 *>(xr + q * 512) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const float v = bcast_f(vl, j + k);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) axpy8_bf16(acc[q], v, xv[k][q]);
+      }
+    }
+    for (; j < n; ++j) {
+      const uint16_t *xr = Xs + (int64_t)bcast_i(cl, j) * ldx;
+      const float v = bcast_f(vl, j);
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        const uint4 xv = ok[q] ? *reinterpret_cast<const uint4 *>(xr + q * 512) : make_uint4(0, 0, 0, 0);
+        axpy8_bf16(acc[q], v, xv);
+      }
+    }
+    e += n;
+  }
+  uint16_t *yr = Y + row * ldy + c0 + lane * 8;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    if (!ok[q]) continue;
+    uint4 o;
+    o.x = f32_to_bf16_rne(acc[q][0]) | (f32_to_bf16_rne(acc[q][1]) << 16);
+    o.y = f32_to_bf16_rne(acc[q][2]) | (f32_to_bf16_rne(acc[q][3]) << 16);
+    o.z = f32_to_bf16_rne(acc[q][4]) | (f32_to_bf16_rne(acc[q][5]) << 16);
+    o.w = f32_to_bf16_rne(acc[q][6]) | (f32_to_bf16_rne(acc[q][7]) << 16);
+    *reinterpret_cast<uint4 *>(yr + q * 512) = o;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
+    int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
+    uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  const int64_t beg = rowptr[row], end = rowptr[row + 1];
+  for (int64_t c = lane; c < F; c += 64) {
+    float acc = 0.f;
+    for (int64_t e = beg; e < end; ++e) acc = acc + val[e] * bf16_to_f32(X[(int64_t)col[e] * ldx + c]);
+    Y[row * ldy + c] = (uint16_t)f32_to_bf16_rne(acc);
+  }
+}
+
+int64_t g_slice_cols = 0;  // lpg_spmm_set_slice; 0 = auto
+
+lpg_status check_csr(const lpg_csr *A) {
+  LPG_REQUIRE(A != nullptr, "lpg_spmm: A is NULL");
+  LPG_REQUIRE(A->n_rows >= 0 && A->n_cols >= 0 && A->nnz >= 0, "lpg_spmm: negative CSR size");
+  LPG_REQUIRE(A->n_rows == 0 || A->rowptr != nullptr, "lpg_spmm: rowptr is NULL");
+  LPG_REQUIRE(A->nnz == 0 || (A->col != nullptr && A->val != nullptr), "lpg_spmm: col/val is NULL");
+  LPG_REQUIRE(A->n_cols <= INT32_MAX, "lpg_spmm: n_cols exceeds int32 column index");
+  return LPG_OK;
+}
+
+template <class K, class... Args>
+lpg_status launch(K kernel, dim3 grid, hipStream_t s, Args... args) {
+  hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, args...);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+template <int NV, int U>
+lpg_status launch_wide_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                           int64_t F, hipStream_t s) {
+  const int64_t W = NV * 256;
+  const int64_t slices = (F + W - 1) / W;
+  dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock), (unsigned)slices);
+  if (F % W == 0)
+    return launch(spmm_f32_rowwave<NV, U, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
+                  Y, ldy, F);
+  return launch(spmm_f32_rowwave<NV, U, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y,
+                ldy, F);
+}
+
+template <int FW>
+lpg_status launch_narrow_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                             int64_t F, hipStream_t s) {
+  constexpr int RPB = kBlock / FW;
+  dim3 grid((unsigned)((A->n_rows + RPB - 1) / RPB));
+  return launch(spmm_f32_narrow<FW, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+}
+
+template <int NV, int U>
+lpg_status launch_wide_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
+                            int64_t F, hipStream_t s) {
+  const int64_t W = NV * 512;
+  const int64_t slices = (F + W - 1) / W;
+  dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock), (unsigned)slices);
+  if (F % W == 0)
+    return launch(spmm_bf16_rowwave<NV, U, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
+                  Y, ldy, F);
+  return launch(spmm_bf16_rowwave<NV, U, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
+                Y, ldy, F);
+}
+
+}  // namespace
+}  // namespace lpg
+
+using namespace lpg;
+
+extern "C" lpg_status lpg_spmm_set_slice(int64_t cols) {
+  LPG_REQUIRE(cols == 0 || cols == 256 || cols == 512 || cols == 1024,
+              "lpg_spmm_set_slice: cols must be 0 (auto), 256, 512 or 1024, got %lld", (long long)cols);
+  g_slice_cols = cols;
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                                   int64_t F, void *stream) {
+  lpg_status st = check_csr(A);
+  if (st != LPG_OK) return st;
+  LPG_REQUIRE(F >= 0, "lpg_spmm_f32: F < 0");
+  LPG_REQUIRE(ldx >= F && ldy >= F, "lpg_spmm_f32: ldx/ldy smaller than F");
+  if (A->n_rows == 0 || F == 0) return LPG_OK;
+  LPG_REQUIRE(Y != nullptr, "lpg_spmm_f32: Y is NULL");
+  LPG_REQUIRE(A->nnz == 0 || X != nullptr, "lpg_spmm_f32: X is NULL");
+  hipStream_t s = as_stream(stream);
+
+  if (F <= 64) {
+    if (F <= 1) return launch_narrow_f32<1>(A, X, ldx, Y, ldy, F, s);
+    if (F <= 2) return launch_narrow_f32<2>(A, X, ldx, Y, ldy, F, s);
+    if (F <= 4) return launch_narrow_f32<4>(A, X, ldx, Y, ldy, F, s);
+    if (F <= 8) return launch_narrow_f32<8>(A, X, ldx, Y, ldy, F, s);
+    if (F <= 16) return launch_narrow_f32<16>(A, X, ldx, Y, ldy, F, s);
+    if (F <= 32) return launch_narrow_f32<32>(A, X, ldx, Y, ldy, F, s);
+    return launch_narrow_f32<64>(A, X, ldx, Y, ldy, F, s);
+  }
+  const bool vec = (F % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && aligned16(X) && aligned16(Y);
+  if (!vec) {
+    dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+    return launch(spmm_f32_generic, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+  }
+  int64_t W = g_slice_cols;
+  if (W == 0) W = F <= 256 ? 256 : (F <= 512 ? 512 : 1024);
+  if (W == 256) return launch_wide_f32<1, 8>(A, X, ldx, Y, ldy, F, s);
+  if (W == 512) return launch_wide_f32<2, 8>(A, X, ldx, Y, ldy, F, s);
+  return launch_wide_f32<4, 4>(A, X, ldx, Y, ldy, F, s);
+}
+
+extern "C" lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,
+                                    int64_t ldy, int64_t F, void *stream) {
+  lpg_status st = check_csr(A);
+  if (st != LPG_OK) return st;
+  LPG_REQUIRE(F >= 0, "lpg_spmm_bf16: F < 0");
+  LPG_REQUIRE(ldx >= F && ldy >= F, "lpg_spmm_bf16: ldx/ldy smaller than F");
+  if (A->n_rows == 0 || F == 0) return LPG_OK;
+  LPG_REQUIRE(Y != nullptr, "lpg_spmm_bf16: Y is NULL");
+  LPG_REQUIRE(A->nnz == 0 || X != nullptr, "lpg_spmm_bf16: X is NULL");
+  hipStream_t s = as_stream(stream);
+  const bool vec = (F % 8 == 0) && (ldx % 8 == 0) && (ldy % 8 == 0) && aligned16(X) && aligned16(Y);
+  if (!vec || F < 256) {
+    dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+    return launch(spmm_bf16_generic, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+  }
+  if (F <= 512) return launch_wide_bf16<1, 8>(A, X, ldx, Y, ldy, F, s);
+  if (F <= 1024) return launch_wide_bf16<2, 8>(A, X, ldx, Y, ldy, F, s);
+  return launch_wide_bf16<4, 4>(A, X, ldx, Y, ldy, F, s);
+}

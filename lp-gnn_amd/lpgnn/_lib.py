@@ -1,0 +1,91 @@
+"""ctypes binding of liblpgnn_hip.so (C ABI: include/lpgnn.h).
+
+This is the same binding a maintainer would add on the reference side
+(INTEGRATION.md): plain pointers and sizes, the HIP stream as a void*, the
+status code turned into a RuntimeError carrying lpg_last_error() -- the
+behaviour of torch_sparse's TORCH_CHECK failures.
+
+There is no fallback: if the library is missing or fails to load, every
+entry point raises.  ``torch`` is imported first on purpose: its bundled
+libamdhip64.so (soname libamdhip64.so.7) is then the HIP runtime that the
+library's NEEDED entry resolves to, so there is one runtime per process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblpgnn_hip.so")
+HEADER_SYMBOLS = (
+    "lpg_last_error",
+    "lpg_build_info",
+    "lpg_csr_pack_host",
+    "lpg_csr_pack_workspace_bytes",
+    "lpg_csr_pack_f32",
+    "lpg_spmm_f32",
+    "lpg_spmm_bf16",
+    "lpg_spmm_set_slice",
+)
+
+c_i64, c_i32, c_p = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
+
+
+class LpgCsr(ctypes.Structure):
+    _fields_ = [("n_rows", c_i64), ("n_cols", c_i64), ("nnz", c_i64),
+                ("rowptr", c_p), ("col", c_p), ("val", c_p)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is not built; run `make -C lp-gnn_amd` or __graft_entry__.build(). "
+                           "There is no CPU fallback for the lpgnn hot path.")
+    L = ctypes.CDLL(LIB_PATH)
+    L.lpg_last_error.restype = ctypes.c_char_p
+    L.lpg_build_info.restype = ctypes.c_char_p
+    L.lpg_csr_pack_host.argtypes = [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_csr_pack_host.restype = c_i32
+    L.lpg_csr_pack_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
+    L.lpg_csr_pack_workspace_bytes.restype = c_i64
+    L.lpg_csr_pack_f32.argtypes = [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_csr_pack_f32.restype = c_i32
+    L.lpg_spmm_f32.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p]
+    L.lpg_spmm_f32.restype = c_i32
+    L.lpg_spmm_bf16.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p]
+    L.lpg_spmm_bf16.restype = c_i32
+    L.lpg_spmm_set_slice.argtypes = [c_i64]
+    L.lpg_spmm_set_slice.restype = c_i32
+    if hasattr(L, "lpg_fc_f32"):
+        L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
+                                 c_i32, c_p, c_p]
+        L.lpg_fc_f32.restype = c_i32
+        L.lpg_fc_workspace_bytes.argtypes = [c_i64, c_i64]
+        L.lpg_fc_workspace_bytes.restype = c_i64
+        L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p]
+        L.lpg_knowledge_f32.restype = c_i32
+    _lib = L
+    return L
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = lib().lpg_last_error().decode(errors="replace")
+        kind = {1: "invalid argument", 2: "HIP error", 3: "unsupported"}.get(status, f"status {status}")
+        raise RuntimeError(f"{what}: {kind}: {msg}")
+
+
+def ptr(t: "torch.Tensor | None") -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t: torch.Tensor) -> int:
+    """The torch current stream of t's device, as a raw hipStream_t."""
+    return torch.cuda.current_stream(t.device).cuda_stream

@@ -1,0 +1,179 @@
+"""GCN_FC on MI355X: the reference's model API with the HIP hot path.
+
+Mirrors arch.py of vbdai/lp-gnn (and the PyG 2.1 ``GraphConv`` it builds on)
+name for name, so that ``GCN_FC(8, 8, hids=1024, depth=3)`` has the same
+constructor, ``forward(batch) -> (logit_cons [m,3], logit_vars [n,3])`` and
+state_dict keys/shapes -- a reference ``mdl.pth`` loads unchanged
+(``GCNBase.load``, arch.py:112-114).
+
+What runs where:
+  aggregation  sum_j A_ij x_j     -> lpgnn.sparse.spmm  (HIP CSR SpMM, both
+                                     directions, fwd and bwd)
+  dense FC     lin_rel / lin_root -> lpgnn.fc (hand-written fp32 MFMA GEMM
+                                     with fused bias + root + ReLU) when the
+                                     FC library entry is present, else
+                                     torch.nn.functional.linear on the GPU
+  heads + add_knowledge           -> GPU (torch elementwise)
+"""
+from __future__ import annotations
+
+import ast
+import math
+import re
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+
+from .sparse import BipartiteCSR, spmm
+from . import fc as _fc
+
+
+class Linear(nn.Module):
+    """torch_geometric.nn.dense.linear.Linear (PyG 2.1), default initialisers:
+    weight kaiming_uniform(fan=in, a=sqrt(5)), bias uniform(1/sqrt(in)).
+    Parameter names ``weight``/``bias`` as in PyG (state_dict compatible)."""
+
+    def __init__(self, in_channels: int, out_channels: int, bias: bool = True):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.weight = nn.Parameter(torch.empty(out_channels, in_channels))
+        if bias:
+            self.bias = nn.Parameter(torch.empty(out_channels))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        bound = math.sqrt(6.0 / ((1 + 5.0) * self.in_channels))
+        self.weight.uniform_(-bound, bound)
+        if self.bias is not None:
+            b = 1.0 / math.sqrt(self.in_channels)
+            self.bias.uniform_(-b, b)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return F.linear(x, self.weight, self.bias)
+
+
+class GraphConv(nn.Module):
+    """PyG 2.1 ``GraphConv((in_src, in_dst), out, aggr='add')`` with a sparse adj_t:
+
+        out = lin_rel(sum_{j} adj_t[i, j] * x_src[j]) + lin_root(x_dst[i])
+
+    lin_rel has a bias, lin_root has none; aggregation precedes lin_rel.
+    ``forward`` may also apply the following ReLU in the same fused kernel
+    (``relu=True``); the reference applies it right after (arch.py:182, 188).
+    """
+
+    def __init__(self, in_channels, out_channels: int, aggr: str = "add", bias: bool = True):
+        super().__init__()
+        if aggr != "add":
+            raise NotImplementedError("GCN_FC uses aggr='add' only (arch.py:57-62)")
+        if isinstance(in_channels, int):
+            in_channels = (in_channels, in_channels)
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.lin_rel = Linear(in_channels[0], out_channels, bias=bias)
+        self.lin_root = Linear(in_channels[1], out_channels, bias=False)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.lin_rel.reset_parameters()
+        self.lin_root.reset_parameters()
+
+    def forward(self, x, edge_index: BipartiteCSR, edge_weight=None, size=None, relu: bool = False) -> Tensor:
+        if isinstance(x, Tensor):
+            x = (x, x)
+        if edge_weight is not None:
+            raise NotImplementedError("edge weights come from the adjacency values (arch.py:77)")
+        agg = spmm(edge_index, x[0])  # message_and_aggregate: matmul(adj_t, x[0], 'add')
+        return _fc.graph_conv_fc(agg, x[1], self.lin_rel.weight, self.lin_rel.bias, self.lin_root.weight, relu)
+
+
+class GraphConvTwoDirection(nn.Module):
+    """arch.py:51-81.  left = constraints, right = variables."""
+
+    def __init__(self, left_dim, right_dim, out_dim):
+        super().__init__()
+        self.left2right = GraphConv((left_dim, right_dim), out_dim)
+        self.right2left = GraphConv((right_dim, left_dim), out_dim)
+
+    def forward(self, left_feas, right_feas, edge_index: BipartiteCSR, edge_weight=None, relu: bool = False):
+        # edge_index is A (m x n, rows = cons).  arch.py:71-74: l2r = A^T, r2l = A.
+        l2r, r2l = edge_index.t(), edge_index
+        right_updated = self.left2right((left_feas, right_feas), l2r, edge_weight, relu=relu)
+        left_updated = self.right2left((right_feas, left_feas), r2l, edge_weight, relu=relu)
+        return left_updated, right_updated
+
+
+def add_knowledge(left_logit, right_logit, left_feas, right_feas, bound=10):
+    """arch.py:129-141: L2-normalise x10, -bound on impossible statuses."""
+    return _fc.knowledge(left_logit, left_feas, bound), _fc.knowledge(right_logit, right_feas, bound)
+
+
+class GCNBase(nn.Module):
+    """arch.py:108-114 (state_dict-only checkpoints)."""
+
+    def save(self, pn):
+        torch.save(self.state_dict(), pn)
+
+    def load(self, pn):
+        st = torch.load(pn, map_location=torch.device("cpu"), weights_only=True)
+        self.load_state_dict(st)
+
+
+class GCN_FC(GCNBase):
+    """arch.py:167-193."""
+
+    def __init__(self, p, q, hids=128, depth=3, dp=.1, *args, **kwargs):
+        super().__init__()
+        self.conv1 = GraphConvTwoDirection(p, q, hids)
+        self.layers = nn.ModuleList()
+        for _ in range(depth - 2):
+            self.layers.append(GraphConvTwoDirection(hids, hids, hids))
+        self.lin_left = nn.Linear(hids, 3)
+        self.lin_right = nn.Linear(hids, 3)
+        self.dp = dp
+
+    def forward(self, batch):
+        x_left, x_right, edge_index = batch.x_s, batch.x_t, batch.edge_index
+        # conv -> ReLU (arch.py:181-182): the ReLU is fused into the FC epilogue.
+        left, right = self.conv1(x_left, x_right, edge_index, relu=True)
+        for conv in self.layers:
+            if self.training and self.dp > 0:
+                # conv -> dropout -> ReLU (arch.py:185-188)
+                left, right = conv(left, right, edge_index)
+                left = F.dropout(left, p=self.dp, training=True).relu_()
+                right = F.dropout(right, p=self.dp, training=True).relu_()
+            else:
+                # dropout is the identity: relu(dropout(x)) == relu(x), fuse it.
+                left, right = conv(left, right, edge_index, relu=True)
+        left, right = self.lin_left(left), self.lin_right(right)
+        return add_knowledge(left, right, x_left, x_right)
+
+
+_ARCH_RE = re.compile(r"^\s*([A-Za-z_]\w*)\s*\((.*)\)\s*$", re.S)
+
+
+def build_model(arch: str) -> nn.Module:
+    """Safe replacement for ``eval(args.arch)`` (train.py:79, val.py:266,
+    pred_basis.py:128): parses e.g. ``GCN_FC(8,8,hids=1024,depth=3)``
+    with literal arguments only."""
+    mt = _ARCH_RE.match(arch)
+    if not mt:
+        raise ValueError(f"cannot parse arch string {arch!r}")
+    name, argstr = mt.group(1), mt.group(2)
+    classes = {"GCN_FC": GCN_FC}
+    if name not in classes:
+        raise ValueError(f"arch {name!r} is outside this build's scope (GCN_FC only; SURVEY.md §2)")
+    call = ast.parse(f"f({argstr})", mode="eval").body
+    args = [ast.literal_eval(a) for a in call.args]
+    kwargs = {k.arg: ast.literal_eval(k.value) for k in call.keywords}
+    return classes[name](*args, **kwargs)
+
+
+def arch_depth(arch: str) -> int:
+    """train.py:108-110 / val.py:14-16: hops = depth - 1 (2 if absent)."""
+    d = re.findall(r"depth=(\d+)", arch)
+    return 2 if len(d) == 0 else int(d[0]) - 1

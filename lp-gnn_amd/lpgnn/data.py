@@ -1,0 +1,138 @@
+"""Batch boundary: LPDataset.get -> MyToBipartite -> HIP dual-CSR pack.
+
+The reference loads one LP per step as a homogeneous graph
+(``UnipartiteData``, dataset.py:16-20, 229-264), and ``MyToBipartite``
+(dataset.py:268-332) relabels it into a bipartite batch with
+``x_s, x_t, y_s, y_t, edge_index: SparseTensor(m x n), bs, s_bs, t_bs``.
+This module keeps that contract attribute for attribute; the only change is
+the type of ``edge_index``: a :class:`~lpgnn.sparse.BipartiteCSR` packed
+once (CSR(A) and CSR(A^T)) instead of a torch_sparse SparseTensor that is
+transposed again in every layer.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .sparse import BipartiteCSR
+
+
+class UnipartiteData:
+    """dataset.py:16-20 / 255-262: x, y, is_vars, edge_index (2,E), edge_attr."""
+
+    def __init__(self, x, y, edge_index, edge_attr=None, is_vars=None, num_nodes=None, **aux):
+        self.x, self.y, self.edge_index, self.edge_attr = x, y, edge_index, edge_attr
+        self.is_vars = is_vars
+        self.num_nodes = int(num_nodes if num_nodes is not None else x.shape[0])
+        for k, v in aux.items():
+            setattr(self, k, v)
+
+
+class BipartiteBatch:
+    """What MyToBipartite returns (dataset.py:307-326)."""
+
+    _TENSORS = ("x_s", "x_t", "y_s", "y_t")
+
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+    def __getitem__(self, k):  # batch_to (utils.py:909-915) indexes by name
+        return getattr(self, k)
+
+    def __setitem__(self, k, v):
+        setattr(self, k, v)
+
+    def to(self, device, non_blocking: bool = False) -> "BipartiteBatch":
+        for k in self._TENSORS:
+            if getattr(self, k, None) is not None:
+                setattr(self, k, getattr(self, k).to(device, non_blocking=non_blocking))
+        self.edge_index = self.edge_index.to(device, non_blocking=non_blocking)
+        return self
+
+    @property
+    def num_nodes(self) -> int:
+        return int(self.x_s.shape[0] + self.x_t.shape[0])
+
+
+def to_undirected(edge_index: torch.Tensor, edge_attr: torch.Tensor, num_nodes: int):
+    """PyG 2.1 ``to_undirected(edge_index, edge_attr)`` (dataset.py:252):
+    both directions, coalesced (sorted by row*N + col, duplicates added)."""
+    row = torch.cat([edge_index[0], edge_index[1]])
+    col = torch.cat([edge_index[1], edge_index[0]])
+    attr = torch.cat([edge_attr, edge_attr])
+    key = row * num_nodes + col
+    key, perm = torch.sort(key, stable=True)
+    attr = attr[perm]
+    uniq, inv = torch.unique_consecutive(key, return_inverse=True)
+    summed = torch.zeros(uniq.numel(), dtype=attr.dtype).index_add_(0, inv, attr)
+    return torch.stack([uniq // num_nodes, uniq % num_nodes]), summed
+
+
+def lp_to_unipartite(row, col, A_data, c_feas, v_feas, y_s, y_t, **aux) -> UnipartiteData:
+    """LPDataset.get after the msgpack load (dataset.py:234-264)."""
+    A_data = np.asarray(A_data)
+    c_feas = np.asarray(c_feas)
+    assert A_data.max() <= 1 and A_data.min() >= -1  # dataset.py:235-236
+    assert c_feas.max() <= 1 and c_feas.min() >= -1  # dataset.py:237-238
+    ncons = c_feas.shape[0]
+    nnodes = ncons + np.asarray(v_feas).shape[0]
+    c_feas, v_feas, y_s, y_t = (torch.as_tensor(np.asarray(a)) for a in (c_feas, v_feas, y_s, y_t))
+    edge_attr = torch.as_tensor(A_data).float()
+    edge_index = torch.as_tensor(np.asarray([row, np.asarray(col) + ncons], dtype=np.int64))
+    edge_index, edge_attr = to_undirected(edge_index, edge_attr, nnodes)
+    is_vars = torch.zeros(nnodes, dtype=torch.long)
+    is_vars[ncons:] = 1
+    return UnipartiteData(x=torch.cat((c_feas, v_feas), 0), y=torch.cat((y_s, y_t), 0), is_vars=is_vars,
+                          edge_index=edge_index, edge_attr=edge_attr, num_nodes=nnodes, **aux)
+
+
+class MyToBipartite:
+    """dataset.py:268-332, with the SparseTensor build replaced by the dual-CSR
+    pack on ``dev`` ('cpu' = host pack in the loader worker, a HIP device =
+    lpg_csr_pack_f32)."""
+
+    def __init__(self, dev="cpu", phase="train", thresh_num=np.inf):
+        self.dev = dev
+        self.phase = phase
+        self.thresh_num = thresh_num
+
+    def __call__(self, batch):
+        if hasattr(batch, "x_s"):  # already bipartite
+            return batch
+        if batch.edge_index.shape[-1] // 2 > self.thresh_num:
+            return batch
+        is_vars = batch.is_vars.bool()
+        is_cons = ~is_vars
+        nnodes = batch.num_nodes
+        nvars = int(is_vars.sum().item())
+        ncons = nnodes - nvars
+
+        mapping_vec = torch.empty(ncons + nvars, dtype=torch.long)
+        mapping_vec[is_cons] = torch.arange(ncons)
+        mapping_vec[is_vars] = torch.arange(nvars) + ncons
+        edge_index = mapping_vec[batch.edge_index]
+
+        edge_mask = edge_index[0, :] < ncons
+        assert edge_mask.sum().item() * 2 == edge_mask.shape[0]  # dataset.py:297
+        edge_index_l2r = edge_index[:, edge_mask].clone()
+        edge_index_l2r[1, :] -= ncons
+        adj = BipartiteCSR.from_edge_index(edge_index_l2r, batch.edge_attr[edge_mask], (ncons, nvars),
+                                           device=self.dev)
+        bs = getattr(batch, "batch_size", None) or batch.num_nodes
+        t_bs = int(batch.is_vars[:bs].sum().item())
+        extra = {k: v for k, v in vars(batch).items()
+                 if k not in ("x", "y", "edge_index", "edge_attr", "is_vars", "num_nodes", "batch")}
+        return BipartiteBatch(x_s=batch.x[is_cons, :], x_t=batch.x[is_vars, :], y_s=batch.y[is_cons],
+                              y_t=batch.y[is_vars], edge_index=adj, bs=bs, s_bs=bs - t_bs, t_bs=t_bs, **extra)
+
+
+def batch_to(batch, dev, half: bool = False):
+    """utils.py:909-915."""
+    for nm in ("x_s", "x_t", "y_s", "y_t"):
+        t = batch[nm]
+        if half and t.is_floating_point():
+            t = t.half()
+        batch[nm] = t.to(dev)
+    batch["edge_index"] = batch["edge_index"].to(dev)
+    return batch

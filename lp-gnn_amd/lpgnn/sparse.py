@@ -1,0 +1,206 @@
+"""Bipartite adjacency (dual CSR) and the differentiable HIP SpMM.
+
+Replaces, for the GCN_FC hot path:
+
+* ``torch_sparse.SparseTensor`` as the batch's ``edge_index``
+  (dataset.py:301-304) and its per-layer ``.t()`` (arch.py:71):
+  :class:`BipartiteCSR` holds CSR(A) and CSR(A^T) on the device, packed once
+  (``lpg_csr_pack_f32``), and ``.t()`` just swaps the two views;
+* ``torch_sparse.matmul(adj_t, x, reduce='add')`` -> ``spmm_sum`` and its
+  autograd ``SPMMSum`` (PyG GraphConv.message_and_aggregate, arch.py:75-80):
+  :func:`spmm` -- forward ``lpg_spmm_f32(adj)``, backward
+  ``lpg_spmm_f32(adj.t())`` (no gradient w.r.t. edge values, which the
+  reference never trains: dataset.py:250).
+
+All compute runs in liblpgnn_hip.so on the tensor's current HIP stream.
+There is no CPU path: a CPU tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from .timing import TIMER
+
+
+@dataclass
+class CSR:
+    """One orientation: rows = destination nodes, cols = source nodes."""
+
+    rowptr: torch.Tensor  # int64 [n_rows+1]
+    col: torch.Tensor     # int32 [nnz]
+    val: torch.Tensor     # f32 [nnz]
+    n_rows: int
+    n_cols: int
+
+    def __post_init__(self):
+        self._c = None
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.numel())
+
+    @property
+    def device(self) -> torch.device:
+        return self.rowptr.device
+
+    def cstruct(self) -> _lib.LpgCsr:
+        if self._c is None:
+            self._c = _lib.LpgCsr(self.n_rows, self.n_cols, self.nnz, self.rowptr.data_ptr(),
+                                  self.col.data_ptr() if self.nnz else None,
+                                  self.val.data_ptr() if self.nnz else None)
+        return self._c
+
+    def to(self, device) -> "CSR":
+        return CSR(self.rowptr.to(device), self.col.to(device), self.val.to(device), self.n_rows, self.n_cols)
+
+    def degrees(self) -> torch.Tensor:
+        return self.rowptr[1:] - self.rowptr[:-1]
+
+
+class BipartiteCSR:
+    """Drop-in for the reference batch's ``edge_index`` SparseTensor(m x n).
+
+    ``sparse_sizes()`` is (rows, cols) of the current orientation; ``t()``
+    returns the transposed view without moving data (the reference re-derives
+    it with a csr2csc gather every layer, arch.py:71).
+    """
+
+    def __init__(self, fwd: CSR, bwd: CSR):
+        self.fwd, self.bwd = fwd, bwd
+
+    # -- SparseTensor-like surface used by the reference call sites --
+    def t(self) -> "BipartiteCSR":
+        return BipartiteCSR(self.bwd, self.fwd)
+
+    def sparse_sizes(self):
+        return (self.fwd.n_rows, self.fwd.n_cols)
+
+    def sparse_size(self, dim: int) -> int:
+        return self.sparse_sizes()[dim]
+
+    def nnz(self) -> int:
+        return self.fwd.nnz
+
+    @property
+    def device(self) -> torch.device:
+        return self.fwd.device
+
+    def to(self, device, non_blocking: bool = False) -> "BipartiteCSR":
+        return BipartiteCSR(self.fwd.to(device), self.bwd.to(device))
+
+    def __repr__(self) -> str:
+        r, c = self.sparse_sizes()
+        return f"BipartiteCSR(sparse_sizes=({r}, {c}), nnz={self.nnz()}, device={self.device})"
+
+    # -- construction --
+    @classmethod
+    def from_edge_index(cls, edge_index: torch.Tensor, edge_attr: torch.Tensor, sparse_sizes,
+                        device=None) -> "BipartiteCSR":
+        """SparseTensor.from_edge_index(edge_index, edge_attr, (m, n)) (dataset.py:301-304).
+
+        On a HIP device the pack runs on the GPU (lpg_csr_pack_f32); for host
+        tensors with ``device`` None/'cpu' it runs in the library's host pack
+        (lpg_csr_pack_host) -- the data-loader worker analogue; the result
+        must be moved to the GPU before any spmm.
+        """
+        m, n = int(sparse_sizes[0]), int(sparse_sizes[1])
+        device = torch.device(device) if device is not None else edge_index.device
+        row = edge_index[0].to(torch.int64).contiguous()
+        col = edge_index[1].to(torch.int64).contiguous()
+        val = edge_attr.to(torch.float32).contiguous().view(-1)
+        nnz = int(row.numel())
+        if val.numel() != nnz:
+            raise ValueError(f"edge_attr has {val.numel()} values for {nnz} edges")
+        if device.type == "cpu":
+            return cls._pack_host(row.cpu(), col.cpu(), val.cpu(), nnz, m, n)
+        return cls._pack_device(row.to(device), col.to(device), val.to(device), nnz, m, n)
+
+    @classmethod
+    def from_coo(cls, row, col, val, m: int, n: int, device) -> "BipartiteCSR":
+        ei = torch.stack([torch.as_tensor(np.asarray(row)), torch.as_tensor(np.asarray(col))])
+        return cls.from_edge_index(ei, torch.as_tensor(np.asarray(val, dtype=np.float32)), (m, n), device)
+
+    @classmethod
+    def _pack_host(cls, row, col, val, nnz, m, n) -> "BipartiteCSR":
+        L = _lib.lib()
+        a_rp = torch.empty(m + 1, dtype=torch.int64)
+        at_rp = torch.empty(n + 1, dtype=torch.int64)
+        a_c, at_c = torch.empty(nnz, dtype=torch.int32), torch.empty(nnz, dtype=torch.int32)
+        a_v, at_v = torch.empty(nnz, dtype=torch.float32), torch.empty(nnz, dtype=torch.float32)
+        p = lambda t: t.data_ptr() if t.numel() else None
+        _lib.check(L.lpg_csr_pack_host(p(row), p(col), p(val), nnz, m, n, a_rp.data_ptr(), p(a_c), p(a_v),
+                                       at_rp.data_ptr(), p(at_c), p(at_v)), "lpg_csr_pack_host")
+        return cls(CSR(a_rp, a_c, a_v, m, n), CSR(at_rp, at_c, at_v, n, m))
+
+    @classmethod
+    def _pack_device(cls, row, col, val, nnz, m, n) -> "BipartiteCSR":
+        L = _lib.lib()
+        dev = row.device
+        ws_bytes = L.lpg_csr_pack_workspace_bytes(nnz, m, n)
+        ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+        kw = dict(device=dev)
+        a_rp, at_rp = torch.empty(m + 1, dtype=torch.int64, **kw), torch.empty(n + 1, dtype=torch.int64, **kw)
+        a_c, at_c = torch.empty(nnz, dtype=torch.int32, **kw), torch.empty(nnz, dtype=torch.int32, **kw)
+        a_v, at_v = torch.empty(nnz, dtype=torch.float32, **kw), torch.empty(nnz, dtype=torch.float32, **kw)
+        p = lambda t: t.data_ptr() if t.numel() else None
+        with torch.cuda.device(dev):
+            _lib.check(L.lpg_csr_pack_f32(p(row), p(col), p(val), nnz, m, n, a_rp.data_ptr(), p(a_c), p(a_v),
+                                          at_rp.data_ptr(), p(at_c), p(at_v), ws.data_ptr(), _lib.stream_of(row)),
+                       "lpg_csr_pack_f32")
+            bad, dup = ws[:16].view(torch.int64).tolist()  # one sync per graph load, not per layer
+        if bad or dup:
+            raise RuntimeError(f"lpg_csr_pack_f32: invalid argument: {bad} edge(s) with an out-of-range index, "
+                               f"{dup} duplicate (row, col) pair(s); coalesce first (dataset.py:252)")
+        return cls(CSR(a_rp, a_c, a_v, m, n), CSR(at_rp, at_c, at_v, n, m))
+
+
+def spmm_forward(adj: CSR, x: torch.Tensor) -> torch.Tensor:
+    """Y = adj @ x on the GPU (no autograd).  fp32 or bf16 storage."""
+    if x.device.type != "cuda" or adj.device != x.device:
+        raise RuntimeError(f"lpgnn.spmm: x ({x.device}) and adj ({adj.device}) must be on the same HIP device; "
+                           "there is no CPU path")
+    if x.dim() != 2 or x.shape[0] != adj.n_cols:
+        raise RuntimeError(f"lpgnn.spmm: x must be [{adj.n_cols}, F], got {tuple(x.shape)}")
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    Fd = x.shape[1]
+    y = torch.empty((adj.n_rows, Fd), dtype=x.dtype, device=x.device)
+    L = _lib.lib()
+    if x.dtype == torch.float32:
+        fn, name = L.lpg_spmm_f32, "lpg_spmm_f32"
+    elif x.dtype == torch.bfloat16:
+        fn, name = L.lpg_spmm_bf16, "lpg_spmm_bf16"
+    else:
+        raise RuntimeError(f"lpgnn.spmm: unsupported dtype {x.dtype}")
+    with torch.cuda.device(x.device):
+        stream = _lib.stream_of(x)
+        tok = TIMER.start(("spmm", adj.n_rows, adj.n_cols, Fd, str(x.dtype)))
+        st = fn(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), Fd, stream)
+        TIMER.stop(tok)
+    _lib.check(st, name)
+    return y
+
+
+class _SpMM(torch.autograd.Function):
+    """torch_sparse SPMMSum: fwd spmm(A, X), bwd dX = spmm(A^T, dY)."""
+
+    @staticmethod
+    def forward(ctx, x, adj):
+        ctx.adj = adj
+        return spmm_forward(adj.fwd, x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        if not ctx.needs_input_grad[0]:
+            return None, None
+        return spmm_forward(ctx.adj.bwd, gy), None
+
+
+def spmm(adj: BipartiteCSR, x: torch.Tensor) -> torch.Tensor:
+    """``torch_sparse.matmul(adj_t, x, reduce='add')`` on the HIP kernels."""
+    return _SpMM.apply(x, adj)

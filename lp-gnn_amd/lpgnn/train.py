@@ -1,0 +1,86 @@
+"""Training caller of the hot path (train.py:18-53, 85-129; utils.py:286-299)."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.optim.lr_scheduler import StepLR
+
+
+@torch.no_grad()
+def labels_to_balanced_weights(labels, merge_lu=True):
+    """utils.py:286-299: w[c] = N / count_c for present classes; with all
+    three classes present, w0 = w2 = mean(w0, w2)."""
+    res = torch.zeros(3).to(labels.device)
+    lbl, cnt = torch.unique(labels, return_counts=True)
+    wei = cnt.sum() / cnt
+    if len(lbl) == 2:
+        res[lbl] = wei
+    else:
+        res[lbl] = wei
+        if merge_lu:
+            res[0] = res[2] = (res[0] + res[2]) / 2.
+    return res
+
+
+def balanced(logpr_cons, logpr_vars, y_s, y_t):
+    """train.py:39-46 (the loss of the published experiment)."""
+    loss = 0.
+    m, n = len(y_s), len(y_t)
+    criterion = nn.CrossEntropyLoss(weight=labels_to_balanced_weights(y_s))
+    loss += (m + n) / m * criterion(logpr_cons, y_s)
+    criterion = nn.CrossEntropyLoss(weight=labels_to_balanced_weights(y_t))
+    loss += (m + n) / n * criterion(logpr_vars, y_t)
+    return loss
+
+
+def unbalanced(logpr_cons, logpr_vars, y_s, y_t):
+    """train.py:32-37."""
+    return nn.CrossEntropyLoss()(torch.cat((logpr_cons, logpr_vars), 0), torch.cat((y_s, y_t), 0))
+
+
+class FocalLoss(nn.modules.loss._WeightedLoss):
+    """train.py:18-28."""
+
+    def __init__(self, weight=None, gamma=2, reduction="mean"):
+        super().__init__(weight, reduction=reduction)
+        self.gamma = gamma
+        self.weight = weight
+
+    def forward(self, input, target):
+        ce_loss = F.cross_entropy(input, target, reduction=self.reduction, weight=self.weight)
+        pt = torch.exp(-ce_loss)
+        return ((1 - pt) ** self.gamma * ce_loss).mean()
+
+
+def focal(logpr_cons, logpr_vars, y_s, y_t):
+    """train.py:49-53."""
+    return FocalLoss()(torch.cat((logpr_cons, logpr_vars), 0), torch.cat((y_s, y_t), 0))
+
+
+LOSSES = {"balanced": balanced, "unbalanced": unbalanced, "focal": focal}
+
+
+def make_optimizer(model, opt="adam", lr=1e-3, epochs=800):
+    """train.py:85-89: Adam/SGD(weight_decay=5e-4) + StepLR(epochs//4, 0.1)."""
+    if opt == "adam":
+        o = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=5e-4)
+    else:
+        o = torch.optim.SGD(model.parameters(), lr=lr, weight_decay=5e-4)
+    return o, StepLR(o, step_size=max(epochs // 4, 1), gamma=0.1)
+
+
+def train_step(model, batch, opt, loss="balanced", check_nan=True):
+    """One inner iteration of train.py:117-129: forward on the batch, slice
+    the seed nodes, loss, backward, optimizer step.  Returns the loss tensor
+    (no host sync unless check_nan)."""
+    logit_cons, logit_vars = model(batch)
+    logit_cons, logit_vars = logit_cons[:batch.s_bs], logit_vars[:batch.t_bs]
+    y_s, y_t = batch.y_s[:batch.s_bs], batch.y_t[:batch.t_bs]
+    L = LOSSES[loss](logit_cons, logit_vars, y_s, y_t)
+    if check_nan:
+        assert not torch.isnan(L).item()  # train.py:126
+    opt.zero_grad()
+    L.backward()
+    opt.step()
+    return L

@@ -1,0 +1,341 @@
+"""ORACLE -- test infrastructure only.
+
+CPU restatement of the reference's GCN_FC hot path, used by tests/,
+``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg as the
+checker / the timed CPU baseline.  Nothing in ``lp-gnn_amd/`` imports this
+module; the product path fails loudly without its HIP library.
+
+Every function cites what it restates:
+
+* reference files (vbdai/lp-gnn @ /root/reference): arch.py, dataset.py,
+  val.py, train.py, utils.py;
+* upstream, NOT vendored in /root/reference, restated from the versions the
+  reference pins (readme.md:51-52): torch_geometric 2.1 (``GraphConv``,
+  ``Linear`` init, ``to_undirected``) and torch_sparse 0.6.12
+  (``SparseTensor.from_edge_index``, ``.t()``/``csr2csc``, ``spmm_sum``).
+
+Parity pinning (see DESIGN.md "Parity"): the pure-torch reference functions
+(add_knowledge arch.py:129-141, inference_gnn val.py:106-124, balanced
+train.py:39-46, labels_to_balanced_weights utils.py:286-299) and the GCN_FC /
+GraphConvTwoDirection orchestration (arch.py:51-81, 167-193) are pinned by
+golden vectors produced by running the reference's own function bodies
+(tests/golden/make_golden.py).  The upstream torch_sparse/PyG arithmetic has
+no vectors anywhere ("parity unpinned" for that layer): it is restated here.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+# --------------------------------------------------------------------------
+# C restatement of torch_sparse spmm_cpu (spmm_ref.c)
+# --------------------------------------------------------------------------
+def lib():
+    """Load (building if needed) oracle/liboracle_spmm.so."""
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle_spmm.so")
+        if not os.path.exists(path):
+            import subprocess
+
+            subprocess.run(["make", "-s", "-C", _HERE], check=True)
+        L = ctypes.CDLL(path)
+        i64, p = ctypes.c_int64, ctypes.c_void_p
+        L.oracle_spmm_f32.argtypes = [i64, p, p, p, p, i64, i64, p, i64, ctypes.c_int]
+        L.oracle_spmm_f32.restype = None
+        L.oracle_spmm_bf16.argtypes = [i64, p, p, p, p, i64, i64, p, i64, ctypes.c_int]
+        L.oracle_spmm_bf16.restype = None
+        L.oracle_max_threads.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def spmm_f32(rowptr, col, val, X, nthreads: int = 0) -> np.ndarray:
+    """Y = CSR(rowptr, col, val) @ X in torch_sparse spmm_cpu order (fp32)."""
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    val = np.ascontiguousarray(val, dtype=np.float32)
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    M = rowptr.shape[0] - 1
+    Fd = X.shape[1]
+    Y = np.empty((M, Fd), dtype=np.float32)
+    if M > 0 and Fd > 0:
+        lib().oracle_spmm_f32(M, _ptr(rowptr), _ptr(col), _ptr(val), _ptr(X), Fd, Fd, _ptr(Y), Fd, nthreads)
+    return Y
+
+
+def spmm_bf16(rowptr, col, val, Xbits, nthreads: int = 0) -> np.ndarray:
+    """bf16-storage variant (uint16 bit patterns in/out, fp32 accumulate)."""
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    val = np.ascontiguousarray(val, dtype=np.float32)
+    Xbits = np.ascontiguousarray(Xbits, dtype=np.uint16)
+    M = rowptr.shape[0] - 1
+    Fd = Xbits.shape[1]
+    Y = np.empty((M, Fd), dtype=np.uint16)
+    if M > 0 and Fd > 0:
+        lib().oracle_spmm_bf16(M, _ptr(rowptr), _ptr(col), _ptr(val), _ptr(Xbits), Fd, Fd, _ptr(Y), Fd, nthreads)
+    return Y
+
+
+# --------------------------------------------------------------------------
+# Sparse layout restatement (torch_sparse 0.6.12 SparseTensor)
+# --------------------------------------------------------------------------
+def csr_from_coo(row, col, val, m: int, n: int):
+    """SparseTensor.from_edge_index(edge_index, edge_attr, (m, n)) -> CSR.
+
+    Upstream: ``idx = row * n + col; perm = idx.argsort()`` (stable for unique
+    keys), ``rowptr = ind2ptr(row[perm], m)``.  Called at dataset.py:301-304.
+    Returns (rowptr int64[m+1], col int32[nnz], val f32[nnz]).
+    """
+    row = np.asarray(row, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    key = row * n + col
+    perm = np.argsort(key, kind="stable")
+    r = row[perm]
+    rowptr = np.zeros(m + 1, dtype=np.int64)
+    np.add.at(rowptr, r + 1, 1)
+    rowptr = np.cumsum(rowptr)
+    return rowptr, col[perm].astype(np.int32), np.asarray(val, dtype=np.float32)[perm]
+
+
+def csr_transpose(rowptr, col, val, m: int, n: int):
+    """SparseTensor.t() (arch.py:71): csr2csc = argsort(col * m + row)."""
+    rowptr = np.asarray(rowptr, dtype=np.int64)
+    row = np.repeat(np.arange(m, dtype=np.int64), np.diff(rowptr))
+    return csr_from_coo(col.astype(np.int64), row, val, n, m)
+
+
+# --------------------------------------------------------------------------
+# Model restatement
+# --------------------------------------------------------------------------
+class _OracleSpMM(torch.autograd.Function):
+    """torch_sparse SPMMSum (csrc/spmm.cpp): fwd spmm(A, X); bwd spmm(A^T, dY)."""
+
+    @staticmethod
+    def forward(ctx, X, fwd, bwd):
+        ctx.bwd = bwd
+        return torch.from_numpy(spmm_f32(*fwd, X.detach().numpy()))
+
+    @staticmethod
+    def backward(ctx, gY):
+        return torch.from_numpy(spmm_f32(*ctx.bwd, gY.contiguous().numpy())), None, None
+
+
+def spmm_t(csr, csr_t, X: torch.Tensor) -> torch.Tensor:
+    """Differentiable fp32 spmm; fp64 inputs use scipy (order-free sanity path)."""
+    if X.dtype == torch.float64:
+        import scipy.sparse as sp
+
+        rowptr, col, val = csr
+        M = rowptr.shape[0] - 1
+        A = sp.csr_matrix((val.astype(np.float64), col, rowptr), shape=(M, X.shape[0]))
+        return torch.from_numpy(A @ X.detach().numpy())
+    return _OracleSpMM.apply(X, csr, csr_t)
+
+
+def graph_conv(x_src, x_dst, adj, adj_t, W_rel, b_rel, W_root):
+    """PyG 2.1 GraphConv.forward with a SparseTensor adj_t (aggr='add'):
+
+    out = propagate(...)      -> message_and_aggregate = matmul(adj_t, x[0], 'add')
+    out = self.lin_rel(out)   -> F.linear(out, W_rel, b_rel)
+    out += self.lin_root(x[1])-> F.linear(x_dst, W_root)   (lin_root: bias=False)
+    """
+    agg = spmm_t(adj, adj_t, x_src)
+    out = F.linear(agg, W_rel, b_rel)
+    out = out + F.linear(x_dst, W_root)
+    return out, agg
+
+
+def conv_two_direction(sd, prefix, left, right, A, AT):
+    """GraphConvTwoDirection.forward, arch.py:65-81.
+
+    l2r, r2l = edge_index, edge_index.t(); l2r, r2l = r2l, l2r  (arch.py:71-74)
+    => left2right aggregates with A^T (rows = vars), right2left with A.
+    Both directions read the same-layer inputs.
+    """
+    g = lambda d, k: sd[f"{prefix}.{d}.{k}"]
+    right_new, agg_r = graph_conv(left, right, AT, A, g("left2right", "lin_rel.weight"),
+                                  g("left2right", "lin_rel.bias"), g("left2right", "lin_root.weight"))
+    left_new, agg_l = graph_conv(right, left, A, AT, g("right2left", "lin_rel.weight"),
+                                 g("right2left", "lin_rel.bias"), g("right2left", "lin_root.weight"))
+    return left_new, right_new, agg_l, agg_r
+
+
+def add_knowledge(left_logit, right_logit, left_feas, right_feas, bound=10):
+    """arch.py:129-141."""
+    cons_l_mask, cons_u_mask = left_feas[:, -3].abs().bool(), left_feas[:, -1].abs().bool()
+    vars_l_mask, vars_u_mask = right_feas[:, -3].abs().bool(), right_feas[:, -1].abs().bool()
+    left_logit = F.normalize(left_logit) * 10
+    right_logit = F.normalize(right_logit) * 10
+    left_logit[cons_l_mask, 0] = left_logit[cons_l_mask, 0] - bound
+    left_logit[cons_u_mask, 2] = left_logit[cons_u_mask, 2] - bound
+    right_logit[vars_l_mask, 0] = right_logit[vars_l_mask, 0] - bound
+    right_logit[vars_u_mask, 2] = right_logit[vars_u_mask, 2] - bound
+    return left_logit, right_logit
+
+
+def gcn_fc_forward(sd, x_s, x_t, A, AT, depth: int, keep=None):
+    """GCN_FC.forward, arch.py:179-193, eval mode (dropout is identity).
+
+    sd: state_dict (tensors), A/AT: (rowptr, col, val) CSR of A and A^T.
+    keep: optional dict that receives per-layer intermediates.
+    """
+    left, right, agg_l, agg_r = conv_two_direction(sd, "conv1", x_s, x_t, A, AT)
+    left, right = torch.relu(left), torch.relu(right)
+    if keep is not None:
+        keep["agg_l0"], keep["agg_r0"], keep["left0"], keep["right0"] = agg_l, agg_r, left, right
+    for i in range(depth - 2):
+        left, right, agg_l, agg_r = conv_two_direction(sd, f"layers.{i}", left, right, A, AT)
+        left, right = torch.relu(left), torch.relu(right)
+        if keep is not None:
+            keep[f"agg_l{i+1}"], keep[f"agg_r{i+1}"] = agg_l, agg_r
+            keep[f"left{i+1}"], keep[f"right{i+1}"] = left, right
+    left = F.linear(left, sd["lin_left.weight"], sd["lin_left.bias"])
+    right = F.linear(right, sd["lin_right.weight"], sd["lin_right.bias"])
+    if keep is not None:
+        keep["head_l"], keep["head_r"] = left, right
+    return add_knowledge(left, right, x_s, x_t)
+
+
+def init_state_dict(p: int, q: int, hids: int, depth: int, seed: int = 0):
+    """GCN_FC(p, q, hids, depth) parameters with the reference's RNG stream.
+
+    PyG 2.1 GraphConv.__init__ builds lin_rel = Linear(in_src, out, bias) and
+    lin_root = Linear(in_dst, out, bias=False) -- each Linear.__init__ calls
+    reset_parameters() -- and then GraphConv.reset_parameters() initialises
+    both again.  PyG Linear init: kaiming_uniform(fan=in, a=sqrt(5)) on the
+    weight, uniform(1/sqrt(in)) on the bias: the same bounds and draw order
+    as torch.nn.Linear.  Heads are torch.nn.Linear (arch.py:175-176).
+    """
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+
+    def lin(out_f, in_f, bias):
+        w = torch.empty(out_f, in_f)
+        bound = math.sqrt(6.0 / ((1 + 5.0) * in_f))
+        w.uniform_(-bound, bound, generator=g)
+        b = None
+        if bias:
+            b = torch.empty(out_f)
+            bb = 1.0 / math.sqrt(in_f)
+            b.uniform_(-bb, bb, generator=g)
+        return w, b
+
+    def conv(prefix, l_dim, r_dim, out):
+        for d, (src, dst) in (("left2right", (l_dim, r_dim)), ("right2left", (r_dim, l_dim))):
+            lin(out, src, True)  # Linear ctor draws (discarded by the re-init below)
+            lin(out, dst, False)
+            w_rel, b_rel = lin(out, src, True)
+            w_root, _ = lin(out, dst, False)
+            sd[f"{prefix}.{d}.lin_rel.weight"] = w_rel
+            sd[f"{prefix}.{d}.lin_rel.bias"] = b_rel
+            sd[f"{prefix}.{d}.lin_root.weight"] = w_root
+
+    conv("conv1", p, q, hids)
+    for i in range(depth - 2):
+        conv(f"layers.{i}", hids, hids, hids)
+    for side in ("lin_left", "lin_right"):
+        w, b = lin(3, hids, True)
+        sd[f"{side}.weight"], sd[f"{side}.bias"] = w, b
+    return sd
+
+
+# --------------------------------------------------------------------------
+# Post-processing / loss restatements
+# --------------------------------------------------------------------------
+@torch.no_grad()
+def inference_gnn(logits, m):
+    """val.py:106-124 (top-m basic, argmax over {0,2} for the rest)."""
+    n = logits.shape[0] - m
+    pr = F.softmax(logits.float(), dim=-1)
+    pr = pr.clone()
+    pr[torch.isnan(pr)] = 0
+    _, topk_idx = pr[:, 1].topk(m)
+    pr[:, 1] = pr.min() - 1
+    pr[topk_idx, 1] = pr.max() + 1
+    pred = pr.argmax(-1)
+    assert (pred == 1).sum().item() == m
+    assert (pred[m:m + n] == 1).sum().item() == ((pred[:m] == 0) | (pred[:m] == 2)).sum().item()
+    return pred
+
+
+@torch.no_grad()
+def labels_to_balanced_weights(labels, merge_lu=True):
+    """utils.py:286-299."""
+    res = torch.zeros(3).to(labels.device)
+    lbl, cnt = torch.unique(labels, return_counts=True)
+    wei = cnt.sum() / cnt
+    if len(lbl) == 2:
+        res[lbl] = wei
+    else:
+        res[lbl] = wei
+        if merge_lu:
+            res[0] = res[2] = (res[0] + res[2]) / 2.
+    return res
+
+
+def balanced(logpr_cons, logpr_vars, y_s, y_t):
+    """train.py:39-46."""
+    loss = 0.
+    m, n = len(y_s), len(y_t)
+    criterion = torch.nn.CrossEntropyLoss(weight=labels_to_balanced_weights(y_s))
+    loss += (m + n) / m * criterion(logpr_cons, y_s)
+    criterion = torch.nn.CrossEntropyLoss(weight=labels_to_balanced_weights(y_t))
+    loss += (m + n) / n * criterion(logpr_vars, y_t)
+    return loss
+
+
+# --------------------------------------------------------------------------
+# Batch boundary restatement (dataset.py)
+# --------------------------------------------------------------------------
+def to_undirected(edge_index: np.ndarray, edge_attr: np.ndarray, num_nodes: int):
+    """PyG 2.1 utils.to_undirected(edge_index, edge_attr) as called at
+    dataset.py:252: cat both directions, coalesce (sort by row*N+col, add
+    duplicate attrs)."""
+    row = np.concatenate([edge_index[0], edge_index[1]])
+    col = np.concatenate([edge_index[1], edge_index[0]])
+    attr = np.concatenate([edge_attr, edge_attr])
+    key = row * num_nodes + col
+    perm = np.argsort(key, kind="stable")
+    key, attr = key[perm], attr[perm]
+    uniq, start = np.unique(key, return_index=True)
+    summed = np.add.reduceat(attr, start) if len(attr) else attr
+    return np.stack([uniq // num_nodes, uniq % num_nodes]), summed.astype(np.float32)
+
+
+def my_to_bipartite(x, y, is_vars, edge_index, edge_attr, num_nodes):
+    """MyToBipartite.__call__, dataset.py:275-332 (batch_size = num_nodes).
+
+    Returns dict(x_s, x_t, y_s, y_t, A=(rowptr,col,val), m, n, s_bs, t_bs).
+    """
+    is_vars = np.asarray(is_vars).astype(bool)
+    is_cons = ~is_vars
+    nvars = int(is_vars.sum())
+    ncons = num_nodes - nvars
+    mapping = np.empty(num_nodes, dtype=np.int64)
+    mapping[is_cons] = np.arange(ncons)
+    mapping[is_vars] = np.arange(nvars) + ncons
+    ei = mapping[edge_index]
+    mask = ei[0] < ncons
+    assert mask.sum() * 2 == mask.shape[0]
+    l2r = ei[:, mask].copy()
+    l2r[1] -= ncons
+    A = csr_from_coo(l2r[0], l2r[1], np.asarray(edge_attr)[mask], ncons, nvars)
+    bs = num_nodes
+    t_bs = int(is_vars[:bs].sum())
+    return dict(x_s=x[is_cons], x_t=x[is_vars], y_s=y[is_cons], y_t=y[is_vars], A=A, m=ncons, n=nvars,
+                s_bs=bs - t_bs, t_bs=t_bs)

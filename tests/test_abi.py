@@ -1,0 +1,100 @@
+"""The C-ABI library: builds for gfx950, loads, exports every declared symbol;
+host pack (no GPU needed) equals the oracle's torch_sparse order."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+from oracle import model_ref as O
+
+HEADER = os.path.join(ROOT, "include", "lpgnn.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lpg_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from lpgnn import _lib
+
+    L = _lib.lib()
+    names = declared_functions()
+    assert len(names) >= 8
+    for name in names:
+        assert hasattr(L, name), f"{name} declared in include/lpgnn.h but not exported"
+    assert b"gfx950" in L.lpg_build_info()
+
+
+def test_library_is_gfx950_code_object():
+    from lpgnn import _lib
+
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_spmm_kernels_have_no_fused_multiply_add():
+    """-ffp-contract=off is what makes the kernel bitwise equal to the CPU
+    loop; guard it at the ISA level."""
+    out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "lp-gnn_amd"), "isa"], capture_output=True,
+                         text=True)
+    assert out.returncode == 0, out.stderr[-2000:]
+    s = open("/tmp/lpg_isa/spmm-hip-amdgcn-amd-amdhsa-gfx950.s").read()
+    assert "v_fma" not in s and "v_fmac" not in s and "v_pk_fma" not in s
+
+
+def _coo(rng, m, n, nnz):
+    keys = rng.choice(m * n, size=nnz, replace=False)
+    return (keys // n).astype(np.int64), (keys % n).astype(np.int64), rng.uniform(-1, 1, nnz).astype(np.float32)
+
+
+@pytest.mark.parametrize("m,n,nnz", [(5, 7, 0), (1, 1, 1), (64, 128, 700), (300, 50, 3000)])
+def test_host_pack_matches_torch_sparse_order(m, n, nnz):
+    from lpgnn import BipartiteCSR
+
+    rng = np.random.default_rng(m * 31 + nnz)
+    row, col, val = _coo(rng, m, n, nnz)
+    adj = BipartiteCSR.from_coo(row, col, val, m, n, device="cpu")
+    A = O.csr_from_coo(row, col, val, m, n)
+    AT = O.csr_transpose(*A, m, n)
+    for csr, ref in ((adj.fwd, A), (adj.bwd, AT)):
+        assert np.array_equal(csr.rowptr.numpy(), ref[0])
+        assert np.array_equal(csr.col.numpy(), ref[1])
+        assert np.array_equal(csr.val.numpy(), ref[2])
+    assert adj.t().sparse_sizes() == (n, m)
+
+
+def test_host_pack_rejects_bad_input():
+    from lpgnn import BipartiteCSR
+
+    with pytest.raises(RuntimeError, match="duplicate edge"):
+        BipartiteCSR.from_coo([0, 0], [1, 1], [0.5, 0.5], 2, 2, device="cpu")
+    with pytest.raises(RuntimeError, match="out of"):
+        BipartiteCSR.from_coo([0, 2], [1, 1], [0.5, 0.5], 2, 2, device="cpu")
+
+
+def test_status_and_error_string():
+    from lpgnn import _lib
+
+    L = _lib.lib()
+    st = L.lpg_spmm_set_slice(300)
+    assert st == 1
+    assert b"slice" in L.lpg_last_error()
+    assert L.lpg_spmm_set_slice(0) == 0
+    # NULL CSR -> invalid argument, no device work
+    assert L.lpg_spmm_f32(None, None, 0, None, 0, 0, None) == 1
+    assert L.lpg_csr_pack_workspace_bytes(-1, 0, 0) == -1
+
+
+def test_no_cpu_path_for_spmm():
+    from lpgnn import BipartiteCSR, spmm
+
+    adj = BipartiteCSR.from_coo([0, 1], [1, 0], [0.5, -0.5], 2, 2, device="cpu")
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        spmm(adj, torch.ones(2, 4))

@@ -1,0 +1,137 @@
+"""GCN_FC on the HIP path vs the reference (golden vectors from the
+reference's own class bodies) and vs the oracle restatement.
+
+Tolerance (north star): per-node logits within 1e-4 (fp32), argmax basis
+labels identical.  The SpMM is bitwise; the dense FC's fp32 summation order
+differs from MKL's, which is what the 1e-4 absorbs.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_ref as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+LOGIT_ATOL = 1e-4
+
+
+def _model_from_sd(sd, depth, hids):
+    from lpgnn import GCN_FC
+
+    model = GCN_FC(8, 8, hids=hids, depth=depth, dp=0.0)
+    model.load_state_dict({k: torch.as_tensor(v) for k, v in sd.items()})
+    return model.to(DEV)
+
+
+def _batch(g, m, n):
+    from lpgnn import BipartiteBatch, BipartiteCSR
+
+    adj = BipartiteCSR.from_coo(g["coo_row"], g["coo_col"], g["coo_val"], m, n, device=DEV)
+    return BipartiteBatch(x_s=torch.from_numpy(g["x_s"]).to(DEV), x_t=torch.from_numpy(g["x_t"]).to(DEV),
+                          y_s=torch.from_numpy(g["y_s"]).to(DEV), y_t=torch.from_numpy(g["y_t"]).to(DEV),
+                          edge_index=adj, s_bs=m, t_bs=n, bs=m + n)
+
+
+@pytest.mark.parametrize("name", ["gcn_fc_d3_h32.npz", "gcn_fc_d4_h16.npz"])
+def test_golden_reference_logits_labels_grads(golden_dir, name):
+    from lpgnn.train import balanced
+    from lpgnn.val import inference_gnn
+
+    g = dict(np.load(f"{golden_dir}/{name}"))
+    m, n, depth, hids = (int(g[k]) for k in ("m", "n", "depth", "hids"))
+    sd = {k[3:]: v for k, v in g.items() if k.startswith("sd.")}
+    model = _model_from_sd(sd, depth, hids)
+    batch = _batch(g, m, n)
+    model.eval()
+    with torch.no_grad():
+        lc, lv = model(batch)
+    np.testing.assert_allclose(lc.cpu().numpy(), g["logit_cons"], rtol=0, atol=LOGIT_ATOL)
+    np.testing.assert_allclose(lv.cpu().numpy(), g["logit_vars"], rtol=0, atol=LOGIT_ATOL)
+    logits = torch.cat((lc, lv)).cpu()
+    assert np.array_equal(logits.argmax(-1).numpy(),
+                          np.concatenate([g["logit_cons"], g["logit_vars"]]).argmax(-1))
+    assert np.array_equal(inference_gnn(logits, m).numpy(), g["labels"])
+    model.train()
+    lc, lv = model(batch)
+    loss = balanced(lc, lv, batch.y_s, batch.y_t)
+    model.zero_grad()
+    loss.backward()
+    assert abs(loss.item() - float(g["loss"])) < 1e-4
+    for k, p in model.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), g["grad." + k], rtol=1e-3, atol=1e-5, err_msg=k)
+
+
+def test_state_dict_compat_and_init_stream():
+    """Same keys/shapes as the reference; same RNG stream as PyG 2.1's
+    double initialisation (oracle.init_state_dict)."""
+    from lpgnn import GCN_FC
+
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=1024, depth=3)
+    ref = O.init_state_dict(8, 8, 1024, 3, seed=0)
+    sd = model.state_dict()
+    assert list(sd.keys()) == list(ref.keys())
+    for k in sd:
+        assert torch.equal(sd[k], ref[k]), k
+    assert sum(p.numel() for p in model.parameters()) == 4_237_318
+
+
+@pytest.mark.parametrize("depth,hids", [(3, 1024), (4, 256)])
+def test_random_graph_vs_oracle(depth, hids):
+    """Mid-size synthetic LP, eval-mode logits vs the oracle fp32 CPU path."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+
+    g = synth.uniform_lp(2000, 4000, 40000, seed=3)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=hids, depth=depth).to(DEV).eval()
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    with torch.no_grad():
+        lc, lv = model(batch)
+    A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
+    AT = O.csr_transpose(*A, g.m, g.n)
+    keep = {}
+    with torch.no_grad():
+        rc, rv = O.gcn_fc_forward(sd, torch.from_numpy(g.x_s), torch.from_numpy(g.x_t), A, AT, depth, keep=keep)
+    np.testing.assert_allclose(lc.cpu().numpy(), rc.numpy(), rtol=0, atol=LOGIT_ATOL)
+    np.testing.assert_allclose(lv.cpu().numpy(), rv.numpy(), rtol=0, atol=LOGIT_ATOL)
+    got = torch.cat((lc, lv)).cpu()
+    ref = torch.cat((rc, rv))
+    top2 = ref.topk(2, dim=-1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 4 * LOGIT_ATOL  # not a near-tie at the tolerance
+    assert torch.equal(got.argmax(-1)[clear], ref.argmax(-1)[clear])
+    assert int((~clear).sum()) <= 2, "unexpectedly many near-ties"
+
+
+def test_training_step_runs_and_matches_oracle_grads():
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.train import balanced, make_optimizer, train_step
+
+    g = synth.uniform_lp(1000, 2000, 20000, seed=5)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=128, depth=3, dp=0.0).to(DEV)
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                           y_s=torch.from_numpy(g.y_s).to(DEV), y_t=torch.from_numpy(g.y_t).to(DEV),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    model.train()
+    lc, lv = model(batch)
+    loss = balanced(lc, lv, batch.y_s, batch.y_t)
+    loss.backward()
+    A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
+    AT = O.csr_transpose(*A, g.m, g.n)
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    rc, rv = O.gcn_fc_forward(params, torch.from_numpy(g.x_s), torch.from_numpy(g.x_t), A, AT, 3)
+    rloss = O.balanced(rc, rv, torch.from_numpy(g.y_s), torch.from_numpy(g.y_t))
+    rloss.backward()
+    assert abs(loss.item() - rloss.item()) < 1e-4
+    for k, p in model.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), params[k].grad.numpy(), rtol=2e-3, atol=2e-5, err_msg=k)
+    opt, _ = make_optimizer(model)
+    for _ in range(3):
+        L = train_step(model, batch, opt)
+    assert torch.isfinite(L).item()

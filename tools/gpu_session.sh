@@ -1,0 +1,52 @@
+#!/bin/bash
+# One GPU-box session: parity tests -> smoke -> bench -> rocprofv3 kernel stats.
+# Usage (from the repo root, via gpurun):  bash tools/gpu_session.sh [stages...]
+# stages: tests smoke bench prof pmc   (default: tests smoke bench prof)
+# Every GPU step has its own time limit; the script stops at the first step
+# that crashes, aborts or times out (exit >= 2 or signal), and continues past
+# a plain test failure (exit 1) so the bench still runs.
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
+cd "$ROOT"
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+STAGES="${*:-tests smoke bench prof}"
+TAG="${LPG_TAG:-r01}"
+
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 tmo=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  local t0=$(date +%s)
+  timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name exit=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
+  tail -n 25 "$OUT/$name.log"
+  if [ $rc -ge 2 ]; then
+    echo "stopping after $name (exit $rc)" | tee -a "$OUT/session.log"
+    exit $rc
+  fi
+  return 0
+}
+
+rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > "$OUT/device.txt" || true
+for s in $STAGES; do
+  case $s in
+    tests) step pytest_gpu 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 900 python bench.py ;;
+    prof)
+      step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python "$ROOT/bench.py" --steps 5 --warmup 2 --profile-only
+      ;;
+    pmc)
+      step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+        python "$ROOT/bench.py" --steps 3 --warmup 1 --profile-only
+      step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+        python "$ROOT/bench.py" --steps 3 --warmup 1 --profile-only
+      ;;
+    *) echo "unknown stage $s"; exit 2 ;;
+  esac
+done
+echo "session done"
