@@ -101,6 +101,33 @@ lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx,
 lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
                          uint16_t *Y, int64_t ldy, int64_t F, void *stream);
 
+/* ---- dense FC (replaces GraphConv's lin_rel + lin_root + ReLU) ----------- */
+
+/* C[m, n] = act( sum_{k<K1} A1[m,k] W1[n,k] + sum_{k<K2} A2[m,k] W2[n,k] + bias[n] )
+ *
+ * PyG 2.1 GraphConv.forward after propagate, as built at arch.py:57-62 and
+ * applied at arch.py:75-80: lin_rel(agg) + lin_root(x_dst), with W in the
+ * torch Linear layout [out, in] (A1 = agg, W1 = lin_rel.weight, bias =
+ * lin_rel.bias, A2 = x_dst, W2 = lin_root.weight).  With K2 = 0 it is a plain
+ * Linear (heads lin_left / lin_right, arch.py:175-176, 190).
+ * flags: bit 0 = ReLU epilogue (arch.py:182, 188).  bias may be NULL.
+ * Row-major fp32, leading dimensions in floats; K1, K2 and the A/W leading
+ * dimensions multiples of 4, A/W 16-byte aligned.
+ * Numerics: one fp32 fma chain per output in k order (A1 part, then A2
+ * part) from +0, then + bias -- bitwise reproducible, see oracle/fc_ref.c. */
+lpg_status lpg_fc_f32(int64_t M, int64_t N,
+                      int64_t K1, const float *A1, int64_t lda1, const float *W1, int64_t ldw1,
+                      int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2,
+                      const float *bias, float *C, int64_t ldc, int32_t flags, void *stream);
+
+/* add_knowledge for one side (arch.py:129-141): out = normalize(logit) * 10,
+ * then out[:,0] -= bound where feas[:, cols-3] != 0 (infinite lower bound)
+ * and out[:,2] -= bound where feas[:, cols-1] != 0 (infinite upper bound).
+ * logit/out [M, 3] (strides ldl/ldo), feas [M, feas_cols] (stride ldf).
+ * Bitwise torch-CPU F.normalize semantics (norm = sqrt(fma(x2,x2,fma(x1,x1,x0*x0)))). */
+lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t ldl, const float *feas, int64_t ldf,
+                             int64_t feas_cols, float bound, float *out, int64_t ldo, void *stream);
+
 /* Tuning knob for lpg_spmm_f32 (process-global, default 0 = auto):
  * columns per slice of F processed by one wave (multiple of 256, or 0).
  * Smaller slices keep the gathered source slice resident in the 256 MiB

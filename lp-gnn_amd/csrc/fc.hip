@@ -1,0 +1,239 @@
+// Dense per-node FC of GraphConv on fp32 MFMA (gfx950), fused:
+//
+//   C[m, n] = act( sum_{k<K1} A1[m,k] W1[n,k] + sum_{k<K2} A2[m,k] W2[n,k] + bias[n] )
+//
+// = PyG 2.1 GraphConv.forward after propagate:  lin_rel(agg) + lin_root(x_dst)
+// (arch.py:57-62, 75-80) with the ReLU of arch.py:182/188 as the epilogue,
+// and -- with K2 = 0, no ReLU -- the heads lin_left / lin_right (arch.py:190).
+// The concat [agg | x_dst] is never materialised: the k loop walks A1 then A2.
+//
+// Numerics (the parity contract, mirrored by oracle/fc_ref.c): every output
+// is ONE fp32 fma chain in k order, k = 0..K1-1 over (A1, W1) then
+// k = 0..K2-1 over (A2, W2), starting from +0, then one add of the bias,
+// then ReLU as (v < 0 ? 0 : v).  v_mfma_f32_32x32x2_f32 is bit-for-bit such a
+// chain (k0 then k1 of each pair; MI355X_MICROARCH.md §Matrix cores), and
+// the accumulator of an output tile visits the k-tiles in increasing order.
+//
+// Tiling: 256 threads = 4 waves; BM x BN output tile, BK = 32; A and W tiles
+// staged global -> registers -> LDS ([row][BK+1] fp32, conflict-free column
+// reads), double-buffered with one barrier per k-tile; each wave owns
+// TM x TN blocks of 32x32 (16 accumulator VGPRs each).  Blocks are remapped
+// so that each XCD walks a contiguous range of m-tiles with all their
+// n-tiles (the A panel is then re-read from that XCD's L2).
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace lpg {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 1;
+
+struct FcArgs {
+  int64_t M, N, K1, K2;
+  const float *A1, *A2, *W1, *W2, *bias;
+  int64_t lda1, lda2, ldw1, ldw2;
+  float *C;
+  int64_t ldc;
+  int64_t mt, nt;  // tiles
+};
+
+// Load one row-chunk of 4 consecutive k of the virtual [X1 | X2] matrix.
+__device__ __forceinline__ float4 load_k4(const float *X1, int64_t ld1, int64_t K1, const float *X2, int64_t ld2,
+                                          int64_t K2, int64_t r, int64_t R, int64_t k) {
+  if (r >= R) return make_float4(0.f, 0.f, 0.f, 0.f);
+  if (k < K1) return *reinterpret_cast<const float4 *>(X1 + r * ld1 + k);
+  k -= K1;
+  if (k < K2) return *reinterpret_cast<const float4 *>(X2 + r * ld2 + k);
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int WAVES_M, int WAVES_N, int TM, int TN, bool RELU>
+__global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
+  constexpr int BM = WAVES_M * TM * 32;
+  constexpr int BN = WAVES_N * TN * 32;
+  constexpr int LA = BM * 8 / 256;  // float4 loads per thread per k-tile
+  constexpr int LB = BN * 8 / 256;
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  static_assert(LA >= 1 && LB >= 1, "tile too small");
+  __shared__ float smem[2 * (BM + BN) * LDK];
+  // buffer b: A tile at smem + b*(BM+BN)*LDK, W tile right after it
+  auto As = [&](int b) { return smem + b * (BM + BN) * LDK; };
+  auto Bs = [&](int b) { return smem + b * (BM + BN) * LDK + BM * LDK; };
+
+  // XCD-aware bijective remap of the 1-D grid.
+  const int64_t nwg = a.mt * a.nt;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  const int64_t m0 = (wgid / a.nt) * BM;
+  const int64_t n0 = (wgid % a.nt) * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int64_t K = a.K1 + a.K2;
+  const int nk = (int)((K + BK - 1) / BK);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float4 ra[LA], rb[LB];
+  auto gload = [&](int t) {
+    const int64_t k0 = (int64_t)t * BK;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + 256 * i;
+      ra[i] = load_k4(a.A1, a.lda1, a.K1, a.A2, a.lda2, a.K2, m0 + idx / 8, a.M, k0 + (idx % 8) * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + 256 * i;
+      rb[i] = load_k4(a.W1, a.ldw1, a.K1, a.W2, a.ldw2, a.K2, n0 + idx / 8, a.N, k0 + (idx % 8) * 4);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + 256 * i;
+      float *p = As(buf) + (idx / 8) * LDK + (idx % 8) * 4;
+      p[0] = ra[i].x; p[1] = ra[i].y; p[2] = ra[i].z; p[3] = ra[i].w;
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + 256 * i;
+      float *p = Bs(buf) + (idx / 8) * LDK + (idx % 8) * 4;
+      p[0] = rb[i].x; p[1] = rb[i].y; p[2] = rb[i].z; p[3] = rb[i].w;
+    }
+  };
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int fr = lane & 31, fk = lane >> 5;
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nk) gload(t + 1);
+    const float *Ab = As(buf) + (wm * TM * 32 + fr) * LDK + fk;
+    const float *Bb = Bs(buf) + (wn * TN * 32 + fr) * LDK + fk;
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = Ab[i * 32 * LDK + 2 * s];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = Bb[j * 32 * LDK + 2 * s];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // Epilogue: C/D map of the 32x32 MFMA: col = lane & 31,
+  // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+    if (col >= a.N) continue;
+    const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int64_t rbase = m0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row < a.M) {
+          float v = acc[i][j][r];
+          if (a.bias) v = v + b;
+          if (RELU) v = (v < 0.f) ? 0.f : v;
+          a.C[row * a.ldc + col] = v;
+        }
+      }
+    }
+  }
+}
+
+// add_knowledge for one side (arch.py:129-141), bitwise torch-CPU semantics:
+//   n = sqrt(fma(x2, x2, fma(x1, x1, x0 * x0)))      (torch.linalg.vector_norm, CPU)
+//   y = x / max(n, 1e-12) * 10                          (F.normalize(x) * 10)
+//   y0 -= bound where feas[:, -3] != 0;  y2 -= bound where feas[:, -1] != 0
+__global__ __launch_bounds__(256) void knowledge_f32(int64_t M, const float *__restrict__ logit, int64_t ldl,
+                                                     const float *__restrict__ feas, int64_t ldf, int64_t fcols,
+                                                     float bound, float *__restrict__ out, int64_t ldo) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const float x0 = logit[m * ldl], x1 = logit[m * ldl + 1], x2 = logit[m * ldl + 2];
+  const float nrm = sqrtf(__builtin_fmaf(x2, x2, __builtin_fmaf(x1, x1, x0 * x0)));
+  const float d = nrm < 1e-12f ? 1e-12f : nrm;
+  float y0 = x0 / d * 10.f, y1 = x1 / d * 10.f, y2 = x2 / d * 10.f;
+  if (feas[m * ldf + fcols - 3] != 0.f) y0 = y0 - bound;
+  if (feas[m * ldf + fcols - 1] != 0.f) y2 = y2 - bound;
+  out[m * ldo] = y0;
+  out[m * ldo + 1] = y1;
+  out[m * ldo + 2] = y2;
+}
+
+template <int WM, int WN, int TM, int TN>
+lpg_status launch_fc(const FcArgs &a0, bool relu, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  FcArgs a = a0;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int64_t nwg = a.mt * a.nt;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_f32: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+}  // namespace
+}  // namespace lpg
+
+using namespace lpg;
+
+extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1, const float *W1,
+                                 int64_t ldw1, int64_t K2, const float *A2, int64_t lda2, const float *W2,
+                                 int64_t ldw2, const float *bias, float *C, int64_t ldc, int32_t flags, void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_f32: negative size");
+  if (M == 0 || N == 0) return LPG_OK;
+  LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_f32: bad C/ldc");
+  LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1), "lpg_fc_f32: bad A1/W1");
+  LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2), "lpg_fc_f32: bad A2/W2");
+  LPG_REQUIRE(K1 % 4 == 0 && K2 % 4 == 0 && lda1 % 4 == 0 && ldw1 % 4 == 0 && (K2 == 0 || (lda2 % 4 == 0 && ldw2 % 4 == 0)),
+              "lpg_fc_f32: K and leading dimensions must be multiples of 4 floats");
+  LPG_REQUIRE(aligned16(A1) && aligned16(W1) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
+              "lpg_fc_f32: A/W must be 16-byte aligned");
+  LPG_REQUIRE((flags & ~1) == 0, "lpg_fc_f32: unknown flags 0x%x", flags);
+  FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0};
+  hipStream_t s = as_stream(stream);
+  const bool relu = flags & 1;
+  if (N <= 32) return launch_fc<4, 1, 1, 1>(a, relu, s);   // heads (N = 3): 128 x 32 tiles
+  return launch_fc<2, 2, 2, 2>(a, relu, s);                // 128 x 128 tiles
+}
+
+extern "C" lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t ldl, const float *feas, int64_t ldf,
+                                        int64_t feas_cols, float bound, float *out, int64_t ldo, void *stream) {
+  LPG_REQUIRE(M >= 0, "lpg_knowledge_f32: M < 0");
+  if (M == 0) return LPG_OK;
+  LPG_REQUIRE(logit && feas && out, "lpg_knowledge_f32: NULL pointer");
+  LPG_REQUIRE(ldl >= 3 && ldo >= 3 && feas_cols >= 3 && ldf >= feas_cols, "lpg_knowledge_f32: bad shapes");
+  hipLaunchKernelGGL(knowledge_f32, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, as_stream(stream), M, logit,
+                     ldl, feas, ldf, feas_cols, bound, out, ldo);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}

@@ -28,6 +28,8 @@ HEADER_SYMBOLS = (
     "lpg_spmm_f32",
     "lpg_spmm_bf16",
     "lpg_spmm_set_slice",
+    "lpg_fc_f32",
+    "lpg_knowledge_f32",
 )
 
 c_i64, c_i32, c_p = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
@@ -63,14 +65,11 @@ def lib() -> ctypes.CDLL:
     L.lpg_spmm_bf16.restype = c_i32
     L.lpg_spmm_set_slice.argtypes = [c_i64]
     L.lpg_spmm_set_slice.restype = c_i32
-    if hasattr(L, "lpg_fc_f32"):
-        L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
-                                 c_i32, c_p, c_p]
-        L.lpg_fc_f32.restype = c_i32
-        L.lpg_fc_workspace_bytes.argtypes = [c_i64, c_i64]
-        L.lpg_fc_workspace_bytes.restype = c_i64
-        L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p]
-        L.lpg_knowledge_f32.restype = c_i32
+    L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
+                             c_p, c_p, c_i64, c_i32, c_p]
+    L.lpg_fc_f32.restype = c_i32
+    L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_i64, ctypes.c_float, c_p, c_i64, c_p]
+    L.lpg_knowledge_f32.restype = c_i32
     _lib = L
     return L
 

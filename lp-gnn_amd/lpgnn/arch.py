@@ -9,11 +9,11 @@ state_dict keys/shapes -- a reference ``mdl.pth`` loads unchanged
 What runs where:
   aggregation  sum_j A_ij x_j     -> lpgnn.sparse.spmm  (HIP CSR SpMM, both
                                      directions, fwd and bwd)
-  dense FC     lin_rel / lin_root -> lpgnn.fc (hand-written fp32 MFMA GEMM
-                                     with fused bias + root + ReLU) when the
-                                     FC library entry is present, else
-                                     torch.nn.functional.linear on the GPU
-  heads + add_knowledge           -> GPU (torch elementwise)
+  dense FC     lin_rel + lin_root -> lpgnn.fc (hand-written fp32 MFMA kernel,
+               + bias + ReLU         one fma chain per output, fused epilogue)
+  heads        lin_left/lin_right -> the same kernel (N = 3 tile)
+  add_knowledge                   -> lpg_knowledge_f32 (bitwise torch-CPU
+                                     F.normalize semantics)
 """
 from __future__ import annotations
 
@@ -138,18 +138,18 @@ class GCN_FC(GCNBase):
 
     def forward(self, batch):
         x_left, x_right, edge_index = batch.x_s, batch.x_t, batch.edge_index
-        # conv -> ReLU (arch.py:181-182): the ReLU is fused into the FC epilogue.
+        # conv -> ReLU (arch.py:181-182): the ReLU is the FC kernel's epilogue.
         left, right = self.conv1(x_left, x_right, edge_index, relu=True)
         for conv in self.layers:
+            # conv -> dropout -> ReLU (arch.py:185-188).  ReLU commutes with
+            # dropout (x * mask / (1-p), a non-negative scale), so the ReLU is
+            # fused into the FC and dropout follows it.
+            left, right = conv(left, right, edge_index, relu=True)
             if self.training and self.dp > 0:
-                # conv -> dropout -> ReLU (arch.py:185-188)
-                left, right = conv(left, right, edge_index)
-                left = F.dropout(left, p=self.dp, training=True).relu_()
-                right = F.dropout(right, p=self.dp, training=True).relu_()
-            else:
-                # dropout is the identity: relu(dropout(x)) == relu(x), fuse it.
-                left, right = conv(left, right, edge_index, relu=True)
-        left, right = self.lin_left(left), self.lin_right(right)
+                left = F.dropout(left, p=self.dp, training=True)
+                right = F.dropout(right, p=self.dp, training=True)
+        left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias)
+        right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias)
         return add_knowledge(left, right, x_left, x_right)
 
 

@@ -1,12 +1,19 @@
-"""Dense per-node FC stack of GraphConv and the add_knowledge epilogue.
+"""Dense per-node FC of GraphConv and the add_knowledge epilogue, on the
+hand-written fp32 MFMA kernels of liblpgnn_hip.so.
 
 ``graph_conv_fc`` computes, for one GraphConv direction (PyG 2.1
-GraphConv.forward after propagate):
+GraphConv.forward after propagate, arch.py:57-62 / 75-80):
 
-    out = lin_rel(agg) + lin_root(x_dst)        [+ ReLU, arch.py:182/188]
+    out = lin_rel(agg) + lin_root(x_dst)  [+ ReLU, arch.py:182/188]
         = agg @ W_rel^T + b_rel + x_dst @ W_root^T
 
-``knowledge`` is arch.py:129-141 for one side.
+in ONE kernel (lpg_fc_f32: no concat, no separate add / ReLU pass), and
+``linear`` the heads lin_left / lin_right (arch.py:190).  ``knowledge`` is
+arch.py:129-141 for one side (lpg_knowledge_f32).
+
+Forward numerics are bitwise reproducible (oracle/fc_ref.c).  Backward:
+dZ = dY * (Y > 0); dA = dZ @ W; dW = dZ^T @ A; db = sum(dZ) -- plain library
+GEMMs through torch on the same stream (hipBLASLt), tolerance-level parity.
 """
 from __future__ import annotations
 
@@ -14,21 +21,114 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
+from . import _lib
+from .timing import TIMER
+
+
+def _prep(t: Tensor | None) -> Tensor | None:
+    if t is None:
+        return None
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"lpgnn FC: fp32 only, got {t.dtype}")
+    if t.stride(-1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+        t = t.contiguous()
+    return t
+
+
+def _pad_k(t: Tensor) -> Tensor:
+    """Zero-pad the reduction dim to a multiple of 4 (zeros are exact no-ops
+    in the fma chain: the accumulator is never -0)."""
+    k = t.shape[1]
+    return t if k % 4 == 0 else F.pad(t, (0, 4 - k % 4))
+
+
+def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
+               relu: bool) -> Tensor:
+    if A1.device.type != "cuda":
+        raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
+    M, N = A1.shape[0], W1.shape[0]
+    if A1.shape[1] % 4:
+        A1, W1 = _pad_k(A1), _pad_k(W1)
+    if A2 is not None and A2.shape[1] % 4:
+        A2, W2 = _pad_k(A2), _pad_k(W2)
+    A1, W1, A2, W2 = _prep(A1), _prep(W1), _prep(A2), _prep(W2)
+    bias = None if bias is None else bias.contiguous()
+    C = torch.empty((M, N), dtype=torch.float32, device=A1.device)
+    K2 = 0 if A2 is None else A2.shape[1]
+    L = _lib.lib()
+    with torch.cuda.device(A1.device):
+        tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
+        st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
+                          K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
+                          None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
+                          None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), 1 if relu else 0,
+                          _lib.stream_of(A1))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_fc_f32")
+    return C
+
+
+class _FC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, A1, A2, W1, W2, b, relu):
+        C = fc_forward(A1, W1, A2, W2, b, relu)
+        ctx.relu, ctx.has_a2, ctx.has_b = relu, A2 is not None, b is not None
+        ctx.save_for_backward(A1, A2 if A2 is not None else A1, W1, W2 if W2 is not None else W1,
+                              C if relu else A1)
+        return C
+
+    @staticmethod
+    def backward(ctx, gC):
+        A1, A2, W1, W2, C = ctx.saved_tensors
+        g = gC.masked_fill(C <= 0, 0.0) if ctx.relu else gC  # threshold_backward of ReLU
+        need = ctx.needs_input_grad
+        dA1 = g @ W1 if need[0] else None
+        dA2 = g @ W2 if ctx.has_a2 and need[1] else None
+        dW1 = g.t() @ A1 if need[2] else None
+        dW2 = g.t() @ A2 if ctx.has_a2 and need[3] else None
+        db = g.sum(0) if ctx.has_b and need[4] else None
+        return dA1, dA2, dW1, dW2, db, None
+
 
 def graph_conv_fc(agg: Tensor, x_dst: Tensor, w_rel: Tensor, b_rel, w_root: Tensor, relu: bool) -> Tensor:
-    if agg.device.type != "cuda":
-        raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only")
-    out = F.linear(agg, w_rel, b_rel)
-    out = out + F.linear(x_dst, w_root)
-    return out.relu_() if relu else out
+    return _FC.apply(agg, x_dst, w_rel, w_root, b_rel, relu)
+
+
+def linear(x: Tensor, weight: Tensor, bias) -> Tensor:
+    """torch.nn.Linear.forward on lpg_fc_f32 (heads, arch.py:190)."""
+    return _FC.apply(x, None, weight, None, bias, False)
+
+
+class _Knowledge(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logit, feas, bound):
+        if logit.device.type != "cuda":
+            raise RuntimeError("lpgnn: add_knowledge runs on a HIP device only (no CPU path)")
+        logit = logit.contiguous()
+        feas = feas.contiguous().float()
+        out = torch.empty_like(logit)
+        L = _lib.lib()
+        with torch.cuda.device(logit.device):
+            st = L.lpg_knowledge_f32(logit.shape[0], logit.data_ptr(), logit.stride(0), feas.data_ptr(),
+                                     feas.stride(0), feas.shape[1], float(bound), out.data_ptr(), out.stride(0),
+                                     _lib.stream_of(logit))
+        _lib.check(st, "lpg_knowledge_f32")
+        ctx.save_for_backward(logit)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        n = torch.linalg.vector_norm(x, dim=1, keepdim=True)
+        d = n.clamp_min(1e-12)
+        xg = (x * g).sum(1, keepdim=True)
+        big = n > 1e-12
+        dx = torch.where(big, 10.0 * (g / d - x * xg / (d * d * d)), 10.0 * g / d)
+        return dx, None, None
 
 
 def knowledge(logit: Tensor, feas: Tensor, bound=10) -> Tensor:
     """One side of add_knowledge: normalize(logit) * 10, then -bound on
     column 0 where feas[:, -3] != 0 (lower bound = -inf) and on column 2
     where feas[:, -1] != 0 (upper bound = +inf)."""
-    l_mask, u_mask = feas[:, -3].abs().bool(), feas[:, -1].abs().bool()
-    logit = F.normalize(logit) * 10
-    logit[l_mask, 0] = logit[l_mask, 0] - bound
-    logit[u_mask, 2] = logit[u_mask, 2] - bound
-    return logit
+    return _Knowledge.apply(logit, feas, bound)

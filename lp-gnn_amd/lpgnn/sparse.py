@@ -202,5 +202,11 @@ class _SpMM(torch.autograd.Function):
 
 
 def spmm(adj: BipartiteCSR, x: torch.Tensor) -> torch.Tensor:
-    """``torch_sparse.matmul(adj_t, x, reduce='add')`` on the HIP kernels."""
+    """``torch_sparse.matmul(adj_t, x, reduce='add')`` on the HIP kernels.
+
+    A partitioned adjacency (lpgnn.partition.PartitionedCSR) runs its local
+    SpMM plus the boundary exchange."""
+    f = getattr(adj, "partitioned_spmm", None)
+    if f is not None:
+        return f(x)
     return _SpMM.apply(x, adj)

@@ -55,6 +55,9 @@ def lib():
         L.oracle_spmm_bf16.argtypes = [i64, p, p, p, p, i64, i64, p, i64, ctypes.c_int]
         L.oracle_spmm_bf16.restype = None
         L.oracle_max_threads.restype = ctypes.c_int
+        L.oracle_fc_f32.argtypes = [i64, i64, i64, p, i64, p, i64, i64, p, i64, p, i64, p, p, i64, ctypes.c_int,
+                                    ctypes.c_int]
+        L.oracle_fc_f32.restype = None
         _LIB = L
     return _LIB
 
@@ -89,6 +92,25 @@ def spmm_bf16(rowptr, col, val, Xbits, nthreads: int = 0) -> np.ndarray:
     if M > 0 and Fd > 0:
         lib().oracle_spmm_bf16(M, _ptr(rowptr), _ptr(col), _ptr(val), _ptr(Xbits), Fd, Fd, _ptr(Y), Fd, nthreads)
     return Y
+
+
+def fc_kchain(A1, W1, A2=None, W2=None, bias=None, relu=False, nthreads: int = 0) -> np.ndarray:
+    """lin_rel(A1) + lin_root(A2) [+ ReLU] as lpg_fc_f32 evaluates it: one
+    fp32 fma chain per output in k order (A1 part then A2 part) from +0, then
+    + bias (fc_ref.c).  Arrays are numpy/torch fp32; weights [out, in]."""
+    f = lambda t: None if t is None else np.ascontiguousarray(
+        t.detach().numpy() if isinstance(t, torch.Tensor) else t, dtype=np.float32)
+    A1, W1, A2, W2, bias = f(A1), f(W1), f(A2), f(W2), f(bias)
+    M, K1 = A1.shape
+    N = W1.shape[0]
+    K2 = 0 if A2 is None else A2.shape[1]
+    C = np.empty((M, N), np.float32)
+    if M and N:
+        z = np.zeros(1, np.float32)
+        lib().oracle_fc_f32(M, N, K1, _ptr(A1), K1, _ptr(W1), K1, K2, _ptr(A2 if K2 else z), max(K2, 1),
+                            _ptr(W2 if K2 else z), max(K2, 1), None if bias is None else _ptr(bias), _ptr(C), N,
+                            int(relu), nthreads)
+    return C
 
 
 # --------------------------------------------------------------------------
@@ -147,20 +169,27 @@ def spmm_t(csr, csr_t, X: torch.Tensor) -> torch.Tensor:
     return _OracleSpMM.apply(X, csr, csr_t)
 
 
-def graph_conv(x_src, x_dst, adj, adj_t, W_rel, b_rel, W_root):
+def graph_conv(x_src, x_dst, adj, adj_t, W_rel, b_rel, W_root, fc="mkl", relu=False):
     """PyG 2.1 GraphConv.forward with a SparseTensor adj_t (aggr='add'):
 
     out = propagate(...)      -> message_and_aggregate = matmul(adj_t, x[0], 'add')
     out = self.lin_rel(out)   -> F.linear(out, W_rel, b_rel)
     out += self.lin_root(x[1])-> F.linear(x_dst, W_root)   (lin_root: bias=False)
+
+    fc="mkl": torch CPU F.linear (the reference's own evaluation, autograd);
+    fc="kchain": the bitwise order of lpg_fc_f32 (forward only).
+    relu: the following ReLU (arch.py:182/188) applied here.
     """
     agg = spmm_t(adj, adj_t, x_src)
+    if fc == "kchain":
+        out = torch.from_numpy(fc_kchain(agg, W_rel, x_dst, W_root, b_rel, relu=relu))
+        return out, agg
     out = F.linear(agg, W_rel, b_rel)
     out = out + F.linear(x_dst, W_root)
-    return out, agg
+    return (torch.relu(out) if relu else out), agg
 
 
-def conv_two_direction(sd, prefix, left, right, A, AT):
+def conv_two_direction(sd, prefix, left, right, A, AT, fc="mkl", relu=False):
     """GraphConvTwoDirection.forward, arch.py:65-81.
 
     l2r, r2l = edge_index, edge_index.t(); l2r, r2l = r2l, l2r  (arch.py:71-74)
@@ -169,9 +198,9 @@ def conv_two_direction(sd, prefix, left, right, A, AT):
     """
     g = lambda d, k: sd[f"{prefix}.{d}.{k}"]
     right_new, agg_r = graph_conv(left, right, AT, A, g("left2right", "lin_rel.weight"),
-                                  g("left2right", "lin_rel.bias"), g("left2right", "lin_root.weight"))
+                                  g("left2right", "lin_rel.bias"), g("left2right", "lin_root.weight"), fc, relu)
     left_new, agg_l = graph_conv(right, left, A, AT, g("right2left", "lin_rel.weight"),
-                                 g("right2left", "lin_rel.bias"), g("right2left", "lin_root.weight"))
+                                 g("right2left", "lin_rel.bias"), g("right2left", "lin_root.weight"), fc, relu)
     return left_new, right_new, agg_l, agg_r
 
 
@@ -188,24 +217,28 @@ def add_knowledge(left_logit, right_logit, left_feas, right_feas, bound=10):
     return left_logit, right_logit
 
 
-def gcn_fc_forward(sd, x_s, x_t, A, AT, depth: int, keep=None):
+def gcn_fc_forward(sd, x_s, x_t, A, AT, depth: int, keep=None, fc="mkl"):
     """GCN_FC.forward, arch.py:179-193, eval mode (dropout is identity).
 
     sd: state_dict (tensors), A/AT: (rowptr, col, val) CSR of A and A^T.
     keep: optional dict that receives per-layer intermediates.
+    fc: "mkl" (torch CPU F.linear, differentiable) or "kchain" (bitwise order
+    of the HIP FC kernel, forward only).
     """
-    left, right, agg_l, agg_r = conv_two_direction(sd, "conv1", x_s, x_t, A, AT)
-    left, right = torch.relu(left), torch.relu(right)
+    left, right, agg_l, agg_r = conv_two_direction(sd, "conv1", x_s, x_t, A, AT, fc, relu=True)
     if keep is not None:
         keep["agg_l0"], keep["agg_r0"], keep["left0"], keep["right0"] = agg_l, agg_r, left, right
     for i in range(depth - 2):
-        left, right, agg_l, agg_r = conv_two_direction(sd, f"layers.{i}", left, right, A, AT)
-        left, right = torch.relu(left), torch.relu(right)
+        left, right, agg_l, agg_r = conv_two_direction(sd, f"layers.{i}", left, right, A, AT, fc, relu=True)
         if keep is not None:
             keep[f"agg_l{i+1}"], keep[f"agg_r{i+1}"] = agg_l, agg_r
             keep[f"left{i+1}"], keep[f"right{i+1}"] = left, right
-    left = F.linear(left, sd["lin_left.weight"], sd["lin_left.bias"])
-    right = F.linear(right, sd["lin_right.weight"], sd["lin_right.bias"])
+    if fc == "kchain":
+        left = torch.from_numpy(fc_kchain(left, sd["lin_left.weight"], bias=sd["lin_left.bias"]))
+        right = torch.from_numpy(fc_kchain(right, sd["lin_right.weight"], bias=sd["lin_right.bias"]))
+    else:
+        left = F.linear(left, sd["lin_left.weight"], sd["lin_left.bias"])
+        right = F.linear(right, sd["lin_right.weight"], sd["lin_right.bias"])
     if keep is not None:
         keep["head_l"], keep["head_r"] = left, right
     return add_knowledge(left, right, x_s, x_t)
