@@ -9,7 +9,8 @@
 //
 // Numerics (the parity contract, mirrored by oracle/fc_ref.c): every output
 // is ONE fp32 fma chain in k order, k = 0..K1-1 over (A1, W1) then
-// k = 0..K2-1 over (A2, W2), starting from +0, then one add of the bias,
+// k = 0..K2-1 over (A2, W2), starting from +0 (the zero padding of each part
+// to a whole k-tile adds fma(0, 0, acc) = acc exactly), then one add of the bias,
 // then ReLU as (v < 0 ? 0 : v).  v_mfma_f32_32x32x2_f32 is bit-for-bit such a
 // chain (k0 then k1 of each pair; MI355X_MICROARCH.md §Matrix cores), and
 // the accumulator of an output tile visits the k-tiles in increasing order.
@@ -41,14 +42,15 @@ struct FcArgs {
   int64_t mt, nt;  // tiles
 };
 
-// Load one row-chunk of 4 consecutive k of the virtual [X1 | X2] matrix.
-__device__ __forceinline__ float4 load_k4(const float *X1, int64_t ld1, int64_t K1, const float *X2, int64_t ld2,
-                                          int64_t K2, int64_t r, int64_t R, int64_t k) {
-  if (r >= R) return make_float4(0.f, 0.f, 0.f, 0.f);
-  if (k < K1) return *reinterpret_cast<const float4 *>(X1 + r * ld1 + k);
-  k -= K1;
-  if (k < K2) return *reinterpret_cast<const float4 *>(X2 + r * ld2 + k);
-  return make_float4(0.f, 0.f, 0.f, 0.f);
+// Branch-free load of 4 consecutive k of row r of X (R rows, K columns):
+// the address is clamped into range.  Rows >= R only feed outputs that are
+// never stored, so they are left as whatever row R-1 holds; k >= K is zeroed
+// later (sstore), only in the partial last k-tile of a phase.  (A conditional
+// load -- or a select right after it -- makes hipcc wait vmcnt per load.)
+__device__ __forceinline__ float4 load_k4(const float *X, int64_t ld, int64_t R, int64_t K, int64_t r, int64_t k) {
+  const int64_t rr = r < R ? r : R - 1;
+  const int64_t kk = k < K ? k : K - 4;
+  return *reinterpret_cast<const float4 *>(X + rr * ld + kk);
 }
 
 template <int WAVES_M, int WAVES_N, int TM, int TN, bool RELU>
@@ -76,8 +78,10 @@ __global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int64_t K = a.K1 + a.K2;
-  const int nk = (int)((K + BK - 1) / BK);
+  // Two uniform phases of k-tiles: (A1, W1) over K1, then (A2, W2) over K2,
+  // each zero-padded to a multiple of BK (zeros are exact no-ops in the chain).
+  const int nk1 = (int)((a.K1 + BK - 1) / BK);
+  const int nk = nk1 + (int)((a.K2 + BK - 1) / BK);
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -89,19 +93,34 @@ __global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
 
   float4 ra[LA], rb[LB];
   auto gload = [&](int t) {
-    const int64_t k0 = (int64_t)t * BK;
+    const bool p2 = t >= nk1;  // wave-uniform phase select
+    const float *A = p2 ? a.A2 : a.A1;
+    const float *W = p2 ? a.W2 : a.W1;
+    const int64_t lda = p2 ? a.lda2 : a.lda1, ldw = p2 ? a.ldw2 : a.ldw1, Kp = p2 ? a.K2 : a.K1;
+    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + 256 * i;
-      ra[i] = load_k4(a.A1, a.lda1, a.K1, a.A2, a.lda2, a.K2, m0 + idx / 8, a.M, k0 + (idx % 8) * 4);
+      ra[i] = load_k4(A, lda, a.M, Kp, m0 + idx / 8, k0 + (idx % 8) * 4);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + 256 * i;
-      rb[i] = load_k4(a.W1, a.ldw1, a.K1, a.W2, a.ldw2, a.K2, n0 + idx / 8, a.N, k0 + (idx % 8) * 4);
+      rb[i] = load_k4(W, ldw, a.N, Kp, n0 + idx / 8, k0 + (idx % 8) * 4);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, int t) {
+    const bool p2 = t >= nk1;
+    const int64_t Kp = p2 ? a.K2 : a.K1;
+    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
+    if (k0 + BK > Kp) {  // wave-uniform: partial k-tile, zero k >= Kp in both operands
+#pragma unroll
+      for (int i = 0; i < LA; ++i)
+        if (k0 + ((tid + 256 * i) % 8) * 4 >= Kp) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < LB; ++i)
+        if (k0 + ((tid + 256 * i) % 8) * 4 >= Kp) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + 256 * i;
@@ -117,7 +136,7 @@ __global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
   };
 
   gload(0);
-  sstore(0);
+  sstore(0, 0);
   __syncthreads();
   const int fr = lane & 31, fk = lane >> 5;
   for (int t = 0; t < nk; ++t) {
@@ -137,7 +156,7 @@ __global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < nk) sstore(buf ^ 1);
+    if (t + 1 < nk) sstore(buf ^ 1, t + 1);
     __syncthreads();
   }
 

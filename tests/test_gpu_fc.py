@@ -98,7 +98,7 @@ def test_knowledge_bitwise_vs_torch_cpu():
     logit[:5] = 0.0  # eps clamp path
     logit[5] = [1e-20, -1e-20, 3e-21]
     feas = np.zeros((M, 8), np.float32)
-    feas[:, 5] = -(rng.random(M) < 0.5)
+    feas[:, 5] = -(rng.random(M) < 0.5).astype(np.float32)
     feas[:, 7] = rng.random(M) < 0.5
     got = knowledge(torch.from_numpy(logit).to(DEV), torch.from_numpy(feas).to(DEV)).cpu()
     ref, _ = O.add_knowledge(torch.from_numpy(logit), torch.from_numpy(logit[:1]), torch.from_numpy(feas),

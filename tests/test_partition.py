@@ -1,0 +1,131 @@
+"""Constraint-row partitioning (lpgnn.partition) with gloo, world size 2, on
+CPU.  The product's local compute (HIP SpMM / FC / knowledge kernels) is
+swapped for the oracle so the distributed logic -- plan, boundary
+all-reduce and its backward, distributed balanced loss, gradient
+all-reduce -- is checked against the single-graph oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from oracle import model_ref as O
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _graph():
+    from lpgnn import synth
+
+    return synth.block_lp(240, 480, 2400, parts=2, rho=0.15, seed=2)
+
+
+def test_plan_invariants():
+    from lpgnn.partition import plan_partition
+
+    g = _graph()
+    for world in (1, 2, 3, 4):
+        plans = [plan_partition(g.row, g.col, g.val, g.m, g.n, world, r) for r in range(world)]
+        # cons blocks tile [0, m)
+        assert plans[0].row_lo == 0 and plans[-1].row_hi == g.m
+        for a, b in zip(plans, plans[1:]):
+            assert a.row_hi == b.row_lo
+        # every edge lands on exactly one rank
+        assert sum(p.nnz_local for p in plans) == g.nnz
+        # every variable owned exactly once; boundary set replicated everywhere
+        owned = np.concatenate([p.local_vars[p.var_owned] for p in plans])
+        assert np.array_equal(np.sort(owned), np.arange(g.n))
+        bsets = [set(p.local_vars[p.boundary].tolist()) for p in plans]
+        assert all(s == bsets[0] for s in bsets)
+        assert len(bsets[0]) == plans[0].n_boundary_global
+        # local numbering is monotone in global ids (keeps per-row edge order)
+        for p in plans:
+            assert np.all(np.diff(p.local_vars) > 0)
+            # reconstruct the global edges of this block
+            gr = p.e_row + p.row_lo
+            gc = p.local_vars[p.e_col]
+            sel = (g.row >= p.row_lo) & (g.row < p.row_hi)
+            assert np.array_equal(np.sort(gr * g.n + gc), np.sort(g.row[sel] * g.n + g.col[sel]))
+
+
+# ------------------------------------------------------- oracle-backed doubles
+def _cpu_local_spmm(adj, x):
+    fwd = (adj.fwd.rowptr.numpy(), adj.fwd.col.numpy(), adj.fwd.val.numpy())
+    bwd = (adj.bwd.rowptr.numpy(), adj.bwd.col.numpy(), adj.bwd.val.numpy())
+    return O.spmm_t(fwd, bwd, x)
+
+
+def _cpu_graph_conv_fc(agg, x_dst, w_rel, b_rel, w_root, relu):
+    out = F.linear(agg, w_rel, b_rel) + F.linear(x_dst, w_root)
+    return torch.relu(out) if relu else out
+
+
+def _cpu_knowledge(logit, feas, bound=10):
+    l, _ = O.add_knowledge(logit, logit[:1], feas, feas[:1], bound)
+    return l
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    try:
+        import lpgnn.fc as fc
+        import lpgnn.partition as part
+        from lpgnn import GCN_FC
+
+        part._local_spmm = _cpu_local_spmm
+        fc.graph_conv_fc = _cpu_graph_conv_fc
+        fc.linear = lambda x, w, b: F.linear(x, w, b)
+        fc.knowledge = _cpu_knowledge
+
+        g = _graph()
+        plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
+        batch = part.make_local_batch(plan, g.x_s, g.x_t, g.y_s, g.y_t, device="cpu")
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=16, depth=4, dp=0.0)
+        sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        model.train()
+        lc, lv = model(batch)
+        loss = part.balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.var_owned)
+        model.zero_grad()
+        loss.backward()
+        part.all_reduce_grads(model)
+        tot = loss.detach().clone()
+        dist.all_reduce(tot)
+
+        # single-graph oracle
+        A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
+        AT = O.csr_transpose(*A, g.m, g.n)
+        params = {k: v.clone().requires_grad_(True) for k, v in sd0.items()}
+        rc, rv = O.gcn_fc_forward(params, torch.from_numpy(g.x_s), torch.from_numpy(g.x_t), A, AT, 4)
+        rloss = O.balanced(rc, rv, torch.from_numpy(g.y_s), torch.from_numpy(g.y_t))
+        rloss.backward()
+
+        np.testing.assert_allclose(lc.detach().numpy(), rc.detach().numpy()[plan.row_lo:plan.row_hi], atol=2e-5)
+        own = plan.var_owned
+        np.testing.assert_allclose(lv.detach().numpy()[own], rv.detach().numpy()[plan.local_vars[own]], atol=2e-5)
+        # replicated boundary rows agree with the full graph too
+        b = plan.boundary
+        np.testing.assert_allclose(lv.detach().numpy()[b], rv.detach().numpy()[plan.local_vars[b]], atol=2e-5)
+        assert abs(tot.item() - rloss.item()) < 1e-4, (tot.item(), rloss.item())
+        for k, p in model.named_parameters():
+            np.testing.assert_allclose(p.grad.numpy(), params[k].grad.numpy(), rtol=1e-3, atol=1e-5, err_msg=k)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write(f"{tot.item()} {plan.n_boundary_global}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_partitioned_training_step_matches_single_graph(tmp_path, world):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").exists()

@@ -40,6 +40,7 @@ for s in $STAGES; do
       step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python "$ROOT/bench.py" --steps 5 --warmup 2 --profile-only
       ;;
+    kbench) step kbench 600 python tools/kbench.py ;;
     pmc)
       step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
         python "$ROOT/bench.py" --steps 3 --warmup 1 --profile-only

@@ -1,0 +1,113 @@
+"""Kernel microbenchmarks on one GPU (HIP events, interleaved rounds, median).
+
+  python tools/kbench.py [fc] [spmm] [bwd]
+
+fc   : lpg_fc_f32 at the c2 shapes vs torch (hipBLASLt) linear+linear+add+relu
+spmm : lpg_spmm_f32 at c2, both directions, slice widths 256/512/1024
+bwd  : the FC backward GEMMs at c2 shapes through torch (hipBLASLt)
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "lp-gnn_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+
+def timeit(fns, rounds=7, iters=5):
+    """fns: {name: callable}; returns {name: median ms per call}."""
+    res = {k: [] for k in fns}
+    for fn in fns.values():
+        fn()
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k, fn in fns.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            res[k].append(e0.elapsed_time(e1) / iters)
+    return {k: float(np.median(v)) for k, v in res.items()}
+
+
+def bench_fc(out):
+    from lpgnn.fc import fc_forward
+
+    dev = "cuda"
+    for M, K in ((200_000, 1024), (100_000, 1024)):
+        A1 = torch.randn(M, K, device=dev)
+        A2 = torch.randn(M, K, device=dev)
+        W1 = torch.randn(1024, K, device=dev) * 0.03
+        W2 = torch.randn(1024, K, device=dev) * 0.03
+        b = torch.randn(1024, device=dev)
+        flops = 2.0 * M * 1024 * 2 * K
+        t = timeit({
+            "lpg_fc_f32": lambda: fc_forward(A1, W1, A2, W2, b, True),
+            "torch_2gemm_add_relu": lambda: torch.relu(F.linear(A1, W1, b) + F.linear(A2, W2)),
+            "torch_1gemm_K2048": lambda: F.linear(torch.cat([A1, A2], 1) if False else A1, torch.cat([W1], 1), b),
+        })
+        for k, v in t.items():
+            f = flops if k != "torch_1gemm_K2048" else flops / 2
+            out[f"fc M={M} K={2*K} {k}"] = dict(ms=v, tflops=f / v / 1e9)
+        # heads and conv1
+        H = torch.randn(M, 1024, device=dev)
+        Wh = torch.randn(3, 1024, device=dev)
+        bh = torch.randn(3, device=dev)
+        X8 = torch.randn(M, 8, device=dev)
+        W8 = torch.randn(1024, 8, device=dev)
+        t = timeit({"heads": lambda: fc_forward(H, Wh, None, None, bh, False),
+                    "conv1": lambda: fc_forward(X8, W8, X8, W8, b, True)})
+        out[f"fc heads M={M}"] = dict(ms=t["heads"], gbs=M * 1024 * 4 / t["heads"] / 1e6)
+        out[f"fc conv1 M={M}"] = dict(ms=t["conv1"], gbs=M * 1024 * 4 / t["conv1"] / 1e6)
+
+
+def bench_bwd(out):
+    dev = "cuda"
+    for M in (200_000, 100_000):
+        g = torch.randn(M, 1024, device=dev)
+        W = torch.randn(1024, 1024, device=dev)
+        A = torch.randn(M, 1024, device=dev)
+        fl = 2.0 * M * 1024 * 1024
+        t = timeit({"dA=g@W": lambda: g @ W, "dW=g.t()@A": lambda: g.t() @ A,
+                    "mask": lambda: g.masked_fill(A <= 0, 0.0), "colsum": lambda: g.sum(0)})
+        for k, v in t.items():
+            out[f"bwd M={M} {k}"] = dict(ms=v, tflops=fl / v / 1e9 if "@" in k else None)
+
+
+def bench_spmm(out):
+    from lpgnn import BipartiteCSR, _lib, synth
+    from lpgnn.sparse import spmm_forward
+
+    g = synth.uniform_lp(100_000, 200_000, 2_000_000, seed=0)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
+    L = _lib.lib()
+    for name, csr, K in (("cons<-vars", adj.fwd, g.n), ("vars<-cons", adj.bwd, g.m)):
+        X = torch.randn(K, 1024, device="cuda")
+        fns = {}
+        for sl in (1024, 512, 256):
+            def f(sl=sl):
+                L.lpg_spmm_set_slice(sl)
+                return spmm_forward(csr, X)
+            fns[f"slice{sl}"] = f
+        t = timeit(fns)
+        L.lpg_spmm_set_slice(0)
+        B = g.nnz * 1024 * 4 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 1024 * 4
+        for k, v in t.items():
+            out[f"spmm {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["fc", "spmm", "bwd"]
+    out = {}
+    for w in which:
+        {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd}[w](out)
+        torch.cuda.empty_cache()
+    for k, v in out.items():
+        print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "kbench.json"), "w"), indent=1)
