@@ -113,12 +113,20 @@ lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  * flags: bit 0 = ReLU epilogue (arch.py:182, 188).  bias may be NULL.
  * Row-major fp32, leading dimensions in floats; K1, K2 and the A/W leading
  * dimensions multiples of 4, A/W 16-byte aligned.
- * Numerics: one fp32 fma chain per output in k order (A1 part, then A2
- * part) from +0, then + bias -- bitwise reproducible, see oracle/fc_ref.c. */
+ * Numerics (bitwise reproducible, see oracle/fc_ref.c): each part (A1 over
+ * K1, then A2 over K2) is cut into k-blocks of 32; a block's products form
+ * one fp32 fma chain in k order from +0, the block sums are added in order
+ * into the running total (+0 initially), then + bias, then ReLU. */
 lpg_status lpg_fc_f32(int64_t M, int64_t N,
                       int64_t K1, const float *A1, int64_t lda1, const float *W1, int64_t ldw1,
                       int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2,
                       const float *bias, float *C, int64_t ldc, int32_t flags, void *stream);
+
+/* Tuning knob for lpg_fc_f32 (process-global, default 0): output tile
+ * variant, 0 = 128x128 (4 waves, 2 blocks/CU), 1 = 256x128 (8 waves),
+ * 2 = 128x256 (8 waves), 3 = 128x128 with 64-deep k staging.  Every variant
+ * produces bitwise identical results (same numerics blocks). */
+lpg_status lpg_fc_set_variant(int32_t variant);
 
 /* add_knowledge for one side (arch.py:129-141): out = normalize(logit) * 10,
  * then out[:,0] -= bound where feas[:, cols-3] != 0 (infinite lower bound)

@@ -32,8 +32,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 32;
-constexpr int LDK = BK + 1;
+constexpr int NB = 32;  // numerics block: k-tile length of one fma chain (the parity contract)
 
 struct FcArgs {
   int64_t M, N, K1, K2;
@@ -55,14 +54,19 @@ __device__ __forceinline__ float4 load_k4(const float *X, int64_t ld, int64_t R,
   return *reinterpret_cast<const float4 *>(X + rr * ld + kk);
 }
 
-template <int WAVES_M, int WAVES_N, int TM, int TN, bool RELU>
-__global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
+// WAVES_M x WAVES_N waves, each owning TM x TN blocks of 32x32; BK = staging
+// k-tile (a multiple of the numerics block NB; chains restart every NB).
+template <int WAVES_M, int WAVES_N, int TM, int TN, int BK, bool RELU>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32(FcArgs a) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * TM * 32;
   constexpr int BN = WAVES_N * TN * 32;
-  constexpr int LA = BM * 8 / 256;  // float4 loads per thread per k-tile
-  constexpr int LB = BN * 8 / 256;
-  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
-  static_assert(LA >= 1 && LB >= 1, "tile too small");
+  constexpr int LDK = BK + 1;
+  constexpr int C4 = BK / 4;         // float4 chunks per staged row
+  constexpr int LA = BM * C4 / NT;  // float4 loads per thread per k-tile
+  constexpr int LB = BN * C4 / NT;
+  static_assert(BK % NB == 0, "BK must be a multiple of NB");
+  static_assert(LA >= 1 && LB >= 1 && BM * C4 % NT == 0 && BN * C4 % NT == 0, "tile/thread mismatch");
   __shared__ float smem[2 * (BM + BN) * LDK];
   // buffer b: A tile at smem + b*(BM+BN)*LDK, W tile right after it
   auto As = [&](int b) { return smem + b * (BM + BN) * LDK; };
@@ -103,13 +107,13 @@ __global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
     const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-      const int idx = tid + 256 * i;
-      ra[i] = load_k4(A, lda, a.M, Kp, m0 + idx / 8, k0 + (idx % 8) * 4);
+      const int idx = tid + NT * i;
+      ra[i] = load_k4(A, lda, a.M, Kp, m0 + idx / C4, k0 + (idx % C4) * 4);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const int idx = tid + 256 * i;
-      rb[i] = load_k4(W, ldw, a.N, Kp, n0 + idx / 8, k0 + (idx % 8) * 4);
+      const int idx = tid + NT * i;
+      rb[i] = load_k4(W, ldw, a.N, Kp, n0 + idx / C4, k0 + (idx % C4) * 4);
     }
   };
   auto sstore = [&](int buf, int t) {
@@ -119,21 +123,21 @@ __global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
     if (k0 + BK > Kp) {  // wave-uniform: partial k-tile, zero k >= Kp in both operands
 #pragma unroll
       for (int i = 0; i < LA; ++i)
-        if (k0 + ((tid + 256 * i) % 8) * 4 >= Kp) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k0 + ((tid + NT * i) % C4) * 4 >= Kp) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int i = 0; i < LB; ++i)
-        if (k0 + ((tid + 256 * i) % 8) * 4 >= Kp) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k0 + ((tid + NT * i) % C4) * 4 >= Kp) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-      const int idx = tid + 256 * i;
-      float *p = As(buf) + (idx / 8) * LDK + (idx % 8) * 4;
+      const int idx = tid + NT * i;
+      float *p = As(buf) + (idx / C4) * LDK + (idx % C4) * 4;
       p[0] = ra[i].x; p[1] = ra[i].y; p[2] = ra[i].z; p[3] = ra[i].w;
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const int idx = tid + 256 * i;
-      float *p = Bs(buf) + (idx / 8) * LDK + (idx % 8) * 4;
+      const int idx = tid + NT * i;
+      float *p = Bs(buf) + (idx / C4) * LDK + (idx % C4) * 4;
       p[0] = rb[i].x; p[1] = rb[i].y; p[2] = rb[i].z; p[3] = rb[i].w;
     }
   };
@@ -159,12 +163,15 @@ __global__ __launch_bounds__(256) void fc_fwd_f32(FcArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], s == 0 ? zero : part[i][j], 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], s % (NB / 2) == 0 ? zero : part[i][j],
+                                                             0, 0, 0);
+      if (s % (NB / 2) == NB / 2 - 1) {  // end of a numerics block: fold into the total
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
+      }
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
     if (t + 1 < nk) sstore(buf ^ 1, t + 1);
     __syncthreads();
   }
@@ -213,21 +220,23 @@ __global__ __launch_bounds__(256) void knowledge_f32(int64_t M, const float *__r
   out[m * ldo + 2] = y2;
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int BK>
 lpg_status launch_fc(const FcArgs &a0, bool relu, hipStream_t s) {
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
   FcArgs a = a0;
   a.mt = (a.M + BM - 1) / BM;
   a.nt = (a.N + BN - 1) / BN;
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_f32: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, BK, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, BK, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
+
+int g_fc_variant = 0;  // lpg_fc_set_variant; 0 = default tile
 
 }  // namespace
 }  // namespace lpg
@@ -250,8 +259,19 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
   FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0};
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
-  if (N <= 32) return launch_fc<4, 1, 1, 1>(a, relu, s);   // heads (N = 3): 128 x 32 tiles
-  return launch_fc<2, 2, 2, 2>(a, relu, s);                // 128 x 128 tiles
+  if (N <= 32) return launch_fc<4, 1, 1, 1, 32>(a, relu, s);  // heads (N = 3): 128 x 32 tiles
+  switch (g_fc_variant) {
+    case 1: return launch_fc<4, 2, 2, 2, 32>(a, relu, s);  // 256 x 128, 8 waves
+    case 2: return launch_fc<2, 4, 2, 2, 32>(a, relu, s);  // 128 x 256, 8 waves
+    case 3: return launch_fc<2, 2, 2, 2, 64>(a, relu, s);  // 128 x 128, BK 64 (1 block / CU)
+    default: return launch_fc<2, 2, 2, 2, 32>(a, relu, s); // 128 x 128, BK 32, 2 blocks / CU
+  }
+}
+
+extern "C" lpg_status lpg_fc_set_variant(int32_t v) {
+  LPG_REQUIRE(v >= 0 && v <= 3, "lpg_fc_set_variant: variant %d not in [0, 3]", v);
+  g_fc_variant = v;
+  return LPG_OK;
 }
 
 extern "C" lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t ldl, const float *feas, int64_t ldf,

@@ -29,6 +29,7 @@ HEADER_SYMBOLS = (
     "lpg_spmm_bf16",
     "lpg_spmm_set_slice",
     "lpg_fc_f32",
+    "lpg_fc_set_variant",
     "lpg_knowledge_f32",
 )
 
@@ -68,6 +69,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
                              c_p, c_p, c_i64, c_i32, c_p]
     L.lpg_fc_f32.restype = c_i32
+    L.lpg_fc_set_variant.argtypes = [c_i32]
+    L.lpg_fc_set_variant.restype = c_i32
     L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_i64, ctypes.c_float, c_p, c_i64, c_p]
     L.lpg_knowledge_f32.restype = c_i32
     _lib = L

@@ -47,11 +47,23 @@ def bench_fc(out):
         W2 = torch.randn(1024, K, device=dev) * 0.03
         b = torch.randn(1024, device=dev)
         flops = 2.0 * M * 1024 * 2 * K
+        from lpgnn import _lib
+        L = _lib.lib()
+
+        def var(v):
+            def f():
+                L.lpg_fc_set_variant(v)
+                return fc_forward(A1, W1, A2, W2, b, True)
+            return f
+        y0 = var(0)()
+        for v in (1, 2, 3):
+            assert torch.equal(var(v)(), y0), f"variant {v} differs"
         t = timeit({
-            "lpg_fc_f32": lambda: fc_forward(A1, W1, A2, W2, b, True),
+            **{f"lpg_fc_f32 v{v}": var(v) for v in range(4)},
             "torch_2gemm_add_relu": lambda: torch.relu(F.linear(A1, W1, b) + F.linear(A2, W2)),
             "torch_1gemm_K2048": lambda: F.linear(torch.cat([A1, A2], 1) if False else A1, torch.cat([W1], 1), b),
         })
+        L.lpg_fc_set_variant(0)
         for k, v in t.items():
             f = flops if k != "torch_1gemm_K2048" else flops / 2
             out[f"fc M={M} K={2*K} {k}"] = dict(ms=v, tflops=f / v / 1e9)
