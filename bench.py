@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--rho", type=float, default=0.02, help="boundary edge fraction for N>1 partitions")
     ap.add_argument("--cpu-steps", type=int, default=1, help="oracle CPU steps for cpu_baseline (0 = skip)")
     ap.add_argument("--profile-only", action="store_true", help="no CPU baseline, no JSON extras (rocprof runs)")
+    ap.add_argument("--print-workload", action="store_true", help="print the N=1 workload string and exit")
     return ap.parse_args()
 
 
@@ -96,8 +97,16 @@ def cpu_baseline(g, hids, depth, steps):
     return dt, threads
 
 
+def workload_name(args) -> str:
+    return (f"c2: synthetic LP {args.m}x{args.n} nnz={args.nnz}, GCN_FC(8,8,hids={args.hids},depth={args.depth}) "
+            f"fwd+bwd+Adam")
+
+
 def main():
     args = parse()
+    if args.print_workload:
+        print(workload_name(args))
+        return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -126,7 +135,7 @@ def main():
         opt, _ = make_optimizer(model)
         step = lambda: train_step(model, batch, opt)
         local_nnz = g.nnz
-        workload = f"c2: synthetic LP {args.m}x{args.n} nnz={args.nnz}, GCN_FC(8,8,hids={args.hids},depth={args.depth}) fwd+bwd+Adam"
+        workload = workload_name(args)
         parallelism = "single"
     else:
         from lpgnn import partition

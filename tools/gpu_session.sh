@@ -41,11 +41,14 @@ for s in $STAGES; do
         python "$ROOT/bench.py" --steps 5 --warmup 2 --profile-only
       ;;
     kbench) step kbench 600 python tools/kbench.py ;;
+    kbfc) step kbench_fc 600 python tools/kbench.py fc ;;
     pmc)
       step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
         python "$ROOT/bench.py" --steps 3 --warmup 1 --profile-only
       step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
         python "$ROOT/bench.py" --steps 3 --warmup 1 --profile-only
+      python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_spmm.json" \
+        "$(python bench.py --print-workload)" || true
       ;;
     *) echo "unknown stage $s"; exit 2 ;;
   esac

@@ -1,0 +1,60 @@
+"""HBM traffic per launch of the hot kernels from two rocprofv3 --pmc runs
+(FETCH_SIZE and WRITE_SIZE in separate passes, as MI355X_MICROARCH.md
+§HBM / rocprofv3 prescribes), with the gfx950 correction: FETCH_SIZE counts
+exactly half the bytes of a wide (16 B/lane) coalesced read, so it is
+doubled; both counters are in KiB.
+
+  python tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/r01_pmc_spmm.json "<workload>"
+
+Writes {"workload", "kernels": {name: {...}}, "hbm_bytes_per_launch"} where
+the last field is the F=hid SpMM kernel's mean (what bench.py reports as
+roofline.traffic).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def read_counter(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
+    per = defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return per
+
+
+def main(fetch_dir, write_dir, out, workload):
+    fetch = read_counter(fetch_dir, "FETCH_SIZE")
+    write = read_counter(write_dir, "WRITE_SIZE")
+    res = {}
+    for name in sorted(set(fetch) | set(write)):
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        if not f or not w:
+            continue
+        fk = sum(f) / len(f)
+        wk = sum(w) / len(w)
+        res[name[:200]] = dict(dispatches=len(f), fetch_kib_raw=fk, write_kib=wk,
+                               hbm_bytes=(2 * fk + wk) * 1024.0)
+    spmm = [v for k, v in res.items() if "spmm_f32_rowwave" in k]
+    hbm = None
+    if spmm:
+        # the rowwave kernel runs only at F = hid in the bench step
+        tot = sum(v["hbm_bytes"] * v["dispatches"] for v in spmm)
+        hbm = tot / sum(v["dispatches"] for v in spmm)
+    json.dump(dict(workload=workload, correction="hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH halving)",
+                   hbm_bytes_per_launch=hbm, kernels=res), open(out, "w"), indent=1)
+    for k, v in res.items():
+        if v["hbm_bytes"] > 1e8:
+            print(f"{v['hbm_bytes'] / 1e9:8.3f} GB/launch  x{v['dispatches']:3d}  {k[:100]}")
+    print("spmm hbm bytes per launch:", hbm)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:5])
