@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=1, help="oracle CPU steps for cpu_baseline (0 = skip)")
     ap.add_argument("--profile-only", action="store_true", help="no CPU baseline, no JSON extras (rocprof runs)")
     ap.add_argument("--print-workload", action="store_true", help="print the N=1 workload string and exit")
+    ap.add_argument("--partitioned", action="store_true",
+                    help="use the row-partitioned RCCL path even at N=1 (the N>1 code path)")
     return ap.parse_args()
 
 
@@ -114,17 +116,20 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or args.partitioned
+    if distributed:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     import lpgnn
     from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
     from lpgnn.timing import TIMER
     from lpgnn.train import make_optimizer, train_step
 
-    if world == 1:
+    if not distributed:
         g = synth.uniform_lp(args.m, args.n, args.nnz, seed=0)
         adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
         batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(dev), x_t=torch.from_numpy(g.x_t).to(dev),
@@ -147,7 +152,7 @@ def main():
 
     def sync():
         torch.cuda.synchronize()
-        if world > 1:
+        if distributed:
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
@@ -173,7 +178,7 @@ def main():
     edges_local = launches * local_nnz / args.steps  # per step
     t = torch.tensor([dt], device=dev)
     e = torch.tensor([edges_local], device=dev, dtype=torch.float64)
-    if world > 1:
+    if distributed:
         import torch.distributed as dist
 
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -220,7 +225,7 @@ def main():
                                "s_per_step": cdt}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         torch.distributed.destroy_process_group()
 
 

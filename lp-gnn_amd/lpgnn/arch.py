@@ -82,13 +82,21 @@ class GraphConv(nn.Module):
         self.lin_rel.reset_parameters()
         self.lin_root.reset_parameters()
 
-    def forward(self, x, edge_index: BipartiteCSR, edge_weight=None, size=None, relu: bool = False) -> Tensor:
+    def forward(self, x, edge_index: BipartiteCSR, edge_weight=None, size=None, relu: bool = False,
+                dropout: float = 0.0) -> Tensor:
         if isinstance(x, Tensor):
             x = (x, x)
         if edge_weight is not None:
             raise NotImplementedError("edge weights come from the adjacency values (arch.py:77)")
-        agg = spmm(edge_index, x[0])  # message_and_aggregate: matmul(adj_t, x[0], 'add')
-        return _fc.graph_conv_fc(agg, x[1], self.lin_rel.weight, self.lin_rel.bias, self.lin_root.weight, relu)
+
+        def fc(agg, x_dst):
+            out = _fc.graph_conv_fc(agg, x_dst, self.lin_rel.weight, self.lin_rel.bias, self.lin_root.weight, relu)
+            return F.dropout(out, p=dropout, training=True) if dropout > 0 else out
+
+        pc = getattr(edge_index, "partitioned_conv", None)  # row-partitioned multi-GPU adjacency
+        if pc is not None:
+            return pc(x, fc)
+        return fc(spmm(edge_index, x[0]), x[1])  # message_and_aggregate: matmul(adj_t, x[0], 'add')
 
 
 class GraphConvTwoDirection(nn.Module):
@@ -99,11 +107,12 @@ class GraphConvTwoDirection(nn.Module):
         self.left2right = GraphConv((left_dim, right_dim), out_dim)
         self.right2left = GraphConv((right_dim, left_dim), out_dim)
 
-    def forward(self, left_feas, right_feas, edge_index: BipartiteCSR, edge_weight=None, relu: bool = False):
+    def forward(self, left_feas, right_feas, edge_index: BipartiteCSR, edge_weight=None, relu: bool = False,
+                dropout: float = 0.0):
         # edge_index is A (m x n, rows = cons).  arch.py:71-74: l2r = A^T, r2l = A.
         l2r, r2l = edge_index.t(), edge_index
-        right_updated = self.left2right((left_feas, right_feas), l2r, edge_weight, relu=relu)
-        left_updated = self.right2left((right_feas, left_feas), r2l, edge_weight, relu=relu)
+        right_updated = self.left2right((left_feas, right_feas), l2r, edge_weight, relu=relu, dropout=dropout)
+        left_updated = self.right2left((right_feas, left_feas), r2l, edge_weight, relu=relu, dropout=dropout)
         return left_updated, right_updated
 
 
@@ -140,14 +149,13 @@ class GCN_FC(GCNBase):
         x_left, x_right, edge_index = batch.x_s, batch.x_t, batch.edge_index
         # conv -> ReLU (arch.py:181-182): the ReLU is the FC kernel's epilogue.
         left, right = self.conv1(x_left, x_right, edge_index, relu=True)
+        dp = self.dp if self.training else 0.0
         for conv in self.layers:
             # conv -> dropout -> ReLU (arch.py:185-188).  ReLU commutes with
             # dropout (x * mask / (1-p), a non-negative scale), so the ReLU is
-            # fused into the FC and dropout follows it.
-            left, right = conv(left, right, edge_index, relu=True)
-            if self.training and self.dp > 0:
-                left = F.dropout(left, p=self.dp, training=True)
-                right = F.dropout(right, p=self.dp, training=True)
+            # fused into the FC and dropout follows it (inside the conv, so a
+            # partitioned run drops each variable once, at its owner).
+            left, right = conv(left, right, edge_index, relu=True, dropout=dp)
         left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias)
         right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias)
         return add_knowledge(left, right, x_left, x_right)

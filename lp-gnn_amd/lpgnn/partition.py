@@ -2,30 +2,35 @@
 
 The reference has no distributed code (train.py:81-82: DataParallel
 commented out); graphs above 12M edges fall back to NeighborLoader
-mini-batches (train.py:103-116).  Here a large LP is split instead:
+mini-batches (train.py:103-116).  Here one large LP is split instead, one
+process per GPU:
 
 * constraint rows -> P contiguous, nnz-balanced blocks, one per rank;
-* a variable touched by one block only is *interior* to it (untouched
-  variables go to the rank of their id block); a variable touched by >= 2
-  blocks is a *boundary* variable, replicated on every rank;
-* each rank packs CSR(A_p) / CSR(A_p^T) over its cons rows and its local
-  variables, numbered in ascending global id -- so every row keeps the
-  reference's per-row edge order and interior results are bitwise those of
-  the single-GPU run;
-* per layer: cons<-vars is purely local (boundary rows are replicated);
-  vars<-cons gives full sums for interior variables and partial sums for
-  boundary ones -> ONE all-reduce(sum) of the boundary aggregate rows over
-  RCCL.  Its autograd backward is the same all-reduce on the gradient.
-  Everything after (FC, ReLU) runs redundantly and identically on every
-  rank for the boundary rows.
-* loss: each node is owned by exactly one rank (boundary variables by the
-  lowest rank touching them); the balanced loss (train.py:39-46) uses
-  all-reduced class counts and weight sums, so the per-rank losses add up
-  to the single-graph loss; weight gradients are summed with one bucketed
-  all-reduce before the optimizer step (identical on every rank).
+* every variable has ONE owner: the rank holding most of its edges (ties:
+  lowest rank; untouched variables: the rank of their id block).  A rank
+  keeps its owned variables plus a *halo* of the remote-owned variables its
+  constraints touch (boundary variables), local ids = [owned | halo], each
+  part ascending in global id;
+* CSR(A_p) keeps every constraint row's edges in GLOBAL variable order (the
+  reference's per-row summation order), CSR(A_p^T) has one row per local
+  variable;
+* per layer, cons<-vars is purely local (halo rows hold the owners' current
+  embeddings); vars<-cons gives partial aggregates on halo rows, which are
+  REDUCED to their owners (RCCL all_to_all, summed in ascending source-rank
+  order after the owner's own partial -- deterministic), the owner runs the
+  FC (+ReLU, +dropout) for its variables only -- no replicated compute --
+  and the result is BROADCAST back to the touching ranks' halo rows (second
+  all_to_all).  The autograd backward of reduce is broadcast and vice versa.
+  Together the pair is the sparse all-reduce of boundary-variable
+  embeddings: every rank ends with the full value of exactly the boundary
+  rows it uses, and only those rows cross xGMI;
+* loss: owned nodes only; the balanced loss (train.py:39-46) uses
+  all-reduced class counts and weight sums so the per-rank losses add up to
+  the single-graph loss; parameter gradients are summed with one bucketed
+  all-reduce (every FC row is computed once, so nothing is double counted).
 
-The local SpMM and the FC are the product HIP kernels; tests swap them for
-the oracle to exercise this module with gloo on CPU.
+Local compute is the product HIP path; tests swap `_local_spmm` and the FC
+for the oracle to exercise this module with gloo on CPU.
 """
 from __future__ import annotations
 
@@ -37,7 +42,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import sparse as _sparse
-from .sparse import BipartiteCSR
+from .sparse import CSR, BipartiteCSR
 
 
 # ----------------------------------------------------------------------- plan
@@ -45,25 +50,43 @@ from .sparse import BipartiteCSR
 class PartitionPlan:
     rank: int
     world: int
-    m: int                 # global cons
-    n: int                 # global vars
-    row_lo: int            # this rank's cons block [row_lo, row_hi)
+    m: int                  # global cons
+    n: int                  # global vars
+    row_lo: int             # this rank's cons block [row_lo, row_hi)
     row_hi: int
-    local_vars: np.ndarray  # int64 [n_p] global var ids, ascending
-    boundary: np.ndarray   # int64 [n_b] local indices of the (replicated) boundary vars
-    var_owned: np.ndarray  # bool [n_p] this rank owns the var's output/loss
-    e_row: np.ndarray      # local edges (local cons id, local var id, value)
+    owned: np.ndarray       # int64 global ids of owned vars (ascending)
+    halo: np.ndarray        # int64 global ids of remote-owned vars touched here (ascending)
+    e_row: np.ndarray       # local edges: local cons id, GLOBAL var id, local var id, value
+    e_gcol: np.ndarray
     e_col: np.ndarray
     e_val: np.ndarray
-    n_boundary_global: int
+    send_idx: np.ndarray    # reduce phase: local halo rows, grouped by owner rank (ascending var in group)
+    send_counts: list
+    recv_idx: np.ndarray    # reduce phase: local owned rows, grouped by source rank
+    recv_counts: list
+    n_boundary_global: int  # variables touched by >= 2 ranks
 
     @property
     def m_local(self) -> int:
         return self.row_hi - self.row_lo
 
     @property
+    def n_own(self) -> int:
+        return int(self.owned.shape[0])
+
+    @property
     def n_local(self) -> int:
-        return int(self.local_vars.shape[0])
+        return int(self.owned.shape[0] + self.halo.shape[0])
+
+    @property
+    def local_vars(self) -> np.ndarray:
+        return np.concatenate([self.owned, self.halo])
+
+    @property
+    def var_owned(self) -> np.ndarray:
+        v = np.zeros(self.n_local, dtype=bool)
+        v[:self.n_own] = True
+        return v
 
     @property
     def nnz_local(self) -> int:
@@ -79,8 +102,7 @@ def row_blocks(row: np.ndarray, m: int, world: int) -> np.ndarray:
     for k in range(1, world):
         b.append(int(np.searchsorted(cum, k * nnz / world, side="left")) + 1)
     b.append(m)
-    b = np.maximum.accumulate(np.minimum(np.array(b, dtype=np.int64), m))
-    return b
+    return np.maximum.accumulate(np.minimum(np.array(b, dtype=np.int64), m))
 
 
 def plan_partition(row, col, val, m: int, n: int, world: int, rank: int) -> PartitionPlan:
@@ -89,25 +111,53 @@ def plan_partition(row, col, val, m: int, n: int, world: int, rank: int) -> Part
     val = np.asarray(val, np.float32)
     bounds = row_blocks(row, m, world)
     blk = np.searchsorted(bounds, row, side="right") - 1
-    vmin = np.full(n, world, np.int64)
-    vmax = np.full(n, -1, np.int64)
-    np.minimum.at(vmin, col, blk)
-    np.maximum.at(vmax, col, blk)
-    untouched = vmax < 0
-    owner = np.where(untouched, (np.arange(n, dtype=np.int64) * world) // max(n, 1), vmin)
-    is_boundary = (~untouched) & (vmin != vmax)
-    local_mask = is_boundary | (owner == rank)
-    local_vars = np.nonzero(local_mask)[0].astype(np.int64)
+    # touches (var, rank) with edge counts, sorted by var then rank
+    ukey, cnt = np.unique(col * world + blk, return_counts=True)
+    tv, tr = ukey // world, ukey % world
+    owner = (np.arange(n, dtype=np.int64) * world) // max(n, 1)
+    order = np.lexsort((tr, -cnt, tv))  # per var: most edges first, then lowest rank
+    first = order[np.r_[True, tv[order][1:] != tv[order][:-1]]] if len(order) else order
+    owner[tv[first]] = tr[first]
+    ntouch = np.bincount(tv, minlength=n)
+    is_halo = tr != owner[tv]
+    hv, hr = tv[is_halo], tr[is_halo]  # var hv is touched by rank hr and owned elsewhere (sorted by var)
+
+    owned = np.nonzero(owner == rank)[0].astype(np.int64)
+    halo = hv[hr == rank]
+    local_vars = np.concatenate([owned, halo])
     g2l = np.full(n, -1, np.int64)
     g2l[local_vars] = np.arange(local_vars.shape[0])
+
+    o = owner[halo]
+    srt = np.argsort(o, kind="stable")
+    send_idx = g2l[halo[srt]]
+    send_counts = np.bincount(o, minlength=world).tolist()
+    mine = owner[hv] == rank
+    rv, rq = hv[mine], hr[mine]
+    srt = np.argsort(rq, kind="stable")
+    recv_idx = g2l[rv[srt]]
+    recv_counts = np.bincount(rq, minlength=world).tolist()
+
     lo, hi = int(bounds[rank]), int(bounds[rank + 1])
     sel = (row >= lo) & (row < hi)
-    e_row, e_col = row[sel] - lo, g2l[col[sel]]
+    e_gcol = col[sel]
+    e_col = g2l[e_gcol]
     assert (e_col >= 0).all()
-    boundary = g2l[np.nonzero(is_boundary)[0]]
-    var_owned = owner[local_vars] == rank
-    return PartitionPlan(rank, world, m, n, lo, hi, local_vars, boundary.astype(np.int64), var_owned,
-                         e_row, e_col, val[sel], int(is_boundary.sum()))
+    return PartitionPlan(rank, world, m, n, lo, hi, owned, halo, row[sel] - lo, e_gcol, e_col, val[sel],
+                         send_idx.astype(np.int64), send_counts, recv_idx.astype(np.int64), recv_counts,
+                         int((ntouch >= 2).sum()))
+
+
+def local_dual_csr(plan: PartitionPlan, device) -> BipartiteCSR:
+    """CSR(A_p) with each row's edges in global variable order (columns then
+    remapped to local ids), CSR(A_p^T) over the local variables."""
+    fwd = BipartiteCSR.from_coo(plan.e_row, plan.e_gcol, plan.e_val, plan.m_local, plan.n, device=device).fwd
+    g2l = torch.full((plan.n,), -1, dtype=torch.int32)
+    g2l[torch.from_numpy(plan.local_vars)] = torch.arange(plan.n_local, dtype=torch.int32)
+    fwd_col = g2l.to(fwd.col.device)[fwd.col.long()] if fwd.nnz else fwd.col
+    fwd = CSR(fwd.rowptr, fwd_col.contiguous(), fwd.val, plan.m_local, plan.n_local)
+    bwd = BipartiteCSR.from_coo(plan.e_row, plan.e_col, plan.e_val, plan.m_local, plan.n_local, device=device).bwd
+    return BipartiteCSR(fwd, bwd)
 
 
 # ------------------------------------------------------------ communication
@@ -124,31 +174,85 @@ def _all_reduce_(t: torch.Tensor, group=None) -> torch.Tensor:
     return t
 
 
-class _BoundaryAllReduce(torch.autograd.Function):
-    """y = x with rows `bidx` replaced by their sum over ranks.  Backward:
-    the same all-reduce on the gradient rows (sum of every rank's share)."""
+def _a2a(send: torch.Tensor, in_counts: list, out_counts: list, group) -> torch.Tensor:
+    recv = send.new_empty((sum(out_counts),) + tuple(send.shape[1:]))
+    if sum(in_counts) == 0 and sum(out_counts) == 0:
+        return recv
+    if dist.get_backend(group) == "gloo" and send.is_cuda:
+        h = torch.empty(recv.shape, dtype=recv.dtype)
+        dist.all_to_all_single(h, send.cpu(), out_counts, in_counts, group=group)
+        recv.copy_(h)
+    else:
+        dist.all_to_all_single(recv, send.contiguous(), out_counts, in_counts, group=group)
+    return recv
 
+
+class Exchange:
+    """The static boundary exchange of one rank (see module docstring)."""
+
+    def __init__(self, plan: PartitionPlan, device, group=None):
+        self.n_own, self.n_local = plan.n_own, plan.n_local
+        self.send_idx = torch.from_numpy(plan.send_idx).to(device)
+        self.recv_idx = torch.from_numpy(plan.recv_idx).to(device)
+        self.send_counts, self.recv_counts = list(plan.send_counts), list(plan.recv_counts)
+        self.group = group
+        # per-source slices of recv_idx (ascending source rank)
+        off = np.concatenate([[0], np.cumsum(self.recv_counts)]).astype(np.int64)
+        self.recv_slices = [(int(off[q]), int(off[q + 1])) for q in range(len(self.recv_counts))
+                            if off[q + 1] > off[q]]
+
+    def add_partials(self, owned: torch.Tensor, recv: torch.Tensor) -> None:
+        for a, b in self.recv_slices:  # deterministic: one index_add_ per source rank, unique rows each
+            owned.index_add_(0, self.recv_idx[a:b], recv[a:b])
+
+    def reduce(self, full: torch.Tensor) -> torch.Tensor:
+        """[n_local, F] partials -> [n_own, F] sums (own partial + sources in rank order)."""
+        recv = _a2a(full.index_select(0, self.send_idx), self.send_counts, self.recv_counts, self.group)
+        owned = full[:self.n_own].clone()
+        self.add_partials(owned, recv)
+        return owned
+
+    def broadcast(self, owned: torch.Tensor) -> torch.Tensor:
+        """[n_own, F] owner values -> [n_local, F] with the halo rows filled."""
+        recv = _a2a(owned.index_select(0, self.recv_idx), self.recv_counts, self.send_counts, self.group)
+        out = owned.new_empty((self.n_local,) + tuple(owned.shape[1:]))
+        out[:self.n_own] = owned
+        if self.send_idx.numel():
+            out.index_copy_(0, self.send_idx, recv)
+        return out
+
+    def broadcast_grad(self, g_owned: torch.Tensor) -> torch.Tensor:
+        """Backward of reduce: every holder of a row gets the owner's gradient."""
+        return self.broadcast(g_owned)
+
+    def reduce_grad(self, g_local: torch.Tensor) -> torch.Tensor:
+        """Backward of broadcast: halo-row gradients are summed into the owner."""
+        return self.reduce(g_local)
+
+
+class _Reduce(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bidx, group):
-        ctx.bidx, ctx.group = bidx, group
-        if bidx.numel():
-            buf = x.index_select(0, bidx)
-            _all_reduce_(buf, group)
-            x.index_copy_(0, bidx, buf)
-        ctx.mark_dirty(x)  # x is a fresh SpMM output that nothing else saved
-        return x
+    def forward(ctx, full, ex):
+        ctx.ex = ex
+        return ex.reduce(full)
 
     @staticmethod
     def backward(ctx, g):
-        g = g.clone()
-        if ctx.bidx.numel():
-            buf = g.index_select(0, ctx.bidx)
-            _all_reduce_(buf, ctx.group)
-            g.index_copy_(0, ctx.bidx, buf)
-        return g, None, None
+        return ctx.ex.broadcast_grad(g.contiguous()), None
 
 
-# local compute hooks (the product HIP kernels; tests swap in the oracle)
+class _Broadcast(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, owned, ex):
+        ctx.ex = ex
+        return ex.broadcast(owned)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.ex.reduce_grad(g.contiguous()), None
+
+
+# local compute hook (the product HIP kernel; tests swap in the oracle)
 def _local_spmm(adj: BipartiteCSR, x: torch.Tensor) -> torch.Tensor:
     return _sparse.spmm(adj, x)
 
@@ -156,16 +260,15 @@ def _local_spmm(adj: BipartiteCSR, x: torch.Tensor) -> torch.Tensor:
 class PartitionedCSR:
     """The edge_index of a rank's batch: local dual CSR + boundary exchange.
 
-    Orientation "cons" = A_p (rows = local cons) -- cons<-vars, local only;
-    orientation "vars" = A_p^T (rows = local vars) -- vars<-cons, partial
-    sums on boundary rows completed by the all-reduce.
+    orient "cons": A_p, rows = local cons (cons<-vars, local only);
+    orient "vars": A_p^T, rows = local vars (vars<-cons, reduce/broadcast).
     """
 
-    def __init__(self, local: BipartiteCSR, bidx: torch.Tensor, group, orient: str = "cons"):
-        self.local, self.bidx, self.group, self.orient = local, bidx, group, orient
+    def __init__(self, local: BipartiteCSR, ex: Exchange, orient: str = "cons"):
+        self.local, self.ex, self.orient = local, ex, orient
 
     def t(self) -> "PartitionedCSR":
-        return PartitionedCSR(self.local.t(), self.bidx, self.group, "vars" if self.orient == "cons" else "cons")
+        return PartitionedCSR(self.local.t(), self.ex, "vars" if self.orient == "cons" else "cons")
 
     def sparse_sizes(self):
         return self.local.sparse_sizes()
@@ -177,34 +280,32 @@ class PartitionedCSR:
     def device(self):
         return self.local.device
 
-    def to(self, device, non_blocking=False):
-        return PartitionedCSR(self.local.to(device), self.bidx.to(device), self.group, self.orient)
+    def partitioned_conv(self, x, fc):
+        """One GraphConv direction: fc(agg, x_dst) is lin_rel + lin_root (+ReLU, +dropout)."""
+        agg = _local_spmm(self.local, x[0])
+        if self.orient == "cons":
+            return fc(agg, x[1])
+        ex = self.ex
+        agg_own = _Reduce.apply(agg, ex)
+        out_own = fc(agg_own, x[1][:ex.n_own])
+        return _Broadcast.apply(out_own, ex)
 
-    def partitioned_spmm(self, x: torch.Tensor) -> torch.Tensor:
-        y = _local_spmm(self.local, x)
-        if self.orient == "vars":
-            y = _BoundaryAllReduce.apply(y, self.bidx, self.group)
-        return y
 
-
-def make_local_batch(plan: PartitionPlan, x_s, x_t, y_s, y_t, device, group=None, pack_device=None):
-    """Rank-local BipartiteBatch with a PartitionedCSR edge_index."""
+def make_local_batch(plan: PartitionPlan, x_s, x_t, y_s, y_t, device, group=None):
+    """Rank-local BipartiteBatch whose edge_index is a PartitionedCSR."""
     from .data import BipartiteBatch
 
-    pd = device if pack_device is None else pack_device
-    local = BipartiteCSR.from_coo(plan.e_row, plan.e_col, plan.e_val, plan.m_local, plan.n_local, device=pd)
-    if str(pd) != str(device):
-        local = local.to(device)
-    lv = torch.from_numpy(plan.local_vars)
-    adj = PartitionedCSR(local, torch.from_numpy(plan.boundary).to(device), group)
+    local = local_dual_csr(plan, device)
+    lv = plan.local_vars
+    adj = PartitionedCSR(local, Exchange(plan, device, group))
     b = BipartiteBatch(
-        x_s=torch.as_tensor(x_s[plan.row_lo:plan.row_hi]).to(device),
-        x_t=torch.as_tensor(np.asarray(x_t)[plan.local_vars]).to(device),
-        y_s=None if y_s is None else torch.as_tensor(y_s[plan.row_lo:plan.row_hi]).to(device),
-        y_t=None if y_t is None else torch.as_tensor(np.asarray(y_t)[plan.local_vars]).to(device),
+        x_s=torch.as_tensor(np.asarray(x_s)[plan.row_lo:plan.row_hi]).to(device),
+        x_t=torch.as_tensor(np.asarray(x_t)[lv]).to(device),
+        y_s=None if y_s is None else torch.as_tensor(np.asarray(y_s)[plan.row_lo:plan.row_hi]).to(device),
+        y_t=None if y_t is None else torch.as_tensor(np.asarray(y_t)[lv]).to(device),
         edge_index=adj, s_bs=plan.m_local, t_bs=plan.n_local, bs=plan.m_local + plan.n_local)
     b.var_owned = torch.from_numpy(plan.var_owned).to(device)
-    b.local_vars = lv
+    b.local_vars = torch.from_numpy(lv)
     b.plan = plan
     return b
 
@@ -287,7 +388,7 @@ def build_bench_job(args, rank: int, world: int, device) -> BenchJob:
     model = GCN_FC(8, 8, hids=args.hids, depth=args.depth).to(device)
     opt, _ = make_optimizer(model)
     step = lambda: train_step_distributed(model, batch, opt)
-    wl = (f"row-partitioned synthetic LP {g.m}x{g.n} nnz={g.nnz} over {world} GPUs (c2-sized block per GPU, "
-          f"rho={args.rho}, {plan.n_boundary_global} boundary vars), GCN_FC(8,8,hids={args.hids},"
-          f"depth={args.depth}) fwd+bwd+Adam")
+    wl = (f"row-partitioned synthetic LP {g.m}x{g.n} nnz={g.nnz} over {world} GPU(s) (c2-sized block per GPU, "
+          f"rho={args.rho}, {plan.n_boundary_global} boundary vars, {plan.halo.shape[0]} halo rows on rank "
+          f"{rank}), GCN_FC(8,8,hids={args.hids},depth={args.depth}) fwd+bwd+Adam")
     return BenchJob(step, plan.nnz_local, wl, plan)

@@ -29,31 +29,50 @@ def _graph():
 
 
 def test_plan_invariants():
-    from lpgnn.partition import plan_partition
+    from lpgnn.partition import local_dual_csr, plan_partition
 
     g = _graph()
     for world in (1, 2, 3, 4):
         plans = [plan_partition(g.row, g.col, g.val, g.m, g.n, world, r) for r in range(world)]
-        # cons blocks tile [0, m)
+        # cons blocks tile [0, m); every edge lands on exactly one rank
         assert plans[0].row_lo == 0 and plans[-1].row_hi == g.m
         for a, b in zip(plans, plans[1:]):
             assert a.row_hi == b.row_lo
-        # every edge lands on exactly one rank
         assert sum(p.nnz_local for p in plans) == g.nnz
-        # every variable owned exactly once; boundary set replicated everywhere
-        owned = np.concatenate([p.local_vars[p.var_owned] for p in plans])
+        # every variable owned exactly once; owned/halo ascending and disjoint
+        owned = np.concatenate([p.owned for p in plans])
         assert np.array_equal(np.sort(owned), np.arange(g.n))
-        bsets = [set(p.local_vars[p.boundary].tolist()) for p in plans]
-        assert all(s == bsets[0] for s in bsets)
-        assert len(bsets[0]) == plans[0].n_boundary_global
-        # local numbering is monotone in global ids (keeps per-row edge order)
         for p in plans:
-            assert np.all(np.diff(p.local_vars) > 0)
-            # reconstruct the global edges of this block
-            gr = p.e_row + p.row_lo
-            gc = p.local_vars[p.e_col]
+            assert np.all(np.diff(p.owned) > 0) and np.all(np.diff(p.halo) > 0)
+            assert not np.intersect1d(p.owned, p.halo).size
+            # the halo is exactly the remote-owned vars this block touches
             sel = (g.row >= p.row_lo) & (g.row < p.row_hi)
+            touched = np.unique(g.col[sel])
+            assert np.array_equal(np.sort(np.union1d(np.intersect1d(touched, p.owned), p.halo)),
+                                  np.union1d(np.intersect1d(touched, p.owned), p.halo))
+            assert np.array_equal(p.halo, np.setdiff1d(touched, p.owned))
+            # local edges reproduce the global block
+            gr, gc = p.e_row + p.row_lo, p.local_vars[p.e_col]
             assert np.array_equal(np.sort(gr * g.n + gc), np.sort(g.row[sel] * g.n + g.col[sel]))
+            assert np.array_equal(gc, p.e_gcol)
+        # reduce-phase sends and receives pair up (same vars, same order)
+        for p in plans:
+            off = np.concatenate([[0], np.cumsum(p.send_counts)])
+            for o in range(world):
+                sent = p.local_vars[p.send_idx[off[o]:off[o + 1]]]
+                q = plans[o]
+                roff = np.concatenate([[0], np.cumsum(q.recv_counts)])
+                got = q.local_vars[q.recv_idx[roff[p.rank]:roff[p.rank + 1]]]
+                assert np.array_equal(sent, got)
+                assert o != p.rank or len(sent) == 0
+    # local CSR(A_p) keeps each row's edges in global variable order
+    p = plan_partition(g.row, g.col, g.val, g.m, g.n, 3, 1)
+    adj = local_dual_csr(p, "cpu")
+    rp, c = adj.fwd.rowptr.numpy(), adj.fwd.col.numpy()
+    gl = p.local_vars[c]
+    for i in range(p.m_local):
+        assert np.all(np.diff(gl[rp[i]:rp[i + 1]]) > 0)
+    assert adj.bwd.n_rows == p.n_local and adj.fwd.n_cols == p.n_local
 
 
 # ------------------------------------------------------- oracle-backed doubles
@@ -111,20 +130,17 @@ def _worker(rank, world, port, out_dir):
         rloss.backward()
 
         np.testing.assert_allclose(lc.detach().numpy(), rc.detach().numpy()[plan.row_lo:plan.row_hi], atol=2e-5)
-        own = plan.var_owned
-        np.testing.assert_allclose(lv.detach().numpy()[own], rv.detach().numpy()[plan.local_vars[own]], atol=2e-5)
-        # replicated boundary rows agree with the full graph too
-        b = plan.boundary
-        np.testing.assert_allclose(lv.detach().numpy()[b], rv.detach().numpy()[plan.local_vars[b]], atol=2e-5)
+        # owned AND halo rows agree with the full graph (halo = owners' values)
+        np.testing.assert_allclose(lv.detach().numpy(), rv.detach().numpy()[plan.local_vars], atol=2e-5)
         assert abs(tot.item() - rloss.item()) < 1e-4, (tot.item(), rloss.item())
         for k, p in model.named_parameters():
             np.testing.assert_allclose(p.grad.numpy(), params[k].grad.numpy(), rtol=1e-3, atol=1e-5, err_msg=k)
-        open(os.path.join(out_dir, f"ok{rank}"), "w").write(f"{tot.item()} {plan.n_boundary_global}")
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write(f"{tot.item()} {plan.n_boundary_global} {len(plan.halo)}")
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_partitioned_training_step_matches_single_graph(tmp_path, world):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
