@@ -14,7 +14,9 @@ absent torch_geometric / torch_sparse imports are never executed):
   val.py    inference_gnn (106-124)
   train.py  balanced (39-46)
   utils.py  labels_to_balanced_weights (286-299)
-  dataset.py MyToBipartite.__call__ (275-332)
+  dataset.py MyToBipartite.__call__ (275-332), scaling (23-76), cvt_to_features (79-96)
+  utils.py  sparse_mat_div_by_vec, count_nonzero_sparse_mat, cos_sim_*, expand_inf,
+            concatenate_on_lst_dim (323-384)
 
 The names those bodies reference but the reference does not define are
 supplied from oracle/model_ref.py (the restatement of the un-vendored
@@ -102,7 +104,9 @@ def ref_namespace():
     extract(f"{REF}/arch.py", ["GraphConvTwoDirection", "GCNBase", "add_knowledge", "GCN_FC"], ns)
     extract(f"{REF}/val.py", ["inference_gnn"], ns)
     extract(f"{REF}/train.py", ["balanced"], ns)
-    extract(f"{REF}/dataset.py", ["MyToBipartite"], ns)
+    extract(f"{REF}/dataset.py", ["MyToBipartite", "scaling", "cvt_to_features"], ns)
+    extract(f"{REF}/utils.py", ["sparse_mat_div_by_vec", "count_nonzero_sparse_mat", "cos_sim_vec_and_sparse_mat",
+                                "cos_sim_sparse_mat_and_vec", "expand_inf", "concatenate_on_lst_dim"], ns)
     return ns
 
 
@@ -233,6 +237,34 @@ def main():
                         x_s=res.x_s.numpy(), x_t=res.x_t.numpy(), y_s=res.y_s.numpy(), y_t=res.y_t.numpy(),
                         l2r=l2r.numpy(), l2r_attr=l2r_attr.numpy(), sizes=np.array(sizes),
                         s_bs=res.s_bs, t_bs=res.t_bs)
+    # ---- LP scaling + node features (dataset.py:23-96 with utils.py helpers) ----
+    import scipy.sparse as sp
+
+    feats = {}
+    for i, (m, n, nnz) in enumerate(((12, 20, 60), (40, 25, 200))):
+        keys = np.sort(rng.choice(m * n, size=nnz, replace=False))
+        r, c = keys // n, keys % n
+        r = r[r != m - 1]  # an empty constraint row
+        c = c[:len(r)]
+        data = rng.normal(0, 50, len(r))
+        cvec = rng.normal(0, 10, n)
+        b_l = rng.normal(-5, 20, m)
+        b_u = b_l + rng.uniform(0, 30, m)
+        b_l[rng.random(m) < 0.4] = -np.inf
+        b_u[rng.random(m) < 0.4] = np.inf
+        b_l[0] = -1e309  # < -1e308 -> -inf (dataset.py:25)
+        l_ = np.where(rng.random(n) < 0.7, 0.0, -np.inf)
+        u_ = np.where(rng.random(n) < 0.5, np.inf, rng.uniform(1, 100, n))
+        A = sp.coo_matrix((data, (r, c)), shape=(m, n)).tocsr()
+        args = [x.copy() for x in (cvec, b_l)] + [A.copy()] + [x.copy() for x in (b_u, l_, u_)]
+        cs, bls, As, bus, ls, us = ns["scaling"](*args)
+        v_f, c_f = ns["cvt_to_features"](cs, bls, As, bus, ls, us)
+        Ac = As.tocoo()
+        feats.update({f"in_row_{i}": r, f"in_col_{i}": c, f"in_data_{i}": data, f"in_c_{i}": cvec,
+                      f"in_bl_{i}": b_l, f"in_bu_{i}": b_u, f"in_l_{i}": l_, f"in_u_{i}": u_,
+                      f"m_{i}": m, f"n_{i}": n, f"out_row_{i}": Ac.row, f"out_col_{i}": Ac.col,
+                      f"out_data_{i}": Ac.data, f"out_c_{i}": cs, f"v_feas_{i}": v_f, f"c_feas_{i}": c_f})
+    np.savez_compressed(os.path.join(HERE, "features_small.npz"), **feats)
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))
 
 
