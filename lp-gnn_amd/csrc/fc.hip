@@ -200,6 +200,143 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32(FcArgs a) {
   }
 }
 
+// Same contract on v_mfma_f32_16x16x4_f32 (lane l: A[l&15][k = l>>4],
+// B[k = l>>4][l&15]; C/D col = l&15, row = 4*(l>>4) + r).  The staged tiles
+// are stored k-permuted inside each 32-wide k-block -- position (k&3)*8 + k/4,
+// rows padded to 36 floats -- so one conflict-free ds_read_b128 gives a lane
+// its operand for 4 consecutive MFMA k-steps.  Chains and block sums are the
+// same as fc_fwd_f32 (bitwise identical results).
+template <int WAVES_M, int WAVES_N, int TM, int TN, bool RELU>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_m16(FcArgs a) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int BM = WAVES_M * TM * 16;
+  constexpr int BN = WAVES_N * TN * 16;
+  constexpr int BKs = 32;            // staging k-tile = one numerics block
+  constexpr int LDK = 36;            // padded row (floats), 16-B aligned
+  constexpr int C4 = BKs / 4;
+  constexpr int LA = BM * C4 / NT;
+  constexpr int LB = BN * C4 / NT;
+  static_assert(LA >= 1 && LB >= 1 && BM * C4 % NT == 0 && BN * C4 % NT == 0, "tile/thread mismatch");
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK];
+  auto As = [&](int b) { return smem + b * (BM + BN) * LDK; };
+  auto Bs = [&](int b) { return smem + b * (BM + BN) * LDK + BM * LDK; };
+
+  const int64_t nwg = a.mt * a.nt;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  const int64_t m0 = (wgid / a.nt) * BM;
+  const int64_t n0 = (wgid % a.nt) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int nk1 = (int)((a.K1 + BKs - 1) / BKs);
+  const int nk = nk1 + (int)((a.K2 + BKs - 1) / BKs);
+
+  f32x4v acc[TM][TN];
+  const f32x4v zero = {};
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero;
+
+  float4 ra[LA], rb[LB];
+  auto gload = [&](int t) {
+    const bool p2 = t >= nk1;
+    const float *A = p2 ? a.A2 : a.A1;
+    const float *W = p2 ? a.W2 : a.W1;
+    const int64_t lda = p2 ? a.lda2 : a.lda1, ldw = p2 ? a.ldw2 : a.ldw1, Kp = p2 ? a.K2 : a.K1;
+    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BKs;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + NT * i;
+      ra[i] = load_k4(A, lda, a.M, Kp, m0 + idx / C4, k0 + (idx % C4) * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + NT * i;
+      rb[i] = load_k4(W, ldw, a.N, Kp, n0 + idx / C4, k0 + (idx % C4) * 4);
+    }
+  };
+  // k = 4c + h  ->  position h*8 + c
+  auto put = [&](float *base, int idx, const float4 &v) {
+    float *p = base + (idx / C4) * LDK + (idx % C4);
+    p[0] = v.x; p[8] = v.y; p[16] = v.z; p[24] = v.w;
+  };
+  auto sstore = [&](int buf, int t) {
+    const bool p2 = t >= nk1;
+    const int64_t Kp = p2 ? a.K2 : a.K1;
+    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BKs;
+    if (k0 + BKs > Kp) {
+#pragma unroll
+      for (int i = 0; i < LA; ++i)
+        if (k0 + ((tid + NT * i) % C4) * 4 >= Kp) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < LB; ++i)
+        if (k0 + ((tid + NT * i) % C4) * 4 >= Kp) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < LA; ++i) put(As(buf), tid + NT * i, ra[i]);
+#pragma unroll
+    for (int i = 0; i < LB; ++i) put(Bs(buf), tid + NT * i, rb[i]);
+  };
+
+  gload(0);
+  sstore(0, 0);
+  __syncthreads();
+  const int fr = lane & 15, fh = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nk) gload(t + 1);
+    const float *Ab = As(buf) + (wm * TM * 16 + fr) * LDK + fh * 8;
+    const float *Bb = Bs(buf) + (wn * TN * 16 + fr) * LDK + fh * 8;
+    f32x4v part[TM][TN];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {  // k-steps 4*half .. 4*half+3 of this block
+      f32x4v av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const f32x4v *>(Ab + i * 16 * LDK + 4 * half);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = *reinterpret_cast<const f32x4v *>(Bb + j * 16 * LDK + 4 * half);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][u], bv[j][u],
+                                                             (half == 0 && u == 0) ? zero : part[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
+    if (t + 1 < nk) sstore(buf ^ 1, t + 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
+    if (col >= a.N) continue;
+    const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int64_t rbase = m0 + wm * TM * 16 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = rbase + r;
+        if (row < a.M) {
+          float v = acc[i][j][r];
+          if (a.bias) v = v + b;
+          if (RELU) v = (v < 0.f) ? 0.f : v;
+          a.C[row * a.ldc + col] = v;
+        }
+      }
+    }
+  }
+}
+
 // add_knowledge for one side (arch.py:129-141), bitwise torch-CPU semantics:
 //   n = sqrt(fma(x2, x2, fma(x1, x1, x0 * x0)))      (torch.linalg.vector_norm, CPU)
 //   y = x / max(n, 1e-12) * 10                          (F.normalize(x) * 10)
@@ -236,6 +373,22 @@ lpg_status launch_fc(const FcArgs &a0, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
+template <int WM, int WN, int TM, int TN>
+lpg_status launch_fc16(const FcArgs &a0, bool relu, hipStream_t s) {
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16, NT = 64 * WM * WN;
+  FcArgs a = a0;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int64_t nwg = a.mt * a.nt;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_f32: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_fwd_f32_m16<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_fwd_f32_m16<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
 int g_fc_variant = 0;  // lpg_fc_set_variant; 0 = default tile
 
 }  // namespace
@@ -264,12 +417,15 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
     case 1: return launch_fc<4, 2, 2, 2, 32>(a, relu, s);  // 256 x 128, 8 waves
     case 2: return launch_fc<2, 4, 2, 2, 32>(a, relu, s);  // 128 x 256, 8 waves
     case 3: return launch_fc<2, 2, 2, 2, 64>(a, relu, s);  // 128 x 128, BK 64 (1 block / CU)
+    case 4: return launch_fc16<2, 2, 4, 4>(a, relu, s);    // 16x16x4 MFMA, 128 x 128
+    case 5: return launch_fc16<2, 2, 4, 8>(a, relu, s);    // 16x16x4 MFMA, 128 x 256
+    case 6: return launch_fc16<4, 2, 4, 4>(a, relu, s);    // 16x16x4 MFMA, 256 x 128, 8 waves
     default: return launch_fc<2, 2, 2, 2, 32>(a, relu, s); // 128 x 128, BK 32, 2 blocks / CU
   }
 }
 
 extern "C" lpg_status lpg_fc_set_variant(int32_t v) {
-  LPG_REQUIRE(v >= 0 && v <= 3, "lpg_fc_set_variant: variant %d not in [0, 3]", v);
+  LPG_REQUIRE(v >= 0 && v <= 6, "lpg_fc_set_variant: variant %d not in [0, 6]", v);
   g_fc_variant = v;
   return LPG_OK;
 }
