@@ -111,6 +111,10 @@ lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  * lin_rel.bias, A2 = x_dst, W2 = lin_root.weight).  With K2 = 0 it is a plain
  * Linear (heads lin_left / lin_right, arch.py:175-176, 190).
  * flags: bit 0 = ReLU epilogue (arch.py:182, 188).  bias may be NULL.
+ * dropout_p > 0 fuses F.dropout after the ReLU (arch.py:186-188, training):
+ * element (m, n) is kept iff a counter-based hash of (seed, m*N + n) is >=
+ * dropout_p * 2^32, and kept values are scaled by 1 / (1 - dropout_p).  The
+ * mask is never stored: the kept set is exactly where the output is > 0.
  * Row-major fp32, leading dimensions in floats; K1, K2 and the A/W leading
  * dimensions multiples of 4, A/W 16-byte aligned.
  * Numerics (bitwise reproducible, see oracle/fc_ref.c): each part (A1 over
@@ -120,7 +124,25 @@ lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
 lpg_status lpg_fc_f32(int64_t M, int64_t N,
                       int64_t K1, const float *A1, int64_t lda1, const float *W1, int64_t ldw1,
                       int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2,
-                      const float *bias, float *C, int64_t ldc, int32_t flags, void *stream);
+                      const float *bias, float *C, int64_t ldc, int32_t flags,
+                      float dropout_p, uint64_t seed, void *stream);
+
+/* Backward of ReLU (+ fused dropout): out[i] = y[i] > 0 ? g[i] * scale : 0,
+ * y = the stored lpg_fc_f32 output, scale = 1/(1-p) (1 without dropout).
+ * n a multiple of 4, buffers 16-byte aligned; out may alias g. */
+lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const float *y, float scale, float *out,
+                                    void *stream);
+
+/* Backward of a Linear with 1 <= N <= 4 outputs (the heads lin_left /
+ * lin_right, arch.py:175-176, 190; torch Linear backward):
+ *   dH = G W (skipped if dH == NULL), dW = G^T H, db = sum_m G[m, :].
+ * G [M, N] (ldg), W [N, K] contiguous, H [M, K] (ldh).  Deterministic
+ * two-pass reduction through `workspace` (16-byte aligned,
+ * lpg_linear_small_bwd_workspace_bytes(M, K, N) bytes). */
+int64_t lpg_linear_small_bwd_workspace_bytes(int64_t M, int64_t K, int64_t N);
+lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
+                                    const float *W, const float *H, int64_t ldh, float *dH, int64_t lddh,
+                                    float *dW, float *db, void *workspace, void *stream);
 
 /* Tuning knob for lpg_fc_f32 (process-global, default 0): output tile
  * variant, 0 = 128x128 (4 waves, 2 blocks/CU), 1 = 256x128 (8 waves),

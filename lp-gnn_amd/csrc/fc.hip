@@ -41,7 +41,31 @@ struct FcArgs {
   float *C;
   int64_t ldc;
   int64_t mt, nt;  // tiles
+  // fused dropout (after the ReLU): keep element (row, col) iff
+  // hash(seed, row * N + col) >= drop_thresh; kept values are scaled.
+  uint64_t seed;
+  uint32_t drop_thresh;  // 0 = no dropout
+  float drop_scale;
 };
+
+// Counter-based dropout RNG: splitmix64 finaliser of (seed, element index).
+// Stateless, so the backward pass never needs the mask (the kept set is
+// exactly where the stored output is > 0).
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9e3779b97f4a7c15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+__device__ __forceinline__ float epilogue(const FcArgs &a, float v, float b, int64_t row, int64_t col, bool relu) {
+  if (a.bias) v = v + b;
+  if (relu) v = (v < 0.f) ? 0.f : v;
+  if (a.drop_thresh) v = drop_hash(a.seed, (uint64_t)row * (uint64_t)a.N + (uint64_t)col) >= a.drop_thresh
+                             ? v * a.drop_scale : 0.f;
+  return v;
+}
 
 // Branch-free load of 4 consecutive k of row r of X (R rows, K columns):
 // the address is clamped into range.  Rows >= R only feed outputs that are
@@ -189,12 +213,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32(FcArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < a.M) {
-          float v = acc[i][j][r];
-          if (a.bias) v = v + b;
-          if (RELU) v = (v < 0.f) ? 0.f : v;
-          a.C[row * a.ldc + col] = v;
-        }
+        if (row < a.M) a.C[row * a.ldc + col] = epilogue(a, acc[i][j][r], b, row, col, RELU);
       }
     }
   }
@@ -326,12 +345,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_m16(FcArgs 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t row = rbase + r;
-        if (row < a.M) {
-          float v = acc[i][j][r];
-          if (a.bias) v = v + b;
-          if (RELU) v = (v < 0.f) ? 0.f : v;
-          a.C[row * a.ldc + col] = v;
-        }
+        if (row < a.M) a.C[row * a.ldc + col] = epilogue(a, acc[i][j][r], b, row, col, RELU);
       }
     }
   }
@@ -355,6 +369,81 @@ __global__ __launch_bounds__(256) void knowledge_f32(int64_t M, const float *__r
   out[m * ldo] = y0;
   out[m * ldo + 1] = y1;
   out[m * ldo + 2] = y2;
+}
+
+// dZ = (Y > 0) ? g * scale : 0 -- backward of ReLU followed by dropout
+// (Y is the stored post-dropout output, so Y > 0 <=> kept and ReLU-active).
+__global__ __launch_bounds__(256) void relu_dropout_bwd_f32(int64_t n4, const float4 *__restrict__ g,
+                                                            const float4 *__restrict__ y, float scale,
+                                                            float4 *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 gv = g[i], yv = y[i];
+    float4 o;
+    o.x = yv.x > 0.f ? gv.x * scale : 0.f;
+    o.y = yv.y > 0.f ? gv.y * scale : 0.f;
+    o.z = yv.z > 0.f ? gv.z * scale : 0.f;
+    o.w = yv.w > 0.f ? gv.w * scale : 0.f;
+    out[i] = o;
+  }
+}
+
+// Backward of a Linear with few outputs (the heads, N = 3, arch.py:190):
+//   dH[m, k] = sum_c G[m, c] W[c, k]        (written if dH != NULL)
+//   dW[c, k] = sum_m G[m, c] H[m, k],  db[c] = sum_m G[m, c]
+// Pass 1: each block owns ROWS rows x all K (256 threads x float4 per
+// 1024-column chunk), streams H once, writes dH and per-block partial dW/db;
+// pass 2 sums the partials in block order (deterministic).
+constexpr int kSmallNMax = 4;
+constexpr int kRowsPerBlock = 512;
+
+__global__ __launch_bounds__(256) void linear_small_bwd_p1(int64_t M, int64_t K, int N, const float *__restrict__ G,
+                                                           int64_t ldg, const float *__restrict__ W,
+                                                           const float *__restrict__ H, int64_t ldh,
+                                                           float *__restrict__ dH, int64_t lddh,
+                                                           float *__restrict__ part) {
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
+  const int64_t r1 = r0 + kRowsPerBlock < M ? r0 + kRowsPerBlock : M;
+  float *pw = part + (int64_t)blockIdx.x * N * (K + 1);  // [N][K] then db[N]
+  for (int64_t k = (int64_t)threadIdx.x * 4; k < K; k += 1024) {
+    float4 w[kSmallNMax], acc[kSmallNMax];
+    for (int c = 0; c < kSmallNMax; ++c) {
+      w[c] = c < N ? *reinterpret_cast<const float4 *>(W + c * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int64_t m = r0; m < r1; ++m) {
+      const float4 h = *reinterpret_cast<const float4 *>(H + m * ldh + k);
+      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int c = 0; c < kSmallNMax; ++c) {
+        if (c >= N) break;
+        const float gc = G[m * ldg + c];
+        d.x = d.x + gc * w[c].x; d.y = d.y + gc * w[c].y; d.z = d.z + gc * w[c].z; d.w = d.w + gc * w[c].w;
+        acc[c].x = acc[c].x + gc * h.x; acc[c].y = acc[c].y + gc * h.y;
+        acc[c].z = acc[c].z + gc * h.z; acc[c].w = acc[c].w + gc * h.w;
+      }
+      if (dH) *reinterpret_cast<float4 *>(dH + m * lddh + k) = d;
+    }
+    for (int c = 0; c < N; ++c) *reinterpret_cast<float4 *>(pw + c * K + k) = acc[c];
+  }
+  if (threadIdx.x < (unsigned)N) {
+    float sgc = 0.f;
+    for (int64_t m = r0; m < r1; ++m) sgc = sgc + G[m * ldg + threadIdx.x];
+    pw[N * K + threadIdx.x] = sgc;
+  }
+}
+
+__global__ __launch_bounds__(256) void linear_small_bwd_p2(int64_t nblk, int64_t K, int N,
+                                                           const float *__restrict__ part, float *__restrict__ dW,
+                                                           float *__restrict__ db) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over N*K + N
+  const int64_t tot = (int64_t)N * K + N;
+  if (i >= tot) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nblk; ++b) s = s + part[b * tot + i];
+  if (i < (int64_t)N * K) {
+    if (dW) dW[i] = s;
+  } else if (db) {
+    db[i - (int64_t)N * K] = s;
+  }
 }
 
 template <int WM, int WN, int TM, int TN, int BK>
@@ -398,7 +487,8 @@ using namespace lpg;
 
 extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1, const float *W1,
                                  int64_t ldw1, int64_t K2, const float *A2, int64_t lda2, const float *W2,
-                                 int64_t ldw2, const float *bias, float *C, int64_t ldc, int32_t flags, void *stream) {
+                                 int64_t ldw2, const float *bias, float *C, int64_t ldc, int32_t flags,
+                                 float dropout_p, uint64_t seed, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_f32: negative size");
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_f32: bad C/ldc");
@@ -409,7 +499,13 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
   LPG_REQUIRE(aligned16(A1) && aligned16(W1) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
               "lpg_fc_f32: A/W must be 16-byte aligned");
   LPG_REQUIRE((flags & ~1) == 0, "lpg_fc_f32: unknown flags 0x%x", flags);
-  FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0};
+  LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
+  FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f};
+  if (dropout_p > 0.f) {
+    const double th = (double)dropout_p * 4294967296.0;
+    a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);
+    a.drop_scale = 1.f / (1.f - dropout_p);
+  }
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
   if (N <= 32) return launch_fc<4, 1, 1, 1, 32>(a, relu, s);  // heads (N = 3): 128 x 32 tiles
@@ -422,6 +518,58 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
     case 6: return launch_fc16<4, 2, 4, 4>(a, relu, s);    // 16x16x4 MFMA, 256 x 128, 8 waves
     default: return launch_fc<2, 2, 2, 2, 32>(a, relu, s); // 128 x 128, BK 32, 2 blocks / CU
   }
+}
+
+extern "C" lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const float *y, float scale, float *out,
+                                                void *stream) {
+  LPG_REQUIRE(n >= 0, "lpg_relu_dropout_bwd_f32: n < 0");
+  if (n == 0) return LPG_OK;
+  LPG_REQUIRE(g && y && out, "lpg_relu_dropout_bwd_f32: NULL pointer");
+  LPG_REQUIRE(n % 4 == 0 && aligned16(g) && aligned16(y) && aligned16(out),
+              "lpg_relu_dropout_bwd_f32: n must be a multiple of 4 and buffers 16-byte aligned");
+  const int64_t n4 = n / 4;
+  int64_t blocks = (n4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(relu_dropout_bwd_f32, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), n4,
+                     reinterpret_cast<const float4 *>(g), reinterpret_cast<const float4 *>(y), scale,
+                     reinterpret_cast<float4 *>(out));
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+extern "C" int64_t lpg_linear_small_bwd_workspace_bytes(int64_t M, int64_t K, int64_t N) {
+  if (M < 0 || K < 0 || N < 0) return -1;
+  const int64_t nblk = (M + kRowsPerBlock - 1) / kRowsPerBlock;
+  return nblk * (N * K + N) * (int64_t)sizeof(float);
+}
+
+extern "C" lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
+                                               const float *W, const float *H, int64_t ldh, float *dH, int64_t lddh,
+                                               float *dW, float *db, void *workspace, void *stream) {
+  LPG_REQUIRE(M >= 0 && K >= 0 && N >= 1 && N <= kSmallNMax, "lpg_linear_small_bwd_f32: need 1 <= N <= %d",
+              kSmallNMax);
+  LPG_REQUIRE(K % 4 == 0 && ldh % 4 == 0 && (dH == nullptr || lddh % 4 == 0), "lpg_linear_small_bwd_f32: K and leading dims must be multiples of 4");
+  LPG_REQUIRE(G && W && H && workspace, "lpg_linear_small_bwd_f32: NULL pointer");
+  LPG_REQUIRE(aligned16(W) && aligned16(H) && (dH == nullptr || aligned16(dH)) && aligned16(workspace),
+              "lpg_linear_small_bwd_f32: W/H/dH/workspace must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int64_t nblk = (M + kRowsPerBlock - 1) / kRowsPerBlock;
+  float *part = static_cast<float *>(workspace);
+  if (nblk > 0) {
+    hipLaunchKernelGGL(linear_small_bwd_p1, dim3((unsigned)nblk), dim3(256), 0, s, M, K, (int)N, G, ldg, W, H, ldh,
+                       dH, lddh, part);
+    LPG_HIP(hipGetLastError());
+  }
+  const int64_t tot = N * K + N;
+  if (nblk == 0) {
+    if (dW) LPG_HIP(hipMemsetAsync(dW, 0, sizeof(float) * N * K, s));
+    if (db) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, s));
+    return LPG_OK;
+  }
+  hipLaunchKernelGGL(linear_small_bwd_p2, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, nblk, K, (int)N,
+                     part, dW, db);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
 }
 
 extern "C" lpg_status lpg_fc_set_variant(int32_t v) {

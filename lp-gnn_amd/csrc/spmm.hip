@@ -358,7 +358,11 @@ extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx
     return launch(spmm_f32_generic, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
   int64_t W = g_slice_cols;
-  if (W == 0) W = F <= 256 ? 256 : (F <= 512 ? 512 : 1024);
+  // auto: 256-column slices (one float4 per lane).  Slices run in order
+  // (blockIdx.y major), so only a quarter-width source table is being
+  // gathered at a time and stays resident in the 256 MiB Infinity Cache;
+  // measured ~3 % faster than full-width rows at c2 (profiles/r01_kbench*).
+  if (W == 0) W = 256;
   if (W == 256) return launch_wide_f32<1, 8>(A, X, ldx, Y, ldy, F, s);
   if (W == 512) return launch_wide_f32<2, 8>(A, X, ldx, Y, ldy, F, s);
   return launch_wide_f32<4, 4>(A, X, ldx, Y, ldy, F, s);

@@ -30,6 +30,9 @@ HEADER_SYMBOLS = (
     "lpg_spmm_set_slice",
     "lpg_fc_f32",
     "lpg_fc_set_variant",
+    "lpg_relu_dropout_bwd_f32",
+    "lpg_linear_small_bwd_workspace_bytes",
+    "lpg_linear_small_bwd_f32",
     "lpg_knowledge_f32",
 )
 
@@ -67,8 +70,15 @@ def lib() -> ctypes.CDLL:
     L.lpg_spmm_set_slice.argtypes = [c_i64]
     L.lpg_spmm_set_slice.restype = c_i32
     L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
-                             c_p, c_p, c_i64, c_i32, c_p]
+                             c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_p]
     L.lpg_fc_f32.restype = c_i32
+    L.lpg_relu_dropout_bwd_f32.argtypes = [c_i64, c_p, c_p, ctypes.c_float, c_p, c_p]
+    L.lpg_relu_dropout_bwd_f32.restype = c_i32
+    L.lpg_linear_small_bwd_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
+    L.lpg_linear_small_bwd_workspace_bytes.restype = c_i64
+    L.lpg_linear_small_bwd_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p,
+                                           c_p, c_p]
+    L.lpg_linear_small_bwd_f32.restype = c_i32
     L.lpg_fc_set_variant.argtypes = [c_i32]
     L.lpg_fc_set_variant.restype = c_i32
     L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_i64, ctypes.c_float, c_p, c_i64, c_p]

@@ -89,9 +89,9 @@ class GraphConv(nn.Module):
         if edge_weight is not None:
             raise NotImplementedError("edge weights come from the adjacency values (arch.py:77)")
 
-        def fc(agg, x_dst):
-            out = _fc.graph_conv_fc(agg, x_dst, self.lin_rel.weight, self.lin_rel.bias, self.lin_root.weight, relu)
-            return F.dropout(out, p=dropout, training=True) if dropout > 0 else out
+        def fc(agg, x_dst):  # lin_rel + lin_root, ReLU and (training) dropout fused in one kernel
+            return _fc.graph_conv_fc(agg, x_dst, self.lin_rel.weight, self.lin_rel.bias, self.lin_root.weight, relu,
+                                     dropout)
 
         pc = getattr(edge_index, "partitioned_conv", None)  # row-partitioned multi-GPU adjacency
         if pc is not None:

@@ -11,9 +11,13 @@ in ONE kernel (lpg_fc_f32: no concat, no separate add / ReLU pass), and
 ``linear`` the heads lin_left / lin_right (arch.py:190).  ``knowledge`` is
 arch.py:129-141 for one side (lpg_knowledge_f32).
 
-Forward numerics are bitwise reproducible (oracle/fc_ref.c).  Backward:
-dZ = dY * (Y > 0); dA = dZ @ W; dW = dZ^T @ A; db = sum(dZ) -- plain library
-GEMMs through torch on the same stream (hipBLASLt), tolerance-level parity.
+Forward numerics are bitwise reproducible (oracle/fc_ref.c).  Training-mode
+dropout (arch.py:186-187) is fused into the FC epilogue with a counter-based
+RNG seeded from torch's generator.  Backward: dZ = (Y > 0) ? dY/(1-p) : 0 in
+one pass (lpg_relu_dropout_bwd_f32); dA = dZ W, dW = dZ^T A, db = sum(dZ)
+as plain library GEMMs through torch on the same stream (hipBLASLt); the
+heads' backward (N = 3) runs in lpg_linear_small_bwd_f32.  Tolerance-level
+parity for gradients.
 """
 from __future__ import annotations
 
@@ -43,7 +47,7 @@ def _pad_k(t: Tensor) -> Tensor:
 
 
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
-               relu: bool) -> Tensor:
+               relu: bool, dropout_p: float = 0.0, seed: int = 0) -> Tensor:
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -62,17 +66,39 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
                           K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
                           None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
                           None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), 1 if relu else 0,
-                          _lib.stream_of(A1))
+                          float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_f32")
     return C
 
 
+def relu_dropout_bwd(g: Tensor, y: Tensor, scale: float) -> Tensor:
+    """(y > 0) ? g * scale : 0 in one pass (ReLU + dropout backward)."""
+    g = g.contiguous()
+    out = torch.empty_like(g)
+    n = g.numel()
+    if n % 4 or g.data_ptr() % 16 or y.data_ptr() % 16 or not y.is_contiguous():
+        return torch.where(y > 0, g * scale, torch.zeros((), device=g.device))
+    with torch.cuda.device(g.device):
+        st = _lib.lib().lpg_relu_dropout_bwd_f32(n, g.data_ptr(), y.data_ptr(), float(scale), out.data_ptr(),
+                                                 _lib.stream_of(g))
+    _lib.check(st, "lpg_relu_dropout_bwd_f32")
+    return out
+
+
+def _new_seed() -> int:
+    """A dropout seed from torch's default generator (torch.manual_seed reproducible)."""
+    return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+
+
 class _FC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, A1, A2, W1, W2, b, relu):
-        C = fc_forward(A1, W1, A2, W2, b, relu)
+    def forward(ctx, A1, A2, W1, W2, b, relu, dropout_p):
+        if dropout_p > 0 and not relu:
+            raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
+        C = fc_forward(A1, W1, A2, W2, b, relu, dropout_p, _new_seed() if dropout_p > 0 else 0)
         ctx.relu, ctx.has_a2, ctx.has_b = relu, A2 is not None, b is not None
+        ctx.scale = 1.0 / (1.0 - dropout_p) if dropout_p > 0 else 1.0
         ctx.save_for_backward(A1, A2 if A2 is not None else A1, W1, W2 if W2 is not None else W1,
                               C if relu else A1)
         return C
@@ -80,23 +106,65 @@ class _FC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gC):
         A1, A2, W1, W2, C = ctx.saved_tensors
-        g = gC.masked_fill(C <= 0, 0.0) if ctx.relu else gC  # threshold_backward of ReLU
+        g = relu_dropout_bwd(gC, C, ctx.scale) if ctx.relu else gC
         need = ctx.needs_input_grad
         dA1 = g @ W1 if need[0] else None
         dA2 = g @ W2 if ctx.has_a2 and need[1] else None
         dW1 = g.t() @ A1 if need[2] else None
         dW2 = g.t() @ A2 if ctx.has_a2 and need[3] else None
         db = g.sum(0) if ctx.has_b and need[4] else None
-        return dA1, dA2, dW1, dW2, db, None
+        return dA1, dA2, dW1, dW2, db, None, None
 
 
-def graph_conv_fc(agg: Tensor, x_dst: Tensor, w_rel: Tensor, b_rel, w_root: Tensor, relu: bool) -> Tensor:
-    return _FC.apply(agg, x_dst, w_rel, w_root, b_rel, relu)
+def graph_conv_fc(agg: Tensor, x_dst: Tensor, w_rel: Tensor, b_rel, w_root: Tensor, relu: bool,
+                  dropout: float = 0.0) -> Tensor:
+    return _FC.apply(agg, x_dst, w_rel, w_root, b_rel, relu, float(dropout))
+
+
+def linear_small_bwd(G: Tensor, W: Tensor, H: Tensor, need_dh: bool):
+    """(dH, dW, db) of a Linear with N <= 4 outputs (lpg_linear_small_bwd_f32)."""
+    M, K = H.shape
+    N = W.shape[0]
+    G, W, H = G.contiguous(), W.contiguous(), H.contiguous()
+    L = _lib.lib()
+    ws = torch.empty(max(L.lpg_linear_small_bwd_workspace_bytes(M, K, N), 16) // 4 + 4, dtype=torch.float32,
+                     device=H.device)
+    dH = torch.empty_like(H) if need_dh else None
+    dW = torch.empty_like(W)
+    db = torch.empty(N, dtype=torch.float32, device=H.device)
+    with torch.cuda.device(H.device):
+        st = L.lpg_linear_small_bwd_f32(M, K, N, G.data_ptr(), G.stride(0), W.data_ptr(), H.data_ptr(), H.stride(0),
+                                        None if dH is None else dH.data_ptr(), K, dW.data_ptr(), db.data_ptr(),
+                                        ws.data_ptr(), _lib.stream_of(H))
+    _lib.check(st, "lpg_linear_small_bwd_f32")
+    return dH, dW, db
+
+
+class _Linear(torch.autograd.Function):
+    """torch.nn.Linear on lpg_fc_f32; few-output backward on the HIP kernel."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return fc_forward(x, W, None, None, b, False)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        if W.shape[0] <= 4 and x.shape[1] % 4 == 0:
+            dx, dW, db = linear_small_bwd(g, W, x, need[0])
+            return dx, dW if need[1] else None, db if (ctx.has_b and need[2]) else None
+        dx = g @ W if need[0] else None
+        dW = g.t() @ x if need[1] else None
+        db = g.sum(0) if ctx.has_b and need[2] else None
+        return dx, dW, db
 
 
 def linear(x: Tensor, weight: Tensor, bias) -> Tensor:
     """torch.nn.Linear.forward on lpg_fc_f32 (heads, arch.py:190)."""
-    return _FC.apply(x, None, weight, None, bias, False)
+    return _Linear.apply(x, weight, bias)
 
 
 class _Knowledge(torch.autograd.Function):

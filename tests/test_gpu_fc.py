@@ -141,3 +141,71 @@ def test_fc_tile_variants_bitwise(variant):
     finally:
         L.lpg_fc_set_variant(0)
     assert np.array_equal(got, O.fc_kchain(A1, W1, A2, W2, b, relu=True))
+
+
+def test_fused_dropout_epilogue_and_backward():
+    """Dropout fused after the ReLU: kept values are exactly relu(v)/(1-p),
+    the drop rate is p, the mask is reproducible from the seed, and the
+    backward equals torch autograd through the realised mask."""
+    from lpgnn.fc import fc_forward, graph_conv_fc
+
+    torch.manual_seed(3)
+    M, N, K = 4000, 256, 64
+    A1 = torch.randn(M, K, device=DEV)
+    A2 = torch.randn(M, K, device=DEV)
+    W1 = torch.randn(N, K, device=DEV) * 0.1
+    W2 = torch.randn(N, K, device=DEV) * 0.1
+    b = torch.randn(N, device=DEV) * 0.1
+    p = 0.1
+    base = fc_forward(A1, W1, A2, W2, b, True)
+    y = fc_forward(A1, W1, A2, W2, b, True, p, seed=1234)
+    assert torch.equal(y, fc_forward(A1, W1, A2, W2, b, True, p, seed=1234))
+    assert not torch.equal(y, fc_forward(A1, W1, A2, W2, b, True, p, seed=99))
+    pos = base > 0
+    kept = (y > 0)
+    assert bool((kept <= pos).all())
+    rate = 1.0 - kept[pos].float().mean().item()
+    assert abs(rate - p) < 0.01, rate
+    scale = torch.tensor(1.0 / (1.0 - p), dtype=torch.float32)
+    assert torch.equal(y[kept], base[kept] * scale.to(DEV))
+    # backward through the fused op == torch through the realised mask
+    A1r, A2r = A1.clone().requires_grad_(True), A2.clone().requires_grad_(True)
+    W1r, W2r, br = (t.clone().requires_grad_(True) for t in (W1, W2, b))
+    torch.manual_seed(7)
+    out = graph_conv_fc(A1r, A2r, W1r, br, W2r, True, dropout=p)
+    g = torch.randn_like(out)
+    out.backward(g)
+    mask = (out > 0).float() * (1.0 / (1.0 - p))
+    A1t, A2t = A1.clone().requires_grad_(True), A2.clone().requires_grad_(True)
+    W1t, W2t, bt = (t.clone().requires_grad_(True) for t in (W1, W2, b))
+    ref = torch.relu(torch.nn.functional.linear(A1t, W1t, bt) + torch.nn.functional.linear(A2t, W2t)) * mask
+    ref.backward(g)
+    for a, t in ((A1r, A1t), (A2r, A2t), (W1r, W1t), (W2r, W2t), (br, bt)):
+        torch.testing.assert_close(a.grad, t.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_relu_dropout_bwd_kernel():
+    from lpgnn.fc import relu_dropout_bwd
+
+    g = torch.randn(1000, 36, device=DEV)
+    y = torch.relu(torch.randn(1000, 36, device=DEV))
+    out = relu_dropout_bwd(g, y, 1.25)
+    assert torch.equal(out, torch.where(y > 0, g * 1.25, torch.zeros((), device=DEV)))
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 4, 3), (1000, 1024, 3), (1537, 260, 2), (70000, 1024, 3)])
+def test_linear_small_bwd_matches_torch(M, K, N):
+    from lpgnn.fc import linear
+
+    torch.manual_seed(M)
+    x = torch.randn(M, K, device=DEV, requires_grad=True)
+    W = torch.randn(N, K, device=DEV, requires_grad=True)
+    b = torch.randn(N, device=DEV, requires_grad=True)
+    g = torch.randn(M, N, device=DEV)
+    linear(x, W, b).backward(g)
+    got = [t.grad.clone() for t in (x, W, b)]
+    for t in (x, W, b):
+        t.grad = None
+    torch.nn.functional.linear(x, W, b).backward(g)
+    for a, t in zip(got, (x, W, b)):
+        torch.testing.assert_close(a, t.grad, rtol=2e-4, atol=2e-4)

@@ -82,9 +82,10 @@ def _cpu_local_spmm(adj, x):
     return O.spmm_t(fwd, bwd, x)
 
 
-def _cpu_graph_conv_fc(agg, x_dst, w_rel, b_rel, w_root, relu):
+def _cpu_graph_conv_fc(agg, x_dst, w_rel, b_rel, w_root, relu, dropout=0.0):
     out = F.linear(agg, w_rel, b_rel) + F.linear(x_dst, w_root)
-    return torch.relu(out) if relu else out
+    out = torch.relu(out) if relu else out
+    return F.dropout(out, p=dropout, training=True) if dropout > 0 else out
 
 
 def _cpu_knowledge(logit, feas, bound=10):
