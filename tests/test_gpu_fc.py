@@ -207,5 +207,9 @@ def test_linear_small_bwd_matches_torch(M, K, N):
     for t in (x, W, b):
         t.grad = None
     torch.nn.functional.linear(x, W, b).backward(g)
-    for a, t in zip(got, (x, W, b)):
-        torch.testing.assert_close(a, t.grad, rtol=2e-4, atol=2e-4)
+    # fp32 sums over M rows in different orders: compare both against fp64
+    xd, Wd, gd = x.detach().double(), W.detach().double(), g.double()
+    ref = (gd @ Wd, gd.t() @ xd, gd.sum(0))
+    for a, t, r in zip(got, (x.grad, W.grad, b.grad), ref):
+        err_mine, err_torch = (a.double() - r).abs().max().item(), (t.double() - r).abs().max().item()
+        assert err_mine <= 4 * err_torch + 1e-5 * max(1.0, r.abs().max().item() / 100), (err_mine, err_torch)
