@@ -133,6 +133,24 @@ lpg_status lpg_fc_f32(int64_t M, int64_t N,
 lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const float *y, float scale, float *out,
                                     void *stream);
 
+/* Same with the bias gradient fused: Y/out [M, N] row-major (ldy/ldo, N and
+ * strides multiples of 4), and db[n] = sum_m out[m, n] when db != NULL
+ * (deterministic two-pass column sum through `workspace`,
+ * lpg_relu_bwd_colsum_workspace_bytes(M, N) bytes, 16-byte aligned). */
+int64_t lpg_relu_bwd_colsum_workspace_bytes(int64_t M, int64_t N);
+lpg_status lpg_relu_bwd_colsum_f32(int64_t M, int64_t N, const float *g, int64_t ldg, const float *y,
+                                   int64_t ldy, float scale, float *out, int64_t ldo, float *db,
+                                   void *workspace, void *stream);
+
+/* Weight gradients of a GraphConv whose inputs are narrow (conv1: the 8 LP
+ * features, arch.py:170): dW1 = dZ^T A1 [N, K1], dW2 = dZ^T A2 [N, K2], in the
+ * torch weight layout, 1 <= K1 + K2 <= 16; dZ [M, N] read once; deterministic
+ * two-pass reduction (lpg_wgrad_smallk_workspace_bytes(M, N, K1 + K2)). */
+int64_t lpg_wgrad_smallk_workspace_bytes(int64_t M, int64_t N, int64_t K);
+lpg_status lpg_wgrad_smallk_f32(int64_t M, int64_t N, const float *dz, int64_t ldz,
+                                int64_t K1, const float *A1, int64_t lda1, int64_t K2, const float *A2, int64_t lda2,
+                                float *dW1, float *dW2, void *workspace, void *stream);
+
 /* Backward of a Linear with 1 <= N <= 4 outputs (the heads lin_left /
  * lin_right, arch.py:175-176, 190; torch Linear backward):
  *   dH = G W (skipped if dH == NULL), dW = G^T H, db = sum_m G[m, :].

@@ -387,65 +387,6 @@ __global__ __launch_bounds__(256) void relu_dropout_bwd_f32(int64_t n4, const fl
   }
 }
 
-// Backward of a Linear with few outputs (the heads, N = 3, arch.py:190):
-//   dH[m, k] = sum_c G[m, c] W[c, k]        (written if dH != NULL)
-//   dW[c, k] = sum_m G[m, c] H[m, k],  db[c] = sum_m G[m, c]
-// Pass 1: each block owns ROWS rows x all K (256 threads x float4 per
-// 1024-column chunk), streams H once, writes dH and per-block partial dW/db;
-// pass 2 sums the partials in block order (deterministic).
-constexpr int kSmallNMax = 4;
-constexpr int kRowsPerBlock = 512;
-
-__global__ __launch_bounds__(256) void linear_small_bwd_p1(int64_t M, int64_t K, int N, const float *__restrict__ G,
-                                                           int64_t ldg, const float *__restrict__ W,
-                                                           const float *__restrict__ H, int64_t ldh,
-                                                           float *__restrict__ dH, int64_t lddh,
-                                                           float *__restrict__ part) {
-  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
-  const int64_t r1 = r0 + kRowsPerBlock < M ? r0 + kRowsPerBlock : M;
-  float *pw = part + (int64_t)blockIdx.x * N * (K + 1);  // [N][K] then db[N]
-  for (int64_t k = (int64_t)threadIdx.x * 4; k < K; k += 1024) {
-    float4 w[kSmallNMax], acc[kSmallNMax];
-    for (int c = 0; c < kSmallNMax; ++c) {
-      w[c] = c < N ? *reinterpret_cast<const float4 *>(W + c * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-      acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    for (int64_t m = r0; m < r1; ++m) {
-      const float4 h = *reinterpret_cast<const float4 *>(H + m * ldh + k);
-      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int c = 0; c < kSmallNMax; ++c) {
-        if (c >= N) break;
-        const float gc = G[m * ldg + c];
-        d.x = d.x + gc * w[c].x; d.y = d.y + gc * w[c].y; d.z = d.z + gc * w[c].z; d.w = d.w + gc * w[c].w;
-        acc[c].x = acc[c].x + gc * h.x; acc[c].y = acc[c].y + gc * h.y;
-        acc[c].z = acc[c].z + gc * h.z; acc[c].w = acc[c].w + gc * h.w;
-      }
-      if (dH) *reinterpret_cast<float4 *>(dH + m * lddh + k) = d;
-    }
-    for (int c = 0; c < N; ++c) *reinterpret_cast<float4 *>(pw + c * K + k) = acc[c];
-  }
-  if (threadIdx.x < (unsigned)N) {
-    float sgc = 0.f;
-    for (int64_t m = r0; m < r1; ++m) sgc = sgc + G[m * ldg + threadIdx.x];
-    pw[N * K + threadIdx.x] = sgc;
-  }
-}
-
-__global__ __launch_bounds__(256) void linear_small_bwd_p2(int64_t nblk, int64_t K, int N,
-                                                           const float *__restrict__ part, float *__restrict__ dW,
-                                                           float *__restrict__ db) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over N*K + N
-  const int64_t tot = (int64_t)N * K + N;
-  if (i >= tot) return;
-  float s = 0.f;
-  for (int64_t b = 0; b < nblk; ++b) s = s + part[b * tot + i];
-  if (i < (int64_t)N * K) {
-    if (dW) dW[i] = s;
-  } else if (db) {
-    db[i - (int64_t)N * K] = s;
-  }
-}
-
 template <int WM, int WN, int TM, int TN, int BK>
 lpg_status launch_fc(const FcArgs &a0, bool relu, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
@@ -478,6 +419,92 @@ lpg_status launch_fc16(const FcArgs &a0, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
+// Narrow-input FC (conv1: K1 = K2 = 8 LP features, arch.py:170): the output
+// write is the whole cost, so no MFMA tile -- each thread holds the weights of
+// 4 output columns in registers and streams rows (A values are block-uniform
+// scalar loads).  Same numerics as the tiled kernels: with K1, K2 <= NB each
+// part is ONE k-tile, i.e. one fma chain from +0 in k order, the tile sums
+// are added into +0 in order, then bias and ReLU -- bitwise identical.
+constexpr int kSmallKRows = 64;
+
+template <int K>
+__device__ __forceinline__ void load_row_k(float (&x)[K > 0 ? K : 1], const float *A, int64_t ld, int64_t m) {
+#pragma unroll
+  for (int k = 0; k < K; k += 4) {
+    const float4 v = *reinterpret_cast<const float4 *>(A + m * ld + k);
+    x[k] = v.x; x[k + 1] = v.y; x[k + 2] = v.z; x[k + 3] = v.w;
+  }
+}
+
+template <int K1, int K2, bool RELU>
+__global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
+  static_assert(K1 % 4 == 0 && K2 % 4 == 0 && K1 >= 4, "small-K kernel: K1, K2 multiples of 4");
+  const int64_t c = (int64_t)blockIdx.y * 1024 + (int64_t)threadIdx.x * 4;
+  if (c >= a.N) return;
+  float w1[4][K1], w2[4][K2 > 0 ? K2 : 1], b[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    load_row_k<K1>(w1[j], a.W1, a.ldw1, c + j);
+    load_row_k<K2>(w2[j], a.W2, a.ldw2, c + j);
+    b[j] = a.bias ? a.bias[c + j] : 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * kSmallKRows;
+  const int64_t r1 = r0 + kSmallKRows < a.M ? r0 + kSmallKRows : a.M;
+  for (int64_t m0 = r0; m0 < r1; m0 += 4) {
+    float x1[4][K1], x2[4][K2 > 0 ? K2 : 1];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // rows past r1 re-read row r1 - 1 (never stored)
+      const int64_t m = m0 + u < r1 ? m0 + u : r1 - 1;
+      load_row_k<K1>(x1[u], a.A1, a.lda1, m);
+      load_row_k<K2>(x2[u], a.A2, a.lda2, m);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t m = m0 + u;
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float p1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < K1; ++k) p1 = __builtin_fmaf(x1[u][k], w1[j][k], p1);
+        float t = 0.f + p1;
+        if (K2 > 0) {
+          float p2 = 0.f;
+#pragma unroll
+          for (int k = 0; k < K2; ++k) p2 = __builtin_fmaf(x2[u][k], w2[j][k], p2);
+          t = t + p2;
+        }
+        o[j] = epilogue(a, t, b[j], m, c + j, RELU);
+      }
+      if (m < r1) *reinterpret_cast<float4 *>(a.C + m * a.ldc + c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+template <int K1, int K2>
+lpg_status launch_smallk(const FcArgs &a, bool relu, hipStream_t s) {
+  const dim3 grid((unsigned)((a.M + kSmallKRows - 1) / kSmallKRows), (unsigned)((a.N + 1023) / 1024));
+  if (relu)
+    hipLaunchKernelGGL((fc_smallk_f32<K1, K2, true>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_smallk_f32<K1, K2, false>), grid, dim3(256), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+// K1, K2 multiples of 4, 4 <= K1, K1 + K2 <= 16; returns false if not covered
+bool try_smallk(const FcArgs &a, bool relu, hipStream_t s, lpg_status *st) {
+  if (a.K1 < 4 || a.K1 + a.K2 > 16 || a.N % 4 || a.ldc % 4 || !aligned16(a.C)) return false;
+  if (a.M >= ((int64_t)1 << 31) * kSmallKRows) return false;
+  switch (a.K1 * 100 + a.K2) {
+#define LPG_SK(X, Y) case X * 100 + Y: *st = launch_smallk<X, Y>(a, relu, s); return true;
+    LPG_SK(4, 0) LPG_SK(4, 4) LPG_SK(4, 8) LPG_SK(4, 12) LPG_SK(8, 0) LPG_SK(8, 4) LPG_SK(8, 8)
+    LPG_SK(12, 0) LPG_SK(12, 4) LPG_SK(16, 0)
+#undef LPG_SK
+  }
+  return false;
+}
+
 int g_fc_variant = 0;  // lpg_fc_set_variant; 0 = default tile
 
 }  // namespace
@@ -508,6 +535,8 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
   }
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
+  lpg_status st;
+  if (try_smallk(a, relu, s, &st)) return st;                // conv1: narrow LP features
   if (N <= 32) return launch_fc<4, 1, 1, 1, 32>(a, relu, s);  // heads (N = 3): 128 x 32 tiles
   switch (g_fc_variant) {
     case 1: return launch_fc<4, 2, 2, 2, 32>(a, relu, s);  // 256 x 128, 8 waves
@@ -533,41 +562,6 @@ extern "C" lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const 
   hipLaunchKernelGGL(relu_dropout_bwd_f32, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), n4,
                      reinterpret_cast<const float4 *>(g), reinterpret_cast<const float4 *>(y), scale,
                      reinterpret_cast<float4 *>(out));
-  LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
-extern "C" int64_t lpg_linear_small_bwd_workspace_bytes(int64_t M, int64_t K, int64_t N) {
-  if (M < 0 || K < 0 || N < 0) return -1;
-  const int64_t nblk = (M + kRowsPerBlock - 1) / kRowsPerBlock;
-  return nblk * (N * K + N) * (int64_t)sizeof(float);
-}
-
-extern "C" lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
-                                               const float *W, const float *H, int64_t ldh, float *dH, int64_t lddh,
-                                               float *dW, float *db, void *workspace, void *stream) {
-  LPG_REQUIRE(M >= 0 && K >= 0 && N >= 1 && N <= kSmallNMax, "lpg_linear_small_bwd_f32: need 1 <= N <= %d",
-              kSmallNMax);
-  LPG_REQUIRE(K % 4 == 0 && ldh % 4 == 0 && (dH == nullptr || lddh % 4 == 0), "lpg_linear_small_bwd_f32: K and leading dims must be multiples of 4");
-  LPG_REQUIRE(G && W && H && workspace, "lpg_linear_small_bwd_f32: NULL pointer");
-  LPG_REQUIRE(aligned16(W) && aligned16(H) && (dH == nullptr || aligned16(dH)) && aligned16(workspace),
-              "lpg_linear_small_bwd_f32: W/H/dH/workspace must be 16-byte aligned");
-  hipStream_t s = as_stream(stream);
-  const int64_t nblk = (M + kRowsPerBlock - 1) / kRowsPerBlock;
-  float *part = static_cast<float *>(workspace);
-  if (nblk > 0) {
-    hipLaunchKernelGGL(linear_small_bwd_p1, dim3((unsigned)nblk), dim3(256), 0, s, M, K, (int)N, G, ldg, W, H, ldh,
-                       dH, lddh, part);
-    LPG_HIP(hipGetLastError());
-  }
-  const int64_t tot = N * K + N;
-  if (nblk == 0) {
-    if (dW) LPG_HIP(hipMemsetAsync(dW, 0, sizeof(float) * N * K, s));
-    if (db) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, s));
-    return LPG_OK;
-  }
-  hipLaunchKernelGGL(linear_small_bwd_p2, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, nblk, K, (int)N,
-                     part, dW, db);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }

@@ -31,6 +31,10 @@ HEADER_SYMBOLS = (
     "lpg_fc_f32",
     "lpg_fc_set_variant",
     "lpg_relu_dropout_bwd_f32",
+    "lpg_relu_bwd_colsum_workspace_bytes",
+    "lpg_relu_bwd_colsum_f32",
+    "lpg_wgrad_smallk_workspace_bytes",
+    "lpg_wgrad_smallk_f32",
     "lpg_linear_small_bwd_workspace_bytes",
     "lpg_linear_small_bwd_f32",
     "lpg_knowledge_f32",
@@ -74,6 +78,16 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_f32.restype = c_i32
     L.lpg_relu_dropout_bwd_f32.argtypes = [c_i64, c_p, c_p, ctypes.c_float, c_p, c_p]
     L.lpg_relu_dropout_bwd_f32.restype = c_i32
+    L.lpg_relu_bwd_colsum_workspace_bytes.argtypes = [c_i64, c_i64]
+    L.lpg_relu_bwd_colsum_workspace_bytes.restype = c_i64
+    L.lpg_relu_bwd_colsum_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_i64, ctypes.c_float, c_p, c_i64, c_p, c_p,
+                                          c_p]
+    L.lpg_relu_bwd_colsum_f32.restype = c_i32
+    L.lpg_wgrad_smallk_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
+    L.lpg_wgrad_smallk_workspace_bytes.restype = c_i64
+    L.lpg_wgrad_smallk_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                                       c_p]
+    L.lpg_wgrad_smallk_f32.restype = c_i32
     L.lpg_linear_small_bwd_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
     L.lpg_linear_small_bwd_workspace_bytes.restype = c_i64
     L.lpg_linear_small_bwd_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p,

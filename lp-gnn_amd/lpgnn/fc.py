@@ -86,6 +86,47 @@ def relu_dropout_bwd(g: Tensor, y: Tensor, scale: float) -> Tensor:
     return out
 
 
+def _workspace(nbytes: int, device) -> Tensor:
+    return torch.empty(max(int(nbytes), 16) // 4 + 4, dtype=torch.float32, device=device)
+
+
+def relu_bwd_colsum(g: Tensor, y: Tensor, scale: float, want_db: bool):
+    """(dZ, db): dZ = (y > 0) ? g * scale : 0 and db = dZ.sum(0) in one pass."""
+    M, N = g.shape
+    g = g if (g.stride(1) == 1 and g.stride(0) % 4 == 0 and g.data_ptr() % 16 == 0) else g.contiguous()
+    if N % 4 or y.stride(1) != 1 or y.stride(0) % 4 or y.data_ptr() % 16:
+        dz = relu_dropout_bwd(g, y, scale)
+        return dz, (dz.sum(0) if want_db else None)
+    out = torch.empty((M, N), dtype=torch.float32, device=g.device)
+    L = _lib.lib()
+    db = torch.empty(N, dtype=torch.float32, device=g.device) if want_db else None
+    ws = _workspace(L.lpg_relu_bwd_colsum_workspace_bytes(M, N), g.device) if want_db else None
+    with torch.cuda.device(g.device):
+        st = L.lpg_relu_bwd_colsum_f32(M, N, g.data_ptr(), g.stride(0), y.data_ptr(), y.stride(0), float(scale),
+                                       out.data_ptr(), N, None if db is None else db.data_ptr(),
+                                       None if ws is None else ws.data_ptr(), _lib.stream_of(g))
+    _lib.check(st, "lpg_relu_bwd_colsum_f32")
+    return out, db
+
+
+def wgrad_smallk(dz: Tensor, A1: Tensor, A2: Tensor | None):
+    """(dW1, dW2) = (dZ^T A1, dZ^T A2) for narrow inputs (K1 + K2 <= 16)."""
+    M, N = dz.shape
+    A1 = A1.contiguous()
+    A2 = None if A2 is None else A2.contiguous()
+    K1, K2 = A1.shape[1], (0 if A2 is None else A2.shape[1])
+    L = _lib.lib()
+    ws = _workspace(L.lpg_wgrad_smallk_workspace_bytes(M, N, K1 + K2), dz.device)
+    dW1 = torch.empty((N, K1), dtype=torch.float32, device=dz.device)
+    dW2 = torch.empty((N, K2), dtype=torch.float32, device=dz.device) if K2 else None
+    with torch.cuda.device(dz.device):
+        st = L.lpg_wgrad_smallk_f32(M, N, dz.data_ptr(), dz.stride(0), K1, A1.data_ptr(), max(K1, 1), K2,
+                                    None if A2 is None else A2.data_ptr(), max(K2, 1), dW1.data_ptr(),
+                                    None if dW2 is None else dW2.data_ptr(), ws.data_ptr(), _lib.stream_of(dz))
+    _lib.check(st, "lpg_wgrad_smallk_f32")
+    return dW1, dW2
+
+
 def _new_seed() -> int:
     """A dropout seed from torch's default generator (torch.manual_seed reproducible)."""
     return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
@@ -106,13 +147,22 @@ class _FC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gC):
         A1, A2, W1, W2, C = ctx.saved_tensors
-        g = relu_dropout_bwd(gC, C, ctx.scale) if ctx.relu else gC
         need = ctx.needs_input_grad
+        want_db = ctx.has_b and need[4]
+        if ctx.relu:
+            g, db = relu_bwd_colsum(gC, C, ctx.scale, want_db)  # ReLU + dropout bwd, bias grad fused
+        else:
+            g, db = gC, (gC.sum(0) if want_db else None)
         dA1 = g @ W1 if need[0] else None
         dA2 = g @ W2 if ctx.has_a2 and need[1] else None
-        dW1 = g.t() @ A1 if need[2] else None
-        dW2 = g.t() @ A2 if ctx.has_a2 and need[3] else None
-        db = g.sum(0) if ctx.has_b and need[4] else None
+        K = A1.shape[1] + (A2.shape[1] if ctx.has_a2 else 0)
+        if (need[2] or need[3]) and K <= 16 and g.shape[1] % 4 == 0:
+            dW1, dW2 = wgrad_smallk(g, A1, A2 if ctx.has_a2 else None)  # conv1: dZ read once
+            dW1 = dW1 if need[2] else None
+            dW2 = dW2 if need[3] else None
+        else:
+            dW1 = g.t() @ A1 if need[2] else None
+            dW2 = g.t() @ A2 if ctx.has_a2 and need[3] else None
         return dA1, dA2, dW1, dW2, db, None, None
 
 

@@ -18,6 +18,11 @@ DEV = "cuda:0"
     (129, 130, 36, 20, False, False),     # ragged tiles, no bias
     (257, 64, 1024, 12, True, True),
     (64, 33, 0, 40, True, True),          # only the root part
+    (1, 4, 4, 0, True, False),            # narrow-input (small-K) kernel ...
+    (5001, 1028, 8, 8, True, True),       # ... ragged column chunk
+    (333, 1024, 12, 4, False, True),
+    (77, 64, 16, 0, True, True),
+    (100, 30, 8, 8, True, True),          # N % 4 != 0: tiled MFMA path
 ])
 def test_fc_bitwise(M, N, K1, K2, relu, bias):
     from lpgnn.fc import fc_forward
@@ -45,6 +50,24 @@ def test_fc_bitwise(M, N, K1, K2, relu, bias):
     if relu:
         want = np.maximum(want, 0)
     np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.25])
+def test_fc_smallk_equals_tiled_path(p):
+    """The narrow-input kernel (K1 + K2 <= 16) and the MFMA tile kernel give
+    the same bits, dropout mask included: zero-padding K1 to 20 moves the
+    same chain onto the tiled path (fma(0, 0, p) = p)."""
+    from lpgnn.fc import fc_forward
+
+    torch.manual_seed(5)
+    M, N = 2050, 1024
+    A1, A2 = torch.randn(M, 8, device=DEV), torch.randn(M, 8, device=DEV)
+    W1, W2 = torch.randn(N, 8, device=DEV) * 0.3, torch.randn(N, 8, device=DEV) * 0.3
+    b = torch.randn(N, device=DEV) * 0.1
+    pad = lambda x: torch.cat([x, torch.zeros(x.shape[0], 12, device=DEV)], 1).contiguous()
+    small = fc_forward(A1, W1, A2, W2, b, True, p, seed=77)
+    tiled = fc_forward(pad(A1), pad(W1), A2, W2, b, True, p, seed=77)
+    assert torch.equal(small, tiled)
 
 
 def test_fc_odd_k_is_padded_exactly():
@@ -207,9 +230,54 @@ def test_linear_small_bwd_matches_torch(M, K, N):
     for t in (x, W, b):
         t.grad = None
     torch.nn.functional.linear(x, W, b).backward(g)
-    # fp32 sums over M rows in different orders: compare both against fp64
+    # fp32 sums over M rows in a different order than torch's: check both against
+    # fp64 with the recursive-summation bound |err| <= L * 2^-24 * sum|terms|,
+    # L = the longest add chain (rows per block + number of blocks)
     xd, Wd, gd = x.detach().double(), W.detach().double(), g.double()
     ref = (gd @ Wd, gd.t() @ xd, gd.sum(0))
-    for a, t, r in zip(got, (x.grad, W.grad, b.grad), ref):
-        err_mine, err_torch = (a.double() - r).abs().max().item(), (t.double() - r).abs().max().item()
-        assert err_mine <= 4 * err_torch + 1e-5 * max(1.0, r.abs().max().item() / 100), (err_mine, err_torch)
+    mag = (gd.abs() @ Wd.abs(), gd.abs().t() @ xd.abs(), gd.abs().sum(0))
+    chain = 128 + (M + 127) // 128 + N
+    for a, t, r, s in zip(got, (x.grad, W.grad, b.grad), ref, mag):
+        err = (a.double() - r).abs()
+        assert bool((err <= chain * 2.0 ** -24 * s + 1e-30).all()), (err.max().item(), (t.double() - r).abs().max().item())
+
+
+@pytest.mark.parametrize("M,N", [(1, 4), (63, 8), (1000, 1024), (4099, 1028), (70000, 256)])
+def test_relu_bwd_colsum(M, N):
+    from lpgnn.fc import relu_bwd_colsum
+
+    torch.manual_seed(M + N)
+    g = torch.randn(M, N, device=DEV)
+    y = torch.relu(torch.randn(M, N, device=DEV))
+    out, db = relu_bwd_colsum(g, y, 1.25, True)
+    want = torch.where(y > 0, g * 1.25, torch.zeros((), device=DEV))
+    assert torch.equal(out, want)
+    # block-ordered deterministic sum: matches fp64 within the recursive-summation bound
+    chain = 64 + (M + 63) // 64
+    err = (db.double() - want.double().sum(0)).abs()
+    assert bool((err <= chain * 2.0 ** -24 * want.double().abs().sum(0) + 1e-30).all())
+    out2, db2 = relu_bwd_colsum(g, y, 1.25, True)
+    assert torch.equal(db, db2)  # run-to-run deterministic
+    out3, none = relu_bwd_colsum(g, y, 1.25, False)
+    assert none is None and torch.equal(out3, want)
+
+
+@pytest.mark.parametrize("M,N,K1,K2", [(1, 4, 8, 8), (1000, 1024, 8, 8), (5000, 260, 3, 0), (70001, 1024, 8, 8),
+                                       (300, 64, 1, 15)])
+def test_wgrad_smallk(M, N, K1, K2):
+    from lpgnn.fc import wgrad_smallk
+
+    torch.manual_seed(M)
+    dz = torch.randn(M, N, device=DEV)
+    A1 = torch.randn(M, K1, device=DEV)
+    A2 = torch.randn(M, K2, device=DEV) if K2 else None
+    dW1, dW2 = wgrad_smallk(dz, A1, A2)
+    chain = 256 + (M + 255) // 256
+    for dW, A in ((dW1, A1), (dW2, A2)):
+        if A is None:
+            assert dW is None
+            continue
+        r = dz.double().t() @ A.double()
+        s = dz.double().abs().t() @ A.double().abs()
+        err = (dW.double() - r).abs()
+        assert dW.shape == (N, A.shape[1]) and bool((err <= chain * 2.0 ** -24 * s + 1e-30).all())
