@@ -182,6 +182,45 @@ lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t ldl, const f
  * Infinity Cache; see DESIGN.md. */
 lpg_status lpg_spmm_set_slice(int64_t cols_per_slice);
 
+/* ---- k-hop neighbour sampling (NeighborLoader collate, train.py:111-116,
+ * val.py:22-27; replaces torch_sparse 0.6.12 neighbor_sample) -------------
+ * Graph = CSC of the homogeneous LP graph: colptr [N+1], row [E] (sources of
+ * node v's in-edges, sorted).  All ids int64.  `local` [N] must hold -1 and
+ * `first` [N] all ones (UINT64_MAX) between batches; the calls below restore
+ * them (lpg_sample_reset for `local`).  A hop is
+ *   count -> lpg_scan_i64 -> fill -> dedupe -> lpg_scan_i64(flag) -> assign;
+ * node ids are assigned in first-appearance order (frontier order, then
+ * neighbour order) exactly as neighbor_sample's sequential insertion.
+ * fanout < 0 = all neighbours; fanout <= 256. */
+int64_t lpg_scan_i64_workspace_bytes(int64_t n);
+/* out [n + 1]: out[0] = 0, out[i + 1] = in[0] + ... + in[i] */
+lpg_status lpg_scan_i64(const int64_t *in, int64_t n, int64_t *out, void *workspace, int64_t workspace_bytes,
+                        void *stream);
+lpg_status lpg_sample_count(const int64_t *frontier, int64_t nf, const int64_t *colptr, int64_t fanout,
+                            int64_t *counts, void *stream);
+/* candidates of frontier node i go to [offsets[i], offsets[i+1]); cand_dst =
+ * base + i (the frontier node's local id), cand_edge = CSC position */
+lpg_status lpg_sample_fill(const int64_t *frontier, int64_t nf, int64_t base, const int64_t *colptr,
+                           const int64_t *row, int64_t fanout, uint64_t seed, const int64_t *offsets,
+                           int64_t *cand, int64_t *cand_edge, int64_t *cand_dst, void *stream);
+/* flag[p] = 1 iff cand[p] is unsampled and p is its first appearance */
+lpg_status lpg_sample_dedupe(const int64_t *cand, int64_t nc, const int64_t *local, uint64_t *first,
+                             int64_t *flag, void *stream);
+/* where flag[p]: nodes[rank[p]] = cand[p] (this hop's chunk) and
+ * local[cand[p]] = base + rank[p] (its local id) */
+lpg_status lpg_sample_assign(const int64_t *cand, int64_t nc, int64_t base, const int64_t *flag,
+                             const int64_t *rank, int64_t *nodes, int64_t *local, uint64_t *first, void *stream);
+/* out[p] = local[cand[p]] (directed=True edge rows) */
+lpg_status lpg_sample_local_ids(const int64_t *cand, int64_t nc, const int64_t *local, int64_t *out, void *stream);
+/* directed=False: edges of the subgraph induced on nodes[0..ns) --
+ * per destination i, in CSC order: (row = local[src], col = i, edge = CSC pos) */
+lpg_status lpg_induced_count(const int64_t *nodes, int64_t ns, const int64_t *colptr, const int64_t *row,
+                             const int64_t *local, int64_t *counts, void *stream);
+lpg_status lpg_induced_fill(const int64_t *nodes, int64_t ns, const int64_t *colptr, const int64_t *row,
+                            const int64_t *local, const int64_t *offsets, int64_t *out_row, int64_t *out_col,
+                            int64_t *out_edge, void *stream);
+lpg_status lpg_sample_reset(const int64_t *nodes, int64_t ns, int64_t *local, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,6 +3,7 @@
 Public surface (mirrors the reference's names):
   arch:  GCN_FC, GraphConvTwoDirection, GraphConv, add_knowledge, build_model
   data:  MyToBipartite, lp_to_unipartite, batch_to, BipartiteBatch
+  loader: NeighborLoader, NeighborSampler (device k-hop sampling)
   sparse: BipartiteCSR (the batch's edge_index), spmm
   val:   inference_gnn, accuracy, model_inference_with_batch
   train: balanced, labels_to_balanced_weights, train_step, make_optimizer
@@ -11,11 +12,12 @@ from . import _lib
 from .sparse import BipartiteCSR, CSR, spmm
 from .arch import GCN_FC, GraphConv, GraphConvTwoDirection, Linear, add_knowledge, build_model
 from .data import BipartiteBatch, MyToBipartite, UnipartiteData, batch_to, lp_to_unipartite
+from .loader import NeighborLoader, NeighborSampler
 
 __all__ = [
     "BipartiteCSR", "CSR", "spmm", "GCN_FC", "GraphConv", "GraphConvTwoDirection", "Linear",
     "add_knowledge", "build_model", "BipartiteBatch", "MyToBipartite", "UnipartiteData", "batch_to",
-    "lp_to_unipartite",
+    "lp_to_unipartite", "NeighborLoader", "NeighborSampler",
 ]
 
 

@@ -38,6 +38,16 @@ HEADER_SYMBOLS = (
     "lpg_linear_small_bwd_workspace_bytes",
     "lpg_linear_small_bwd_f32",
     "lpg_knowledge_f32",
+    "lpg_scan_i64_workspace_bytes",
+    "lpg_scan_i64",
+    "lpg_sample_count",
+    "lpg_sample_fill",
+    "lpg_sample_dedupe",
+    "lpg_sample_assign",
+    "lpg_sample_local_ids",
+    "lpg_induced_count",
+    "lpg_induced_fill",
+    "lpg_sample_reset",
 )
 
 c_i64, c_i32, c_p = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
@@ -97,6 +107,20 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_set_variant.restype = c_i32
     L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_i64, ctypes.c_float, c_p, c_i64, c_p]
     L.lpg_knowledge_f32.restype = c_i32
+    L.lpg_scan_i64_workspace_bytes.argtypes = [c_i64]
+    L.lpg_scan_i64_workspace_bytes.restype = c_i64
+    L.lpg_scan_i64.argtypes = [c_p, c_i64, c_p, c_p, c_i64, c_p]
+    L.lpg_sample_count.argtypes = [c_p, c_i64, c_p, c_i64, c_p, c_p]
+    L.lpg_sample_fill.argtypes = [c_p, c_i64, c_i64, c_p, c_p, c_i64, ctypes.c_uint64, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_sample_dedupe.argtypes = [c_p, c_i64, c_p, c_p, c_p, c_p]
+    L.lpg_sample_assign.argtypes = [c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_sample_local_ids.argtypes = [c_p, c_i64, c_p, c_p, c_p]
+    L.lpg_induced_count.argtypes = [c_p, c_i64, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_induced_fill.argtypes = [c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_sample_reset.argtypes = [c_p, c_i64, c_p, c_p]
+    for nm in ("lpg_scan_i64", "lpg_sample_count", "lpg_sample_fill", "lpg_sample_dedupe", "lpg_sample_assign",
+               "lpg_sample_local_ids", "lpg_induced_count", "lpg_induced_fill", "lpg_sample_reset"):
+        getattr(L, nm).restype = c_i32
     _lib = L
     return L
 

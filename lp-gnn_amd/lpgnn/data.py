@@ -108,21 +108,24 @@ class MyToBipartite:
         nvars = int(is_vars.sum().item())
         ncons = nnodes - nvars
 
-        mapping_vec = torch.empty(ncons + nvars, dtype=torch.long)
-        mapping_vec[is_cons] = torch.arange(ncons)
-        mapping_vec[is_vars] = torch.arange(nvars) + ncons
+        where = batch.edge_index.device
+        mapping_vec = torch.empty(ncons + nvars, dtype=torch.long, device=where)
+        mapping_vec[is_cons] = torch.arange(ncons, device=where)
+        mapping_vec[is_vars] = torch.arange(nvars, device=where) + ncons
         edge_index = mapping_vec[batch.edge_index]
 
         edge_mask = edge_index[0, :] < ncons
         assert edge_mask.sum().item() * 2 == edge_mask.shape[0]  # dataset.py:297
         edge_index_l2r = edge_index[:, edge_mask].clone()
         edge_index_l2r[1, :] -= ncons
+        # a batch already in HBM (the device NeighborLoader) is packed where it is
+        pack_dev = where if where.type == "cuda" else self.dev
         adj = BipartiteCSR.from_edge_index(edge_index_l2r, batch.edge_attr[edge_mask], (ncons, nvars),
-                                           device=self.dev)
+                                           device=pack_dev)
         bs = getattr(batch, "batch_size", None) or batch.num_nodes
         t_bs = int(batch.is_vars[:bs].sum().item())
         extra = {k: v for k, v in vars(batch).items()
-                 if k not in ("x", "y", "edge_index", "edge_attr", "is_vars", "num_nodes", "batch")}
+                 if k not in ("x", "y", "edge_index", "edge_attr", "is_vars", "num_nodes", "batch", "batch_size")}
         return BipartiteBatch(x_s=batch.x[is_cons, :], x_t=batch.x[is_vars, :], y_s=batch.y[is_cons],
                               y_t=batch.y[is_vars], edge_index=adj, bs=bs, s_bs=bs - t_bs, t_bs=t_bs, **extra)
 

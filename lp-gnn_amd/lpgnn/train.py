@@ -70,6 +70,27 @@ def make_optimizer(model, opt="adam", lr=1e-3, epochs=800):
     return o, StepLR(o, step_size=max(epochs // 4, 1), gamma=0.1)
 
 
+def epoch_batches(graph, arch: str = "GCN_FC(8,8)", batch_size: int = 10240 * 8 * 4, dev="cuda", seed=None):
+    """train.py:103-116: a bipartite graph is one batch; a homogeneous one
+    (above the MyToBipartite threshold) is cut into seed batches by the
+    device k-hop NeighborLoader (6 sampled neighbours per hop, depth-1 hops,
+    shuffled, drop_last, induced subgraphs)."""
+    import numpy as np
+
+    from .arch import arch_depth
+    from .data import MyToBipartite
+    from .loader import NeighborLoader
+
+    if hasattr(graph, "x_s"):
+        return [graph]
+    if graph.edge_index.shape[-1] == 0:
+        return []
+    bs = min(int(batch_size), int(graph.num_nodes))
+    return NeighborLoader(graph, num_neighbors=[6] * arch_depth(arch), input_nodes=None, directed=False,
+                          shuffle=True, transform=MyToBipartite(thresh_num=np.inf), batch_size=bs,
+                          drop_last=True, device=dev, seed=seed)
+
+
 def train_step(model, batch, opt, loss="balanced", check_nan=True):
     """One inner iteration of train.py:117-129: forward on the batch, slice
     the seed nodes, loss, backward, optimizer step.  Returns the loss tensor

@@ -54,16 +54,29 @@ def accuracy(logits, gt, num_cons, return_pr=False, dataset_name=""):
 
 
 @torch.no_grad()
-def model_inference_with_batch(model, batch, arch: str = "GCN_FC(8,8)", dev="cuda"):
-    """val.py:12-36 for a bipartite batch (full-graph forward).
+def model_inference_with_batch(model, batched_graphs, arch: str = "GCN_FC(8,8)", dev="cuda",
+                               batch_size: int = 10240 * 8 * 4):
+    """val.py:12-36.  A bipartite batch runs full-graph; a homogeneous graph
+    (above MyToBipartite's threshold) goes through the device k-hop
+    NeighborLoader with every neighbour (num_neighbors=[-1]*(depth-1),
+    directed=False, val.py:22-27) in seed order, and the seed logits are
+    concatenated -- equal to the full-graph logits up to summation order
+    (the reference's own check, val.py:37-41)."""
+    from .data import MyToBipartite
+    from .loader import NeighborLoader
 
-    Graphs above the NeighborLoader threshold (nnz > 12e6, utils.py:808) are
-    run full-graph too: one MI355X holds the whole graph (288 GB HBM) and
-    the partitioned path (lpgnn.partition) covers multi-GPU; the k-hop
-    sampler is §8f rank 4 ("next").
-    """
-    _ = arch_depth(arch)
+    depth = arch_depth(arch)
     model.eval()
-    batch = batch.to(dev)
-    lc, lv = model(batch)
-    return lc[:batch.s_bs].cpu(), lv[:batch.t_bs].cpu()
+    if hasattr(batched_graphs, "x_s"):
+        loader = [batched_graphs]
+    else:
+        bs = min(int(batch_size), int(batched_graphs.num_nodes))
+        loader = NeighborLoader(batched_graphs, num_neighbors=[-1] * depth, input_nodes=None, directed=False,
+                                shuffle=False, transform=MyToBipartite(thresh_num=np.inf), batch_size=bs,
+                                drop_last=False, device=dev)
+    lc, lv = [], []
+    for batch in loader:
+        batch = batch.to(dev)
+        logit_cons, logit_vars = model(batch)
+        lc.append(logit_cons[:batch.s_bs].cpu()), lv.append(logit_vars[:batch.t_bs].cpu())
+    return torch.cat(lc, 0), torch.cat(lv, 0)

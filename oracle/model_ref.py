@@ -12,7 +12,8 @@ Every function cites what it restates:
 * upstream, NOT vendored in /root/reference, restated from the versions the
   reference pins (readme.md:51-52): torch_geometric 2.1 (``GraphConv``,
   ``Linear`` init, ``to_undirected``) and torch_sparse 0.6.12
-  (``SparseTensor.from_edge_index``, ``.t()``/``csr2csc``, ``spmm_sum``).
+  (``SparseTensor.from_edge_index``, ``.t()``/``csr2csc``, ``spmm_sum``,
+  ``neighbor_sample`` behind PyG's ``NeighborLoader``).
 
 Parity pinning (see DESIGN.md "Parity"): the pure-torch reference functions
 (add_knowledge arch.py:129-141, inference_gnn val.py:106-124, balanced
@@ -350,7 +351,72 @@ def to_undirected(edge_index: np.ndarray, edge_attr: np.ndarray, num_nodes: int)
     return np.stack([uniq // num_nodes, uniq % num_nodes]), summed.astype(np.float32)
 
 
-def my_to_bipartite(x, y, is_vars, edge_index, edge_attr, num_nodes):
+def to_csc(edge_index: np.ndarray, num_nodes: int):
+    """PyG 2.1 ``loader.utils.to_csc`` (what NeighborSampler builds at
+    construction): perm = argsort(col * N + row); colptr from the sorted
+    destinations; row = sources in that order."""
+    row, col = np.asarray(edge_index[0], np.int64), np.asarray(edge_index[1], np.int64)
+    perm = np.argsort(col * num_nodes + row, kind="stable")
+    colptr = np.searchsorted(col[perm], np.arange(num_nodes + 1))
+    return colptr.astype(np.int64), row[perm], perm
+
+
+def neighbor_sample(colptr, row, input_node, num_neighbors, directed: bool):
+    """torch_sparse 0.6.12 ``neighbor_sample`` (csrc/cpu/neighbor_sample_cpu.cpp,
+    replace=False), the sampler of PyG 2.1 NeighborLoader (train.py:111-116,
+    val.py:22-27).  Only fanout -1 (all neighbours, val.py:23) is
+    deterministic; a positive fanout is restated with Floyd's algorithm and
+    Python's RNG, so only its properties are comparable.
+
+    samples = input nodes; per hop, for every frontier node in order, every
+    (or each sampled) in-neighbour v in CSC order is inserted into
+    to_local_node if new (appended to samples); directed=True records the
+    edge (local(v) -> frontier index).  directed=False instead returns, for
+    every sample i in order, each in-edge whose source is sampled."""
+    import random
+
+    samples = [int(v) for v in input_node]
+    to_local = {}
+    for i, v in enumerate(samples):
+        to_local.setdefault(v, i)
+    rows, cols, edges = [], [], []
+    begin, end = 0, len(samples)
+    for k in num_neighbors:
+        for i in range(begin, end):
+            w = samples[i]
+            c0, c1 = int(colptr[w]), int(colptr[w + 1])
+            deg = c1 - c0
+            if deg == 0:
+                continue
+            if k < 0 or k >= deg:
+                picks = range(deg)
+            else:
+                chosen, picks = set(), []
+                for j in range(deg - k, deg):
+                    t = random.randint(0, j)
+                    if t in chosen:
+                        t = j
+                    chosen.add(t)
+                    picks.append(t)
+            for t in picks:
+                v = int(row[c0 + t])
+                if v not in to_local:
+                    to_local[v] = len(samples)
+                    samples.append(v)
+                if directed:
+                    rows.append(to_local[v]), cols.append(i), edges.append(c0 + t)
+        begin, end = end, len(samples)
+    if not directed:
+        for i, w in enumerate(samples):
+            for e in range(int(colptr[w]), int(colptr[w + 1])):
+                v = int(row[e])
+                if v in to_local:
+                    rows.append(to_local[v]), cols.append(i), edges.append(e)
+    a = lambda x: np.asarray(x, dtype=np.int64)
+    return a(samples), a(rows), a(cols), a(edges)
+
+
+def my_to_bipartite(x, y, is_vars, edge_index, edge_attr, num_nodes, bs=None):
     """MyToBipartite.__call__, dataset.py:275-332 (batch_size = num_nodes).
 
     Returns dict(x_s, x_t, y_s, y_t, A=(rowptr,col,val), m, n, s_bs, t_bs).
@@ -368,7 +434,7 @@ def my_to_bipartite(x, y, is_vars, edge_index, edge_attr, num_nodes):
     l2r = ei[:, mask].copy()
     l2r[1] -= ncons
     A = csr_from_coo(l2r[0], l2r[1], np.asarray(edge_attr)[mask], ncons, nvars)
-    bs = num_nodes
+    bs = num_nodes if bs is None else bs
     t_bs = int(is_vars[:bs].sum())
     return dict(x_s=x[is_cons], x_t=x[is_vars], y_s=y[is_cons], y_t=y[is_vars], A=A, m=ncons, n=nvars,
                 s_bs=bs - t_bs, t_bs=t_bs)
