@@ -48,22 +48,30 @@ struct FcArgs {
   float drop_scale;
 };
 
-// Counter-based dropout RNG: splitmix64 finaliser of (seed, element index).
-// Stateless, so the backward pass never needs the mask (the kept set is
-// exactly where the stored output is > 0).
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9e3779b97f4a7c15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+// Counter-based dropout RNG over (seed, row, col): two rounds of the 32-bit
+// "lowbias32" integer hash, the inner one keyed by the row only (so a lane
+// reuses it across its columns).  Stateless, so the backward pass never needs
+// the mask (the kept set is exactly where the stored output is > 0).  32-bit
+// on purpose: 64-bit multiplies are multi-instruction on CDNA and made the
+// epilogue ~10% of a hidden-layer FC.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int64_t row, int64_t col) {
+  const uint32_t hr = lowbias32((uint32_t)row ^ (uint32_t)seed);
+  return lowbias32(hr ^ ((uint32_t)col * 0x9e3779b9u) ^ (uint32_t)(seed >> 32));
 }
 
 __device__ __forceinline__ float epilogue(const FcArgs &a, float v, float b, int64_t row, int64_t col, bool relu) {
   if (a.bias) v = v + b;
   if (relu) v = (v < 0.f) ? 0.f : v;
-  if (a.drop_thresh) v = drop_hash(a.seed, (uint64_t)row * (uint64_t)a.N + (uint64_t)col) >= a.drop_thresh
-                             ? v * a.drop_scale : 0.f;
+  if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
   return v;
 }
 

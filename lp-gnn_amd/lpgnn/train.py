@@ -9,17 +9,23 @@ from torch.optim.lr_scheduler import StepLR
 
 @torch.no_grad()
 def labels_to_balanced_weights(labels, merge_lu=True):
-    """utils.py:286-299: w[c] = N / count_c for present classes; with all
-    three classes present, w0 = w2 = mean(w0, w2)."""
-    res = torch.zeros(3).to(labels.device)
-    lbl, cnt = torch.unique(labels, return_counts=True)
+    """utils.py:286-299: w[c] = N / count_c for present classes; unless
+    exactly two classes are present, w0 = w2 = mean(w0, w2).
+
+    Restated without torch.unique / len(lbl) (which force a device->host
+    sync every step): class counts by scatter-add,
+    the same N / count_c division, branch choices as tensor selects --
+    bitwise the reference's result (tests/test_gpu_model.py)."""
+    labels = labels.view(-1)
+    cnt = torch.zeros(3, dtype=torch.int64, device=labels.device)
+    cnt.scatter_add_(0, labels, torch.ones_like(labels))
+    present = cnt > 0
     wei = cnt.sum() / cnt
-    if len(lbl) == 2:
-        res[lbl] = wei
-    else:
-        res[lbl] = wei
-        if merge_lu:
-            res[0] = res[2] = (res[0] + res[2]) / 2.
+    res = torch.where(present, wei, torch.zeros((), dtype=wei.dtype, device=labels.device))
+    if merge_lu:
+        merged = (res[0] + res[2]) / 2.
+        two = present.sum() == 2
+        res = torch.stack([torch.where(two, res[0], merged), res[1], torch.where(two, res[2], merged)])
     return res
 
 

@@ -15,8 +15,9 @@ from .arch import arch_depth
 
 
 @torch.no_grad()
-def inference_gnn(logits, m, **kwargs):
-    """val.py:106-124."""
+def inference_gnn(logits, m, check: bool = True, **kwargs):
+    """val.py:106-124.  ``check=False`` skips the two invariant asserts
+    (val.py:119-122), the only host syncs, for per-step use on the device."""
     n = logits.shape[0] - m
     pr = F.softmax(logits.float(), dim=-1)
     pr = pr.clone()
@@ -25,9 +26,31 @@ def inference_gnn(logits, m, **kwargs):
     pr[:, 1] = pr.min() - 1
     pr[topk_idx, 1] = pr.max() + 1
     pred = pr.argmax(-1)
-    assert (pred == 1).sum().item() == m
-    assert (pred[m:m + n] == 1).sum().item() == ((pred[:m] == 0) | (pred[:m] == 2)).sum().item()
+    if check:
+        assert (pred == 1).sum().item() == m
+        assert (pred[m:m + n] == 1).sum().item() == ((pred[:m] == 0) | (pred[:m] == 2)).sum().item()
     return pred
+
+
+@torch.no_grad()
+def accuracy_device(logits, gt, num_cons):
+    """accuracy(..., return_pr=True) (val.py:199-237) computed on the device
+    with no host sync: per-side accuracy averaged, and sklearn's
+    precision/recall for labels=[1], zero_division=0, averaged over sides.
+    Returns three 0-dim tensors."""
+    pred = inference_gnn(logits, num_cons, check=False)
+
+    def side(p, g):
+        acc = (p == g).float().mean()
+        tp = ((p == 1) & (g == 1)).sum().float()
+        pp, gp = (p == 1).sum().float(), (g == 1).sum().float()
+        prec = torch.where(pp > 0, tp / pp.clamp(min=1), torch.zeros_like(tp))
+        rec = torch.where(gp > 0, tp / gp.clamp(min=1), torch.zeros_like(tp))
+        return acc, prec, rec
+
+    a1, p1, r1 = side(pred[:num_cons], gt[:num_cons])
+    a2, p2, r2 = side(pred[num_cons:], gt[num_cons:])
+    return (a1 + a2) / 2., (p1 + p2) / 2., (r1 + r2) / 2.
 
 
 @torch.no_grad()

@@ -163,3 +163,30 @@ def test_training_step_runs_and_matches_oracle_grads():
     for _ in range(3):
         L = train_step(model, batch, opt)
     assert torch.isfinite(L).item()
+
+
+@pytest.mark.parametrize("labels", [[0, 1, 2, 1, 1, 0], [1, 1, 2, 2, 2], [0, 0, 0], [1, 1], [2, 1, 2],
+                                    [0, 2, 0, 2, 0], list(np.random.default_rng(0).integers(0, 3, 50000))])
+@pytest.mark.parametrize("merge", [True, False])
+def test_balanced_weights_sync_free_equal_reference(labels, merge):
+    """The sync-free class weights == the reference formula (oracle
+    restatement of utils.py:286-299, pinned by golden vectors) bit for bit."""
+    from lpgnn.train import labels_to_balanced_weights
+
+    t = torch.tensor(labels, dtype=torch.int64)
+    want = O.labels_to_balanced_weights(t, merge_lu=merge)
+    got = labels_to_balanced_weights(t.to(DEV), merge_lu=merge).cpu()
+    assert torch.equal(got, want), (got, want)
+
+
+def test_accuracy_device_matches_sklearn_path():
+    from lpgnn.val import accuracy, accuracy_device
+
+    rng = np.random.default_rng(1)
+    for m, n in ((300, 500), (50, 7), (1, 1)):
+        logits = torch.from_numpy(rng.standard_normal((m + n, 3)).astype(np.float32))
+        gt = torch.from_numpy(rng.integers(0, 3, m + n))
+        want = accuracy(logits, gt, m, return_pr=True)
+        got = accuracy_device(logits.to(DEV), gt.to(DEV), m)
+        for a, b in zip(got, want):
+            assert abs(a.item() - float(b)) < 1e-6
