@@ -12,6 +12,10 @@ grads), Adam step.  value = (hid-width SpMM edge traversals in the step) /
 step time, whole job.  N>1: one process per GPU (torchrun), each owning a
 c2-sized constraint-row partition of an N-times larger graph (see
 lpgnn.partition); boundary-variable rows are all-reduced over RCCL.
+
+``--config c5`` runs BASELINE.json configs[4] instead (same graph,
+GCN_FC hids=2048 depth=6, bf16 activations / SpMM storage / MFMA FC, fp32
+master weights) -- the MFMA-utilisation stress line, not the headline.
 """
 from __future__ import annotations
 
@@ -30,11 +34,14 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense (MI355X_MICROARCH.md; the 5 PF figure is 2:1 sparse)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=("c2", "c5"), default="c2",
+                    help="c2 = headline fp32 hid 1024 depth 3; c5 = bf16 hid 2048 depth 6")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--m", type=int, default=100_000)
@@ -48,7 +55,11 @@ def parse():
     ap.add_argument("--print-workload", action="store_true", help="print the N=1 workload string and exit")
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned RCCL path even at N=1 (the N>1 code path)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    args.bf16 = args.config == "c5"
+    if args.bf16:
+        args.hids, args.depth = 2048, 6
+    return args
 
 
 def spmm_bytes(n_rows: int, nnz: int, F: int, s: int = 4) -> int:
@@ -100,8 +111,9 @@ def cpu_baseline(g, hids, depth, steps):
 
 
 def workload_name(args) -> str:
-    return (f"c2: synthetic LP {args.m}x{args.n} nnz={args.nnz}, GCN_FC(8,8,hids={args.hids},depth={args.depth}) "
-            f"fwd+bwd+Adam")
+    dt = ", bf16" if args.bf16 else ""
+    return (f"{args.config}: synthetic LP {args.m}x{args.n} nnz={args.nnz}, "
+            f"GCN_FC(8,8,hids={args.hids},depth={args.depth}{dt}) fwd+bwd+Adam")
 
 
 def main():
@@ -136,7 +148,8 @@ def main():
                                y_s=torch.from_numpy(g.y_s).to(dev), y_t=torch.from_numpy(g.y_t).to(dev),
                                edge_index=adj, s_bs=g.m, t_bs=g.n)
         torch.manual_seed(0)
-        model = GCN_FC(8, 8, hids=args.hids, depth=args.depth).to(dev)
+        model = GCN_FC(8, 8, hids=args.hids, depth=args.depth,
+                       compute_dtype=torch.bfloat16 if args.bf16 else torch.float32).to(dev)
         opt, _ = make_optimizer(model)
         step = lambda: train_step(model, batch, opt)
         local_nnz = g.nnz
@@ -174,7 +187,14 @@ def main():
     launches = sum(kern[k][0] for k in hid_keys)
     spmm_ms = sum(kern[k][1] for k in hid_keys)
     nnz_of = lambda k: local_nnz  # every launch traverses the local graph's edges once
-    bytes_total = sum(kern[k][0] * spmm_bytes(k[1], nnz_of(k), k[3]) for k in hid_keys)
+    esz = 2 if args.bf16 else 4
+    bytes_total = sum(kern[k][0] * spmm_bytes(k[1], nnz_of(k), k[3], esz) for k in hid_keys)
+    # dense FC launches of hidden width (K = 2 * hid): MFMA utilisation
+    fc_keys = [k for k in kern if k[0] == "fc" and k[3] >= 2 * args.hids]
+    fc_flops = sum(kern[k][0] * 2.0 * k[1] * k[2] * k[3] for k in fc_keys)
+    fc_ms = sum(kern[k][1] for k in fc_keys)
+    fc_peak = BF16_MFMA_PEAK_TFLOPS if args.bf16 else FP32_MFMA_PEAK_TFLOPS
+    fc_tf = fc_flops / (fc_ms / 1e3) / 1e12 if fc_ms > 0 else 0.0
     edges_local = launches * local_nnz / args.steps  # per step
     t = torch.tensor([dt], device=dev)
     e = torch.tensor([edges_local], device=dev, dtype=torch.float64)
@@ -200,23 +220,27 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "bf16" if args.bf16 else "fp32",
         "data": "synthetic (seeded uniform LP graph, LP feature layout; random-init GCN_FC weights)",
         "config": {"workload": workload, "n_cons": args.m * world, "n_vars": args.n * world,
                    "nnz": args.nnz * world, "hid": args.hids, "depth": args.depth, "parallelism": parallelism},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "lpg spmm_f32_rowwave (F=hid, both directions, fwd+bwd)",
+                     "kernel": ("lpg spmm_bf16_rowwave" if args.bf16 else "lpg spmm_f32_rowwave")
+                               + " (F=hid, both directions, fwd+bwd)",
                      "bytes_per_launch": per_launch_bytes,
                      "avg_launch_ms": spmm_ms / max(launches, 1), "launches": launches,
                      "traffic_source": traffic_src},
+        "fc_roofline": {"bound": "mfma", "achieved": fc_tf, "peak": fc_peak, "unit": "TFLOP/s",
+                        "frac": fc_tf / fc_peak, "launches": sum(kern[k][0] for k in fc_keys),
+                        "kernel": "lpg fc_fwd_" + ("bf16" if args.bf16 else "f32") + " (hidden GraphConv FC, fwd)"},
         "spmm_edges_per_s_kernel": launches * local_nnz / (spmm_ms / 1e3) if spmm_ms > 0 else None,
         "spmm_ms_per_step": spmm_ms / args.steps,
         "kernels": {f"{k[0]}[{k[1]}x{k[2]},F={k[3]},{k[4]}]": {"launches": v[0], "ms": v[1]}
                     for k, v in sorted(kern.items())},
         "library": lpgnn.library_path(),
     }
-    if rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None:
+    if rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None and not args.bf16:
         cdt, threads = cpu_baseline(g, args.hids, args.depth, args.cpu_steps)
         out["cpu_baseline"] = {"value": edges_local / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
                                "sample": f"{args.cpu_steps} full fwd+bwd+Adam step(s) of the same c2 workload: "

@@ -151,6 +151,16 @@ lpg_status lpg_wgrad_smallk_f32(int64_t M, int64_t N, const float *dz, int64_t l
                                 int64_t K1, const float *A1, int64_t lda1, int64_t K2, const float *A2, int64_t lda2,
                                 float *dW1, float *dW2, void *workspace, void *stream);
 
+/* bf16 variant (c5 configuration, BASELINE.json configs[4]): A1/A2/W1/W2
+ * bf16 bit patterns (uint16), K1 and K2 multiples of 64 (zero-pad), leading
+ * dims multiples of 8 and 16-byte aligned; fp32 accumulation on
+ * v_mfma_f32_16x16x32_bf16, fp32 bias, same epilogue (ReLU, fused dropout
+ * with the same mask function), C stored as bf16 (round to nearest even). */
+lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1, const uint16_t *W1,
+                       int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
+                       const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                       void *stream);
+
 /* Backward of a Linear with 1 <= N <= 4 outputs (the heads lin_left /
  * lin_right, arch.py:175-176, 190; torch Linear backward):
  *   dH = G W (skipped if dH == NULL), dW = G^T H, db = sum_m G[m, :].

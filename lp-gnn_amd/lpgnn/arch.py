@@ -135,8 +135,16 @@ class GCNBase(nn.Module):
 class GCN_FC(GCNBase):
     """arch.py:167-193."""
 
-    def __init__(self, p, q, hids=128, depth=3, dp=.1, *args, **kwargs):
+    def __init__(self, p, q, hids=128, depth=3, dp=.1, *args, compute_dtype=torch.float32, **kwargs):
         super().__init__()
+        # bf16 = the c5 configuration (BASELINE.json configs[4]): activations,
+        # SpMM storage and FC operands in bf16 (fp32 accumulation, fp32 master
+        # weights); logits return to fp32 before add_knowledge.
+        if compute_dtype in ("bf16", "bfloat16"):
+            compute_dtype = torch.bfloat16
+        if compute_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"compute_dtype must be float32 or bfloat16, got {compute_dtype}")
+        self.compute_dtype = compute_dtype
         self.conv1 = GraphConvTwoDirection(p, q, hids)
         self.layers = nn.ModuleList()
         for _ in range(depth - 2):
@@ -147,8 +155,9 @@ class GCN_FC(GCNBase):
 
     def forward(self, batch):
         x_left, x_right, edge_index = batch.x_s, batch.x_t, batch.edge_index
+        cd = self.compute_dtype
         # conv -> ReLU (arch.py:181-182): the ReLU is the FC kernel's epilogue.
-        left, right = self.conv1(x_left, x_right, edge_index, relu=True)
+        left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True)
         dp = self.dp if self.training else 0.0
         for conv in self.layers:
             # conv -> dropout -> ReLU (arch.py:185-188).  ReLU commutes with
@@ -158,7 +167,7 @@ class GCN_FC(GCNBase):
             left, right = conv(left, right, edge_index, relu=True, dropout=dp)
         left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias)
         right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias)
-        return add_knowledge(left, right, x_left, x_right)
+        return add_knowledge(left.float(), right.float(), x_left, x_right)
 
 
 _ARCH_RE = re.compile(r"^\s*([A-Za-z_]\w*)\s*\((.*)\)\s*$", re.S)

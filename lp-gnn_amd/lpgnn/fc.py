@@ -72,6 +72,44 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
     return C
 
 
+_BF16_BK = 64  # lpg_fc_bf16's k-tile: K1, K2 are zero-padded to a multiple of it
+
+
+def _prep_bf16(t: Tensor | None) -> Tensor | None:
+    if t is None:
+        return None
+    if t.dtype != torch.bfloat16:
+        raise RuntimeError(f"lpgnn bf16 FC: bf16 operands expected, got {t.dtype}")
+    if t.shape[1] % _BF16_BK:
+        t = F.pad(t, (0, _BF16_BK - t.shape[1] % _BF16_BK))
+    if t.stride(-1) != 1 or t.stride(0) % 8 or t.data_ptr() % 16:
+        t = t.contiguous()
+    return t
+
+
+def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
+                    relu: bool, dropout_p: float = 0.0, seed: int = 0) -> Tensor:
+    """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16)."""
+    if A1.device.type != "cuda":
+        raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
+    M, N = A1.shape[0], W1.shape[0]
+    A1, W1, A2, W2 = _prep_bf16(A1), _prep_bf16(W1), _prep_bf16(A2), _prep_bf16(W2)
+    bias = None if bias is None else bias.float().contiguous()
+    C = torch.empty((M, N), dtype=torch.bfloat16, device=A1.device)
+    K2 = 0 if A2 is None else A2.shape[1]
+    L = _lib.lib()
+    with torch.cuda.device(A1.device):
+        tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu-bf16" if relu else "lin-bf16"))
+        st = L.lpg_fc_bf16(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
+                           K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
+                           None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
+                           None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), 1 if relu else 0,
+                           float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_fc_bf16")
+    return C
+
+
 def relu_dropout_bwd(g: Tensor, y: Tensor, scale: float) -> Tensor:
     """(y > 0) ? g * scale : 0 in one pass (ReLU + dropout backward)."""
     g = g.contiguous()
@@ -137,7 +175,14 @@ class _FC(torch.autograd.Function):
     def forward(ctx, A1, A2, W1, W2, b, relu, dropout_p):
         if dropout_p > 0 and not relu:
             raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
-        C = fc_forward(A1, W1, A2, W2, b, relu, dropout_p, _new_seed() if dropout_p > 0 else 0)
+        seed = _new_seed() if dropout_p > 0 else 0
+        ctx.bf16 = A1.dtype == torch.bfloat16
+        if ctx.bf16:  # c5 path: bf16 activations, fp32 master weights cast per call
+            W1 = W1.to(torch.bfloat16)
+            W2 = None if W2 is None else W2.to(torch.bfloat16)
+            C = fc_forward_bf16(A1, W1, A2, W2, b, relu, dropout_p, seed)
+        else:
+            C = fc_forward(A1, W1, A2, W2, b, relu, dropout_p, seed)
         ctx.relu, ctx.has_a2, ctx.has_b = relu, A2 is not None, b is not None
         ctx.scale = 1.0 / (1.0 - dropout_p) if dropout_p > 0 else 1.0
         ctx.save_for_backward(A1, A2 if A2 is not None else A1, W1, W2 if W2 is not None else W1,
@@ -149,6 +194,15 @@ class _FC(torch.autograd.Function):
         A1, A2, W1, W2, C = ctx.saved_tensors
         need = ctx.needs_input_grad
         want_db = ctx.has_b and need[4]
+        if ctx.bf16:  # bf16 grads through hipBLASLt; weight/bias grads returned in fp32
+            g = torch.where(C > 0, gC * ctx.scale, torch.zeros((), dtype=gC.dtype, device=gC.device)) \
+                if ctx.relu else gC
+            db = g.float().sum(0) if want_db else None
+            dA1 = g @ W1 if need[0] else None
+            dA2 = g @ W2 if ctx.has_a2 and need[1] else None
+            dW1 = (g.t() @ A1).float() if need[2] else None
+            dW2 = (g.t() @ A2).float() if ctx.has_a2 and need[3] else None
+            return dA1, dA2, dW1, dW2, db, None, None
         if ctx.relu:
             g, db = relu_bwd_colsum(gC, C, ctx.scale, want_db)  # ReLU + dropout bwd, bias grad fused
         else:
@@ -195,14 +249,25 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, b):
-        ctx.save_for_backward(x, W)
         ctx.has_b = b is not None
+        ctx.bf16 = x.dtype == torch.bfloat16
+        if ctx.bf16:
+            W = W.to(torch.bfloat16)
+            ctx.save_for_backward(x, W)
+            return fc_forward_bf16(x, W, None, None, b, False)
+        ctx.save_for_backward(x, W)
         return fc_forward(x, W, None, None, b, False)
 
     @staticmethod
     def backward(ctx, g):
         x, W = ctx.saved_tensors
         need = ctx.needs_input_grad
+        if ctx.bf16:
+            g = g.to(torch.bfloat16)
+            dx = g @ W if need[0] else None
+            dW = (g.t() @ x).float() if need[1] else None
+            db = g.float().sum(0) if ctx.has_b and need[2] else None
+            return dx, dW, db
         if W.shape[0] <= 4 and x.shape[1] % 4 == 0:
             dx, dW, db = linear_small_bwd(g, W, x, need[0])
             return dx, dW if need[1] else None, db if (ctx.has_b and need[2]) else None

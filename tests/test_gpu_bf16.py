@@ -1,0 +1,105 @@
+"""bf16 path (c5, BASELINE.json configs[4]): lpg_fc_bf16 against an fp32
+GEMM of the same bf16-rounded operands, and the bf16 GCN_FC against the
+fp32 model.  No bitwise contract: bf16 outputs are compared within one
+bf16 rounding of the fp32-accumulated reference (rtol 2^-7)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+BF = torch.bfloat16
+
+
+def _ref(A1, W1, A2, W2, b, relu):
+    r = A1.float() @ W1.float().t()
+    if A2 is not None:
+        r = r + A2.float() @ W2.float().t()
+    if b is not None:
+        r = r + b
+    return torch.relu(r) if relu else r
+
+
+@pytest.mark.parametrize("M,N,K1,K2,relu,bias", [
+    (1, 1, 64, 0, False, True),
+    (300, 1024, 64, 64, True, True),
+    (129, 130, 128, 0, False, False),     # ragged tiles
+    (37, 3, 2048, 0, False, True),        # heads
+    (200, 256, 8, 8, True, True),         # conv1: K padded to 64
+    (1000, 2048, 2048, 2048, True, True), # c5 hidden layer shape
+    (4099, 512, 192, 320, True, True),
+])
+def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
+    from lpgnn.fc import fc_forward_bf16
+
+    g = torch.Generator().manual_seed(M * 31 + N)
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(BF).to(DEV)
+    A1, W1 = mk(M, K1), mk(N, K1, sc=0.05)
+    A2, W2 = (mk(M, K2), mk(N, K2, sc=0.05)) if K2 else (None, None)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV) if bias else None
+    got = fc_forward_bf16(A1, W1, A2, W2, b, relu).float()
+    ref = _ref(A1, W1, A2, W2, b, relu)
+    torch.testing.assert_close(got, ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
+
+
+def test_fc_bf16_asymmetric_identity():
+    """A = I with an asymmetric W catches a transposed C/D or operand map."""
+    from lpgnn.fc import fc_forward_bf16
+
+    K = 128
+    A = torch.eye(K, dtype=BF, device=DEV)
+    W = (torch.arange(96 * K, dtype=torch.float32).view(96, K) % 61 - 30).to(BF).to(DEV)
+    got = fc_forward_bf16(A, W, None, None, None, False)
+    assert torch.equal(got, W.t().contiguous())
+
+
+def test_fc_bf16_dropout_same_mask_as_fp32():
+    """The bf16 and fp32 kernels share the mask function: identical kept sets."""
+    from lpgnn.fc import fc_forward, fc_forward_bf16
+
+    torch.manual_seed(0)
+    M, N, K = 3000, 256, 64
+    A = torch.rand(M, K, device=DEV).to(BF)
+    W = torch.rand(N, K, device=DEV).to(BF)  # all outputs > 0 before dropout
+    p = 0.25
+    y16 = fc_forward_bf16(A, W, None, None, None, True, p, seed=4321)
+    y32 = fc_forward(A.float(), W.float(), None, None, None, True, p, seed=4321)
+    assert torch.equal(y16 > 0, y32 > 0)
+    rate = 1.0 - (y16 > 0).float().mean().item()
+    assert abs(rate - p) < 0.01
+
+
+def test_gcn_fc_bf16_close_to_fp32_and_trains():
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.train import balanced
+
+    g = synth.uniform_lp(3000, 5000, 30000, seed=2)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                           y_s=torch.from_numpy(g.y_s).to(DEV), y_t=torch.from_numpy(g.y_t).to(DEV),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    torch.manual_seed(0)
+    m32 = GCN_FC(8, 8, hids=256, depth=4).to(DEV).eval()
+    m16 = GCN_FC(8, 8, hids=256, depth=4, compute_dtype="bf16").to(DEV).eval()
+    m16.load_state_dict(m32.state_dict())
+    with torch.no_grad():
+        l32, r32 = m32(batch)
+        l16, r16 = m16(batch)
+    assert l16.dtype == torch.float32 and torch.isfinite(l16).all() and torch.isfinite(r16).all()
+    # knowledge-normalised logits live in [-20, 10]; bf16 activations move them by ~1e-2 typically
+    # (more where a node's raw logit vector is near zero: normalize() amplifies it)
+    d = torch.cat([l16 - l32, r16 - r32]).abs().flatten()
+    assert d.mean().item() < 0.05 and torch.quantile(d, 0.99).item() < 0.25, (d.mean().item(), d.max().item())
+    agree = (torch.cat([l16, r16]).argmax(1) == torch.cat([l32, r32]).argmax(1)).float().mean().item()
+    assert agree > 0.97
+    # one training step: finite fp32 grads close in direction to the fp32 model's
+    m16.train(), m32.train()
+    m16.dp = m32.dp = 0.0
+    for m in (m16, m32):
+        m.zero_grad()
+        lc, lv = m(batch)
+        balanced(lc, lv, batch.y_s, batch.y_t).backward()
+    for (k, p16), (_, p32) in zip(m16.named_parameters(), m32.named_parameters()):
+        assert p16.grad is not None and p16.grad.dtype == torch.float32 and torch.isfinite(p16.grad).all(), k
+        cos = torch.nn.functional.cosine_similarity(p16.grad.flatten(), p32.grad.flatten(), dim=0).item()
+        assert cos > 0.95, (k, cos)
