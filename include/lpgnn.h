@@ -160,6 +160,11 @@ lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int
                        int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
                        const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
                        void *stream);
+/* Tile choice for lpg_fc_bf16 (tuning/benchmarks): 0 = default (128 x 128 below
+ * 4096 rows, else 256 x 256 BK 64), 1 = 128 x 128, 2 = 256 x 256 with
+ * BK 64 and 2 buffers, 3 = 256 x 256 with BK 32 and 3 buffers.  All give
+ * identical bits. */
+lpg_status lpg_fc_bf16_set_variant(int32_t v);
 
 /* Backward of a Linear with 1 <= N <= 4 outputs (the heads lin_left /
  * lin_right, arch.py:175-176, 190; torch Linear backward):

@@ -31,6 +31,7 @@ HEADER_SYMBOLS = (
     "lpg_fc_f32",
     "lpg_fc_set_variant",
     "lpg_fc_bf16",
+    "lpg_fc_bf16_set_variant",
     "lpg_relu_dropout_bwd_f32",
     "lpg_relu_bwd_colsum_workspace_bytes",
     "lpg_relu_bwd_colsum_f32",
@@ -89,6 +90,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_f32.restype = c_i32
     L.lpg_fc_bf16.argtypes = L.lpg_fc_f32.argtypes
     L.lpg_fc_bf16.restype = c_i32
+    L.lpg_fc_bf16_set_variant.argtypes = [c_i32]
+    L.lpg_fc_bf16_set_variant.restype = c_i32
     L.lpg_relu_dropout_bwd_f32.argtypes = [c_i64, c_p, c_p, ctypes.c_float, c_p, c_p]
     L.lpg_relu_dropout_bwd_f32.restype = c_i32
     L.lpg_relu_bwd_colsum_workspace_bytes.argtypes = [c_i64, c_i64]

@@ -27,7 +27,8 @@ def _ref(A1, W1, A2, W2, b, relu):
     (37, 3, 2048, 0, False, True),        # heads
     (200, 256, 8, 8, True, True),         # conv1: K padded to 64
     (1000, 2048, 2048, 2048, True, True), # c5 hidden layer shape
-    (4099, 512, 192, 320, True, True),
+    (4099, 512, 192, 320, True, True),    # 256 x 256 tiles from here (M >= 4096)
+    (9000, 1000, 1024, 64, False, True),
 ])
 def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
     from lpgnn.fc import fc_forward_bf16
@@ -40,6 +41,27 @@ def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
     got = fc_forward_bf16(A1, W1, A2, W2, b, relu).float()
     ref = _ref(A1, W1, A2, W2, b, relu)
     torch.testing.assert_close(got, ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
+
+
+def test_fc_bf16_tile_variants_identical():
+    """Both tilings run the same per-output MFMA chain order: identical bits."""
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward_bf16
+
+    torch.manual_seed(1)
+    A1, A2 = (torch.randn(5000, 256, device=DEV).to(BF) for _ in range(2))
+    W1, W2 = ((torch.randn(384, 256, device=DEV) * 0.05).to(BF) for _ in range(2))
+    b = torch.randn(384, device=DEV)
+    L = _lib.lib()
+    outs = []
+    try:
+        for v in (1, 2, 3):
+            L.lpg_fc_bf16_set_variant(v)
+            outs.append(fc_forward_bf16(A1, W1, A2, W2, b, True, 0.2, seed=9))
+    finally:
+        L.lpg_fc_bf16_set_variant(0)
+    for o in outs:
+        assert torch.equal(o, outs[0])
 
 
 def test_fc_bf16_asymmetric_identity():

@@ -3,6 +3,8 @@
   python tools/kbench.py [fc] [spmm] [bwd]
 
 fc   : lpg_fc_f32 at the c2 shapes vs torch (hipBLASLt) linear+linear+add+relu
+fcpmc: only the two hidden-layer FC kernels (fp32 c2 and bf16 c5 shapes), for PMC passes
+bf16 : lpg_fc_bf16 at the c5 shape vs torch bf16 (hipBLASLt)
 spmm : lpg_spmm_f32 at c2, both directions, slice widths 256/512/1024
 bwd  : the FC backward GEMMs at c2 shapes through torch (hipBLASLt)
 """
@@ -114,11 +116,56 @@ def bench_spmm(out):
             out[f"spmm {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000)
 
 
+def bench_fcpmc(out):
+    from lpgnn.fc import fc_forward, fc_forward_bf16
+
+    M = 200_000
+    A1, A2 = torch.randn(M, 1024, device="cuda"), torch.randn(M, 1024, device="cuda")
+    W1, W2 = torch.randn(1024, 1024, device="cuda") * 0.03, torch.randn(1024, 1024, device="cuda") * 0.03
+    b = torch.randn(1024, device="cuda")
+    t = timeit({"f32": lambda: fc_forward(A1, W1, A2, W2, b, True)}, rounds=3, iters=3)
+    out["fcpmc f32 M=200000 K=2048"] = dict(ms=t["f32"], tflops=2.0 * M * 1024 * 2048 / t["f32"] / 1e9)
+    del A1, A2
+    B1, B2 = (torch.randn(M, 2048, device="cuda").to(torch.bfloat16) for _ in range(2))
+    V1, V2 = ((torch.randn(2048, 2048, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(2))
+    b2 = torch.randn(2048, device="cuda")
+    t = timeit({"bf16": lambda: fc_forward_bf16(B1, V1, B2, V2, b2, True)}, rounds=3, iters=3)
+    out["fcpmc bf16 M=200000 K=4096"] = dict(ms=t["bf16"], tflops=2.0 * M * 2048 * 4096 / t["bf16"] / 1e9)
+
+
+def bench_bf16(out):
+    from lpgnn.fc import fc_forward_bf16
+
+    M = 200_000
+    B1, B2 = (torch.randn(M, 2048, device="cuda").to(torch.bfloat16) for _ in range(2))
+    V1, V2 = ((torch.randn(2048, 2048, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(2))
+    b2 = torch.randn(2048, device="cuda")
+    Bc = torch.cat([B1, B2], 1)
+    Vc = torch.cat([V1, V2], 1)
+    from lpgnn import _lib
+    L = _lib.lib()
+
+    def var(v):
+        def f():
+            L.lpg_fc_bf16_set_variant(v)
+            return fc_forward_bf16(B1, V1, B2, V2, b2, True)
+        return f
+    y0 = var(0)()
+    for v in (1, 2, 3):
+        assert torch.equal(var(v)(), y0), f"bf16 variant {v} differs"
+    t = timeit({"lpg_fc_bf16 v0 (default)": var(0), "lpg_fc_bf16 v1 128x128": var(1),
+                "lpg_fc_bf16 v2 256x256 2buf": var(2), "lpg_fc_bf16 v3 256x256 3buf": var(3),
+                "torch_bf16_1gemm_relu": lambda: torch.relu(F.linear(Bc, Vc, b2.to(torch.bfloat16)))})
+    L.lpg_fc_bf16_set_variant(0)
+    for k, v in t.items():
+        out[f"bf16 M={M} K=4096 {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * 4096 / v / 1e9)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["fc", "spmm", "bwd"]
     out = {}
     for w in which:
-        {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd}[w](out)
+        {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
