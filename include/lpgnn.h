@@ -179,7 +179,10 @@ lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float
 
 /* Tuning knob for lpg_fc_f32 (process-global, default 0): output tile
  * variant, 0 = 128x128 (4 waves, 2 blocks/CU), 1 = 256x128 (8 waves),
- * 2 = 128x256 (8 waves), 3 = 128x128 with 64-deep k staging.  Every variant
+ * 2 = 128x256 (8 waves), 3 = 128x128 with 64-deep k staging, 4-6 = the
+ * 16x16x4 MFMA with b128 operand reads (128x128, 128x256, 256x128),
+ * 7 = 128x128 staged by LDS-DMA (global_load_lds; K1, K2 multiples of 32,
+ * else variant 0), 8 = the same at 128x256 with 8 waves.  Every variant
  * produces bitwise identical results (same numerics blocks). */
 lpg_status lpg_fc_set_variant(int32_t variant);
 

@@ -513,6 +513,148 @@ bool try_smallk(const FcArgs &a, bool relu, hipStream_t s, lpg_status *st) {
   return false;
 }
 
+// Same contract staged by global_load_lds (LDS-DMA, no register round trip,
+// no ds_write pass): K1, K2 multiples of BK = 32.  LDS image: unpadded
+// 128-B rows (32 fp32 of k), 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)
+// -- applied on the DMA source address (the DMA destination is lane-linear)
+// and on the operand reads.  A wave-instruction moves 8 rows (1 KiB); two
+// buffers, one barrier per k-tile, the next tile's DMA in flight under the
+// current tile's MFMAs.  Operand reads are ds_read_b32 with a 2-way bank
+// conflict (rows r and r+16), one per MFMA.
+__device__ __forceinline__ int swz8(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int WAVES_M, int WAVES_N, int TM, int TN, bool RELU>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_glds(FcArgs a) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int BM = WAVES_M * TM * 32, BN = WAVES_N * TN * 32, BK = 32;
+  constexpr int TILE_BYTES = (BM + BN) * BK * 4;
+  constexpr int PA = BM / 8 / NW, PB = BN / 8 / NW;
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split into whole pieces per wave");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
+
+  const int64_t nwg = a.mt * a.nt;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  const int64_t m0 = (wgid / a.nt) * BM;
+  const int64_t n0 = (wgid % a.nt) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int nk1 = (int)(a.K1 / BK);
+  const int nk = nk1 + (int)(a.K2 / BK);
+
+  // per-lane source rows, clamped once (rows past M / N feed outputs never stored)
+  const float *srcA1[PA], *srcA2[PA], *srcW1[PB], *srcW2[PB];
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int row = (wave + NW * p) * 8 + (lane >> 3);
+    int64_t gr = m0 + row;
+    gr = gr < a.M ? gr : a.M - 1;
+    const int off = swz8(row, lane & 7) * 4;
+    srcA1[p] = a.A1 + gr * a.lda1 + off;
+    srcA2[p] = a.A2 + gr * a.lda2 + off;
+  }
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    const int row = (wave + NW * p) * 8 + (lane >> 3);
+    int64_t gn = n0 + row;
+    gn = gn < a.N ? gn : a.N - 1;
+    const int off = swz8(row, lane & 7) * 4;
+    srcW1[p] = a.W1 + gn * a.ldw1 + off;
+    srcW2[p] = a.W2 + gn * a.ldw2 + off;
+  }
+  auto stage = [&](int b, int t) {
+    typedef __attribute__((address_space(3))) unsigned char lds_t;
+    unsigned char *base = smem + b * TILE_BYTES;
+    const bool p2 = t >= nk1;
+    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
+#pragma unroll
+    for (int p = 0; p < PA; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcA2[p] : srcA1[p]) + k0),
+                                       (lds_t *)(base + (wave + NW * p) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcW2[p] : srcW1[p]) + k0),
+                                       (lds_t *)(base + BM * BK * 4 + (wave + NW * p) * 1024), 16, 0, 0);
+  };
+
+  f32x16 acc[TM][TN];
+  const f32x16 zero = {};
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero;
+
+  const int fr = lane & 31, fk = lane >> 5;
+  if (nk > 0) stage(0, 0);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1;
+    if (t + 1 < nk) stage(b ^ 1, t + 1);
+    const unsigned char *As = smem + b * TILE_BYTES;
+    const unsigned char *Bs = As + BM * BK * 4;
+    f32x16 part[TM][TN];
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      const int k = 2 * s + fk;
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * TM * 32 + i * 32 + fr;
+        av[i] = *reinterpret_cast<const float *>(As + row * 128 + swz8(row, k >> 2) * 16 + (k & 3) * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * TN * 32 + j * 32 + fr;
+        bv[j] = *reinterpret_cast<const float *>(Bs + row * 128 + swz8(row, k >> 2) * 16 + (k & 3) * 4);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], s == 0 ? zero : part[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
+    __syncthreads();  // DMA of tile t+1 landed (vmcnt(0)); every wave done reading tile t
+  }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+    if (col >= a.N) continue;
+    const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int64_t rbase = m0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row < a.M) a.C[row * a.ldc + col] = epilogue(a, acc[i][j][r], b, row, col, RELU);
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN>
+lpg_status launch_fc_glds(const FcArgs &a0, bool relu, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
+  FcArgs a = a0;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int64_t nwg = a.mt * a.nt;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_f32: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_fwd_f32_glds<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_fwd_f32_glds<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
 int g_fc_variant = 0;  // lpg_fc_set_variant; 0 = default tile
 
 }  // namespace
@@ -553,6 +695,12 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
     case 4: return launch_fc16<2, 2, 4, 4>(a, relu, s);    // 16x16x4 MFMA, 128 x 128
     case 5: return launch_fc16<2, 2, 4, 8>(a, relu, s);    // 16x16x4 MFMA, 128 x 256
     case 6: return launch_fc16<4, 2, 4, 4>(a, relu, s);    // 16x16x4 MFMA, 256 x 128, 8 waves
+    case 7:
+      if (K1 % 32 == 0 && K2 % 32 == 0) return launch_fc_glds<2, 2, 2, 2>(a, relu, s);  // LDS-DMA staging
+      return launch_fc<2, 2, 2, 2, 32>(a, relu, s);
+    case 8:
+      if (K1 % 32 == 0 && K2 % 32 == 0) return launch_fc_glds<2, 4, 2, 2>(a, relu, s);  // 128 x 256, 8 waves
+      return launch_fc<2, 2, 2, 2, 32>(a, relu, s);
     default: return launch_fc<2, 2, 2, 2, 32>(a, relu, s); // 128 x 128, BK 32, 2 blocks / CU
   }
 }
@@ -575,7 +723,7 @@ extern "C" lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const 
 }
 
 extern "C" lpg_status lpg_fc_set_variant(int32_t v) {
-  LPG_REQUIRE(v >= 0 && v <= 6, "lpg_fc_set_variant: variant %d not in [0, 6]", v);
+  LPG_REQUIRE(v >= 0 && v <= 8, "lpg_fc_set_variant: variant %d not in [0, 8]", v);
   g_fc_variant = v;
   return LPG_OK;
 }

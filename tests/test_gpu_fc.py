@@ -145,25 +145,25 @@ def test_knowledge_backward_matches_torch():
     torch.testing.assert_close(got, x.grad, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("variant", range(7))
+@pytest.mark.parametrize("variant", range(9))
 def test_fc_tile_variants_bitwise(variant):
     """Every lpg_fc_set_variant tile/MFMA shape gives the same bits as the oracle."""
     from lpgnn import _lib
     from lpgnn.fc import fc_forward
 
     rng = np.random.default_rng(variant)
-    M, N, K1, K2 = 777, 300, 96, 40
-    A1, A2 = rng.standard_normal((M, K1)).astype(np.float32), rng.standard_normal((M, K2)).astype(np.float32)
-    W1, W2 = rng.standard_normal((N, K1)).astype(np.float32), rng.standard_normal((N, K2)).astype(np.float32)
-    b = rng.standard_normal(N).astype(np.float32)
     L = _lib.lib()
     t = lambda x: torch.from_numpy(x).to(DEV)
-    try:
-        assert L.lpg_fc_set_variant(variant) == 0
-        got = fc_forward(t(A1), t(W1), t(A2), t(W2), t(b), True).cpu().numpy()
-    finally:
-        L.lpg_fc_set_variant(0)
-    assert np.array_equal(got, O.fc_kchain(A1, W1, A2, W2, b, relu=True))
+    for M, N, K1, K2 in ((777, 300, 96, 40), (777, 300, 96, 64), (1000, 1024, 256, 256)):
+        A1, A2 = rng.standard_normal((M, K1)).astype(np.float32), rng.standard_normal((M, K2)).astype(np.float32)
+        W1, W2 = rng.standard_normal((N, K1)).astype(np.float32), rng.standard_normal((N, K2)).astype(np.float32)
+        b = rng.standard_normal(N).astype(np.float32)
+        try:
+            assert L.lpg_fc_set_variant(variant) == 0
+            got = fc_forward(t(A1), t(W1), t(A2), t(W2), t(b), True).cpu().numpy()
+        finally:
+            L.lpg_fc_set_variant(0)
+        assert np.array_equal(got, O.fc_kchain(A1, W1, A2, W2, b, relu=True)), (M, N, K1, K2)
 
 
 def test_fused_dropout_epilogue_and_backward():

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests -> smoke -> bench -> rocprofv3 kernel stats.
 # Usage (from the repo root, via gpurun):  bash tools/gpu_session.sh [stages...]
-# stages: tests smoke bench prof pmc   (default: tests smoke bench prof)
+# stages: tests smoke bench prof pmc bench_c5 prof_c5 kbench kbfc   (default: tests smoke bench prof)
 # Every GPU step has its own time limit; the script stops at the first step
 # that crashes, aborts or times out (exit >= 2 or signal), and continues past
 # a plain test failure (exit 1) so the bench still runs.
@@ -39,6 +39,11 @@ for s in $STAGES; do
     prof)
       step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python "$ROOT/bench.py" --steps 5 --warmup 2 --profile-only
+      ;;
+    bench_c5) step bench_c5 900 python bench.py --config c5 --steps 10 --warmup 3 ;;
+    prof_c5)
+      step prof_c5 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run -- \
+        python "$ROOT/bench.py" --config c5 --steps 3 --warmup 2 --profile-only
       ;;
     kbench) step kbench 600 python tools/kbench.py ;;
     kbfc) step kbench_fc 600 python tools/kbench.py fc ;;

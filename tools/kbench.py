@@ -58,10 +58,10 @@ def bench_fc(out):
                 return fc_forward(A1, W1, A2, W2, b, True)
             return f
         y0 = var(0)()
-        for v in range(1, 7):
+        for v in range(1, 9):
             assert torch.equal(var(v)(), y0), f"variant {v} differs"
         t = timeit({
-            **{f"lpg_fc_f32 v{v}": var(v) for v in range(7)},
+            **{f"lpg_fc_f32 v{v}": var(v) for v in range(9)},
             "torch_2gemm_add_relu": lambda: torch.relu(F.linear(A1, W1, b) + F.linear(A2, W2)),
             "torch_1gemm_K2048": lambda: F.linear(torch.cat([A1, A2], 1) if False else A1, torch.cat([W1], 1), b),
         })
