@@ -142,6 +142,13 @@ lpg_status lpg_relu_bwd_colsum_f32(int64_t M, int64_t N, const float *g, int64_t
                                    int64_t ldy, float scale, float *out, int64_t ldo, float *db,
                                    void *workspace, void *stream);
 
+/* bf16 twin (c5 path): g, y, out bf16 (uint16), N and leading dims multiples
+ * of 8; dZ = bf16(g * scale) where y > 0; db (fp32) = column sums of dZ.
+ * Workspace: lpg_relu_bwd_colsum_workspace_bytes(M, N). */
+lpg_status lpg_relu_bwd_colsum_bf16(int64_t M, int64_t N, const uint16_t *g, int64_t ldg, const uint16_t *y,
+                                    int64_t ldy, float scale, uint16_t *out, int64_t ldo, float *db,
+                                    void *workspace, void *stream);
+
 /* Weight gradients of a GraphConv whose inputs are narrow (conv1: the 8 LP
  * features, arch.py:170): dW1 = dZ^T A1 [N, K1], dW2 = dZ^T A2 [N, K2], in the
  * torch weight layout, 1 <= K1 + K2 <= 16; dZ [M, N] read once; deterministic

@@ -73,6 +73,64 @@ __global__ __launch_bounds__(kT) void relu_bwd_colsum_p1(int64_t M, int64_t N, c
   }
 }
 
+// bf16 twin (c5 path): g, y, out bf16; db fp32.  8 columns per thread (16-B
+// loads), 2048 per pass; dZ = RNE(bf16)(g * scale) where y > 0, the value
+// torch's bf16 `g * scale` gives; db sums the rounded dZ in fp32.
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+
+__device__ __forceinline__ uint32_t f32_to_bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+__global__ __launch_bounds__(kT) void relu_bwd_colsum_bf16_p1(int64_t M, int64_t N, const uint16_t *__restrict__ g,
+                                                              int64_t ldg, const uint16_t *__restrict__ y,
+                                                              int64_t ldy, float scale, uint16_t *__restrict__ out,
+                                                              int64_t ldo, float *__restrict__ part) {
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsColsum;
+  const int64_t r1 = r0 + kRowsColsum < M ? r0 + kRowsColsum : M;
+  for (int64_t c = (int64_t)threadIdx.x * 8; c < N; c += kT * 8) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto row = [&](uint4 gv, uint4 yv, int64_t m) {
+      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
+      uint32_t ow[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float yf = bf16_to_f32((yw[h] >> (16 * e)) & 0xffffu);
+          const uint32_t d = yf > 0.f ? f32_to_bf16_rne(bf16_to_f32((gw[h] >> (16 * e)) & 0xffffu) * scale) : 0u;
+          s[2 * h + e] = s[2 * h + e] + bf16_to_f32(d);
+          o |= d << (16 * e);
+        }
+        ow[h] = o;
+      }
+      *reinterpret_cast<uint4 *>(out + m * ldo + c) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    };
+    int64_t m = r0;
+    for (; m + 4 <= r1; m += 4) {
+      uint4 gv[4], yv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        gv[u] = *reinterpret_cast<const uint4 *>(g + (m + u) * ldg + c);
+        yv[u] = *reinterpret_cast<const uint4 *>(y + (m + u) * ldy + c);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) row(gv[u], yv[u], m + u);
+    }
+    for (; m < r1; ++m)
+      row(*reinterpret_cast<const uint4 *>(g + m * ldg + c), *reinterpret_cast<const uint4 *>(y + m * ldy + c), m);
+    if (part) {
+      float *pp = part + (int64_t)blockIdx.x * N + c;
+      *reinterpret_cast<float4 *>(pp) = make_float4(s[0], s[1], s[2], s[3]);
+      *reinterpret_cast<float4 *>(pp + 4) = make_float4(s[4], s[5], s[6], s[7]);
+    }
+  }
+}
+
 // Fold stage: seg[s][i] = sum of part[b][i] over b in segment s of [0, nblk),
 // in b order (grid: n / kT x kFold).
 __global__ __launch_bounds__(kT) void fold_partials(int64_t nblk, int64_t n, const float *__restrict__ part,
@@ -294,6 +352,34 @@ extern "C" lpg_status lpg_relu_bwd_colsum_f32(int64_t M, int64_t N, const float 
   float *part = db ? static_cast<float *>(workspace) : nullptr;
   hipLaunchKernelGGL(relu_bwd_colsum_p1, dim3((unsigned)nblk), dim3(kT), 0, s, M, N, g, ldg, y, ldy, scale, out, ldo,
                      part);
+  LPG_HIP(hipGetLastError());
+  if (db) {
+    const float *img;
+    const int64_t nrow = fold(nblk, N, part, part + nblk * N, &img, s);
+    hipLaunchKernelGGL(sum_partials, dim3((unsigned)((N + kT - 1) / kT)), dim3(kT), 0, s, nrow, N, img, db);
+    LPG_HIP(hipGetLastError());
+  }
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_relu_bwd_colsum_bf16(int64_t M, int64_t N, const uint16_t *g, int64_t ldg, const uint16_t *y,
+                                               int64_t ldy, float scale, uint16_t *out, int64_t ldo, float *db,
+                                               void *workspace, void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0, "lpg_relu_bwd_colsum_bf16: negative size");
+  if (M == 0 || N == 0) {
+    if (db && N > 0) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, as_stream(stream)));
+    return LPG_OK;
+  }
+  LPG_REQUIRE(g && y && out, "lpg_relu_bwd_colsum_bf16: NULL pointer");
+  LPG_REQUIRE(N % 8 == 0 && ldg % 8 == 0 && ldy % 8 == 0 && ldo % 8 == 0 && aligned16(g) && aligned16(y) &&
+                  aligned16(out),
+              "lpg_relu_bwd_colsum_bf16: N / leading dims must be multiples of 8, buffers 16-byte aligned");
+  LPG_REQUIRE(db == nullptr || (workspace && aligned16(workspace)), "lpg_relu_bwd_colsum_bf16: db needs a workspace");
+  hipStream_t s = as_stream(stream);
+  const int64_t nblk = (M + kRowsColsum - 1) / kRowsColsum;
+  float *part = db ? static_cast<float *>(workspace) : nullptr;
+  hipLaunchKernelGGL(relu_bwd_colsum_bf16_p1, dim3((unsigned)nblk), dim3(kT), 0, s, M, N, g, ldg, y, ldy, scale, out,
+                     ldo, part);
   LPG_HIP(hipGetLastError());
   if (db) {
     const float *img;

@@ -147,6 +147,27 @@ def relu_bwd_colsum(g: Tensor, y: Tensor, scale: float, want_db: bool):
     return out, db
 
 
+def relu_bwd_colsum_bf16(g: Tensor, y: Tensor, scale: float, want_db: bool):
+    """bf16 twin of relu_bwd_colsum: (dZ bf16, db fp32) in one pass."""
+    M, N = g.shape
+    g = g.to(torch.bfloat16)
+    if g.stride(1) != 1 or g.stride(0) % 8 or g.data_ptr() % 16:
+        g = g.contiguous()
+    if N % 8 or y.stride(1) != 1 or y.stride(0) % 8 or y.data_ptr() % 16:
+        dz = torch.where(y > 0, g * scale, torch.zeros((), dtype=g.dtype, device=g.device))
+        return dz, (dz.float().sum(0) if want_db else None)
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=g.device)
+    L = _lib.lib()
+    db = torch.empty(N, dtype=torch.float32, device=g.device) if want_db else None
+    ws = _workspace(L.lpg_relu_bwd_colsum_workspace_bytes(M, N), g.device) if want_db else None
+    with torch.cuda.device(g.device):
+        st = L.lpg_relu_bwd_colsum_bf16(M, N, g.data_ptr(), g.stride(0), y.data_ptr(), y.stride(0), float(scale),
+                                        out.data_ptr(), N, None if db is None else db.data_ptr(),
+                                        None if ws is None else ws.data_ptr(), _lib.stream_of(g))
+    _lib.check(st, "lpg_relu_bwd_colsum_bf16")
+    return out, db
+
+
 def wgrad_smallk(dz: Tensor, A1: Tensor, A2: Tensor | None):
     """(dW1, dW2) = (dZ^T A1, dZ^T A2) for narrow inputs (K1 + K2 <= 16)."""
     M, N = dz.shape
@@ -195,9 +216,10 @@ class _FC(torch.autograd.Function):
         need = ctx.needs_input_grad
         want_db = ctx.has_b and need[4]
         if ctx.bf16:  # bf16 grads through hipBLASLt; weight/bias grads returned in fp32
-            g = torch.where(C > 0, gC * ctx.scale, torch.zeros((), dtype=gC.dtype, device=gC.device)) \
-                if ctx.relu else gC
-            db = g.float().sum(0) if want_db else None
+            if ctx.relu:
+                g, db = relu_bwd_colsum_bf16(gC, C, ctx.scale, want_db)
+            else:
+                g, db = gC, (gC.float().sum(0) if want_db else None)
             dA1 = g @ W1 if need[0] else None
             dA2 = g @ W2 if ctx.has_a2 and need[1] else None
             dW1 = (g.t() @ A1).float() if need[2] else None

@@ -125,3 +125,19 @@ def test_gcn_fc_bf16_close_to_fp32_and_trains():
         assert p16.grad is not None and p16.grad.dtype == torch.float32 and torch.isfinite(p16.grad).all(), k
         cos = torch.nn.functional.cosine_similarity(p16.grad.flatten(), p32.grad.flatten(), dim=0).item()
         assert cos > 0.95, (k, cos)
+
+
+@pytest.mark.parametrize("M,N", [(1, 8), (63, 16), (1000, 2048), (4099, 1032), (70000, 256)])
+def test_relu_bwd_colsum_bf16(M, N):
+    from lpgnn.fc import relu_bwd_colsum_bf16
+
+    torch.manual_seed(M + N)
+    g = torch.randn(M, N, device=DEV).to(BF)
+    y = torch.relu(torch.randn(M, N, device=DEV)).to(BF)
+    for scale in (1.0, 1.0 / 0.9):
+        out, db = relu_bwd_colsum_bf16(g, y, scale, True)
+        want = torch.where(y > 0, g * scale, torch.zeros((), dtype=BF, device=DEV))
+        assert out.dtype == BF and torch.equal(out, want)
+        ref = want.double().sum(0)
+        chain = 64 + (M + 63) // 64
+        assert bool(((db.double() - ref).abs() <= chain * 2.0 ** -24 * want.double().abs().sum(0) + 1e-30).all())
