@@ -587,6 +587,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_glds(FcArgs
     for (int j = 0; j < TN; ++j) acc[i][j] = zero;
 
   const int fr = lane & 31, fk = lane >> 5;
+  // Tile t-1's sums are folded into acc lazily, block by block, right before
+  // tile t's first MFMA overwrites that block's sum register: the fold then
+  // sits between MFMAs instead of stalling behind the tile's last one.  Same
+  // order as fc_fwd_f32 (acc += tile t-1, then tile t).
+  f32x16 part[TM][TN];
   if (nk > 0) stage(0, 0);
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
@@ -594,7 +599,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_glds(FcArgs
     if (t + 1 < nk) stage(b ^ 1, t + 1);
     const unsigned char *As = smem + b * TILE_BYTES;
     const unsigned char *Bs = As + BM * BK * 4;
-    f32x16 part[TM][TN];
 #pragma unroll
     for (int s = 0; s < BK / 2; ++s) {
       const int k = 2 * s + fk;
@@ -612,14 +616,22 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_glds(FcArgs
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], s == 0 ? zero : part[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) {
+          if (s == 0) {
+            if (t > 0) acc[i][j] = acc[i][j] + part[i][j];
+            part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], zero, 0, 0, 0);
+          } else {
+            part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], part[i][j], 0, 0, 0);
+          }
+        }
     }
+    __syncthreads();  // DMA of tile t+1 landed (vmcnt(0)); every wave done reading tile t
+  }
+  if (nk > 0) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
-    __syncthreads();  // DMA of tile t+1 landed (vmcnt(0)); every wave done reading tile t
   }
 
 #pragma unroll

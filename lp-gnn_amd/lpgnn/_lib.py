@@ -18,7 +18,7 @@ import os
 import torch  # noqa: F401  (see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblpgnn_hip.so")
+LIB_PATH = os.environ.get("LPGNN_LIB") or os.path.join(_HERE, "liblpgnn_hip.so")  # override: tools/ experiments
 HEADER_SYMBOLS = (
     "lpg_last_error",
     "lpg_build_info",

@@ -117,3 +117,27 @@ def test_minibatch_logits_equal_full_graph():
     torch.testing.assert_close(lv, lv_f, rtol=0, atol=1e-4)
     m = lc.shape[0]
     assert torch.equal(inference_gnn(torch.cat([lc, lv]), m), inference_gnn(torch.cat([lc_f, lv_f]), m))
+
+
+def test_epoch_batches_train_step_on_sampled_subgraphs():
+    """train.py:103-129 on a homogeneous graph: NeighborLoader(fanout 6,
+    shuffled, drop_last) batches -> GCN_FC step on each seed slice."""
+    from lpgnn import synth
+    from lpgnn.arch import GCN_FC
+    from lpgnn.data import lp_to_unipartite
+    from lpgnn.train import epoch_batches, make_optimizer, train_step
+
+    lp = synth.uniform_lp(500, 900, 5000, seed=7)
+    g = lp_to_unipartite(lp.row, lp.col, lp.val, lp.x_s, lp.x_t, lp.y_s, lp.y_t)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=32, depth=3).to(DEV)
+    opt, _ = make_optimizer(model, lr=1e-2)
+    batches = epoch_batches(g, "GCN_FC(8,8,hids=32,depth=3)", batch_size=300, dev=DEV, seed=0)
+    assert len(batches) == (500 + 900) // 300
+    seen = 0
+    for b in batches:
+        assert b.s_bs + b.t_bs == 300 and b.x_s.is_cuda
+        loss = train_step(model, b, opt)
+        assert torch.isfinite(loss)
+        seen += 1
+    assert seen == len(batches)
