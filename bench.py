@@ -110,6 +110,41 @@ def cpu_baseline(g, hids, depth, steps):
     return dt, threads
 
 
+def cpu_spmm(g, F, reps=3):
+    """SURVEY.md §8d's two CPU SpMM numbers at F = hid, per direction (median of
+    `reps`): (1) the oracle's C restatement of torch_sparse spmm_cpu (OpenMP,
+    the reference's loop order), (2) torch.sparse CSR mm (MKL)."""
+    from oracle import model_ref as O
+
+    rs = np.random.default_rng(5)
+    A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
+    AT = O.csr_transpose(*A, g.m, g.n)
+    X = {"cons<-vars": rs.standard_normal((g.n, F), dtype=np.float32),
+         "vars<-cons": rs.standard_normal((g.m, F), dtype=np.float32)}
+    mats = {"cons<-vars": A, "vars<-cons": AT}
+    out = {}
+    for d, (rp, col, val) in mats.items():
+        x = X[d]
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            O.spmm_f32(rp, col, val, x)
+            ts.append(time.perf_counter() - t0)
+        sp = torch.sparse_csr_tensor(torch.from_numpy(rp), torch.from_numpy(col.astype(np.int64)),
+                                     torch.from_numpy(val), size=(len(rp) - 1, x.shape[0]))
+        xt = torch.from_numpy(x)
+        tm = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            torch.sparse.mm(sp, xt)
+            tm.append(time.perf_counter() - t0)
+        nnz = len(col)
+        out[d] = {"oracle_c_ms": float(np.median(ts)) * 1e3, "oracle_c_edges_per_s": nnz / float(np.median(ts)),
+                  "torch_sparse_mm_ms": float(np.median(tm)) * 1e3,
+                  "torch_sparse_mm_edges_per_s": nnz / float(np.median(tm))}
+    return out
+
+
 def workload_name(args) -> str:
     dt = ", bf16" if args.bf16 else ""
     return (f"{args.config}: synthetic LP {args.m}x{args.n} nnz={args.nnz}, "
@@ -181,6 +216,7 @@ def main():
     dt = time.perf_counter() - t0
     TIMER.enabled = False
     kern = TIMER.summary()
+    per_launch = TIMER.launches()
 
     # hid-width SpMM launches (the metric's kernel) measured on their stream
     hid_keys = [k for k in kern if k[0] == "spmm" and k[3] == args.hids]
@@ -234,6 +270,14 @@ def main():
         "fc_roofline": {"bound": "mfma", "achieved": fc_tf, "peak": fc_peak, "unit": "TFLOP/s",
                         "frac": fc_tf / fc_peak, "launches": sum(kern[k][0] for k in fc_keys),
                         "kernel": "lpg fc_fwd_" + ("bf16" if args.bf16 else "f32") + " (hidden GraphConv FC, fwd)"},
+        "spmm_directions": {
+            ("cons<-vars" if (k[1], k[2]) == (args.m, args.n) and not distributed else
+             "vars<-cons" if (k[1], k[2]) == (args.n, args.m) and not distributed else f"{k[1]}x{k[2]}"):
+            {"median_ms": float(np.median(v)), "launches": len(v),
+             "edges_per_s": local_nnz / (float(np.median(v)) / 1e3),
+             "roofline_frac": spmm_bytes(k[1], local_nnz, k[3], esz) / (float(np.median(v)) / 1e3) / 1e9
+             / HBM_PEAK_GBS}
+            for k, v in per_launch.items() if k[0] == "spmm" and k[3] == args.hids},
         "spmm_edges_per_s_kernel": launches * local_nnz / (spmm_ms / 1e3) if spmm_ms > 0 else None,
         "spmm_ms_per_step": spmm_ms / args.steps,
         "kernels": {f"{k[0]}[{k[1]}x{k[2]},F={k[3]},{k[4]}]": {"launches": v[0], "ms": v[1]}
@@ -247,6 +291,8 @@ def main():
                                          f"oracle C spmm_cpu loop (OpenMP) + torch CPU GEMMs, "
                                          f"{cdt:.2f} s/step",
                                "s_per_step": cdt}
+        out["cpu_spmm"] = dict(cpu_spmm(g, args.hids), threads=threads,
+                               note="F=hid SpMM alone on the host, median of 3 (SURVEY.md 8d CPU numbers)")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

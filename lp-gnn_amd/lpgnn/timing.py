@@ -44,4 +44,13 @@ class KernelTimer:
         return {k: tuple(v) for k, v in out.items()}
 
 
+    def launches(self):
+        """{key: [ms of each launch]} -- synchronises."""
+        torch.cuda.synchronize()
+        out = defaultdict(list)
+        for key, e0, e1 in self._pending:
+            out[key].append(e0.elapsed_time(e1))
+        return dict(out)
+
+
 TIMER = KernelTimer()
