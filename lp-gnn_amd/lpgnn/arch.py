@@ -27,6 +27,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .sparse import BipartiteCSR, spmm
+from . import conv as _conv
 from . import fc as _fc
 
 
@@ -110,6 +111,12 @@ class GraphConvTwoDirection(nn.Module):
     def forward(self, left_feas, right_feas, edge_index: BipartiteCSR, edge_weight=None, relu: bool = False,
                 dropout: float = 0.0):
         # edge_index is A (m x n, rows = cons).  arch.py:71-74: l2r = A^T, r2l = A.
+        if edge_weight is None and isinstance(edge_index, BipartiteCSR) and \
+                getattr(edge_index, "partitioned_conv", None) is None:
+            # one autograd node for both directions (lpgnn.conv): same forward,
+            # fused gradient sums and the cheaper association in backward
+            return _conv.two_direction(left_feas, right_feas, edge_index, self.left2right, self.right2left,
+                                       relu, dropout)
         l2r, r2l = edge_index.t(), edge_index
         right_updated = self.left2right((left_feas, right_feas), l2r, edge_weight, relu=relu, dropout=dropout)
         left_updated = self.right2left((right_feas, left_feas), r2l, edge_weight, relu=relu, dropout=dropout)

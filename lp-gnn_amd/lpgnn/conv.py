@@ -1,0 +1,132 @@
+"""One GraphConvTwoDirection layer (arch.py:65-81) as a single autograd node.
+
+Forward is exactly the per-direction path of ``GraphConv`` (PyG 2.1,
+arch.py:57-62): for each direction the HIP SpMM aggregates the source side
+(aggregation before ``lin_rel``, the reference's order) and one fused FC
+kernel adds ``lin_rel``, its bias, ``lin_root`` and the ReLU (+ training
+dropout).  Both directions read the same-layer inputs (arch.py:74-80).
+
+Owning both directions in one backward lets the layer do what two separate
+autograd nodes cannot:
+
+* each input receives two gradients -- as the destination (root) of one
+  direction and as the source (aggregated) side of the other -- and they are
+  summed inside the second GEMM (``addmm_``, hipBLASLt beta = 1) instead of by
+  a separate autograd accumulation pass over [rows, F];
+* the source-side gradient Sᵀ(dZ·W_rel) is evaluated as (Sᵀ dZ)·W_rel
+  whenever that puts the GEMM on the smaller node set (c2: the 100 K
+  constraints instead of the 200 K variables for left2right): the same
+  product, one GEMM over half the rows.
+
+Gradients are tolerance-level (the reference's own backward is autograd
+through MKL); the forward is unchanged bit for bit.
+"""
+from __future__ import annotations
+
+import torch
+from torch import Tensor
+
+from . import fc as _fc
+from .sparse import BipartiteCSR, CSR, spmm_forward
+
+_GEMM_FLOPS = 120e12  # in-step rates used only to pick the cheaper association
+_SPMM_BYTES = 7e12
+
+
+def _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, p, seed, bf16):
+    if bf16:
+        return _fc.fc_forward_bf16(agg, w_rel, x_dst, w_root, b, relu, p, seed)
+    return _fc.fc_forward(agg, w_rel, x_dst, w_root, b, relu, p, seed)
+
+
+def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
+    """True if grad_src = (Sᵀ dZ) W is cheaper than Sᵀ (dZ W) (S: dst x src)."""
+    gemm = lambda rows: 2.0 * rows * f_out * f_in / _GEMM_FLOPS
+    spmm = lambda f: (S.nnz * f + S.n_cols * f) * esz / _SPMM_BYTES
+    return spmm(f_out) + gemm(S.n_cols) < gemm(S.n_rows) + spmm(f_in)
+
+
+class _TwoDirection(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+        if dropout > 0 and not relu:
+            raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
+        bf16 = left.dtype == torch.bfloat16
+        ws = (w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l)
+        if bf16:
+            ws = tuple(w.to(torch.bfloat16) for w in ws)
+        A, AT = adj.fwd, adj.bwd  # A: cons x vars (right2left), AT: vars x cons (left2right)
+        # arch.py:75-77: right' = left2right((left, right), A^T)
+        agg_r = spmm_forward(AT, left)
+        right_new = _fc_fwd(agg_r, right, ws[0], b_l2r, ws[1], relu, dropout,
+                            _fc._new_seed() if dropout > 0 else 0, bf16)
+        # arch.py:78-80: left' = right2left((right, left), A)
+        agg_l = spmm_forward(A, right)
+        left_new = _fc_fwd(agg_l, left, ws[2], b_r2l, ws[3], relu, dropout,
+                           _fc._new_seed() if dropout > 0 else 0, bf16)
+        ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
+        ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
+        ctx.has_b = (b_l2r is not None, b_r2l is not None)
+        ctx.save_for_backward(left, right, agg_l, agg_r, left_new, right_new, *ws)
+        return left_new, right_new
+
+    @staticmethod
+    def backward(ctx, g_left, g_right):
+        left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = \
+            ctx.saved_tensors
+        need = ctx.needs_input_grad
+        A, AT = ctx.adj.fwd, ctx.adj.bwd
+        bf16 = ctx.bf16
+        dt = torch.bfloat16 if bf16 else torch.float32
+
+        def mask(g, y, want_db):
+            if g is None:
+                g = torch.zeros_like(y)
+            if not ctx.relu:
+                g = g.to(dt).contiguous()
+                return g, (g.float().sum(0) if want_db else None)
+            if bf16:
+                return _fc.relu_bwd_colsum_bf16(g, y, ctx.scale, want_db)
+            return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
+
+        dz_r, db_l2r = mask(g_right, right_new, ctx.has_b[0] and need[4])
+        dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
+
+        def wgrads(dz, agg, x_dst, need_rel, need_root):
+            if not (need_rel or need_root):
+                return None, None
+            k = agg.shape[1] + x_dst.shape[1]
+            if not bf16 and k <= 16 and dz.shape[1] % 4 == 0:  # conv1: dZ read once
+                d_rel, d_root = _fc.wgrad_smallk(dz, agg, x_dst)
+            else:
+                d_rel = (dz.t() @ agg).float() if need_rel else None
+                d_root = (dz.t() @ x_dst).float() if need_root else None
+            return (d_rel if need_rel else None), (d_root if need_root else None)
+
+        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r, right, need[3], need[5])
+        dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
+
+        def src_grad(S: CSR, dz, w_rel):
+            """Sᵀ (dZ W_rel), S = dst x src, in the cheaper association."""
+            if _src_first(S, dz.shape[1], w_rel.shape[1], 2 if bf16 else 4):
+                St = A if S is AT else AT
+                return spmm_forward(St, dz) @ w_rel
+            St = A if S is AT else AT
+            return spmm_forward(St, dz @ w_rel)
+
+        g_l = g_r = None
+        if need[0]:  # left = src of left2right (S = A^T), dst of right2left
+            g_l = src_grad(AT, dz_r, w_rel_l2r)
+            g_l.addmm_(dz_l, w_root_r2l)
+        if need[1]:  # right = src of right2left (S = A), dst of left2right
+            g_r = src_grad(A, dz_l, w_rel_r2l)
+            g_r.addmm_(dz_r, w_root_l2r)
+        return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
+
+
+def two_direction(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, relu: bool = False,
+                  dropout: float = 0.0):
+    """GraphConvTwoDirection.forward (arch.py:65-81) through one autograd node."""
+    return _TwoDirection.apply(left, right, adj, left2right.lin_rel.weight, left2right.lin_rel.bias,
+                               left2right.lin_root.weight, right2left.lin_rel.weight, right2left.lin_rel.bias,
+                               right2left.lin_root.weight, bool(relu), float(dropout))
