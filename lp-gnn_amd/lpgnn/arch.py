@@ -117,6 +117,11 @@ class GraphConvTwoDirection(nn.Module):
             # fused gradient sums and the cheaper association in backward
             return _conv.two_direction(left_feas, right_feas, edge_index, self.left2right, self.right2left,
                                        relu, dropout)
+        tdc = getattr(edge_index, "two_direction_conv", None)  # row-partitioned multi-GPU adjacency
+        if tdc is not None and edge_weight is None:
+            out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout)
+            if out is not None:
+                return out
         l2r, r2l = edge_index.t(), edge_index
         right_updated = self.left2right((left_feas, right_feas), l2r, edge_weight, relu=relu, dropout=dropout)
         left_updated = self.right2left((right_feas, left_feas), r2l, edge_weight, relu=relu, dropout=dropout)

@@ -47,7 +47,7 @@ def _pad_k(t: Tensor) -> Tensor:
 
 
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
-               relu: bool, dropout_p: float = 0.0, seed: int = 0) -> Tensor:
+               relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None) -> Tensor:
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -57,7 +57,12 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
         A2, W2 = _pad_k(A2), _pad_k(W2)
     A1, W1, A2, W2 = _prep(A1), _prep(W1), _prep(A2), _prep(W2)
     bias = None if bias is None else bias.contiguous()
-    C = torch.empty((M, N), dtype=torch.float32, device=A1.device)
+    if out is not None:  # caller-provided rows (e.g. the owned rows of a partition's [owned | halo] buffer)
+        if out.shape != (M, N) or out.dtype != torch.float32 or out.stride(1) != 1 or out.device != A1.device:
+            raise RuntimeError("lpgnn FC: `out` must be a float32 [M, N] row-major view on the same device")
+        C = out
+    else:
+        C = torch.empty((M, N), dtype=torch.float32, device=A1.device)
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
     with torch.cuda.device(A1.device):

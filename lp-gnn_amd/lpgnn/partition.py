@@ -200,6 +200,38 @@ class Exchange:
         off = np.concatenate([[0], np.cumsum(self.recv_counts)]).astype(np.int64)
         self.recv_slices = [(int(off[q]), int(off[q + 1])) for q in range(len(self.recv_counts))
                             if off[q + 1] > off[q]]
+        # all_to_all is a collective: every rank calls it, or (no boundary
+        # rows anywhere in the partition) none does -- decided once, globally
+        tot = torch.tensor([float(sum(self.send_counts) + sum(self.recv_counts))])
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            if dist.get_backend(group) != "gloo":
+                tot = tot.to(device)
+            dist.all_reduce(tot, group=group)
+        self.active = bool(tot.item() > 0)
+
+    def _a2a(self, send, in_counts, out_counts):
+        if not self.active:
+            return send.new_empty((0,) + tuple(send.shape[1:]))
+        return _a2a(send, in_counts, out_counts, self.group)
+
+    def reduce_rows(self, full: torch.Tensor, inplace: bool) -> torch.Tensor:
+        """[n_local, F] partials -> [n_own, F] owner sums.  With inplace the
+        owners' rows of `full` are updated and a view is returned; otherwise
+        they are copied only if something is received."""
+        recv = self._a2a(full.index_select(0, self.send_idx), self.send_counts, self.recv_counts)
+        owned = full[:self.n_own]
+        if self.recv_slices:
+            if not inplace:
+                owned = owned.clone()
+            self.add_partials(owned, recv)
+        return owned
+
+    def broadcast_rows_(self, full: torch.Tensor) -> torch.Tensor:
+        """Fill the halo rows of [n_local, F] `full` from their owners, in place."""
+        recv = self._a2a(full[:self.n_own].index_select(0, self.recv_idx), self.recv_counts, self.send_counts)
+        if self.send_idx.numel():
+            full.index_copy_(0, self.send_idx, recv)
+        return full
 
     def add_partials(self, owned: torch.Tensor, recv: torch.Tensor) -> None:
         for a, b in self.recv_slices:  # deterministic: one index_add_ per source rank, unique rows each
@@ -207,14 +239,14 @@ class Exchange:
 
     def reduce(self, full: torch.Tensor) -> torch.Tensor:
         """[n_local, F] partials -> [n_own, F] sums (own partial + sources in rank order)."""
-        recv = _a2a(full.index_select(0, self.send_idx), self.send_counts, self.recv_counts, self.group)
+        recv = self._a2a(full.index_select(0, self.send_idx), self.send_counts, self.recv_counts)
         owned = full[:self.n_own].clone()
         self.add_partials(owned, recv)
         return owned
 
     def broadcast(self, owned: torch.Tensor) -> torch.Tensor:
         """[n_own, F] owner values -> [n_local, F] with the halo rows filled."""
-        recv = _a2a(owned.index_select(0, self.recv_idx), self.recv_counts, self.send_counts, self.group)
+        recv = self._a2a(owned.index_select(0, self.recv_idx), self.recv_counts, self.send_counts)
         out = owned.new_empty((self.n_local,) + tuple(owned.shape[1:]))
         out[:self.n_own] = owned
         if self.send_idx.numel():
@@ -257,6 +289,112 @@ def _local_spmm(adj: BipartiteCSR, x: torch.Tensor) -> torch.Tensor:
     return _sparse.spmm(adj, x)
 
 
+_product_spmm = _local_spmm
+
+
+class _PartTwoDirection(torch.autograd.Function):
+    """One GraphConvTwoDirection layer on a rank's partition, one autograd node
+    (the partitioned twin of lpgnn.conv._TwoDirection).
+
+    right = local variables [owned | halo], left = local constraints.
+    left2right: partial aggregates for every local variable, REDUCED to the
+    owners in place; the owners' FC writes straight into the first n_own rows
+    of the [n_local, F] output, whose halo rows are then BROADCAST from the
+    owners.  right2left is local (the halo rows are current).  Backward
+    mirrors it: the halo-row gradients of right' are reduced to their owners,
+    the aggregate gradient of the owned rows is broadcast back before the
+    transposed SpMM.  Gradient sums go through addmm_ as in the one-GPU node.
+    """
+
+    @staticmethod
+    def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+        from . import fc as _fc
+        from .sparse import spmm_forward
+
+        if dropout > 0 and not relu:
+            raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
+        if left.dtype != torch.float32:
+            raise RuntimeError("the row-partitioned path runs fp32 (the c2/c4 configurations)")
+        ex = padj.ex
+        A, AT = padj.local.fwd, padj.local.bwd  # A: local cons x local vars
+        n_own = ex.n_own
+        agg_r = spmm_forward(AT, left)              # partials for [owned | halo]
+        ex.reduce_rows(agg_r, inplace=True)         # owners' rows now hold the full sums
+        right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
+        _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout,
+                       _fc._new_seed() if dropout > 0 else 0, out=right_new[:n_own])
+        ex.broadcast_rows_(right_new)
+        agg_l = spmm_forward(A, right)
+        left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout,
+                                  _fc._new_seed() if dropout > 0 else 0)
+        ctx.padj, ctx.relu = padj, relu
+        ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
+        ctx.has_b = (b_l2r is not None, b_r2l is not None)
+        ctx.save_for_backward(left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l,
+                              w_root_r2l)
+        return left_new, right_new
+
+    @staticmethod
+    def backward(ctx, g_left, g_right):
+        from . import fc as _fc
+        from .conv import _src_first
+        from .sparse import spmm_forward
+
+        left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = \
+            ctx.saved_tensors
+        need = ctx.needs_input_grad
+        ex = ctx.padj.ex
+        A, AT = ctx.padj.local.fwd, ctx.padj.local.bwd
+        n_own = ex.n_own
+        if g_right is None:
+            g_right = torch.zeros_like(right_new)
+        if g_left is None:
+            g_left = torch.zeros_like(left_new)
+        g_right_own = ex.reduce_rows(g_right.contiguous(), inplace=False)  # halo grads -> owners
+
+        def mask(g, y, want_db):
+            if not ctx.relu:
+                g = g.contiguous()
+                return g, (g.sum(0) if want_db else None)
+            return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
+
+        dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
+        dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
+
+        def wgrads(dz, agg, x_dst, need_rel, need_root):
+            if not (need_rel or need_root):
+                return None, None
+            if agg.shape[1] + x_dst.shape[1] <= 16 and dz.shape[1] % 4 == 0:
+                d_rel, d_root = _fc.wgrad_smallk(dz, agg.contiguous(), x_dst.contiguous())
+            else:
+                d_rel = dz.t() @ agg if need_rel else None
+                d_root = dz.t() @ x_dst if need_root else None
+            return (d_rel if need_rel else None), (d_root if need_root else None)
+
+        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r[:n_own], right[:n_own], need[3], need[5])
+        dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
+
+        g_l = g_r = None
+        if need[0]:  # left: source of left2right through reduce(AT @ left)[:n_own]
+            f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
+            full = torch.zeros((right.shape[0], f_out if _src_first(AT, f_out, f_in, 4) else f_in),
+                               dtype=torch.float32, device=left.device)
+            if full.shape[1] == f_out:  # (A bcast(dZ)) W
+                full[:n_own] = dz_r
+                g_l = spmm_forward(A, ex.broadcast_rows_(full)) @ w_rel_l2r
+            else:                        # A bcast(dZ W)
+                torch.mm(dz_r, w_rel_l2r, out=full[:n_own])
+                g_l = spmm_forward(A, ex.broadcast_rows_(full))
+            g_l.addmm_(dz_l, w_root_r2l)
+        if need[1]:  # right [owned | halo]: source of right2left (all rows), destination of left2right (owned)
+            if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
+                g_r = spmm_forward(AT, dz_l) @ w_rel_r2l
+            else:
+                g_r = spmm_forward(AT, dz_l @ w_rel_r2l)
+            g_r[:n_own].addmm_(dz_r, w_root_l2r)
+        return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
+
+
 class PartitionedCSR:
     """The edge_index of a rank's batch: local dual CSR + boundary exchange.
 
@@ -279,6 +417,15 @@ class PartitionedCSR:
     @property
     def device(self):
         return self.local.device
+
+    def two_direction_conv(self, left, right, left2right, right2left, relu=False, dropout=0.0):
+        """GraphConvTwoDirection.forward on this partition (one autograd node)."""
+        if self.orient != "cons" or left.dtype != torch.float32 or _local_spmm is not _product_spmm:
+            return None  # generic per-direction path (oracle tests, bf16)
+        return _PartTwoDirection.apply(left, right, self, left2right.lin_rel.weight, left2right.lin_rel.bias,
+                                       left2right.lin_root.weight, right2left.lin_rel.weight,
+                                       right2left.lin_rel.bias, right2left.lin_root.weight, bool(relu),
+                                       float(dropout))
 
     def partitioned_conv(self, x, fc):
         """One GraphConv direction: fc(agg, x_dst) is lin_rel + lin_root (+ReLU, +dropout)."""
@@ -305,6 +452,7 @@ def make_local_batch(plan: PartitionPlan, x_s, x_t, y_s, y_t, device, group=None
         y_t=None if y_t is None else torch.as_tensor(np.asarray(y_t)[lv]).to(device),
         edge_index=adj, s_bs=plan.m_local, t_bs=plan.n_local, bs=plan.m_local + plan.n_local)
     b.var_owned = torch.from_numpy(plan.var_owned).to(device)
+    b.n_own = plan.n_own
     b.local_vars = torch.from_numpy(lv)
     b.plan = plan
     return b
@@ -312,32 +460,40 @@ def make_local_batch(plan: PartitionPlan, x_s, x_t, y_s, y_t, device, group=None
 
 # ----------------------------------------------------------------------- loss
 def _balanced_weights_from_counts(cnt: torch.Tensor) -> torch.Tensor:
-    """labels_to_balanced_weights (utils.py:286-299) from global counts."""
+    """labels_to_balanced_weights (utils.py:286-299) from global counts,
+    without host syncs (the same formula as lpgnn.train's)."""
     present = cnt > 0
-    res = torch.zeros(3, dtype=torch.float32, device=cnt.device)
     tot = cnt.sum().to(torch.float32)
-    res[present] = tot / cnt[present].to(torch.float32)
-    if int(present.sum()) != 2:
-        res[0] = res[2] = (res[0] + res[2]) / 2.
-    return res
+    res = torch.where(present, tot / cnt.to(torch.float32), torch.zeros((), device=cnt.device))
+    merged = (res[0] + res[2]) / 2.
+    two = present.sum() == 2
+    return torch.stack([torch.where(two, res[0], merged), res[1], torch.where(two, res[2], merged)])
 
 
 def balanced_distributed(lc, lv, y_s, y_t, var_owned, group=None):
     """Per-rank share of train.py:39-46 so that sum over ranks == the
     single-graph balanced loss (class weights and the weighted-mean
-    denominators are global)."""
-    ys, yt = y_s, y_t[var_owned]
-    lv = lv[var_owned]
-    cnt = torch.cat([torch.bincount(ys, minlength=3), torch.bincount(yt, minlength=3)]).to(torch.float64)
+    denominators are global).  `var_owned`: the number of owned variables
+    (they are the first local rows) or the legacy boolean mask.  No host sync."""
+    if isinstance(var_owned, int):
+        yt, lv = y_t[:var_owned], lv[:var_owned]
+    else:
+        yt, lv = y_t[var_owned], lv[var_owned]
+    ys = y_s
+    cnt = torch.zeros(6, dtype=torch.int64, device=ys.device)  # integer atomics: fp64 ones serialise on 3 bins
+    cnt[:3].scatter_add_(0, ys, torch.ones_like(ys))
+    cnt[3:].scatter_add_(0, yt, torch.ones_like(yt))
+    cnt = cnt.to(torch.float64)
     _all_reduce_(cnt, group)
     cs, ct = cnt[:3], cnt[3:]
-    m, n = cs.sum().item(), ct.sum().item()
+    m, n = cs.sum(), ct.sum()
     ws, wt = _balanced_weights_from_counts(cs), _balanced_weights_from_counts(ct)
     ce_s = F.cross_entropy(lc, ys, reduction="none")
     ce_t = F.cross_entropy(lv, yt, reduction="none")
     den = torch.stack([ws[ys].sum(), wt[yt].sum()]).to(torch.float64)
     _all_reduce_(den, group)
-    return (m + n) / m * (ws[ys] * ce_s).sum() / den[0].float() + (m + n) / n * (wt[yt] * ce_t).sum() / den[1].float()
+    return ((m + n) / m).float() * (ws[ys] * ce_s).sum() / den[0].float() + \
+        ((m + n) / n).float() * (wt[yt] * ce_t).sum() / den[1].float()
 
 
 def all_reduce_grads(model, group=None):
@@ -356,7 +512,7 @@ def all_reduce_grads(model, group=None):
 
 def train_step_distributed(model, batch, opt, group=None):
     lc, lv = model(batch)
-    loss = balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.var_owned, group)
+    loss = balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.n_own, group)
     opt.zero_grad()
     loss.backward()
     all_reduce_grads(model, group)

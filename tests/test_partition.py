@@ -116,6 +116,8 @@ def _worker(rank, world, port, out_dir):
         model.train()
         lc, lv = model(batch)
         loss = part.balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.var_owned)
+        loss_n = part.balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.n_own)  # owned rows come first
+        assert torch.allclose(loss, loss_n, rtol=1e-6, atol=1e-7)
         model.zero_grad()
         loss.backward()
         part.all_reduce_grads(model)
