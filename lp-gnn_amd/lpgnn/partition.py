@@ -187,6 +187,32 @@ def _a2a(send: torch.Tensor, in_counts: list, out_counts: list, group) -> torch.
     return recv
 
 
+class _Pending:
+    """An all_to_all in flight (RCCL runs it on its own stream; `finish`
+    makes the current stream wait, then applies `then` to the received rows).
+    gloo with HIP tensors stages through the host synchronously."""
+
+    def __init__(self, recv, work=None, host=None, then=None):
+        self.recv, self.work, self.host, self.then = recv, work, host, then
+
+    def finish(self):
+        if self.work is not None:
+            self.work.wait()
+        if self.host is not None:
+            self.recv.copy_(self.host)
+        return self.then(self.recv) if self.then is not None else self.recv
+
+
+def _a2a_start(send: torch.Tensor, in_counts: list, out_counts: list, group) -> _Pending:
+    recv = send.new_empty((sum(out_counts),) + tuple(send.shape[1:]))
+    if dist.get_backend(group) == "gloo" and send.is_cuda:
+        h = torch.empty(recv.shape, dtype=recv.dtype)
+        dist.all_to_all_single(h, send.cpu(), out_counts, in_counts, group=group)
+        return _Pending(recv, host=h)
+    work = dist.all_to_all_single(recv, send.contiguous(), out_counts, in_counts, group=group, async_op=True)
+    return _Pending(recv, work=work)
+
+
 class Exchange:
     """The static boundary exchange of one rank (see module docstring)."""
 
@@ -213,6 +239,34 @@ class Exchange:
         if not self.active:
             return send.new_empty((0,) + tuple(send.shape[1:]))
         return _a2a(send, in_counts, out_counts, self.group)
+
+    def start_reduce(self, full: torch.Tensor, inplace: bool) -> _Pending:
+        """Asynchronous reduce_rows: finish() returns the [n_own, F] owner sums."""
+        def then(recv):
+            owned = full[:self.n_own]
+            if self.recv_slices:
+                if not inplace:
+                    owned = owned.clone()
+                self.add_partials(owned, recv)
+            return owned
+        if not self.active:
+            return _Pending(None, then=lambda _: full[:self.n_own])
+        p = _a2a_start(full.index_select(0, self.send_idx), self.send_counts, self.recv_counts, self.group)
+        p.then = then
+        return p
+
+    def start_broadcast_(self, full: torch.Tensor) -> _Pending:
+        """Asynchronous broadcast_rows_: finish() fills the halo rows and returns `full`."""
+        def then(recv):
+            if self.send_idx.numel():
+                full.index_copy_(0, self.send_idx, recv)
+            return full
+        if not self.active:
+            return _Pending(None, then=lambda _: full)
+        p = _a2a_start(full[:self.n_own].index_select(0, self.recv_idx), self.recv_counts, self.send_counts,
+                       self.group)
+        p.then = then
+        return p
 
     def reduce_rows(self, full: torch.Tensor, inplace: bool) -> torch.Tensor:
         """[n_local, F] partials -> [n_own, F] owner sums.  With inplace the
@@ -318,15 +372,17 @@ class _PartTwoDirection(torch.autograd.Function):
         ex = padj.ex
         A, AT = padj.local.fwd, padj.local.bwd  # A: local cons x local vars
         n_own = ex.n_own
+        seed_r = _fc._new_seed() if dropout > 0 else 0
+        seed_l = _fc._new_seed() if dropout > 0 else 0
         agg_r = spmm_forward(AT, left)              # partials for [owned | halo]
-        ex.reduce_rows(agg_r, inplace=True)         # owners' rows now hold the full sums
+        red = ex.start_reduce(agg_r, inplace=True)  # halo partials -> owners, in flight ...
+        agg_l = spmm_forward(A, right)              # ... under the purely local constraint side
+        left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l)
+        red.finish()                                # owners' rows of agg_r now hold the full sums
         right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
-        _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout,
-                       _fc._new_seed() if dropout > 0 else 0, out=right_new[:n_own])
-        ex.broadcast_rows_(right_new)
-        agg_l = spmm_forward(A, right)
-        left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout,
-                                  _fc._new_seed() if dropout > 0 else 0)
+        _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
+                       out=right_new[:n_own])
+        ex.start_broadcast_(right_new).finish()
         ctx.padj, ctx.relu = padj, relu
         ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
         ctx.has_b = (b_l2r is not None, b_r2l is not None)
@@ -350,16 +406,13 @@ class _PartTwoDirection(torch.autograd.Function):
             g_right = torch.zeros_like(right_new)
         if g_left is None:
             g_left = torch.zeros_like(left_new)
-        g_right_own = ex.reduce_rows(g_right.contiguous(), inplace=False)  # halo grads -> owners
+        red = ex.start_reduce(g_right.contiguous(), inplace=False)  # halo grads -> owners, in flight ...
 
         def mask(g, y, want_db):
             if not ctx.relu:
                 g = g.contiguous()
                 return g, (g.sum(0) if want_db else None)
             return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
-
-        dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
-        dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
 
         def wgrads(dz, agg, x_dst, need_rel, need_root):
             if not (need_rel or need_root):
@@ -371,27 +424,37 @@ class _PartTwoDirection(torch.autograd.Function):
                 d_root = dz.t() @ x_dst if need_root else None
             return (d_rel if need_rel else None), (d_root if need_root else None)
 
-        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r[:n_own], right[:n_own], need[3], need[5])
+        # ... under everything that only needs the constraint side's gradient
+        dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
         dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
-
-        g_l = g_r = None
-        if need[0]:  # left: source of left2right through reduce(AT @ left)[:n_own]
-            f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
-            full = torch.zeros((right.shape[0], f_out if _src_first(AT, f_out, f_in, 4) else f_in),
-                               dtype=torch.float32, device=left.device)
-            if full.shape[1] == f_out:  # (A bcast(dZ)) W
-                full[:n_own] = dz_r
-                g_l = spmm_forward(A, ex.broadcast_rows_(full)) @ w_rel_l2r
-            else:                        # A bcast(dZ W)
-                torch.mm(dz_r, w_rel_l2r, out=full[:n_own])
-                g_l = spmm_forward(A, ex.broadcast_rows_(full))
-            g_l.addmm_(dz_l, w_root_r2l)
-        if need[1]:  # right [owned | halo]: source of right2left (all rows), destination of left2right (owned)
+        g_r = None
+        if need[1]:  # right [owned | halo] as the source of right2left: every local row
             if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
                 g_r = spmm_forward(AT, dz_l) @ w_rel_r2l
             else:
                 g_r = spmm_forward(AT, dz_l @ w_rel_r2l)
+        g_right_own = red.finish()
+        dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
+        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r[:n_own], right[:n_own], need[3], need[5])
+        if need[1]:  # ... and as the destination of left2right (owned rows)
             g_r[:n_own].addmm_(dz_r, w_root_l2r)
+
+        g_l = None
+        if need[0]:  # left: source of left2right through reduce(AT @ left)[:n_own]
+            f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
+            first = _src_first(AT, f_out, f_in, 4)
+            full = torch.empty((right.shape[0], f_out if first else f_in), dtype=torch.float32, device=left.device)
+            if first:
+                full[:n_own] = dz_r
+            else:
+                torch.mm(dz_r, w_rel_l2r, out=full[:n_own])
+            bc = ex.start_broadcast_(full)           # owners' aggregate gradient -> halo rows, in flight ...
+            root = dz_l @ w_root_r2l                 # ... under the root-path gradient of left
+            bc.finish()
+            if first:
+                g_l = torch.addmm(root, spmm_forward(A, full), w_rel_l2r)
+            else:
+                g_l = spmm_forward(A, full).add_(root)
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 
