@@ -157,6 +157,14 @@ int64_t lpg_wgrad_smallk_workspace_bytes(int64_t M, int64_t N, int64_t K);
 lpg_status lpg_wgrad_smallk_f32(int64_t M, int64_t N, const float *dz, int64_t ldz,
                                 int64_t K1, const float *A1, int64_t lda1, int64_t K2, const float *A2, int64_t lda2,
                                 float *dW1, float *dW2, void *workspace, void *stream);
+/* Same with the ReLU/dropout backward fused: dZ = (y > 0) ? g * scale : 0 is
+ * formed on the fly from the output gradient g and the stored output y (never
+ * written), and db[n] = sum_m dZ[m, n] when db != NULL.  For layers whose
+ * inputs need no gradient (conv1).  Same workspace size. */
+lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const float *g, int64_t ldg, const float *y, int64_t ldy,
+                                     float scale, int64_t K1, const float *A1, int64_t lda1, int64_t K2,
+                                     const float *A2, int64_t lda2, float *dW1, float *dW2, float *db,
+                                     void *workspace, void *stream);
 
 /* bf16 variant (c5 configuration, BASELINE.json configs[4]): A1/A2/W1/W2
  * bf16 bit patterns (uint16), K1 and K2 multiples of 64 (zero-pad), leading

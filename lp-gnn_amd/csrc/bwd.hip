@@ -4,6 +4,7 @@
 //   lpg_relu_bwd_colsum_f32   dZ = (Y > 0) ? dY * scale : 0   (ReLU + fused dropout backward)
 //                             and db = sum_m dZ[m, :]          (lin_rel.bias grad) in the same pass
 //   lpg_wgrad_smallk_f32      dW1 = dZ^T A1, dW2 = dZ^T A2 for small K (conv1: K1 = K2 = 8 LP features)
+//   lpg_relu_wgrad_smallk_f32 the same from (g, y) with the ReLU/dropout backward and db fused (dZ never stored)
 //   lpg_linear_small_bwd_f32  the heads' backward (N = 3 outputs): dH = G W, dW = G^T H, db = sum G
 //
 // All are row-block kernels: a block owns R consecutive rows and all columns
@@ -192,13 +193,19 @@ int64_t fold_floats(int64_t nblk, int64_t n) { return (nblk + (nblk > 2 * kFold 
 // The block's [A1 | A2] rows are staged once into LDS ([row][KP], zero-padded
 // to KP = K rounded up to 4) and read back as broadcast b128 loads.  (Weight
 // gradients carry no bitwise contract: fused multiply-adds, checked against
-// fp64 within the summation bound.)
-template <int K>
+// fp64 within the summation bound.)  With MASK the kernel reads the output
+// gradient g and the stored output y instead of dZ and applies the ReLU /
+// dropout backward on the fly, dZ = (y > 0) ? g * scale : 0, adding a K-th
+// partial row for the bias gradient -- conv1 (whose inputs need no gradient)
+// never materialises dZ.
+template <int K, bool MASK>
 __global__ __launch_bounds__(kT) void wgrad_smallk_p1(int64_t M, int64_t N, const float *__restrict__ dz,
-                                                      int64_t ldz, int K1, const float *__restrict__ A1,
+                                                      int64_t ldz, const float *__restrict__ y, int64_t ldy,
+                                                      float scale, int K1, const float *__restrict__ A1,
                                                       int64_t lda1, const float *__restrict__ A2, int64_t lda2,
                                                       float *__restrict__ part) {
   constexpr int KP = (K + 3) / 4 * 4;
+  constexpr int KR = K + (MASK ? 1 : 0);  // partial rows per block
   __shared__ float4 sa[kRowsWgrad * KP / 4];
   const int64_t r0 = (int64_t)blockIdx.x * kRowsWgrad;
   const int64_t r1 = r0 + kRowsWgrad < M ? r0 + kRowsWgrad : M;
@@ -212,9 +219,9 @@ __global__ __launch_bounds__(kT) void wgrad_smallk_p1(int64_t M, int64_t N, cons
   }
   __syncthreads();
   for (int64_t c = (int64_t)threadIdx.x * 4; c < N; c += kT * 4) {
-    float4 acc[K];
+    float4 acc[KR];
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < KR; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     auto row = [&](int r, float4 z) {
       float a[KP];
 #pragma unroll
@@ -227,36 +234,45 @@ __global__ __launch_bounds__(kT) void wgrad_smallk_p1(int64_t M, int64_t N, cons
         acc[k].x = __builtin_fmaf(a[k], z.x, acc[k].x); acc[k].y = __builtin_fmaf(a[k], z.y, acc[k].y);
         acc[k].z = __builtin_fmaf(a[k], z.z, acc[k].z); acc[k].w = __builtin_fmaf(a[k], z.w, acc[k].w);
       }
+      if (MASK) add4(acc[KR - 1], z);
+    };
+    auto load_z = [&](int64_t m) {
+      const float4 g = *reinterpret_cast<const float4 *>(dz + m * ldz + c);
+      if (!MASK) return g;
+      return relu_scale(g, *reinterpret_cast<const float4 *>(y + m * ldy + c), scale);
     };
     const int nr = (int)(r1 - r0);
     int r = 0;
     for (; r + 4 <= nr; r += 4) {
       float4 z[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) z[u] = *reinterpret_cast<const float4 *>(dz + (r0 + r + u) * ldz + c);
+      for (int u = 0; u < 4; ++u) z[u] = load_z(r0 + r + u);
 #pragma unroll
       for (int u = 0; u < 4; ++u) row(r + u, z[u]);
     }
-    for (; r < nr; ++r) row(r, *reinterpret_cast<const float4 *>(dz + (r0 + r) * ldz + c));
-    float *pb = part + (int64_t)blockIdx.x * K * N;
+    for (; r < nr; ++r) row(r, load_z(r0 + r));
+    float *pb = part + (int64_t)blockIdx.x * KR * N;
 #pragma unroll
-    for (int k = 0; k < K; ++k) *reinterpret_cast<float4 *>(pb + k * N + c) = acc[k];
+    for (int k = 0; k < KR; ++k) *reinterpret_cast<float4 *>(pb + k * N + c) = acc[k];
   }
 }
 
-// dW1[n][k] (k < K1) and dW2[n][k - K1] from the [K][N] partial image
-__global__ __launch_bounds__(kT) void wgrad_smallk_p2(int64_t nrow, int64_t N, int K, int K1,
+// dW1[n][k] (k < K1), dW2[n][k - K1] (k < K) and db[n] (k = K) from the
+// [KR][N] partial image
+__global__ __launch_bounds__(kT) void wgrad_smallk_p2(int64_t nrow, int64_t N, int K, int KR, int K1,
                                                       const float *__restrict__ img, float *__restrict__ dW1,
-                                                      float *__restrict__ dW2) {
-  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;  // over K * N, i = k * N + n
-  if (i >= (int64_t)K * N) return;
-  const float s = sum_rows(nrow, (int64_t)K * N, img, i);
+                                                      float *__restrict__ dW2, float *__restrict__ db) {
+  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;  // over KR * N, i = k * N + n
+  if (i >= (int64_t)KR * N) return;
+  const float s = sum_rows(nrow, (int64_t)KR * N, img, i);
   const int k = (int)(i / N);
   const int64_t n = i % N;
   if (k < K1) {
     if (dW1) dW1[n * K1 + k] = s;
-  } else if (dW2) {
-    dW2[n * (K - K1) + (k - K1)] = s;
+  } else if (k < K) {
+    if (dW2) dW2[n * (K - K1) + (k - K1)] = s;
+  } else if (db) {
+    db[n] = s;
   }
 }
 
@@ -392,42 +408,75 @@ extern "C" lpg_status lpg_relu_bwd_colsum_bf16(int64_t M, int64_t N, const uint1
 
 extern "C" int64_t lpg_wgrad_smallk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N < 0 || K < 0) return -1;
-  return fold_floats((M + kRowsWgrad - 1) / kRowsWgrad, K * N) * (int64_t)sizeof(float);
+  return fold_floats((M + kRowsWgrad - 1) / kRowsWgrad, (K + 1) * N) * (int64_t)sizeof(float);
 }
 
-extern "C" lpg_status lpg_wgrad_smallk_f32(int64_t M, int64_t N, const float *dz, int64_t ldz, int64_t K1,
-                                           const float *A1, int64_t lda1, int64_t K2, const float *A2, int64_t lda2,
-                                           float *dW1, float *dW2, void *workspace, void *stream) {
+namespace lpg {
+namespace {
+
+lpg_status wgrad_smallk(int64_t M, int64_t N, const float *dz, int64_t ldz, const float *y, int64_t ldy, float scale,
+                        int64_t K1, const float *A1, int64_t lda1, int64_t K2, const float *A2, int64_t lda2,
+                        float *dW1, float *dW2, float *db, void *workspace, void *stream, const char *name) {
   const int64_t K = K1 + K2;
-  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0 && K >= 1 && K <= kMaxSmallK,
-              "lpg_wgrad_smallk_f32: need 1 <= K1 + K2 <= %d", kMaxSmallK);
-  LPG_REQUIRE(dz && workspace && (K1 == 0 || A1) && (K2 == 0 || A2), "lpg_wgrad_smallk_f32: NULL pointer");
-  LPG_REQUIRE(N % 4 == 0 && ldz % 4 == 0 && aligned16(dz) && aligned16(workspace),
-              "lpg_wgrad_smallk_f32: N / ldz multiples of 4, dZ and workspace 16-byte aligned");
+  const bool mask = y != nullptr;
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0 && K >= 1 && K <= kMaxSmallK, "%s: need 1 <= K1 + K2 <= %d",
+              name, kMaxSmallK);
+  LPG_REQUIRE(dz && workspace && (K1 == 0 || A1) && (K2 == 0 || A2), "%s: NULL pointer", name);
+  LPG_REQUIRE(N % 4 == 0 && ldz % 4 == 0 && aligned16(dz) && aligned16(workspace) &&
+                  (!mask || (ldy % 4 == 0 && aligned16(y))),
+              "%s: N / leading dims multiples of 4, gradient / output / workspace 16-byte aligned", name);
   hipStream_t s = as_stream(stream);
   if (M == 0 || N == 0) {
     if (dW1 && N * K1) LPG_HIP(hipMemsetAsync(dW1, 0, sizeof(float) * N * K1, s));
     if (dW2 && N * K2) LPG_HIP(hipMemsetAsync(dW2, 0, sizeof(float) * N * K2, s));
+    if (db && N) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, s));
     return LPG_OK;
   }
   const int64_t nblk = (M + kRowsWgrad - 1) / kRowsWgrad;
+  const int64_t KR = K + (mask ? 1 : 0);
   float *part = static_cast<float *>(workspace);
   const int k1 = (int)K1;
   const dim3 grid((unsigned)nblk), block(kT);
-  switch (K) {
-#define LPG_WG(KK) \
-  case KK: hipLaunchKernelGGL(wgrad_smallk_p1<KK>, grid, block, 0, s, M, N, dz, ldz, k1, A1, lda1, A2, lda2, part); break;
+  switch (K * 2 + (mask ? 1 : 0)) {
+#define LPG_WG(KK)                                                                                                  \
+  case 2 * KK:                                                                                                      \
+    hipLaunchKernelGGL((wgrad_smallk_p1<KK, false>), grid, block, 0, s, M, N, dz, ldz, y, ldy, scale, k1, A1, lda1, \
+                       A2, lda2, part);                                                                             \
+    break;                                                                                                          \
+  case 2 * KK + 1:                                                                                                  \
+    hipLaunchKernelGGL((wgrad_smallk_p1<KK, true>), grid, block, 0, s, M, N, dz, ldz, y, ldy, scale, k1, A1, lda1,  \
+                       A2, lda2, part);                                                                             \
+    break;
     LPG_WG(1) LPG_WG(2) LPG_WG(3) LPG_WG(4) LPG_WG(5) LPG_WG(6) LPG_WG(7) LPG_WG(8)
     LPG_WG(9) LPG_WG(10) LPG_WG(11) LPG_WG(12) LPG_WG(13) LPG_WG(14) LPG_WG(15) LPG_WG(16)
 #undef LPG_WG
   }
   LPG_HIP(hipGetLastError());
   const float *img;
-  const int64_t nrow = fold(nblk, K * N, part, part + nblk * K * N, &img, s);
-  hipLaunchKernelGGL(wgrad_smallk_p2, dim3((unsigned)((K * N + kT - 1) / kT)), dim3(kT), 0, s, nrow, N, (int)K, k1,
-                     img, dW1, dW2);
+  const int64_t nrow = fold(nblk, KR * N, part, part + nblk * KR * N, &img, s);
+  hipLaunchKernelGGL(wgrad_smallk_p2, dim3((unsigned)((KR * N + kT - 1) / kT)), dim3(kT), 0, s, nrow, N, (int)K,
+                     (int)KR, k1, img, dW1, dW2, db);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
+}
+
+}  // namespace
+}  // namespace lpg
+
+extern "C" lpg_status lpg_wgrad_smallk_f32(int64_t M, int64_t N, const float *dz, int64_t ldz, int64_t K1,
+                                           const float *A1, int64_t lda1, int64_t K2, const float *A2, int64_t lda2,
+                                           float *dW1, float *dW2, void *workspace, void *stream) {
+  return wgrad_smallk(M, N, dz, ldz, nullptr, 0, 1.f, K1, A1, lda1, K2, A2, lda2, dW1, dW2, nullptr, workspace,
+                      stream, "lpg_wgrad_smallk_f32");
+}
+
+extern "C" lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const float *g, int64_t ldg, const float *y,
+                                                int64_t ldy, float scale, int64_t K1, const float *A1, int64_t lda1,
+                                                int64_t K2, const float *A2, int64_t lda2, float *dW1, float *dW2,
+                                                float *db, void *workspace, void *stream) {
+  LPG_REQUIRE(y != nullptr, "lpg_relu_wgrad_smallk_f32: NULL output");
+  return wgrad_smallk(M, N, g, ldg, y, ldy, scale, K1, A1, lda1, K2, A2, lda2, dW1, dW2, db, workspace, stream,
+                      "lpg_relu_wgrad_smallk_f32");
 }
 
 extern "C" int64_t lpg_linear_small_bwd_workspace_bytes(int64_t M, int64_t K, int64_t N) {

@@ -38,6 +38,7 @@ HEADER_SYMBOLS = (
     "lpg_relu_bwd_colsum_bf16",
     "lpg_wgrad_smallk_workspace_bytes",
     "lpg_wgrad_smallk_f32",
+    "lpg_relu_wgrad_smallk_f32",
     "lpg_linear_small_bwd_workspace_bytes",
     "lpg_linear_small_bwd_f32",
     "lpg_knowledge_f32",
@@ -107,6 +108,9 @@ def lib() -> ctypes.CDLL:
     L.lpg_wgrad_smallk_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p,
                                        c_p]
     L.lpg_wgrad_smallk_f32.restype = c_i32
+    L.lpg_relu_wgrad_smallk_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_i64, ctypes.c_float, c_i64, c_p, c_i64,
+                                            c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_relu_wgrad_smallk_f32.restype = c_i32
     L.lpg_linear_small_bwd_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
     L.lpg_linear_small_bwd_workspace_bytes.restype = c_i64
     L.lpg_linear_small_bwd_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p,

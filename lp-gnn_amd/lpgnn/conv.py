@@ -89,6 +89,20 @@ class _TwoDirection(torch.autograd.Function):
                 return _fc.relu_bwd_colsum_bf16(g, y, ctx.scale, want_db)
             return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
 
+        small = (not bf16 and ctx.relu and agg_r.shape[1] + right.shape[1] <= 16
+                 and agg_l.shape[1] + left.shape[1] <= 16 and right_new.shape[1] % 4 == 0)
+        if small and not (need[0] or need[1]):
+            # conv1: the inputs are features -- weight and bias gradients straight from (g, y)
+            g_r0 = torch.zeros_like(right_new) if g_right is None else g_right
+            g_l0 = torch.zeros_like(left_new) if g_left is None else g_left
+            dw_rel_l2r, dw_root_l2r, db_l2r = _fc.relu_wgrad_smallk(g_r0, right_new, ctx.scale, agg_r, right,
+                                                                    ctx.has_b[0] and need[4])
+            dw_rel_r2l, dw_root_r2l, db_r2l = _fc.relu_wgrad_smallk(g_l0, left_new, ctx.scale, agg_l, left,
+                                                                    ctx.has_b[1] and need[7])
+            keep = lambda t, i: t if need[i] else None
+            return (None, None, None, keep(dw_rel_l2r, 3), db_l2r, keep(dw_root_l2r, 5), keep(dw_rel_r2l, 6), db_r2l,
+                    keep(dw_root_r2l, 8), None, None)
+
         dz_r, db_l2r = mask(g_right, right_new, ctx.has_b[0] and need[4])
         dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
 

@@ -191,6 +191,28 @@ def wgrad_smallk(dz: Tensor, A1: Tensor, A2: Tensor | None):
     return dW1, dW2
 
 
+def relu_wgrad_smallk(g: Tensor, y: Tensor, scale: float, A1: Tensor, A2: Tensor | None, want_db: bool):
+    """(dW1, dW2, db) of a narrow-input FC straight from (g, y): the ReLU /
+    dropout backward is applied on the fly and dZ is never stored."""
+    M, N = g.shape
+    g, y = g.contiguous(), y.contiguous()
+    A1 = A1.contiguous()
+    A2 = None if A2 is None else A2.contiguous()
+    K1, K2 = A1.shape[1], (0 if A2 is None else A2.shape[1])
+    L = _lib.lib()
+    ws = _workspace(L.lpg_wgrad_smallk_workspace_bytes(M, N, K1 + K2), g.device)
+    dW1 = torch.empty((N, K1), dtype=torch.float32, device=g.device)
+    dW2 = torch.empty((N, K2), dtype=torch.float32, device=g.device) if K2 else None
+    db = torch.empty(N, dtype=torch.float32, device=g.device) if want_db else None
+    with torch.cuda.device(g.device):
+        st = L.lpg_relu_wgrad_smallk_f32(M, N, g.data_ptr(), g.stride(0), y.data_ptr(), y.stride(0), float(scale),
+                                         K1, A1.data_ptr(), max(K1, 1), K2, None if A2 is None else A2.data_ptr(),
+                                         max(K2, 1), dW1.data_ptr(), None if dW2 is None else dW2.data_ptr(),
+                                         None if db is None else db.data_ptr(), ws.data_ptr(), _lib.stream_of(g))
+    _lib.check(st, "lpg_relu_wgrad_smallk_f32")
+    return dW1, dW2, db
+
+
 def _new_seed() -> int:
     """A dropout seed from torch's default generator (torch.manual_seed reproducible)."""
     return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())

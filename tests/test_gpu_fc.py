@@ -281,3 +281,27 @@ def test_wgrad_smallk(M, N, K1, K2):
         s = dz.double().abs().t() @ A.double().abs()
         err = (dW.double() - r).abs()
         assert dW.shape == (N, A.shape[1]) and bool((err <= chain * 2.0 ** -24 * s + 1e-30).all())
+
+
+@pytest.mark.parametrize("M,N,K1,K2,scale", [(1, 4, 8, 8, 1.0), (1000, 1024, 8, 8, 1.0), (70001, 1024, 8, 8, 1.25),
+                                             (300, 64, 3, 0, 1.0)])
+def test_relu_wgrad_smallk_equals_unfused(M, N, K1, K2, scale):
+    """conv1's fused backward == mask -> wgrad_smallk / colsum (same products, same bound vs fp64)."""
+    from lpgnn.fc import relu_wgrad_smallk
+
+    torch.manual_seed(M + N)
+    g = torch.randn(M, N, device=DEV)
+    y = torch.relu(torch.randn(M, N, device=DEV))
+    A1 = torch.randn(M, K1, device=DEV)
+    A2 = torch.randn(M, K2, device=DEV) if K2 else None
+    dW1, dW2, db = relu_wgrad_smallk(g, y, scale, A1, A2, True)
+    dz = torch.where(y > 0, g * scale, torch.zeros((), device=DEV)).double()
+    chain = 256 + (M + 255) // 256
+    for dW, A in ((dW1, A1), (dW2, A2)):
+        if A is None:
+            assert dW is None
+            continue
+        r = dz.t() @ A.double()
+        bound = chain * 2.0 ** -24 * (dz.abs().t() @ A.double().abs())
+        assert bool(((dW.double() - r).abs() <= bound + 1e-30).all())
+    assert bool(((db.double() - dz.sum(0)).abs() <= chain * 2.0 ** -24 * dz.abs().sum(0) + 1e-30).all())
