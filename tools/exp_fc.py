@@ -18,7 +18,12 @@ W1, W2 = torch.randn(1024, 1024, device="cuda") * 0.03, torch.randn(1024, 1024, 
 b = torch.randn(1024, device="cuda")
 L = _lib.lib()
 res = {}
+ref = fc_forward(A1, W1, A2, W2, b, True)
 for v in (0, 7):
-    L.lpg_fc_set_variant(v)
-    res[v] = timeit({"x": lambda: fc_forward(A1, W1, A2, W2, b, True)})["x"]
-print(os.environ.get("LPGNN_LIB", "default"), {v: (ms, 2.0 * M * 1024 * 2048 / ms / 1e9) for v, ms in res.items()})
+    for ng in (0,):
+        L.lpg_fc_set_variant(v)
+        assert torch.equal(fc_forward(A1, W1, A2, W2, b, True), ref)
+        res[(v, ng)] = timeit({"x": lambda: fc_forward(A1, W1, A2, W2, b, True)})["x"]
+L.lpg_fc_set_variant(0)
+for k, ms in res.items():
+    print(f"variant {k[0]}: {ms:.3f} ms {2.0 * M * 1024 * 2048 / ms / 1e9:.1f} TF/s")
