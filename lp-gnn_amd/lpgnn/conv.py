@@ -23,6 +23,8 @@ through MKL); the forward is unchanged bit for bit.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import Tensor
 
@@ -31,6 +33,15 @@ from .sparse import BipartiteCSR, CSR, spmm_forward
 
 _GEMM_FLOPS = 120e12  # in-step rates used only to pick the cheaper association
 _SPMM_BYTES = 7e12
+# HBM-bound SpMMs on a second stream beside the MFMA-bound FC / GEMMs (LPGNN_OVERLAP=0 disables)
+_OVERLAP = os.environ.get("LPGNN_OVERLAP", "1") == "1"
+_SIDE = {}
+
+
+def _side_stream(device):
+    if device not in _SIDE:
+        _SIDE[device] = torch.cuda.Stream(device)
+    return _SIDE[device]
 
 
 def _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, p, seed, bf16):
@@ -56,14 +67,23 @@ class _TwoDirection(torch.autograd.Function):
         if bf16:
             ws = tuple(w.to(torch.bfloat16) for w in ws)
         A, AT = adj.fwd, adj.bwd  # A: cons x vars (right2left), AT: vars x cons (left2right)
+        seed_r = _fc._new_seed() if dropout > 0 else 0
+        seed_l = _fc._new_seed() if dropout > 0 else 0
+        side = _side_stream(left.device) if _OVERLAP else None
         # arch.py:75-77: right' = left2right((left, right), A^T)
         agg_r = spmm_forward(AT, left)
-        right_new = _fc_fwd(agg_r, right, ws[0], b_l2r, ws[1], relu, dropout,
-                            _fc._new_seed() if dropout > 0 else 0, bf16)
-        # arch.py:78-80: left' = right2left((right, left), A)
-        agg_l = spmm_forward(A, right)
-        left_new = _fc_fwd(agg_l, left, ws[2], b_r2l, ws[3], relu, dropout,
-                           _fc._new_seed() if dropout > 0 else 0, bf16)
+        if side is not None:  # right2left's HBM-bound SpMM beside left2right's MFMA-bound FC
+            side.wait_stream(torch.cuda.current_stream(left.device))
+            with torch.cuda.stream(side):
+                agg_l = spmm_forward(A, right)
+            right_new = _fc_fwd(agg_r, right, ws[0], b_l2r, ws[1], relu, dropout, seed_r, bf16)
+            torch.cuda.current_stream(left.device).wait_stream(side)
+            agg_l.record_stream(torch.cuda.current_stream(left.device))
+        else:
+            right_new = _fc_fwd(agg_r, right, ws[0], b_l2r, ws[1], relu, dropout, seed_r, bf16)
+            # arch.py:78-80: left' = right2left((right, left), A)
+            agg_l = spmm_forward(A, right)
+        left_new = _fc_fwd(agg_l, left, ws[2], b_r2l, ws[3], relu, dropout, seed_l, bf16)
         ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
         ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
         ctx.has_b = (b_l2r is not None, b_r2l is not None)
@@ -105,6 +125,16 @@ class _TwoDirection(torch.autograd.Function):
 
         dz_r, db_l2r = mask(g_right, right_new, ctx.has_b[0] and need[4])
         dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
+        main = torch.cuda.current_stream(dz_r.device)
+        side = _side_stream(dz_r.device) if _OVERLAP else None
+        esz = 2 if bf16 else 4
+        # left2right source gradient: when the SpMM comes first it only needs dZ_r -- start it
+        # on the side stream so it streams HBM under the weight-gradient GEMMs
+        t_l2r = None
+        if need[0] and side is not None and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], esz):
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                t_l2r = spmm_forward(A, dz_r)
 
         def wgrads(dz, agg, x_dst, need_rel, need_root):
             if not (need_rel or need_root):
@@ -122,19 +152,23 @@ class _TwoDirection(torch.autograd.Function):
 
         def src_grad(S: CSR, dz, w_rel):
             """Sᵀ (dZ W_rel), S = dst x src, in the cheaper association."""
-            if _src_first(S, dz.shape[1], w_rel.shape[1], 2 if bf16 else 4):
-                St = A if S is AT else AT
-                return spmm_forward(St, dz) @ w_rel
             St = A if S is AT else AT
+            if _src_first(S, dz.shape[1], w_rel.shape[1], esz):
+                return spmm_forward(St, dz) @ w_rel
             return spmm_forward(St, dz @ w_rel)
 
         g_l = g_r = None
-        if need[0]:  # left = src of left2right (S = A^T), dst of right2left
-            g_l = src_grad(AT, dz_r, w_rel_l2r)
-            g_l.addmm_(dz_l, w_root_r2l)
         if need[1]:  # right = src of right2left (S = A), dst of left2right
             g_r = src_grad(A, dz_l, w_rel_r2l)
             g_r.addmm_(dz_r, w_root_l2r)
+        if need[0]:  # left = src of left2right (S = A^T), dst of right2left
+            if t_l2r is not None:
+                main.wait_stream(side)
+                t_l2r.record_stream(main)
+                g_l = torch.addmm(dz_l @ w_root_r2l, t_l2r, w_rel_l2r)
+            else:
+                g_l = src_grad(AT, dz_r, w_rel_l2r)
+                g_l.addmm_(dz_l, w_root_r2l)
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 
