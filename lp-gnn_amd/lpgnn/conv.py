@@ -128,13 +128,19 @@ class _TwoDirection(torch.autograd.Function):
         main = torch.cuda.current_stream(dz_r.device)
         side = _side_stream(dz_r.device) if _OVERLAP else None
         esz = 2 if bf16 else 4
-        # left2right source gradient: when the SpMM comes first it only needs dZ_r -- start it
-        # on the side stream so it streams HBM under the weight-gradient GEMMs
+        # left2right source gradient: when the SpMM comes first, T = S^T dZ_r (S = A^T, so
+        # T = A dZ_r) only needs dZ_r -- start it on the side stream so it streams HBM under
+        # the weight-gradient GEMMs.  T also gives lin_rel's weight gradient over the smaller
+        # node set: dZ_r^T (A^T left) = T^T left.
         t_l2r = None
-        if need[0] and side is not None and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], esz):
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
+        if need[0] and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], esz):
+            if side is not None:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    t_l2r = spmm_forward(A, dz_r)
+            else:
                 t_l2r = spmm_forward(A, dz_r)
+        rel_from_t = t_l2r is not None and AT.n_cols < AT.n_rows and need[3]
 
         def wgrads(dz, agg, x_dst, need_rel, need_root):
             if not (need_rel or need_root):
@@ -147,7 +153,7 @@ class _TwoDirection(torch.autograd.Function):
                 d_root = (dz.t() @ x_dst).float() if need_root else None
             return (d_rel if need_rel else None), (d_root if need_root else None)
 
-        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r, right, need[3], need[5])
+        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r, right, need[3] and not rel_from_t, need[5])
         dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
 
         def src_grad(S: CSR, dz, w_rel):
@@ -163,9 +169,13 @@ class _TwoDirection(torch.autograd.Function):
             g_r.addmm_(dz_r, w_root_l2r)
         if need[0]:  # left = src of left2right (S = A^T), dst of right2left
             if t_l2r is not None:
-                main.wait_stream(side)
-                t_l2r.record_stream(main)
-                g_l = torch.addmm(dz_l @ w_root_r2l, t_l2r, w_rel_l2r)
+                root = dz_l @ w_root_r2l
+                if side is not None:
+                    main.wait_stream(side)
+                    t_l2r.record_stream(main)
+                if rel_from_t:
+                    dw_rel_l2r = (t_l2r.t() @ left).float()
+                g_l = torch.addmm(root, t_l2r, w_rel_l2r)
             else:
                 g_l = src_grad(AT, dz_r, w_rel_l2r)
                 g_l.addmm_(dz_l, w_root_r2l)

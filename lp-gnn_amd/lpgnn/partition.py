@@ -435,14 +435,17 @@ class _PartTwoDirection(torch.autograd.Function):
                 g_r = spmm_forward(AT, dz_l @ w_rel_r2l)
         g_right_own = red.finish()
         dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
-        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r[:n_own], right[:n_own], need[3], need[5])
+        # with T = A bcast(dZ_r) (computed for left's gradient below), lin_rel's weight gradient
+        # dZ_r^T reduce(A^T left) = T^T left runs over the local constraints instead of the variables
+        first = need[0] and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], 4)
+        rel_from_t = first and A.n_rows < ex.n_own and need[3]
+        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r[:n_own], right[:n_own], need[3] and not rel_from_t, need[5])
         if need[1]:  # ... and as the destination of left2right (owned rows)
             g_r[:n_own].addmm_(dz_r, w_root_l2r)
 
         g_l = None
         if need[0]:  # left: source of left2right through reduce(AT @ left)[:n_own]
             f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
-            first = _src_first(AT, f_out, f_in, 4)
             full = torch.empty((right.shape[0], f_out if first else f_in), dtype=torch.float32, device=left.device)
             if first:
                 full[:n_own] = dz_r
@@ -452,7 +455,10 @@ class _PartTwoDirection(torch.autograd.Function):
             root = dz_l @ w_root_r2l                 # ... under the root-path gradient of left
             bc.finish()
             if first:
-                g_l = torch.addmm(root, spmm_forward(A, full), w_rel_l2r)
+                t = spmm_forward(A, full)
+                if rel_from_t:
+                    dw_rel_l2r = t.t() @ left
+                g_l = torch.addmm(root, t, w_rel_l2r)
             else:
                 g_l = spmm_forward(A, full).add_(root)
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
