@@ -112,9 +112,10 @@ lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  * Linear (heads lin_left / lin_right, arch.py:175-176, 190).
  * flags: bit 0 = ReLU epilogue (arch.py:182, 188).  bias may be NULL.
  * dropout_p > 0 fuses F.dropout after the ReLU (arch.py:186-188, training):
- * element (m, n) is kept iff a counter-based hash of (seed, m*N + n) is >=
- * dropout_p * 2^32, and kept values are scaled by 1 / (1 - dropout_p).  The
- * mask is never stored: the kept set is exactly where the output is > 0.
+ * element (m, n) is kept iff a counter-based hash of (seed, m, n) (two
+ * rounds of the 32-bit lowbias32 mix) is >= dropout_p * 2^32, and kept
+ * values are scaled by 1 / (1 - dropout_p).  The mask is never stored: the
+ * kept set is exactly where the output is > 0.
  * Row-major fp32, leading dimensions in floats; K1, K2 and the A/W leading
  * dimensions multiples of 4, A/W 16-byte aligned.
  * Numerics (bitwise reproducible, see oracle/fc_ref.c): each part (A1 over
