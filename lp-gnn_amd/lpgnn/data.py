@@ -130,6 +130,35 @@ class MyToBipartite:
                               y_t=batch.y[is_vars], edge_index=adj, bs=bs, s_bs=bs - t_bs, t_bs=t_bs, **extra)
 
 
+def bipartite_from_lp(row, col, A_data, c_feas, v_feas, y_s, y_t, device, **aux) -> BipartiteBatch:
+    """LPDataset.get + MyToBipartite without the detour.
+
+    The reference symmetrises the LP's edge list (to_undirected, dataset.py:252),
+    relabels it and keeps only the cons->var half again (dataset.py:296-304).
+    For a coalesced LP matrix -- one entry per (row, col), which scipy's CSR
+    and the msgpack records hold -- that round trip returns the original
+    entries, so the dual CSR is packed straight from (row, col, value) on
+    `device` (one device sort, no host coalesce over 2·nnz edges).  The result
+    equals the reference chain attribute for attribute (tests/test_lpio.py);
+    an LP with duplicate entries takes the reference chain, which sums them.
+    """
+    A_data = np.asarray(A_data)
+    c_feas, v_feas = np.asarray(c_feas), np.asarray(v_feas)
+    assert A_data.max() <= 1 and A_data.min() >= -1  # dataset.py:235-236
+    assert c_feas.max() <= 1 and c_feas.min() >= -1  # dataset.py:237-238
+    m, n = c_feas.shape[0], v_feas.shape[0]
+    try:
+        adj = BipartiteCSR.from_coo(np.asarray(row, np.int64), np.asarray(col, np.int64),
+                                    A_data.astype(np.float32), m, n, device=device)
+    except RuntimeError as e:
+        if "duplicate" not in str(e):
+            raise
+        return MyToBipartite(dev=device)(lp_to_unipartite(row, col, A_data, c_feas, v_feas, y_s, y_t, **aux))
+    t = lambda a: torch.as_tensor(np.asarray(a))
+    return BipartiteBatch(x_s=t(c_feas), x_t=t(v_feas), y_s=t(y_s), y_t=t(y_t), edge_index=adj, bs=m + n,
+                          s_bs=m, t_bs=n, **aux)
+
+
 def batch_to(batch, dev, half: bool = False):
     """utils.py:909-915."""
     for nm in ("x_s", "x_t", "y_s", "y_t"):

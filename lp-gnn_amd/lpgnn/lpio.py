@@ -223,3 +223,13 @@ def load_processed(path, device="cpu", thresh_num=np.inf):
     data = lp_to_unipartite(row, col, A_data, c_feas, v_feas, y_s, y_t, processed_path=str(path))
     assert data.num_nodes == int(nnodes)
     return MyToBipartite(dev=device, thresh_num=thresh_num)(data)
+
+
+def load_bipartite(path, device="cpu"):
+    """load_processed without the to_undirected / split round trip: the .pk
+    record straight to a BipartiteBatch (data.bipartite_from_lp)."""
+    from .data import bipartite_from_lp
+
+    row, col, A_data, c_feas, v_feas, y_s, y_t, nnodes = msgpack_load(path)
+    assert int(nnodes) == np.asarray(c_feas).shape[0] + np.asarray(v_feas).shape[0]
+    return bipartite_from_lp(row, col, A_data, c_feas, v_feas, y_s, y_t, device, processed_path=str(path))

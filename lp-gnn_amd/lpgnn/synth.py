@@ -34,7 +34,9 @@ class LPGraph:
 
 
 def _distinct_cols_per_row(rng, m: int, n: int, deg: int) -> np.ndarray:
-    """[m, deg] column ids, distinct within each row, sorted."""
+    """[m, deg] column ids, distinct within each row, sorted (rejection
+    sampling: meant for deg^2 << n, where a row is duplicate-free with
+    probability ~exp(-deg^2 / 2n))."""
     cols = np.sort(rng.integers(0, n, size=(m, deg), dtype=np.int64), axis=1)
     while True:
         dup = (np.diff(cols, axis=1) == 0).any(axis=1)
@@ -97,7 +99,7 @@ def skewed_lp(m: int, n: int, nnz: int, a: float = 1.5, seed: int = 0) -> LPGrap
     order = np.argsort(d)
     for deg in np.unique(d):
         ids = order[d[order] == deg]
-        if deg * 4 < n:
+        if deg * deg < 2 * n:  # rejection sampling only where a row is likely duplicate-free (birthday bound)
             c = _distinct_cols_per_row(rs, len(ids), n, int(deg))
         else:
             c = np.stack([np.sort(rs.choice(n, int(deg), replace=False)) for _ in ids])

@@ -224,3 +224,20 @@ def test_full_size_c2_sampled_rows_and_linearity():
         rs = spmm_forward(csr, ones)[:, 0].double().cpu().numpy()
         exact = np.add.reduceat(np.concatenate([v.astype(np.float64), [0]]), rp[:-1]) * (np.diff(rp) > 0)
         np.testing.assert_allclose(rs, exact, atol=1e-4)
+
+
+def test_direct_bipartite_device_pack_equals_reference_chain():
+    """bipartite_from_lp on the GPU == MyToBipartite(lp_to_unipartite(...)) (the reference chain)."""
+    from lpgnn import synth
+    from lpgnn.data import MyToBipartite, bipartite_from_lp, lp_to_unipartite
+
+    g = synth.skewed_lp(3000, 5000, 40000, seed=3)
+    args = (g.row, g.col, g.val, g.x_s, g.x_t, g.y_s, g.y_t)
+    a = MyToBipartite(dev=DEV)(lp_to_unipartite(*args))
+    b = bipartite_from_lp(*args, device=DEV)
+    for k in ("x_s", "x_t", "y_s", "y_t"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    for o in ("fwd", "bwd"):
+        ca, cb = getattr(a.edge_index, o), getattr(b.edge_index, o)
+        for f in ("rowptr", "col", "val"):
+            assert torch.equal(getattr(ca, f), getattr(cb, f)), (o, f)

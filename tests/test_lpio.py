@@ -74,3 +74,35 @@ def test_raw_to_processed_to_bipartite(tmp_path, golden_dir):
     assert torch.equal(batch.y_s, torch.from_numpy(r["y_s"])) and (batch.s_bs, batch.t_bs) == (r["s_bs"], r["t_bs"])
     for a, b in zip((batch.edge_index.fwd.rowptr, batch.edge_index.fwd.col, batch.edge_index.fwd.val), r["A"]):
         assert np.array_equal(a.numpy(), b)
+
+
+def test_direct_bipartite_equals_reference_chain(tmp_path, golden_dir):
+    """load_bipartite (no to_undirected round trip) == load_processed (the
+    reference chain) attribute for attribute, host pack."""
+    from lpgnn import lpio
+
+    g = dict(np.load(f"{golden_dir}/features_small.npz"))
+    i = 1
+    m, n = int(g[f"m_{i}"]), int(g[f"n_{i}"])
+    rng = np.random.default_rng(1)
+    rec = [g[f"out_row_{i}"], g[f"out_col_{i}"], g[f"out_data_{i}"].astype(np.float32),
+           g[f"c_feas_{i}"].astype(np.float32), g[f"v_feas_{i}"].astype(np.float32),
+           rng.integers(0, 3, m), rng.integers(0, 3, n), m + n]
+    p = tmp_path / "p.pk"
+    lpio.msgpack_dump(rec, p)
+    a, b = lpio.load_processed(p), lpio.load_bipartite(p)
+    for k in ("x_s", "x_t", "y_s", "y_t"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert (a.s_bs, a.t_bs, a.bs) == (b.s_bs, b.t_bs, b.bs)
+    for o in ("fwd", "bwd"):
+        ca, cb = getattr(a.edge_index, o), getattr(b.edge_index, o)
+        for f in ("rowptr", "col", "val"):
+            assert torch.equal(getattr(ca, f), getattr(cb, f)), (o, f)
+    # duplicate entries take the reference chain (summed by to_undirected)
+    rec2 = list(rec)
+    rec2[0] = np.r_[rec[0], rec[0][:1]]
+    rec2[1] = np.r_[rec[1], rec[1][:1]]
+    rec2[2] = np.r_[rec[2], rec[2][:1]]
+    lpio.msgpack_dump(rec2, p)
+    c = lpio.load_bipartite(p)
+    assert c.edge_index.nnz() == a.edge_index.nnz()

@@ -5,6 +5,7 @@
 fc   : lpg_fc_f32 at the c2 shapes vs torch (hipBLASLt) linear+linear+add+relu
 fcpmc: only the two hidden-layer FC kernels (fp32 c2 and bf16 c5 shapes), for PMC passes
 bf16 : lpg_fc_bf16 at the c5 shape vs torch bf16 (hipBLASLt)
+load : graph load at c2 -- reference chain (to_undirected + MyToBipartite + device pack) vs direct pack
 spmm : lpg_spmm_f32 at c2, both directions, slice widths 256/512/1024
 bwd  : the FC backward GEMMs at c2 shapes through torch (hipBLASLt)
 """
@@ -161,11 +162,40 @@ def bench_bf16(out):
         out[f"bf16 M={M} K=4096 {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * 4096 / v / 1e9)
 
 
+def bench_load(out):
+    import time
+
+    from lpgnn import synth
+    from lpgnn.data import MyToBipartite, bipartite_from_lp, lp_to_unipartite
+
+    g = synth.uniform_lp(100_000, 200_000, 2_000_000, seed=0)
+    args = (g.row, g.col, g.val, g.x_s, g.x_t, g.y_s, g.y_t)
+
+    def ref():
+        return MyToBipartite(dev="cuda")(lp_to_unipartite(*args))
+
+    def direct():
+        return bipartite_from_lp(*args, device="cuda")
+
+    for name, fn in (("reference chain (host to_undirected + relabel, device pack)", ref),
+                     ("direct (device pack of the LP entries)", direct)):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        out[f"load c2 {name}"] = dict(ms=float(np.median(ts)) * 1e3)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["fc", "spmm", "bwd"]
     out = {}
     for w in which:
-        {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16}[w](out)
+        {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
+         "load": bench_load}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
