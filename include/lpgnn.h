@@ -215,6 +215,10 @@ lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t ldl, const f
  * Smaller slices keep the gathered source slice resident in the 256 MiB
  * Infinity Cache; see DESIGN.md. */
 lpg_status lpg_spmm_set_slice(int64_t cols_per_slice);
+/* Tuning knob: edges gathered ahead per wave in the wide fp32 kernel (8, 16,
+ * 32; 0 = auto).  Results are bitwise identical for every setting (the
+ * accumulation order does not change). */
+lpg_status lpg_spmm_set_depth(int64_t edges);
 
 /* ---- k-hop neighbour sampling (NeighborLoader collate, train.py:111-116,
  * val.py:22-27; replaces torch_sparse 0.6.12 neighbor_sample) -------------

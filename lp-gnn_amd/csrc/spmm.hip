@@ -269,6 +269,7 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
 }
 
 int64_t g_slice_cols = 0;  // lpg_spmm_set_slice; 0 = auto
+int g_depth = 0;           // lpg_spmm_set_depth: edges gathered ahead per wave (0 = auto)
 
 lpg_status check_csr(const lpg_csr *A) {
   LPG_REQUIRE(A != nullptr, "lpg_spmm: A is NULL");
@@ -332,6 +333,13 @@ extern "C" lpg_status lpg_spmm_set_slice(int64_t cols) {
   return LPG_OK;
 }
 
+extern "C" lpg_status lpg_spmm_set_depth(int64_t edges) {
+  LPG_REQUIRE(edges == 0 || edges == 8 || edges == 16 || edges == 32,
+              "lpg_spmm_set_depth: %lld not in {0, 8, 16, 32}", (long long)edges);
+  g_depth = (int)edges;
+  return LPG_OK;
+}
+
 extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
                                    int64_t F, void *stream) {
   lpg_status st = check_csr(A);
@@ -363,8 +371,16 @@ extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx
   // gathered at a time and stays resident in the 256 MiB Infinity Cache;
   // measured ~3 % faster than full-width rows at c2 (profiles/r01_kbench*).
   if (W == 0) W = 256;
-  if (W == 256) return launch_wide_f32<1, 8>(A, X, ldx, Y, ldy, F, s);
-  if (W == 512) return launch_wide_f32<2, 8>(A, X, ldx, Y, ldy, F, s);
+  const int U = g_depth == 0 ? 8 : g_depth;
+  if (W == 256) {
+    if (U == 16) return launch_wide_f32<1, 16>(A, X, ldx, Y, ldy, F, s);
+    if (U == 32) return launch_wide_f32<1, 32>(A, X, ldx, Y, ldy, F, s);
+    return launch_wide_f32<1, 8>(A, X, ldx, Y, ldy, F, s);
+  }
+  if (W == 512) {
+    if (U == 16) return launch_wide_f32<2, 16>(A, X, ldx, Y, ldy, F, s);
+    return launch_wide_f32<2, 8>(A, X, ldx, Y, ldy, F, s);
+  }
   return launch_wide_f32<4, 4>(A, X, ldx, Y, ldy, F, s);
 }
 

@@ -99,22 +99,33 @@ def bench_spmm(out):
     from lpgnn import BipartiteCSR, _lib, synth
     from lpgnn.sparse import spmm_forward
 
-    g = synth.uniform_lp(100_000, 200_000, 2_000_000, seed=0)
-    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
     L = _lib.lib()
+    for gname, g in (("uniform", synth.uniform_lp(100_000, 200_000, 2_000_000, seed=0)),
+                     ("skewed", synth.skewed_lp(100_000, 200_000, 2_000_000, seed=0))):
+        _spmm_graph(out, L, gname, g, spmm_forward, BipartiteCSR)
+
+
+def _spmm_graph(out, L, gname, g, spmm_forward, BipartiteCSR):
+    """c2-sized graph (uniform rows, or Zipf(1.5) row degrees -- SURVEY.md 8d's load-balance variant)."""
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
     for name, csr, K in (("cons<-vars", adj.fwd, g.n), ("vars<-cons", adj.bwd, g.m)):
         X = torch.randn(K, 1024, device="cuda")
         fns = {}
-        for sl in (1024, 512, 256):
-            def f(sl=sl):
+        ref = spmm_forward(csr, X)
+        for sl, u in ((1024, 0), (512, 8), (512, 16), (256, 8), (256, 16), (256, 32)):
+            def f(sl=sl, u=u):
                 L.lpg_spmm_set_slice(sl)
+                L.lpg_spmm_set_depth(u)
                 return spmm_forward(csr, X)
-            fns[f"slice{sl}"] = f
+            assert torch.equal(f(), ref)
+            fns[f"slice{sl} depth{u}"] = f
         t = timeit(fns)
         L.lpg_spmm_set_slice(0)
+        L.lpg_spmm_set_depth(0)
         B = g.nnz * 1024 * 4 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 1024 * 4
         for k, v in t.items():
-            out[f"spmm {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000)
+            out[f"spmm {gname} {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000,
+                                                   max_deg=int(csr.degrees().max().item()))
 
 
 def bench_fcpmc(out):
