@@ -31,6 +31,7 @@ namespace lpg {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int NB = 32;  // numerics block: k-tile length of one fma chain (the parity contract)
 
@@ -447,6 +448,19 @@ __device__ __forceinline__ void load_row_k(float (&x)[K > 0 ? K : 1], const floa
 template <int K1, int K2, bool RELU>
 __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
   static_assert(K1 % 4 == 0 && K2 % 4 == 0 && K1 >= 4, "small-K kernel: K1, K2 multiples of 4");
+  constexpr int KT = K1 + K2;
+  // the block's rows of [A1 | A2] staged once in LDS (coalesced), so the row
+  // loop never waits on a global load; every lane then reads the same row
+  // values (LDS broadcast)
+  __shared__ __attribute__((aligned(16))) float sx[kSmallKRows * KT];
+  const int64_t r0 = (int64_t)blockIdx.x * kSmallKRows;
+  const int64_t r1 = r0 + kSmallKRows < a.M ? r0 + kSmallKRows : a.M;
+  for (int i = threadIdx.x; i < kSmallKRows * KT; i += 256) {
+    const int r = i / KT, k = i % KT;
+    const int64_t m = r0 + r < r1 ? r0 + r : r1 - 1;  // rows past r1 are never stored
+    sx[i] = k < K1 ? a.A1[m * a.lda1 + k] : a.A2[m * a.lda2 + (k - K1)];
+  }
+  __syncthreads();
   const int64_t c = (int64_t)blockIdx.y * 1024 + (int64_t)threadIdx.x * 4;
   if (c >= a.N) return;
   float w1[4][K1], w2[4][K2 > 0 ? K2 : 1], b[4];
@@ -456,36 +470,35 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
     load_row_k<K2>(w2[j], a.W2, a.ldw2, c + j);
     b[j] = a.bias ? a.bias[c + j] : 0.f;
   }
-  const int64_t r0 = (int64_t)blockIdx.x * kSmallKRows;
-  const int64_t r1 = r0 + kSmallKRows < a.M ? r0 + kSmallKRows : a.M;
-  for (int64_t m0 = r0; m0 < r1; m0 += 4) {
-    float x1[4][K1], x2[4][K2 > 0 ? K2 : 1];
+  f32x2 wp1[2][K1], wp2[2][K2 > 0 ? K2 : 1];  // column pairs (0,1), (2,3), packed once
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // rows past r1 re-read row r1 - 1 (never stored)
-      const int64_t m = m0 + u < r1 ? m0 + u : r1 - 1;
-      load_row_k<K1>(x1[u], a.A1, a.lda1, m);
-      load_row_k<K2>(x2[u], a.A2, a.lda2, m);
-    }
+  for (int jp = 0; jp < 2; ++jp) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t m = m0 + u;
-      float o[4];
+    for (int k = 0; k < K1; ++k) wp1[jp][k] = f32x2{w1[2 * jp][k], w1[2 * jp + 1][k]};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float p1 = 0.f;
+    for (int k = 0; k < K2; ++k) wp2[jp][k] = f32x2{w2[2 * jp][k], w2[2 * jp + 1][k]};
+  }
+  for (int64_t m = r0; m < r1; ++m) {
+    const float *xr = sx + (m - r0) * KT;
+    float o[4];
+    // columns in pairs: one v_pk_fma_f32 advances two independent chains
+    // (a true fma per element -- the same bits as the scalar chains)
 #pragma unroll
-        for (int k = 0; k < K1; ++k) p1 = __builtin_fmaf(x1[u][k], w1[j][k], p1);
-        float t = 0.f + p1;
-        if (K2 > 0) {
-          float p2 = 0.f;
+    for (int j = 0; j < 4; j += 2) {
+      f32x2 p1 = {0.f, 0.f};
 #pragma unroll
-          for (int k = 0; k < K2; ++k) p2 = __builtin_fmaf(x2[u][k], w2[j][k], p2);
-          t = t + p2;
-        }
-        o[j] = epilogue(a, t, b[j], m, c + j, RELU);
+      for (int k = 0; k < K1; ++k) p1 = __builtin_elementwise_fma(f32x2{xr[k], xr[k]}, wp1[j / 2][k], p1);
+      f32x2 t = f32x2{0.f, 0.f} + p1;
+      if (K2 > 0) {
+        f32x2 p2 = {0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < K2; ++k) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[j / 2][k], p2);
+        t = t + p2;
       }
-      if (m < r1) *reinterpret_cast<float4 *>(a.C + m * a.ldc + c) = make_float4(o[0], o[1], o[2], o[3]);
+      o[j] = epilogue(a, t[0], b[j], m, c + j, RELU);
+      o[j + 1] = epilogue(a, t[1], b[j + 1], m, c + j + 1, RELU);
     }
+    *reinterpret_cast<float4 *>(a.C + m * a.ldc + c) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
 
