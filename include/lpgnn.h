@@ -110,7 +110,11 @@ lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  * torch Linear layout [out, in] (A1 = agg, W1 = lin_rel.weight, bias =
  * lin_rel.bias, A2 = x_dst, W2 = lin_root.weight).  With K2 = 0 it is a plain
  * Linear (heads lin_left / lin_right, arch.py:175-176, 190).
- * flags: bit 0 = ReLU epilogue (arch.py:182, 188).  bias may be NULL.
+ * flags: bit 0 = ReLU epilogue (arch.py:182, 188); bit 1 = accumulate: C
+ * holds an addend P on entry and C = act(A1 W1^T + A2 W2^T + P + bias), in
+ * place (GraphConv re-associated as lin_root(x_dst) + S (x_src W_rel^T) + b,
+ * with S (x_src W_rel^T) computed by lpg_fc_f32 + lpg_spmm_f32 into C first).
+ * bias may be NULL.
  * dropout_p > 0 fuses F.dropout after the ReLU (arch.py:186-188, training):
  * element (m, n) is kept iff a counter-based hash of (seed, m, n) (two
  * rounds of the 32-bit lowbias32 mix) is >= dropout_p * 2^32, and kept
@@ -121,7 +125,8 @@ lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  * Numerics (bitwise reproducible, see oracle/fc_ref.c): each part (A1 over
  * K1, then A2 over K2) is cut into k-blocks of 32; a block's products form
  * one fp32 fma chain in k order from +0, the block sums are added in order
- * into the running total (+0 initially), then + bias, then ReLU. */
+ * into the running total (+0 initially), then + P (accumulate), then + bias,
+ * then ReLU. */
 lpg_status lpg_fc_f32(int64_t M, int64_t N,
                       int64_t K1, const float *A1, int64_t lda1, const float *W1, int64_t ldw1,
                       int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2,

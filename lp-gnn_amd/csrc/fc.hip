@@ -47,6 +47,9 @@ struct FcArgs {
   uint64_t seed;
   uint32_t drop_thresh;  // 0 = no dropout
   float drop_scale;
+  // flags bit 1: C holds an addend on entry, C = act(A1 W1^T + A2 W2^T + C + bias);
+  // each element is read and rewritten by the lane that owns it
+  int32_t accum;
 };
 
 // Counter-based dropout RNG over (seed, row, col): two rounds of the 32-bit
@@ -85,6 +88,27 @@ __device__ __forceinline__ float4 load_k4(const float *X, int64_t ld, int64_t R,
   const int64_t rr = r < R ? r : R - 1;
   const int64_t kk = k < K ? k : K - 4;
   return *reinterpret_cast<const float4 *>(X + rr * ld + kk);
+}
+
+// flags bit 1 (accumulate): acc[i][j][r] += C at the lane's 32x32-MFMA output
+// positions, every load issued before the first store (C is read and then
+// rewritten in place, so loads cannot be moved past stores by the compiler).
+// Rows/cols past the edge load a clamped in-range element (never stored).
+template <int TM, int TN, typename Acc>
+__device__ __forceinline__ void add_c32(const FcArgs &a, Acc (&acc)[TM][TN], int64_t mw, int64_t nw, int lane) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int64_t col = nw + j * 32 + (lane & 31);
+    col = col < a.N ? col : a.N - 1;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int64_t row = mw + i * 32 + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2);
+        row = row < a.M ? row : a.M - 1;
+        acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
+      }
+  }
 }
 
 // WAVES_M x WAVES_N waves, each owning TM x TN blocks of 32x32; BK = staging
@@ -211,6 +235,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32(FcArgs a) {
 
   // Epilogue: C/D map of the 32x32 MFMA: col = lane & 31,
   // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
+  if (a.accum) add_c32<TM, TN>(a, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int64_t col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
@@ -343,6 +368,21 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_m16(FcArgs 
     __syncthreads();
   }
 
+  if (a.accum) {  // addends first, all loads in flight before the first store
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int64_t col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
+      col = col < a.N ? col : a.N - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int64_t row = m0 + wm * TM * 16 + i * 16 + 4 * (lane >> 4) + r;
+          row = row < a.M ? row : a.M - 1;
+          acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
+        }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int64_t col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
@@ -495,6 +535,7 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
         for (int k = 0; k < K2; ++k) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[j / 2][k], p2);
         t = t + p2;
       }
+      if (a.accum) t = t + f32x2{a.C[m * a.ldc + c + j], a.C[m * a.ldc + c + j + 1]};
       o[j] = epilogue(a, t[0], b[j], m, c + j, RELU);
       o[j + 1] = epilogue(a, t[1], b[j + 1], m, c + j + 1, RELU);
     }
@@ -646,6 +687,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_glds(FcArgs
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
   }
+  if (a.accum) add_c32<TM, TN>(a, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
 
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -700,9 +742,9 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
               "lpg_fc_f32: K and leading dimensions must be multiples of 4 floats");
   LPG_REQUIRE(aligned16(A1) && aligned16(W1) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
               "lpg_fc_f32: A/W must be 16-byte aligned");
-  LPG_REQUIRE((flags & ~1) == 0, "lpg_fc_f32: unknown flags 0x%x", flags);
+  LPG_REQUIRE((flags & ~3) == 0, "lpg_fc_f32: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
-  FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f};
+  FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1};
   if (dropout_p > 0.f) {
     const double th = (double)dropout_p * 4294967296.0;
     a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);

@@ -18,8 +18,20 @@ autograd nodes cannot:
   constraints instead of the 200 K variables for left2right): the same
   product, one GEMM over half the rows.
 
-Gradients are tolerance-level (the reference's own backward is autograd
-through MKL); the forward is unchanged bit for bit.
+* a direction whose source side has fewer rows than its destination side
+  (c2 left2right: 100 K constraints -> 200 K variables) and does not widen
+  (f_out <= f_src) is evaluated re-associated, lin_rel(S x) = S (x W_rel^T):
+  the lin_rel GEMM runs over the source rows, the SpMM aggregates the product,
+  and the FC kernel adds lin_root + bias + ReLU onto it in place (lpg_fc_f32
+  accumulate flag).  Same product, one GEMM over half the rows; its
+  backward is the one the source-side gradient already uses (T = S^T dZ gives
+  lin_rel's weight gradient as T^T x_src).  ``REASSOCIATE = False``
+  (LPGNN_REASSOC=0) keeps the reference's association everywhere.
+
+Forward numerics are bitwise the oracle's kchain order with the same
+association rule (oracle/model_ref.py); logits stay within the north-star
+1e-4 of the reference's MKL evaluation either way.  Gradients are
+tolerance-level (the reference's own backward is autograd through MKL).
 """
 from __future__ import annotations
 
@@ -38,6 +50,7 @@ _SPMM_BYTES = 7e12
 # overlapped SpMM launches then share CUs and HBM with the FC and each takes ~2x longer, which
 # hides the kernel's own roofline fraction in the bench -- off by default.
 _OVERLAP = os.environ.get("LPGNN_OVERLAP", "0") == "1"
+REASSOCIATE = os.environ.get("LPGNN_REASSOC", "1") == "1"
 _SIDE = {}
 
 
@@ -51,6 +64,13 @@ def _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, p, seed, bf16):
     if bf16:
         return _fc.fc_forward_bf16(agg, w_rel, x_dst, w_root, b, relu, p, seed)
     return _fc.fc_forward(agg, w_rel, x_dst, w_root, b, relu, p, seed)
+
+
+def reassociate(n_src: int, n_dst: int, f_src: int, f_out: int, bf16: bool = False) -> bool:
+    """The association rule: lin_rel(S x) evaluated as S (x W_rel^T) iff the
+    source side is the smaller node set and the SpMM does not get wider
+    (never worse on either the GEMM or the SpMM); fp32 path only."""
+    return REASSOCIATE and not bf16 and n_src < n_dst and f_out <= f_src
 
 
 def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
@@ -72,21 +92,30 @@ class _TwoDirection(torch.autograd.Function):
         A, AT = adj.fwd, adj.bwd  # A: cons x vars (right2left), AT: vars x cons (left2right)
         seed_r = _fc._new_seed() if dropout > 0 else 0
         seed_l = _fc._new_seed() if dropout > 0 else 0
-        side = _side_stream(left.device) if _OVERLAP else None
-        # arch.py:75-77: right' = left2right((left, right), A^T)
-        agg_r = spmm_forward(AT, left)
+        f_out = ws[0].shape[0]
+        ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out, bf16)
+        ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out, bf16)
+
+        def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None):
+            if ra:  # S (x_src W_rel^T), then lin_root + bias + ReLU accumulated onto it in place
+                y = spmm_forward(S, _fc.fc_forward(x_src, w_rel, None, None, None, False))
+                return _fc.fc_forward(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None
+            agg = spmm_forward(S, x_src) if agg is None else agg
+            return _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, dropout, seed, bf16), agg
+
+        side = _side_stream(left.device) if _OVERLAP and not ra_l else None
+        agg_l = None
         if side is not None:  # right2left's HBM-bound SpMM beside left2right's MFMA-bound FC
             side.wait_stream(torch.cuda.current_stream(left.device))
             with torch.cuda.stream(side):
                 agg_l = spmm_forward(A, right)
-            right_new = _fc_fwd(agg_r, right, ws[0], b_l2r, ws[1], relu, dropout, seed_r, bf16)
+        # arch.py:75-77: right' = left2right((left, right), A^T)
+        right_new, agg_r = direction(AT, left, right, ws[0], b_l2r, ws[1], seed_r, ra_r)
+        if side is not None:
             torch.cuda.current_stream(left.device).wait_stream(side)
             agg_l.record_stream(torch.cuda.current_stream(left.device))
-        else:
-            right_new = _fc_fwd(agg_r, right, ws[0], b_l2r, ws[1], relu, dropout, seed_r, bf16)
-            # arch.py:78-80: left' = right2left((right, left), A)
-            agg_l = spmm_forward(A, right)
-        left_new = _fc_fwd(agg_l, left, ws[2], b_r2l, ws[3], relu, dropout, seed_l, bf16)
+        # arch.py:78-80: left' = right2left((right, left), A)
+        left_new, agg_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l)
         ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
         ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
         ctx.has_b = (b_l2r is not None, b_r2l is not None)
@@ -112,8 +141,9 @@ class _TwoDirection(torch.autograd.Function):
                 return _fc.relu_bwd_colsum_bf16(g, y, ctx.scale, want_db)
             return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
 
-        small = (not bf16 and ctx.relu and agg_r.shape[1] + right.shape[1] <= 16
-                 and agg_l.shape[1] + left.shape[1] <= 16 and right_new.shape[1] % 4 == 0)
+        small = (not bf16 and ctx.relu and agg_r is not None and agg_l is not None
+                 and agg_r.shape[1] + right.shape[1] <= 16 and agg_l.shape[1] + left.shape[1] <= 16
+                 and right_new.shape[1] % 4 == 0)
         if small and not (need[0] or need[1]):
             # conv1: the inputs are features -- weight and bias gradients straight from (g, y)
             g_r0 = torch.zeros_like(right_new) if g_right is None else g_right
@@ -131,57 +161,61 @@ class _TwoDirection(torch.autograd.Function):
         main = torch.cuda.current_stream(dz_r.device)
         side = _side_stream(dz_r.device) if _OVERLAP else None
         esz = 2 if bf16 else 4
-        # left2right source gradient: when the SpMM comes first, T = S^T dZ_r (S = A^T, so
-        # T = A dZ_r) only needs dZ_r -- start it on the side stream so it streams HBM under
-        # the weight-gradient GEMMs.  T also gives lin_rel's weight gradient over the smaller
-        # node set: dZ_r^T (A^T left) = T^T left.
-        t_l2r = None
-        if need[0] and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], esz):
-            if side is not None:
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    t_l2r = spmm_forward(A, dz_r)
-            else:
-                t_l2r = spmm_forward(A, dz_r)
-        rel_from_t = t_l2r is not None and AT.n_cols < AT.n_rows and need[3]
+
+        # Per direction (S = dst x src): T = S^T dZ serves the source-side gradient T W_rel when
+        # that association is cheaper, and lin_rel's weight gradient T^T x_src when the source
+        # side is the smaller node set (or the forward was re-associated and kept no S x_src).
+        # T only needs dZ -- on the side stream it streams HBM under the weight-gradient GEMMs.
+        def plan(S, St, dz, x_src, w_rel, agg, need_src, need_rel):
+            t_src = need_src and _src_first(S, dz.shape[1], w_rel.shape[1], esz)
+            rel_t = need_rel and (agg is None or (t_src and S.n_cols < S.n_rows))
+            T = None
+            if t_src or rel_t:
+                if side is not None:
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        T = spmm_forward(St, dz)
+                else:
+                    T = spmm_forward(St, dz)
+            return T, t_src, rel_t
+
+        t_r, tsrc_r, relt_r = plan(AT, A, dz_r, left, w_rel_l2r, agg_r, need[0], need[3])
+        t_l, tsrc_l, relt_l = plan(A, AT, dz_l, right, w_rel_r2l, agg_l, need[1], need[6])
 
         def wgrads(dz, agg, x_dst, need_rel, need_root):
             if not (need_rel or need_root):
                 return None, None
-            k = agg.shape[1] + x_dst.shape[1]
-            if not bf16 and k <= 16 and dz.shape[1] % 4 == 0:  # conv1: dZ read once
+            k = x_dst.shape[1] + (agg.shape[1] if agg is not None else 0)
+            if not bf16 and agg is not None and k <= 16 and dz.shape[1] % 4 == 0:  # conv1: dZ read once
                 d_rel, d_root = _fc.wgrad_smallk(dz, agg, x_dst)
             else:
                 d_rel = (dz.t() @ agg).float() if need_rel else None
                 d_root = (dz.t() @ x_dst).float() if need_root else None
             return (d_rel if need_rel else None), (d_root if need_root else None)
 
-        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r, right, need[3] and not rel_from_t, need[5])
-        dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
+        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r, right, need[3] and not relt_r, need[5])
+        dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6] and not relt_l, need[8])
+        if side is not None and (t_r is not None or t_l is not None):
+            main.wait_stream(side)
+            for t in (t_r, t_l):
+                if t is not None:
+                    t.record_stream(main)
+        if relt_r:
+            dw_rel_l2r = (t_r.t() @ left).float()
+        if relt_l:
+            dw_rel_r2l = (t_l.t() @ right).float()
 
-        def src_grad(S: CSR, dz, w_rel):
-            """Sᵀ (dZ W_rel), S = dst x src, in the cheaper association."""
-            St = A if S is AT else AT
-            if _src_first(S, dz.shape[1], w_rel.shape[1], esz):
-                return spmm_forward(St, dz) @ w_rel
-            return spmm_forward(St, dz @ w_rel)
+        def src_grad(St, dz, w_rel, T, t_src):
+            """S^T (dZ W_rel) in the cheaper association."""
+            return T @ w_rel if t_src else spmm_forward(St, dz @ w_rel)
 
         g_l = g_r = None
         if need[1]:  # right = src of right2left (S = A), dst of left2right
-            g_r = src_grad(A, dz_l, w_rel_r2l)
+            g_r = src_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l)
             g_r.addmm_(dz_r, w_root_l2r)
         if need[0]:  # left = src of left2right (S = A^T), dst of right2left
-            if t_l2r is not None:
-                root = dz_l @ w_root_r2l
-                if side is not None:
-                    main.wait_stream(side)
-                    t_l2r.record_stream(main)
-                if rel_from_t:
-                    dw_rel_l2r = (t_l2r.t() @ left).float()
-                g_l = torch.addmm(root, t_l2r, w_rel_l2r)
-            else:
-                g_l = src_grad(AT, dz_r, w_rel_l2r)
-                g_l.addmm_(dz_l, w_root_r2l)
+            g_l = src_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r)
+            g_l.addmm_(dz_l, w_root_r2l)
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 

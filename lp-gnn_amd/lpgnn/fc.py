@@ -47,7 +47,10 @@ def _pad_k(t: Tensor) -> Tensor:
 
 
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
-               relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None) -> Tensor:
+               relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
+               accumulate: bool = False) -> Tensor:
+    """act(A1 W1^T + A2 W2^T [+ out] + bias) through lpg_fc_f32; with
+    ``accumulate`` the caller's ``out`` holds the addend and is overwritten."""
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -61,16 +64,19 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
         if out.shape != (M, N) or out.dtype != torch.float32 or out.stride(1) != 1 or out.device != A1.device:
             raise RuntimeError("lpgnn FC: `out` must be a float32 [M, N] row-major view on the same device")
         C = out
+    elif accumulate:
+        raise RuntimeError("lpgnn FC: accumulate needs the addend in `out`")
     else:
         C = torch.empty((M, N), dtype=torch.float32, device=A1.device)
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
+    flags = (1 if relu else 0) | (2 if accumulate else 0)
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
         st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
                           K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
                           None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
-                          None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), 1 if relu else 0,
+                          None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags,
                           float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_f32")

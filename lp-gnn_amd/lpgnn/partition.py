@@ -218,6 +218,7 @@ class Exchange:
 
     def __init__(self, plan: PartitionPlan, device, group=None):
         self.n_own, self.n_local = plan.n_own, plan.n_local
+        self.m, self.n = plan.m, plan.n  # global sizes: rank-independent layout decisions
         self.send_idx = torch.from_numpy(plan.send_idx).to(device)
         self.recv_idx = torch.from_numpy(plan.recv_idx).to(device)
         self.send_counts, self.recv_counts = list(plan.send_counts), list(plan.recv_counts)
@@ -358,11 +359,15 @@ class _PartTwoDirection(torch.autograd.Function):
     mirrors it: the halo-row gradients of right' are reduced to their owners,
     the aggregate gradient of the owned rows is broadcast back before the
     transposed SpMM.  Gradient sums go through addmm_ as in the one-GPU node.
+    left2right follows conv.py's association rule (on the global node counts):
+    re-associated, the reduced partials are those of A^T (left W_rel^T) and the
+    owners' lin_root + bias + ReLU is accumulated onto them in place.
     """
 
     @staticmethod
     def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
         from . import fc as _fc
+        from .conv import reassociate
         from .sparse import spmm_forward
 
         if dropout > 0 and not relu:
@@ -374,14 +379,25 @@ class _PartTwoDirection(torch.autograd.Function):
         n_own = ex.n_own
         seed_r = _fc._new_seed() if dropout > 0 else 0
         seed_l = _fc._new_seed() if dropout > 0 else 0
-        agg_r = spmm_forward(AT, left)              # partials for [owned | halo]
+        # conv.py's association rule on the GLOBAL node counts (every rank decides alike, so the
+        # reduced rows have the same width everywhere)
+        ra = reassociate(ex.m, ex.n, left.shape[1], w_rel_l2r.shape[0])
+        if ra:  # partials of A^T (left W_rel^T) for [owned | halo]
+            agg_r = spmm_forward(AT, _fc.fc_forward(left, w_rel_l2r, None, None, None, False))
+        else:
+            agg_r = spmm_forward(AT, left)          # partials for [owned | halo]
         red = ex.start_reduce(agg_r, inplace=True)  # halo partials -> owners, in flight ...
         agg_l = spmm_forward(A, right)              # ... under the purely local constraint side
         left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l)
         red.finish()                                # owners' rows of agg_r now hold the full sums
-        right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
-        _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
-                       out=right_new[:n_own])
+        if ra:  # lin_root + bias + ReLU accumulated onto the owners' sums, in place
+            right_new, agg_r = agg_r, None
+            _fc.fc_forward(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
+                           out=right_new[:n_own], accumulate=True)
+        else:
+            right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
+            _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
+                           out=right_new[:n_own])
         ex.start_broadcast_(right_new).finish()
         ctx.padj, ctx.relu = padj, relu
         ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
@@ -417,7 +433,7 @@ class _PartTwoDirection(torch.autograd.Function):
         def wgrads(dz, agg, x_dst, need_rel, need_root):
             if not (need_rel or need_root):
                 return None, None
-            if agg.shape[1] + x_dst.shape[1] <= 16 and dz.shape[1] % 4 == 0:
+            if agg is not None and agg.shape[1] + x_dst.shape[1] <= 16 and dz.shape[1] % 4 == 0:
                 d_rel, d_root = _fc.wgrad_smallk(dz, agg.contiguous(), x_dst.contiguous())
             else:
                 d_rel = dz.t() @ agg if need_rel else None
@@ -437,28 +453,32 @@ class _PartTwoDirection(torch.autograd.Function):
         dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
         # with T = A bcast(dZ_r) (computed for left's gradient below), lin_rel's weight gradient
         # dZ_r^T reduce(A^T left) = T^T left runs over the local constraints instead of the variables
+        # (and is the only route when the forward was re-associated: agg_r was not kept)
         first = need[0] and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], 4)
-        rel_from_t = first and A.n_rows < ex.n_own and need[3]
-        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r[:n_own], right[:n_own], need[3] and not rel_from_t, need[5])
+        rel_from_t = need[3] and (agg_r is None or (first and A.n_rows < ex.n_own))
+        use_t = first or rel_from_t
+        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, None if agg_r is None else agg_r[:n_own], right[:n_own],
+                                         need[3] and not rel_from_t, need[5])
         if need[1]:  # ... and as the destination of left2right (owned rows)
             g_r[:n_own].addmm_(dz_r, w_root_l2r)
 
         g_l = None
-        if need[0]:  # left: source of left2right through reduce(AT @ left)[:n_own]
+        if need[0] or use_t:  # left: source of left2right through reduce(AT @ left)[:n_own]
             f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
-            full = torch.empty((right.shape[0], f_out if first else f_in), dtype=torch.float32, device=left.device)
-            if first:
+            full = torch.empty((right.shape[0], f_out if use_t else f_in), dtype=torch.float32, device=left.device)
+            if use_t:
                 full[:n_own] = dz_r
             else:
                 torch.mm(dz_r, w_rel_l2r, out=full[:n_own])
             bc = ex.start_broadcast_(full)           # owners' aggregate gradient -> halo rows, in flight ...
-            root = dz_l @ w_root_r2l                 # ... under the root-path gradient of left
+            root = dz_l @ w_root_r2l if need[0] else None  # ... under the root-path gradient of left
             bc.finish()
-            if first:
+            if use_t:
                 t = spmm_forward(A, full)
                 if rel_from_t:
                     dw_rel_l2r = t.t() @ left
-                g_l = torch.addmm(root, t, w_rel_l2r)
+                if need[0]:
+                    g_l = torch.addmm(root, t, w_rel_l2r)
             else:
                 g_l = spmm_forward(A, full).add_(root)
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)

@@ -5,7 +5,8 @@
  * PyG 2.1 GraphConv after propagate, out = lin_rel(agg) + lin_root(x_dst)
  * (arch.py:57-62, 75-80), ReLU (arch.py:182, 188), and the heads
  * lin_left/lin_right (arch.py:190), evaluated in a fixed blocked k order
- * (see oracle_fc_f32) then + bias, then ReLU as (v < 0 ? 0 : v).  torch.nn.functional.linear on CPU (MKL) is the
+ * (see oracle_fc_f32) then + P (lpg_fc_f32's accumulate flag), then + bias,
+ * then ReLU as (v < 0 ? 0 : v).  torch.nn.functional.linear on CPU (MKL) is the
  * reference's own evaluation; it sums in an unspecified blocked order, so it
  * agrees with this chain to fp32 rounding only (tests report both).
  *
@@ -47,7 +48,7 @@ static void phase(const float *A, int64_t lda, const float *Wt, int64_t N, int64
 
 void oracle_fc_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1, const float *W1, int64_t ldw1,
                    int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2, const float *bias,
-                   float *C, int64_t ldc, int relu, int nthreads) {
+                   float *C, int64_t ldc, const float *P, int64_t ldp, int relu, int nthreads) {
   float *W1t = (float *)malloc(sizeof(float) * (size_t)(K1 * N + 1));
   float *W2t = (float *)malloc(sizeof(float) * (size_t)(K2 * N + 1));
   transpose(W1, ldw1, N, K1, W1t);
@@ -66,6 +67,8 @@ void oracle_fc_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t ld
       for (int64_t n = 0; n < N; ++n) c[n] = 0.0f;
       phase(A1, lda1, W1t, N, K1, m, c, part);
       phase(A2, lda2, W2t, N, K2, m, c, part);
+      if (P) /* accumulate flag: the re-associated GraphConv's S (x W_rel^T) */
+        for (int64_t n = 0; n < N; ++n) c[n] = c[n] + P[m * ldp + n];
       if (bias)
         for (int64_t n = 0; n < N; ++n) c[n] = c[n] + bias[n];
       if (relu)

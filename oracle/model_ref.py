@@ -56,8 +56,8 @@ def lib():
         L.oracle_spmm_bf16.argtypes = [i64, p, p, p, p, i64, i64, p, i64, ctypes.c_int]
         L.oracle_spmm_bf16.restype = None
         L.oracle_max_threads.restype = ctypes.c_int
-        L.oracle_fc_f32.argtypes = [i64, i64, i64, p, i64, p, i64, i64, p, i64, p, i64, p, p, i64, ctypes.c_int,
-                                    ctypes.c_int]
+        L.oracle_fc_f32.argtypes = [i64, i64, i64, p, i64, p, i64, i64, p, i64, p, i64, p, p, i64, p, i64,
+                                    ctypes.c_int, ctypes.c_int]
         L.oracle_fc_f32.restype = None
         _LIB = L
     return _LIB
@@ -95,13 +95,14 @@ def spmm_bf16(rowptr, col, val, Xbits, nthreads: int = 0) -> np.ndarray:
     return Y
 
 
-def fc_kchain(A1, W1, A2=None, W2=None, bias=None, relu=False, nthreads: int = 0) -> np.ndarray:
+def fc_kchain(A1, W1, A2=None, W2=None, bias=None, relu=False, nthreads: int = 0, add=None) -> np.ndarray:
     """lin_rel(A1) + lin_root(A2) [+ ReLU] as lpg_fc_f32 evaluates it: one
     fp32 fma chain per output in k order (A1 part then A2 part) from +0, then
-    + bias (fc_ref.c).  Arrays are numpy/torch fp32; weights [out, in]."""
+    + add (the accumulate flag's addend, [M, N]), then + bias (fc_ref.c).
+    Arrays are numpy/torch fp32; weights [out, in]."""
     f = lambda t: None if t is None else np.ascontiguousarray(
         t.detach().numpy() if isinstance(t, torch.Tensor) else t, dtype=np.float32)
-    A1, W1, A2, W2, bias = f(A1), f(W1), f(A2), f(W2), f(bias)
+    A1, W1, A2, W2, bias, add = f(A1), f(W1), f(A2), f(W2), f(bias), f(add)
     M, K1 = A1.shape
     N = W1.shape[0]
     K2 = 0 if A2 is None else A2.shape[1]
@@ -110,7 +111,7 @@ def fc_kchain(A1, W1, A2=None, W2=None, bias=None, relu=False, nthreads: int = 0
         z = np.zeros(1, np.float32)
         lib().oracle_fc_f32(M, N, K1, _ptr(A1), K1, _ptr(W1), K1, K2, _ptr(A2 if K2 else z), max(K2, 1),
                             _ptr(W2 if K2 else z), max(K2, 1), None if bias is None else _ptr(bias), _ptr(C), N,
-                            int(relu), nthreads)
+                            None if add is None else _ptr(add), N, int(relu), nthreads)
     return C
 
 
@@ -170,7 +171,14 @@ def spmm_t(csr, csr_t, X: torch.Tensor) -> torch.Tensor:
     return _OracleSpMM.apply(X, csr, csr_t)
 
 
-def graph_conv(x_src, x_dst, adj, adj_t, W_rel, b_rel, W_root, fc="mkl", relu=False):
+def reassociate(n_src: int, n_dst: int, f_src: int, f_out: int) -> bool:
+    """The association rule of lpgnn/conv.py restated: lin_rel(S x) is
+    evaluated as S (x W_rel^T) iff the source side has fewer rows than the
+    destination side and f_out <= f_src."""
+    return n_src < n_dst and f_out <= f_src
+
+
+def graph_conv(x_src, x_dst, adj, adj_t, W_rel, b_rel, W_root, fc="mkl", relu=False, reassoc=False):
     """PyG 2.1 GraphConv.forward with a SparseTensor adj_t (aggr='add'):
 
     out = propagate(...)      -> message_and_aggregate = matmul(adj_t, x[0], 'add')
@@ -180,7 +188,13 @@ def graph_conv(x_src, x_dst, adj, adj_t, W_rel, b_rel, W_root, fc="mkl", relu=Fa
     fc="mkl": torch CPU F.linear (the reference's own evaluation, autograd);
     fc="kchain": the bitwise order of lpg_fc_f32 (forward only).
     relu: the following ReLU (arch.py:182/188) applied here.
+    reassoc (kchain only): apply the association rule -- when it holds, the
+    HIP path's order: h = kchain(x_src W_rel^T), P = S h (spmm), then
+    kchain(x_dst W_root^T) + P + b_rel (returns agg = None).
     """
+    if fc == "kchain" and reassoc and reassociate(x_src.shape[0], x_dst.shape[0], x_src.shape[1], W_rel.shape[0]):
+        P = spmm_f32(*adj, fc_kchain(x_src, W_rel))
+        return torch.from_numpy(fc_kchain(x_dst, W_root, bias=b_rel, relu=relu, add=P)), None
     agg = spmm_t(adj, adj_t, x_src)
     if fc == "kchain":
         out = torch.from_numpy(fc_kchain(agg, W_rel, x_dst, W_root, b_rel, relu=relu))
@@ -190,7 +204,7 @@ def graph_conv(x_src, x_dst, adj, adj_t, W_rel, b_rel, W_root, fc="mkl", relu=Fa
     return (torch.relu(out) if relu else out), agg
 
 
-def conv_two_direction(sd, prefix, left, right, A, AT, fc="mkl", relu=False):
+def conv_two_direction(sd, prefix, left, right, A, AT, fc="mkl", relu=False, reassoc=False):
     """GraphConvTwoDirection.forward, arch.py:65-81.
 
     l2r, r2l = edge_index, edge_index.t(); l2r, r2l = r2l, l2r  (arch.py:71-74)
@@ -199,9 +213,11 @@ def conv_two_direction(sd, prefix, left, right, A, AT, fc="mkl", relu=False):
     """
     g = lambda d, k: sd[f"{prefix}.{d}.{k}"]
     right_new, agg_r = graph_conv(left, right, AT, A, g("left2right", "lin_rel.weight"),
-                                  g("left2right", "lin_rel.bias"), g("left2right", "lin_root.weight"), fc, relu)
+                                  g("left2right", "lin_rel.bias"), g("left2right", "lin_root.weight"), fc, relu,
+                                  reassoc)
     left_new, agg_l = graph_conv(right, left, A, AT, g("right2left", "lin_rel.weight"),
-                                 g("right2left", "lin_rel.bias"), g("right2left", "lin_root.weight"), fc, relu)
+                                 g("right2left", "lin_rel.bias"), g("right2left", "lin_root.weight"), fc, relu,
+                                 reassoc)
     return left_new, right_new, agg_l, agg_r
 
 
@@ -218,19 +234,21 @@ def add_knowledge(left_logit, right_logit, left_feas, right_feas, bound=10):
     return left_logit, right_logit
 
 
-def gcn_fc_forward(sd, x_s, x_t, A, AT, depth: int, keep=None, fc="mkl"):
+def gcn_fc_forward(sd, x_s, x_t, A, AT, depth: int, keep=None, fc="mkl", reassoc=False):
     """GCN_FC.forward, arch.py:179-193, eval mode (dropout is identity).
 
     sd: state_dict (tensors), A/AT: (rowptr, col, val) CSR of A and A^T.
     keep: optional dict that receives per-layer intermediates.
     fc: "mkl" (torch CPU F.linear, differentiable) or "kchain" (bitwise order
-    of the HIP FC kernel, forward only).
+    of the HIP FC kernel, forward only); reassoc: with "kchain", the HIP
+    path's association rule (graph_conv).
     """
-    left, right, agg_l, agg_r = conv_two_direction(sd, "conv1", x_s, x_t, A, AT, fc, relu=True)
+    left, right, agg_l, agg_r = conv_two_direction(sd, "conv1", x_s, x_t, A, AT, fc, relu=True, reassoc=reassoc)
     if keep is not None:
         keep["agg_l0"], keep["agg_r0"], keep["left0"], keep["right0"] = agg_l, agg_r, left, right
     for i in range(depth - 2):
-        left, right, agg_l, agg_r = conv_two_direction(sd, f"layers.{i}", left, right, A, AT, fc, relu=True)
+        left, right, agg_l, agg_r = conv_two_direction(sd, f"layers.{i}", left, right, A, AT, fc, relu=True,
+                                                       reassoc=reassoc)
         if keep is not None:
             keep[f"agg_l{i+1}"], keep[f"agg_r{i+1}"] = agg_l, agg_r
             keep[f"left{i+1}"], keep[f"right{i+1}"] = left, right

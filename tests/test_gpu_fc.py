@@ -52,6 +52,43 @@ def test_fc_bitwise(M, N, K1, K2, relu, bias):
     np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("variant", [0, 4, 7])
+@pytest.mark.parametrize("M,N,K,relu,bias", [
+    (1000, 1024, 1024, True, True),   # re-associated left2right root part
+    (129, 130, 36, False, True),      # ragged tiles (clamped addend loads)
+    (77, 64, 8, True, False),         # narrow-input kernel
+    (37, 3, 64, False, True),         # head-shaped tile
+])
+def test_fc_accumulate_bitwise(M, N, K, relu, bias, variant):
+    """Accumulate flag: C = act(A W^T + C + b) in place, bitwise the oracle
+    chain + P + bias, and equal to the non-accumulating product + P + b."""
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward
+
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    W = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+    P = rng.standard_normal((M, N)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32) if bias else None
+    t = lambda x: None if x is None else torch.from_numpy(x).to(DEV)
+    _lib.check(_lib.lib().lpg_fc_set_variant(variant), "set_variant")
+    try:
+        out = t(P).clone()
+        got = fc_forward(t(A), t(W), None, None, t(b), relu, out=out, accumulate=True)
+        plain = fc_forward(t(A), t(W), None, None, None, False)
+    finally:
+        _lib.lib().lpg_fc_set_variant(0)
+    assert got.data_ptr() == out.data_ptr()
+    got = got.cpu().numpy()
+    assert np.array_equal(got, O.fc_kchain(A, W, bias=b, relu=relu, add=P))
+    want = plain.cpu() + torch.from_numpy(P)
+    if bias:
+        want = want + torch.from_numpy(b)
+    if relu:
+        want = torch.relu(want)
+    assert np.array_equal(got, want.numpy())
+
+
 @pytest.mark.parametrize("p", [0.0, 0.25])
 def test_fc_smallk_equals_tiled_path(p):
     """The narrow-input kernel (K1 + K2 <= 16) and the MFMA tile kernel give

@@ -77,13 +77,19 @@ def test_state_dict_compat_and_init_stream():
     assert sum(p.numel() for p in model.parameters()) == 4_237_318
 
 
+@pytest.mark.parametrize("reassoc", [True, False])
 @pytest.mark.parametrize("depth,hids", [(3, 1024), (4, 256), (3, 40)])
-def test_forward_bitwise_vs_kchain_oracle(depth, hids):
+def test_forward_bitwise_vs_kchain_oracle(depth, hids, reassoc, monkeypatch):
     """Eval-mode logits are BITWISE equal to the oracle evaluated in the
     kernels' documented order (spmm_cpu loop + k-ordered FC chain + torch-CPU
-    F.normalize): SpMM, FC, heads and add_knowledge all reproduce exactly."""
+    F.normalize): SpMM, FC, heads and add_knowledge all reproduce exactly --
+    with the re-associated left2right (conv.py's association rule) and with
+    the reference's association everywhere."""
     from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn import conv
     from lpgnn.val import inference_gnn
+
+    monkeypatch.setattr(conv, "REASSOCIATE", reassoc)
 
     g = synth.uniform_lp(1500, 3000, 30000, seed=4)
     torch.manual_seed(0)
@@ -97,7 +103,8 @@ def test_forward_bitwise_vs_kchain_oracle(depth, hids):
     A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
     AT = O.csr_transpose(*A, g.m, g.n)
     with torch.no_grad():
-        rc, rv = O.gcn_fc_forward(sd, torch.from_numpy(g.x_s), torch.from_numpy(g.x_t), A, AT, depth, fc="kchain")
+        rc, rv = O.gcn_fc_forward(sd, torch.from_numpy(g.x_s), torch.from_numpy(g.x_t), A, AT, depth, fc="kchain",
+                                  reassoc=reassoc)
     assert torch.equal(lc.cpu(), rc)
     assert torch.equal(lv.cpu(), rv)
     got = inference_gnn(torch.cat((lc, lv)).cpu(), g.m)
