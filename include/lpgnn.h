@@ -176,7 +176,9 @@ lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const float *g, int64
  * bf16 bit patterns (uint16), K1 and K2 multiples of 64 (zero-pad), leading
  * dims multiples of 8 and 16-byte aligned; fp32 accumulation on
  * v_mfma_f32_16x16x32_bf16, fp32 bias, same epilogue (ReLU, fused dropout
- * with the same mask function), C stored as bf16 (round to nearest even). */
+ * with the same mask function), C stored as bf16 (round to nearest even).
+ * flags as lpg_fc_f32 (bit 1: C holds a bf16 addend, added in fp32 before
+ * the bias). */
 lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1, const uint16_t *W1,
                        int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
                        const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,

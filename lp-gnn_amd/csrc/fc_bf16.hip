@@ -42,7 +42,10 @@ struct FcB16Args {
   uint64_t seed;
   uint32_t drop_thresh;
   float drop_scale;
+  int32_t accum;  // flags bit 1: C holds a bf16 addend, C = bf16(act(A1 W1^T + A2 W2^T + C + bias))
 };
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16;
@@ -171,6 +174,20 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
     // stores it as 16-B chunks, 8 lanes per 128-B row segment -- one
     // global_store_dwordx4 per 8 outputs instead of one 2-byte store each.
     unsigned char *img = smem + wave * (FM * 16 * EP_PITCH);
+    constexpr int CPR = FN * 16 / 8;  // 16-B chunks per row
+    if (a.accum) {  // the addend tile, coalesced 16-B loads into the same image
+#pragma unroll
+      for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
+        const int q = it * 64 + lane;
+        const int lr = q / CPR, ch = q % CPR;
+        const int64_t row = wrow0 + lr < a.M ? wrow0 + lr : a.M - 1, col = wcol0 + ch * 8;
+        if (col < a.N)
+          *reinterpret_cast<uint4 *>(img + lr * EP_PITCH + ch * 16) =
+              *reinterpret_cast<const uint4 *>(a.C + row * a.ldc + col);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int64_t col = wcol0 + j * 16 + fr;
@@ -180,7 +197,9 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int lr = i * 16 + fq * 4 + r;
-          float v = acc[i][j][r] + bb;
+          float v = acc[i][j][r];
+          if (a.accum) v = v + bf16_to_f32(*reinterpret_cast<const uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2));
+          v = v + bb;
           if (RELU) v = v < 0.f ? 0.f : v;
           if (a.drop_thresh) v = drop_hash(a.seed, wrow0 + lr, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
           *reinterpret_cast<uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2) = to_bf16_rne(v);
@@ -189,7 +208,6 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    constexpr int CPR = FN * 16 / 8;  // 16-B chunks per row
 #pragma unroll
     for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
       const int q = it * 64 + lane;
@@ -211,7 +229,9 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
       for (int r = 0; r < 4; ++r) {
         const int64_t row = wrow0 + i * 16 + fq * 4 + r;
         if (row >= a.M) continue;
-        float v = acc[i][j][r] + bb;
+        float v = acc[i][j][r];
+        if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
+        v = v + bb;
         if (RELU) v = v < 0.f ? 0.f : v;
         if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         a.C[row * a.ldc + col] = to_bf16_rne(v);
@@ -345,6 +365,7 @@ __global__ __launch_bounds__(512) void fc_fwd_bf16_p3(FcB16Args a) {
         const int64_t row = m0 + wm * FM * 16 + i * 16 + fq * 4 + r;
         if (row >= a.M) continue;
         float v = acc[i][j][r];
+        if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
         if (a.bias) v = v + bb;
         if (RELU) v = v < 0.f ? 0.f : v;
         if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
@@ -402,9 +423,9 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
   LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
                   (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
               "lpg_fc_bf16: A/W must be 16-byte aligned with leading dimensions multiple of 8");
-  LPG_REQUIRE((flags & ~1) == 0, "lpg_fc_bf16: unknown flags 0x%x", flags);
+  LPG_REQUIRE((flags & ~3) == 0, "lpg_fc_bf16: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_bf16: dropout_p %g not in [0, 1)", (double)dropout_p);
-  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f};
+  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1};
   if (dropout_p > 0.f) {
     const double th = (double)dropout_p * 4294967296.0;
     a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);

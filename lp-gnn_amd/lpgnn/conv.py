@@ -66,11 +66,11 @@ def _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, p, seed, bf16):
     return _fc.fc_forward(agg, w_rel, x_dst, w_root, b, relu, p, seed)
 
 
-def reassociate(n_src: int, n_dst: int, f_src: int, f_out: int, bf16: bool = False) -> bool:
+def reassociate(n_src: int, n_dst: int, f_src: int, f_out: int) -> bool:
     """The association rule: lin_rel(S x) evaluated as S (x W_rel^T) iff the
     source side is the smaller node set and the SpMM does not get wider
-    (never worse on either the GEMM or the SpMM); fp32 path only."""
-    return REASSOCIATE and not bf16 and n_src < n_dst and f_out <= f_src
+    (never worse on either the GEMM or the SpMM)."""
+    return REASSOCIATE and n_src < n_dst and f_out <= f_src
 
 
 def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
@@ -93,13 +93,14 @@ class _TwoDirection(torch.autograd.Function):
         seed_r = _fc._new_seed() if dropout > 0 else 0
         seed_l = _fc._new_seed() if dropout > 0 else 0
         f_out = ws[0].shape[0]
-        ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out, bf16)
-        ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out, bf16)
+        ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out)
+        ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out)
 
         def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None):
             if ra:  # S (x_src W_rel^T), then lin_root + bias + ReLU accumulated onto it in place
-                y = spmm_forward(S, _fc.fc_forward(x_src, w_rel, None, None, None, False))
-                return _fc.fc_forward(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None
+                fc = _fc.fc_forward_bf16 if bf16 else _fc.fc_forward
+                y = spmm_forward(S, fc(x_src, w_rel, None, None, None, False))
+                return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None
             agg = spmm_forward(S, x_src) if agg is None else agg
             return _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, dropout, seed, bf16), agg
 

@@ -99,22 +99,32 @@ def _prep_bf16(t: Tensor | None) -> Tensor | None:
 
 
 def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
-                    relu: bool, dropout_p: float = 0.0, seed: int = 0) -> Tensor:
-    """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16)."""
+                    relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
+                    accumulate: bool = False) -> Tensor:
+    """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16);
+    ``accumulate`` adds the bf16 addend held in ``out`` (overwritten)."""
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
     A1, W1, A2, W2 = _prep_bf16(A1), _prep_bf16(W1), _prep_bf16(A2), _prep_bf16(W2)
     bias = None if bias is None else bias.float().contiguous()
-    C = torch.empty((M, N), dtype=torch.bfloat16, device=A1.device)
+    if out is not None:
+        if out.shape != (M, N) or out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.device != A1.device:
+            raise RuntimeError("lpgnn bf16 FC: `out` must be a bfloat16 [M, N] row-major view on the same device")
+        C = out
+    elif accumulate:
+        raise RuntimeError("lpgnn bf16 FC: accumulate needs the addend in `out`")
+    else:
+        C = torch.empty((M, N), dtype=torch.bfloat16, device=A1.device)
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
+    flags = (1 if relu else 0) | (2 if accumulate else 0)
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu-bf16" if relu else "lin-bf16"))
         st = L.lpg_fc_bf16(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
                            K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
                            None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
-                           None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), 1 if relu else 0,
+                           None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags,
                            float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_bf16")

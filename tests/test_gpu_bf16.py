@@ -43,6 +43,43 @@ def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
     torch.testing.assert_close(got, ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("M,N,K,relu,bias", [
+    (5000, 1024, 1024, True, True),  # re-associated left2right root part
+    (129, 130, 64, False, True),     # N % 8 != 0: per-element epilogue
+    (4099, 264, 128, True, False),   # ragged 256 x 256 tiles
+])
+def test_fc_bf16_accumulate(M, N, K, relu, bias, variant):
+    """Accumulate flag: C = bf16(act(A W^T + C + b)) in place; every tile
+    variant gives the same bits, within one bf16 rounding of fp32."""
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward_bf16
+
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(BF).to(DEV)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(BF).to(DEV)
+    P = torch.randn(M, N, generator=g).to(BF).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV) if bias else None
+    L = _lib.lib()
+    outs = []
+    try:
+        for v in (variant, 0):
+            L.lpg_fc_bf16_set_variant(v)
+            out = P.clone()
+            got = fc_forward_bf16(A, W, None, None, b, relu, out=out, accumulate=True)
+            assert got.data_ptr() == out.data_ptr()
+            outs.append(got)
+    finally:
+        L.lpg_fc_bf16_set_variant(0)
+    assert torch.equal(outs[0], outs[1])
+    ref = A.float() @ W.float().t() + P.float()
+    if bias:
+        ref = ref + b
+    if relu:
+        ref = torch.relu(ref)
+    torch.testing.assert_close(outs[0].float(), ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
+
+
 def test_fc_bf16_tile_variants_identical():
     """Both tilings run the same per-output MFMA chain order: identical bits."""
     from lpgnn import _lib
