@@ -5,6 +5,7 @@ Public surface (mirrors the reference's names):
   data:  MyToBipartite, lp_to_unipartite, batch_to, BipartiteBatch
   loader: NeighborLoader, NeighborSampler (device k-hop sampling)
   sparse: BipartiteCSR (the batch's edge_index), spmm
+  ops:   torch.ops.lpgnn.spmm_sum (torch_sparse's spmm_sum schema + autograd)
   val:   inference_gnn, accuracy, model_inference_with_batch
   train: balanced, labels_to_balanced_weights, train_step, make_optimizer
 """
@@ -13,6 +14,7 @@ from .sparse import BipartiteCSR, CSR, spmm
 from .arch import GCN_FC, GraphConv, GraphConvTwoDirection, Linear, add_knowledge, build_model
 from .data import BipartiteBatch, MyToBipartite, UnipartiteData, batch_to, lp_to_unipartite
 from .loader import NeighborLoader, NeighborSampler
+from . import ops  # registers torch.ops.lpgnn.spmm_sum
 
 __all__ = [
     "BipartiteCSR", "CSR", "spmm", "GCN_FC", "GraphConv", "GraphConvTwoDirection", "Linear",

@@ -98,3 +98,18 @@ def test_no_cpu_path_for_spmm():
     adj = BipartiteCSR.from_coo([0, 1], [1, 0], [0.5, -0.5], 2, 2, device="cpu")
     with pytest.raises(RuntimeError, match="no CPU path"):
         spmm(adj, torch.ones(2, 4))
+
+
+def test_spmm_sum_op_registered_with_torch_sparse_schema():
+    """torch.ops.lpgnn.spmm_sum takes torch_sparse 0.6.12's spmm_sum
+    arguments (row, rowptr, col, value, colptr, csr2csc, mat) and has no CPU
+    path."""
+    import lpgnn  # noqa: F401  (registers the op)
+
+    schema = str(torch.ops.lpgnn.spmm_sum.default._schema)
+    assert "Tensor? row, Tensor rowptr, Tensor col, Tensor? value, Tensor? colptr, Tensor? csr2csc, Tensor mat" \
+        in schema, schema
+    rowptr = torch.tensor([0, 1, 2])
+    col = torch.tensor([1, 0])
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        torch.ops.lpgnn.spmm_sum(None, rowptr, col, None, None, None, torch.ones(2, 4))

@@ -1,0 +1,77 @@
+"""torch.ops.lpgnn.spmm_sum (torch_sparse's spmm_sum schema) on the HIP
+kernel: forward and mat-gradient bitwise vs the oracle's spmm_cpu order."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_ref as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _torch_sparse_args(rng, m, n, nnz):
+    """(row, rowptr, col, value, colptr, csr2csc) as SparseTensor stores them."""
+    keys = np.sort(rng.choice(m * n, size=nnz, replace=False))  # row-major sorted = CSR order
+    row, col = keys // n, keys % n
+    val = rng.uniform(-1, 1, nnz).astype(np.float32)
+    rowptr = np.zeros(m + 1, np.int64)
+    np.add.at(rowptr, row + 1, 1)
+    rowptr = np.cumsum(rowptr)
+    csr2csc = np.argsort(col * m + row, kind="stable")
+    colptr = np.zeros(n + 1, np.int64)
+    np.add.at(colptr, col + 1, 1)
+    colptr = np.cumsum(colptr)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t(row), t(rowptr), t(col), t(val), t(colptr), t(csr2csc), (rowptr, col, val)
+
+
+@pytest.mark.parametrize("m,n,nnz,F", [(300, 500, 4000, 64), (1, 7, 7, 8), (50, 40, 0, 16), (2000, 100, 30000, 1024)])
+def test_spmm_sum_forward_backward_bitwise(m, n, nnz, F):
+    import lpgnn  # noqa: F401
+
+    rng = np.random.default_rng(m + nnz)
+    row, rowptr, col, val, colptr, csr2csc, (rp, c, v) = _torch_sparse_args(rng, m, n, nnz)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    mat = torch.from_numpy(X).to(DEV).requires_grad_(True)
+    out = torch.ops.lpgnn.spmm_sum(row, rowptr, col, val, colptr, csr2csc, mat)
+    assert np.array_equal(out.detach().cpu().numpy(), O.spmm_f32(rp, c, v, X))
+    G = rng.standard_normal((m, F)).astype(np.float32)
+    out.backward(torch.from_numpy(G).to(DEV))
+    AT = O.csr_transpose(rp, c.astype(np.int32), v, m, n)
+    assert np.array_equal(mat.grad.cpu().numpy(), O.spmm_f32(*AT, G))
+    # row=None (derived from rowptr) and value=None (ones) as upstream allows
+    mat2 = torch.from_numpy(X).to(DEV).requires_grad_(True)
+    out2 = torch.ops.lpgnn.spmm_sum(None, rowptr, col, None, colptr, csr2csc, mat2)
+    assert np.array_equal(out2.detach().cpu().numpy(), O.spmm_f32(rp, c, np.ones_like(v), X))
+    out2.sum().backward()
+    assert np.array_equal(mat2.grad.cpu().numpy(),
+                          O.spmm_f32(*O.csr_transpose(rp, c.astype(np.int32), np.ones_like(v), m, n),
+                                     np.ones((m, F), np.float32)))
+
+
+def test_spmm_sum_errors_like_upstream():
+    import lpgnn  # noqa: F401
+
+    rng = np.random.default_rng(0)
+    row, rowptr, col, val, colptr, csr2csc, _ = _torch_sparse_args(rng, 20, 30, 100)
+    mat = torch.randn(30, 8, device=DEV, requires_grad=True)
+    out = torch.ops.lpgnn.spmm_sum(row, rowptr, col, val, None, None, mat)
+    with pytest.raises(RuntimeError, match="colptr and csr2csc"):
+        out.sum().backward()
+    v = val.clone().requires_grad_(True)
+    out = torch.ops.lpgnn.spmm_sum(row, rowptr, col, v, colptr, csr2csc, mat)
+    with pytest.raises(RuntimeError, match="edge values"):
+        out.sum().backward()
+    with pytest.raises(RuntimeError, match="2-D"):
+        torch.ops.lpgnn.spmm_sum(row, rowptr, col, val, colptr, csr2csc, torch.randn(2, 30, 8, device=DEV))
+
+
+def test_spmm_sum_opcheck():
+    import lpgnn  # noqa: F401
+
+    rng = np.random.default_rng(1)
+    row, rowptr, col, val, colptr, csr2csc, _ = _torch_sparse_args(rng, 40, 60, 300)
+    mat = torch.randn(60, 16, device=DEV, requires_grad=True)
+    torch.library.opcheck(torch.ops.lpgnn.spmm_sum.default, (row, rowptr, col, val, colptr, csr2csc, mat),
+                          test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
