@@ -120,13 +120,18 @@ lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  * rounds of the 32-bit lowbias32 mix) is >= dropout_p * 2^32, and kept
  * values are scaled by 1 / (1 - dropout_p).  The mask is never stored: the
  * kept set is exactly where the output is > 0.
- * Row-major fp32, leading dimensions in floats; K1, K2 and the A/W leading
- * dimensions multiples of 4, A/W 16-byte aligned.
+ * Row-major fp32, leading dimensions in floats; A/W leading dimensions
+ * multiples of 4, A/W 16-byte aligned; K1 and K2 multiples of 32 (zero-pad:
+ * padded k are exact no-ops), except for the narrow-input kernel (4 <= K1,
+ * K1 + K2 <= 16, K multiples of 4, N and ldc multiples of 4) -- otherwise
+ * LPG_ERR_INVALID.
  * Numerics (bitwise reproducible, see oracle/fc_ref.c): each part (A1 over
- * K1, then A2 over K2) is cut into k-blocks of 32; a block's products form
- * one fp32 fma chain in k order from +0, the block sums are added in order
- * into the running total (+0 initially), then + P (accumulate), then + bias,
- * then ReLU. */
+ * K1, then A2 over K2) is cut into blocks of 128 k (the last one shorter); a
+ * block's products form one fp32 fma chain from +0, its k visited in groups
+ * of 8 consecutive k, inside a group in the order 0,4,1,5,2,6,3,7 (the
+ * 32x32x2 MFMA operand order of the tiled kernel); the block sums are added
+ * in order into the running total (+0 initially), then + P (accumulate),
+ * then + bias, then ReLU. */
 lpg_status lpg_fc_f32(int64_t M, int64_t N,
                       int64_t K1, const float *A1, int64_t lda1, const float *W1, int64_t ldw1,
                       int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2,
@@ -200,13 +205,11 @@ lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float
                                     const float *W, const float *H, int64_t ldh, float *dH, int64_t lddh,
                                     float *dW, float *db, void *workspace, void *stream);
 
-/* Tuning knob for lpg_fc_f32 (process-global, default 0): output tile
- * variant, 0 = 128x128 (4 waves, 2 blocks/CU), 1 = 256x128 (8 waves),
- * 2 = 128x256 (8 waves), 3 = 128x128 with 64-deep k staging, 4-6 = the
- * 16x16x4 MFMA with b128 operand reads (128x128, 128x256, 256x128),
- * 7 = 128x128 staged by LDS-DMA (global_load_lds; K1, K2 multiples of 32,
- * else variant 0), 8 = the same at 128x256 with 8 waves.  Every variant
- * produces bitwise identical results (same numerics blocks). */
+/* Tuning knob for lpg_fc_f32 (process-global, default 0): tiled-kernel
+ * variant, 0 = 128x128 tile, 2-stage LDS-DMA ring (2 blocks/CU), 1 = the same
+ * with a 3-stage ring (1 block/CU), 2 = 64-deep k-tiles (K1, K2 multiples of
+ * 64, else variant 0), 3 = 128x256 (8 waves), 4 = 256x128 (8 waves).  Every
+ * variant produces bitwise identical results (same chain order). */
 lpg_status lpg_fc_set_variant(int32_t variant);
 
 /* add_knowledge for one side (arch.py:129-141): out = normalize(logit) * 10,

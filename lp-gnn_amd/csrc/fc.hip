@@ -1,28 +1,39 @@
 // Dense per-node FC of GraphConv on fp32 MFMA (gfx950), fused:
 //
-//   C[m, n] = act( sum_{k<K1} A1[m,k] W1[n,k] + sum_{k<K2} A2[m,k] W2[n,k] + bias[n] )
+//   C[m, n] = act( sum_{k<K1} A1[m,k] W1[n,k] + sum_{k<K2} A2[m,k] W2[n,k] [+ C[m,n]] + bias[n] )
 //
 // = PyG 2.1 GraphConv.forward after propagate:  lin_rel(agg) + lin_root(x_dst)
 // (arch.py:57-62, 75-80) with the ReLU of arch.py:182/188 as the epilogue,
 // and -- with K2 = 0, no ReLU -- the heads lin_left / lin_right (arch.py:190).
 // The concat [agg | x_dst] is never materialised: the k loop walks A1 then A2.
+// [+ C]: the accumulate flag (re-associated GraphConv, lpgnn/conv.py).
 //
-// Numerics (the parity contract, mirrored by oracle/fc_ref.c): blocked k
-// order.  Each part (A1, W1) over K1, then (A2, W2) over K2, is cut into
-// k-tiles of BK = 32 (the last one zero-padded: fma(0, 0, p) = p exactly);
-// a tile's products form ONE fp32 fma chain in k order from +0 --
-// v_mfma_f32_32x32x2_f32 is bit-for-bit such a chain, k0 then k1 of each
-// pair (MI355X_MICROARCH.md §Matrix cores) -- and the tile sums are added in
-// tile order into the running total (+0 initially); then + bias, then ReLU
-// as (v < 0 ? 0 : v).  The blocking keeps the rounding error at the level
-// of MKL's blocked sgemm (~(32 + K/32) ulps worst case instead of K).
+// Numerics (the parity contract, mirrored by oracle/fc_ref.c): each part
+// (A1, W1) over K1, then (A2, W2) over K2, is cut into numerics blocks of
+// NB = 128 k (the last one shorter; zero padding: fma(0, 0, s) = s exactly,
+// the chain is never -0).  A block's products form ONE fp32 fma chain from
+// +0, its k visited in groups of 8 consecutive k, inside a group in the
+// order 0,4,1,5,2,6,3,7; the block sums are added in order into the running
+// total (+0 initially); then + C (accumulate), + bias, ReLU as
+// (v < 0 ? 0 : v), dropout.  The group order is what v_mfma_f32_32x32x2_f32
+// -- bit-for-bit an fma chain, k0 then k1 of its pair (MI355X_MICROARCH.md
+// §Matrix cores) -- sees when a lane's 16-B LDS read of 4 consecutive k
+// feeds 4 MFMA steps and the two lane halves hold k and k + 4.  The blocks
+// keep the rounding error at the level of MKL's blocked sgemm (one chain of
+// K = 2048 drifted past the 1e-4 logit tolerance); 128-k blocks cost one
+// fold (64 adds per wave) per 4 k-tiles.
 //
-// Tiling: 256 threads = 4 waves; BM x BN output tile, BK = 32; A and W tiles
-// staged global -> registers -> LDS ([row][BK+1] fp32, conflict-free column
-// reads), double-buffered with one barrier per k-tile; each wave owns
-// TM x TN blocks of 32x32 (16 accumulator VGPRs each).  Blocks are remapped
-// so that each XCD walks a contiguous range of m-tiles with all their
-// n-tiles (the A panel is then re-read from that XCD's L2).
+// Tiling (fc_fwd_f32): 4 waves (2 x 2), 128 x 128 output tile, each wave
+// 2 x 2 blocks of 32x32 (64 accumulators in AGPRs).  A and W k-tiles of
+// BK = 32 are staged global -> LDS by global_load_lds (LDS-DMA, no register
+// round trip) into an NS-stage ring, the DMA of the next tile in flight under
+// the current tile's MFMAs; one barrier per k-tile.  LDS image: 16-B chunk c
+// of row r at c ^ ((r >> 1) & 7) (128-B rows), which makes the ds_read_b128
+// operand reads conflict-free for the b128 lane groups; the next k-group's
+// operands are read halfway through the current group's 16 MFMAs.  Two
+// blocks per CU (64 KiB LDS each).  Blocks are remapped so that each XCD
+// walks a contiguous range of m-tiles with all their n-tiles (the A panel is
+// re-read from that XCD's L2).  K1, K2 multiples of 32 (the host pads).
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -33,7 +44,8 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int NB = 32;  // numerics block: k-tile length of one fma chain (the parity contract)
+constexpr int NB = 128;  // numerics block: k per fma chain (the parity contract), a multiple of every BK
+
 
 struct FcArgs {
   int64_t M, N, K1, K2;
@@ -79,17 +91,6 @@ __device__ __forceinline__ float epilogue(const FcArgs &a, float v, float b, int
   return v;
 }
 
-// Branch-free load of 4 consecutive k of row r of X (R rows, K columns):
-// the address is clamped into range.  Rows >= R only feed outputs that are
-// never stored, so they are left as whatever row R-1 holds; k >= K is zeroed
-// later (sstore), only in the partial last k-tile of a phase.  (A conditional
-// load -- or a select right after it -- makes hipcc wait vmcnt per load.)
-__device__ __forceinline__ float4 load_k4(const float *X, int64_t ld, int64_t R, int64_t K, int64_t r, int64_t k) {
-  const int64_t rr = r < R ? r : R - 1;
-  const int64_t kk = k < K ? k : K - 4;
-  return *reinterpret_cast<const float4 *>(X + rr * ld + kk);
-}
-
 // flags bit 1 (accumulate): acc[i][j][r] += C at the lane's 32x32-MFMA output
 // positions, every load issued before the first store (C is read and then
 // rewritten in place, so loads cannot be moved past stores by the compiler).
@@ -111,293 +112,188 @@ __device__ __forceinline__ void add_c32(const FcArgs &a, Acc (&acc)[TM][TN], int
   }
 }
 
-// WAVES_M x WAVES_N waves, each owning TM x TN blocks of 32x32; BK = staging
-// k-tile (a multiple of the numerics block NB; chains restart every NB).
-template <int WAVES_M, int WAVES_N, int TM, int TN, int BK, bool RELU>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32(FcArgs a) {
-  constexpr int NT = 64 * WAVES_M * WAVES_N;
-  constexpr int BM = WAVES_M * TM * 32;
-  constexpr int BN = WAVES_N * TN * 32;
-  constexpr int LDK = BK + 1;
-  constexpr int C4 = BK / 4;         // float4 chunks per staged row
-  constexpr int LA = BM * C4 / NT;  // float4 loads per thread per k-tile
-  constexpr int LB = BN * C4 / NT;
-  static_assert(BK % NB == 0, "BK must be a multiple of NB");
-  static_assert(LA >= 1 && LB >= 1 && BM * C4 % NT == 0 && BN * C4 % NT == 0, "tile/thread mismatch");
-  __shared__ float smem[2 * (BM + BN) * LDK];
-  // buffer b: A tile at smem + b*(BM+BN)*LDK, W tile right after it
-  auto As = [&](int b) { return smem + b * (BM + BN) * LDK; };
-  auto Bs = [&](int b) { return smem + b * (BM + BN) * LDK + BM * LDK; };
+// The tiled FC (see the header): lane half fk of the 32x32x2 MFMA holds
+// k = 8q + 4fk + u at step u of k-group q.  BK-deep k-tiles (32 or 64; 256-B
+// rows use the swizzle c ^ (r & 15)), NS-stage ring (NS - 1 tiles in flight).
+// K1, K2 multiples of BK.
+template <int BK>
+__device__ __forceinline__ int swzk(int row, int chunk) {
+  return BK == 32 ? chunk ^ ((row >> 1) & 7) : chunk ^ (row & 15);
+}
 
-  // XCD-aware bijective remap of the 1-D grid.
+template <int WM, int WN, int TM, int TN, int BK, int NS, bool RELU>
+__global__ __launch_bounds__(64 * WM * WN) void fc_fwd_f32(FcArgs a) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int ROWB = BK * 4, CPR = ROWB / 16, RPP = 1024 / ROWB;  // row bytes, chunks/row, rows/piece
+  constexpr int TILE_BYTES = (BM + BN) * ROWB;
+  constexpr int PA = BM / RPP / NW, PB = BN / RPP / NW;
+  constexpr int NQ = BK / 8;
+  static_assert(BK == 32 || BK == 64, "BK 32 or 64");
+  static_assert(BM % (RPP * NW) == 0 && BN % (RPP * NW) == 0, "tile rows must split into whole pieces per wave");
+  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * TILE_BYTES];
+
   const int64_t nwg = a.mt * a.nt;
   const int64_t bid = blockIdx.x;
-  const int64_t xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
-  const int64_t wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
   const int64_t m0 = (wgid / a.nt) * BM;
   const int64_t n0 = (wgid % a.nt) * BN;
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  // Two uniform phases of k-tiles: (A1, W1) over K1, then (A2, W2) over K2,
-  // each zero-padded to a multiple of BK (zeros are exact no-ops in the chain).
-  const int nk1 = (int)((a.K1 + BK - 1) / BK);
-  const int nk = nk1 + (int)((a.K2 + BK - 1) / BK);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nk1 = (int)(a.K1 / BK);
+  const int nk = nk1 + (int)(a.K2 / BK);
 
-  // acc: running total over k-tiles; each k-tile's 32 products are summed
-  // in their own chain (part, from +0) and then added to acc in tile order.
-  f32x16 acc[TM][TN];
+  const float *srcA1[PA], *srcA2[PA], *srcW1[PB], *srcW2[PB];
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int row = (wave + NW * p) * RPP + lane / CPR;
+    int64_t gr = m0 + row;
+    gr = gr < a.M ? gr : a.M - 1;
+    const int off = swzk<BK>(row, lane % CPR) * 4;
+    srcA1[p] = a.A1 + gr * a.lda1 + off;
+    srcA2[p] = a.A2 + gr * a.lda2 + off;
+  }
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    const int row = (wave + NW * p) * RPP + lane / CPR;
+    int64_t gn = n0 + row;
+    gn = gn < a.N ? gn : a.N - 1;
+    const int off = swzk<BK>(row, lane % CPR) * 4;
+    srcW1[p] = a.W1 + gn * a.ldw1 + off;
+    srcW2[p] = a.W2 + gn * a.ldw2 + off;
+  }
+  auto stage = [&](int b, int t) {
+    typedef __attribute__((address_space(3))) unsigned char lds_t;
+    unsigned char *base = smem + b * TILE_BYTES;
+    const bool p2 = t >= nk1;
+    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
+#pragma unroll
+    for (int p = 0; p < PA; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcA2[p] : srcA1[p]) + k0),
+                                       (lds_t *)(base + (wave + NW * p) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcW2[p] : srcW1[p]) + k0),
+                                       (lds_t *)(base + BM * ROWB + (wave + NW * p) * 1024), 16, 0, 0);
+  };
+  auto barrier_keep = [&](bool keep_newest) {
+    if (keep_newest)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(PA + PB) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // acc: running total over numerics blocks; each block's products form their
+  // own chain (part, from +0), added to acc in block order at the start of
+  // the next block (part starts at +0: the first fold is +0 + +0)
+  f32x16 acc[TM][TN], part[TM][TN];
   const f32x16 zero = {};
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = zero;
+    for (int j = 0; j < TN; ++j) acc[i][j] = part[i][j] = zero;
 
-  float4 ra[LA], rb[LB];
-  auto gload = [&](int t) {
-    const bool p2 = t >= nk1;  // wave-uniform phase select
-    const float *A = p2 ? a.A2 : a.A1;
-    const float *W = p2 ? a.W2 : a.W1;
-    const int64_t lda = p2 ? a.lda2 : a.lda1, ldw = p2 ? a.ldw2 : a.ldw1, Kp = p2 ? a.K2 : a.K1;
-    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int idx = tid + NT * i;
-      ra[i] = load_k4(A, lda, a.M, Kp, m0 + idx / C4, k0 + (idx % C4) * 4);
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int idx = tid + NT * i;
-      rb[i] = load_k4(W, ldw, a.N, Kp, n0 + idx / C4, k0 + (idx % C4) * 4);
-    }
-  };
-  auto sstore = [&](int buf, int t) {
-    const bool p2 = t >= nk1;
-    const int64_t Kp = p2 ? a.K2 : a.K1;
-    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
-    if (k0 + BK > Kp) {  // wave-uniform: partial k-tile, zero k >= Kp in both operands
-#pragma unroll
-      for (int i = 0; i < LA; ++i)
-        if (k0 + ((tid + NT * i) % C4) * 4 >= Kp) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int i = 0; i < LB; ++i)
-        if (k0 + ((tid + NT * i) % C4) * 4 >= Kp) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int idx = tid + NT * i;
-      float *p = As(buf) + (idx / C4) * LDK + (idx % C4) * 4;
-      p[0] = ra[i].x; p[1] = ra[i].y; p[2] = ra[i].z; p[3] = ra[i].w;
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int idx = tid + NT * i;
-      float *p = Bs(buf) + (idx / C4) * LDK + (idx % C4) * 4;
-      p[0] = rb[i].x; p[1] = rb[i].y; p[2] = rb[i].z; p[3] = rb[i].w;
-    }
-  };
-
-  gload(0);
-  sstore(0, 0);
-  __syncthreads();
   const int fr = lane & 31, fk = lane >> 5;
+  int offA[TM], offB[TN];  // byte offset of the lane's row in a tile image
+#pragma unroll
+  for (int i = 0; i < TM; ++i) offA[i] = (wm * TM * 32 + i * 32 + fr) * ROWB;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) offB[j] = BM * ROWB + (wn * TN * 32 + j * 32 + fr) * ROWB;
+  const int rA0 = wm * TM * 32 + fr, rB0 = wn * TN * 32 + fr;
+
+  if (nk > 0) stage(0, 0);
+  if (NS == 3 && nk > 1) stage(1, 1);
+  barrier_keep(NS == 3 && nk > 1);
+  constexpr int FOLD = NB / BK;  // k-tiles per numerics block
+  int b = 0;
   for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nk) gload(t + 1);
-    const float *Ab = As(buf) + (wm * TM * 32 + fr) * LDK + fk;
-    const float *Bb = Bs(buf) + (wn * TN * 32 + fr) * LDK + fk;
-    f32x16 part[TM][TN];
+    const bool more = t + NS - 1 < nk;
+    if (more) stage(b == 0 ? NS - 1 : b - 1, t + NS - 1);  // buffer (t + NS - 1) % NS, read last in t - 1
+    const unsigned char *T = smem + b * TILE_BYTES;
+    f32x4v av[2][TM], bv[2][TN];
+    auto lread = [&](int slot, int q) {
 #pragma unroll
-    for (int s = 0; s < BK / 2; ++s) {
-      float av[TM], bv[TN];
+      for (int i = 0; i < TM; ++i)
+        av[slot][i] = *reinterpret_cast<const f32x4v *>(T + offA[i] + swzk<BK>(rA0 + i * 32, 2 * q + fk) * 16);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = Ab[i * 32 * LDK + 2 * s];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = Bb[j * 32 * LDK + 2 * s];
+      for (int j = 0; j < TN; ++j)
+        bv[slot][j] = *reinterpret_cast<const f32x4v *>(T + offB[j] + swzk<BK>(rB0 + j * 32, 2 * q + fk) * 16);
+    };
+    const int tp = t < nk1 ? t : t - nk1;  // k-tile index within its part
+    if (tp % FOLD == 0) {  // a numerics block starts (they restart in each part): fold, restart the chain
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], s % (NB / 2) == 0 ? zero : part[i][j],
-                                                             0, 0, 0);
-      if (s % (NB / 2) == NB / 2 - 1) {  // end of a numerics block: fold into the total
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = acc[i][j] + part[i][j];
+          part[i][j] = zero;
+        }
+    }
+    lread(0, 0);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      // the next group's reads are issued halfway through this group's MFMAs (kept
+      // there by the scheduling fences): half a group of MFMAs covers their latency
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u == 2 && q + 1 < NQ) {
+          __builtin_amdgcn_sched_barrier(0);
+          lread((q + 1) & 1, q + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
+          for (int j = 0; j < TN; ++j)
+            part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q & 1][i][u], bv[q & 1][j][u], part[i][j], 0, 0, 0);
       }
     }
-    if (t + 1 < nk) sstore(buf ^ 1, t + 1);
-    __syncthreads();
+    barrier_keep(NS == 3 && more);  // tile t+1 landed; every wave done with tile t
+    b = b == NS - 1 ? 0 : b + 1;
   }
-
-  // Epilogue: C/D map of the 32x32 MFMA: col = lane & 31,
-  // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
   if (a.accum) add_c32<TM, TN>(a, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
+
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int64_t col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
     if (col >= a.N) continue;
-    const float b = a.bias ? a.bias[col] : 0.f;
+    const float bb = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int64_t rbase = m0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < a.M) a.C[row * a.ldc + col] = epilogue(a, acc[i][j][r], b, row, col, RELU);
+        if (row < a.M) a.C[row * a.ldc + col] = epilogue(a, acc[i][j][r], bb, row, col, RELU);
       }
     }
   }
 }
 
-// Same contract on v_mfma_f32_16x16x4_f32 (lane l: A[l&15][k = l>>4],
-// B[k = l>>4][l&15]; C/D col = l&15, row = 4*(l>>4) + r).  The staged tiles
-// are stored k-permuted inside each 32-wide k-block -- position (k&3)*8 + k/4,
-// rows padded to 36 floats -- so one conflict-free ds_read_b128 gives a lane
-// its operand for 4 consecutive MFMA k-steps.  Chains and block sums are the
-// same as fc_fwd_f32 (bitwise identical results).
-template <int WAVES_M, int WAVES_N, int TM, int TN, bool RELU>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_m16(FcArgs a) {
-  typedef float f32x4v __attribute__((ext_vector_type(4)));
-  constexpr int NT = 64 * WAVES_M * WAVES_N;
-  constexpr int BM = WAVES_M * TM * 16;
-  constexpr int BN = WAVES_N * TN * 16;
-  constexpr int BKs = 32;            // staging k-tile = one numerics block
-  constexpr int LDK = 36;            // padded row (floats), 16-B aligned
-  constexpr int C4 = BKs / 4;
-  constexpr int LA = BM * C4 / NT;
-  constexpr int LB = BN * C4 / NT;
-  static_assert(LA >= 1 && LB >= 1 && BM * C4 % NT == 0 && BN * C4 % NT == 0, "tile/thread mismatch");
-  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK];
-  auto As = [&](int b) { return smem + b * (BM + BN) * LDK; };
-  auto Bs = [&](int b) { return smem + b * (BM + BN) * LDK + BM * LDK; };
-
+template <int WM, int WN, int TM, int TN, int BK, int NS>
+lpg_status launch_fc(const FcArgs &a0, bool relu, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
+  FcArgs a = a0;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
   const int64_t nwg = a.mt * a.nt;
-  const int64_t bid = blockIdx.x;
-  const int64_t xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
-  const int64_t wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
-  const int64_t m0 = (wgid / a.nt) * BM;
-  const int64_t n0 = (wgid % a.nt) * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int nk1 = (int)((a.K1 + BKs - 1) / BKs);
-  const int nk = nk1 + (int)((a.K2 + BKs - 1) / BKs);
-
-  f32x4v acc[TM][TN];
-  const f32x4v zero = {};
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = zero;
-
-  float4 ra[LA], rb[LB];
-  auto gload = [&](int t) {
-    const bool p2 = t >= nk1;
-    const float *A = p2 ? a.A2 : a.A1;
-    const float *W = p2 ? a.W2 : a.W1;
-    const int64_t lda = p2 ? a.lda2 : a.lda1, ldw = p2 ? a.ldw2 : a.ldw1, Kp = p2 ? a.K2 : a.K1;
-    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BKs;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int idx = tid + NT * i;
-      ra[i] = load_k4(A, lda, a.M, Kp, m0 + idx / C4, k0 + (idx % C4) * 4);
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int idx = tid + NT * i;
-      rb[i] = load_k4(W, ldw, a.N, Kp, n0 + idx / C4, k0 + (idx % C4) * 4);
-    }
-  };
-  // k = 4c + h  ->  position h*8 + c
-  auto put = [&](float *base, int idx, const float4 &v) {
-    float *p = base + (idx / C4) * LDK + (idx % C4);
-    p[0] = v.x; p[8] = v.y; p[16] = v.z; p[24] = v.w;
-  };
-  auto sstore = [&](int buf, int t) {
-    const bool p2 = t >= nk1;
-    const int64_t Kp = p2 ? a.K2 : a.K1;
-    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BKs;
-    if (k0 + BKs > Kp) {
-#pragma unroll
-      for (int i = 0; i < LA; ++i)
-        if (k0 + ((tid + NT * i) % C4) * 4 >= Kp) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int i = 0; i < LB; ++i)
-        if (k0 + ((tid + NT * i) % C4) * 4 >= Kp) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < LA; ++i) put(As(buf), tid + NT * i, ra[i]);
-#pragma unroll
-    for (int i = 0; i < LB; ++i) put(Bs(buf), tid + NT * i, rb[i]);
-  };
-
-  gload(0);
-  sstore(0, 0);
-  __syncthreads();
-  const int fr = lane & 15, fh = lane >> 4;
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nk) gload(t + 1);
-    const float *Ab = As(buf) + (wm * TM * 16 + fr) * LDK + fh * 8;
-    const float *Bb = Bs(buf) + (wn * TN * 16 + fr) * LDK + fh * 8;
-    f32x4v part[TM][TN];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {  // k-steps 4*half .. 4*half+3 of this block
-      f32x4v av[TM], bv[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const f32x4v *>(Ab + i * 16 * LDK + 4 * half);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = *reinterpret_cast<const f32x4v *>(Bb + j * 16 * LDK + 4 * half);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][u], bv[j][u],
-                                                             (half == 0 && u == 0) ? zero : part[i][j], 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
-    if (t + 1 < nk) sstore(buf ^ 1, t + 1);
-    __syncthreads();
-  }
-
-  if (a.accum) {  // addends first, all loads in flight before the first store
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      int64_t col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
-      col = col < a.N ? col : a.N - 1;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int64_t row = m0 + wm * TM * 16 + i * 16 + 4 * (lane >> 4) + r;
-          row = row < a.M ? row : a.M - 1;
-          acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
-        }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int64_t col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
-    if (col >= a.N) continue;
-    const float b = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int64_t rbase = m0 + wm * TM * 16 + i * 16 + 4 * (lane >> 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = rbase + r;
-        if (row < a.M) a.C[row * a.ldc + col] = epilogue(a, acc[i][j][r], b, row, col, RELU);
-      }
-    }
-  }
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_f32: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, BK, NS, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, BK, NS, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
 }
 
 // add_knowledge for one side (arch.py:129-141), bitwise torch-CPU semantics:
@@ -436,44 +332,14 @@ __global__ __launch_bounds__(256) void relu_dropout_bwd_f32(int64_t n4, const fl
   }
 }
 
-template <int WM, int WN, int TM, int TN, int BK>
-lpg_status launch_fc(const FcArgs &a0, bool relu, hipStream_t s) {
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
-  FcArgs a = a0;
-  a.mt = (a.M + BM - 1) / BM;
-  a.nt = (a.N + BN - 1) / BN;
-  const int64_t nwg = a.mt * a.nt;
-  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_f32: grid too large");
-  if (relu)
-    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, BK, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
-  else
-    hipLaunchKernelGGL((fc_fwd_f32<WM, WN, TM, TN, BK, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
-  LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
-template <int WM, int WN, int TM, int TN>
-lpg_status launch_fc16(const FcArgs &a0, bool relu, hipStream_t s) {
-  constexpr int BM = WM * TM * 16, BN = WN * TN * 16, NT = 64 * WM * WN;
-  FcArgs a = a0;
-  a.mt = (a.M + BM - 1) / BM;
-  a.nt = (a.N + BN - 1) / BN;
-  const int64_t nwg = a.mt * a.nt;
-  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_f32: grid too large");
-  if (relu)
-    hipLaunchKernelGGL((fc_fwd_f32_m16<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
-  else
-    hipLaunchKernelGGL((fc_fwd_f32_m16<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
-  LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
 // Narrow-input FC (conv1: K1 = K2 = 8 LP features, arch.py:170): the output
 // write is the whole cost, so no MFMA tile -- each thread holds the weights of
-// 4 output columns in registers and streams rows (A values are block-uniform
-// scalar loads).  Same numerics as the tiled kernels: with K1, K2 <= NB each
-// part is ONE k-tile, i.e. one fma chain from +0 in k order, the tile sums
-// are added into +0 in order, then bias and ReLU -- bitwise identical.
+// 4 output columns in registers and streams rows (staged in LDS, read as
+// broadcasts).  Same numerics as the tiled kernel: each part is one numerics
+// block (K <= 16 < NB), a chain from +0 in the contract's group-of-8 order
+// (pik), added into the +0 total in order -- bitwise identical.
+// Position i of a part's chain -> k: groups of 8, inside a group 0,4,1,5,2,6,3,7.
+__host__ __device__ constexpr int pik(int i) { return (i & ~7) + (i & 1) * 4 + ((i >> 1) & 3); }
 constexpr int kSmallKRows = 64;
 
 template <int K>
@@ -525,14 +391,21 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
     // (a true fma per element -- the same bits as the scalar chains)
 #pragma unroll
     for (int j = 0; j < 4; j += 2) {
+      // each part (<= 16 k) is one numerics block: its own chain from +0, then added to the total
       f32x2 p1 = {0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < K1; ++k) p1 = __builtin_elementwise_fma(f32x2{xr[k], xr[k]}, wp1[j / 2][k], p1);
+      for (int i = 0; i < (K1 + 7) / 8 * 8; ++i) {
+        const int k = pik(i);
+        if (k < K1) p1 = __builtin_elementwise_fma(f32x2{xr[k], xr[k]}, wp1[j / 2][k], p1);
+      }
       f32x2 t = f32x2{0.f, 0.f} + p1;
       if (K2 > 0) {
         f32x2 p2 = {0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < K2; ++k) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[j / 2][k], p2);
+        for (int i = 0; i < (K2 + 7) / 8 * 8; ++i) {
+          const int k = pik(i);
+          if (k < K2) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[j / 2][k], p2);
+        }
         t = t + p2;
       }
       if (a.accum) t = t + f32x2{a.C[m * a.ldc + c + j], a.C[m * a.ldc + c + j + 1]};
@@ -567,161 +440,6 @@ bool try_smallk(const FcArgs &a, bool relu, hipStream_t s, lpg_status *st) {
   return false;
 }
 
-// Same contract staged by global_load_lds (LDS-DMA, no register round trip,
-// no ds_write pass): K1, K2 multiples of BK = 32.  LDS image: unpadded
-// 128-B rows (32 fp32 of k), 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)
-// -- applied on the DMA source address (the DMA destination is lane-linear)
-// and on the operand reads.  A wave-instruction moves 8 rows (1 KiB); two
-// buffers, one barrier per k-tile, the next tile's DMA in flight under the
-// current tile's MFMAs.  Operand reads are ds_read_b32 with a 2-way bank
-// conflict (rows r and r+16), one per MFMA.
-__device__ __forceinline__ int swz8(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-
-template <int WAVES_M, int WAVES_N, int TM, int TN, bool RELU>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void fc_fwd_f32_glds(FcArgs a) {
-  constexpr int NW = WAVES_M * WAVES_N;
-  constexpr int BM = WAVES_M * TM * 32, BN = WAVES_N * TN * 32, BK = 32;
-  constexpr int TILE_BYTES = (BM + BN) * BK * 4;
-  constexpr int PA = BM / 8 / NW, PB = BN / 8 / NW;
-  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split into whole pieces per wave");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
-
-  const int64_t nwg = a.mt * a.nt;
-  const int64_t bid = blockIdx.x;
-  const int64_t xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
-  const int64_t wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
-  const int64_t m0 = (wgid / a.nt) * BM;
-  const int64_t n0 = (wgid % a.nt) * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int nk1 = (int)(a.K1 / BK);
-  const int nk = nk1 + (int)(a.K2 / BK);
-
-  // per-lane source rows, clamped once (rows past M / N feed outputs never stored)
-  const float *srcA1[PA], *srcA2[PA], *srcW1[PB], *srcW2[PB];
-#pragma unroll
-  for (int p = 0; p < PA; ++p) {
-    const int row = (wave + NW * p) * 8 + (lane >> 3);
-    int64_t gr = m0 + row;
-    gr = gr < a.M ? gr : a.M - 1;
-    const int off = swz8(row, lane & 7) * 4;
-    srcA1[p] = a.A1 + gr * a.lda1 + off;
-    srcA2[p] = a.A2 + gr * a.lda2 + off;
-  }
-#pragma unroll
-  for (int p = 0; p < PB; ++p) {
-    const int row = (wave + NW * p) * 8 + (lane >> 3);
-    int64_t gn = n0 + row;
-    gn = gn < a.N ? gn : a.N - 1;
-    const int off = swz8(row, lane & 7) * 4;
-    srcW1[p] = a.W1 + gn * a.ldw1 + off;
-    srcW2[p] = a.W2 + gn * a.ldw2 + off;
-  }
-  auto stage = [&](int b, int t) {
-    typedef __attribute__((address_space(3))) unsigned char lds_t;
-    unsigned char *base = smem + b * TILE_BYTES;
-    const bool p2 = t >= nk1;
-    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
-#pragma unroll
-    for (int p = 0; p < PA; ++p)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcA2[p] : srcA1[p]) + k0),
-                                       (lds_t *)(base + (wave + NW * p) * 1024), 16, 0, 0);
-#pragma unroll
-    for (int p = 0; p < PB; ++p)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcW2[p] : srcW1[p]) + k0),
-                                       (lds_t *)(base + BM * BK * 4 + (wave + NW * p) * 1024), 16, 0, 0);
-  };
-
-  f32x16 acc[TM][TN];
-  const f32x16 zero = {};
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = zero;
-
-  const int fr = lane & 31, fk = lane >> 5;
-  // Tile t-1's sums are folded into acc lazily, block by block, right before
-  // tile t's first MFMA overwrites that block's sum register: the fold then
-  // sits between MFMAs instead of stalling behind the tile's last one.  Same
-  // order as fc_fwd_f32 (acc += tile t-1, then tile t).
-  f32x16 part[TM][TN];
-  if (nk > 0) stage(0, 0);
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const int b = t & 1;
-    if (t + 1 < nk) stage(b ^ 1, t + 1);
-    const unsigned char *As = smem + b * TILE_BYTES;
-    const unsigned char *Bs = As + BM * BK * 4;
-#pragma unroll
-    for (int s = 0; s < BK / 2; ++s) {
-      const int k = 2 * s + fk;
-      float av[TM], bv[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * TM * 32 + i * 32 + fr;
-        av[i] = *reinterpret_cast<const float *>(As + row * 128 + swz8(row, k >> 2) * 16 + (k & 3) * 4);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * TN * 32 + j * 32 + fr;
-        bv[j] = *reinterpret_cast<const float *>(Bs + row * 128 + swz8(row, k >> 2) * 16 + (k & 3) * 4);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if (s == 0) {
-            if (t > 0) acc[i][j] = acc[i][j] + part[i][j];
-            part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], zero, 0, 0, 0);
-          } else {
-            part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], part[i][j], 0, 0, 0);
-          }
-        }
-    }
-    __syncthreads();  // DMA of tile t+1 landed (vmcnt(0)); every wave done reading tile t
-  }
-  if (nk > 0) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] + part[i][j];
-  }
-  if (a.accum) add_c32<TM, TN>(a, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
-
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int64_t col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
-    if (col >= a.N) continue;
-    const float b = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int64_t rbase = m0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < a.M) a.C[row * a.ldc + col] = epilogue(a, acc[i][j][r], b, row, col, RELU);
-      }
-    }
-  }
-}
-
-template <int WM, int WN, int TM, int TN>
-lpg_status launch_fc_glds(const FcArgs &a0, bool relu, hipStream_t s) {
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
-  FcArgs a = a0;
-  a.mt = (a.M + BM - 1) / BM;
-  a.nt = (a.N + BN - 1) / BN;
-  const int64_t nwg = a.mt * a.nt;
-  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_f32: grid too large");
-  if (relu)
-    hipLaunchKernelGGL((fc_fwd_f32_glds<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
-  else
-    hipLaunchKernelGGL((fc_fwd_f32_glds<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
-  LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
 int g_fc_variant = 0;  // lpg_fc_set_variant; 0 = default tile
 
 }  // namespace
@@ -753,22 +471,18 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
   lpg_status st;
-  if (try_smallk(a, relu, s, &st)) return st;                // conv1: narrow LP features
-  if (N <= 32) return launch_fc<4, 1, 1, 1, 32>(a, relu, s);  // heads (N = 3): 128 x 32 tiles
+  if (try_smallk(a, relu, s, &st)) return st;  // conv1: narrow LP features
+  LPG_REQUIRE(K1 % 32 == 0 && K2 % 32 == 0,
+              "lpg_fc_f32: K1, K2 must be multiples of 32 (zero-pad) unless 4 <= K1, K1 + K2 <= 16 and N %% 4 == 0");
+  if (N <= 32) return launch_fc<4, 1, 1, 1, 32, 2>(a, relu, s);  // heads (N = 3): 128 x 32 tiles
   switch (g_fc_variant) {
-    case 1: return launch_fc<4, 2, 2, 2, 32>(a, relu, s);  // 256 x 128, 8 waves
-    case 2: return launch_fc<2, 4, 2, 2, 32>(a, relu, s);  // 128 x 256, 8 waves
-    case 3: return launch_fc<2, 2, 2, 2, 64>(a, relu, s);  // 128 x 128, BK 64 (1 block / CU)
-    case 4: return launch_fc16<2, 2, 4, 4>(a, relu, s);    // 16x16x4 MFMA, 128 x 128
-    case 5: return launch_fc16<2, 2, 4, 8>(a, relu, s);    // 16x16x4 MFMA, 128 x 256
-    case 6: return launch_fc16<4, 2, 4, 4>(a, relu, s);    // 16x16x4 MFMA, 256 x 128, 8 waves
-    case 7:
-      if (K1 % 32 == 0 && K2 % 32 == 0) return launch_fc_glds<2, 2, 2, 2>(a, relu, s);  // LDS-DMA staging
-      return launch_fc<2, 2, 2, 2, 32>(a, relu, s);
-    case 8:
-      if (K1 % 32 == 0 && K2 % 32 == 0) return launch_fc_glds<2, 4, 2, 2>(a, relu, s);  // 128 x 256, 8 waves
-      return launch_fc<2, 2, 2, 2, 32>(a, relu, s);
-    default: return launch_fc<2, 2, 2, 2, 32>(a, relu, s); // 128 x 128, BK 32, 2 blocks / CU
+    case 1: return launch_fc<2, 2, 2, 2, 32, 3>(a, relu, s);  // 3-stage ring, 96 KiB: 1 block / CU
+    case 2:
+      if (K1 % 64 == 0 && K2 % 64 == 0) return launch_fc<2, 2, 2, 2, 64, 2>(a, relu, s);  // BK 64, 128 KiB
+      return launch_fc<2, 2, 2, 2, 32, 2>(a, relu, s);
+    case 3: return launch_fc<2, 4, 2, 2, 32, 2>(a, relu, s);  // 128 x 256, 8 waves, 96 KiB
+    case 4: return launch_fc<4, 2, 2, 2, 32, 2>(a, relu, s);  // 256 x 128, 8 waves, 96 KiB
+    default: return launch_fc<2, 2, 2, 2, 32, 2>(a, relu, s);  // 128 x 128, 64 KiB: 2 blocks / CU
   }
 }
 
@@ -790,7 +504,7 @@ extern "C" lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const 
 }
 
 extern "C" lpg_status lpg_fc_set_variant(int32_t v) {
-  LPG_REQUIRE(v >= 0 && v <= 8, "lpg_fc_set_variant: variant %d not in [0, 8]", v);
+  LPG_REQUIRE(v >= 0 && v <= 4, "lpg_fc_set_variant: variant %d not in [0, 4]", v);
   g_fc_variant = v;
   return LPG_OK;
 }

@@ -39,11 +39,14 @@ def _prep(t: Tensor | None) -> Tensor | None:
     return t
 
 
-def _pad_k(t: Tensor) -> Tensor:
-    """Zero-pad the reduction dim to a multiple of 4 (zeros are exact no-ops
-    in the fma chain: the accumulator is never -0)."""
+def _pad_k(t: Tensor, mult: int = 4) -> Tensor:
+    """Zero-pad the reduction dim to a multiple of `mult` (zeros are exact
+    no-ops in the fma chain: the accumulator is never -0)."""
     k = t.shape[1]
-    return t if k % 4 == 0 else F.pad(t, (0, 4 - k % 4))
+    return t if k % mult == 0 else F.pad(t, (0, mult - k % mult))
+
+
+_FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless the narrow-input kernel applies
 
 
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
@@ -54,10 +57,15 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
-    if A1.shape[1] % 4:
-        A1, W1 = _pad_k(A1), _pad_k(W1)
-    if A2 is not None and A2.shape[1] % 4:
-        A2, W2 = _pad_k(A2), _pad_k(W2)
+    k4 = lambda k: -(-k // 4) * 4
+    K1_4, K2_4 = k4(A1.shape[1]), (0 if A2 is None else k4(A2.shape[1]))
+    small = 4 <= K1_4 and K1_4 + K2_4 <= 16 and N % 4 == 0 and (out is None or (
+        out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0))
+    mult = 4 if small else _FC_BK
+    if A1.shape[1] % mult:
+        A1, W1 = _pad_k(A1, mult), _pad_k(W1, mult)
+    if A2 is not None and A2.shape[1] % mult:
+        A2, W2 = _pad_k(A2, mult), _pad_k(W2, mult)
     A1, W1, A2, W2 = _prep(A1), _prep(W1), _prep(A2), _prep(W2)
     bias = None if bias is None else bias.contiguous()
     if out is not None:  # caller-provided rows (e.g. the owned rows of a partition's [owned | halo] buffer)

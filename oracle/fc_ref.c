@@ -5,12 +5,12 @@
  * PyG 2.1 GraphConv after propagate, out = lin_rel(agg) + lin_root(x_dst)
  * (arch.py:57-62, 75-80), ReLU (arch.py:182, 188), and the heads
  * lin_left/lin_right (arch.py:190), evaluated in a fixed blocked k order
- * (see oracle_fc_f32) then + P (lpg_fc_f32's accumulate flag), then + bias,
+ * (see phase()) then + P (lpg_fc_f32's accumulate flag), then + bias,
  * then ReLU as (v < 0 ? 0 : v).  torch.nn.functional.linear on CPU (MKL) is the
  * reference's own evaluation; it sums in an unspecified blocked order, so it
  * agrees with this chain to fp32 rounding only (tests report both).
  *
- * Loop order m -> k -> n keeps each output's chains in k order while the
+ * Loop order m -> k -> n keeps each output's chains in the contract's order while the
  * inner loop vectorises across n (W is transposed once per call).
  */
 #include <math.h>
@@ -26,18 +26,25 @@ static void transpose(const float *W, int64_t ldw, int64_t N, int64_t K, float *
     for (int64_t k = 0; k < K; ++k) Wt[k * N + n] = W[n * ldw + k];
 }
 
-/* Blocked order: each phase (A1 over K1, then A2 over K2) is cut into
- * k-tiles of FC_BK = 32 (the last one zero-padded); a tile's 32 products are
- * one fma chain from +0, and the tile sums are added in order into the
- * running total (+0 initially).  out = total + bias, then ReLU. */
-#define FC_BK 32
+/* The order of lpg_fc_f32 (fc.hip header): each part (A1 over K1, then A2
+ * over K2) is cut into blocks of FC_NB = 128 k (the last one shorter); a
+ * block's products form ONE fma chain from +0 whose k are visited in groups
+ * of 8 consecutive k (the last group zero-padded -- exact no-ops, skipped
+ * here), inside a group in the order 0,4,1,5,2,6,3,7; block sums are added
+ * in order into the running total (+0 initially).
+ * out = total [+ P] + bias, then ReLU. */
+#define FC_NB 128
+
+static int64_t pik(int64_t i) { return (i & ~7) + (i & 1) * 4 + ((i >> 1) & 3); }
 
 static void phase(const float *A, int64_t lda, const float *Wt, int64_t N, int64_t K, int64_t m, float *tot,
                   float *part) {
-  for (int64_t k0 = 0; k0 < K; k0 += FC_BK) {
+  for (int64_t k0 = 0; k0 < K; k0 += FC_NB) {
+    const int64_t kb = K - k0 < FC_NB ? K - k0 : FC_NB;
     for (int64_t n = 0; n < N; ++n) part[n] = 0.0f;
-    const int64_t k1 = k0 + FC_BK < K ? k0 + FC_BK : K;  /* zero padding: exact no-ops */
-    for (int64_t k = k0; k < k1; ++k) {
+    for (int64_t i = 0; i < (kb + 7) / 8 * 8; ++i) {
+      const int64_t k = k0 + pik(i);
+      if (k >= k0 + kb) continue;
       const float a = A[m * lda + k];
       const float *w = Wt + k * N;
       for (int64_t n = 0; n < N; ++n) part[n] = fmaf(a, w[n], part[n]);

@@ -113,3 +113,14 @@ def test_spmm_sum_op_registered_with_torch_sparse_schema():
     col = torch.tensor([1, 0])
     with pytest.raises(RuntimeError, match="no CPU path"):
         torch.ops.lpgnn.spmm_sum(None, rowptr, col, None, None, None, torch.ones(2, 4))
+
+
+def test_fc_rejects_unpadded_k_on_the_tiled_path():
+    """lpg_fc_f32's tiled kernel needs K1, K2 multiples of 32 (the host pads);
+    the check fails before any device work."""
+    from lpgnn import _lib
+
+    L = _lib.lib()
+    fake = 1 << 20  # 16-byte aligned, never dereferenced: validation fails first
+    st = L.lpg_fc_f32(10, 64, 40, fake, 40, fake, 40, 0, None, 0, None, 0, None, fake, 64, 0, 0.0, 0, None)
+    assert st == 1 and b"multiples of 32" in L.lpg_last_error()

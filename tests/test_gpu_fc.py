@@ -52,7 +52,7 @@ def test_fc_bitwise(M, N, K1, K2, relu, bias):
     np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [0, 4, 7])
+@pytest.mark.parametrize("variant", [0, 1, 3])
 @pytest.mark.parametrize("M,N,K,relu,bias", [
     (1000, 1024, 1024, True, True),   # re-associated left2right root part
     (129, 130, 36, False, True),      # ragged tiles (clamped addend loads)
@@ -182,9 +182,9 @@ def test_knowledge_backward_matches_torch():
     torch.testing.assert_close(got, x.grad, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("variant", range(9))
+@pytest.mark.parametrize("variant", range(5))
 def test_fc_tile_variants_bitwise(variant):
-    """Every lpg_fc_set_variant tile/MFMA shape gives the same bits as the oracle."""
+    """Every lpg_fc_set_variant tile / staging depth gives the same bits as the oracle."""
     from lpgnn import _lib
     from lpgnn.fc import fc_forward
 

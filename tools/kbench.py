@@ -201,12 +201,50 @@ def bench_load(out):
         out[f"load c2 {name}"] = dict(ms=float(np.median(ts)) * 1e3)
 
 
+def bench_fcpi(out):
+    """FC kernel variants at the c2 hidden-layer shapes vs hipBLASLt (torch)."""
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward
+
+    L = _lib.lib()
+    dev = "cuda"
+    variants = [int(v) for v in os.environ.get("LPG_FCV", "0,1,2,3,4").split(",")]
+    for M, K1, K2 in ((200_000, 1024, 1024), (200_000, 1024, 0), (100_000, 1024, 0)):
+        A1 = torch.randn(M, K1, device=dev).relu_()
+        A2 = torch.randn(M, K2, device=dev).relu_() if K2 else None
+        W1 = torch.randn(1024, K1, device=dev) * 0.03
+        W2 = torch.randn(1024, K2, device=dev) * 0.03 if K2 else None
+        b = torch.randn(1024, device=dev)
+        flops = 2.0 * M * 1024 * (K1 + K2)
+
+        def var(v):
+            def f():
+                L.lpg_fc_set_variant(v)
+                return fc_forward(A1, W1, A2, W2, b, True)
+            return f
+        ys = {v: var(v)() for v in variants}
+        ref = ys[variants[0]]
+        for v, y in ys.items():
+            d = (y - ref).abs().max().item()
+            out[f"fcpi M={M} K={K1}+{K2} v{v} maxdiff"] = dict(d=d)
+        fns = {f"v{v}": var(v) for v in variants}
+        if K2:
+            fns["torch"] = lambda: torch.relu(torch.addmm(b, A1, W1.t()).addmm_(A2, W2.t()))
+        else:
+            fns["torch"] = lambda: torch.relu(torch.addmm(b, A1, W1.t()))
+        t = timeit(fns)
+        L.lpg_fc_set_variant(0)
+        for k, v in t.items():
+            out[f"fcpi M={M} K={K1}+{K2} {k}"] = dict(ms=v, tflops=flops / v / 1e9)
+        del A1, A2
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["fc", "spmm", "bwd"]
     out = {}
     for w in which:
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
-         "load": bench_load}[w](out)
+         "load": bench_load, "fcpi": bench_fcpi}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
