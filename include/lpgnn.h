@@ -138,6 +138,38 @@ lpg_status lpg_fc_f32(int64_t M, int64_t N,
                       const float *bias, float *C, int64_t ldc, int32_t flags,
                       float dropout_p, uint64_t seed, void *stream);
 
+/* fp32 FC on the bf16 matrix cores (same operation and epilogue as
+ * lpg_fc_f32; also the input-gradient GEMMs dZ W of its backward, with W
+ * given transposed).  A1/A2 fp32 as in lpg_fc_f32 (K1, K2 multiples of 32,
+ * lda multiples of 4, 16-byte aligned); W1/W2 PRE-SPLIT by lpg_split3_f32
+ * into three bf16 planes (plane p at W + p * ps, [N, K] with leading
+ * dimension ldw, ldw and ps multiples of 8, 16-byte aligned).  Each fp32
+ * operand is split exactly, a = a0 + a1 + a2 (bf16 terms, RNE), and the
+ * product keeps the six terms down to 2^-16 relative size (the three dropped
+ * terms are <= 2^-23 |a b|, below the fp32 rounding of the product);
+ * bf16 x bf16 products are exact and accumulate in fp32 (a0 b0 and the small
+ * terms in separate accumulators).  fp32-GEMM accuracy at 6/16 of the fp32
+ * MFMA cost; not bitwise reproducible on the CPU (the bf16 MFMA's internal
+ * summation order is unspecified) -- lpg_fc_f32 keeps the bitwise contract.
+ * flags, bias, dropout as lpg_fc_f32. */
+lpg_status lpg_fc_x3_f32(int64_t M, int64_t N,
+                         int64_t K1, const float *A1, int64_t lda1, const uint16_t *W1, int64_t ldw1, int64_t ps1,
+                         int64_t K2, const float *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2,
+                         const float *bias, float *C, int64_t ldc, int32_t flags,
+                         float dropout_p, uint64_t seed, void *stream);
+
+/* The exact three-way bf16 split of an fp32 matrix for lpg_fc_x3_f32:
+ * plane p of dst ([rows, cols], leading dimension ldd, plane p at
+ * dst + p * plane_stride) holds term p of S, S = src ([rows, cols], lds) or,
+ * with transpose != 0, S = src^T (src [cols, rows]).  t0 = RNE_bf16(x),
+ * t1 = RNE_bf16(x - t0), t2 = RNE_bf16(x - t0 - t1) = x - t0 - t1 exactly. */
+lpg_status lpg_split3_f32(int64_t rows, int64_t cols, const float *src, int64_t lds, int32_t transpose,
+                          uint16_t *dst, int64_t ldd, int64_t plane_stride, void *stream);
+
+/* Tile choice for lpg_fc_x3_f32 (tuning): 0 = 128 x 128 (4 waves, 2 blocks
+ * per CU), 1 = 256 x 128, 2 = 128 x 256 (8 waves). */
+lpg_status lpg_fc_x3_set_variant(int32_t v);
+
 /* Backward of ReLU (+ fused dropout): out[i] = y[i] > 0 ? g[i] * scale : 0,
  * y = the stored lpg_fc_f32 output, scale = 1/(1-p) (1 without dropout).
  * n a multiple of 4, buffers 16-byte aligned; out may alias g. */

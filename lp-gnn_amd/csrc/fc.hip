@@ -35,6 +35,7 @@
 // walks a contiguous range of m-tiles with all their n-tiles (the A panel is
 // re-read from that XCD's L2).  K1, K2 multiples of 32 (the host pads).
 #include "common.h"
+#include "fc_common.h"
 
 #pragma clang fp contract(off)
 
@@ -63,26 +64,6 @@ struct FcArgs {
   // each element is read and rewritten by the lane that owns it
   int32_t accum;
 };
-
-// Counter-based dropout RNG over (seed, row, col): two rounds of the 32-bit
-// "lowbias32" integer hash, the inner one keyed by the row only (so a lane
-// reuses it across its columns).  Stateless, so the backward pass never needs
-// the mask (the kept set is exactly where the stored output is > 0).  32-bit
-// on purpose: 64-bit multiplies are multi-instruction on CDNA and made the
-// epilogue ~10% of a hidden-layer FC.
-__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int64_t row, int64_t col) {
-  const uint32_t hr = lowbias32((uint32_t)row ^ (uint32_t)seed);
-  return lowbias32(hr ^ ((uint32_t)col * 0x9e3779b9u) ^ (uint32_t)(seed >> 32));
-}
 
 __device__ __forceinline__ float epilogue(const FcArgs &a, float v, float b, int64_t row, int64_t col, bool relu) {
   if (a.bias) v = v + b;

@@ -22,6 +22,7 @@
 // ds_read_b128 fragment reads, so the 16 rows a read quarter-wave touches land
 // in 16 distinct 16-B bank groups.  XCD-aware bijective block remap as in fc.hip.
 #include "common.h"
+#include "fc_common.h"
 
 namespace lpg {
 namespace {
@@ -46,21 +47,6 @@ struct FcB16Args {
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-
-__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-// Same mask function as fc.hip's fp32 epilogue.
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int64_t row, int64_t col) {
-  const uint32_t hr = lowbias32((uint32_t)row ^ (uint32_t)seed);
-  return lowbias32(hr ^ ((uint32_t)col * 0x9e3779b9u) ^ (uint32_t)(seed >> 32));
-}
 
 __device__ __forceinline__ uint16_t to_bf16_rne(float f) {
   uint32_t u = __float_as_uint(f);

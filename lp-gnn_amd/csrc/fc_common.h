@@ -1,0 +1,41 @@
+// Device helpers shared by the FC kernels (fc.hip, fc_bf16.hip, fc_x3.hip):
+// the fused-dropout mask function must be one definition, since the backward
+// of every FC variant relies on "kept <=> stored output > 0".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lpg {
+
+// Counter-based dropout RNG over (seed, row, col): two rounds of the 32-bit
+// "lowbias32" integer hash, the inner one keyed by the row only (so a lane
+// reuses it across its columns).  Stateless, so the backward pass never needs
+// the mask (the kept set is exactly where the stored output is > 0).  32-bit
+// on purpose: 64-bit multiplies are multi-instruction on CDNA and made the
+// epilogue ~10% of a hidden-layer FC.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int64_t row, int64_t col) {
+  const uint32_t hr = lowbias32((uint32_t)row ^ (uint32_t)seed);
+  return lowbias32(hr ^ ((uint32_t)col * 0x9e3779b9u) ^ (uint32_t)(seed >> 32));
+}
+
+// Host-side dropout threshold / scale shared by the FC entry points.
+inline void dropout_params(float p, uint32_t *thresh, float *scale) {
+  *thresh = 0u;
+  *scale = 1.f;
+  if (p > 0.f) {
+    const double th = (double)p * 4294967296.0;
+    *thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);
+    *scale = 1.f / (1.f - p);
+  }
+}
+
+}  // namespace lpg

@@ -1,0 +1,355 @@
+// fp32 FC on the bf16 matrix cores: the GraphConv FC of fc.hip
+//
+//   C[m, n] = act( sum_{k<K1} A1[m,k] W1[n,k] + sum_{k<K2} A2[m,k] W2[n,k] [+ C[m,n]] + bias[n] )
+//
+// (PyG 2.1 GraphConv lin_rel + lin_root + ReLU/dropout, arch.py:57-62, 75-80,
+// 182-188; and, with W = a transposed weight, the input-gradient GEMMs of its
+// backward) with fp32 operands and fp32 accumulation, evaluated through an
+// EXACT three-way bf16 split instead of the fp32 MFMA.
+//
+// Why: gfx950 issues v_mfma_f32_32x32x16_bf16 at 512 MAC/clk/SIMD and
+// v_mfma_f32_32x32x2_f32 at 32 (MI355X_MICROARCH.md, constants table).  Every
+// fp32 value splits exactly into three bf16 terms, a = a0 + a1 + a2 with
+// a0 = RNE_bf16(a), a1 = RNE_bf16(a - a0), a2 = a - a0 - a1 (8 + 8 + 8
+// significant bits = the 24-bit fp32 significand; |a1| <= 2^-8 |a|,
+// |a2| <= 2^-16 |a|, every subtraction exact).  The product keeps every term
+// down to 2^-16 relative size:
+//   a b = a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0) + d,
+//   |d| = |a1 b2 + a2 b1 + a2 b2| <= 2^-23 |a b|,
+// i.e. below the fp32 rounding of the product itself.  Each bf16 x bf16
+// product is exact in fp32.  a0 b0 accumulates in its own fp32 accumulator
+// (accH) and the five small products in another (accL), added once at the
+// end, so the small terms' roundings sit 2^-8 below the main chain's.  Cost:
+// 6 bf16 MFMAs = 6/16 of one fp32 MFMA.  Accuracy is fp32 GEMM accuracy
+// (fp32 operands are never rounded); tests/test_gpu_fc.py measures it against
+// fp64 beside the exact-fp32 kernel.  Not a bitwise contract: the bf16 MFMA's
+// internal summation order is unspecified, so there is no CPU restatement of
+// the bits (the exact-fp32 kernel, lpg_fc_f32, keeps that contract).
+//
+// Operands: A (activations) fp32 as in lpg_fc_f32, split in registers by the
+// lane that feeds it to the MFMA; W pre-split once per call (lpg_split3_f32:
+// three bf16 planes, weights are small) so only A costs VALU in the k loop.
+// Tiling: 4 waves (2 x 2), 128 x 128 output tile, each wave 2 x 2 fragments of
+// 32 x 32 (accH + accL: 128 VGPRs).  k-tiles of BK = 32 staged by LDS-DMA
+// (global_load_lds) into a 2-stage ring: A as 128-B fp32 rows (16-B chunk c of
+// row r at c ^ ((r >> 1) & 7)), each W plane as 64-B bf16 rows (chunk c at
+// c ^ ((r >> 2) & 3)); both make the ds_read_b128 fragment reads
+// conflict-free.  80 KiB LDS per block (2 blocks per CU).  XCD-aware
+// bijective block remap (each XCD walks contiguous m-tiles with all their
+// n-tiles, so the A panel is re-read from that XCD's L2).
+#include "common.h"
+#include "fc_common.h"
+
+#pragma clang fp contract(off)
+
+namespace lpg {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 32;
+
+struct X3Args {
+  int64_t M, N, K1, K2;
+  const float *A1, *A2;
+  const uint16_t *W1, *W2;  // three bf16 planes each, plane p at W + p * ps
+  const float *bias;
+  int64_t lda1, lda2, ldw1, ldw2, ps1, ps2;
+  float *C;
+  int64_t ldc;
+  int64_t mt, nt;
+  uint64_t seed;
+  uint32_t drop_thresh;
+  float drop_scale;
+  int32_t accum;
+};
+
+__device__ __forceinline__ unsigned pk_bf16(float x, float y) {  // v_cvt_pk_bf16_f32: RNE, x in the low half
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x, y}, bf16x2));
+}
+
+// one split level of a pair: the packed RNE bf16 terms; the exact residuals are left in x, y
+__device__ __forceinline__ unsigned split_lvl(float &x, float &y) {
+  const unsigned p = pk_bf16(x, y);
+  x = x - __uint_as_float(p << 16);
+  y = y - __uint_as_float(p & 0xffff0000u);
+  return p;
+}
+
+struct Split3 {
+  bf16x8 h, m, l;
+};
+
+// 8 consecutive k (lo = k 0..3, hi = k 4..7) -> the three bf16x8 MFMA operands
+__device__ __forceinline__ Split3 split3(f32x4 lo, f32x4 hi) {
+  u32x4 H, Mi, L;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float x = i < 2 ? lo[2 * i] : hi[2 * i - 4], y = i < 2 ? lo[2 * i + 1] : hi[2 * i - 3];
+    H[i] = split_lvl(x, y);
+    Mi[i] = split_lvl(x, y);
+    L[i] = pk_bf16(x, y);
+  }
+  return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, Mi), __builtin_bit_cast(bf16x8, L)};
+}
+
+// dst plane p [rows, cols] (ldd) = term p of src (transposed: src is [cols, rows]).
+// One thread per output pair (2 consecutive columns).
+__global__ __launch_bounds__(256) void split3_planes(int64_t rows, int64_t cols, const float *__restrict__ src,
+                                                     int64_t lds, int32_t transpose, uint16_t *__restrict__ dst,
+                                                     int64_t ldd, int64_t ps) {
+  const int64_t cp = (cols + 1) / 2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows * cp; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cp, c = 2 * (i % cp);
+    const bool two = c + 1 < cols;
+    float x = transpose ? src[c * lds + r] : src[r * lds + c];
+    float y = two ? (transpose ? src[(c + 1) * lds + r] : src[r * lds + c + 1]) : 0.f;
+    const unsigned h = split_lvl(x, y), m = split_lvl(x, y), l = pk_bf16(x, y);
+    uint16_t *d = dst + r * ldd + c;
+    d[0] = (uint16_t)h;
+    d[ps] = (uint16_t)m;
+    d[2 * ps] = (uint16_t)l;
+    if (two) {
+      d[1] = (uint16_t)(h >> 16);
+      d[ps + 1] = (uint16_t)(m >> 16);
+      d[2 * ps + 1] = (uint16_t)(l >> 16);
+    }
+  }
+}
+
+__device__ __forceinline__ int swzA(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }  // 128-B rows
+__device__ __forceinline__ int swzW(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }  // 64-B rows
+
+template <int WM, int WN, int TM, int TN, bool RELU>
+__global__ __launch_bounds__(64 * WM * WN) void fc_fwd_x3(X3Args a) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int A_BYTES = BM * BK * 4, WP_BYTES = BN * BK * 2;  // A image, one W plane image
+  constexpr int TILE_BYTES = A_BYTES + 3 * WP_BYTES;
+  constexpr int PA = BM / 8 / NW;            // A pieces (8 rows x 128 B) per wave
+  constexpr int PB = 3 * (BN / 16) / NW;     // W pieces (16 rows x 64 B, all planes) per wave
+  static_assert(BM % (8 * NW) == 0 && (3 * BN / 16) % NW == 0, "tile rows must split into whole pieces per wave");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
+
+  const int64_t nwg = a.mt * a.nt;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
+  const int64_t m0 = (wgid / a.nt) * BM;
+  const int64_t n0 = (wgid % a.nt) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nk1 = (int)(a.K1 / BK);
+  const int nk = nk1 + (int)(a.K2 / BK);
+
+  const float *srcA1[PA], *srcA2[PA];
+  const uint16_t *srcW1[PB], *srcW2[PB];
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int row = (wave + NW * p) * 8 + (lane >> 3);
+    int64_t gr = m0 + row;
+    gr = gr < a.M ? gr : a.M - 1;  // rows past M feed outputs that are never stored
+    const int off = swzA(row, lane & 7) * 4;
+    srcA1[p] = a.A1 + gr * a.lda1 + off;
+    srcA2[p] = a.A2 + gr * a.lda2 + off;
+  }
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    const int q = wave + NW * p, plane = q / (BN / 16);
+    const int row = (q % (BN / 16)) * 16 + (lane >> 2);
+    int64_t gn = n0 + row;
+    gn = gn < a.N ? gn : a.N - 1;
+    const int off = swzW(row, lane & 3) * 8;
+    srcW1[p] = a.W1 + plane * a.ps1 + gn * a.ldw1 + off;
+    srcW2[p] = a.W2 + plane * a.ps2 + gn * a.ldw2 + off;
+  }
+  auto stage = [&](int b, int t) {
+    typedef __attribute__((address_space(3))) unsigned char lds_t;
+    unsigned char *base = smem + b * TILE_BYTES;
+    const bool p2 = t >= nk1;
+    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
+#pragma unroll
+    for (int p = 0; p < PA; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcA2[p] : srcA1[p]) + k0),
+                                       (lds_t *)(base + (wave + NW * p) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcW2[p] : srcW1[p]) + k0),
+                                       (lds_t *)(base + A_BYTES + (wave + NW * p) * 1024), 16, 0, 0);
+  };
+
+  f32x16 accH[TM][TN], accL[TM][TN];
+  const f32x16 zero = {};
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) accH[i][j] = accL[i][j] = zero;
+
+  const int fr = lane & 31, fk = lane >> 5;
+  const int rA0 = wm * TM * 32 + fr, rB0 = wn * TN * 32 + fr;
+
+  if (nk > 0) stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int b = 0;
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) stage(b ^ 1, t + 1);
+    const unsigned char *T = smem + b * TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {  // lane half fk feeds k = 16 s + 8 fk + 0..7 of one 32x32x16 MFMA
+      Split3 av[TM];
+      bf16x8 bv[TN][3];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const unsigned char *ra = T + (rA0 + i * 32) * (BK * 4);
+        av[i] = split3(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 32, 4 * s + 2 * fk) * 16),
+                       *reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 32, 4 * s + 2 * fk + 1) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bv[j][p] = *reinterpret_cast<const bf16x8 *>(T + A_BYTES + p * WP_BYTES + (rB0 + j * 32) * (BK * 2) +
+                                                       swzW(rB0 + j * 32, 2 * s + fk) * 16);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].l, bv[j][0], accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].m, bv[j][1], accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].h, bv[j][2], accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].m, bv[j][0], accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].h, bv[j][1], accL[i][j], 0, 0, 0);
+          accH[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].h, bv[j][0], accH[i][j], 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile t+1 landed; every wave done with tile t
+    asm volatile("" ::: "memory");
+    b ^= 1;
+  }
+
+  // Epilogue.  32x32 MFMA output map: col = lane & 31, row = 4 (lane >> 5) + (r & 3) + 8 (r >> 2).
+  // With the accumulate flag every C load is issued before the first store.
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = accH[i][j] + accL[i][j];
+  const int64_t mw = m0 + wm * TM * 32, nw = n0 + wn * TN * 32;
+  if (a.accum) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int64_t col = nw + j * 32 + (lane & 31);
+      col = col < a.N ? col : a.N - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int64_t row = mw + i * 32 + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2);
+          row = row < a.M ? row : a.M - 1;
+          acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
+        }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = nw + j * 32 + (lane & 31);
+    if (col >= a.N) continue;
+    const float bb = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int64_t rbase = mw + i * 32 + 4 * (lane >> 5);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row >= a.M) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v = v + bb;
+        if (RELU) v = (v < 0.f) ? 0.f : v;
+        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        a.C[row * a.ldc + col] = v;
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN>
+lpg_status launch_x3(X3Args a, bool relu, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int64_t nwg = a.mt * a.nt;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_fwd_x3<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_fwd_x3<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+int g_x3_variant = 0;
+
+}  // namespace
+}  // namespace lpg
+
+using namespace lpg;
+
+extern "C" lpg_status lpg_split3_f32(int64_t rows, int64_t cols, const float *src, int64_t lds, int32_t transpose,
+                                     uint16_t *dst, int64_t ldd, int64_t plane_stride, void *stream) {
+  LPG_REQUIRE(rows >= 0 && cols >= 0, "lpg_split3_f32: negative size");
+  if (rows == 0 || cols == 0) return LPG_OK;
+  LPG_REQUIRE(src && dst, "lpg_split3_f32: NULL pointer");
+  LPG_REQUIRE(lds >= (transpose ? rows : cols) && ldd >= cols && plane_stride >= rows * ldd,
+              "lpg_split3_f32: bad leading dimension / plane stride");
+  int64_t blocks = (rows * ((cols + 1) / 2) + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(split3_planes, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), rows, cols, src, lds,
+                     transpose, dst, ldd, plane_stride);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                    const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                    int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
+                                    float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                                    void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_f32: negative size");
+  if (M == 0 || N == 0) return LPG_OK;
+  LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_x3_f32: bad C/ldc");
+  LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "lpg_fc_x3_f32: K1, K2 must be multiples of %d (zero-pad)", BK);
+  LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1 && ps1 >= N * ldw1), "lpg_fc_x3_f32: bad A1/W1");
+  LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2 && ps2 >= N * ldw2), "lpg_fc_x3_f32: bad A2/W2");
+  LPG_REQUIRE(lda1 % 4 == 0 && ldw1 % 8 == 0 && ps1 % 8 == 0 &&
+                  (K2 == 0 || (lda2 % 4 == 0 && ldw2 % 8 == 0 && ps2 % 8 == 0)) &&
+                  (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
+              "lpg_fc_x3_f32: A rows must be 16-byte aligned (lda multiple of 4), W planes 16-byte aligned "
+              "(ldw and plane stride multiples of 8)");
+  LPG_REQUIRE((flags & ~3) == 0, "lpg_fc_x3_f32: unknown flags 0x%x", flags);
+  LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_x3_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
+  X3Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, ps1, ps2, C, ldc, 0, 0, seed, 0u, 1.f,
+           (flags >> 1) & 1};
+  dropout_params(dropout_p, &a.drop_thresh, &a.drop_scale);
+  hipStream_t s = as_stream(stream);
+  const bool relu = flags & 1;
+  switch (g_x3_variant) {
+    case 1: return launch_x3<4, 2, 2, 2>(a, relu, s);  // 256 x 128, 8 waves
+    case 2: return launch_x3<2, 4, 2, 2>(a, relu, s);  // 128 x 256, 8 waves
+    default: return launch_x3<2, 2, 2, 2>(a, relu, s);  // 128 x 128, 4 waves
+  }
+}
+
+extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
+  LPG_REQUIRE(v >= 0 && v <= 2, "lpg_fc_x3_set_variant: variant %d not in [0, 2]", v);
+  g_x3_variant = v;
+  return LPG_OK;
+}

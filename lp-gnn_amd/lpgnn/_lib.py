@@ -33,6 +33,9 @@ HEADER_SYMBOLS = (
     "lpg_fc_set_variant",
     "lpg_fc_bf16",
     "lpg_fc_bf16_set_variant",
+    "lpg_split3_f32",
+    "lpg_fc_x3_f32",
+    "lpg_fc_x3_set_variant",
     "lpg_relu_dropout_bwd_f32",
     "lpg_relu_bwd_colsum_workspace_bytes",
     "lpg_relu_bwd_colsum_f32",
@@ -94,6 +97,13 @@ def lib() -> ctypes.CDLL:
                              c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_p]
     L.lpg_fc_f32.restype = c_i32
     L.lpg_fc_bf16.argtypes = L.lpg_fc_f32.argtypes
+    L.lpg_split3_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_i64, c_p]
+    L.lpg_split3_f32.restype = c_i32
+    L.lpg_fc_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
+                                c_i64, c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_p]
+    L.lpg_fc_x3_f32.restype = c_i32
+    L.lpg_fc_x3_set_variant.argtypes = [c_i32]
+    L.lpg_fc_x3_set_variant.restype = c_i32
     L.lpg_fc_bf16.restype = c_i32
     L.lpg_fc_bf16_set_variant.argtypes = [c_i32]
     L.lpg_fc_bf16_set_variant.restype = c_i32

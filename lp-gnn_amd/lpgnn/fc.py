@@ -21,6 +21,8 @@ parity for gradients.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import Tensor
@@ -46,14 +48,19 @@ def _pad_k(t: Tensor, mult: int = 4) -> Tensor:
     return t if k % mult == 0 else F.pad(t, (0, mult - k % mult))
 
 
+# fp32 FC arithmetic: "fp32" = the exact fp32 MFMA kernel (bitwise contract of oracle/fc_ref.c),
+# "x3" = fp32 on the bf16 matrix cores through the exact three-way bf16 split (lpg_fc_f32 flag 4).
+ARITH = os.environ.get("LPGNN_FC_ARITH", "fp32")
+
 _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless the narrow-input kernel applies
 
 
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
-               accumulate: bool = False) -> Tensor:
+               accumulate: bool = False, arith: str | None = None) -> Tensor:
     """act(A1 W1^T + A2 W2^T [+ out] + bias) through lpg_fc_f32; with
-    ``accumulate`` the caller's ``out`` holds the addend and is overwritten."""
+    ``accumulate`` the caller's ``out`` holds the addend and is overwritten.
+    ``arith`` ("fp32" | "x3", default ``ARITH``) picks the tiled kernel's arithmetic."""
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -79,6 +86,8 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0)
+    if (arith or ARITH) == "x3" and not small and N > 32:
+        return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu)
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
         st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
@@ -88,6 +97,43 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
                           float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_f32")
+    return C
+
+
+def split3(W: Tensor, transpose: bool = False) -> Tensor:
+    """The exact three-way bf16 split of an fp32 matrix (lpg_split3_f32):
+    int16 [3, R, C] holding the bf16 terms t0 + t1 + t2 = S exactly, S = W or
+    W^T; C padded to a multiple of 8 (zero terms)."""
+    W = W.detach()
+    if W.dtype != torch.float32:
+        raise RuntimeError(f"lpgnn split3: fp32 only, got {W.dtype}")
+    if W.stride(-1) != 1:
+        W = W.contiguous()
+    R, Cc = (W.shape[1], W.shape[0]) if transpose else W.shape
+    ld = -(-Cc // 8) * 8
+    out = torch.zeros((3, R, ld), dtype=torch.int16, device=W.device) if ld != Cc else \
+        torch.empty((3, R, ld), dtype=torch.int16, device=W.device)
+    with torch.cuda.device(W.device):
+        st = _lib.lib().lpg_split3_f32(R, Cc, W.data_ptr(), W.stride(0), 1 if transpose else 0, out.data_ptr(),
+                                       ld, R * ld, _lib.stream_of(W))
+    _lib.check(st, "lpg_split3_f32")
+    return out
+
+
+def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=None, W2s=None):
+    """lpg_fc_x3_f32 on fp32 A and pre-split W (split here unless given)."""
+    W1s = split3(W1) if W1s is None else W1s
+    W2s = (split3(W2) if W2s is None else W2s) if K2 else None
+    L = _lib.lib()
+    with torch.cuda.device(A1.device):
+        tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, ("relu" if relu else "lin") + "-x3"))
+        st = L.lpg_fc_x3_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1s.data_ptr(), W1s.stride(1),
+                             W1s.stride(0), K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
+                             None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0,
+                             W2s.stride(0) if K2 else 0, None if bias is None else bias.data_ptr(), C.data_ptr(),
+                             C.stride(0), flags, float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_fc_x3_f32")
     return C
 
 

@@ -1,0 +1,152 @@
+"""fp32 FC on the bf16 matrix cores (lpg_fc_x3_f32, lpg_split3_f32): exact
+split, fp32-GEMM accuracy against fp64 beside the exact-fp32 kernel, and the
+epilogue (bias, ReLU, accumulate, fused dropout) semantics."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+# Error bound of the three-way split (csrc/fc_x3.hip): every dropped term is
+# <= 2^-23 |a b| and the fp32 accumulation of K products rounds like an fp32
+# GEMM; we require |y - y64| <= 16 * 2^-24 * sum_k |a_k b_k| + 2^-24 |y64|
+# (observed maxima are ~3x below this at K = 2048; an exact-fp32 sequential
+# chain is bounded by K * 2^-24 * sum|ab|, 128x looser).
+U = 2.0 ** -24
+
+
+def _bf16_bits_to_f64(t):
+    return (t.to(torch.int32) & 0xFFFF).bitwise_left_shift(16).view(torch.float32).double()
+
+
+@pytest.mark.parametrize("transpose", [False, True])
+def test_split3_is_exact(transpose):
+    from lpgnn.fc import split3
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(67, 45, generator=g) * torch.logspace(-20, 20, 45)
+    x[0, :5] = torch.tensor([0.0, -0.0, 1.0, -3.0e38, 1.1754944e-38])
+    x[1, :3] = torch.tensor([float(np.float32(1 + 2 ** -23)), 2 ** -126, float(np.nextafter(np.float32(1), 2))])
+    s = split3(x.to(DEV), transpose=transpose).cpu()
+    want = (x.t() if transpose else x).double()
+    R, C = want.shape
+    assert s.shape[0] == 3 and s.shape[1] == R and s.shape[2] >= C
+    parts = [_bf16_bits_to_f64(s[p, :, :C]) for p in range(3)]
+    assert torch.equal(parts[0] + parts[1] + parts[2], want)
+    # term sizes: |t1| <= 2^-8 |x|, |t2| <= 2^-16 |x|
+    assert (parts[1].abs() <= want.abs() * 2 ** -8).all()
+    assert (parts[2].abs() <= want.abs() * 2 ** -16).all()
+    # padded columns are zero terms
+    if s.shape[2] > C:
+        assert (s[:, :, C:] == 0).all()
+
+
+def _ref64(A1, W1, A2, W2, b, relu):
+    y = A1.double() @ W1.double().t()
+    s = A1.double().abs() @ W1.double().abs().t()
+    if A2 is not None:
+        y += A2.double() @ W2.double().t()
+        s += A2.double().abs() @ W2.double().abs().t()
+    if b is not None:
+        y += b.double()
+    if relu:
+        y = y.relu()
+    return y, s
+
+
+@pytest.mark.parametrize("M,N,K1,K2,relu,bias", [
+    (1000, 1024, 1024, 1024, True, True),  # hidden layer
+    (4096, 1024, 1024, 0, False, False),   # re-associated lin_rel GEMM / input gradient
+    (129, 130, 64, 32, False, True),       # ragged tiles
+    (257, 96, 2048, 0, True, True),
+    (1, 33, 32, 32, True, True),
+    (300, 200, 96, 0, False, True),
+])
+def test_x3_accuracy_vs_fp64(M, N, K1, K2, relu, bias):
+    from lpgnn.fc import fc_forward
+
+    g = torch.Generator().manual_seed(M + 3 * N)
+    A1 = torch.randn(M, K1, generator=g)
+    W1 = torch.randn(N, K1, generator=g) * 0.05
+    A2 = torch.randn(M, K2, generator=g) if K2 else None
+    W2 = torch.randn(N, K2, generator=g) * 0.05 if K2 else None
+    b = torch.randn(N, generator=g) if bias else None
+    t = lambda x: None if x is None else x.to(DEV)
+    y = fc_forward(t(A1), t(W1), t(A2), t(W2), t(b), relu, arith="x3").cpu().double()
+    y32 = fc_forward(t(A1), t(W1), t(A2), t(W2), t(b), relu, arith="fp32").cpu().double()
+    ref, s = _ref64(A1, W1, A2, W2, b, relu)
+    bound = 16 * U * s + U * ref.abs() + 1e-30
+    err = (y - ref).abs()
+    assert (err <= bound).all(), f"max err/bound {(err / bound).max().item():.3f}"
+    # and in the same error class as the exact-fp32 kernel (blocked fma chains)
+    e32 = (y32 - ref).abs()
+    assert err.mean().item() <= 4 * e32.mean().item() + 1e-12
+
+
+def test_x3_variants_identical():
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward
+
+    g = torch.Generator().manual_seed(5)
+    A1, A2 = torch.randn(700, 256, generator=g).to(DEV), torch.randn(700, 128, generator=g).to(DEV)
+    W1, W2 = torch.randn(300, 256, generator=g).to(DEV), torch.randn(300, 128, generator=g).to(DEV)
+    b = torch.randn(300, generator=g).to(DEV)
+    L = _lib.lib()
+    outs = []
+    for v in (0, 1, 2):
+        L.lpg_fc_x3_set_variant(v)
+        outs.append(fc_forward(A1, W1, A2, W2, b, True, arith="x3"))
+    L.lpg_fc_x3_set_variant(0)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_x3_accumulate(relu):
+    """flags bit 1: C = act(A W^T + C + b), the addend read before the store."""
+    from lpgnn.fc import fc_forward
+
+    g = torch.Generator().manual_seed(9)
+    M, N, K = 333, 160, 96
+    A = torch.randn(M, K, generator=g).to(DEV)
+    W = torch.randn(N, K, generator=g).to(DEV) * 0.1
+    P = torch.randn(M, N, generator=g).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    plain = fc_forward(A, W, None, None, None, False, arith="x3")
+    C = P.clone()
+    got = fc_forward(A, W, None, None, b, relu, out=C, accumulate=True, arith="x3")
+    assert got.data_ptr() == C.data_ptr()
+    want = plain + P + b
+    if relu:
+        want = want.relu()
+    assert torch.equal(got, want)
+
+
+def test_x3_dropout_mask_matches_fp32_kernel():
+    """Same counter-based mask as the exact kernel (the backward relies on
+    kept <=> output > 0 for every FC variant)."""
+    from lpgnn.fc import fc_forward
+
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 513, 256, 64
+    A = torch.randn(M, K, generator=g).to(DEV)
+    W = torch.randn(N, K, generator=g).to(DEV) * 0.2
+    b = torch.full((N,), 5.0, device=DEV)  # every pre-dropout value > 0
+    y3 = fc_forward(A, W, None, None, b, True, 0.3, 1234, arith="x3")
+    y32 = fc_forward(A, W, None, None, b, True, 0.3, 1234, arith="fp32")
+    assert torch.equal(y3 == 0, y32 == 0)
+    kept = (y3 != 0).float().mean().item()
+    assert 0.66 < kept < 0.74
+    torch.testing.assert_close(y3, y32, rtol=1e-5, atol=1e-5)
+
+
+def test_x3_rejects_bad_shapes():
+    from lpgnn import _lib
+
+    L = _lib.lib()
+    a = torch.zeros(4, 40, device=DEV)
+    w = torch.zeros(3, 4, 40, dtype=torch.int16, device=DEV)
+    c = torch.zeros(4, 4, device=DEV)
+    st = L.lpg_fc_x3_f32(4, 4, 40, a.data_ptr(), 40, w.data_ptr(), 40, 160, 0, None, 0, None, 0, 0, None,
+                         c.data_ptr(), 4, 0, 0.0, 0, None)
+    assert st != 0 and b"multiples of 32" in L.lpg_last_error()

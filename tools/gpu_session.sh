@@ -33,7 +33,7 @@ step() {  # step <name> <timeout> <cmd...>
 rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > "$OUT/device.txt" || true
 for s in $STAGES; do
   case $s in
-    tests) step pytest_gpu 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py ;;
     prof)
