@@ -225,11 +225,14 @@ def main():
     nnz_of = lambda k: local_nnz  # every launch traverses the local graph's edges once
     esz = 2 if args.bf16 else 4
     bytes_total = sum(kern[k][0] * spmm_bytes(k[1], nnz_of(k), k[3], esz) for k in hid_keys)
-    # dense FC launches of hidden width (K = 2 * hid): MFMA utilisation
-    fc_keys = [k for k in kern if k[0] == "fc" and k[3] >= 2 * args.hids]
+    # dense GEMMs of hidden width on the hand-written kernels (FC forward + x3 input and weight
+    # gradients; K >= hid): MFMA utilisation.  x3 = fp32 through the exact three-way bf16 split,
+    # 6 bf16 MFMA products per fp32 product, so its MFMA-bound peak is the dense bf16 peak / 6.
+    fc_keys = [k for k in kern if k[0] in ("fc", "wgrad") and k[3] >= args.hids and k[2] >= 64]
+    x3 = any(str(k[4]).endswith("x3") for k in fc_keys)
     fc_flops = sum(kern[k][0] * 2.0 * k[1] * k[2] * k[3] for k in fc_keys)
     fc_ms = sum(kern[k][1] for k in fc_keys)
-    fc_peak = BF16_MFMA_PEAK_TFLOPS if args.bf16 else FP32_MFMA_PEAK_TFLOPS
+    fc_peak = BF16_MFMA_PEAK_TFLOPS if args.bf16 else (BF16_MFMA_PEAK_TFLOPS / 6 if x3 else FP32_MFMA_PEAK_TFLOPS)
     fc_tf = fc_flops / (fc_ms / 1e3) / 1e12 if fc_ms > 0 else 0.0
     edges_local = launches * local_nnz / args.steps  # per step
     t = torch.tensor([dt], device=dev)
@@ -269,7 +272,11 @@ def main():
                      "traffic_source": traffic_src},
         "fc_roofline": {"bound": "mfma", "achieved": fc_tf, "peak": fc_peak, "unit": "TFLOP/s",
                         "frac": fc_tf / fc_peak, "launches": sum(kern[k][0] for k in fc_keys),
-                        "kernel": "lpg fc_fwd_" + ("bf16" if args.bf16 else "f32") + " (hidden GraphConv FC, fwd)"},
+                        "kernel": ("lpg fc_fwd_bf16 (hidden GraphConv FC, fwd)" if args.bf16 else
+                                   "lpg fc_fwd_x3 + wgrad_x3 (hidden-width GEMMs, fwd + bwd; fp32 via exact "
+                                   "3-way bf16 split, peak = dense bf16 / 6)" if x3 else
+                                   "lpg fc_fwd_f32 (hidden GraphConv FC, fwd)"),
+                        "fp32_mfma_peak_frac": None if args.bf16 else fc_tf / FP32_MFMA_PEAK_TFLOPS},
         "spmm_directions": {
             ("cons<-vars" if (k[1], k[2]) == (args.m, args.n) and not distributed else
              "vars<-cons" if (k[1], k[2]) == (args.n, args.m) and not distributed else f"{k[1]}x{k[2]}"):

@@ -166,6 +166,17 @@ lpg_status lpg_fc_x3_f32(int64_t M, int64_t N,
 lpg_status lpg_split3_f32(int64_t rows, int64_t cols, const float *src, int64_t lds, int32_t transpose,
                           uint16_t *dst, int64_t ldd, int64_t plane_stride, void *stream);
 
+/* Weight gradient on the same arithmetic: dW[n, k] = sum_r G[r, n] X[r, k]
+ * (G = dZ [R, N], ldg; X = the layer input [R, K], ldx; dW [N, K], lddw, the
+ * torch Linear weight layout) -- the lin_rel / lin_root weight gradients of
+ * GraphConv's backward.  N, K and the leading dimensions multiples of 4
+ * floats, buffers 16-byte aligned.  R is split into contiguous ranges whose
+ * partial products go to `workspace` (lpg_wgrad_x3_workspace_bytes(R, N, K)
+ * bytes, 16-byte aligned) and are added in a fixed order: deterministic. */
+int64_t lpg_wgrad_x3_workspace_bytes(int64_t R, int64_t N, int64_t K);
+lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
+                            int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream);
+
 /* Tile choice for lpg_fc_x3_f32 (tuning): 0 = 128 x 128 (4 waves, 2 blocks
  * per CU), 1 = 256 x 128, 2 = 128 x 256 (8 waves). */
 lpg_status lpg_fc_x3_set_variant(int32_t v);

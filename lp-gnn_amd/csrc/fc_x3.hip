@@ -296,6 +296,182 @@ lpg_status launch_x3(X3Args a, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
+// ---- weight gradient dW = G^T X on the same arithmetic -----------------------
+//
+// dW[n, k] = sum_r G[r, n] X[r, k] (G = dZ [R, N], X = the layer input [R, K]:
+// the lin_rel / lin_root weight gradients of GraphConv, torch Linear layout).
+// Both operands are r-major, so a lane's 8 consecutive MFMA k (= rows r) of
+// one output row n are 8 separate dwords: the LDS image keeps the natural
+// 512-B rows (32 r-rows x 128 columns per operand and k-tile, LDS-DMA, no
+// swizzle needed: a ds_read_b32's two 32-lane halves each read 32 consecutive
+// dwords of one row -- conflict-free), each lane reads its 8 values with
+// ds_read_b32 and splits them (three bf16 terms, as above) in registers.
+// The output (N x K, 64 tiles at 1024^2) is far too small to fill 256 CUs, so
+// R is split into S contiguous ranges (whole 32-row chunks); block (tile, s)
+// writes its partial tile to workspace[s], and a fold kernel adds the S
+// partials in s order (deterministic, no atomics).  Rows past R are DMA'd
+// from a zeroed 512-B row at the end of the workspace.
+constexpr int WG_T = 128;  // output tile (n and k)
+
+__device__ __forceinline__ void wg_read8(const unsigned char *img, int col, int r0, float (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = *reinterpret_cast<const float *>(img + (r0 + e) * (WG_T * 4) + col * 4);
+}
+
+__device__ __forceinline__ Split3 split3_8(const float (&v)[8]) {
+  return split3(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]});
+}
+
+__global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
+                                                int64_t ldg, const float *__restrict__ X, int64_t ldx,
+                                                float *__restrict__ part, const float *__restrict__ zrow,
+                                                int64_t nt, int64_t kt, int64_t S, int64_t chunks_per_split) {
+  constexpr int OP_BYTES = 32 * WG_T * 4;  // one operand's k-tile image: 32 rows x 512 B
+  constexpr int TILE_BYTES = 2 * OP_BYTES;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
+
+  // block -> (split s, output tile); consecutive blocks share s (same rows of G and X in L2)
+  const int64_t bid = blockIdx.x;
+  const int64_t tiles = nt * kt;
+  const int64_t s = bid / tiles, tile = bid % tiles;
+  const int64_t n0 = (tile / kt) * WG_T, k0 = (tile % kt) * WG_T;
+  const int64_t nchunks = (R + 31) / 32;
+  const int64_t c0 = s * chunks_per_split;
+  const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // DMA: piece = 2 rows x 512 B; wave w moves pieces w, w+4, w+8, w+12 of G and of X
+  const float *srcG[4], *srcX[4], *srcZ;
+  int prow[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int piece = wave + 4 * p;
+    prow[p] = piece * 2 + (lane >> 5);
+    const int ch = lane & 31;
+    int64_t gn = n0 + ch * 4, gk = k0 + ch * 4;
+    gn = gn < N ? gn : N - 4;  // N, K multiples of 4: columns past the edge feed outputs never stored
+    gk = gk < K ? gk : K - 4;
+    srcG[p] = G + gn;
+    srcX[p] = X + gk;
+  }
+  srcZ = zrow + (lane & 31) * 4;
+  auto stage = [&](int b, int64_t c) {
+    typedef __attribute__((address_space(3))) unsigned char lds_t;
+    unsigned char *base = smem + b * TILE_BYTES;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int64_t r = c * 32 + prow[p];
+      const bool in = r < R;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(in ? srcG[p] + r * ldg : srcZ),
+                                       (lds_t *)(base + (wave + 4 * p) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(in ? srcX[p] + r * ldx : srcZ),
+                                       (lds_t *)(base + OP_BYTES + (wave + 4 * p) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 accH[2][2], accL[2][2];
+  const f32x16 zero = {};
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) accH[i][j] = accL[i][j] = zero;
+  const int fr = lane & 31, fk = lane >> 5;
+
+  auto body = [&](const unsigned char *T) {
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const int r0 = 16 * ss + 8 * fk;
+      Split3 bv[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float v[8];
+        wg_read8(T + OP_BYTES, wn * 64 + j * 32 + fr, r0, v);
+        bv[j] = split3_8(v);
+      }
+      // one A fragment's split live at a time (register pressure: 128 accumulators)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float v[8];
+        wg_read8(T, wm * 64 + i * 32 + fr, r0, v);
+        const Split3 av = split3_8(v);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.l, bv[j].h, accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv[j].m, accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv[j].l, accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv[j].h, accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv[j].m, accL[i][j], 0, 0, 0);
+          accH[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv[j].h, accH[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  if (c0 < c1) stage(0, c0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int b = 0;
+  for (int64_t c = c0; c < c1; ++c) {
+    if (c + 1 < c1) stage(b ^ 1, c + 1);
+    const unsigned char *T = smem + b * TILE_BYTES;
+    body(T);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    b ^= 1;
+  }
+
+  // partial tile -> part[s] ([N, K] row-major); 32x32 output map: col = lane & 31,
+  // row = 4 (lane >> 5) + (r & 3) + 8 (r >> 2)
+  float *P = part + s * N * K;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t col = k0 + wn * 64 + j * 32 + (lane & 31);
+    if (col >= K) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t rbase = n0 + wm * 64 + i * 32 + 4 * (lane >> 5);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
+      }
+    }
+  }
+}
+
+// dW[n, k] = sum_s part[s][n, k], s ascending (fixed order), float4 per thread
+__global__ __launch_bounds__(256) void wgrad_fold(int64_t N, int64_t K, int64_t S, const float *__restrict__ part,
+                                                  float *__restrict__ dW, int64_t lddw) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t k4 = K / 4;
+  if (i4 >= N * k4) return;
+  const int64_t n = i4 / k4, k = (i4 % k4) * 4;
+  float4 acc = *reinterpret_cast<const float4 *>(part + n * K + k);
+  for (int64_t s = 1; s < S; ++s) {
+    const float4 v = *reinterpret_cast<const float4 *>(part + s * N * K + n * K + k);
+    acc.x = acc.x + v.x;
+    acc.y = acc.y + v.y;
+    acc.z = acc.z + v.z;
+    acc.w = acc.w + v.w;
+  }
+  *reinterpret_cast<float4 *>(dW + n * lddw + k) = acc;
+}
+
+int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
+  const int64_t tiles = ((N + WG_T - 1) / WG_T) * ((K + WG_T - 1) / WG_T);
+  const int64_t nchunks = (R + 31) / 32;
+  int64_t S = (2048 + tiles - 1) / tiles;  // aim at >= 2048 blocks (8 per CU)
+  const int64_t maxS = nchunks / 8 > 1 ? nchunks / 8 : 1;  // >= 8 chunks (256 rows) per split
+  if (S > maxS) S = maxS;
+  if (S > 64) S = 64;
+  return S < 1 ? 1 : S;
+}
+
 int g_x3_variant = 0;
 
 }  // namespace
@@ -351,5 +527,43 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
 extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
   LPG_REQUIRE(v >= 0 && v <= 2, "lpg_fc_x3_set_variant: variant %d not in [0, 2]", v);
   g_x3_variant = v;
+  return LPG_OK;
+}
+
+extern "C" int64_t lpg_wgrad_x3_workspace_bytes(int64_t R, int64_t N, int64_t K) {
+  if (R <= 0 || N <= 0 || K <= 0) return 0;
+  return wgrad_splits(R, N, K) * N * K * (int64_t)sizeof(float) + 512;  // + the zero row
+}
+
+extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
+                                       int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream) {
+  LPG_REQUIRE(R >= 0 && N >= 0 && K >= 0, "lpg_wgrad_x3_f32: negative size");
+  if (N == 0 || K == 0) return LPG_OK;
+  LPG_REQUIRE(dW && lddw >= K && lddw % 4 == 0 && aligned16(dW), "lpg_wgrad_x3_f32: bad dW/lddw");
+  if (R == 0) {
+    LPG_HIP(hipMemset2DAsync(dW, lddw * sizeof(float), 0, K * sizeof(float), N, as_stream(stream)));
+    return LPG_OK;
+  }
+  LPG_REQUIRE(G && X && workspace, "lpg_wgrad_x3_f32: NULL pointer");
+  LPG_REQUIRE(N % 4 == 0 && K % 4 == 0 && ldg >= N && ldx >= K && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) &&
+                  aligned16(X) && aligned16(workspace),
+              "lpg_wgrad_x3_f32: N, K and leading dimensions must be multiples of 4 floats, buffers 16-byte aligned");
+  const int64_t nt = (N + WG_T - 1) / WG_T, kt = (K + WG_T - 1) / WG_T;
+  const int64_t S = wgrad_splits(R, N, K);
+  const int64_t nchunks = (R + 31) / 32;
+  const int64_t cps = (nchunks + S - 1) / S;
+  const int64_t S_used = (nchunks + cps - 1) / cps;
+  const int64_t nblk = S_used * nt * kt;
+  LPG_REQUIRE(nblk < (int64_t)1 << 31, "lpg_wgrad_x3_f32: grid too large");
+  float *part = reinterpret_cast<float *>(workspace);
+  float *zrow = part + S * N * K;  // 128 zero floats after the partials (lpg_wgrad_x3_workspace_bytes)
+  hipStream_t st = as_stream(stream);
+  LPG_HIP(hipMemsetAsync(zrow, 0, 512, st));
+  hipLaunchKernelGGL(wgrad_x3, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow, nt, kt,
+                     S_used, cps);
+  LPG_HIP(hipGetLastError());
+  const int64_t n4 = N * (K / 4);
+  hipLaunchKernelGGL(wgrad_fold, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, N, K, S_used, part, dW, lddw);
+  LPG_HIP(hipGetLastError());
   return LPG_OK;
 }

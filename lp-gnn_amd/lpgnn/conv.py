@@ -43,7 +43,7 @@ from torch import Tensor
 from . import fc as _fc
 from .sparse import BipartiteCSR, CSR, spmm_forward
 
-_GEMM_FLOPS = 120e12  # in-step rates used only to pick the cheaper association
+_GEMM_FLOPS = 160e12  # in-step rates used only to pick the cheaper association
 _SPMM_BYTES = 7e12
 # LPGNN_OVERLAP=1: run the HBM-bound SpMMs that are independent of the current FC / GEMM on a
 # second stream beside it.  Measured on c2: ~1 ms (2.6 %) more whole-step throughput, but the
@@ -183,6 +183,10 @@ class _TwoDirection(torch.autograd.Function):
         t_r, tsrc_r, relt_r = plan(AT, A, dz_r, left, w_rel_l2r, agg_r, need[0], need[3])
         t_l, tsrc_l, relt_l = plan(A, AT, dz_l, right, w_rel_r2l, agg_l, need[1], need[6])
 
+        # fp32: the x3 kernels (weight gradient G^T X, input gradient G W) unless LPGNN_FC_ARITH=fp32
+        wg = (lambda g, x: (g.t() @ x).float()) if bf16 else _fc.wgrad
+        ig = None if bf16 else _fc.input_grad
+
         def wgrads(dz, agg, x_dst, need_rel, need_root):
             if not (need_rel or need_root):
                 return None, None
@@ -190,8 +194,8 @@ class _TwoDirection(torch.autograd.Function):
             if not bf16 and agg is not None and k <= 16 and dz.shape[1] % 4 == 0:  # conv1: dZ read once
                 d_rel, d_root = _fc.wgrad_smallk(dz, agg, x_dst)
             else:
-                d_rel = (dz.t() @ agg).float() if need_rel else None
-                d_root = (dz.t() @ x_dst).float() if need_root else None
+                d_rel = wg(dz, agg) if need_rel else None
+                d_root = wg(dz, x_dst) if need_root else None
             return (d_rel if need_rel else None), (d_root if need_root else None)
 
         dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r, right, need[3] and not relt_r, need[5])
@@ -202,21 +206,24 @@ class _TwoDirection(torch.autograd.Function):
                 if t is not None:
                     t.record_stream(main)
         if relt_r:
-            dw_rel_l2r = (t_r.t() @ left).float()
+            dw_rel_l2r = wg(t_r, left)
         if relt_l:
-            dw_rel_r2l = (t_l.t() @ right).float()
+            dw_rel_r2l = wg(t_l, right)
 
-        def src_grad(St, dz, w_rel, T, t_src):
-            """S^T (dZ W_rel) in the cheaper association."""
-            return T @ w_rel if t_src else spmm_forward(St, dz @ w_rel)
+        def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root):
+            """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients)."""
+            if ig is None:
+                g = T @ w_rel if t_src else spmm_forward(St, dz @ w_rel)
+                return g.addmm_(dz_root, w_root)
+            if t_src:  # both terms over the same rows: one two-part GEMM
+                return ig(T, w_rel, dz_root, w_root)
+            return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True)
 
         g_l = g_r = None
         if need[1]:  # right = src of right2left (S = A), dst of left2right
-            g_r = src_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l)
-            g_r.addmm_(dz_r, w_root_l2r)
+            g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r)
         if need[0]:  # left = src of left2right (S = A^T), dst of right2left
-            g_l = src_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r)
-            g_l.addmm_(dz_l, w_root_r2l)
+            g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l)
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 

@@ -50,7 +50,7 @@ def _pad_k(t: Tensor, mult: int = 4) -> Tensor:
 
 # fp32 FC arithmetic: "fp32" = the exact fp32 MFMA kernel (bitwise contract of oracle/fc_ref.c),
 # "x3" = fp32 on the bf16 matrix cores through the exact three-way bf16 split (lpg_fc_f32 flag 4).
-ARITH = os.environ.get("LPGNN_FC_ARITH", "fp32")
+ARITH = os.environ.get("LPGNN_FC_ARITH", "x3")
 
 _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless the narrow-input kernel applies
 
@@ -135,6 +135,55 @@ def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_x3_f32")
     return C
+
+
+def wgrad(G: Tensor, X: Tensor, arith: str | None = None) -> Tensor:
+    """G^T X (the weight gradient dZ^T x of a Linear, [N, K]) in fp32:
+    lpg_wgrad_x3_f32 (deterministic split-R reduction) or, with arith
+    "fp32", the library GEMM (hipBLASLt)."""
+    if (arith or ARITH) != "x3" or G.shape[1] % 4 or X.shape[1] % 4:
+        return G.t() @ X
+    G, X = _prep(G), _prep(X)
+    R, N, K = G.shape[0], G.shape[1], X.shape[1]
+    L = _lib.lib()
+    dW = torch.empty((N, K), dtype=torch.float32, device=G.device)
+    ws = torch.empty(max(1, L.lpg_wgrad_x3_workspace_bytes(R, N, K)), dtype=torch.uint8, device=G.device)
+    with torch.cuda.device(G.device):
+        tok = TIMER.start(("wgrad", R, N, K, "x3"))
+        st = L.lpg_wgrad_x3_f32(R, N, K, G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), dW.data_ptr(),
+                                dW.stride(0), ws.data_ptr(), _lib.stream_of(G))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_wgrad_x3_f32")
+    return dW
+
+
+def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | None = None,
+               out: Tensor | None = None, accumulate: bool = False, arith: str | None = None) -> Tensor:
+    """G1 W1 [+ G2 W2] [+ out] for Linear weights W [out, in] (the input
+    gradient of lin_rel / lin_root): the x3 FC kernel with the weights split
+    transposed, or the library GEMMs with arith "fp32"."""
+    if (arith or ARITH) != "x3" or G1.shape[1] % 32 or (G2 is not None and G2.shape[1] % 32) \
+            or W1.shape[1] <= 32:
+        r = out if accumulate else None
+        if r is None:
+            r = G1 @ W1
+        else:
+            r.addmm_(G1, W1)
+        if G2 is not None:
+            r.addmm_(G2, W2)
+        if out is not None and r is not out:
+            out.copy_(r)
+            r = out
+        return r
+    G1, G2 = _prep(G1), _prep(G2)
+    M, N = G1.shape[0], W1.shape[1]
+    if out is None:
+        if accumulate:
+            raise RuntimeError("lpgnn input_grad: accumulate needs the addend in `out`")
+        out = torch.empty((M, N), dtype=torch.float32, device=G1.device)
+    K2 = 0 if G2 is None else G2.shape[1]
+    return _fc_x3(M, N, G1, None, G2, None, K2, None, out, 2 if accumulate else 0, 0.0, 0, False,
+                  W1s=split3(W1, transpose=True), W2s=split3(W2, transpose=True) if K2 else None)
 
 
 _BF16_BK = 64  # lpg_fc_bf16's k-tile: K1, K2 are zero-padded to a multiple of it

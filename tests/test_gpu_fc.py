@@ -10,6 +10,15 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
+@pytest.fixture(autouse=True)
+def _exact_fp32(monkeypatch):
+    """These tests pin the exact-fp32 kernel's bitwise contract (fc_ref.c);
+    the default x3 arithmetic is tested in test_gpu_x3.py."""
+    from lpgnn import fc
+
+    monkeypatch.setattr(fc, "ARITH", "fp32")
+
+
 @pytest.mark.parametrize("M,N,K1,K2,relu,bias", [
     (1, 1, 4, 0, False, True),
     (37, 3, 1024, 0, False, True),        # heads

@@ -86,10 +86,11 @@ def test_forward_bitwise_vs_kchain_oracle(depth, hids, reassoc, monkeypatch):
     with the re-associated left2right (conv.py's association rule) and with
     the reference's association everywhere."""
     from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
-    from lpgnn import conv
+    from lpgnn import conv, fc
     from lpgnn.val import inference_gnn
 
     monkeypatch.setattr(conv, "REASSOCIATE", reassoc)
+    monkeypatch.setattr(fc, "ARITH", "fp32")  # the exact-fp32 FC kernel (the bitwise contract)
 
     g = synth.uniform_lp(1500, 3000, 30000, seed=4)
     torch.manual_seed(0)
@@ -111,10 +112,14 @@ def test_forward_bitwise_vs_kchain_oracle(depth, hids, reassoc, monkeypatch):
     assert torch.equal(got, O.inference_gnn(torch.cat((rc, rv)), g.m))
 
 
+@pytest.mark.parametrize("arith", ["x3", "fp32"])
 @pytest.mark.parametrize("depth,hids", [(3, 1024), (4, 256)])
-def test_random_graph_vs_oracle(depth, hids):
-    """Mid-size synthetic LP, eval-mode logits vs the oracle fp32 CPU path."""
-    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+def test_random_graph_vs_oracle(depth, hids, arith, monkeypatch):
+    """Mid-size synthetic LP, eval-mode logits vs the oracle fp32 CPU path
+    (MKL F.linear, the reference's own evaluation), for both FC arithmetics."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, fc, synth
+
+    monkeypatch.setattr(fc, "ARITH", arith)
 
     g = synth.uniform_lp(2000, 4000, 40000, seed=3)
     torch.manual_seed(0)
@@ -141,13 +146,16 @@ def test_random_graph_vs_oracle(depth, hids):
     assert int((~clear).sum()) <= 2, "unexpectedly many near-ties"
 
 
-def test_training_step_runs_and_matches_oracle_grads():
-    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+@pytest.mark.parametrize("arith,hids", [("x3", 128), ("fp32", 128), ("x3", 1024)])
+def test_training_step_runs_and_matches_oracle_grads(arith, hids, monkeypatch):
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, fc, synth
     from lpgnn.train import balanced, make_optimizer, train_step
+
+    monkeypatch.setattr(fc, "ARITH", arith)
 
     g = synth.uniform_lp(1000, 2000, 20000, seed=5)
     torch.manual_seed(0)
-    model = GCN_FC(8, 8, hids=128, depth=3, dp=0.0).to(DEV)
+    model = GCN_FC(8, 8, hids=hids, depth=3, dp=0.0).to(DEV)
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
     batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),

@@ -150,3 +150,62 @@ def test_x3_rejects_bad_shapes():
     st = L.lpg_fc_x3_f32(4, 4, 40, a.data_ptr(), 40, w.data_ptr(), 40, 160, 0, None, 0, None, 0, 0, None,
                          c.data_ptr(), 4, 0, 0.0, 0, None)
     assert st != 0 and b"multiples of 32" in L.lpg_last_error()
+
+
+@pytest.mark.parametrize("R,N,K", [
+    (4096, 1024, 1024),   # hidden-layer weight gradient shape (fewer rows)
+    (1000, 256, 128),     # R not a multiple of the 32-row chunk
+    (37, 132, 260),       # ragged output tiles, a single partial chunk
+    (0, 64, 64),          # no rows: zeros
+    (70000, 128, 64),     # many R splits
+])
+def test_wgrad_x3_accuracy_vs_fp64(R, N, K):
+    from lpgnn.fc import wgrad
+
+    g = torch.Generator().manual_seed(R + N)
+    G = torch.randn(R, N, generator=g)
+    X = torch.randn(R, K, generator=g).relu()
+    got = wgrad(G.to(DEV), X.to(DEV), arith="x3").cpu().double()
+    ref = G.double().t() @ X.double()
+    s = G.double().abs().t() @ X.double().abs()
+    bound = 16 * U * s + U * ref.abs() + 1e-30
+    err = (got - ref).abs()
+    assert (err <= bound).all(), f"max err/bound {(err / bound).max().item():.3f}"
+    again = wgrad(G.to(DEV), X.to(DEV), arith="x3").cpu().double()
+    assert torch.equal(got, again)  # fixed-order split reduction: run-to-run identical
+
+
+def test_wgrad_x3_strided_inputs():
+    from lpgnn.fc import wgrad
+
+    g = torch.Generator().manual_seed(3)
+    big = torch.randn(900, 300, generator=g).to(DEV)
+    G, X = big[:, :64], big[:, 100:228]  # row stride 300 (a multiple of 4)
+    got = wgrad(G, X, arith="x3")
+    torch.testing.assert_close(got, G.t() @ X, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("two", [False, True])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_input_grad_x3(two, accumulate):
+    """dZ1 W1 [+ dZ2 W2] [+ out] with Linear weights [out, in] split transposed."""
+    from lpgnn.fc import input_grad
+
+    g = torch.Generator().manual_seed(17)
+    M, F, H = 777, 256, 160
+    G1, W1 = torch.randn(M, F, generator=g), torch.randn(F, H, generator=g) * 0.1
+    G2, W2 = torch.randn(M, F, generator=g), torch.randn(F, H, generator=g) * 0.1
+    P = torch.randn(M, H, generator=g)
+    ref = G1.double() @ W1.double()
+    s = G1.double().abs() @ W1.double().abs()
+    if two:
+        ref += G2.double() @ W2.double()
+        s += G2.double().abs() @ W2.double().abs()
+    if accumulate:
+        ref += P.double()
+        s += P.double().abs()
+    out = P.to(DEV).clone() if accumulate else None
+    got = input_grad(G1.to(DEV), W1.to(DEV), G2.to(DEV) if two else None, W2.to(DEV) if two else None,
+                     out=out, accumulate=accumulate, arith="x3").cpu().double()
+    bound = 16 * U * s + U * ref.abs() + 1e-30
+    assert ((got - ref).abs() <= bound).all()
