@@ -125,8 +125,8 @@ __global__ __launch_bounds__(256) void split3_planes(int64_t rows, int64_t cols,
 __device__ __forceinline__ int swzA(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }  // 128-B rows
 __device__ __forceinline__ int swzW(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }  // 64-B rows
 
-template <int WM, int WN, int TM, int TN, bool RELU>
-__global__ __launch_bounds__(64 * WM * WN) void fc_fwd_x3(X3Args a) {
+template <int WM, int WN, int TM, int TN, bool PIPE, bool RELU>
+__global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3(X3Args a) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int A_BYTES = BM * BK * 4, WP_BYTES = BN * BK * 2;  // A image, one W plane image
@@ -194,46 +194,120 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_x3(X3Args a) {
   const int fr = lane & 31, fk = lane >> 5;
   const int rA0 = wm * TM * 32 + fr, rB0 = wn * TN * 32 + fr;
 
-  if (nk > 0) stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  int b = 0;
-  for (int t = 0; t < nk; ++t) {
-    if (t + 1 < nk) stage(b ^ 1, t + 1);
-    const unsigned char *T = smem + b * TILE_BYTES;
+  // operand reads of one 16-k substep (s) of the tile image T
+  struct RawA {
+    f32x4 v[TM][2];
+  };
+  struct OpB {
+    bf16x8 v[TN][3];
+  };
+  auto ldA = [&](const unsigned char *T, int s) {
+    RawA r;
 #pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {  // lane half fk feeds k = 16 s + 8 fk + 0..7 of one 32x32x16 MFMA
-      Split3 av[TM];
-      bf16x8 bv[TN][3];
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const unsigned char *ra = T + (rA0 + i * 32) * (BK * 4);
-        av[i] = split3(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 32, 4 * s + 2 * fk) * 16),
-                       *reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 32, 4 * s + 2 * fk + 1) * 16));
-      }
+      for (int h = 0; h < 2; ++h)
+        r.v[i][h] = *reinterpret_cast<const f32x4 *>(T + (rA0 + i * 32) * (BK * 4) +
+                                                     swzA(rA0 + i * 32, 4 * s + 2 * fk + h) * 16);
+    return r;
+  };
+  auto ldB = [&](const unsigned char *T, int s) {
+    OpB r;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          bv[j][p] = *reinterpret_cast<const bf16x8 *>(T + A_BYTES + p * WP_BYTES + (rB0 + j * 32) * (BK * 2) +
-                                                       swzW(rB0 + j * 32, 2 * s + fk) * 16);
+      for (int p = 0; p < 3; ++p)
+        r.v[j][p] = *reinterpret_cast<const bf16x8 *>(T + A_BYTES + p * WP_BYTES + (rB0 + j * 32) * (BK * 2) +
+                                                      swzW(rB0 + j * 32, 2 * s + fk) * 16);
+    return r;
+  };
+  auto mfma_row = [&](int i, const Split3 &av, const OpB &bv) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].l, bv[j][0], accL[i][j], 0, 0, 0);
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].m, bv[j][1], accL[i][j], 0, 0, 0);
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].h, bv[j][2], accL[i][j], 0, 0, 0);
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].m, bv[j][0], accL[i][j], 0, 0, 0);
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].h, bv[j][1], accL[i][j], 0, 0, 0);
-          accH[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i].h, bv[j][0], accH[i][j], 0, 0, 0);
-        }
+    for (int j = 0; j < TN; ++j) {
+      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.l, bv.v[j][0], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv.v[j][1], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.v[j][2], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv.v[j][0], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.v[j][1], accL[i][j], 0, 0, 0);
+      accH[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.v[j][0], accH[i][j], 0, 0, 0);
     }
+  };
+
+  if (!PIPE) {
+    if (nk > 0) stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // tile t+1 landed; every wave done with tile t
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    b ^= 1;
+    int b = 0;
+    for (int t = 0; t < nk; ++t) {
+      if (t + 1 < nk) stage(b ^ 1, t + 1);
+      const unsigned char *T = smem + b * TILE_BYTES;
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {  // lane half fk feeds k = 16 s + 8 fk + 0..7 of one 32x32x16 MFMA
+        const RawA ra = ldA(T, s);
+        const OpB bv = ldB(T, s);
+        Split3 av[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) av[i] = split3(ra.v[i][0], ra.v[i][1]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) mfma_row(i, av[i], bv);
+      }
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // tile t+1 landed; every wave done with tile t
+      asm volatile("" ::: "memory");
+      b ^= 1;
+    }
+  } else {
+    // Software-pipelined: a substep's operands are read one substep ahead, and
+    // each A fragment is split while the previous fragment's MFMAs run.  The
+    // DMA of tile t+2 goes into tile t's buffer right after the barrier that
+    // follows every wave's last read of tile t (issued during substep 0), so
+    // each DMA has a whole tile of MFMAs to land.
+    if (nk > 0) stage(0, 0);
+    if (nk > 1) {
+      stage(1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(PA + PB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    RawA ra = ldA(smem, 0);
+    for (int t = 0; t < nk; ++t) {
+      const int b = t & 1;
+      const unsigned char *T = smem + b * TILE_BYTES;
+      // substep 0 of tile t; prefetch substep 1's A
+      {
+        const OpB bv = ldB(T, 0);
+        const Split3 a0 = split3(ra.v[0][0], ra.v[0][1]);
+        const RawA nra = ldA(T, 1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const Split3 ai = i == 0 ? a0 : split3(ra.v[i][0], ra.v[i][1]);
+          mfma_row(i, ai, bv);
+        }
+        ra = nra;
+      }
+      // substep 1; prefetch substep 0's A of tile t+1
+      {
+        const OpB bv = ldB(T, 1);
+        const Split3 a0 = split3(ra.v[0][0], ra.v[0][1]);
+        RawA nra = ra;
+        if (t + 1 < nk) {
+          asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();  // tile t+1 landed; every wave's reads of tile t are done
+          asm volatile("" ::: "memory");
+          if (t + 2 < nk) stage(b, t + 2);
+          nra = ldA(smem + (b ^ 1) * TILE_BYTES, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const Split3 ai = i == 0 ? a0 : split3(ra.v[i][0], ra.v[i][1]);
+          mfma_row(i, ai, bv);
+        }
+        ra = nra;
+      }
+    }
   }
 
   // Epilogue.  32x32 MFMA output map: col = lane & 31, row = 4 (lane >> 5) + (r & 3) + 8 (r >> 2).
@@ -281,7 +355,178 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_x3(X3Args a) {
   }
 }
 
+// The same GEMM on v_mfma_f32_16x16x32_bf16 (MI355X_MICROARCH.md 'DVFS
+// give-back' item 7: on random operands the chip holds a higher clock on this
+// shape, ~1.12-1.15x the FLOP/s of 32x32x16 at equal cycles per FLOP).  One
+// MFMA consumes a whole BK = 32 k-tile: lane group g = lane >> 4 feeds
+// k = 8g .. 8g+7 (A: two 16-B chunks of its row, W: chunk g of each plane);
+// the LDS images and swizzles are those of fc_fwd_x3 (16 consecutive rows at
+// one logical chunk land in 16 distinct bank slots).  Each wave owns
+// (TM x TN) fragments of 16 x 16; output map col = lane & 15,
+// row = 4 (lane >> 4) + r.
+template <int WM, int WN, int TM, int TN, bool RELU>
+__global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+  constexpr int A_BYTES = BM * BK * 4, WP_BYTES = BN * BK * 2;
+  constexpr int TILE_BYTES = A_BYTES + 3 * WP_BYTES;
+  constexpr int PA = BM / 8 / NW;
+  constexpr int PB = 3 * (BN / 16) / NW;
+  static_assert(BM % (8 * NW) == 0 && (3 * BN / 16) % NW == 0, "tile rows must split into whole pieces per wave");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
+
+  const int64_t nwg = a.mt * a.nt;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
+  const int64_t m0 = (wgid / a.nt) * BM;
+  const int64_t n0 = (wgid % a.nt) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nk1 = (int)(a.K1 / BK);
+  const int nk = nk1 + (int)(a.K2 / BK);
+
+  const float *srcA1[PA], *srcA2[PA];
+  const uint16_t *srcW1[PB], *srcW2[PB];
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int row = (wave + NW * p) * 8 + (lane >> 3);
+    int64_t gr = m0 + row;
+    gr = gr < a.M ? gr : a.M - 1;
+    const int off = swzA(row, lane & 7) * 4;
+    srcA1[p] = a.A1 + gr * a.lda1 + off;
+    srcA2[p] = a.A2 + gr * a.lda2 + off;
+  }
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    const int q = wave + NW * p, plane = q / (BN / 16);
+    const int row = (q % (BN / 16)) * 16 + (lane >> 2);
+    int64_t gn = n0 + row;
+    gn = gn < a.N ? gn : a.N - 1;
+    const int off = swzW(row, lane & 3) * 8;
+    srcW1[p] = a.W1 + plane * a.ps1 + gn * a.ldw1 + off;
+    srcW2[p] = a.W2 + plane * a.ps2 + gn * a.ldw2 + off;
+  }
+  auto stage = [&](int b, int t) {
+    typedef __attribute__((address_space(3))) unsigned char lds_t;
+    unsigned char *base = smem + b * TILE_BYTES;
+    const bool p2 = t >= nk1;
+    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
+#pragma unroll
+    for (int p = 0; p < PA; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcA2[p] : srcA1[p]) + k0),
+                                       (lds_t *)(base + (wave + NW * p) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcW2[p] : srcW1[p]) + k0),
+                                       (lds_t *)(base + A_BYTES + (wave + NW * p) * 1024), 16, 0, 0);
+  };
+
+  f32x4 accH[TM][TN], accL[TM][TN];
+  const f32x4 zero = {};
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) accH[i][j] = accL[i][j] = zero;
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int rA0 = wm * TM * 16 + fr, rB0 = wn * TN * 16 + fr;
+
+  if (nk > 0) stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int b = 0;
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) stage(b ^ 1, t + 1);
+    const unsigned char *T = smem + b * TILE_BYTES;
+    bf16x8 bv[TN][3];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bv[j][p] = *reinterpret_cast<const bf16x8 *>(T + A_BYTES + p * WP_BYTES + (rB0 + j * 16) * (BK * 2) +
+                                                     swzW(rB0 + j * 16, fg) * 16);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const unsigned char *ra = T + (rA0 + i * 16) * (BK * 4);
+      const Split3 av = split3(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16),
+                               *reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg + 1) * 16));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.l, bv[j][0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bv[j][1], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv[j][2], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bv[j][0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv[j][1], accL[i][j], 0, 0, 0);
+        accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv[j][0], accH[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    b ^= 1;
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = accH[i][j] + accL[i][j];
+  const int64_t mw = m0 + wm * TM * 16, nw = n0 + wn * TN * 16;
+  if (a.accum) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int64_t col = nw + j * 16 + fr;
+      col = col < a.N ? col : a.N - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int64_t row = mw + i * 16 + 4 * fg + r;
+          row = row < a.M ? row : a.M - 1;
+          acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
+        }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = nw + j * 16 + fr;
+    if (col >= a.N) continue;
+    const float bb = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = mw + i * 16 + 4 * fg + r;
+        if (row >= a.M) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v = v + bb;
+        if (RELU) v = (v < 0.f) ? 0.f : v;
+        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        a.C[row * a.ldc + col] = v;
+      }
+    }
+  }
+}
+
 template <int WM, int WN, int TM, int TN>
+lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16, NT = 64 * WM * WN;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int64_t nwg = a.mt * a.nt;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+template <int WM, int WN, int TM, int TN, bool PIPE = false>
 lpg_status launch_x3(X3Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
   a.mt = (a.M + BM - 1) / BM;
@@ -289,9 +534,9 @@ lpg_status launch_x3(X3Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_fwd_x3<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_x3<WM, WN, TM, TN, PIPE, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_fwd_x3<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_x3<WM, WN, TM, TN, PIPE, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -520,12 +765,20 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
   switch (g_x3_variant) {
     case 1: return launch_x3<4, 2, 2, 2>(a, relu, s);  // 256 x 128, 8 waves
     case 2: return launch_x3<2, 4, 2, 2>(a, relu, s);  // 128 x 256, 8 waves
-    default: return launch_x3<2, 2, 2, 2>(a, relu, s);  // 128 x 128, 4 waves
+    case 3: return launch_x3<2, 2, 2, 2, true>(a, relu, s);  // 128 x 128, software-pipelined
+    case 4: return launch_x3<4, 2, 2, 2, true>(a, relu, s);  // 256 x 128, software-pipelined
+    case 5: return launch_x3_16<2, 2, 4, 4>(a, relu, s);  // 128 x 128, 16x16x32 MFMA
+    case 6: return launch_x3_16<4, 2, 4, 4>(a, relu, s);  // 256 x 128, 16x16x32 MFMA
+    case 7: return launch_x3_16<2, 2, 4, 2>(a, relu, s);  // 128 x 64, 16x16x32 MFMA
+    case 8: return launch_x3<2, 2, 2, 2>(a, relu, s);  // 128 x 128, 4 waves
+    default:  // by shape (tools/exp_x3.py at the c2 shapes): 16x16x32 on 256 x 128 for tall GEMMs
+      if (M >= 150000 || K1 + K2 >= 2048) return launch_x3_16<4, 2, 4, 4>(a, relu, s);
+      return launch_x3<2, 2, 2, 2>(a, relu, s);
   }
 }
 
 extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
-  LPG_REQUIRE(v >= 0 && v <= 2, "lpg_fc_x3_set_variant: variant %d not in [0, 2]", v);
+  LPG_REQUIRE(v >= 0 && v <= 8, "lpg_fc_x3_set_variant: variant %d not in [0, 8]", v);
   g_x3_variant = v;
   return LPG_OK;
 }

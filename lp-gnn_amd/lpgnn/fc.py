@@ -141,8 +141,10 @@ def wgrad(G: Tensor, X: Tensor, arith: str | None = None) -> Tensor:
     """G^T X (the weight gradient dZ^T x of a Linear, [N, K]) in fp32:
     lpg_wgrad_x3_f32 (deterministic split-R reduction) or, with arith
     "fp32", the library GEMM (hipBLASLt)."""
-    if (arith or ARITH) != "x3" or G.shape[1] % 4 or X.shape[1] % 4:
+    if (arith or ARITH) != "x3" or G.shape[1] % 4 or X.shape[1] % 4 or G.dtype != torch.float32:
         return G.t() @ X
+    if G.device.type != "cuda":
+        raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     G, X = _prep(G), _prep(X)
     R, N, K = G.shape[0], G.shape[1], X.shape[1]
     L = _lib.lib()
@@ -163,7 +165,7 @@ def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | No
     gradient of lin_rel / lin_root): the x3 FC kernel with the weights split
     transposed, or the library GEMMs with arith "fp32"."""
     if (arith or ARITH) != "x3" or G1.shape[1] % 32 or (G2 is not None and G2.shape[1] % 32) \
-            or W1.shape[1] <= 32:
+            or W1.shape[1] <= 32 or G1.dtype != torch.float32:
         r = out if accumulate else None
         if r is None:
             r = G1 @ W1
@@ -175,6 +177,8 @@ def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | No
             out.copy_(r)
             r = out
         return r
+    if G1.device.type != "cuda":
+        raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     G1, G2 = _prep(G1), _prep(G2)
     M, N = G1.shape[0], W1.shape[1]
     if out is None:

@@ -358,7 +358,8 @@ class _PartTwoDirection(torch.autograd.Function):
     owners.  right2left is local (the halo rows are current).  Backward
     mirrors it: the halo-row gradients of right' are reduced to their owners,
     the aggregate gradient of the owned rows is broadcast back before the
-    transposed SpMM.  Gradient sums go through addmm_ as in the one-GPU node.
+    transposed SpMM.  Gradient sums accumulate inside the GEMMs (x3 accumulate flag / addmm_) as in the
+    one-GPU node.
     left2right follows conv.py's association rule (on the global node counts):
     re-associated, the reduced partials are those of A^T (left W_rel^T) and the
     owners' lin_root + bias + ReLU is accumulated onto them in place.
@@ -436,8 +437,8 @@ class _PartTwoDirection(torch.autograd.Function):
             if agg is not None and agg.shape[1] + x_dst.shape[1] <= 16 and dz.shape[1] % 4 == 0:
                 d_rel, d_root = _fc.wgrad_smallk(dz, agg.contiguous(), x_dst.contiguous())
             else:
-                d_rel = dz.t() @ agg if need_rel else None
-                d_root = dz.t() @ x_dst if need_root else None
+                d_rel = _fc.wgrad(dz, agg) if need_rel else None
+                d_root = _fc.wgrad(dz, x_dst) if need_root else None
             return (d_rel if need_rel else None), (d_root if need_root else None)
 
         # ... under everything that only needs the constraint side's gradient
@@ -446,9 +447,9 @@ class _PartTwoDirection(torch.autograd.Function):
         g_r = None
         if need[1]:  # right [owned | halo] as the source of right2left: every local row
             if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
-                g_r = spmm_forward(AT, dz_l) @ w_rel_r2l
+                g_r = _fc.input_grad(spmm_forward(AT, dz_l), w_rel_r2l)
             else:
-                g_r = spmm_forward(AT, dz_l @ w_rel_r2l)
+                g_r = spmm_forward(AT, _fc.input_grad(dz_l, w_rel_r2l))
         g_right_own = red.finish()
         dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
         # with T = A bcast(dZ_r) (computed for left's gradient below), lin_rel's weight gradient
@@ -460,7 +461,7 @@ class _PartTwoDirection(torch.autograd.Function):
         dw_rel_l2r, dw_root_l2r = wgrads(dz_r, None if agg_r is None else agg_r[:n_own], right[:n_own],
                                          need[3] and not rel_from_t, need[5])
         if need[1]:  # ... and as the destination of left2right (owned rows)
-            g_r[:n_own].addmm_(dz_r, w_root_l2r)
+            _fc.input_grad(dz_r, w_root_l2r, out=g_r[:n_own], accumulate=True)
 
         g_l = None
         if need[0] or use_t:  # left: source of left2right through reduce(AT @ left)[:n_own]
@@ -469,16 +470,16 @@ class _PartTwoDirection(torch.autograd.Function):
             if use_t:
                 full[:n_own] = dz_r
             else:
-                torch.mm(dz_r, w_rel_l2r, out=full[:n_own])
+                _fc.input_grad(dz_r, w_rel_l2r, out=full[:n_own])
             bc = ex.start_broadcast_(full)           # owners' aggregate gradient -> halo rows, in flight ...
-            root = dz_l @ w_root_r2l if need[0] else None  # ... under the root-path gradient of left
+            root = _fc.input_grad(dz_l, w_root_r2l) if need[0] else None  # ... under the root-path gradient
             bc.finish()
             if use_t:
                 t = spmm_forward(A, full)
                 if rel_from_t:
-                    dw_rel_l2r = t.t() @ left
+                    dw_rel_l2r = _fc.wgrad(t, left)
                 if need[0]:
-                    g_l = torch.addmm(root, t, w_rel_l2r)
+                    g_l = _fc.input_grad(t, w_rel_l2r, out=root, accumulate=True)
             else:
                 g_l = spmm_forward(A, full).add_(root)
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
