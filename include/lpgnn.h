@@ -177,11 +177,15 @@ int64_t lpg_wgrad_x3_workspace_bytes(int64_t R, int64_t N, int64_t K);
 lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
                             int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream);
 
-/* Tile choice for lpg_fc_x3_f32 (tuning; every variant gives identical bits):
- * 0 = by shape (256 x 128 on 16x16x32 MFMAs when M >= 150000 or K1 + K2 >=
- * 2048, else 8), 1 = 256 x 128, 2 = 128 x 256 (8 waves, 32x32x16),
- * 3 / 4 = 128 x 128 / 256 x 128 software-pipelined, 5 / 6 / 7 = 128 x 128 /
- * 256 x 128 / 128 x 64 on 16x16x32, 8 = 128 x 128 (4 waves, 32x32x16). */
+/* Tile choice for lpg_fc_x3_f32 (tuning).  On 16x16x32 MFMAs: 0 = default =
+ * 10, 5 / 6 / 7 = 128 x 128 / 256 x 128 / 128 x 64 tiles of 64 x 64 (or
+ * 64 x 32) wave tiles, 9 / 10 = 256 x 128 / 128 x 128 tiles of 32 x 128 wave
+ * tiles (each A row split by one wave only), 11 = 256 x 128 of 64 x 128; on
+ * 32x32x16 MFMAs: 1 = 256 x 128, 2 = 128 x 256, 3 / 4 = 128 x 128 / 256 x 128
+ * software-pipelined, 8 = 128 x 128.  Variants on the same MFMA shape give
+ * identical bits (the two shapes differ in in-instruction summation).
+ * 100 / 101: the weight-gradient kernel's MFMA shape (32x32x16 / 16x16x32,
+ * default 101). */
 lpg_status lpg_fc_x3_set_variant(int32_t v);
 
 /* Backward of ReLU (+ fused dropout): out[i] = y[i] > 0 ? g[i] * scale : 0,

@@ -40,6 +40,8 @@
 #include "common.h"
 #include "fc_common.h"
 
+#include <type_traits>
+
 #pragma clang fp contract(off)
 
 namespace lpg {
@@ -364,7 +366,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3(X3Args a) {
 // one logical chunk land in 16 distinct bank slots).  Each wave owns
 // (TM x TN) fragments of 16 x 16; output map col = lane & 15,
 // row = 4 (lane >> 4) + r.
-template <int WM, int WN, int TM, int TN, bool RELU>
+template <int WM, int WN, int TM, int TN, bool RELU, bool PROBE = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
@@ -441,26 +443,57 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
   for (int t = 0; t < nk; ++t) {
     if (t + 1 < nk) stage(b ^ 1, t + 1);
     const unsigned char *T = smem + b * TILE_BYTES;
-    bf16x8 bv[TN][3];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
+    auto ldb = [&](int j, bf16x8 (&bj)[3]) {
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        bv[j][p] = *reinterpret_cast<const bf16x8 *>(T + A_BYTES + p * WP_BYTES + (rB0 + j * 16) * (BK * 2) +
-                                                     swzW(rB0 + j * 16, fg) * 16);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
+        bj[p] = *reinterpret_cast<const bf16x8 *>(T + A_BYTES + p * WP_BYTES + (rB0 + j * 16) * (BK * 2) +
+                                                  swzW(rB0 + j * 16, fg) * 16);
+    };
+    auto mfma6 = [&](int i, int j, const Split3 &av, const bf16x8 (&bj)[3]) {
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.l, bj[0], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bj[1], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bj[2], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bj[0], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bj[1], accL[i][j], 0, 0, 0);
+      accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bj[0], accH[i][j], 0, 0, 0);
+    };
+    auto lda = [&](int i) {
       const unsigned char *ra = T + (rA0 + i * 16) * (BK * 4);
-      const Split3 av = split3(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16),
-                               *reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg + 1) * 16));
+      Split3 av;
+      if constexpr (PROBE) {  // timing probe only (wrong results): A's bytes reinterpreted, no split VALU
+        av.h = *reinterpret_cast<const bf16x8 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16);
+        av.m = *reinterpret_cast<const bf16x8 *>(ra + swzA(rA0 + i * 16, 2 * fg + 1) * 16);
+        av.l = av.h;
+      } else {
+        av = split3(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16),
+                    *reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg + 1) * 16));
+      }
+      return av;
+    };
+    if constexpr (TN <= 4) {
+      bf16x8 bv[TN][3];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.l, bv[j][0], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bv[j][1], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv[j][2], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bv[j][0], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv[j][1], accL[i][j], 0, 0, 0);
-        accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv[j][0], accH[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) ldb(j, bv[j]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const Split3 av = lda(i);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma6(i, j, av, bv[j]);
+      }
+    } else {  // wide wave tile (few A rows, many W columns): all A splits first, W streamed two fragments at a time
+      Split3 av[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = lda(i);
+#pragma unroll
+      for (int j = 0; j < TN; j += 2) {
+        bf16x8 b0[3], b1[3];
+        ldb(j, b0);
+        ldb(j + 1, b1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          mfma6(i, j, av[i], b0);
+          mfma6(i, j + 1, av[i], b1);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -511,7 +544,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
   }
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, bool PROBE = false>
 lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16, NT = 64 * WM * WN;
   a.mt = (a.M + BM - 1) / BM;
@@ -519,9 +552,9 @@ lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, true, PROBE>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, false, PROBE>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -558,22 +591,24 @@ lpg_status launch_x3(X3Args a, bool relu, hipStream_t s) {
 // from a zeroed 512-B row at the end of the workspace.
 constexpr int WG_T = 128;  // output tile (n and k)
 
-__device__ __forceinline__ void wg_read8(const unsigned char *img, int col, int r0, float (&v)[8]) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = *reinterpret_cast<const float *>(img + (r0 + e) * (WG_T * 4) + col * 4);
-}
-
 __device__ __forceinline__ Split3 split3_8(const float (&v)[8]) {
   return split3(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]});
 }
 
+// M16: v_mfma_f32_16x16x32_bf16 (one MFMA per 32-row chunk, wave tile 4 x 4
+// fragments of 16 x 16; lane group g = lane >> 4 feeds rows 8g .. 8g+7).  Its
+// ds_read_b32 halves hold rows r and r + 8 at the same columns, so the image
+// XORs the 16-B chunk index with 4 on rows whose bit 3 is set (applied on the
+// DMA source address): the two rows land 16 banks apart.
+template <bool M16>
 __global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
-                                                int64_t ldg, const float *__restrict__ X, int64_t ldx,
-                                                float *__restrict__ part, const float *__restrict__ zrow,
-                                                int64_t nt, int64_t kt, int64_t S, int64_t chunks_per_split) {
+                                                   int64_t ldg, const float *__restrict__ X, int64_t ldx,
+                                                   float *__restrict__ part, const float *__restrict__ zrow,
+                                                   int64_t nt, int64_t kt, int64_t S, int64_t chunks_per_split) {
   constexpr int OP_BYTES = 32 * WG_T * 4;  // one operand's k-tile image: 32 rows x 512 B
   constexpr int TILE_BYTES = 2 * OP_BYTES;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
+  auto swz = [](int row) { return M16 ? ((row >> 3) & 1) * 4 : 0; };  // 16-B chunk XOR of a row
 
   // block -> (split s, output tile); consecutive blocks share s (same rows of G and X in L2)
   const int64_t bid = blockIdx.x;
@@ -594,7 +629,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t
   for (int p = 0; p < 4; ++p) {
     const int piece = wave + 4 * p;
     prow[p] = piece * 2 + (lane >> 5);
-    const int ch = lane & 31;
+    const int ch = (lane & 31) ^ swz(prow[p]);
     int64_t gn = n0 + ch * 4, gk = k0 + ch * 4;
     gn = gn < N ? gn : N - 4;  // N, K multiples of 4: columns past the edge feed outputs never stored
     gk = gk < K ? gk : K - 4;
@@ -615,41 +650,64 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t
                                        (lds_t *)(base + OP_BYTES + (wave + 4 * p) * 1024), 16, 0, 0);
     }
   };
-
-  f32x16 accH[2][2], accL[2][2];
-  const f32x16 zero = {};
+  // the lane's 8 values of column col, rows r0 .. r0+7, from an operand image
+  auto read8 = [&](const unsigned char *img, int col, int r0, float (&v)[8]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) accH[i][j] = accL[i][j] = zero;
-  const int fr = lane & 31, fk = lane >> 5;
+    for (int e = 0; e < 8; ++e) {
+      const int r = r0 + e;
+      v[e] = *reinterpret_cast<const float *>(img + r * (WG_T * 4) + (((col >> 2) ^ swz(r)) * 4 + (col & 3)) * 4);
+    }
+  };
 
+  constexpr int FT = M16 ? 4 : 2;  // fragments per wave and dimension
+  typedef typename std::conditional<M16, f32x4, f32x16>::type acc_t;
+  acc_t accH[FT][FT], accL[FT][FT];
+  const acc_t zero = {};
+#pragma unroll
+  for (int i = 0; i < FT; ++i)
+#pragma unroll
+    for (int j = 0; j < FT; ++j) accH[i][j] = accL[i][j] = zero;
+  auto mfma6 = [&](acc_t &h, acc_t &l, const Split3 &av, const Split3 &bv) {
+    if constexpr (M16) {
+      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.l, bv.h, l, 0, 0, 0);
+      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bv.m, l, 0, 0, 0);
+      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv.l, l, 0, 0, 0);
+      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bv.h, l, 0, 0, 0);
+      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv.m, l, 0, 0, 0);
+      h = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv.h, h, 0, 0, 0);
+    } else {
+      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.l, bv.h, l, 0, 0, 0);
+      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv.m, l, 0, 0, 0);
+      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.l, l, 0, 0, 0);
+      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv.h, l, 0, 0, 0);
+      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.m, l, 0, 0, 0);
+      h = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.h, h, 0, 0, 0);
+    }
+  };
+
+  // 32x32x16: lane (fr = lane & 31, fk = lane >> 5) feeds rows 16 ss + 8 fk .. +7 of substep ss;
+  // 16x16x32: lane (fr = lane & 15, g = lane >> 4) feeds rows 8 g .. +7 of the whole chunk
   auto body = [&](const unsigned char *T) {
+    constexpr int FW = M16 ? 16 : 32;  // fragment width
+    const int fr = lane & (FW - 1);
 #pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      const int r0 = 16 * ss + 8 * fk;
-      Split3 bv[2];
+    for (int ss = 0; ss < (M16 ? 1 : 2); ++ss) {
+      const int r0 = M16 ? 8 * (lane >> 4) : 16 * ss + 8 * (lane >> 5);
+      Split3 bv[FT];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < FT; ++j) {
         float v[8];
-        wg_read8(T + OP_BYTES, wn * 64 + j * 32 + fr, r0, v);
+        read8(T + OP_BYTES, wn * 64 + j * FW + fr, r0, v);
         bv[j] = split3_8(v);
       }
       // one A fragment's split live at a time (register pressure: 128 accumulators)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < FT; ++i) {
         float v[8];
-        wg_read8(T, wm * 64 + i * 32 + fr, r0, v);
+        read8(T, wm * 64 + i * FW + fr, r0, v);
         const Split3 av = split3_8(v);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.l, bv[j].h, accL[i][j], 0, 0, 0);
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv[j].m, accL[i][j], 0, 0, 0);
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv[j].l, accL[i][j], 0, 0, 0);
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv[j].h, accL[i][j], 0, 0, 0);
-          accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv[j].m, accL[i][j], 0, 0, 0);
-          accH[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv[j].h, accH[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < FT; ++j) mfma6(accH[i][j], accL[i][j], av, bv[j]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -662,27 +720,26 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t
   int b = 0;
   for (int64_t c = c0; c < c1; ++c) {
     if (c + 1 < c1) stage(b ^ 1, c + 1);
-    const unsigned char *T = smem + b * TILE_BYTES;
-    body(T);
+    body(smem + b * TILE_BYTES);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     b ^= 1;
   }
 
-  // partial tile -> part[s] ([N, K] row-major); 32x32 output map: col = lane & 31,
-  // row = 4 (lane >> 5) + (r & 3) + 8 (r >> 2)
+  // partial tile -> part[s] ([N, K] row-major).  32x32 output map: col = lane & 31,
+  // row = 4 (lane >> 5) + (r & 3) + 8 (r >> 2); 16x16: col = lane & 15, row = 4 (lane >> 4) + r
   float *P = part + s * N * K;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t col = k0 + wn * 64 + j * 32 + (lane & 31);
+  for (int j = 0; j < FT; ++j) {
+    const int64_t col = k0 + wn * 64 + j * (M16 ? 16 : 32) + (lane & (M16 ? 15 : 31));
     if (col >= K) continue;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t rbase = n0 + wm * 64 + i * 32 + 4 * (lane >> 5);
+    for (int i = 0; i < FT; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
+      for (int r = 0; r < (M16 ? 4 : 16); ++r) {
+        const int64_t row = M16 ? n0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r
+                                : n0 + wm * 64 + i * 32 + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2);
         if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
       }
     }
@@ -718,6 +775,7 @@ int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
 }
 
 int g_x3_variant = 0;
+int g_wgrad_m16 = 1;  // lpg_fc_x3_set_variant(100 + v): wgrad MFMA shape (1 = 16x16x32)
 
 }  // namespace
 }  // namespace lpg
@@ -771,14 +829,21 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
     case 6: return launch_x3_16<4, 2, 4, 4>(a, relu, s);  // 256 x 128, 16x16x32 MFMA
     case 7: return launch_x3_16<2, 2, 4, 2>(a, relu, s);  // 128 x 64, 16x16x32 MFMA
     case 8: return launch_x3<2, 2, 2, 2>(a, relu, s);  // 128 x 128, 4 waves
-    default:  // by shape (tools/exp_x3.py at the c2 shapes): 16x16x32 on 256 x 128 for tall GEMMs
-      if (M >= 150000 || K1 + K2 >= 2048) return launch_x3_16<4, 2, 4, 4>(a, relu, s);
-      return launch_x3<2, 2, 2, 2>(a, relu, s);
+    case 9: return launch_x3_16<8, 1, 2, 8>(a, relu, s);   // 256 x 128, 8 waves of 32 x 128 (A split once)
+    case 10: return launch_x3_16<4, 1, 2, 8>(a, relu, s);  // 128 x 128, 4 waves of 32 x 128
+    case 11: return launch_x3_16<4, 1, 4, 8>(a, relu, s);  // 256 x 128, 4 waves of 64 x 128
+    case 99: return launch_x3_16<4, 2, 4, 4, true>(a, relu, s);  // timing probe: no A split (WRONG results)
+    default:  // (tools/exp_x3.py at the c2 shapes: 199-212 TF/s, 5-10 % over 5 / 6)
+      return launch_x3_16<4, 1, 2, 8>(a, relu, s);
   }
 }
 
 extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
-  LPG_REQUIRE(v >= 0 && v <= 8, "lpg_fc_x3_set_variant: variant %d not in [0, 8]", v);
+  if (v == 100 || v == 101) {
+    g_wgrad_m16 = v - 100;
+    return LPG_OK;
+  }
+  LPG_REQUIRE((v >= 0 && v <= 11) || v == 99, "lpg_fc_x3_set_variant: variant %d not in [0, 11]", v);
   g_x3_variant = v;
   return LPG_OK;
 }
@@ -812,8 +877,12 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   float *zrow = part + S * N * K;  // 128 zero floats after the partials (lpg_wgrad_x3_workspace_bytes)
   hipStream_t st = as_stream(stream);
   LPG_HIP(hipMemsetAsync(zrow, 0, 512, st));
-  hipLaunchKernelGGL(wgrad_x3, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow, nt, kt,
-                     S_used, cps);
+  if (g_wgrad_m16)
+    hipLaunchKernelGGL(wgrad_x3<true>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
+                       nt, kt, S_used, cps);
+  else
+    hipLaunchKernelGGL(wgrad_x3<false>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
+                       nt, kt, S_used, cps);
   LPG_HIP(hipGetLastError());
   const int64_t n4 = N * (K / 4);
   hipLaunchKernelGGL(wgrad_fold, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, N, K, S_used, part, dW, lddw);

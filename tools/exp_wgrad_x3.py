@@ -9,7 +9,17 @@ import torch  # noqa: E402
 
 from tools.kbench import timeit  # noqa: E402
 
+from lpgnn import _lib  # noqa: E402
 from lpgnn.fc import input_grad, wgrad  # noqa: E402
+
+L = _lib.lib()
+
+
+def wg(v):
+    def f():
+        L.lpg_fc_x3_set_variant(v)
+        return wgrad(G, X, arith="x3")
+    return f
 
 for R in (100_000, 200_000):
     G = torch.randn(R, 1024, device="cuda")
@@ -17,8 +27,10 @@ for R in (100_000, 200_000):
     W = torch.randn(1024, 1024, device="cuda") * 0.03
     fl = 2.0 * R * 1024 * 1024
     d = (wgrad(G, X, arith="x3") - G.t() @ X).abs().max().item()
-    t = timeit({"wgrad_x3": lambda: wgrad(G, X, arith="x3"), "wgrad_torch": lambda: G.t() @ X,
+    d16 = (wg(101)() - wg(100)()).abs().max().item()
+    t = timeit({"wgrad_x3_m32": wg(100), "wgrad_x3_m16": wg(101), "wgrad_torch": lambda: G.t() @ X,
                 "igrad_x3": lambda: input_grad(G, W, arith="x3"), "igrad_torch": lambda: G @ W})
     for k, ms in t.items():
         print(f"R={R} {k:12s} {ms:.3f} ms {fl / ms / 1e9:.1f} TF/s", flush=True)
-    print(f"R={R} wgrad max|x3 - torch| = {d:.3e}")
+    print(f"R={R} wgrad max|x3 - torch| = {d:.3e}  max|m16 - m32| = {d16:.3e}")
+    L.lpg_fc_x3_set_variant(101)
