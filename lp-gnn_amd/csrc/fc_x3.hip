@@ -746,6 +746,124 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t
   }
 }
 
+// Cooperative variant: every element of a chunk is split ONCE per block.
+// Threads 0-127 take G, 128-255 take X; a thread loads 8 consecutive rows x 4
+// columns (8 global float4 loads straight to registers, issued one chunk
+// ahead, under the previous chunk's MFMAs), splits each column's 8 values
+// into three bf16x8 (k = the 8 rows) and writes them with ds_write_b128 into
+// plane images laid out for the MFMA: [column][32 rows] bf16, 64-B rows,
+// chunk c at c ^ ((col >> 2) & 3) (the fc kernel's W-plane image, read
+// conflict-free by 16 consecutive columns).  Then 4 waves (2 x 2, 64 x 64
+// each, 16x16x32) read b128 fragments.  One plane buffer (48 KiB), two
+// barriers per chunk.  Per lane and chunk: 32 splits (vs 64 when each wave
+// splits what it reads) and 24 ds_read_b128 (vs 64 ds_read_b32).
+__global__ __launch_bounds__(256, 2) void wgrad_x3c(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
+                                                    int64_t ldg, const float *__restrict__ X, int64_t ldx,
+                                                    float *__restrict__ part, const float *__restrict__ zrow,
+                                                    int64_t nt, int64_t kt, int64_t S, int64_t chunks_per_split) {
+  constexpr int PLANE = WG_T * 32 * 2;  // one plane image: 128 columns x 32 rows x bf16 = 8 KiB
+  constexpr int OPB = 3 * PLANE;        // one operand's three planes
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * OPB];
+
+  const int64_t bid = blockIdx.x;
+  const int64_t tiles = nt * kt;
+  const int64_t s = bid / tiles, tile = bid % tiles;
+  const int64_t n0 = (tile / kt) * WG_T, k0 = (tile % kt) * WG_T;
+  const int64_t nchunks = (R + 31) / 32;
+  const int64_t c0 = s * chunks_per_split;
+  const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // load/split task: operand (G or X), 4 columns cg*4 .. +3, rows rg*8 .. +7 of the chunk
+  const int op = tid >> 7, cg = tid & 31, rg = (tid >> 5) & 3;
+  const float *base;
+  int64_t ld, col0;
+  {
+    const int64_t lim = op ? K : N;
+    col0 = (op ? k0 : n0) + cg * 4;
+    col0 = col0 < lim ? col0 : lim - 4;  // N, K multiples of 4: columns past the edge are never stored
+    base = (op ? X : G) + col0;
+    ld = op ? ldx : ldg;
+  }
+  unsigned char *img = smem + op * OPB;
+  f32x4 raw[8];
+  auto load = [&](int64_t c) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t r = c * 32 + rg * 8 + e;
+      raw[e] = r < R ? *reinterpret_cast<const f32x4 *>(base + r * ld) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto split_store = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // column cg*4 + q: its 8 rows -> three bf16x8
+      const Split3 t = split3(f32x4{raw[0][q], raw[1][q], raw[2][q], raw[3][q]},
+                              f32x4{raw[4][q], raw[5][q], raw[6][q], raw[7][q]});
+      const int col = cg * 4 + q;
+      unsigned char *dst = img + col * 64 + swzW(col, rg) * 16;
+      *reinterpret_cast<bf16x8 *>(dst) = t.h;
+      *reinterpret_cast<bf16x8 *>(dst + PLANE) = t.m;
+      *reinterpret_cast<bf16x8 *>(dst + 2 * PLANE) = t.l;
+    }
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  f32x4 accH[4][4], accL[4][4];
+  const f32x4 zero = {};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accH[i][j] = accL[i][j] = zero;
+  auto frag = [&](const unsigned char *im, int col, bf16x8 (&f)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8 *>(im + p * PLANE + col * 64 + swzW(col, fg) * 16);
+  };
+
+  if (c0 < c1) load(c0);
+  for (int64_t c = c0; c < c1; ++c) {
+    split_store();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // planes of chunk c visible
+    asm volatile("" ::: "memory");
+    if (c + 1 < c1) load(c + 1);   // in flight under this chunk's MFMAs
+    bf16x8 bv[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) frag(smem + OPB, wn * 64 + j * 16 + fr, bv[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 av[3];
+      frag(smem, wm * 64 + i * 16 + fr, av);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], bv[j][0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][1], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][2], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][1], accL[i][j], 0, 0, 0);
+        accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][0], accH[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's fragment reads of chunk c done before the next planes
+    asm volatile("" ::: "memory");
+  }
+
+  float *P = part + s * N * K;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t col = k0 + wn * 64 + j * 16 + fr;
+    if (col >= K) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = n0 + wm * 64 + i * 16 + 4 * fg + r;
+        if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
+      }
+  }
+}
+
 // dW[n, k] = sum_s part[s][n, k], s ascending (fixed order), float4 per thread
 __global__ __launch_bounds__(256) void wgrad_fold(int64_t N, int64_t K, int64_t S, const float *__restrict__ part,
                                                   float *__restrict__ dW, int64_t lddw) {
@@ -775,7 +893,7 @@ int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
 }
 
 int g_x3_variant = 0;
-int g_wgrad_m16 = 1;  // lpg_fc_x3_set_variant(100 + v): wgrad MFMA shape (1 = 16x16x32)
+int g_wgrad_m16 = 2;  // lpg_fc_x3_set_variant(100 + v): wgrad kernel (0 = 32x32x16, 1 = 16x16x32, 2 = cooperative)
 
 }  // namespace
 }  // namespace lpg
@@ -839,7 +957,7 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
 }
 
 extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
-  if (v == 100 || v == 101) {
+  if (v >= 100 && v <= 102) {
     g_wgrad_m16 = v - 100;
     return LPG_OK;
   }
@@ -877,7 +995,10 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   float *zrow = part + S * N * K;  // 128 zero floats after the partials (lpg_wgrad_x3_workspace_bytes)
   hipStream_t st = as_stream(stream);
   LPG_HIP(hipMemsetAsync(zrow, 0, 512, st));
-  if (g_wgrad_m16)
+  if (g_wgrad_m16 == 2)
+    hipLaunchKernelGGL(wgrad_x3c, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
+                       nt, kt, S_used, cps);
+  else if (g_wgrad_m16)
     hipLaunchKernelGGL(wgrad_x3<true>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
                        nt, kt, S_used, cps);
   else

@@ -28,9 +28,12 @@ for R in (100_000, 200_000):
     fl = 2.0 * R * 1024 * 1024
     d = (wgrad(G, X, arith="x3") - G.t() @ X).abs().max().item()
     d16 = (wg(101)() - wg(100)()).abs().max().item()
-    t = timeit({"wgrad_x3_m32": wg(100), "wgrad_x3_m16": wg(101), "wgrad_torch": lambda: G.t() @ X,
+    dc = (wg(102)() - wg(101)()).abs().max().item()
+    print(f"R={R} max|coop - m16| = {dc:.3e}")
+    t = timeit({"wgrad_x3_m32": wg(100), "wgrad_x3_m16": wg(101), "wgrad_x3_coop": wg(102),
+                "wgrad_torch": lambda: G.t() @ X,
                 "igrad_x3": lambda: input_grad(G, W, arith="x3"), "igrad_torch": lambda: G @ W})
     for k, ms in t.items():
         print(f"R={R} {k:12s} {ms:.3f} ms {fl / ms / 1e9:.1f} TF/s", flush=True)
     print(f"R={R} wgrad max|x3 - torch| = {d:.3e}  max|m16 - m32| = {d16:.3e}")
-    L.lpg_fc_x3_set_variant(101)
+    L.lpg_fc_x3_set_variant(102)
