@@ -180,12 +180,14 @@ lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int
 /* Tile choice for lpg_fc_x3_f32 (tuning).  On 16x16x32 MFMAs: 0 = default =
  * 10, 5 / 6 / 7 = 128 x 128 / 256 x 128 / 128 x 64 tiles of 64 x 64 (or
  * 64 x 32) wave tiles, 9 / 10 = 256 x 128 / 128 x 128 tiles of 32 x 128 wave
- * tiles (each A row split by one wave only), 11 = 256 x 128 of 64 x 128; on
+ * tiles (each A row split by one wave only); on
  * 32x32x16 MFMAs: 1 = 256 x 128, 2 = 128 x 256, 3 / 4 = 128 x 128 / 256 x 128
  * software-pipelined, 8 = 128 x 128.  Variants on the same MFMA shape give
  * identical bits (the two shapes differ in in-instruction summation).
- * 100 / 101: the weight-gradient kernel's MFMA shape (32x32x16 / 16x16x32,
- * default 101). */
+ * 100 / 101 / 102: the weight-gradient kernel (32x32x16 / 16x16x32 /
+ * cooperative 16x16x32 with one split per element, default 102; 101 and 102
+ * give identical bits).  99: a timing probe without the activation split
+ * (WRONG results, measurement only). */
 lpg_status lpg_fc_x3_set_variant(int32_t v);
 
 /* Backward of ReLU (+ fused dropout): out[i] = y[i] > 0 ? g[i] * scale : 0,
@@ -261,6 +263,23 @@ lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float
  * 64, else variant 0), 3 = 128x256 (8 waves), 4 = 256x128 (8 waves).  Every
  * variant produces bitwise identical results (same chain order). */
 lpg_status lpg_fc_set_variant(int32_t variant);
+
+/* ---- balanced loss (train.py:39-46) ---------------------------------------- */
+
+/* nn.CrossEntropyLoss(weight=w)(x, y) * coef (mean reduction, ignore_index
+ * -100) for C <= 4 classes: loss[0] = coef * sum_i w[y_i] l_i / sum_i w[y_i],
+ * wsum[0] = sum_i w[y_i] (device scalars; kept for the backward).  w may be
+ * NULL (unit weights).  Deterministic fixed-order reduction through
+ * `workspace` (lpg_weighted_ce_workspace_bytes(M)).  An out-of-range label
+ * makes the loss NaN. */
+int64_t lpg_weighted_ce_workspace_bytes(int64_t M);
+lpg_status lpg_weighted_ce_fwd_f32(int64_t M, int64_t C, const float *x, int64_t ldx, const int64_t *y,
+                                   const float *w, float coef, float *loss, float *wsum, void *workspace,
+                                   void *stream);
+/* dx[i, c] = gout[0] * coef * w[y_i] / wsum[0] * (softmax(x_i)_c - [c == y_i]) (gout may be NULL: 1). */
+lpg_status lpg_weighted_ce_bwd_f32(int64_t M, int64_t C, const float *x, int64_t ldx, const int64_t *y,
+                                   const float *w, const float *wsum, const float *gout, float coef,
+                                   float *dx, int64_t lddx, void *stream);
 
 /* add_knowledge for one side (arch.py:129-141): out = normalize(logit) * 10,
  * then out[:,0] -= bound where feas[:, cols-3] != 0 (infinite lower bound)

@@ -949,7 +949,6 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
     case 8: return launch_x3<2, 2, 2, 2>(a, relu, s);  // 128 x 128, 4 waves
     case 9: return launch_x3_16<8, 1, 2, 8>(a, relu, s);   // 256 x 128, 8 waves of 32 x 128 (A split once)
     case 10: return launch_x3_16<4, 1, 2, 8>(a, relu, s);  // 128 x 128, 4 waves of 32 x 128
-    case 11: return launch_x3_16<4, 1, 4, 8>(a, relu, s);  // 256 x 128, 4 waves of 64 x 128
     case 99: return launch_x3_16<4, 2, 4, 4, true>(a, relu, s);  // timing probe: no A split (WRONG results)
     default:  // (tools/exp_x3.py at the c2 shapes: 199-212 TF/s, 5-10 % over 5 / 6)
       return launch_x3_16<4, 1, 2, 8>(a, relu, s);
@@ -961,7 +960,7 @@ extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
     g_wgrad_m16 = v - 100;
     return LPG_OK;
   }
-  LPG_REQUIRE((v >= 0 && v <= 11) || v == 99, "lpg_fc_x3_set_variant: variant %d not in [0, 11]", v);
+  LPG_REQUIRE((v >= 0 && v <= 10) || v == 99, "lpg_fc_x3_set_variant: variant %d not in [0, 10]", v);
   g_x3_variant = v;
   return LPG_OK;
 }

@@ -38,6 +38,9 @@ HEADER_SYMBOLS = (
     "lpg_fc_x3_set_variant",
     "lpg_wgrad_x3_workspace_bytes",
     "lpg_wgrad_x3_f32",
+    "lpg_weighted_ce_workspace_bytes",
+    "lpg_weighted_ce_fwd_f32",
+    "lpg_weighted_ce_bwd_f32",
     "lpg_relu_dropout_bwd_f32",
     "lpg_relu_bwd_colsum_workspace_bytes",
     "lpg_relu_bwd_colsum_f32",
@@ -109,6 +112,13 @@ def lib() -> ctypes.CDLL:
     L.lpg_wgrad_x3_workspace_bytes.restype = c_i64
     L.lpg_wgrad_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p]
     L.lpg_wgrad_x3_f32.restype = c_i32
+    L.lpg_weighted_ce_workspace_bytes.argtypes = [c_i64]
+    L.lpg_weighted_ce_workspace_bytes.restype = c_i64
+    L.lpg_weighted_ce_fwd_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, ctypes.c_float, c_p, c_p, c_p, c_p]
+    L.lpg_weighted_ce_fwd_f32.restype = c_i32
+    L.lpg_weighted_ce_bwd_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, ctypes.c_float, c_p, c_i64,
+                                          c_p]
+    L.lpg_weighted_ce_bwd_f32.restype = c_i32
     L.lpg_fc_x3_set_variant.restype = c_i32
     L.lpg_fc_bf16.restype = c_i32
     L.lpg_fc_bf16_set_variant.argtypes = [c_i32]

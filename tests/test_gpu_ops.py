@@ -75,3 +75,35 @@ def test_spmm_sum_opcheck():
     mat = torch.randn(60, 16, device=DEV, requires_grad=True)
     torch.library.opcheck(torch.ops.lpgnn.spmm_sum.default, (row, rowptr, col, val, colptr, csr2csc, mat),
                           test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
+
+
+@pytest.mark.parametrize("M,C,weighted,ignore", [(100_000, 3, True, False), (777, 3, False, True), (5, 2, True, True),
+                                                 (1, 4, True, False)])
+def test_weighted_ce_matches_torch(M, C, weighted, ignore):
+    """lpg_weighted_ce_{fwd,bwd}_f32 == coef * nn.CrossEntropyLoss(weight=w) (value and gradient)."""
+    from lpgnn.train import weighted_ce
+
+    g = torch.Generator().manual_seed(M)
+    x = (torch.randn(M, C, generator=g) * 5).to(DEV)
+    y = torch.randint(0, C, (M,), generator=g)
+    if ignore:
+        y[::3] = -100
+    y = y.to(DEV)
+    w = (torch.rand(C, generator=g) + 0.5).to(DEV) if weighted else None
+    coef = 1.7
+    xa = x.clone().requires_grad_(True)
+    got = weighted_ce(xa, y, w, coef)
+    (got * 0.3).backward()
+    xr = x.clone().requires_grad_(True)
+    ref = coef * torch.nn.CrossEntropyLoss(weight=w)(xr, y)
+    (ref * 0.3).backward()
+    torch.testing.assert_close(got, ref, rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(xa.grad, xr.grad, rtol=1e-4, atol=1e-9)
+
+
+def test_weighted_ce_bad_label_is_nan():
+    from lpgnn.train import weighted_ce
+
+    x = torch.randn(10, 3, device=DEV)
+    y = torch.tensor([0, 1, 2, 3, 0, 1, 2, 0, 1, 2], device=DEV)
+    assert torch.isnan(weighted_ce(x, y, None, 1.0)).item()
