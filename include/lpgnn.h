@@ -257,6 +257,16 @@ lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float
                                     const float *W, const float *H, int64_t ldh, float *dH, int64_t lddh,
                                     float *dW, float *db, void *workspace, void *stream);
 
+/* The heads' backward fused with the ReLU/dropout backward of the layer that
+ * produced their input (GCN_FC: the last hidden layer's output Y feeds
+ * lin_left / lin_right, arch.py:186-190): one pass over Y,
+ *   dZ[m, k] = Y[m, k] > 0 ? scale * sum_c G[m, c] W[c, k] : 0   (the layer's dZ),
+ *   dW = G^T Y, db = sum_m G[m, :], dbY[k] = sum_m dZ[m, k]       (the layer's bias gradient),
+ * 1 <= N <= 4; db / dbY may be NULL; workspace lpg_linear_small_bwd_workspace_bytes(M, K, N). */
+lpg_status lpg_heads_relu_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W,
+                                  const float *Y, int64_t ldy, float scale, float *dZ, int64_t lddz, float *dW,
+                                  float *db, float *dbY, void *workspace, void *stream);
+
 /* Tuning knob for lpg_fc_f32 (process-global, default 0): tiled-kernel
  * variant, 0 = 128x128 tile, 2-stage LDS-DMA ring (2 blocks/CU), 1 = the same
  * with a 3-stage ring (1 block/CU), 2 = 64-deep k-tiles (K1, K2 multiples of

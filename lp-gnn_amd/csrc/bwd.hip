@@ -291,17 +291,24 @@ __global__ __launch_bounds__(kT) void wgrad_smallk_p2(int64_t nrow, int64_t N, i
 //   dH[m, k] = sum_c G[m, c] W[c, k]        (written if dH != NULL)
 //   dW[c, k] = sum_m G[m, c] H[m, k],  db[c] = sum_m G[m, c]
 // Pass 1 streams H once, writes dH and the block's partial [dW | db] row.
-template <int N>
+// MASK (lpg_heads_relu_bwd_f32): H is the output Y of the previous layer's
+// ReLU (+ dropout), and the gradient leaves already through that layer's
+// ReLU/dropout backward: dH[m, k] = Y[m, k] > 0 ? scale * sum_c G W : 0 (the
+// layer's dZ), plus its bias gradient dbY[k] = sum_m dH[m, k] as K more
+// partial columns -- the pass relu_bwd_colsum would make over dH and Y again.
+template <int N, bool MASK>
 __global__ __launch_bounds__(kT) void linear_small_bwd_p1(int64_t M, int64_t K, const float *__restrict__ G,
                                                           int64_t ldg, const float *__restrict__ W,
                                                           const float *__restrict__ H, int64_t ldh,
-                                                          float *__restrict__ dH, int64_t lddh,
+                                                          float *__restrict__ dH, int64_t lddh, float scale,
                                                           float *__restrict__ part) {
   const int64_t r0 = (int64_t)blockIdx.x * kRowsLinear;
   const int64_t r1 = r0 + kRowsLinear < M ? r0 + kRowsLinear : M;
-  float *pw = part + (int64_t)blockIdx.x * (N * K + N);  // [N][K] then db[N]
+  const int64_t tot = N * K + N + (MASK ? K : 0);
+  float *pw = part + (int64_t)blockIdx.x * tot;  // [N][K], db[N], (MASK) dbY[K]
   for (int64_t k = (int64_t)threadIdx.x * 4; k < K; k += kT * 4) {
     float4 w[N], acc[N];
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int c = 0; c < N; ++c) {
       w[c] = *reinterpret_cast<const float4 *>(W + c * K + k);
@@ -316,6 +323,13 @@ __global__ __launch_bounds__(kT) void linear_small_bwd_p1(int64_t M, int64_t K, 
         acc[c].x = acc[c].x + gc * h.x; acc[c].y = acc[c].y + gc * h.y;
         acc[c].z = acc[c].z + gc * h.z; acc[c].w = acc[c].w + gc * h.w;
       }
+      if (MASK) {
+        d.x = h.x > 0.f ? d.x * scale : 0.f;
+        d.y = h.y > 0.f ? d.y * scale : 0.f;
+        d.z = h.z > 0.f ? d.z * scale : 0.f;
+        d.w = h.w > 0.f ? d.w * scale : 0.f;
+        cs.x = cs.x + d.x; cs.y = cs.y + d.y; cs.z = cs.z + d.z; cs.w = cs.w + d.w;
+      }
       if (dH) *reinterpret_cast<float4 *>(dH + m * lddh + k) = d;
     };
     int64_t m = r0;
@@ -329,6 +343,7 @@ __global__ __launch_bounds__(kT) void linear_small_bwd_p1(int64_t M, int64_t K, 
     for (; m < r1; ++m) row(m, *reinterpret_cast<const float4 *>(H + m * ldh + k));
 #pragma unroll
     for (int c = 0; c < N; ++c) *reinterpret_cast<float4 *>(pw + c * K + k) = acc[c];
+    if (MASK) *reinterpret_cast<float4 *>(pw + N * K + N + k) = cs;
   }
   if (threadIdx.x < (unsigned)N) {
     float sgc = 0.f;
@@ -337,17 +352,18 @@ __global__ __launch_bounds__(kT) void linear_small_bwd_p1(int64_t M, int64_t K, 
   }
 }
 
-__global__ __launch_bounds__(kT) void linear_small_bwd_p2(int64_t nrow, int64_t K, int N,
+__global__ __launch_bounds__(kT) void linear_small_bwd_p2(int64_t nrow, int64_t K, int N, int64_t tot,
                                                           const float *__restrict__ img, float *__restrict__ dW,
-                                                          float *__restrict__ db) {
-  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;  // over N*K + N
-  const int64_t tot = (int64_t)N * K + N;
+                                                          float *__restrict__ db, float *__restrict__ dbY) {
+  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;  // over N*K + N (+ K)
   if (i >= tot) return;
   const float s = sum_rows(nrow, tot, img, i);
   if (i < (int64_t)N * K) {
     if (dW) dW[i] = s;
-  } else if (db) {
-    db[i - (int64_t)N * K] = s;
+  } else if (i < (int64_t)N * K + N) {
+    if (db) db[i - (int64_t)N * K] = s;
+  } else if (dbY) {
+    dbY[i - (int64_t)N * K - N] = s;
   }
 }
 
@@ -490,42 +506,72 @@ extern "C" lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const floa
                       "lpg_relu_wgrad_smallk_f32");
 }
 
-extern "C" int64_t lpg_linear_small_bwd_workspace_bytes(int64_t M, int64_t K, int64_t N) {
-  if (M < 0 || K < 0 || N < 0) return -1;
-  return fold_floats((M + kRowsLinear - 1) / kRowsLinear, N * K + N) * (int64_t)sizeof(float);
-}
+namespace lpg {
+namespace {
 
-extern "C" lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
-                                               const float *W, const float *H, int64_t ldh, float *dH, int64_t lddh,
-                                               float *dW, float *db, void *workspace, void *stream) {
-  LPG_REQUIRE(M >= 0 && K >= 0 && N >= 1 && N <= kSmallNMax, "lpg_linear_small_bwd_f32: need 1 <= N <= %d",
-              kSmallNMax);
+lpg_status linear_small_bwd(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W,
+                            const float *H, int64_t ldh, float *dH, int64_t lddh, float scale, float *dW, float *db,
+                            float *dbY, bool mask, void *workspace, void *stream, const char *what) {
+  LPG_REQUIRE(M >= 0 && K >= 0 && N >= 1 && N <= kSmallNMax, "%s: need 1 <= N <= %d", what, kSmallNMax);
   LPG_REQUIRE(K % 4 == 0 && ldh % 4 == 0 && (dH == nullptr || lddh % 4 == 0),
-              "lpg_linear_small_bwd_f32: K and leading dims must be multiples of 4");
-  LPG_REQUIRE(G && W && H && workspace, "lpg_linear_small_bwd_f32: NULL pointer");
+              "%s: K and leading dims must be multiples of 4", what);
+  LPG_REQUIRE(G && W && H && workspace, "%s: NULL pointer", what);
   LPG_REQUIRE(aligned16(W) && aligned16(H) && (dH == nullptr || aligned16(dH)) && aligned16(workspace),
-              "lpg_linear_small_bwd_f32: W/H/dH/workspace must be 16-byte aligned");
+              "%s: W/H/dH/workspace must be 16-byte aligned", what);
   hipStream_t s = as_stream(stream);
   const int64_t nblk = (M + kRowsLinear - 1) / kRowsLinear;
   if (nblk == 0) {
     if (dW) LPG_HIP(hipMemsetAsync(dW, 0, sizeof(float) * N * K, s));
     if (db) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, s));
+    if (dbY) LPG_HIP(hipMemsetAsync(dbY, 0, sizeof(float) * K, s));
     return LPG_OK;
   }
   float *part = static_cast<float *>(workspace);
   const dim3 grid((unsigned)nblk), block(kT);
+#define LPG_LSB(NN)                                                                                               \
+  if (mask)                                                                                                       \
+    hipLaunchKernelGGL((linear_small_bwd_p1<NN, true>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh,     \
+                       scale, part);                                                                              \
+  else                                                                                                            \
+    hipLaunchKernelGGL((linear_small_bwd_p1<NN, false>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh,    \
+                       scale, part);
   switch (N) {
-    case 1: hipLaunchKernelGGL(linear_small_bwd_p1<1>, grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh, part); break;
-    case 2: hipLaunchKernelGGL(linear_small_bwd_p1<2>, grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh, part); break;
-    case 3: hipLaunchKernelGGL(linear_small_bwd_p1<3>, grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh, part); break;
-    default: hipLaunchKernelGGL(linear_small_bwd_p1<4>, grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh, part);
+    case 1: LPG_LSB(1) break;
+    case 2: LPG_LSB(2) break;
+    case 3: LPG_LSB(3) break;
+    default: LPG_LSB(4)
   }
+#undef LPG_LSB
   LPG_HIP(hipGetLastError());
-  const int64_t tot = N * K + N;
+  const int64_t tot = N * K + N + (mask ? K : 0);
   const float *img;
   const int64_t nrow = fold(nblk, tot, part, part + nblk * tot, &img, s);
-  hipLaunchKernelGGL(linear_small_bwd_p2, dim3((unsigned)((tot + kT - 1) / kT)), dim3(kT), 0, s, nrow, K, (int)N, img,
-                     dW, db);
+  hipLaunchKernelGGL(linear_small_bwd_p2, dim3((unsigned)((tot + kT - 1) / kT)), dim3(kT), 0, s, nrow, K, (int)N, tot,
+                     img, dW, db, dbY);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
+}
+
+}  // namespace
+}  // namespace lpg
+
+extern "C" int64_t lpg_linear_small_bwd_workspace_bytes(int64_t M, int64_t K, int64_t N) {
+  if (M < 0 || K < 0 || N < 0) return -1;
+  return fold_floats((M + kRowsLinear - 1) / kRowsLinear, N * K + N + K) * (int64_t)sizeof(float);
+}
+
+extern "C" lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
+                                               const float *W, const float *H, int64_t ldh, float *dH, int64_t lddh,
+                                               float *dW, float *db, void *workspace, void *stream) {
+  return linear_small_bwd(M, K, N, G, ldg, W, H, ldh, dH, lddh, 1.f, dW, db, nullptr, false, workspace, stream,
+                          "lpg_linear_small_bwd_f32");
+}
+
+extern "C" lpg_status lpg_heads_relu_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
+                                             const float *W, const float *Y, int64_t ldy, float scale, float *dZ,
+                                             int64_t lddz, float *dW, float *db, float *dbY, void *workspace,
+                                             void *stream) {
+  LPG_REQUIRE(dZ != nullptr, "lpg_heads_relu_bwd_f32: NULL dZ");
+  return linear_small_bwd(M, K, N, G, ldg, W, Y, ldy, dZ, lddz, scale, dW, db, dbY, true, workspace, stream,
+                          "lpg_heads_relu_bwd_f32");
 }

@@ -50,6 +50,7 @@ HEADER_SYMBOLS = (
     "lpg_relu_wgrad_smallk_f32",
     "lpg_linear_small_bwd_workspace_bytes",
     "lpg_linear_small_bwd_f32",
+    "lpg_heads_relu_bwd_f32",
     "lpg_knowledge_f32",
     "lpg_scan_i64_workspace_bytes",
     "lpg_scan_i64",
@@ -145,6 +146,9 @@ def lib() -> ctypes.CDLL:
     L.lpg_linear_small_bwd_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p,
                                            c_p, c_p]
     L.lpg_linear_small_bwd_f32.restype = c_i32
+    L.lpg_heads_relu_bwd_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, ctypes.c_float, c_p, c_i64,
+                                         c_p, c_p, c_p, c_p, c_p]
+    L.lpg_heads_relu_bwd_f32.restype = c_i32
     L.lpg_fc_set_variant.argtypes = [c_i32]
     L.lpg_fc_set_variant.restype = c_i32
     L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_i64, ctypes.c_float, c_p, c_i64, c_p]

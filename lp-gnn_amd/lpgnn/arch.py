@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ast
 import math
+import os
 import re
 from typing import Optional, Tuple
 
@@ -29,6 +30,9 @@ from torch import Tensor, nn
 from .sparse import BipartiteCSR, spmm
 from . import conv as _conv
 from . import fc as _fc
+
+# LPGNN_FUSE_HEADS=0: heads as their own autograd node (the last layer's ReLU backward then runs separately)
+FUSE_HEADS = os.environ.get("LPGNN_FUSE_HEADS", "1") == "1"
 
 
 class Linear(nn.Module):
@@ -171,14 +175,22 @@ class GCN_FC(GCNBase):
         # conv -> ReLU (arch.py:181-182): the ReLU is the FC kernel's epilogue.
         left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True)
         dp = self.dp if self.training else 0.0
-        for conv in self.layers:
+        layers = list(self.layers)
+        fuse_heads = (FUSE_HEADS and len(layers) > 0 and cd == torch.float32 and isinstance(edge_index, BipartiteCSR)
+                      and getattr(edge_index, "partitioned_conv", None) is None)
+        for conv in (layers[:-1] if fuse_heads else layers):
             # conv -> dropout -> ReLU (arch.py:185-188).  ReLU commutes with
             # dropout (x * mask / (1-p), a non-negative scale), so the ReLU is
             # fused into the FC and dropout follows it (inside the conv, so a
             # partitioned run drops each variable once, at its owner).
             left, right = conv(left, right, edge_index, relu=True, dropout=dp)
-        left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias)
-        right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias)
+        if fuse_heads:  # last layer + heads (arch.py:184-190) as one node: one backward pass over its output
+            last = layers[-1]
+            left, right = _conv.two_direction_heads(left, right, edge_index, last.left2right, last.right2left,
+                                                    self.lin_left, self.lin_right, dp)
+        else:
+            left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias)
+            right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias)
         return add_knowledge(left.float(), right.float(), x_left, x_right)
 
 

@@ -80,9 +80,10 @@ def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
     return spmm(f_out) + gemm(S.n_cols) < gemm(S.n_rows) + spmm(f_in)
 
 
-class _TwoDirection(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+    """The layer's forward (both directions); records on ctx what the backward
+    needs and returns (left_new, right_new, tensors to save)."""
+    if True:
         if dropout > 0 and not relu:
             raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
         bf16 = left.dtype == torch.bfloat16
@@ -120,14 +121,28 @@ class _TwoDirection(torch.autograd.Function):
         ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
         ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
         ctx.has_b = (b_l2r is not None, b_r2l is not None)
-        ctx.save_for_backward(left, right, agg_l, agg_r, left_new, right_new, *ws)
+        return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, *ws)
+
+
+class _TwoDirection(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+        left_new, right_new, saved = _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l,
+                                                   b_r2l, w_root_r2l, relu, dropout)
+        ctx.save_for_backward(*saved)
         return left_new, right_new
 
     @staticmethod
     def backward(ctx, g_left, g_right):
-        left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = \
-            ctx.saved_tensors
-        need = ctx.needs_input_grad
+        return _backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right)
+
+
+def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
+    """The layer's backward from its output gradients (g_left, g_right), or --
+    dz = (dz_l, db_r2l, dz_r, db_l2r) -- from gradients that already went
+    through its ReLU/dropout (the fused heads' backward)."""
+    if True:
+        left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
         A, AT = ctx.adj.fwd, ctx.adj.bwd
         bf16 = ctx.bf16
         dt = torch.bfloat16 if bf16 else torch.float32
@@ -142,7 +157,7 @@ class _TwoDirection(torch.autograd.Function):
                 return _fc.relu_bwd_colsum_bf16(g, y, ctx.scale, want_db)
             return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
 
-        small = (not bf16 and ctx.relu and agg_r is not None and agg_l is not None
+        small = (dz is None and not bf16 and ctx.relu and agg_r is not None and agg_l is not None
                  and agg_r.shape[1] + right.shape[1] <= 16 and agg_l.shape[1] + left.shape[1] <= 16
                  and right_new.shape[1] % 4 == 0)
         if small and not (need[0] or need[1]):
@@ -157,8 +172,11 @@ class _TwoDirection(torch.autograd.Function):
             return (None, None, None, keep(dw_rel_l2r, 3), db_l2r, keep(dw_root_l2r, 5), keep(dw_rel_r2l, 6), db_r2l,
                     keep(dw_root_r2l, 8), None, None)
 
-        dz_r, db_l2r = mask(g_right, right_new, ctx.has_b[0] and need[4])
-        dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
+        if dz is None:
+            dz_r, db_l2r = mask(g_right, right_new, ctx.has_b[0] and need[4])
+            dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
+        else:
+            dz_l, db_r2l, dz_r, db_l2r = dz
         main = torch.cuda.current_stream(dz_r.device)
         side = _side_stream(dz_r.device) if _OVERLAP else None
         esz = 2 if bf16 else 4
@@ -225,6 +243,49 @@ class _TwoDirection(torch.autograd.Function):
         if need[0]:  # left = src of left2right (S = A^T), dst of right2left
             g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l)
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
+
+
+class _TwoDirectionHeads(torch.autograd.Function):
+    """The last hidden layer and the heads (arch.py:184-190) as one node: the
+    hidden outputs feed only lin_left / lin_right, so the heads' backward and
+    the layer's ReLU/dropout backward (+ its bias column sums) are one pass
+    over the layer output (lpg_heads_relu_bwd_f32) instead of two (the heads'
+    dH, then relu_bwd_colsum re-reading dH and Y).  fp32, ReLU layers only."""
+
+    @staticmethod
+    def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
+                wh_l, bh_l, wh_r, bh_r):
+        left_new, right_new, saved = _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l,
+                                                   b_r2l, w_root_r2l, relu, dropout)
+        logit_l = _fc.fc_forward(left_new, wh_l, None, None, bh_l, False)
+        logit_r = _fc.fc_forward(right_new, wh_r, None, None, bh_r, False)
+        ctx.heads_b = (bh_l is not None, bh_r is not None)
+        ctx.save_for_backward(*saved, wh_l, wh_r)
+        return logit_l, logit_r
+
+    @staticmethod
+    def backward(ctx, g_ll, g_lr):
+        *saved, wh_l, wh_r = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        left_new, right_new = saved[4], saved[5]
+        g_ll = torch.zeros(left_new.shape[0], wh_l.shape[0], device=left_new.device) if g_ll is None else g_ll
+        g_lr = torch.zeros(right_new.shape[0], wh_r.shape[0], device=right_new.device) if g_lr is None else g_lr
+        dz_l, dwh_l, dbh_l, db_r2l = _fc.heads_relu_bwd(g_ll, wh_l, left_new, ctx.scale, ctx.has_b[1] and need[7])
+        dz_r, dwh_r, dbh_r, db_l2r = _fc.heads_relu_bwd(g_lr, wh_r, right_new, ctx.scale, ctx.has_b[0] and need[4])
+        core = _backward_core(ctx, saved, need, None, None, dz=(dz_l, db_r2l, dz_r, db_l2r))
+        keep = lambda t, i, has=True: t if (need[i] and has) else None
+        return (*core, keep(dwh_l, 11), keep(dbh_l, 12, ctx.heads_b[0]), keep(dwh_r, 13),
+                keep(dbh_r, 14, ctx.heads_b[1]))
+
+
+def two_direction_heads(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, lin_left, lin_right,
+                        dropout: float = 0.0):
+    """GraphConvTwoDirection (ReLU, dropout) followed by the heads lin_left /
+    lin_right (arch.py:184-190) through one autograd node: (logit_l, logit_r)."""
+    return _TwoDirectionHeads.apply(left, right, adj, left2right.lin_rel.weight, left2right.lin_rel.bias,
+                                    left2right.lin_root.weight, right2left.lin_rel.weight, right2left.lin_rel.bias,
+                                    right2left.lin_root.weight, True, float(dropout), lin_left.weight,
+                                    lin_left.bias, lin_right.weight, lin_right.bias)
 
 
 def two_direction(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, relu: bool = False,

@@ -416,6 +416,30 @@ def linear_small_bwd(G: Tensor, W: Tensor, H: Tensor, need_dh: bool):
     return dH, dW, db
 
 
+def heads_relu_bwd(G: Tensor, W: Tensor, Y: Tensor, scale: float, want_dby: bool):
+    """(dZ, dW, db, dbY): the heads' backward through the producing layer's
+    ReLU/dropout in one pass over Y (lpg_heads_relu_bwd_f32)."""
+    M, K = Y.shape
+    N = W.shape[0]
+    G, W = G.contiguous(), W.contiguous()
+    Y = Y if (Y.stride(1) == 1 and Y.stride(0) % 4 == 0 and Y.data_ptr() % 16 == 0) else Y.contiguous()
+    L = _lib.lib()
+    ws = torch.empty(max(L.lpg_linear_small_bwd_workspace_bytes(M, K, N), 16) // 4 + 4, dtype=torch.float32,
+                     device=Y.device)
+    dZ = torch.empty((M, K), dtype=torch.float32, device=Y.device)
+    dW = torch.empty_like(W)
+    db = torch.empty(N, dtype=torch.float32, device=Y.device)
+    dbY = torch.empty(K, dtype=torch.float32, device=Y.device) if want_dby else None
+    with torch.cuda.device(Y.device):
+        tok = TIMER.start(("heads_relu_bwd", M, N, K, "f32"))
+        st = L.lpg_heads_relu_bwd_f32(M, K, N, G.data_ptr(), G.stride(0), W.data_ptr(), Y.data_ptr(), Y.stride(0),
+                                      float(scale), dZ.data_ptr(), K, dW.data_ptr(), db.data_ptr(),
+                                      None if dbY is None else dbY.data_ptr(), ws.data_ptr(), _lib.stream_of(Y))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_heads_relu_bwd_f32")
+    return dZ, dW, db, dbY
+
+
 class _Linear(torch.autograd.Function):
     """torch.nn.Linear on lpg_fc_f32; few-output backward on the HIP kernel."""
 

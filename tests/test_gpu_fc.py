@@ -351,3 +351,22 @@ def test_relu_wgrad_smallk_equals_unfused(M, N, K1, K2, scale):
         bound = chain * 2.0 ** -24 * (dz.abs().t() @ A.double().abs())
         assert bool(((dW.double() - r).abs() <= bound + 1e-30).all())
     assert bool(((db.double() - dz.sum(0)).abs() <= chain * 2.0 ** -24 * dz.abs().sum(0) + 1e-30).all())
+
+
+@pytest.mark.parametrize("M,K,N,scale", [(1000, 1024, 3, 1.0), (777, 256, 3, 1.0 / 0.9), (5, 64, 2, 2.0)])
+def test_heads_relu_bwd_matches_unfused(M, K, N, scale):
+    """lpg_heads_relu_bwd_f32 == linear backward then ReLU/dropout backward + bias column sums."""
+    from lpgnn.fc import heads_relu_bwd
+
+    g = torch.Generator().manual_seed(M)
+    Y = torch.randn(M, K, generator=g).relu_().to(DEV)  # a ReLU output (zeros = dropped or inactive)
+    G = torch.randn(M, N, generator=g).to(DEV)
+    W = torch.randn(N, K, generator=g).to(DEV)
+    dZ, dW, db, dbY = heads_relu_bwd(G, W, Y, scale, True)
+    dH = G.double() @ W.double()
+    want_dz = torch.where(Y > 0, dH * scale, torch.zeros_like(dH))
+    torch.testing.assert_close(dZ.double(), want_dz, rtol=1e-5, atol=1e-5)
+    assert torch.equal(dZ == 0, Y == 0) or bool(((dZ == 0) | (Y > 0)).all())
+    torch.testing.assert_close(dW.double(), G.double().t() @ Y.double(), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(db.double(), G.double().sum(0), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(dbY.double(), want_dz.sum(0), rtol=1e-5, atol=1e-3)

@@ -205,3 +205,31 @@ def test_accuracy_device_matches_sklearn_path():
         got = accuracy_device(logits.to(DEV), gt.to(DEV), m)
         for a, b in zip(got, want):
             assert abs(a.item() - float(b)) < 1e-6
+
+
+def test_fused_heads_node_equals_separate_heads(monkeypatch):
+    """The last layer + heads as one autograd node (one backward pass over the
+    layer output) gives the same loss and gradients as heads as their own
+    node, with training dropout (same dropout seeds)."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, arch, synth
+    from lpgnn.train import balanced
+
+    g = synth.uniform_lp(900, 1700, 18000, seed=8)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                           y_s=torch.from_numpy(g.y_s).to(DEV), y_t=torch.from_numpy(g.y_t).to(DEV),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=256, depth=4, dp=0.1).to(DEV).train()
+    out = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(arch, "FUSE_HEADS", fuse)
+        model.zero_grad()
+        torch.manual_seed(123)  # same dropout seeds
+        lc, lv = model(batch)
+        loss = balanced(lc, lv, batch.y_s, batch.y_t)
+        loss.backward()
+        out[fuse] = (loss.item(), {k: p.grad.clone() for k, p in model.named_parameters()})
+    assert abs(out[True][0] - out[False][0]) < 1e-6
+    for k, v in out[True][1].items():
+        torch.testing.assert_close(v, out[False][1][k], rtol=1e-4, atol=1e-6, msg=k)
