@@ -176,18 +176,27 @@ class GCN_FC(GCNBase):
         left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True)
         dp = self.dp if self.training else 0.0
         layers = list(self.layers)
-        fuse_heads = (FUSE_HEADS and len(layers) > 0 and cd == torch.float32 and isinstance(edge_index, BipartiteCSR)
-                      and getattr(edge_index, "partitioned_conv", None) is None)
+        single = isinstance(edge_index, BipartiteCSR) and getattr(edge_index, "partitioned_conv", None) is None
+        part_heads = getattr(edge_index, "two_direction_heads", None)  # row-partitioned multi-GPU adjacency
+        fuse_heads = FUSE_HEADS and len(layers) > 0 and cd == torch.float32 and (single or part_heads is not None)
         for conv in (layers[:-1] if fuse_heads else layers):
             # conv -> dropout -> ReLU (arch.py:185-188).  ReLU commutes with
             # dropout (x * mask / (1-p), a non-negative scale), so the ReLU is
             # fused into the FC and dropout follows it (inside the conv, so a
             # partitioned run drops each variable once, at its owner).
             left, right = conv(left, right, edge_index, relu=True, dropout=dp)
+        out = None
         if fuse_heads:  # last layer + heads (arch.py:184-190) as one node: one backward pass over its output
             last = layers[-1]
-            left, right = _conv.two_direction_heads(left, right, edge_index, last.left2right, last.right2left,
-                                                    self.lin_left, self.lin_right, dp)
+            if single:
+                out = _conv.two_direction_heads(left, right, edge_index, last.left2right, last.right2left,
+                                                self.lin_left, self.lin_right, dp)
+            else:
+                out = part_heads(left, right, last.left2right, last.right2left, self.lin_left, self.lin_right, dp)
+                if out is None:  # not applicable on this adjacency: the separate path
+                    left, right = last(left, right, edge_index, relu=True, dropout=dp)
+        if out is not None:
+            left, right = out
         else:
             left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias)
             right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias)

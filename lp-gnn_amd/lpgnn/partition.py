@@ -367,6 +367,20 @@ class _PartTwoDirection(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+        left_new, right_new, saved = _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r,
+                                                        w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
+        ctx.save_for_backward(*saved)
+        return left_new, right_new
+
+    @staticmethod
+    def backward(ctx, g_left, g_right):
+        return _part_backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right)
+
+
+def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu,
+                       dropout):
+    """_PartTwoDirection's forward; returns (left_new, right_new, tensors to save)."""
+    if True:
         from . import fc as _fc
         from .conv import reassociate
         from .sparse import spmm_forward
@@ -403,27 +417,29 @@ class _PartTwoDirection(torch.autograd.Function):
         ctx.padj, ctx.relu = padj, relu
         ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
         ctx.has_b = (b_l2r is not None, b_r2l is not None)
-        ctx.save_for_backward(left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l,
-                              w_root_r2l)
-        return left_new, right_new
+        return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r,
+                                     w_rel_r2l, w_root_r2l)
 
-    @staticmethod
-    def backward(ctx, g_left, g_right):
+
+def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
+    """_PartTwoDirection's backward from the output gradients, or -- dz =
+    (dz_l, db_r2l, dz_r_own, db_l2r) -- from gradients that already went
+    through the layer's ReLU/dropout, owners' rows reduced (fused heads)."""
+    if True:
         from . import fc as _fc
         from .conv import _src_first
         from .sparse import spmm_forward
 
-        left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = \
-            ctx.saved_tensors
-        need = ctx.needs_input_grad
+        left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
         ex = ctx.padj.ex
         A, AT = ctx.padj.local.fwd, ctx.padj.local.bwd
         n_own = ex.n_own
-        if g_right is None:
-            g_right = torch.zeros_like(right_new)
-        if g_left is None:
-            g_left = torch.zeros_like(left_new)
-        red = ex.start_reduce(g_right.contiguous(), inplace=False)  # halo grads -> owners, in flight ...
+        if dz is None:
+            if g_right is None:
+                g_right = torch.zeros_like(right_new)
+            if g_left is None:
+                g_left = torch.zeros_like(left_new)
+            red = ex.start_reduce(g_right.contiguous(), inplace=False)  # halo grads -> owners, in flight ...
 
         def mask(g, y, want_db):
             if not ctx.relu:
@@ -441,17 +457,38 @@ class _PartTwoDirection(torch.autograd.Function):
                 d_root = _fc.wgrad(dz, x_dst) if need_root else None
             return (d_rel if need_rel else None), (d_root if need_root else None)
 
+        def narrow(agg, x_dst):  # conv1: the inputs are features -- weight gradients straight from (g, y)
+            return (dz is None and ctx.relu and not (need[0] or need[1]) and agg is not None
+                    and agg.shape[1] + x_dst.shape[1] <= 16 and left_new.shape[1] % 4 == 0)
+
         # ... under everything that only needs the constraint side's gradient
-        dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
-        dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
+        if dz is not None:
+            dz_l, db_r2l = dz[0], dz[1]
+            dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
+        elif narrow(agg_l, left):
+            dz_l = None
+            dw_rel_r2l, dw_root_r2l, db_r2l = _fc.relu_wgrad_smallk(g_left, left_new, ctx.scale, agg_l, left,
+                                                                    ctx.has_b[1] and need[7])
+        else:
+            dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
+            dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
         g_r = None
         if need[1]:  # right [owned | halo] as the source of right2left: every local row
             if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
                 g_r = _fc.input_grad(spmm_forward(AT, dz_l), w_rel_r2l)
             else:
                 g_r = spmm_forward(AT, _fc.input_grad(dz_l, w_rel_r2l))
-        g_right_own = red.finish()
-        dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
+        g_right_own = red.finish() if dz is None else None
+        if narrow(agg_r, right):
+            dw_rel_l2r, dw_root_l2r, db_l2r = _fc.relu_wgrad_smallk(g_right_own, right_new[:n_own], ctx.scale,
+                                                                    agg_r[:n_own], right[:n_own],
+                                                                    ctx.has_b[0] and need[4])
+            return (None, None, None, dw_rel_l2r if need[3] else None, db_l2r, dw_root_l2r if need[5] else None,
+                    dw_rel_r2l if need[6] else None, db_r2l, dw_root_r2l if need[8] else None, None, None)
+        if dz is None:
+            dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
+        else:
+            dz_r, db_l2r = dz[2], dz[3]
         # with T = A bcast(dZ_r) (computed for left's gradient below), lin_rel's weight gradient
         # dZ_r^T reduce(A^T left) = T^T left runs over the local constraints instead of the variables
         # (and is the only route when the forward was re-associated: agg_r was not kept)
@@ -485,6 +522,48 @@ class _PartTwoDirection(torch.autograd.Function):
         return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 
+class _PartTwoDirectionHeads(torch.autograd.Function):
+    """The last hidden layer + heads on a partition (conv._TwoDirectionHeads'
+    twin).  Backward: the halo rows' LOGIT gradients (3 wide) are reduced to
+    their owners -- a halo row is a copy of its owner's output, so the owner's
+    layer-output gradient is (its own + its halo copies' logit gradients) W --
+    then one pass over the owned rows gives dZ, the head and bias gradients
+    (lpg_heads_relu_bwd_f32)."""
+
+    @staticmethod
+    def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
+                wh_l, bh_l, wh_r, bh_r):
+        from . import fc as _fc
+
+        left_new, right_new, saved = _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r,
+                                                        w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
+        logit_l = _fc.fc_forward(left_new, wh_l, None, None, bh_l, False)
+        logit_r = _fc.fc_forward(right_new, wh_r, None, None, bh_r, False)
+        ctx.heads_b = (bh_l is not None, bh_r is not None)
+        ctx.save_for_backward(*saved, wh_l, wh_r)
+        return logit_l, logit_r
+
+    @staticmethod
+    def backward(ctx, g_ll, g_lr):
+        from . import fc as _fc
+
+        *saved, wh_l, wh_r = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        left_new, right_new = saved[4], saved[5]
+        ex = ctx.padj.ex
+        g_ll = torch.zeros(left_new.shape[0], wh_l.shape[0], device=left_new.device) if g_ll is None else g_ll
+        g_lr = torch.zeros(right_new.shape[0], wh_r.shape[0], device=right_new.device) if g_lr is None else g_lr
+        red = ex.start_reduce(g_lr.contiguous(), inplace=False)  # halo logit grads -> owners, in flight ...
+        dz_l, dwh_l, dbh_l, db_r2l = _fc.heads_relu_bwd(g_ll, wh_l, left_new, ctx.scale, ctx.has_b[1] and need[7])
+        g_own = red.finish()
+        dz_r, dwh_r, dbh_r, db_l2r = _fc.heads_relu_bwd(g_own, wh_r, right_new[:ex.n_own], ctx.scale,
+                                                        ctx.has_b[0] and need[4])
+        core = _part_backward_core(ctx, saved, need, None, None, dz=(dz_l, db_r2l, dz_r, db_l2r))
+        keep = lambda t, i, has=True: t if (need[i] and has) else None
+        return (*core, keep(dwh_l, 11), keep(dbh_l, 12, ctx.heads_b[0]), keep(dwh_r, 13),
+                keep(dbh_r, 14, ctx.heads_b[1]))
+
+
 class PartitionedCSR:
     """The edge_index of a rank's batch: local dual CSR + boundary exchange.
 
@@ -516,6 +595,16 @@ class PartitionedCSR:
                                        left2right.lin_root.weight, right2left.lin_rel.weight,
                                        right2left.lin_rel.bias, right2left.lin_root.weight, bool(relu),
                                        float(dropout))
+
+    def two_direction_heads(self, left, right, left2right, right2left, lin_left, lin_right, dropout=0.0):
+        """The last layer + heads (arch.py:184-190) on this partition, one autograd node (None: not applicable)."""
+        if self.orient != "cons" or left.dtype != torch.float32 or _local_spmm is not _product_spmm:
+            return None
+        return _PartTwoDirectionHeads.apply(left, right, self, left2right.lin_rel.weight, left2right.lin_rel.bias,
+                                            left2right.lin_root.weight, right2left.lin_rel.weight,
+                                            right2left.lin_rel.bias, right2left.lin_root.weight, True,
+                                            float(dropout), lin_left.weight, lin_left.bias, lin_right.weight,
+                                            lin_right.bias)
 
     def partitioned_conv(self, x, fc):
         """One GraphConv direction: fc(agg, x_dst) is lin_rel + lin_root (+ReLU, +dropout)."""
