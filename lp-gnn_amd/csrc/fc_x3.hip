@@ -611,7 +611,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t
   auto swz = [](int row) { return M16 ? ((row >> 3) & 1) * 4 : 0; };  // 16-B chunk XOR of a row
 
   // block -> (split s, output tile); consecutive blocks share s (same rows of G and X in L2)
-  const int64_t bid = blockIdx.x;
+  // XCD-aware remap (blocks go round-robin to the 8 XCDs): each XCD walks a contiguous range of
+  // (split, tile) ids, so the tiles of one R range run on one XCD and share its rows of G and X
+  // in that XCD's L2 (round-robin spread them over all 8 L2s: 4x the bytes fetched past L2)
+  const int64_t nwg = (int64_t)gridDim.x, xcd = (int64_t)blockIdx.x % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t bid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (int64_t)blockIdx.x / 8;
   const int64_t tiles = nt * kt;
   const int64_t s = bid / tiles, tile = bid % tiles;
   const int64_t n0 = (tile / kt) * WG_T, k0 = (tile % kt) * WG_T;
@@ -765,7 +769,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3c(int64_t R, int64_t N, int64_
   constexpr int OPB = 3 * PLANE;        // one operand's three planes
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * OPB];
 
-  const int64_t bid = blockIdx.x;
+  // XCD-aware remap (blocks go round-robin to the 8 XCDs): each XCD walks a contiguous range of
+  // (split, tile) ids, so the tiles of one R range run on one XCD and share its rows of G and X
+  // in that XCD's L2 (round-robin spread them over all 8 L2s: 4x the bytes fetched past L2)
+  const int64_t nwg = (int64_t)gridDim.x, xcd = (int64_t)blockIdx.x % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t bid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (int64_t)blockIdx.x / 8;
   const int64_t tiles = nt * kt;
   const int64_t s = bid / tiles, tile = bid % tiles;
   const int64_t n0 = (tile / kt) * WG_T, k0 = (tile % kt) * WG_T;
