@@ -49,7 +49,7 @@ def _pad_k(t: Tensor, mult: int = 4) -> Tensor:
 
 
 # fp32 FC arithmetic: "fp32" = the exact fp32 MFMA kernel (bitwise contract of oracle/fc_ref.c),
-# "x3" = fp32 on the bf16 matrix cores through the exact three-way bf16 split (lpg_fc_f32 flag 4).
+# "x3" = fp32 on the bf16 matrix cores through the exact three-way bf16 split (lpg_fc_x3_f32, lpg_wgrad_x3_f32).
 ARITH = os.environ.get("LPGNN_FC_ARITH", "x3")
 
 _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless the narrow-input kernel applies
