@@ -29,8 +29,11 @@
 // Operands: A (activations) fp32 as in lpg_fc_f32, split in registers by the
 // lane that feeds it to the MFMA; W pre-split once per call (lpg_split3_f32:
 // three bf16 planes, weights are small) so only A costs VALU in the k loop.
-// Tiling: 4 waves (2 x 2), 128 x 128 output tile, each wave 2 x 2 fragments of
-// 32 x 32 (accH + accL: 128 VGPRs).  k-tiles of BK = 32 staged by LDS-DMA
+// Two kernel families.  fc_fwd_x3 (variants 1-4, 8): 4 waves (2 x 2),
+// 128 x 128 output tile, each wave 2 x 2 fragments of 32 x 32 from
+// v_mfma_f32_32x32x16_bf16 (accH + accL: 128 VGPRs).  fc_fwd_x3_16 (the
+// default, variant 0 = <4,1,2,8>, and 5-7, 9, 10): v_mfma_f32_16x16x32_bf16
+// fragments, which hold a higher clock under DVFS on gfx950.  Both:  k-tiles of BK = 32 staged by LDS-DMA
 // (global_load_lds) into a 2-stage ring: A as 128-B fp32 rows (16-B chunk c of
 // row r at c ^ ((r >> 1) & 7)), each W plane as 64-B bf16 rows (chunk c at
 // c ^ ((r >> 2) & 3)); both make the ds_read_b128 fragment reads
@@ -795,11 +798,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3c(int64_t R, int64_t N, int64_
   }
   unsigned char *img = smem + op * OPB;
   f32x4 raw[8];
-  auto load = [&](int64_t c) {
+  auto load = [&](int64_t c) {  // rows past R read the zero row: no branch, every load stays in flight
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int64_t r = c * 32 + rg * 8 + e;
-      raw[e] = r < R ? *reinterpret_cast<const f32x4 *>(base + r * ld) : f32x4{0.f, 0.f, 0.f, 0.f};
+      raw[e] = *reinterpret_cast<const f32x4 *>(r < R ? base + r * ld : zrow + cg * 4);
     }
   };
   auto split_store = [&]() {
@@ -872,6 +875,133 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3c(int64_t R, int64_t N, int64_
   }
 }
 
+// Producer/consumer variant of wgrad_x3c: 8 waves, one block per CU.  Waves
+// 0-3 multiply (wgrad_x3c's 2 x 2 wave tiles of 64 x 64); waves 4-7 load and
+// split (wgrad_x3c's tasks) the NEXT chunk into the other of two plane buffers
+// (2 x 48 KiB).  Every SIMD then holds one multiplying and one splitting wave
+// (SIMD partners are waves w and w + 4): the split VALU issues under the
+// partner's MFMAs instead of in a phase of its own, and one barrier per chunk
+// separates the buffers.  Each producer's global loads for the next chunk
+// are in flight across the barrier.  Same products in the same order as wgrad_x3c: bitwise the same
+// partials.
+__global__ __launch_bounds__(512, 1) void wgrad_x3p(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
+                                                    int64_t ldg, const float *__restrict__ X, int64_t ldx,
+                                                    float *__restrict__ part, const float *__restrict__ zrow,
+                                                    int64_t nt, int64_t kt, int64_t chunks_per_split) {
+  constexpr int PLANE = WG_T * 32 * 2;
+  constexpr int OPB = 3 * PLANE;
+  constexpr int BUF = 2 * OPB;  // G planes, then X planes: 48 KiB
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+
+  const int64_t nwg = (int64_t)gridDim.x, xcd = (int64_t)blockIdx.x % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t bid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (int64_t)blockIdx.x / 8;
+  const int64_t tiles = nt * kt;
+  const int64_t s = bid / tiles, tile = bid % tiles;
+  const int64_t n0 = (tile / kt) * WG_T, k0 = (tile % kt) * WG_T;
+  const int64_t nchunks = (R + 31) / 32;
+  const int64_t c0 = s * chunks_per_split;
+  const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
+  const int T = (int)(c1 - c0);  // >= 1 (the host sizes the splits so)
+
+  const int tid = threadIdx.x, wave = tid >> 6;
+  if (wave >= 4) {  // ---- producers
+    const int pt = tid - 256;
+    const int op = pt >> 7, cg = pt & 31, rg = (pt >> 5) & 3;
+    const int64_t lim = op ? K : N;
+    int64_t col0 = (op ? k0 : n0) + cg * 4;
+    col0 = col0 < lim ? col0 : lim - 4;  // N, K multiples of 4: columns past the edge are never stored
+    const float *base = (op ? X : G) + col0;
+    const int64_t ld = op ? ldx : ldg;
+    f32x4 raw[8];
+    auto load = [&](int64_t c) {  // rows past R read the zero row (no branch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int64_t r = c * 32 + rg * 8 + e;
+        raw[e] = *reinterpret_cast<const f32x4 *>(r < R ? base + r * ld : zrow + cg * 4);
+      }
+    };
+    // iteration t: chunk t into buffer t & 1 (the consumers multiply chunk t - 1 meanwhile), then
+    // the loads of chunk t + 1 (the last iteration re-reads chunk T - 1, unused), in flight under
+    // the next iteration's barrier wait
+    load(c0);
+    for (int t = 0; t <= T; ++t) {
+      if (t < T) {
+        unsigned char *img = smem + (t & 1) * BUF + op * OPB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const Split3 sp = split3(f32x4{raw[0][q], raw[1][q], raw[2][q], raw[3][q]},
+                                   f32x4{raw[4][q], raw[5][q], raw[6][q], raw[7][q]});
+          const int col = cg * 4 + q;
+          unsigned char *dst = img + col * 64 + swzW(col, rg) * 16;
+          *reinterpret_cast<bf16x8 *>(dst) = sp.h;
+          *reinterpret_cast<bf16x8 *>(dst + PLANE) = sp.m;
+          *reinterpret_cast<bf16x8 *>(dst + 2 * PLANE) = sp.l;
+        }
+        load(c0 + (t + 1 < T ? t + 1 : T - 1));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
+
+  // ---- consumers
+  const int lane = tid & 63, wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  f32x4 accH[4][4], accL[4][4];
+  const f32x4 zero = {};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accH[i][j] = accL[i][j] = zero;
+  auto frag = [&](const unsigned char *im, int col, bf16x8 (&f)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8 *>(im + p * PLANE + col * 64 + swzW(col, fg) * 16);
+  };
+  auto multiply = [&](int b) {
+    const unsigned char *buf = smem + b * BUF;
+    bf16x8 bv[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) frag(buf + OPB, wn * 64 + j * 16 + fr, bv[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 av[3];
+      frag(buf, wm * 64 + i * 16 + fr, av);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], bv[j][0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][1], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][2], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][1], accL[i][j], 0, 0, 0);
+        accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][0], accH[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  // the producers' barrier sequence: T + 1 barriers
+  for (int t = 0; t <= T; ++t) {
+    if (t >= 1) multiply((t - 1) & 1);  // chunk t - 1
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  float *P = part + s * N * K;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t col = k0 + wn * 64 + j * 16 + fr;
+    if (col >= K) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = n0 + wm * 64 + i * 16 + 4 * fg + r;
+        if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
+      }
+  }
+}
+
 // dW[n, k] = sum_s part[s][n, k], s ascending (fixed order), float4 per thread
 __global__ __launch_bounds__(256) void wgrad_fold(int64_t N, int64_t K, int64_t S, const float *__restrict__ part,
                                                   float *__restrict__ dW, int64_t lddw) {
@@ -901,7 +1031,9 @@ int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
 }
 
 int g_x3_variant = 0;
-int g_wgrad_m16 = 2;  // lpg_fc_x3_set_variant(100 + v): wgrad kernel (0 = 32x32x16, 1 = 16x16x32, 2 = cooperative)
+// lpg_fc_x3_set_variant(100 + v): wgrad kernel (0 = 32x32x16, 1 = 16x16x32, 2 = cooperative,
+// 3 = producer/consumer)
+int g_wgrad_m16 = 2;
 
 }  // namespace
 }  // namespace lpg
@@ -964,7 +1096,7 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
 }
 
 extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
-  if (v >= 100 && v <= 102) {
+  if (v >= 100 && v <= 103) {
     g_wgrad_m16 = v - 100;
     return LPG_OK;
   }
@@ -1002,7 +1134,10 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   float *zrow = part + S * N * K;  // 128 zero floats after the partials (lpg_wgrad_x3_workspace_bytes)
   hipStream_t st = as_stream(stream);
   LPG_HIP(hipMemsetAsync(zrow, 0, 512, st));
-  if (g_wgrad_m16 == 2)
+  if (g_wgrad_m16 == 3)
+    hipLaunchKernelGGL(wgrad_x3p, dim3((unsigned)nblk), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, zrow, nt, kt,
+                       cps);
+  else if (g_wgrad_m16 == 2)
     hipLaunchKernelGGL(wgrad_x3c, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
                        nt, kt, S_used, cps);
   else if (g_wgrad_m16)

@@ -182,6 +182,37 @@ def test_wgrad_x3_accuracy_vs_fp64(R, N, K):
     assert torch.equal(got, again)  # fixed-order split reduction: run-to-run identical
 
 
+@pytest.mark.parametrize("R,N,K", [
+    (20, 64, 64),         # one partial chunk per split (T = 1)
+    (37, 132, 260),       # ragged tiles, T = 2
+    (1000, 256, 128),     # T = 8
+    (3000, 128, 128),     # T = 9 (odd), shorter last split
+    (70000, 128, 64),     # T = 35, many splits
+    (4096, 1024, 1024),   # hidden-layer tile grid
+])
+def test_wgrad_x3_kernels_bitwise_equal(R, N, K):
+    """The producer/consumer weight-gradient kernel (variant 103) forms the
+    cooperative kernel's products in the same order: identical bits."""
+    from lpgnn import _lib
+    from lpgnn.fc import wgrad
+
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(R * 7 + K)
+    G = torch.randn(R, N, generator=g).to(DEV)
+    X = torch.randn(R, K, generator=g).relu().to(DEV)
+    out = {}
+    try:
+        for v in (102, 103):
+            assert L.lpg_fc_x3_set_variant(v) == 0
+            out[v] = wgrad(G, X, arith="x3")
+    finally:
+        L.lpg_fc_x3_set_variant(100 + _DEFAULT_WGRAD)
+    assert torch.equal(out[102], out[103])
+
+
+_DEFAULT_WGRAD = 2  # csrc/fc_x3.hip g_wgrad_m16
+
+
 def test_wgrad_x3_strided_inputs():
     from lpgnn.fc import wgrad
 
