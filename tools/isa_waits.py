@@ -9,7 +9,7 @@ import sys
 
 src, want = sys.argv[1], sys.argv[2]
 text = open(src).read()
-start = next(m.start() for m in re.finditer(r"^(\S+):\s*$", text, re.M) if want in m.group(1))
+start = next(m.start() for m in re.finditer(r"^([A-Za-z_.$][^\s:]*):", text, re.M) if want in m.group(1))
 end = text.find(".Lfunc_end", start)
 lines = text[start:end].split("\n")
 print(f"{len(lines)} lines")
