@@ -184,9 +184,10 @@ lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int
  * 32x32x16 MFMAs: 1 = 256 x 128, 2 = 128 x 256, 3 / 4 = 128 x 128 / 256 x 128
  * software-pipelined, 8 = 128 x 128.  Variants on the same MFMA shape give
  * identical bits (the two shapes differ in in-instruction summation).
- * 100 / 101 / 102: the weight-gradient kernel (32x32x16 / 16x16x32 /
- * cooperative 16x16x32 with one split per element, default 102; 101 and 102
- * give identical bits).  99: a timing probe without the activation split
+ * 100 / 101 / 102 / 103: the weight-gradient kernel (32x32x16 / 16x16x32 /
+ * cooperative 16x16x32 with one split per element, default 102 /
+ * producer-consumer form of 102; 101, 102 and 103 give identical bits).
+ * 99: a timing probe without the activation split
  * (WRONG results, measurement only). */
 lpg_status lpg_fc_x3_set_variant(int32_t v);
 
