@@ -764,6 +764,23 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t
 // each, 16x16x32) read b128 fragments.  One plane buffer (48 KiB), two
 // barriers per chunk.  Per lane and chunk: 32 splits (vs 64 when each wave
 // splits what it reads) and 24 ds_read_b128 (vs 64 ds_read_b32).
+// 16-B raw buffer load (v# in SGPRs: base and size wave-uniform): offsets at or past `nbytes`
+// return zeros, with no branch and no compare in the kernel
+__device__ __forceinline__ f32x4 buf_load4(const float *base, uint32_t nbytes, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), (short)0, (int)nbytes, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+#else
+  return f32x4{};
+#endif
+}
+
+// BUF: loads through a buffer descriptor over the block's R range (wave-uniform base, per-lane
+// offsets fixed for the whole loop, the chunk/row step as the scalar offset, rows past R out of
+// range = zeros): no per-load 64-bit address arithmetic or bounds compare (the host picks it
+// when the range's byte offsets fit 31 bits)
+template <bool BUF>
 __global__ __launch_bounds__(256, 2) void wgrad_x3c(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
                                                     int64_t ldg, const float *__restrict__ X, int64_t ldx,
                                                     float *__restrict__ part, const float *__restrict__ zrow,
@@ -785,24 +802,35 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3c(int64_t R, int64_t N, int64_
   const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // load/split task: operand (G or X), 4 columns cg*4 .. +3, rows rg*8 .. +7 of the chunk
-  const int op = tid >> 7, cg = tid & 31, rg = (tid >> 5) & 3;
+  // load/split task: operand (G or X; waves 0-1 / 2-3, so wave-uniform), 4 columns cg*4 .. +3,
+  // rows rg*8 .. +7 of the chunk
+  const int op = __builtin_amdgcn_readfirstlane(tid >> 7), cg = tid & 31, rg = (tid >> 5) & 3;
   const float *base;
   int64_t ld, col0;
+  const int64_t colb = op ? k0 : n0;
   {
     const int64_t lim = op ? K : N;
-    col0 = (op ? k0 : n0) + cg * 4;
+    col0 = colb + cg * 4;
     col0 = col0 < lim ? col0 : lim - 4;  // N, K multiples of 4: columns past the edge are never stored
     base = (op ? X : G) + col0;
     ld = op ? ldx : ldg;
   }
+  // BUF: descriptor from row c0 * 32, column colb of the operand
+  const float *sbase = (op ? X : G) + c0 * 32 * ld + colb;
+  const int64_t left = (R - c0 * 32) * ld * 4;
+  const uint32_t nbytes = (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff);
+  const int voff = (int)((col0 - colb) * 4 + rg * 8 * ld * 4);
   unsigned char *img = smem + op * OPB;
   f32x4 raw[8];
-  auto load = [&](int64_t c) {  // rows past R read the zero row: no branch, every load stays in flight
+  auto load = [&](int64_t c) {  // rows past R read zeros: no branch, every load stays in flight
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int64_t r = c * 32 + rg * 8 + e;
-      raw[e] = *reinterpret_cast<const f32x4 *>(r < R ? base + r * ld : zrow + cg * 4);
+      if constexpr (BUF) {
+        raw[e] = buf_load4(sbase, nbytes, voff, (int)(((c - c0) * 32 + e) * ld * 4));
+      } else {
+        const int64_t r = c * 32 + rg * 8 + e;
+        raw[e] = *reinterpret_cast<const f32x4 *>(r < R ? base + r * ld : zrow + cg * 4);
+      }
     }
   };
   auto split_store = [&]() {
@@ -1137,9 +1165,12 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   if (g_wgrad_m16 == 3)
     hipLaunchKernelGGL(wgrad_x3p, dim3((unsigned)nblk), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, zrow, nt, kt,
                        cps);
-  else if (g_wgrad_m16 == 2)
-    hipLaunchKernelGGL(wgrad_x3c, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
+  else if (g_wgrad_m16 == 2 && (cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31))
+    hipLaunchKernelGGL(wgrad_x3c<true>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
                        nt, kt, S_used, cps);
+  else if (g_wgrad_m16 == 2)
+    hipLaunchKernelGGL(wgrad_x3c<false>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part,
+                       zrow, nt, kt, S_used, cps);
   else if (g_wgrad_m16)
     hipLaunchKernelGGL(wgrad_x3<true>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
                        nt, kt, S_used, cps);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over the x3 FC kernel at the c2 hidden-layer shape (tools/x3_drive.py):
+# PMC passes over the x3 weight-gradient kernel at the c2 shape (tools/wgrad_drive.py):
 # SQ issue/wait counters + GRBM_GUI_ACTIVE (clock), then FETCH_SIZE, then WRITE_SIZE (separate passes).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"; mkdir -p gpurun_out; export TMPDIR=/tmp
