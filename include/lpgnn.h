@@ -180,7 +180,8 @@ lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int
 /* Tile choice for lpg_fc_x3_f32 (tuning).  On 16x16x32 MFMAs: 0 = default =
  * 10, 5 / 6 / 7 = 128 x 128 / 256 x 128 / 128 x 64 tiles of 64 x 64 (or
  * 64 x 32) wave tiles, 9 / 10 = 256 x 128 / 128 x 128 tiles of 32 x 128 wave
- * tiles (each A row split by one wave only); on
+ * tiles (each A row split by one wave only), 11 = 10 with XCD pairs sharing
+ * n-tile pairs when N spans 8 tiles (N = 1024); on
  * 32x32x16 MFMAs: 1 = 256 x 128, 2 = 128 x 256, 3 / 4 = 128 x 128 / 256 x 128
  * software-pipelined, 8 = 128 x 128.  Variants on the same MFMA shape give
  * identical bits (the two shapes differ in in-instruction summation).

@@ -72,6 +72,7 @@ struct X3Args {
   uint32_t drop_thresh;
   float drop_scale;
   int32_t accum;
+  int32_t xmap;  // fc_fwd_x3_16 block -> tile map: 0 = m-major per XCD, 1 = n-tile pairs per XCD pair
 };
 
 __device__ __forceinline__ unsigned pk_bf16(float x, float y) {  // v_cvt_pk_bf16_f32: RNE, x in the low half
@@ -383,9 +384,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
   const int64_t nwg = a.mt * a.nt;
   const int64_t bid = blockIdx.x;
   const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
-  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
-  const int64_t m0 = (wgid / a.nt) * BM;
-  const int64_t n0 = (wgid % a.nt) * BN;
+  int64_t m0, n0;
+  if (a.xmap) {  // nt == 8: XCDs x and x + 4 share n-tiles 2(x%4), +1 (their W planes stay in L2)
+    // and split the m-tiles: the pair's 2 * mt tiles in (m, n) order, first mt on x, rest on x + 4
+    const int64_t t = (xcd >> 2) * a.mt + bid / 8;
+    m0 = (t >> 1) * BM;
+    n0 = ((xcd & 3) * 2 + (t & 1)) * BN;
+  } else {
+    const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
+    m0 = (wgid / a.nt) * BM;
+    n0 = (wgid % a.nt) * BN;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -1117,6 +1126,9 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
     case 8: return launch_x3<2, 2, 2, 2>(a, relu, s);  // 128 x 128, 4 waves
     case 9: return launch_x3_16<8, 1, 2, 8>(a, relu, s);   // 256 x 128, 8 waves of 32 x 128 (A split once)
     case 10: return launch_x3_16<4, 1, 2, 8>(a, relu, s);  // 128 x 128, 4 waves of 32 x 128
+    case 11:  // variant 10 with the n-tile-pair XCD map (N = 1024: 8 n-tiles)
+      a.xmap = (a.N + 127) / 128 == 8;
+      return launch_x3_16<4, 1, 2, 8>(a, relu, s);
     case 99: return launch_x3_16<4, 2, 4, 4, true>(a, relu, s);  // timing probe: no A split (WRONG results)
     default:  // (tools/exp_x3.py at the c2 shapes: 199-212 TF/s, 5-10 % over 5 / 6)
       return launch_x3_16<4, 1, 2, 8>(a, relu, s);
@@ -1128,7 +1140,7 @@ extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
     g_wgrad_m16 = v - 100;
     return LPG_OK;
   }
-  LPG_REQUIRE((v >= 0 && v <= 10) || v == 99, "lpg_fc_x3_set_variant: variant %d not in [0, 10]", v);
+  LPG_REQUIRE((v >= 0 && v <= 11) || v == 99, "lpg_fc_x3_set_variant: variant %d not in [0, 11]", v);
   g_x3_variant = v;
   return LPG_OK;
 }

@@ -97,15 +97,36 @@ def test_x3_variants_identical():
     b = torch.randn(300, generator=g).to(DEV)
     L = _lib.lib()
     outs = {}
-    for v in range(11):
+    for v in range(12):
         assert L.lpg_fc_x3_set_variant(v) == 0
         outs[v] = fc_forward(A1, W1, A2, W2, b, True, arith="x3")
     L.lpg_fc_x3_set_variant(0)
     for v in (2, 3, 4, 8):  # 32x32x16
         assert torch.equal(outs[v], outs[1]), v
-    for v in (5, 6, 7, 9, 10):  # 16x16x32 (the default)
+    for v in (5, 6, 7, 9, 10, 11):  # 16x16x32 (the default)
         assert torch.equal(outs[v], outs[0]), v
     torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M", [1024, 1100, 37])
+def test_x3_xcd_pair_map_covers_every_tile(M):
+    """Variant 11 (N = 1024: XCD pairs share n-tile pairs, odd m-tile counts split mid-pair) computes
+    every tile once: identical bits to the default map."""
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward
+
+    g = torch.Generator().manual_seed(M)
+    A1, W1 = torch.randn(M, 256, generator=g).to(DEV), torch.randn(1024, 256, generator=g).to(DEV)
+    b = torch.randn(1024, generator=g).to(DEV)
+    L = _lib.lib()
+    outs = {}
+    try:
+        for v in (0, 11):
+            assert L.lpg_fc_x3_set_variant(v) == 0
+            outs[v] = fc_forward(A1, W1, None, None, b, True, arith="x3")
+    finally:
+        L.lpg_fc_x3_set_variant(0)
+    assert torch.equal(outs[0], outs[11])
 
 
 @pytest.mark.parametrize("relu", [False, True])
