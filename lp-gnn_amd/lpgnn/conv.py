@@ -83,45 +83,44 @@ def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
 def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
     """The layer's forward (both directions); records on ctx what the backward
     needs and returns (left_new, right_new, tensors to save)."""
-    if True:
-        if dropout > 0 and not relu:
-            raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
-        bf16 = left.dtype == torch.bfloat16
-        ws = (w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l)
-        if bf16:
-            ws = tuple(w.to(torch.bfloat16) for w in ws)
-        A, AT = adj.fwd, adj.bwd  # A: cons x vars (right2left), AT: vars x cons (left2right)
-        seed_r = _fc._new_seed() if dropout > 0 else 0
-        seed_l = _fc._new_seed() if dropout > 0 else 0
-        f_out = ws[0].shape[0]
-        ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out)
-        ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out)
+    if dropout > 0 and not relu:
+        raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
+    bf16 = left.dtype == torch.bfloat16
+    ws = (w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l)
+    if bf16:
+        ws = tuple(w.to(torch.bfloat16) for w in ws)
+    A, AT = adj.fwd, adj.bwd  # A: cons x vars (right2left), AT: vars x cons (left2right)
+    seed_r = _fc._new_seed() if dropout > 0 else 0
+    seed_l = _fc._new_seed() if dropout > 0 else 0
+    f_out = ws[0].shape[0]
+    ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out)
+    ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out)
 
-        def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None):
-            if ra:  # S (x_src W_rel^T), then lin_root + bias + ReLU accumulated onto it in place
-                fc = _fc.fc_forward_bf16 if bf16 else _fc.fc_forward
-                y = spmm_forward(S, fc(x_src, w_rel, None, None, None, False))
-                return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None
-            agg = spmm_forward(S, x_src) if agg is None else agg
-            return _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, dropout, seed, bf16), agg
+    def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None):
+        if ra:  # S (x_src W_rel^T), then lin_root + bias + ReLU accumulated onto it in place
+            fc = _fc.fc_forward_bf16 if bf16 else _fc.fc_forward
+            y = spmm_forward(S, fc(x_src, w_rel, None, None, None, False))
+            return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None
+        agg = spmm_forward(S, x_src) if agg is None else agg
+        return _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, dropout, seed, bf16), agg
 
-        side = _side_stream(left.device) if _OVERLAP and not ra_l else None
-        agg_l = None
-        if side is not None:  # right2left's HBM-bound SpMM beside left2right's MFMA-bound FC
-            side.wait_stream(torch.cuda.current_stream(left.device))
-            with torch.cuda.stream(side):
-                agg_l = spmm_forward(A, right)
-        # arch.py:75-77: right' = left2right((left, right), A^T)
-        right_new, agg_r = direction(AT, left, right, ws[0], b_l2r, ws[1], seed_r, ra_r)
-        if side is not None:
-            torch.cuda.current_stream(left.device).wait_stream(side)
-            agg_l.record_stream(torch.cuda.current_stream(left.device))
-        # arch.py:78-80: left' = right2left((right, left), A)
-        left_new, agg_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l)
-        ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
-        ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
-        ctx.has_b = (b_l2r is not None, b_r2l is not None)
-        return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, *ws)
+    side = _side_stream(left.device) if _OVERLAP and not ra_l else None
+    agg_l = None
+    if side is not None:  # right2left's HBM-bound SpMM beside left2right's MFMA-bound FC
+        side.wait_stream(torch.cuda.current_stream(left.device))
+        with torch.cuda.stream(side):
+            agg_l = spmm_forward(A, right)
+    # arch.py:75-77: right' = left2right((left, right), A^T)
+    right_new, agg_r = direction(AT, left, right, ws[0], b_l2r, ws[1], seed_r, ra_r)
+    if side is not None:
+        torch.cuda.current_stream(left.device).wait_stream(side)
+        agg_l.record_stream(torch.cuda.current_stream(left.device))
+    # arch.py:78-80: left' = right2left((right, left), A)
+    left_new, agg_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l)
+    ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
+    ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
+    ctx.has_b = (b_l2r is not None, b_r2l is not None)
+    return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, *ws)
 
 
 class _TwoDirection(torch.autograd.Function):
@@ -141,108 +140,107 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
     """The layer's backward from its output gradients (g_left, g_right), or --
     dz = (dz_l, db_r2l, dz_r, db_l2r) -- from gradients that already went
     through its ReLU/dropout (the fused heads' backward)."""
-    if True:
-        left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
-        A, AT = ctx.adj.fwd, ctx.adj.bwd
-        bf16 = ctx.bf16
-        dt = torch.bfloat16 if bf16 else torch.float32
+    left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
+    A, AT = ctx.adj.fwd, ctx.adj.bwd
+    bf16 = ctx.bf16
+    dt = torch.bfloat16 if bf16 else torch.float32
 
-        def mask(g, y, want_db):
-            if g is None:
-                g = torch.zeros_like(y)
-            if not ctx.relu:
-                g = g.to(dt).contiguous()
-                return g, (g.float().sum(0) if want_db else None)
-            if bf16:
-                return _fc.relu_bwd_colsum_bf16(g, y, ctx.scale, want_db)
-            return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
+    def mask(g, y, want_db):
+        if g is None:
+            g = torch.zeros_like(y)
+        if not ctx.relu:
+            g = g.to(dt).contiguous()
+            return g, (g.float().sum(0) if want_db else None)
+        if bf16:
+            return _fc.relu_bwd_colsum_bf16(g, y, ctx.scale, want_db)
+        return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
 
-        small = (dz is None and not bf16 and ctx.relu and agg_r is not None and agg_l is not None
-                 and agg_r.shape[1] + right.shape[1] <= 16 and agg_l.shape[1] + left.shape[1] <= 16
-                 and right_new.shape[1] % 4 == 0)
-        if small and not (need[0] or need[1]):
-            # conv1: the inputs are features -- weight and bias gradients straight from (g, y)
-            g_r0 = torch.zeros_like(right_new) if g_right is None else g_right
-            g_l0 = torch.zeros_like(left_new) if g_left is None else g_left
-            dw_rel_l2r, dw_root_l2r, db_l2r = _fc.relu_wgrad_smallk(g_r0, right_new, ctx.scale, agg_r, right,
-                                                                    ctx.has_b[0] and need[4])
-            dw_rel_r2l, dw_root_r2l, db_r2l = _fc.relu_wgrad_smallk(g_l0, left_new, ctx.scale, agg_l, left,
-                                                                    ctx.has_b[1] and need[7])
-            keep = lambda t, i: t if need[i] else None
-            return (None, None, None, keep(dw_rel_l2r, 3), db_l2r, keep(dw_root_l2r, 5), keep(dw_rel_r2l, 6), db_r2l,
-                    keep(dw_root_r2l, 8), None, None)
+    small = (dz is None and not bf16 and ctx.relu and agg_r is not None and agg_l is not None
+             and agg_r.shape[1] + right.shape[1] <= 16 and agg_l.shape[1] + left.shape[1] <= 16
+             and right_new.shape[1] % 4 == 0)
+    if small and not (need[0] or need[1]):
+        # conv1: the inputs are features -- weight and bias gradients straight from (g, y)
+        g_r0 = torch.zeros_like(right_new) if g_right is None else g_right
+        g_l0 = torch.zeros_like(left_new) if g_left is None else g_left
+        dw_rel_l2r, dw_root_l2r, db_l2r = _fc.relu_wgrad_smallk(g_r0, right_new, ctx.scale, agg_r, right,
+                                                                ctx.has_b[0] and need[4])
+        dw_rel_r2l, dw_root_r2l, db_r2l = _fc.relu_wgrad_smallk(g_l0, left_new, ctx.scale, agg_l, left,
+                                                                ctx.has_b[1] and need[7])
+        keep = lambda t, i: t if need[i] else None
+        return (None, None, None, keep(dw_rel_l2r, 3), db_l2r, keep(dw_root_l2r, 5), keep(dw_rel_r2l, 6), db_r2l,
+                keep(dw_root_r2l, 8), None, None)
 
-        if dz is None:
-            dz_r, db_l2r = mask(g_right, right_new, ctx.has_b[0] and need[4])
-            dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
-        else:
-            dz_l, db_r2l, dz_r, db_l2r = dz
-        main = torch.cuda.current_stream(dz_r.device)
-        side = _side_stream(dz_r.device) if _OVERLAP else None
-        esz = 2 if bf16 else 4
+    if dz is None:
+        dz_r, db_l2r = mask(g_right, right_new, ctx.has_b[0] and need[4])
+        dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
+    else:
+        dz_l, db_r2l, dz_r, db_l2r = dz
+    main = torch.cuda.current_stream(dz_r.device)
+    side = _side_stream(dz_r.device) if _OVERLAP else None
+    esz = 2 if bf16 else 4
 
-        # Per direction (S = dst x src): T = S^T dZ serves the source-side gradient T W_rel when
-        # that association is cheaper, and lin_rel's weight gradient T^T x_src when the source
-        # side is the smaller node set (or the forward was re-associated and kept no S x_src).
-        # T only needs dZ -- on the side stream it streams HBM under the weight-gradient GEMMs.
-        def plan(S, St, dz, x_src, w_rel, agg, need_src, need_rel):
-            t_src = need_src and _src_first(S, dz.shape[1], w_rel.shape[1], esz)
-            rel_t = need_rel and (agg is None or (t_src and S.n_cols < S.n_rows))
-            T = None
-            if t_src or rel_t:
-                if side is not None:
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
-                        T = spmm_forward(St, dz)
-                else:
+    # Per direction (S = dst x src): T = S^T dZ serves the source-side gradient T W_rel when
+    # that association is cheaper, and lin_rel's weight gradient T^T x_src when the source
+    # side is the smaller node set (or the forward was re-associated and kept no S x_src).
+    # T only needs dZ -- on the side stream it streams HBM under the weight-gradient GEMMs.
+    def plan(S, St, dz, x_src, w_rel, agg, need_src, need_rel):
+        t_src = need_src and _src_first(S, dz.shape[1], w_rel.shape[1], esz)
+        rel_t = need_rel and (agg is None or (t_src and S.n_cols < S.n_rows))
+        T = None
+        if t_src or rel_t:
+            if side is not None:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
                     T = spmm_forward(St, dz)
-            return T, t_src, rel_t
-
-        t_r, tsrc_r, relt_r = plan(AT, A, dz_r, left, w_rel_l2r, agg_r, need[0], need[3])
-        t_l, tsrc_l, relt_l = plan(A, AT, dz_l, right, w_rel_r2l, agg_l, need[1], need[6])
-
-        # fp32: the x3 kernels (weight gradient G^T X, input gradient G W) unless LPGNN_FC_ARITH=fp32
-        wg = (lambda g, x: (g.t() @ x).float()) if bf16 else _fc.wgrad
-        ig = None if bf16 else _fc.input_grad
-
-        def wgrads(dz, agg, x_dst, need_rel, need_root):
-            if not (need_rel or need_root):
-                return None, None
-            k = x_dst.shape[1] + (agg.shape[1] if agg is not None else 0)
-            if not bf16 and agg is not None and k <= 16 and dz.shape[1] % 4 == 0:  # conv1: dZ read once
-                d_rel, d_root = _fc.wgrad_smallk(dz, agg, x_dst)
             else:
-                d_rel = wg(dz, agg) if need_rel else None
-                d_root = wg(dz, x_dst) if need_root else None
-            return (d_rel if need_rel else None), (d_root if need_root else None)
+                T = spmm_forward(St, dz)
+        return T, t_src, rel_t
 
-        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r, right, need[3] and not relt_r, need[5])
-        dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6] and not relt_l, need[8])
-        if side is not None and (t_r is not None or t_l is not None):
-            main.wait_stream(side)
-            for t in (t_r, t_l):
-                if t is not None:
-                    t.record_stream(main)
-        if relt_r:
-            dw_rel_l2r = wg(t_r, left)
-        if relt_l:
-            dw_rel_r2l = wg(t_l, right)
+    t_r, tsrc_r, relt_r = plan(AT, A, dz_r, left, w_rel_l2r, agg_r, need[0], need[3])
+    t_l, tsrc_l, relt_l = plan(A, AT, dz_l, right, w_rel_r2l, agg_l, need[1], need[6])
 
-        def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root):
-            """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients)."""
-            if ig is None:
-                g = T @ w_rel if t_src else spmm_forward(St, dz @ w_rel)
-                return g.addmm_(dz_root, w_root)
-            if t_src:  # both terms over the same rows: one two-part GEMM
-                return ig(T, w_rel, dz_root, w_root)
-            return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True)
+    # fp32: the x3 kernels (weight gradient G^T X, input gradient G W) unless LPGNN_FC_ARITH=fp32
+    wg = (lambda g, x: (g.t() @ x).float()) if bf16 else _fc.wgrad
+    ig = None if bf16 else _fc.input_grad
 
-        g_l = g_r = None
-        if need[1]:  # right = src of right2left (S = A), dst of left2right
-            g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r)
-        if need[0]:  # left = src of left2right (S = A^T), dst of right2left
-            g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l)
-        return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
+    def wgrads(dz, agg, x_dst, need_rel, need_root):
+        if not (need_rel or need_root):
+            return None, None
+        k = x_dst.shape[1] + (agg.shape[1] if agg is not None else 0)
+        if not bf16 and agg is not None and k <= 16 and dz.shape[1] % 4 == 0:  # conv1: dZ read once
+            d_rel, d_root = _fc.wgrad_smallk(dz, agg, x_dst)
+        else:
+            d_rel = wg(dz, agg) if need_rel else None
+            d_root = wg(dz, x_dst) if need_root else None
+        return (d_rel if need_rel else None), (d_root if need_root else None)
+
+    dw_rel_l2r, dw_root_l2r = wgrads(dz_r, agg_r, right, need[3] and not relt_r, need[5])
+    dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6] and not relt_l, need[8])
+    if side is not None and (t_r is not None or t_l is not None):
+        main.wait_stream(side)
+        for t in (t_r, t_l):
+            if t is not None:
+                t.record_stream(main)
+    if relt_r:
+        dw_rel_l2r = wg(t_r, left)
+    if relt_l:
+        dw_rel_r2l = wg(t_l, right)
+
+    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root):
+        """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients)."""
+        if ig is None:
+            g = T @ w_rel if t_src else spmm_forward(St, dz @ w_rel)
+            return g.addmm_(dz_root, w_root)
+        if t_src:  # both terms over the same rows: one two-part GEMM
+            return ig(T, w_rel, dz_root, w_root)
+        return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True)
+
+    g_l = g_r = None
+    if need[1]:  # right = src of right2left (S = A), dst of left2right
+        g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r)
+    if need[0]:  # left = src of left2right (S = A^T), dst of right2left
+        g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l)
+    return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 
 class _TwoDirectionHeads(torch.autograd.Function):

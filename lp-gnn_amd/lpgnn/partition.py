@@ -380,146 +380,144 @@ class _PartTwoDirection(torch.autograd.Function):
 def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu,
                        dropout):
     """_PartTwoDirection's forward; returns (left_new, right_new, tensors to save)."""
-    if True:
-        from . import fc as _fc
-        from .conv import reassociate
-        from .sparse import spmm_forward
+    from . import fc as _fc
+    from .conv import reassociate
+    from .sparse import spmm_forward
 
-        if dropout > 0 and not relu:
-            raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
-        if left.dtype != torch.float32:
-            raise RuntimeError("the row-partitioned path runs fp32 (the c2/c4 configurations)")
-        ex = padj.ex
-        A, AT = padj.local.fwd, padj.local.bwd  # A: local cons x local vars
-        n_own = ex.n_own
-        seed_r = _fc._new_seed() if dropout > 0 else 0
-        seed_l = _fc._new_seed() if dropout > 0 else 0
-        # conv.py's association rule on the GLOBAL node counts (every rank decides alike, so the
-        # reduced rows have the same width everywhere)
-        ra = reassociate(ex.m, ex.n, left.shape[1], w_rel_l2r.shape[0])
-        if ra:  # partials of A^T (left W_rel^T) for [owned | halo]
-            agg_r = spmm_forward(AT, _fc.fc_forward(left, w_rel_l2r, None, None, None, False))
-        else:
-            agg_r = spmm_forward(AT, left)          # partials for [owned | halo]
-        red = ex.start_reduce(agg_r, inplace=True)  # halo partials -> owners, in flight ...
-        agg_l = spmm_forward(A, right)              # ... under the purely local constraint side
-        left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l)
-        red.finish()                                # owners' rows of agg_r now hold the full sums
-        if ra:  # lin_root + bias + ReLU accumulated onto the owners' sums, in place
-            right_new, agg_r = agg_r, None
-            _fc.fc_forward(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
-                           out=right_new[:n_own], accumulate=True)
-        else:
-            right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
-            _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
-                           out=right_new[:n_own])
-        ex.start_broadcast_(right_new).finish()
-        ctx.padj, ctx.relu = padj, relu
-        ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
-        ctx.has_b = (b_l2r is not None, b_r2l is not None)
-        return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r,
-                                     w_rel_r2l, w_root_r2l)
+    if dropout > 0 and not relu:
+        raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
+    if left.dtype != torch.float32:
+        raise RuntimeError("the row-partitioned path runs fp32 (the c2/c4 configurations)")
+    ex = padj.ex
+    A, AT = padj.local.fwd, padj.local.bwd  # A: local cons x local vars
+    n_own = ex.n_own
+    seed_r = _fc._new_seed() if dropout > 0 else 0
+    seed_l = _fc._new_seed() if dropout > 0 else 0
+    # conv.py's association rule on the GLOBAL node counts (every rank decides alike, so the
+    # reduced rows have the same width everywhere)
+    ra = reassociate(ex.m, ex.n, left.shape[1], w_rel_l2r.shape[0])
+    if ra:  # partials of A^T (left W_rel^T) for [owned | halo]
+        agg_r = spmm_forward(AT, _fc.fc_forward(left, w_rel_l2r, None, None, None, False))
+    else:
+        agg_r = spmm_forward(AT, left)          # partials for [owned | halo]
+    red = ex.start_reduce(agg_r, inplace=True)  # halo partials -> owners, in flight ...
+    agg_l = spmm_forward(A, right)              # ... under the purely local constraint side
+    left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l)
+    red.finish()                                # owners' rows of agg_r now hold the full sums
+    if ra:  # lin_root + bias + ReLU accumulated onto the owners' sums, in place
+        right_new, agg_r = agg_r, None
+        _fc.fc_forward(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
+                       out=right_new[:n_own], accumulate=True)
+    else:
+        right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
+        _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
+                       out=right_new[:n_own])
+    ex.start_broadcast_(right_new).finish()
+    ctx.padj, ctx.relu = padj, relu
+    ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
+    ctx.has_b = (b_l2r is not None, b_r2l is not None)
+    return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r,
+                                 w_rel_r2l, w_root_r2l)
 
 
 def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     """_PartTwoDirection's backward from the output gradients, or -- dz =
     (dz_l, db_r2l, dz_r_own, db_l2r) -- from gradients that already went
     through the layer's ReLU/dropout, owners' rows reduced (fused heads)."""
-    if True:
-        from . import fc as _fc
-        from .conv import _src_first
-        from .sparse import spmm_forward
+    from . import fc as _fc
+    from .conv import _src_first
+    from .sparse import spmm_forward
 
-        left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
-        ex = ctx.padj.ex
-        A, AT = ctx.padj.local.fwd, ctx.padj.local.bwd
-        n_own = ex.n_own
-        if dz is None:
-            if g_right is None:
-                g_right = torch.zeros_like(right_new)
-            if g_left is None:
-                g_left = torch.zeros_like(left_new)
-            red = ex.start_reduce(g_right.contiguous(), inplace=False)  # halo grads -> owners, in flight ...
+    left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
+    ex = ctx.padj.ex
+    A, AT = ctx.padj.local.fwd, ctx.padj.local.bwd
+    n_own = ex.n_own
+    if dz is None:
+        if g_right is None:
+            g_right = torch.zeros_like(right_new)
+        if g_left is None:
+            g_left = torch.zeros_like(left_new)
+        red = ex.start_reduce(g_right.contiguous(), inplace=False)  # halo grads -> owners, in flight ...
 
-        def mask(g, y, want_db):
-            if not ctx.relu:
-                g = g.contiguous()
-                return g, (g.sum(0) if want_db else None)
-            return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
+    def mask(g, y, want_db):
+        if not ctx.relu:
+            g = g.contiguous()
+            return g, (g.sum(0) if want_db else None)
+        return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
 
-        def wgrads(dz, agg, x_dst, need_rel, need_root):
-            if not (need_rel or need_root):
-                return None, None
-            if agg is not None and agg.shape[1] + x_dst.shape[1] <= 16 and dz.shape[1] % 4 == 0:
-                d_rel, d_root = _fc.wgrad_smallk(dz, agg.contiguous(), x_dst.contiguous())
-            else:
-                d_rel = _fc.wgrad(dz, agg) if need_rel else None
-                d_root = _fc.wgrad(dz, x_dst) if need_root else None
-            return (d_rel if need_rel else None), (d_root if need_root else None)
-
-        def narrow(agg, x_dst):  # conv1: the inputs are features -- weight gradients straight from (g, y)
-            return (dz is None and ctx.relu and not (need[0] or need[1]) and agg is not None
-                    and agg.shape[1] + x_dst.shape[1] <= 16 and left_new.shape[1] % 4 == 0)
-
-        # ... under everything that only needs the constraint side's gradient
-        if dz is not None:
-            dz_l, db_r2l = dz[0], dz[1]
-            dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
-        elif narrow(agg_l, left):
-            dz_l = None
-            dw_rel_r2l, dw_root_r2l, db_r2l = _fc.relu_wgrad_smallk(g_left, left_new, ctx.scale, agg_l, left,
-                                                                    ctx.has_b[1] and need[7])
+    def wgrads(dz, agg, x_dst, need_rel, need_root):
+        if not (need_rel or need_root):
+            return None, None
+        if agg is not None and agg.shape[1] + x_dst.shape[1] <= 16 and dz.shape[1] % 4 == 0:
+            d_rel, d_root = _fc.wgrad_smallk(dz, agg.contiguous(), x_dst.contiguous())
         else:
-            dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
-            dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
-        g_r = None
-        if need[1]:  # right [owned | halo] as the source of right2left: every local row
-            if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
-                g_r = _fc.input_grad(spmm_forward(AT, dz_l), w_rel_r2l)
-            else:
-                g_r = spmm_forward(AT, _fc.input_grad(dz_l, w_rel_r2l))
-        g_right_own = red.finish() if dz is None else None
-        if narrow(agg_r, right):
-            dw_rel_l2r, dw_root_l2r, db_l2r = _fc.relu_wgrad_smallk(g_right_own, right_new[:n_own], ctx.scale,
-                                                                    agg_r[:n_own], right[:n_own],
-                                                                    ctx.has_b[0] and need[4])
-            return (None, None, None, dw_rel_l2r if need[3] else None, db_l2r, dw_root_l2r if need[5] else None,
-                    dw_rel_r2l if need[6] else None, db_r2l, dw_root_r2l if need[8] else None, None, None)
-        if dz is None:
-            dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
-        else:
-            dz_r, db_l2r = dz[2], dz[3]
-        # with T = A bcast(dZ_r) (computed for left's gradient below), lin_rel's weight gradient
-        # dZ_r^T reduce(A^T left) = T^T left runs over the local constraints instead of the variables
-        # (and is the only route when the forward was re-associated: agg_r was not kept)
-        first = need[0] and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], 4)
-        rel_from_t = need[3] and (agg_r is None or (first and A.n_rows < ex.n_own))
-        use_t = first or rel_from_t
-        dw_rel_l2r, dw_root_l2r = wgrads(dz_r, None if agg_r is None else agg_r[:n_own], right[:n_own],
-                                         need[3] and not rel_from_t, need[5])
-        if need[1]:  # ... and as the destination of left2right (owned rows)
-            _fc.input_grad(dz_r, w_root_l2r, out=g_r[:n_own], accumulate=True)
+            d_rel = _fc.wgrad(dz, agg) if need_rel else None
+            d_root = _fc.wgrad(dz, x_dst) if need_root else None
+        return (d_rel if need_rel else None), (d_root if need_root else None)
 
-        g_l = None
-        if need[0] or use_t:  # left: source of left2right through reduce(AT @ left)[:n_own]
-            f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
-            full = torch.empty((right.shape[0], f_out if use_t else f_in), dtype=torch.float32, device=left.device)
-            if use_t:
-                full[:n_own] = dz_r
-            else:
-                _fc.input_grad(dz_r, w_rel_l2r, out=full[:n_own])
-            bc = ex.start_broadcast_(full)           # owners' aggregate gradient -> halo rows, in flight ...
-            root = _fc.input_grad(dz_l, w_root_r2l) if need[0] else None  # ... under the root-path gradient
-            bc.finish()
-            if use_t:
-                t = spmm_forward(A, full)
-                if rel_from_t:
-                    dw_rel_l2r = _fc.wgrad(t, left)
-                if need[0]:
-                    g_l = _fc.input_grad(t, w_rel_l2r, out=root, accumulate=True)
-            else:
-                g_l = spmm_forward(A, full).add_(root)
-        return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
+    def narrow(agg, x_dst):  # conv1: the inputs are features -- weight gradients straight from (g, y)
+        return (dz is None and ctx.relu and not (need[0] or need[1]) and agg is not None
+                and agg.shape[1] + x_dst.shape[1] <= 16 and left_new.shape[1] % 4 == 0)
+
+    # ... under everything that only needs the constraint side's gradient
+    if dz is not None:
+        dz_l, db_r2l = dz[0], dz[1]
+        dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
+    elif narrow(agg_l, left):
+        dz_l = None
+        dw_rel_r2l, dw_root_r2l, db_r2l = _fc.relu_wgrad_smallk(g_left, left_new, ctx.scale, agg_l, left,
+                                                                ctx.has_b[1] and need[7])
+    else:
+        dz_l, db_r2l = mask(g_left, left_new, ctx.has_b[1] and need[7])
+        dw_rel_r2l, dw_root_r2l = wgrads(dz_l, agg_l, left, need[6], need[8])
+    g_r = None
+    if need[1]:  # right [owned | halo] as the source of right2left: every local row
+        if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
+            g_r = _fc.input_grad(spmm_forward(AT, dz_l), w_rel_r2l)
+        else:
+            g_r = spmm_forward(AT, _fc.input_grad(dz_l, w_rel_r2l))
+    g_right_own = red.finish() if dz is None else None
+    if narrow(agg_r, right):
+        dw_rel_l2r, dw_root_l2r, db_l2r = _fc.relu_wgrad_smallk(g_right_own, right_new[:n_own], ctx.scale,
+                                                                agg_r[:n_own], right[:n_own],
+                                                                ctx.has_b[0] and need[4])
+        return (None, None, None, dw_rel_l2r if need[3] else None, db_l2r, dw_root_l2r if need[5] else None,
+                dw_rel_r2l if need[6] else None, db_r2l, dw_root_r2l if need[8] else None, None, None)
+    if dz is None:
+        dz_r, db_l2r = mask(g_right_own, right_new[:n_own], ctx.has_b[0] and need[4])
+    else:
+        dz_r, db_l2r = dz[2], dz[3]
+    # with T = A bcast(dZ_r) (computed for left's gradient below), lin_rel's weight gradient
+    # dZ_r^T reduce(A^T left) = T^T left runs over the local constraints instead of the variables
+    # (and is the only route when the forward was re-associated: agg_r was not kept)
+    first = need[0] and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], 4)
+    rel_from_t = need[3] and (agg_r is None or (first and A.n_rows < ex.n_own))
+    use_t = first or rel_from_t
+    dw_rel_l2r, dw_root_l2r = wgrads(dz_r, None if agg_r is None else agg_r[:n_own], right[:n_own],
+                                     need[3] and not rel_from_t, need[5])
+    if need[1]:  # ... and as the destination of left2right (owned rows)
+        _fc.input_grad(dz_r, w_root_l2r, out=g_r[:n_own], accumulate=True)
+
+    g_l = None
+    if need[0] or use_t:  # left: source of left2right through reduce(AT @ left)[:n_own]
+        f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
+        full = torch.empty((right.shape[0], f_out if use_t else f_in), dtype=torch.float32, device=left.device)
+        if use_t:
+            full[:n_own] = dz_r
+        else:
+            _fc.input_grad(dz_r, w_rel_l2r, out=full[:n_own])
+        bc = ex.start_broadcast_(full)           # owners' aggregate gradient -> halo rows, in flight ...
+        root = _fc.input_grad(dz_l, w_root_r2l) if need[0] else None  # ... under the root-path gradient
+        bc.finish()
+        if use_t:
+            t = spmm_forward(A, full)
+            if rel_from_t:
+                dw_rel_l2r = _fc.wgrad(t, left)
+            if need[0]:
+                g_l = _fc.input_grad(t, w_rel_l2r, out=root, accumulate=True)
+        else:
+            g_l = spmm_forward(A, full).add_(root)
+    return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 
 class _PartTwoDirectionHeads(torch.autograd.Function):
