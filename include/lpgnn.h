@@ -166,6 +166,22 @@ lpg_status lpg_fc_x3_f32(int64_t M, int64_t N,
 lpg_status lpg_split3_f32(int64_t rows, int64_t cols, const float *src, int64_t lds, int32_t transpose,
                           uint16_t *dst, int64_t ldd, int64_t plane_stride, void *stream);
 
+/* lpg_fc_x3_f32 with the heads fused into its epilogue: besides C, writes
+ * logits[m, c] = sum_n C[m, n] hw[c, n] + hb[c] for c < hn (hn <= 4; hw
+ * [hn, ldhw] fp32, hb may be NULL) -- lin_left / lin_right (arch.py:175-176,
+ * 190) applied to the last hidden layer's output (arch.py:184-188) without
+ * re-reading it.  Each 128-column tile's partial sums go to `workspace`
+ * (lpg_fc_x3_heads_workspace_bytes(M, N) bytes, 16-byte aligned) and are added
+ * in column order: deterministic, fp32-rounding-equal to the separate Linear
+ * (not bitwise: a different summation order). */
+int64_t lpg_fc_x3_heads_workspace_bytes(int64_t M, int64_t N);
+lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                               const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                               int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
+                               float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                               int32_t hn, const float *hw, int64_t ldhw, const float *hb, float *logits,
+                               int64_t ldl, void *workspace, void *stream);
+
 /* Weight gradient on the same arithmetic: dW[n, k] = sum_r G[r, n] X[r, k]
  * (G = dZ [R, N], ldg; X = the layer input [R, K], ldx; dW [N, K], lddw, the
  * torch Linear weight layout) -- the lin_rel / lin_root weight gradients of

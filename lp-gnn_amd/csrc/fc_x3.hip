@@ -73,6 +73,12 @@ struct X3Args {
   float drop_scale;
   int32_t accum;
   int32_t xmap;  // fc_fwd_x3_16 block -> tile map: 0 = m-major per XCD, 1 = n-tile pairs per XCD pair
+  // fused heads (fc_fwd_x3_16 only): hw [hn][ldhw] fp32; per-(wave column tile, row) partial logits
+  // to hpart [N / (TN * 16)][M][4]
+  const float *hw;
+  int64_t ldhw;
+  int32_t hn;
+  float *hpart;
 };
 
 __device__ __forceinline__ unsigned pk_bf16(float x, float y) {  // v_cvt_pk_bf16_f32: RNE, x in the low half
@@ -126,6 +132,16 @@ __global__ __launch_bounds__(256) void split3_planes(int64_t rows, int64_t cols,
       d[2 * ps + 1] = (uint16_t)(l >> 16);
     }
   }
+}
+
+// sum over the 16 lanes of a DPP row (all lanes get it; fixed order): quad swaps, then the
+// half-row and row mirrors -- VALU only (no LDS crossbar, no lgkmcnt waits)
+__device__ __forceinline__ float sum16(float v) {
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));  // half mirror
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));  // row mirror
+  return v;
 }
 
 __device__ __forceinline__ int swzA(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }  // 128-B rows
@@ -535,11 +551,21 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
         }
     }
   }
+  float hs[4][TM][4];  // fused heads: this lane's partial logits [head][i][r]
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hs[c][i][r] = 0.f;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int64_t col = nw + j * 16 + fr;
     if (col >= a.N) continue;
     const float bb = a.bias ? a.bias[col] : 0.f;
+    float hwv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) hwv[c] = (a.hw && c < a.hn) ? a.hw[c * a.ldhw + col] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -551,9 +577,49 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
         if (RELU) v = (v < 0.f) ? 0.f : v;
         if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         a.C[row * a.ldc + col] = v;
+        if (a.hw) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
+        }
       }
     }
   }
+  if (a.hw) {  // sum over the 16 lanes (columns) of each row group, fixed DPP order; lane fr = 0 writes
+    const int64_t pidx = nw / (TN * 16);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          hs[c][i][r] = c < a.hn ? sum16(hs[c][i][r]) : 0.f;
+        }
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = mw + i * 16 + 4 * fg + r;
+          if (row < a.M)
+            *reinterpret_cast<f32x4 *>(a.hpart + (pidx * a.M + row) * 4) =
+                f32x4{hs[0][i][r], hs[1][i][r], hs[2][i][r], hs[3][i][r]};
+        }
+    }
+  }
+}
+
+// logits[m, c] = sum_t hpart[t][m][c] (t ascending) + hb[c]: the fused heads' fold
+__global__ __launch_bounds__(256) void heads_fold(int64_t M, int64_t nparts, int32_t hn,
+                                                  const float *__restrict__ hpart, const float *__restrict__ hb,
+                                                  float *__restrict__ logits, int64_t ldl) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * hn) return;
+  const int64_t m = i / hn;
+  const int c = (int)(i % hn);
+  float v = hpart[m * 4 + c];
+  for (int64_t t = 1; t < nparts; ++t) v = v + hpart[(t * M + m) * 4 + c];
+  if (hb) v = v + hb[c];
+  logits[m * ldl + c] = v;
 }
 
 template <int WM, int WN, int TM, int TN, bool PROBE = false>
@@ -1092,13 +1158,11 @@ extern "C" lpg_status lpg_split3_f32(int64_t rows, int64_t cols, const float *sr
   return LPG_OK;
 }
 
-extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
-                                    const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
-                                    int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
-                                    float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                                    void *stream) {
-  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_f32: negative size");
-  if (M == 0 || N == 0) return LPG_OK;
+static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                          const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                          int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
+                          float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                          X3Args *out) {
   LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_x3_f32: bad C/ldc");
   LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "lpg_fc_x3_f32: K1, K2 must be multiples of %d (zero-pad)", BK);
   LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1 && ps1 >= N * ldw1), "lpg_fc_x3_f32: bad A1/W1");
@@ -1110,9 +1174,23 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
               "(ldw and plane stride multiples of 8)");
   LPG_REQUIRE((flags & ~3) == 0, "lpg_fc_x3_f32: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_x3_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
-  X3Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, ps1, ps2, C, ldc, 0, 0, seed, 0u, 1.f,
-           (flags >> 1) & 1};
-  dropout_params(dropout_p, &a.drop_thresh, &a.drop_scale);
+  *out = X3Args{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, ps1, ps2, C, ldc, 0, 0, seed, 0u, 1.f,
+                (flags >> 1) & 1};
+  dropout_params(dropout_p, &out->drop_thresh, &out->drop_scale);
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                    const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                    int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
+                                    float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                                    void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_f32: negative size");
+  if (M == 0 || N == 0) return LPG_OK;
+  X3Args a;
+  const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
+                                dropout_p, seed, &a);
+  if (st != LPG_OK) return st;
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
   switch (g_x3_variant) {
@@ -1133,6 +1211,42 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
     default:  // (tools/exp_x3.py at the c2 shapes: 199-212 TF/s, 5-10 % over 5 / 6)
       return launch_x3_16<4, 1, 2, 8>(a, relu, s);
   }
+}
+
+extern "C" int64_t lpg_fc_x3_heads_workspace_bytes(int64_t M, int64_t N) {
+  if (M <= 0 || N <= 0) return 0;
+  return ((N + 127) / 128) * M * 4 * (int64_t)sizeof(float);
+}
+
+extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                          const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                          int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2,
+                                          const float *bias, float *C, int64_t ldc, int32_t flags, float dropout_p,
+                                          uint64_t seed, int32_t hn, const float *hw, int64_t ldhw, const float *hb,
+                                          float *logits, int64_t ldl, void *workspace, void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_heads_f32: negative size");
+  if (M == 0) return LPG_OK;
+  LPG_REQUIRE(N > 0, "lpg_fc_x3_heads_f32: N must be positive");
+  LPG_REQUIRE(hn >= 1 && hn <= 4, "lpg_fc_x3_heads_f32: %d heads outputs not in [1, 4]", (int)hn);
+  LPG_REQUIRE(hw && ldhw >= N && logits && ldl >= hn, "lpg_fc_x3_heads_f32: bad head weight / logits");
+  LPG_REQUIRE(workspace && aligned16(workspace), "lpg_fc_x3_heads_f32: workspace missing or not 16-byte aligned");
+  X3Args a;
+  const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
+                                dropout_p, seed, &a);
+  if (st != LPG_OK) return st;
+  a.hw = hw;
+  a.ldhw = ldhw;
+  a.hn = hn;
+  a.hpart = reinterpret_cast<float *>(workspace);
+  a.xmap = g_x3_variant == 11 && (N + 127) / 128 == 8;
+  hipStream_t s = as_stream(stream);
+  const lpg_status r = launch_x3_16<4, 1, 2, 8>(a, flags & 1, s);  // 32 x 128 wave tiles: N / 128 partials
+  if (r != LPG_OK) return r;
+  const int64_t nparts = (N + 127) / 128;
+  hipLaunchKernelGGL(heads_fold, dim3((unsigned)((M * hn + 255) / 256)), dim3(256), 0, s, M, nparts, hn,
+                     a.hpart, hb, logits, ldl);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
 }
 
 extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {

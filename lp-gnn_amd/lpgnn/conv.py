@@ -51,6 +51,8 @@ _SPMM_BYTES = 7e12
 # hides the kernel's own roofline fraction in the bench -- off by default.
 _OVERLAP = os.environ.get("LPGNN_OVERLAP", "0") == "1"
 REASSOCIATE = os.environ.get("LPGNN_REASSOC", "1") == "1"
+# LPGNN_FUSE_HEAD_FWD=0: the heads' forward as its own Linear kernels instead of in the last layer's FC epilogue
+FUSE_HEAD_FWD = os.environ.get("LPGNN_FUSE_HEAD_FWD", "1") == "1"
 _SIDE = {}
 
 
@@ -80,9 +82,12 @@ def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
     return spmm(f_out) + gemm(S.n_cols) < gemm(S.n_rows) + spmm(f_in)
 
 
-def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
+                  heads=None):
     """The layer's forward (both directions); records on ctx what the backward
-    needs and returns (left_new, right_new, tensors to save)."""
+    needs and returns (left_new, right_new, tensors to save, logits).  With
+    heads = ((Wh_l, bh_l), (Wh_r, bh_r)) the heads run in the FC epilogues
+    (fp32) and logits = (logit_l, logit_r), else None."""
     if dropout > 0 and not relu:
         raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
     bf16 = left.dtype == torch.bfloat16
@@ -96,13 +101,23 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out)
     ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out)
 
-    def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None):
+    hd = heads if heads is not None and not bf16 else (None, None)
+
+    def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None, head=None):
+        """(output, aggregate kept for the backward, logits of `head` or None)."""
         if ra:  # S (x_src W_rel^T), then lin_root + bias + ReLU accumulated onto it in place
             fc = _fc.fc_forward_bf16 if bf16 else _fc.fc_forward
             y = spmm_forward(S, fc(x_src, w_rel, None, None, None, False))
-            return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None
+            if head is not None:
+                y, lg = _fc.fc_forward(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True,
+                                       heads=head)
+                return y, None, lg
+            return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None, None
         agg = spmm_forward(S, x_src) if agg is None else agg
-        return _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, dropout, seed, bf16), agg
+        if head is not None:
+            y, lg = _fc.fc_forward(agg, w_rel, x_dst, w_root, b, relu, dropout, seed, heads=head)
+            return y, agg, lg
+        return _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, dropout, seed, bf16), agg, None
 
     side = _side_stream(left.device) if _OVERLAP and not ra_l else None
     agg_l = None
@@ -111,23 +126,24 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
         with torch.cuda.stream(side):
             agg_l = spmm_forward(A, right)
     # arch.py:75-77: right' = left2right((left, right), A^T)
-    right_new, agg_r = direction(AT, left, right, ws[0], b_l2r, ws[1], seed_r, ra_r)
+    right_new, agg_r, logit_r = direction(AT, left, right, ws[0], b_l2r, ws[1], seed_r, ra_r, head=hd[1])
     if side is not None:
         torch.cuda.current_stream(left.device).wait_stream(side)
         agg_l.record_stream(torch.cuda.current_stream(left.device))
     # arch.py:78-80: left' = right2left((right, left), A)
-    left_new, agg_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l)
+    left_new, agg_l, logit_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l, head=hd[0])
     ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
     ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
-    return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, *ws)
+    logits = None if heads is None or bf16 else (logit_l, logit_r)
+    return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, *ws), logits
 
 
 class _TwoDirection(torch.autograd.Function):
     @staticmethod
     def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
-        left_new, right_new, saved = _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l,
-                                                   b_r2l, w_root_r2l, relu, dropout)
+        left_new, right_new, saved, _ = _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r,
+                                                      w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
         ctx.save_for_backward(*saved)
         return left_new, right_new
 
@@ -253,10 +269,14 @@ class _TwoDirectionHeads(torch.autograd.Function):
     @staticmethod
     def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
                 wh_l, bh_l, wh_r, bh_r):
-        left_new, right_new, saved = _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l,
-                                                   b_r2l, w_root_r2l, relu, dropout)
-        logit_l = _fc.fc_forward(left_new, wh_l, None, None, bh_l, False)
-        logit_r = _fc.fc_forward(right_new, wh_r, None, None, bh_r, False)
+        # the heads fused into the layer's FC epilogues (x3 arithmetic), else their own Linear kernels
+        left_new, right_new, saved, logits = _forward_core(
+            ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
+            heads=((wh_l, bh_l), (wh_r, bh_r)) if FUSE_HEAD_FWD else None)
+        if logits is None:
+            logits = (_fc.fc_forward(left_new, wh_l, None, None, bh_l, False),
+                      _fc.fc_forward(right_new, wh_r, None, None, bh_r, False))
+        logit_l, logit_r = logits
         ctx.heads_b = (bh_l is not None, bh_r is not None)
         ctx.save_for_backward(*saved, wh_l, wh_r)
         return logit_l, logit_r

@@ -57,10 +57,26 @@ _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless th
 
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
-               accumulate: bool = False, arith: str | None = None) -> Tensor:
+               accumulate: bool = False, arith: str | None = None, heads=None):
     """act(A1 W1^T + A2 W2^T [+ out] + bias) through lpg_fc_f32; with
     ``accumulate`` the caller's ``out`` holds the addend and is overwritten.
-    ``arith`` ("fp32" | "x3", default ``ARITH``) picks the tiled kernel's arithmetic."""
+    ``arith`` ("fp32" | "x3", default ``ARITH``) picks the tiled kernel's arithmetic.
+    ``heads`` = (Wh [<= 4, N], bh or None): also return the logits C Wh^T + bh
+    -- fused into the x3 kernel's epilogue (lpg_fc_x3_heads_f32), else the
+    separate Linear on C (the fp32 contract's own kernel)."""
+    if heads is not None:
+        M, N = A1.shape[0], W1.shape[0]
+        k4 = lambda k: -(-k // 4) * 4
+        small = 4 <= k4(A1.shape[1]) and k4(A1.shape[1]) + (0 if A2 is None else k4(A2.shape[1])) <= 16
+        if (arith or ARITH) == "x3" and not small and N > 32 and heads[0].shape[0] <= 4:
+            return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, heads)
+        C = _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith)
+        return C, _fc_forward(C, heads[0], None, None, heads[1], False, arith=arith)
+    return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith)
+
+
+def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, accumulate=False, arith=None,
+                heads=None):
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -87,7 +103,7 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0)
     if (arith or ARITH) == "x3" and not small and N > 32:
-        return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu)
+        return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, heads=heads)
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
         st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
@@ -120,21 +136,38 @@ def split3(W: Tensor, transpose: bool = False) -> Tensor:
     return out
 
 
-def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=None, W2s=None):
-    """lpg_fc_x3_f32 on fp32 A and pre-split W (split here unless given)."""
+def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=None, W2s=None, heads=None):
+    """lpg_fc_x3_f32 on fp32 A and pre-split W (split here unless given); with
+    ``heads`` = (Wh, bh) lpg_fc_x3_heads_f32, returning (C, logits)."""
     W1s = split3(W1) if W1s is None else W1s
     W2s = (split3(W2) if W2s is None else W2s) if K2 else None
     L = _lib.lib()
+    args = (M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1s.data_ptr(), W1s.stride(1), W1s.stride(0), K2,
+            None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
+            None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0, W2s.stride(0) if K2 else 0,
+            None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags, float(dropout_p),
+            int(seed) & (2**64 - 1))
+    key = ("fc", M, N, A1.shape[1] + K2, ("relu" if relu else "lin") + "-x3")
     with torch.cuda.device(A1.device):
-        tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, ("relu" if relu else "lin") + "-x3"))
-        st = L.lpg_fc_x3_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1s.data_ptr(), W1s.stride(1),
-                             W1s.stride(0), K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
-                             None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0,
-                             W2s.stride(0) if K2 else 0, None if bias is None else bias.data_ptr(), C.data_ptr(),
-                             C.stride(0), flags, float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
+        if heads is None:
+            tok = TIMER.start(key)
+            st = L.lpg_fc_x3_f32(*args, _lib.stream_of(A1))
+            TIMER.stop(tok)
+            _lib.check(st, "lpg_fc_x3_f32")
+            return C
+        Wh = heads[0].detach().contiguous()
+        bh = None if heads[1] is None else heads[1].detach().contiguous()
+        if Wh.dtype != torch.float32 or Wh.shape[1] != N:
+            raise RuntimeError("lpgnn fused heads: fp32 head weight [hn, N] expected")
+        logits = torch.empty((M, Wh.shape[0]), dtype=torch.float32, device=A1.device)
+        ws = torch.empty(max(16, L.lpg_fc_x3_heads_workspace_bytes(M, N)), dtype=torch.uint8, device=A1.device)
+        tok = TIMER.start(key)
+        st = L.lpg_fc_x3_heads_f32(*args, Wh.shape[0], Wh.data_ptr(), Wh.stride(0),
+                                   None if bh is None else bh.data_ptr(), logits.data_ptr(), logits.stride(0),
+                                   ws.data_ptr(), _lib.stream_of(A1))
         TIMER.stop(tok)
-    _lib.check(st, "lpg_fc_x3_f32")
-    return C
+    _lib.check(st, "lpg_fc_x3_heads_f32")
+    return C, logits
 
 
 def wgrad(G: Tensor, X: Tensor, arith: str | None = None) -> Tensor:

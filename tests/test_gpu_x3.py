@@ -129,6 +129,38 @@ def test_x3_xcd_pair_map_covers_every_tile(M):
     assert torch.equal(outs[0], outs[11])
 
 
+@pytest.mark.parametrize("M,N,K,hn,accum,drop", [
+    (1000, 1024, 1024, 3, False, 0.0),  # the last hidden layer + lin_left / lin_right
+    (333, 200, 96, 3, True, 0.0),       # ragged 128-column tiles, accumulate (re-associated direction)
+    (37, 130, 64, 1, False, 0.2),       # one head, dropout
+    (5000, 1024, 2048, 4, False, 0.0),
+])
+def test_x3_fused_heads_match_separate_linear(M, N, K, hn, accum, drop):
+    """lpg_fc_x3_heads_f32: C is bitwise the unfused kernel's; the logits are the Linear on C to fp32
+    rounding (bound: 32 * 2^-24 * sum|y w| + 2^-24 |logit|)."""
+    from lpgnn.fc import fc_forward
+
+    g = torch.Generator().manual_seed(M + N)
+    A = torch.randn(M, K, generator=g).to(DEV)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    Wh = (torch.randn(hn, N, generator=g) * 0.1).to(DEV)
+    bh = torch.randn(hn, generator=g).to(DEV)
+    P = torch.randn(M, N, generator=g).to(DEV) if accum else None
+    y0 = fc_forward(A, W, None, None, b, True, drop, 77, out=None if P is None else P.clone(), accumulate=accum,
+                    arith="x3")
+    y, lg = fc_forward(A, W, None, None, b, True, drop, 77, out=None if P is None else P.clone(), accumulate=accum,
+                       arith="x3", heads=(Wh, bh))
+    assert torch.equal(y, y0)
+    assert lg.shape == (M, hn)
+    ref = y0.double() @ Wh.double().t() + bh.double()
+    s = y0.double().abs() @ Wh.double().abs().t()
+    err = (lg.double() - ref).abs()
+    bound = 32 * U * s + U * ref.abs() + 1e-30
+    assert (err <= bound).all(), f"max err/bound {(err / bound).max().item():.3f}"
+    torch.testing.assert_close(lg, fc_forward(y0, Wh, None, None, bh, False), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("relu", [False, True])
 def test_x3_accumulate(relu):
     """flags bit 1: C = act(A W^T + C + b), the addend read before the store."""
