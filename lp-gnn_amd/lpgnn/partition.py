@@ -367,8 +367,8 @@ class _PartTwoDirection(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
-        left_new, right_new, saved = _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r,
-                                                        w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
+        left_new, right_new, saved, _ = _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r,
+                                                           w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
         ctx.save_for_backward(*saved)
         return left_new, right_new
 
@@ -378,8 +378,10 @@ class _PartTwoDirection(torch.autograd.Function):
 
 
 def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu,
-                       dropout):
-    """_PartTwoDirection's forward; returns (left_new, right_new, tensors to save)."""
+                       dropout, heads=None):
+    """_PartTwoDirection's forward; returns (left_new, right_new, tensors to save, logits).
+    heads = ((Wh_l, bh_l), (Wh_r, bh_r)): the heads in the FC epilogues (conv._forward_core's
+    rule) for the rows the FCs compute, a separate Linear for the halo rows; logits None without."""
     from . import fc as _fc
     from .conv import reassociate
     from .sparse import spmm_forward
@@ -402,22 +404,32 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
         agg_r = spmm_forward(AT, left)          # partials for [owned | halo]
     red = ex.start_reduce(agg_r, inplace=True)  # halo partials -> owners, in flight ...
     agg_l = spmm_forward(A, right)              # ... under the purely local constraint side
-    left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l)
+    hl, hr = heads if heads is not None else (None, None)
+    left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l, heads=hl)
+    if hl is not None:
+        left_new, logit_l = left_new
     red.finish()                                # owners' rows of agg_r now hold the full sums
     if ra:  # lin_root + bias + ReLU accumulated onto the owners' sums, in place
         right_new, agg_r = agg_r, None
-        _fc.fc_forward(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
-                       out=right_new[:n_own], accumulate=True)
+        own = _fc.fc_forward(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
+                             out=right_new[:n_own], accumulate=True, heads=hr)
     else:
         right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
-        _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
-                       out=right_new[:n_own])
+        own = _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
+                             out=right_new[:n_own], heads=hr)
     ex.start_broadcast_(right_new).finish()
+    logits = None
+    if heads is not None:
+        logit_r = torch.empty((right_new.shape[0], hr[0].shape[0]), dtype=torch.float32, device=left.device)
+        logit_r[:n_own] = own[1]
+        if right_new.shape[0] > n_own:  # halo rows: copies of other ranks' outputs
+            logit_r[n_own:] = _fc.fc_forward(right_new[n_own:], hr[0], None, None, hr[1], False)
+        logits = (logit_l, logit_r)
     ctx.padj, ctx.relu = padj, relu
     ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
     return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r,
-                                 w_rel_r2l, w_root_r2l)
+                                 w_rel_r2l, w_root_r2l), logits
 
 
 def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
@@ -533,10 +545,15 @@ class _PartTwoDirectionHeads(torch.autograd.Function):
                 wh_l, bh_l, wh_r, bh_r):
         from . import fc as _fc
 
-        left_new, right_new, saved = _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r,
-                                                        w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
-        logit_l = _fc.fc_forward(left_new, wh_l, None, None, bh_l, False)
-        logit_r = _fc.fc_forward(right_new, wh_r, None, None, bh_r, False)
+        from .conv import FUSE_HEAD_FWD
+
+        left_new, right_new, saved, logits = _part_forward_core(
+            ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
+            heads=((wh_l, bh_l), (wh_r, bh_r)) if FUSE_HEAD_FWD else None)
+        if logits is None:
+            logits = (_fc.fc_forward(left_new, wh_l, None, None, bh_l, False),
+                      _fc.fc_forward(right_new, wh_r, None, None, bh_r, False))
+        logit_l, logit_r = logits
         ctx.heads_b = (bh_l is not None, bh_r is not None)
         ctx.save_for_backward(*saved, wh_l, wh_r)
         return logit_l, logit_r
