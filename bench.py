@@ -9,9 +9,15 @@ train.py:117-129 on the synthetic c2 graph (100K cons x 200K vars, nnz 2M,
 BASELINE.json configs[1]): forward (2 SpMM at F=8 + 2 at F=1024, FC stacks,
 heads, add_knowledge), balanced loss, backward (2 SpMM at F=1024 + FC
 grads), Adam step.  value = (hid-width SpMM edge traversals in the step) /
-step time, whole job.  N>1: one process per GPU (torchrun), each owning a
-c2-sized constraint-row partition of an N-times larger graph (see
-lpgnn.partition); boundary-variable rows are all-reduced over RCCL.
+step time, whole job.
+
+N>1 defaults to ``--config c4`` (BASELINE.json configs[3]): the fixed
+2M cons x 4M vars, nnz 40M block LP, constraint-row partitioned over the N
+ranks (one process per GPU, torchrun) -- STRONG scaling; each rank generates
+and plans only its own row blocks (lpgnn.partition.plan_partition_blocks),
+boundary-variable rows are reduced to their owners and broadcast back over
+RCCL.  ``--config c2`` with N>1 is the weak-scaling variant (N c2-sized
+blocks).  ``--config c4`` at N=1 runs the whole c4 graph on one GPU.
 
 ``--config c5`` runs BASELINE.json configs[4] instead (same graph,
 GCN_FC hids=2048 depth=6, bf16 activations / SpMM storage / MFMA FC, fp32
@@ -40,15 +46,16 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense (MI355X_MICROARCH.md; the 5 PF figure is
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=("c2", "c5"), default="c2",
-                    help="c2 = headline fp32 hid 1024 depth 3; c5 = bf16 hid 2048 depth 6")
+    ap.add_argument("--config", choices=("c2", "c4", "c5"), default=None,
+                    help="c2 = headline fp32 hid 1024 depth 3 (default at N=1); c4 = 2M x 4M nnz 40M "
+                         "row-partitioned, strong scaling (default at N>1); c5 = bf16 hid 2048 depth 6")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--m", type=int, default=100_000)
-    ap.add_argument("--n", type=int, default=200_000)
-    ap.add_argument("--nnz", type=int, default=2_000_000)
-    ap.add_argument("--hids", type=int, default=1024)
-    ap.add_argument("--depth", type=int, default=3)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--nnz", type=int, default=None)
+    ap.add_argument("--hids", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--rho", type=float, default=0.02, help="boundary edge fraction for N>1 partitions")
     ap.add_argument("--cpu-steps", type=int, default=1, help="oracle CPU steps for cpu_baseline (0 = skip)")
     ap.add_argument("--profile-only", action="store_true", help="no CPU baseline, no JSON extras (rocprof runs)")
@@ -56,9 +63,14 @@ def parse():
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned RCCL path even at N=1 (the N>1 code path)")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "c2" if args.gpus == 1 else "c4"
+    from lpgnn.synth import CONFIGS
+
+    for k, v in CONFIGS[args.config].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
     args.bf16 = args.config == "c5"
-    if args.bf16:
-        args.hids, args.depth = 2048, 6
     return args
 
 
@@ -147,7 +159,8 @@ def cpu_spmm(g, F, reps=3):
 
 def workload_name(args) -> str:
     dt = ", bf16" if args.bf16 else ""
-    return (f"{args.config}: synthetic LP {args.m}x{args.n} nnz={args.nnz}, "
+    kind = "synthetic block LP (8 row blocks, rho=%g)" % args.rho if args.config == "c4" else "synthetic LP"
+    return (f"{args.config}: {kind} {args.m}x{args.n} nnz={args.nnz}, "
             f"GCN_FC(8,8,hids={args.hids},depth={args.depth}{dt}) fwd+bwd+Adam")
 
 
@@ -176,8 +189,14 @@ def main():
     from lpgnn.timing import TIMER
     from lpgnn.train import make_optimizer, train_step
 
+    exch = None
     if not distributed:
-        g = synth.uniform_lp(args.m, args.n, args.nnz, seed=0)
+        if args.config == "c4":  # the whole c4 graph on one GPU
+            from lpgnn.partition import bench_spec
+
+            g = bench_spec(args, 1).full()
+        else:
+            g = synth.uniform_lp(args.m, args.n, args.nnz, seed=0)
         adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
         batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(dev), x_t=torch.from_numpy(g.x_t).to(dev),
                                y_s=torch.from_numpy(g.y_s).to(dev), y_t=torch.from_numpy(g.y_t).to(dev),
@@ -197,6 +216,7 @@ def main():
         step, local_nnz, g = job.step, job.local_nnz, None
         workload = job.workload
         parallelism = f"rowpart{world}"
+        spec = job.spec
 
     def sync():
         torch.cuda.synchronize()
@@ -217,6 +237,15 @@ def main():
     TIMER.enabled = False
     kern = TIMER.summary()
     per_launch = TIMER.launches()
+    if distributed:  # the boundary exchange on its own, after the timed steps
+        exch = partition.time_exchange(job.batch.edge_index.ex, args.hids, dev)
+        exch.update(halo_rows=int(job.plan.halo.shape[0]), owned_vars=job.plan.n_own,
+                    boundary_vars_global=job.plan.n_boundary_global)
+        gathered = [None] * world
+        torch.distributed.all_gather_object(gathered, exch)
+        exch = {"per_rank": gathered,
+                "note": "standalone F=hid owner-reduce / halo-broadcast of [n_local, F] fp32 rows (median ms, "
+                        "barrier + sync around each); in the step they run async under independent compute"}
 
     # hid-width SpMM launches (the metric's kernel) measured on their stream
     hid_keys = [k for k in kern if k[0] == "spmm" and k[3] == args.hids]
@@ -257,12 +286,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt_max / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config == "c4" else "weak",
         "vs_baseline": None,
         "dtype": "bf16" if args.bf16 else "fp32",
         "data": "synthetic (seeded uniform LP graph, LP feature layout; random-init GCN_FC weights)",
-        "config": {"workload": workload, "n_cons": args.m * world, "n_vars": args.n * world,
-                   "nnz": args.nnz * world, "hid": args.hids, "depth": args.depth, "parallelism": parallelism},
+        "config": {"workload": workload, "n_cons": spec.m if distributed else args.m,
+                   "n_vars": spec.n if distributed else args.n, "nnz": spec.nnz if distributed else args.nnz,
+                   "hid": args.hids, "depth": args.depth, "parallelism": parallelism},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("lpg spmm_bf16_rowwave" if args.bf16 else "lpg spmm_f32_rowwave")
@@ -290,8 +320,11 @@ def main():
         "kernels": {f"{k[0]}[{k[1]}x{k[2]},F={k[3]},{k[4]}]": {"launches": v[0], "ms": v[1]}
                     for k, v in sorted(kern.items())},
         "library": lpgnn.library_path(),
+        "max_hbm_allocated_gb": torch.cuda.max_memory_allocated(dev) / 1e9,
     }
-    if rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None and not args.bf16:
+    if exch is not None:
+        out["exchange"] = exch
+    if rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None and args.config == "c2":
         cdt, threads = cpu_baseline(g, args.hids, args.depth, args.cpu_steps)
         out["cpu_baseline"] = {"value": edges_local / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
                                "sample": f"{args.cpu_steps} full fwd+bwd+Adam step(s) of the same c2 workload: "

@@ -169,9 +169,26 @@ class GCN_FC(GCNBase):
         self.lin_right = nn.Linear(hids, 3)
         self.dp = dp
 
+    def set_compute_dtype(self, dtype) -> "GCN_FC":
+        """fp32 (default) or bf16 activations / SpMM / MFMA FC (fp32 master
+        weights either way) -- the 16-bit path the CLI's --fp16 selects."""
+        if dtype in ("bf16", "bfloat16"):
+            dtype = torch.bfloat16
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"compute_dtype must be float32 or bfloat16, got {dtype}")
+        self.compute_dtype = dtype
+        return self
+
     def forward(self, batch):
         x_left, x_right, edge_index = batch.x_s, batch.x_t, batch.edge_index
         cd = self.compute_dtype
+        if x_left.dtype == torch.float16 or x_right.dtype == torch.float16 or \
+                self.lin_left.weight.dtype == torch.float16:
+            # val.py:269 model.half() / batch_to(half=True): there are no fp16 kernels in this build --
+            # refuse rather than silently promote to fp32.  The 16-bit path is bf16.
+            raise TypeError("GCN_FC: float16 inputs/weights are not supported on MI355X in this build; "
+                            "use GCN_FC(..., compute_dtype='bf16') (or set_compute_dtype('bf16')) with fp32 "
+                            "weights and inputs for 16-bit inference (the CLI's --fp16 does this)")
         # conv -> ReLU (arch.py:181-182): the ReLU is the FC kernel's epilogue.
         left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True)
         dp = self.dp if self.training else 0.0

@@ -105,19 +105,26 @@ def row_blocks(row: np.ndarray, m: int, world: int) -> np.ndarray:
     return np.maximum.accumulate(np.minimum(np.array(b, dtype=np.int64), m))
 
 
-def plan_partition(row, col, val, m: int, n: int, world: int, rank: int) -> PartitionPlan:
+def plan_partition(row, col, val, m: int, n: int, world: int, rank: int, bounds=None,
+                   owner=None) -> PartitionPlan:
+    """The plan of `rank` from the global edge list (tests, small graphs).
+    bounds: cons block split points (default nnz-balanced); owner: int64 [n]
+    owner rank per variable (default: the rank holding most of its edges)."""
     row = np.asarray(row, np.int64)
     col = np.asarray(col, np.int64)
     val = np.asarray(val, np.float32)
-    bounds = row_blocks(row, m, world)
+    bounds = row_blocks(row, m, world) if bounds is None else np.asarray(bounds, np.int64)
     blk = np.searchsorted(bounds, row, side="right") - 1
     # touches (var, rank) with edge counts, sorted by var then rank
     ukey, cnt = np.unique(col * world + blk, return_counts=True)
     tv, tr = ukey // world, ukey % world
-    owner = (np.arange(n, dtype=np.int64) * world) // max(n, 1)
-    order = np.lexsort((tr, -cnt, tv))  # per var: most edges first, then lowest rank
-    first = order[np.r_[True, tv[order][1:] != tv[order][:-1]]] if len(order) else order
-    owner[tv[first]] = tr[first]
+    if owner is None:
+        owner = (np.arange(n, dtype=np.int64) * world) // max(n, 1)
+        order = np.lexsort((tr, -cnt, tv))  # per var: most edges first, then lowest rank
+        first = order[np.r_[True, tv[order][1:] != tv[order][:-1]]] if len(order) else order
+        owner[tv[first]] = tr[first]
+    else:
+        owner = np.asarray(owner, np.int64)
     ntouch = np.bincount(tv, minlength=n)
     is_halo = tr != owner[tv]
     hv, hr = tv[is_halo], tr[is_halo]  # var hv is touched by rank hr and owned elsewhere (sorted by var)
@@ -146,6 +153,74 @@ def plan_partition(row, col, val, m: int, n: int, world: int, rank: int) -> Part
     return PartitionPlan(rank, world, m, n, lo, hi, owned, halo, row[sel] - lo, e_gcol, e_col, val[sel],
                          send_idx.astype(np.int64), send_counts, recv_idx.astype(np.int64), recv_counts,
                          int((ntouch >= 2).sum()))
+
+
+def _block_owner_ranges(blocks: int, world: int):
+    if blocks % world:
+        raise ValueError(f"{blocks} row blocks do not split evenly over {world} ranks")
+    return blocks // world
+
+
+def block_owner(spec, world: int) -> np.ndarray:
+    """Variable owners of plan_partition_blocks (int64 [n]): the rank whose
+    row blocks share the variable's block (tests compare against it)."""
+    per = _block_owner_ranges(spec.blocks, world)
+    return (np.arange(spec.n, dtype=np.int64) // spec.nb) // per
+
+
+def _a2a_ids(send: np.ndarray, send_counts: list, group) -> tuple:
+    """all_to_all of int64 id lists (the plan's setup exchange, once per
+    graph).  Returns (received ids grouped by source rank, recv counts)."""
+    world = dist.get_world_size(group)
+    dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else torch.device("cuda",
+                                                                                      torch.cuda.current_device())
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = rc.cpu().tolist()
+    out = torch.empty(sum(recv_counts), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(out, torch.from_numpy(np.ascontiguousarray(send)).to(dev), recv_counts, send_counts,
+                           group=group)
+    return out.cpu().numpy(), recv_counts
+
+
+def plan_partition_blocks(spec, world: int, rank: int, group=None, edges=None) -> PartitionPlan:
+    """The plan of `rank` for a synth.BlockLP, built from the rank's OWN rows
+    only (no global edge list): rank r holds row blocks [r*B/P, (r+1)*B/P)
+    and owns the variables of the same blocks' variable ranges; its halo is
+    the remote variables its rows touch.  The owners learn who touches their
+    variables with one all_to_all of id lists (the only O(halo) setup
+    traffic).  Equal to plan_partition(global graph, bounds, block_owner)
+    field for field (tests/test_partition.py).  `edges`: the rank's
+    (row, col, val) if already generated."""
+    per = _block_owner_ranges(spec.blocks, world)
+    b0, b1 = rank * per, (rank + 1) * per
+    row, col, val = edges if edges is not None else spec.rows(b0, b1)[:3]
+    row, col, val = np.asarray(row, np.int64), np.asarray(col, np.int64), np.asarray(val, np.float32)
+    lo, hi = b0 * spec.mb, b1 * spec.mb
+    v_lo, v_hi = b0 * spec.nb, b1 * spec.nb
+    owned = np.arange(v_lo, v_hi, dtype=np.int64)
+    far = col[(col < v_lo) | (col >= v_hi)]
+    halo = np.unique(far)  # ascending, hence grouped by owner rank
+    local_vars = np.concatenate([owned, halo])
+    h_owner = (halo // spec.nb) // per
+    send_counts = np.bincount(h_owner, minlength=world).tolist()
+    send_idx = np.arange(owned.shape[0], local_vars.shape[0], dtype=np.int64)
+    if world > 1:
+        got, recv_counts = _a2a_ids(halo, send_counts, group)
+        recv_idx = got - v_lo
+        nb_glob = torch.tensor([float(np.unique(got).shape[0])])
+        if dist.get_backend(group) != "gloo":
+            nb_glob = nb_glob.cuda()
+        dist.all_reduce(nb_glob, group=group)
+        n_boundary = int(nb_glob.item())
+    else:
+        recv_idx, recv_counts, n_boundary = np.empty(0, np.int64), [0], 0
+    # local column ids: owned = v - v_lo, halo = n_own + position in halo
+    e_col = np.where((col >= v_lo) & (col < v_hi), col - v_lo,
+                     owned.shape[0] + np.searchsorted(halo, col))
+    return PartitionPlan(rank, world, spec.m, spec.n, lo, hi, owned, halo, row - lo, col, e_col, val,
+                         send_idx, send_counts, recv_idx.astype(np.int64), recv_counts, n_boundary)
 
 
 def local_dual_csr(plan: PartitionPlan, device) -> BipartiteCSR:
@@ -633,18 +708,38 @@ class PartitionedCSR:
 
 
 def make_local_batch(plan: PartitionPlan, x_s, x_t, y_s, y_t, device, group=None):
-    """Rank-local BipartiteBatch whose edge_index is a PartitionedCSR."""
+    """Rank-local BipartiteBatch whose edge_index is a PartitionedCSR, from
+    GLOBAL node arrays (sliced here)."""
+    lv = plan.local_vars
+    sl = lambda a, idx: None if a is None else np.asarray(a)[idx]
+    rows = slice(plan.row_lo, plan.row_hi)
+    return local_batch(plan, sl(x_s, rows), sl(x_t, lv), sl(y_s, rows), sl(y_t, lv), device, group)
+
+
+def make_block_batch(spec, plan: PartitionPlan, device, group=None, cons=None):
+    """Rank-local batch of a synth.BlockLP partition: only this rank's
+    constraint blocks and its [owned | halo] variables are generated.
+    cons: the rank's (x_s, y_s) if already generated."""
+    per = spec.blocks // plan.world
+    b0 = plan.rank * per
+    if cons is None:
+        cons = [spec.cons_block(b) for b in range(b0, b0 + per)]
+        cons = (np.concatenate([c[0] for c in cons]), np.concatenate([c[1] for c in cons]))
+    x_t, y_t = spec.var_rows(plan.local_vars)
+    return local_batch(plan, cons[0], x_t, cons[1], y_t, device, group)
+
+
+def local_batch(plan: PartitionPlan, x_s, x_t, y_s, y_t, device, group=None):
+    """Rank-local BipartiteBatch from rank-LOCAL node arrays: x_s/y_s of the
+    rows [row_lo, row_hi), x_t/y_t of local_vars ([owned | halo])."""
     from .data import BipartiteBatch
 
     local = local_dual_csr(plan, device)
     lv = plan.local_vars
     adj = PartitionedCSR(local, Exchange(plan, device, group))
-    b = BipartiteBatch(
-        x_s=torch.as_tensor(np.asarray(x_s)[plan.row_lo:plan.row_hi]).to(device),
-        x_t=torch.as_tensor(np.asarray(x_t)[lv]).to(device),
-        y_s=None if y_s is None else torch.as_tensor(np.asarray(y_s)[plan.row_lo:plan.row_hi]).to(device),
-        y_t=None if y_t is None else torch.as_tensor(np.asarray(y_t)[lv]).to(device),
-        edge_index=adj, s_bs=plan.m_local, t_bs=plan.n_local, bs=plan.m_local + plan.n_local)
+    dev = lambda a: None if a is None else torch.as_tensor(np.ascontiguousarray(a)).to(device)
+    b = BipartiteBatch(x_s=dev(x_s), x_t=dev(x_t), y_s=dev(y_s), y_t=dev(y_t),
+                       edge_index=adj, s_bs=plan.m_local, t_bs=plan.n_local, bs=plan.m_local + plan.n_local)
     b.var_owned = torch.from_numpy(plan.var_owned).to(device)
     b.n_own = plan.n_own
     b.local_vars = torch.from_numpy(lv)
@@ -721,24 +816,64 @@ class BenchJob:
     local_nnz: int
     workload: str
     plan: PartitionPlan
+    batch: object
+    spec: object
+
+
+def bench_spec(args, world: int):
+    """c4 (BASELINE.json configs[3]): the fixed 2M x 4M, nnz 40M, 8-block
+    graph split over `world` ranks -- strong scaling.  Otherwise weak
+    scaling: `world` blocks of args.m x args.n, args.nnz each."""
+    from . import synth
+
+    if args.config == "c4":
+        return synth.BlockLP(args.m, args.n, args.nnz, blocks=8, rho=args.rho, seed=0)
+    return synth.BlockLP(args.m * world, args.n * world, args.nnz * world, blocks=world, rho=args.rho, seed=0)
 
 
 def build_bench_job(args, rank: int, world: int, device) -> BenchJob:
-    """Weak scaling: the global graph is `world` c2-sized row blocks
-    (world*m cons x world*n vars, world*nnz edges), a fraction rho of each
-    block's edges landing on other blocks' variables."""
-    from . import synth
+    """One rank's share of the bench graph: the rank generates and plans only
+    its own row blocks and [owned | halo] variables (plan_partition_blocks)."""
     from .arch import GCN_FC
     from .train import make_optimizer
 
-    g = synth.block_lp(args.m * world, args.n * world, args.nnz * world, parts=world, rho=args.rho, seed=0)
-    plan = plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
-    batch = make_local_batch(plan, g.x_s, g.x_t, g.y_s, g.y_t, device)
+    spec = bench_spec(args, world)
+    per = spec.blocks // world
+    row, col, val, x_s, y_s = spec.rows(rank * per, (rank + 1) * per)
+    plan = plan_partition_blocks(spec, world, rank, edges=(row, col, val))
+    del row, col, val
+    batch = make_block_batch(spec, plan, device, cons=(x_s, y_s))
     torch.manual_seed(0)
     model = GCN_FC(8, 8, hids=args.hids, depth=args.depth).to(device)
     opt, _ = make_optimizer(model)
     step = lambda: train_step_distributed(model, batch, opt)
-    wl = (f"row-partitioned synthetic LP {g.m}x{g.n} nnz={g.nnz} over {world} GPU(s) (c2-sized block per GPU, "
-          f"rho={args.rho}, {plan.n_boundary_global} boundary vars, {plan.halo.shape[0]} halo rows on rank "
-          f"{rank}), GCN_FC(8,8,hids={args.hids},depth={args.depth}) fwd+bwd+Adam")
-    return BenchJob(step, plan.nnz_local, wl, plan)
+    kind = ("c4: synthetic block LP" if args.config == "c4" else
+            f"{args.config} weak scaling: {world} x ({args.m}x{args.n}, nnz {args.nnz}) blocks,")
+    wl = (f"{kind} {spec.m}x{spec.n} nnz={spec.nnz} ({spec.blocks} row blocks, rho={spec.rho}) row-partitioned "
+          f"over {world} GPU(s), GCN_FC(8,8,hids={args.hids},depth={args.depth}) fwd+bwd+Adam")
+    return BenchJob(step, plan.nnz_local, wl, plan, batch, spec)
+
+
+def time_exchange(ex: Exchange, F: int, device, reps: int = 5) -> dict:
+    """Standalone cost of one boundary exchange at width F (outside the timed
+    steps): an owner reduce and a halo broadcast of [n_local, F] fp32 rows,
+    barrier + device sync around each; median ms.  Inside the training step
+    the same exchanges run asynchronously under independent compute."""
+    import time
+
+    full = torch.zeros((ex.n_local, F), dtype=torch.float32, device=device)
+    out = {"reduce_ms": [], "broadcast_ms": []}
+    for _ in range(reps + 1):
+        for name, fn in (("reduce_ms", lambda: ex.reduce_rows(full, inplace=True)),
+                         ("broadcast_ms", lambda: ex.broadcast_rows_(full))):
+            torch.cuda.synchronize(device)
+            dist.barrier()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(device)
+            out[name].append((time.perf_counter() - t0) * 1e3)
+    res = {k: float(np.median(v[1:])) for k, v in out.items()}
+    res["rows_out"] = int(sum(ex.send_counts))
+    res["rows_in"] = int(sum(ex.recv_counts))
+    res["bytes_per_exchange"] = (res["rows_out"] + res["rows_in"]) * F * 4
+    return res

@@ -146,6 +146,101 @@ def block_lp(m: int, n: int, nnz: int, parts: int, rho: float = 0.02, seed: int 
     return LPGraph(m, n, row, cols.reshape(-1), val, x_s, x_t, _labels(rf, x_s), _labels(rf, x_t))
 
 
+@dataclass
+class BlockLP:
+    """A block-structured LP defined block by block, so a
+    rank generates only the rows it owns (and the variable features it
+    needs) -- no rank ever materialises the global edge list.
+
+    `blocks` row blocks of m/blocks constraints; block b's edges stay in
+    variable block b's range with probability 1 - rho, else land on a uniform
+    variable.  Every constraint row has exactly nnz/m distinct columns.  Each
+    block is seeded on its own (numpy SeedSequence([seed, tag, b])), so the
+    graph is the same whatever the number of ranks it is split over: a
+    strong-scaling workload."""
+    m: int
+    n: int
+    nnz: int
+    blocks: int
+    rho: float = 0.02
+    seed: int = 0
+
+    def __post_init__(self):
+        if self.nnz % self.m or self.m % self.blocks or self.n % self.blocks:
+            raise ValueError("BlockLP needs nnz % m == 0 and m, n divisible by blocks")
+
+    @property
+    def mb(self) -> int:
+        return self.m // self.blocks
+
+    @property
+    def nb(self) -> int:
+        return self.n // self.blocks
+
+    def _rng(self, tag: int, b: int):
+        return np.random.default_rng(np.random.SeedSequence([self.seed, tag, b]))
+
+    def block_edges(self, b: int):
+        """(row, col, val) of row block b, global ids, sorted by (row, col)."""
+        deg, mb, nb = self.nnz // self.m, self.mb, self.nb
+        rs = self._rng(0, b)
+        c = _distinct_cols_per_row(rs, mb, nb, deg) + b * nb
+        far = rs.random((mb, deg)) < self.rho
+        c = np.where(far, rs.integers(0, self.n, size=(mb, deg), dtype=np.int64), c)
+        c = np.sort(c, axis=1)
+        bad = (np.diff(c, axis=1) == 0).any(axis=1)  # a far pick may hit a local one: re-draw those rows local
+        while bad.any():
+            c[bad] = _distinct_cols_per_row(rs, int(bad.sum()), nb, deg) + b * nb
+            bad = (np.diff(c, axis=1) == 0).any(axis=1)
+        row = np.repeat(np.arange(b * mb, (b + 1) * mb, dtype=np.int64), deg)
+        return row, c.reshape(-1), _values(rs, mb * deg)
+
+    def cons_block(self, b: int):
+        """(x_s, y_s) of the constraints of row block b."""
+        rf = self._rng(1, b)
+        x = _features(rf, self.mb, 0.5, 0.5)
+        return x, _labels(rf, x)
+
+    def var_block(self, b: int):
+        """(x_t, y_t) of the variables of variable block b."""
+        rf = self._rng(2, b)
+        x = _features(rf, self.nb, 0.1, 0.7)
+        return x, _labels(rf, x)
+
+    def var_rows(self, ids: np.ndarray):
+        """(x_t, y_t) of arbitrary global variable ids (generates only the
+        variable blocks they fall in)."""
+        ids = np.asarray(ids, np.int64)
+        x = np.empty((ids.shape[0], 8), np.float32)
+        y = np.empty(ids.shape[0], np.int64)
+        blk = ids // self.nb
+        for b in np.unique(blk):
+            sel = blk == b
+            xb, yb = self.var_block(int(b))
+            x[sel], y[sel] = xb[ids[sel] - b * self.nb], yb[ids[sel] - b * self.nb]
+        return x, y
+
+    def rows(self, b0: int, b1: int):
+        """Edges and constraint features of row blocks [b0, b1)."""
+        parts = [self.block_edges(b) for b in range(b0, b1)]
+        cons = [self.cons_block(b) for b in range(b0, b1)]
+        cat = lambda xs: np.concatenate(xs) if xs else np.empty(0)
+        return (cat([p[0] for p in parts]), cat([p[1] for p in parts]), cat([p[2] for p in parts]).astype(np.float32),
+                cat([c[0] for c in cons]).reshape(-1, 8).astype(np.float32), cat([c[1] for c in cons]).astype(np.int64))
+
+    def full(self) -> LPGraph:
+        """The whole graph (single-GPU runs and tests)."""
+        row, col, val, x_s, y_s = self.rows(0, self.blocks)
+        x_t, y_t = self.var_rows(np.arange(self.n, dtype=np.int64))
+        return LPGraph(self.m, self.n, row, col, val, x_s, x_t, y_s, y_t)
+
+
+def c4_spec(scale: int = 1, seed: int = 0) -> BlockLP:
+    """BASELINE.json configs[3]: 2M cons x 4M vars, nnz 40M, 8 row blocks,
+    rho = 0.02 (1/scale of it per dimension for reduced-size tests)."""
+    return BlockLP(2_000_000 // scale, 4_000_000 // scale, 40_000_000 // scale, blocks=8, rho=0.02, seed=seed)
+
+
 CONFIGS = {
     # BASELINE.json configs[1]: 100K cons x 200K vars, nnz 2M, hid 1024, depth 3
     "c2": dict(m=100_000, n=200_000, nnz=2_000_000, hids=1024, depth=3),

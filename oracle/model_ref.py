@@ -159,15 +159,33 @@ class _OracleSpMM(torch.autograd.Function):
         return torch.from_numpy(spmm_f32(*ctx.bwd, gY.contiguous().numpy())), None, None
 
 
-def spmm_t(csr, csr_t, X: torch.Tensor) -> torch.Tensor:
-    """Differentiable fp32 spmm; fp64 inputs use scipy (order-free sanity path)."""
-    if X.dtype == torch.float64:
-        import scipy.sparse as sp
+def _scipy64(csr, n_cols: int):
+    import scipy.sparse as sp
 
-        rowptr, col, val = csr
-        M = rowptr.shape[0] - 1
-        A = sp.csr_matrix((val.astype(np.float64), col, rowptr), shape=(M, X.shape[0]))
-        return torch.from_numpy(A @ X.detach().numpy())
+    rowptr, col, val = csr
+    return sp.csr_matrix((np.asarray(val, np.float64), col, rowptr), shape=(rowptr.shape[0] - 1, n_cols))
+
+
+class _OracleSpMM64(torch.autograd.Function):
+    """fp64 spmm (scipy, order-free: the 'truth' side of the fp32 comparisons);
+    bwd = A^T dY, as SPMMSum's."""
+
+    @staticmethod
+    def forward(ctx, X, fwd, bwd):
+        ctx.bwd, ctx.n_src = bwd, X.shape[0]
+        return torch.from_numpy(_scipy64(fwd, X.shape[0]) @ X.detach().numpy())
+
+    @staticmethod
+    def backward(ctx, gY):
+        A_t = _scipy64(ctx.bwd, gY.shape[0])
+        return torch.from_numpy(A_t @ gY.detach().contiguous().numpy()), None, None
+
+
+def spmm_t(csr, csr_t, X: torch.Tensor) -> torch.Tensor:
+    """Differentiable spmm: fp32 in torch_sparse spmm_cpu order; fp64 through
+    scipy (the order-free fp64 truth)."""
+    if X.dtype == torch.float64:
+        return _OracleSpMM64.apply(X, csr, csr_t)
     return _OracleSpMM.apply(X, csr, csr_t)
 
 
@@ -344,9 +362,9 @@ def balanced(logpr_cons, logpr_vars, y_s, y_t):
     """train.py:39-46."""
     loss = 0.
     m, n = len(y_s), len(y_t)
-    criterion = torch.nn.CrossEntropyLoss(weight=labels_to_balanced_weights(y_s))
+    criterion = torch.nn.CrossEntropyLoss(weight=labels_to_balanced_weights(y_s).to(logpr_cons.dtype))
     loss += (m + n) / m * criterion(logpr_cons, y_s)
-    criterion = torch.nn.CrossEntropyLoss(weight=labels_to_balanced_weights(y_t))
+    criterion = torch.nn.CrossEntropyLoss(weight=labels_to_balanced_weights(y_t).to(logpr_vars.dtype))
     loss += (m + n) / n * criterion(logpr_vars, y_t)
     return loss
 

@@ -1,0 +1,262 @@
+"""Full-size parity at the BASELINE.json configurations that fit one GPU.
+
+c2 (configs[1]: 100K cons x 200K vars, nnz 2M, GCN_FC(8,8,hids=1024,depth=3)),
+against the oracle's MKL fp32 evaluation -- the reference's own CPU
+arithmetic (PyG GraphConv = torch_sparse spmm_sum + torch F.linear,
+arch.py:167-193) -- and against an fp64 evaluation of the same function.
+
+Why the north-star 1e-4 is asserted on the pre-normalisation head outputs
+and the normalised logits get a derived bound: add_knowledge (arch.py:134-135)
+returns 10 * h / |h|.  Its Jacobian has norm 10 / |h|, so any two fp32
+evaluations of the network that agree to e on h agree only to ~10 e / |h| on
+the logits; at c2 a few nodes have |h| ~ 1e-2, and the reference's own MKL
+fp32 evaluation is ~3e-4 from fp64 there.  The test therefore asserts:
+
+* heads h (the model output before add_knowledge): |h_HIP - h_MKL| <= 1e-4
+  everywhere (the north-star bar, on the quantity the network computes);
+* logits: every node is within 1e-4 of MKL, OR within the exact Lipschitz
+  bound of the normalisation, |n(a) - n(b)| <= 2 |a - b| / |b| (times 10),
+  evaluated with that node's own head difference -- so every excess over
+  1e-4 is explained by add_knowledge's amplification of a head difference
+  that itself meets 1e-4; the number of such nodes is printed and bounded;
+* argmax basis labels identical to MKL's wherever MKL's top-2 gap exceeds
+  twice the largest logit difference (where no fp32 evaluation can flip);
+* inference_gnn labels (val.py:106-124) identical to MKL's except at nodes
+  that are near-ties for the rule itself (P[:,1] within the propagated error
+  of the m-th largest, or a {0,2} gap within it);
+* the same against fp64 with the reference's own fp32 distance as the yard
+  stick (the HIP path is at least as close to fp64 as MKL is).
+
+Training (train mode, dropout 0): loss and every parameter gradient of one
+c2 step vs the oracle's MKL autograd and vs fp64 autograd.
+
+c5 (configs[4]: the c2 graph, hids=2048, depth=6, bf16 activations/SpMM/MFMA,
+fp32 master weights): logits vs the oracle's fp32 MKL evaluation within a
+stated bf16 tolerance, argmax agreement, and one training step's gradients.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_ref as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+DEV = "cuda:0"
+LOGIT_ATOL = 1e-4
+
+_CACHE = {}
+
+
+def _graph():
+    if "g" not in _CACHE:
+        from lpgnn import synth
+
+        g = synth.uniform_lp(100_000, 200_000, 2_000_000, seed=0)
+        A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
+        AT = O.csr_transpose(*A, g.m, g.n)
+        _CACHE.update(g=g, A=A, AT=AT)
+    return _CACHE["g"], _CACHE["A"], _CACHE["AT"]
+
+
+def _weights(hids, depth):
+    from lpgnn import GCN_FC
+
+    torch.manual_seed(0)
+    return {k: v.detach().clone() for k, v in GCN_FC(8, 8, hids=hids, depth=depth).state_dict().items()}
+
+
+def _oracle(hids, depth, dtype, grads):
+    """Oracle logits (+ heads, + loss and grads with `grads`) for the c2 graph
+    with the seed-0 weights, in `dtype` (float32 = MKL, the reference's
+    arithmetic; float64 = truth)."""
+    key = (hids, depth, dtype, grads)
+    if key not in _CACHE:
+        g, A, AT = _graph()
+        sd = {k: v.to(dtype).requires_grad_(grads) for k, v in _weights(hids, depth).items()}
+        xs, xt = torch.from_numpy(g.x_s).to(dtype), torch.from_numpy(g.x_t).to(dtype)
+        keep = {}
+        with torch.set_grad_enabled(grads):
+            lc, lv = O.gcn_fc_forward(sd, xs, xt, A, AT, depth, keep=keep)
+            out = dict(logits=torch.cat((lc, lv)).detach(),
+                       heads=torch.cat((keep["head_l"], keep["head_r"])).detach())
+            if grads:
+                loss = O.balanced(lc, lv, torch.from_numpy(g.y_s), torch.from_numpy(g.y_t))
+                loss.backward()
+                out["loss"] = loss.item()
+                out["grads"] = {k: v.grad.detach().clone() for k, v in sd.items()}
+        _CACHE[key] = out
+    return _CACHE[key]
+
+
+def _batch(with_labels=True):
+    from lpgnn import BipartiteBatch, BipartiteCSR
+
+    g, _, _ = _graph()
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    kw = dict(y_s=torch.from_numpy(g.y_s).to(DEV), y_t=torch.from_numpy(g.y_t).to(DEV)) if with_labels else {}
+    return BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                          edge_index=adj, s_bs=g.m, t_bs=g.n, **kw)
+
+
+def _model(hids, depth, dtype=torch.float32, dp=0.1):
+    from lpgnn import GCN_FC
+
+    model = GCN_FC(8, 8, hids=hids, depth=depth, dp=dp, compute_dtype=dtype)
+    model.load_state_dict(_weights(hids, depth))
+    return model.to(DEV)
+
+
+def _hip_eval_with_heads(model, batch, monkeypatch):
+    """Eval logits plus the head outputs the model hands to add_knowledge."""
+    from lpgnn import arch
+
+    seen = {}
+    real = arch.add_knowledge
+
+    def spy(left, right, xl, xr, bound=10):
+        seen["heads"] = torch.cat((left, right)).detach().clone()
+        return real(left, right, xl, xr, bound)
+
+    monkeypatch.setattr(arch, "add_knowledge", spy)
+    model.eval()
+    with torch.no_grad():
+        logits = torch.cat(model(batch))
+    return logits.cpu().double(), seen["heads"].cpu().double()
+
+
+def _near_tie_labels(logits, m, eps):
+    """Nodes where inference_gnn (val.py:106-124) can change under a logit
+    perturbation of at most eps: P[:,1] within the propagated error of the
+    m-th largest P[:,1] (softmax is 1/2-Lipschitz per coordinate in the max
+    norm, so |dP| <= eps), or |logit0 - logit2| <= 2 eps."""
+    p1 = torch.softmax(logits, -1)[:, 1]
+    thr = p1.topk(m).values[-1]
+    return ((p1 - thr).abs() <= 2 * eps) | ((logits[:, 0] - logits[:, 2]).abs() <= 2 * eps)
+
+
+@pytest.mark.parametrize("arith", ["x3", "fp32"])
+def test_c2_eval_logits_labels_vs_reference_arithmetic(arith, monkeypatch):
+    from lpgnn import fc
+    from lpgnn.val import inference_gnn
+
+    monkeypatch.setattr(fc, "ARITH", arith)
+    g, _, _ = _graph()
+    r32, r64 = _oracle(1024, 3, torch.float32, False), _oracle(1024, 3, torch.float64, False)
+    got, heads = _hip_eval_with_heads(_model(1024, 3), _batch(False), monkeypatch)
+    ref, ref_h = r32["logits"].double(), r32["heads"].double()
+
+    # (1) the heads meet the north-star 1e-4 against the reference arithmetic, everywhere
+    dh = (heads - ref_h).abs()
+    # (2) logits: within 1e-4, or within add_knowledge's Lipschitz bound of the node's own head difference
+    d = (got - ref).abs().max(-1).values
+    bound = 10 * 2 * (heads - ref_h).norm(dim=-1) / ref_h.norm(dim=-1) * (1 + 1e-6) + 4e-6
+    over = d > LOGIT_ATOL
+    n_nodes = got.shape[0]
+    print(f"[{arith}] c2: max|h_HIP - h_MKL| = {dh.max():.3e}; max|logit_HIP - logit_MKL| = {d.max():.3e}, "
+          f"mean {d.mean():.3e}; nodes > 1e-4: {int(over.sum())} of {n_nodes} "
+          f"(min |h| among them {ref_h.norm(dim=-1)[over].min() if over.any() else float('nan'):.3e}); "
+          f"max|MKL - fp64| = {(ref - r64['logits']).abs().max():.3e}, "
+          f"max|HIP - fp64| = {(got - r64['logits']).abs().max():.3e}")
+    assert dh.max() <= LOGIT_ATOL
+    assert bool((~over | (d <= bound)).all()), "a logit difference not explained by add_knowledge's amplification"
+    # round 2: 13 (x3) / 9 (exact fp32) of 300 000 nodes, all with |h| < 1e-2
+    assert int(over.sum()) <= n_nodes // 5000, "more than 0.02 % of nodes beyond 1e-4 of the reference arithmetic"
+    # (3) argmax == MKL's outside near-ties at the observed difference
+    emax = float(d.max())
+    top2 = ref.topk(2, dim=-1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 2 * emax
+    assert torch.equal(got.argmax(-1)[clear], ref.argmax(-1)[clear])
+    # (4) inference_gnn labels == MKL's except at the rule's own near-ties
+    lab, lab32 = inference_gnn(got.float(), g.m), inference_gnn(ref.float(), g.m)
+    tie = _near_tie_labels(ref, g.m, emax)
+    diff = lab != lab32
+    print(f"[{arith}] c2: inference_gnn labels differing from MKL's: {int(diff.sum())} "
+          f"(near-tie nodes at eps={emax:.2e}: {int(tie.sum())})")
+    assert bool((~diff | tie).all()), "a basis label differs from the reference arithmetic outside a near-tie"
+    # (5) against fp64: at least as close as the reference's fp32 arithmetic
+    t = r64["logits"]
+    e_got, e_ref = (got - t).abs(), (ref - t).abs()
+    assert e_got.max() <= 1.5 * e_ref.max() and e_got.mean() <= 1.5 * e_ref.mean()
+
+
+@pytest.mark.parametrize("arith", ["x3"])
+def test_c2_training_step_grads_vs_oracle_autograd(arith, monkeypatch):
+    """One c2 training step (train.py:117-128, dropout 0): loss and every
+    parameter gradient vs the oracle's MKL autograd; each gradient's distance
+    to fp64 is at most 2x MKL's own (+ a floor at fp32 resolution of the
+    tensor), and within rtol 1e-3 of MKL in the relative Frobenius norm."""
+    from lpgnn import fc
+    from lpgnn.train import balanced
+
+    monkeypatch.setattr(fc, "ARITH", arith)
+    r32, r64 = _oracle(1024, 3, torch.float32, True), _oracle(1024, 3, torch.float64, True)
+    model = _model(1024, 3, dp=0.0).train()
+    batch = _batch()
+    lc, lv = model(batch)
+    loss = balanced(lc, lv, batch.y_s, batch.y_t)
+    loss.backward()
+    assert abs(loss.item() - r32["loss"]) <= 1e-4 * max(1.0, abs(r32["loss"]))
+    worst = []
+    for k, p in model.named_parameters():
+        got = p.grad.detach().cpu().double()
+        mkl, t = r32["grads"][k].double(), r64["grads"][k]
+        scale = t.norm()
+        rel_mkl = ((got - mkl).norm() / scale).item()
+        e_got, e_ref = (got - t).norm().item(), (mkl - t).norm().item()
+        worst.append((rel_mkl, k, e_got / scale.item(), e_ref / scale.item()))
+        assert rel_mkl <= 1e-3, (k, rel_mkl)
+        assert e_got <= 2 * e_ref + 2 ** -22 * scale.item(), (k, e_got, e_ref)
+        np.testing.assert_allclose(got.numpy(), mkl.numpy(), rtol=1e-2, atol=1e-3 * t.abs().max().item(), err_msg=k)
+    worst.sort(reverse=True)
+    print("c2 grads, worst relative |HIP - MKL| (rel |HIP - fp64|, rel |MKL - fp64|):",
+          ", ".join(f"{k} {a:.1e} ({b:.1e}, {c:.1e})" for a, k, b, c in worst[:4]))
+
+
+# c5 tolerance: bf16 activations (8-bit significand, relative rounding 2^-9) through 6 layers;
+# the knowledge-normalised logits live in [-20, 10].
+# Round-2 measurement: mean 0.032, p99 0.18, argmax agreement 0.9976.  A node whose raw head output
+# |h| is small is amplified by add_knowledge's 10/|h| (the same effect as the c2 test's, at bf16's
+# 2^-9 instead of fp32's 2^-24), so even a top-2 gap of 1.0 can flip there: a rate, not all-equal.
+C5_MEAN, C5_P99, C5_ARGMAX, C5_ARGMAX_CLEAR = 0.05, 0.25, 0.995, 0.999
+
+
+def test_c5_bf16_logits_and_step_vs_fp32_oracle(monkeypatch):
+    """BASELINE configs[4] at its full size: GCN_FC(8,8,hids=2048,depth=6) in
+    bf16 on the c2 graph vs the oracle's fp32 MKL evaluation (logits: mean
+    |d| <= 0.05, p99 <= 0.25, argmax agreement >= 99.5 % overall and
+    >= 99.9 % where MKL's top-2 gap exceeds 1.0), then one training step: finite fp32
+    master-weight gradients with cosine >= 0.95 to the oracle's autograd."""
+    from lpgnn.train import balanced
+
+    r32 = _oracle(2048, 6, torch.float32, True)
+    model = _model(2048, 6, dtype=torch.bfloat16, dp=0.0)
+    batch = _batch()
+    model.eval()
+    with torch.no_grad():
+        got = torch.cat(model(batch)).cpu().double()
+    ref = r32["logits"].double()
+    d = (got - ref).abs().flatten()
+    agree = (got.argmax(-1) == ref.argmax(-1)).double().mean().item()
+    top2 = ref.topk(2, dim=-1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1.0
+    print(f"c5 bf16 vs fp32 MKL: mean |d| {d.mean():.3e}, p99 {torch.quantile(d[:1 << 24], 0.99):.3e}, "
+          f"max {d.max():.3e}; argmax agreement {agree:.5f}")
+    assert torch.isfinite(got).all()
+    assert d.mean().item() <= C5_MEAN and torch.quantile(d[:1 << 24], 0.99).item() <= C5_P99
+    assert agree >= C5_ARGMAX
+    agree_clear = (got.argmax(-1)[clear] == ref.argmax(-1)[clear]).double().mean().item()
+    print(f"c5: argmax agreement where MKL's top-2 gap > 1: {agree_clear:.5f} over {int(clear.sum())} nodes")
+    assert agree_clear >= C5_ARGMAX_CLEAR
+    model.train()
+    lc, lv = model(batch)
+    loss = balanced(lc, lv, batch.y_s, batch.y_t)
+    loss.backward()
+    assert abs(loss.item() - r32["loss"]) <= 0.02 * abs(r32["loss"]) + 1e-3
+    cos_min = 1.0
+    for k, p in model.named_parameters():
+        assert p.grad is not None and p.grad.dtype == torch.float32 and torch.isfinite(p.grad).all(), k
+        cos = torch.nn.functional.cosine_similarity(p.grad.detach().cpu().double().flatten(),
+                                                    r32["grads"][k].double().flatten(), dim=0).item()
+        cos_min = min(cos_min, cos)
+        assert cos >= 0.95, (k, cos)
+    print(f"c5 bf16 step: loss {loss.item():.5f} (MKL {r32['loss']:.5f}), min grad cosine {cos_min:.4f}")

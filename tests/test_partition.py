@@ -93,7 +93,13 @@ def _cpu_knowledge(logit, feas, bound=10):
     return l
 
 
-def _worker(rank, world, port, out_dir):
+def _c4_small():
+    from lpgnn import synth
+
+    return synth.c4_spec(scale=50, seed=3)  # 40K x 80K, nnz 800K, the c4 generator at 1/50 size
+
+
+def _worker(rank, world, port, out_dir, mode="global"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
@@ -107,9 +113,16 @@ def _worker(rank, world, port, out_dir):
         fc.linear = lambda x, w, b: F.linear(x, w, b)
         fc.knowledge = _cpu_knowledge
 
-        g = _graph()
-        plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
-        batch = part.make_local_batch(plan, g.x_s, g.x_t, g.y_s, g.y_t, device="cpu")
+        if mode == "c4":  # each rank generates and plans only its own blocks
+            spec = _c4_small()
+            plan = part.plan_partition_blocks(spec, world, rank)
+            batch = part.make_block_batch(spec, plan, device="cpu")
+            g = spec.full()  # the single-graph reference below
+            _check_block_plan(plan, g, spec, world, rank)
+        else:
+            g = _graph()
+            plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
+            batch = part.make_local_batch(plan, g.x_s, g.x_t, g.y_s, g.y_t, device="cpu")
         torch.manual_seed(0)
         model = GCN_FC(8, 8, hids=16, depth=4, dp=0.0)
         sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
@@ -146,5 +159,52 @@ def _worker(rank, world, port, out_dir):
 @pytest.mark.parametrize("world", [2, 3])
 def test_partitioned_training_step_matches_single_graph(tmp_path, world):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").exists()
+
+
+def _check_block_plan(plan, g, spec, world, rank):
+    """The rank-local plan equals the global planner's with the same cons
+    blocks and the block owner rule, field for field."""
+    from lpgnn import partition as part
+
+    per = spec.blocks // world
+    bounds = np.arange(world + 1, dtype=np.int64) * per * spec.mb
+    ref = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank, bounds=bounds,
+                              owner=part.block_owner(spec, world))
+    for f in ("row_lo", "row_hi", "send_counts", "recv_counts"):
+        assert getattr(plan, f) == getattr(ref, f), f
+    for f in ("owned", "halo", "e_row", "e_gcol", "e_col", "e_val", "send_idx", "recv_idx"):
+        assert np.array_equal(getattr(plan, f), getattr(ref, f)), f
+
+
+def test_block_lp_generator_is_rank_independent():
+    """BlockLP is defined block by block: any split of the blocks generates
+    the same graph (strong scaling keeps the workload fixed)."""
+    spec = _c4_small()
+    g = spec.full()
+    assert g.nnz == spec.nnz and g.m == spec.m and g.n == spec.n
+    row, col, val, xs, ys = spec.rows(2, 4)
+    sel = (g.row >= 2 * spec.mb) & (g.row < 4 * spec.mb)
+    assert np.array_equal(row, g.row[sel]) and np.array_equal(col, g.col[sel]) and np.array_equal(val, g.val[sel])
+    assert np.array_equal(xs, g.x_s[2 * spec.mb:4 * spec.mb]) and np.array_equal(ys, g.y_s[2 * spec.mb:4 * spec.mb])
+    ids = np.array([5, spec.n - 1, spec.nb, 3 * spec.nb + 7])
+    x, y = spec.var_rows(ids)
+    assert np.array_equal(x, g.x_t[ids]) and np.array_equal(y, g.y_t[ids])
+    # rows have exactly nnz/m distinct, sorted columns; about rho of the edges leave their block
+    deg = np.diff(np.searchsorted(g.row, np.arange(g.m + 1)))
+    assert (deg == spec.nnz // spec.m).all()
+    key = g.row * g.n + g.col
+    assert (np.diff(key) > 0).all()
+    far = (g.col // spec.nb) != (g.row // spec.mb)
+    assert abs(far.mean() - spec.rho * (1 - 1 / spec.blocks)) < 0.005
+
+
+def test_c4_reduced_two_ranks_match_single_graph(tmp_path):
+    """The c4 generator at 1/50 size on 2 gloo ranks: rank-local planning ==
+    the global planner, and the partitioned training step (logits of owned
+    and halo rows, loss, gradients) == the single-graph oracle."""
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), "c4"), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"ok{r}").exists()

@@ -1,0 +1,183 @@
+"""The run_exp / validation driver and CLI (lpgnn.run) on the host: dataset
+layout and split, LR schedule, checkpoints, and the data-parallel replicas
+over gloo.  The product model needs the GPU, so these tests drive the loop
+with a small stand-in module of the same API (forward(batch) -> logits);
+tests/test_gpu_run.py runs the same driver with GCN_FC on the device."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def write_dataset(root, k=4, seed=0, sizes=((60, 120, 600), (50, 90, 500), (80, 100, 800), (40, 70, 400))):
+    """k synthetic LPs as processed .pk records (dataset.py:213-217 layout)
+    under {root}/processed, named like the reference's files."""
+    from lpgnn import lpio, synth
+
+    os.makedirs(os.path.join(root, "processed"), exist_ok=True)
+    for i in range(k):
+        m, n, nnz = sizes[i % len(sizes)]
+        g = synth.uniform_lp(m, n, nnz, seed=seed + i)
+        rec = [g.row.astype(np.int32), g.col.astype(np.int32), g.val.astype(np.float64), g.x_s, g.x_t, g.y_s, g.y_t,
+               m + n]
+        lpio.msgpack_dump(rec, os.path.join(root, "processed", f"lp{i}.pk"))
+    return root
+
+
+class TinyModel(torch.nn.Module):
+    """Stand-in with GCN_FC's call contract (and GCNBase save/load)."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.lin_left = torch.nn.Linear(8, 3)
+        self.lin_right = torch.nn.Linear(8, 3)
+
+    def forward(self, batch):
+        return self.lin_left(batch.x_s), self.lin_right(batch.x_t)
+
+    def save(self, pn):
+        torch.save(self.state_dict(), pn)
+
+    def load(self, pn):
+        self.load_state_dict(torch.load(pn, map_location="cpu", weights_only=True))
+
+
+def _args(tmp_path, *extra):
+    from lpgnn import run
+
+    return run.parse_args(["train", "--dataset", "synth", "--data_prefix", str(tmp_path / "data"), "--log_prefix",
+                           str(tmp_path / "runs"), "--epochs", "2", "--exp_nm", "t", *extra])
+
+
+def test_cli_flags_and_paths(tmp_path):
+    from lpgnn import run
+
+    a = run.parse_args(["val", "--arch", "GCN_FC(8,8,hids=1024,depth=3)", "--dataset", "mirp", "--data_prefix", "/d",
+                        "--lp_method", "primal", "--solver_prefix", "highs", "--fp16", "1"])
+    assert a.phase == "val" and a.lp_method == 4 and a.fp16 == 1
+    assert a.dataset_processed_prefix == "/d/mirp/highs-inp_tgt-m4/"  # utils.py:836-837
+    assert a.edge_num_thresh == 12e6 and a.batch_size == 327680  # utils.py:812-813
+    b = run.parse_args([])
+    assert b.phase == "train" and b.lr == 1e-3 and b.opt == "adam" and b.loss == "balanced"
+    assert b.dataset_processed_prefix.endswith("/None/highs-inp_tgt/")
+
+
+def test_split_matches_reference_rule():
+    """utils.py:256-262: int(max(0.7 n, 1)) train graphs from a seed-0 permutation."""
+    from lpgnn import run
+
+    for n in (1, 2, 3, 4, 10, 37):
+        tr, va = run.split_idxs_train_val(n, 0)
+        np.random.seed(0)
+        p = np.random.permutation(n)
+        k = int(max(n * 7 / 10, 1))
+        assert np.array_equal(tr, np.sort(p[:k])) and np.array_equal(va, np.sort(p[k:]))
+
+
+def test_dataset_order_and_loading(tmp_path):
+    from lpgnn import run
+
+    root = write_dataset(str(tmp_path / "ds"), k=4)
+    for nm in ("lp10.pk", "lp2b.pk"):  # (len, name) ordering, dataset.py:164
+        os.link(os.path.join(root, "processed", "lp1.pk"), os.path.join(root, "processed", nm))
+    ds = run.LPDataset(root, device="cpu")
+    assert [os.path.basename(ds.path(i)) for i in range(len(ds))] == \
+        ["lp0.pk", "lp1.pk", "lp2.pk", "lp3.pk", "lp10.pk", "lp2b.pk"]
+    b = ds[1]
+    assert hasattr(b, "x_s") and b.x_s.shape == (50, 8) and b.edge_index.nnz() == 500
+    small = run.LPDataset(root, device="cpu", thresh_num=450)  # above the threshold: homogeneous graph
+    assert not hasattr(small[1], "x_s") and small[1].num_nodes == 140 and hasattr(small[3], "x_s")
+    sub = ds[np.array([3, 0])]
+    assert len(sub) == 2 and os.path.basename(sub.path(0)) == "lp3.pk"
+
+
+def test_run_exp_schedule_checkpoint_and_resume(tmp_path):
+    from lpgnn import run
+
+    write_dataset(str(tmp_path / "data" / "synth" / "highs-inp_tgt"), k=4)
+    args = _args(tmp_path)
+    args.dev = "cpu"
+    hist = run.run_exp(args, model=TinyModel())
+    assert hist["lr"] == [1e-3, 1e-4]  # StepLR(step_size=max(2 // 4, 1), gamma=0.1), stepped per epoch
+    assert hist["steps"] == 2 * 2 and all(np.isfinite(hist["epoch_loss"]))  # 2 train graphs x 2 epochs
+    ck = torch.load(hist["checkpoint"], map_location="cpu", weights_only=True)
+    assert set(ck) == set(TinyModel().state_dict())
+    assert os.path.exists(os.path.join(args.log_dir, "args.json"))
+    # --load_from resumes from the checkpoint
+    m2 = TinyModel()
+    m2.load(hist["checkpoint"])
+    for k, v in ck.items():
+        assert torch.equal(m2.state_dict()[k], v)
+    # validation on the held-out graphs
+    ds = run.LPDataset(args.dataset_processed_prefix, device="cpu")
+    _, va = run.split_train_val(ds)
+    import lpgnn.val as V
+
+    real = V.model_inference_with_batch
+    try:
+        V.model_inference_with_batch = lambda model, g, *a, **k: model(g)
+        _, acc, rows = run.validation(m2, va, args)
+    finally:
+        V.model_inference_with_batch = real
+    assert 0.0 <= acc <= 1.0 and len(rows) == 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _replica_worker(rank, world, port, tmp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    try:
+        from lpgnn import run
+
+        args = run.parse_args(["train", "--dataset", "synth", "--data_prefix", os.path.join(tmp, "data"),
+                               "--log_prefix", os.path.join(tmp, f"runs{rank}"), "--epochs", "1", "--replicas", "1"])
+        args.dev = "cpu"
+        model = TinyModel()
+        run.run_exp(args, model=model)
+        torch.save(model.state_dict(), os.path.join(tmp, f"final{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_replicas_gloo(tmp_path):
+    """2 gloo ranks, 4 graphs -> 2 train graphs = one round: both ranks end
+    with identical parameters, equal to one Adam step on the mean of the two
+    graphs' gradients (computed here in one process)."""
+    from lpgnn import run
+    from lpgnn.train import balanced, make_optimizer
+
+    write_dataset(str(tmp_path / "data" / "synth" / "highs-inp_tgt"), k=4)
+    mp.spawn(_replica_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    p0 = torch.load(tmp_path / "final0.pt", weights_only=True)
+    p1 = torch.load(tmp_path / "final1.pt", weights_only=True)
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
+    # reference: same init, mean gradient of the two train graphs, one Adam step
+    args = _args(tmp_path)
+    ds = run.LPDataset(args.dataset_processed_prefix, device="cpu")
+    tr, _ = run.split_train_val(ds)
+    model = TinyModel()
+    opt, _ = make_optimizer(model, "adam", 1e-3, 1)
+    grads = []
+    for i in range(len(tr)):
+        model.zero_grad()
+        b = tr[i]
+        lc, lv = model(b)
+        balanced(lc, lv, b.y_s, b.y_t).backward()
+        grads.append([p.grad.clone() for p in model.parameters()])
+    for p, ga, gb in zip(model.parameters(), *grads):
+        p.grad = (ga + gb) / 2
+    opt.step()
+    for k, v in model.state_dict().items():
+        torch.testing.assert_close(p0[k], v, rtol=1e-6, atol=1e-7, msg=k)
