@@ -96,6 +96,19 @@ lpg_status lpg_csr_pack_f32(const int64_t *row, const int64_t *col, const float 
 lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx,
                         float *Y, int64_t ldy, int64_t F, void *stream);
 
+/* lpg_spmm_f32 with degree-aware scheduling for skewed rows: heavy_rows
+ * (device int32 [n_heavy]) must list exactly the rows of A with more than
+ * `thresh` edges (any order).  Those rows run as (row, 64-column) wave units
+ * at the head of the grid instead of (row, 256-column) units, so a long
+ * constraint row's sequential chain is spread over 4x the waves; every
+ * element is still summed over its row's edges in CSR order -- the result
+ * is bitwise lpg_spmm_f32's.  F < 256 and unaligned shapes ignore the list.
+ * Same fwd/bwd use as lpg_spmm_f32 (torch_sparse spmm_sum / SPMMSum). */
+lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64_t ldx,
+                              float *Y, int64_t ldy, int64_t F,
+                              const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
+                              void *stream);
+
 /* Same, bf16 storage (uint16 bit patterns) with fp32 accumulation; the
  * accumulated row is rounded to bf16 once (round-to-nearest-even). */
 lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,

@@ -386,7 +386,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3(X3Args a) {
 // one logical chunk land in 16 distinct bank slots).  Each wave owns
 // (TM x TN) fragments of 16 x 16; output map col = lane & 15,
 // row = 4 (lane >> 4) + r.
-template <int WM, int WN, int TM, int TN, bool RELU, bool PROBE = false>
+// HEADS: the fused-heads epilogue (lpg_fc_x3_heads_f32) is compiled only into the instantiations that
+// use it, so the plain FC and input-gradient GEMMs carry none of its registers.
+template <int WM, int WN, int TM, int TN, bool RELU, bool PROBE = false, bool HEADS = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
@@ -551,21 +553,25 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
         }
     }
   }
-  float hs[4][TM][4];  // fused heads: this lane's partial logits [head][i][r]
+  float hs[HEADS ? 4 : 1][TM][4];  // fused heads: this lane's partial logits [head][i][r]
+  if constexpr (HEADS) {
 #pragma unroll
-  for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) hs[c][i][r] = 0.f;
+        for (int r = 0; r < 4; ++r) hs[c][i][r] = 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int64_t col = nw + j * 16 + fr;
     if (col >= a.N) continue;
     const float bb = a.bias ? a.bias[col] : 0.f;
-    float hwv[4];
+    float hwv[HEADS ? 4 : 1];
+    if constexpr (HEADS) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) hwv[c] = (a.hw && c < a.hn) ? a.hw[c * a.ldhw + col] : 0.f;
+      for (int c = 0; c < 4; ++c) hwv[c] = c < a.hn ? a.hw[c * a.ldhw + col] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -577,14 +583,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
         if (RELU) v = (v < 0.f) ? 0.f : v;
         if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         a.C[row * a.ldc + col] = v;
-        if (a.hw) {
+        if constexpr (HEADS) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
         }
       }
     }
   }
-  if (a.hw) {  // sum over the 16 lanes (columns) of each row group, fixed DPP order; lane fr = 0 writes
+  if constexpr (HEADS) {  // sum over the 16 lanes (columns) of each row group, fixed DPP order; lane fr = 0 writes
     const int64_t pidx = nw / (TN * 16);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -622,7 +628,7 @@ __global__ __launch_bounds__(256) void heads_fold(int64_t M, int64_t nparts, int
   logits[m * ldl + c] = v;
 }
 
-template <int WM, int WN, int TM, int TN, bool PROBE = false>
+template <int WM, int WN, int TM, int TN, bool PROBE = false, bool HEADS = false>
 lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16, NT = 64 * WM * WN;
   a.mt = (a.M + BM - 1) / BM;
@@ -630,9 +636,9 @@ lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, true, PROBE>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, true, PROBE, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, false, PROBE>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, false, PROBE, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -1230,6 +1236,14 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   LPG_REQUIRE(hn >= 1 && hn <= 4, "lpg_fc_x3_heads_f32: %d heads outputs not in [1, 4]", (int)hn);
   LPG_REQUIRE(hw && ldhw >= N && logits && ldl >= hn, "lpg_fc_x3_heads_f32: bad head weight / logits");
   LPG_REQUIRE(workspace && aligned16(workspace), "lpg_fc_x3_heads_f32: workspace missing or not 16-byte aligned");
+  // the heads epilogue lives in the 16x16x32 kernel <4,1,2,8> (variants 0, 10, 11); its C equals
+  // lpg_fc_x3_f32's bit for bit under every 16x16x32 variant (one MFMA shape, one k order), not
+  // under the 32x32x16 ones: those report "unsupported" and the caller runs FC + a separate Linear
+  if (g_x3_variant == 1 || g_x3_variant == 2 || g_x3_variant == 3 || g_x3_variant == 4 || g_x3_variant == 8 ||
+      g_x3_variant == 99) {
+    set_error("lpg_fc_x3_heads_f32: x3 variant %d (32x32x16 MFMA / probe) has no fused heads", (int)g_x3_variant);
+    return LPG_ERR_UNSUPPORTED;
+  }
   X3Args a;
   const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
                                 dropout_p, seed, &a);
@@ -1240,7 +1254,7 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   a.hpart = reinterpret_cast<float *>(workspace);
   a.xmap = g_x3_variant == 11 && (N + 127) / 128 == 8;
   hipStream_t s = as_stream(stream);
-  const lpg_status r = launch_x3_16<4, 1, 2, 8>(a, flags & 1, s);  // 32 x 128 wave tiles: N / 128 partials
+  const lpg_status r = launch_x3_16<4, 1, 2, 8, false, true>(a, flags & 1, s);  // 32 x 128 wave tiles: N / 128 partials
   if (r != LPG_OK) return r;
   const int64_t nparts = (N + 127) / 128;
   hipLaunchKernelGGL(heads_fold, dim3((unsigned)((M * hn + 255) / 256)), dim3(256), 0, s, M, nparts, hn,

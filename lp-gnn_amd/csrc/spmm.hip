@@ -42,16 +42,87 @@ __device__ __forceinline__ void axpy4(float4 &acc, float v, const float4 &x) {
   acc.w = acc.w + v * x.w;
 }
 
+// Heavy rows (degree > thresh; SpMM skew, e.g. a dense LP constraint): one block per heavy row
+// and column slice, its 4 waves on interleaved 64-column pieces (lane l of wave w holds columns
+// c0 + 256 q + 64 w + l, q < NV: one float per lane, every gather a contiguous 256 B), HU edges
+// gathered ahead.  The row's chain is split over 4x the waves of a (row, slice) wave, every
+// element still summed over the row's edges in CSR order (bitwise the same result), so a
+// 6 000-edge row no longer sets the kernel's tail.
+struct HeavyRows {
+  const int32_t *rows;  // heavy row ids (rows with degree > thresh)
+  int64_t blocks;       // = number of heavy rows: the leading blocks of every y plane
+  int64_t thresh;       // the main waves skip rows with more edges than this
+};
+
+template <int NV, int HU>
+__device__ __forceinline__ void spmm_f32_heavy_row(int64_t row, int64_t c0, int wave,
+                                                   const int64_t *__restrict__ rowptr,
+                                                   const int32_t *__restrict__ col, const float *__restrict__ val,
+                                                   const float *__restrict__ X, int64_t ldx, float *__restrict__ Y,
+                                                   int64_t ldy, int64_t F) {
+  const int lane = threadIdx.x & 63;
+  const int64_t cw = c0 + wave * 64 + lane;
+  bool ok[NV];
+  float acc[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) ok[q] = cw + q * 256 < F, acc[q] = 0.f;
+  const float *Xs = X + cw;
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  while (e < end) {
+    const int n = (int)(end - e < 64 ? end - e : 64);
+    int cl = 0;
+    float vl = 0.f;
+    if (lane < n) {
+      cl = col[e + lane];
+      vl = val[e + lane];
+    }
+    int j = 0;
+    for (; j + HU <= n; j += HU) {
+      float xv[HU][NV];
+#pragma unroll
+      for (int k = 0; k < HU; ++k) {
+        const float *xr = Xs + (int64_t)bcast_i(cl, j + k) * ldx;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) xv[k][q] = ok[q] ? xr[q * 256] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < HU; ++k) {
+        const float v = bcast_f(vl, j + k);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) acc[q] = acc[q] + v * xv[k][q];
+      }
+    }
+    for (; j < n; ++j) {
+      const float *xr = Xs + (int64_t)bcast_i(cl, j) * ldx;
+      const float v = bcast_f(vl, j);
+#pragma unroll
+      for (int q = 0; q < NV; ++q) acc[q] = acc[q] + v * (ok[q] ? xr[q * 256] : 0.f);
+    }
+    e += n;
+  }
+  float *yr = Y + row * ldy + cw;
+#pragma unroll
+  for (int q = 0; q < NV; ++q)
+    if (ok[q]) yr[q * 256] = acc[q];
+}
+
 // ---------------------------------------------------------------- fp32 wide
 template <int NV, int U, bool FULL>
 __global__ __launch_bounds__(kBlock) void spmm_f32_rowwave(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
-    float *__restrict__ Y, int64_t ldy, int64_t F) {
+    float *__restrict__ Y, int64_t ldy, int64_t F, HeavyRows hv) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if ((int64_t)blockIdx.x < hv.blocks) {  // heavy rows first: dispatched at the head of each plane
+    spmm_f32_heavy_row<NV, 16>(hv.rows[blockIdx.x], (int64_t)blockIdx.y * (NV * 256), wave, rowptr, col, val, X,
+                               ldx, Y, ldy, F);
+    return;
+  }
+  const int64_t row = ((int64_t)blockIdx.x - hv.blocks) * kWavesPerBlock + wave;
   if (row >= n_rows) return;
+  if (rowptr[row + 1] - rowptr[row] > hv.thresh) return;  // a heavy row: done by the units above
   const int64_t c0 = (int64_t)blockIdx.y * (NV * 256);
 
   bool ok[NV];
@@ -289,15 +360,17 @@ lpg_status launch(K kernel, dim3 grid, hipStream_t s, Args... args) {
 
 template <int NV, int U>
 lpg_status launch_wide_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
-                           int64_t F, hipStream_t s) {
+                           int64_t F, hipStream_t s, HeavyRows hv) {
   const int64_t W = NV * 256;
   const int64_t slices = (F + W - 1) / W;
-  dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock), (unsigned)slices);
+  const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock + hv.blocks;
+  LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_f32: grid too large");
+  dim3 grid((unsigned)nblk, (unsigned)slices);
   if (F % W == 0)
     return launch(spmm_f32_rowwave<NV, U, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
-                  Y, ldy, F);
+                  Y, ldy, F, hv);
   return launch(spmm_f32_rowwave<NV, U, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y,
-                ldy, F);
+                ldy, F, hv);
 }
 
 template <int FW>
@@ -340,8 +413,8 @@ extern "C" lpg_status lpg_spmm_set_depth(int64_t edges) {
   return LPG_OK;
 }
 
-extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
-                                   int64_t F, void *stream) {
+static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                                HeavyRows hv, void *stream) {
   lpg_status st = check_csr(A);
   if (st != LPG_OK) return st;
   LPG_REQUIRE(F >= 0, "lpg_spmm_f32: F < 0");
@@ -373,15 +446,29 @@ extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx
   if (W == 0) W = 256;
   const int U = g_depth == 0 ? 8 : g_depth;
   if (W == 256) {
-    if (U == 16) return launch_wide_f32<1, 16>(A, X, ldx, Y, ldy, F, s);
-    if (U == 32) return launch_wide_f32<1, 32>(A, X, ldx, Y, ldy, F, s);
-    return launch_wide_f32<1, 8>(A, X, ldx, Y, ldy, F, s);
+    if (U == 16) return launch_wide_f32<1, 16>(A, X, ldx, Y, ldy, F, s, hv);
+    if (U == 32) return launch_wide_f32<1, 32>(A, X, ldx, Y, ldy, F, s, hv);
+    return launch_wide_f32<1, 8>(A, X, ldx, Y, ldy, F, s, hv);
   }
   if (W == 512) {
-    if (U == 16) return launch_wide_f32<2, 16>(A, X, ldx, Y, ldy, F, s);
-    return launch_wide_f32<2, 8>(A, X, ldx, Y, ldy, F, s);
+    if (U == 16) return launch_wide_f32<2, 16>(A, X, ldx, Y, ldy, F, s, hv);
+    return launch_wide_f32<2, 8>(A, X, ldx, Y, ldy, F, s, hv);
   }
-  return launch_wide_f32<4, 4>(A, X, ldx, Y, ldy, F, s);
+  return launch_wide_f32<4, 4>(A, X, ldx, Y, ldy, F, s, hv);
+}
+
+extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                                   int64_t F, void *stream) {
+  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX}, stream);
+}
+
+extern "C" lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                                         int64_t F, const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
+                                         void *stream) {
+  LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_f32_heavy: negative n_heavy / thresh");
+  LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_f32_heavy: heavy_rows is NULL");
+  LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_f32_heavy: more heavy rows than rows");
+  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX}, stream);
 }
 
 extern "C" lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,

@@ -26,6 +26,7 @@ HEADER_SYMBOLS = (
     "lpg_csr_pack_workspace_bytes",
     "lpg_csr_pack_f32",
     "lpg_spmm_f32",
+    "lpg_spmm_f32_heavy",
     "lpg_spmm_bf16",
     "lpg_spmm_set_slice",
     "lpg_spmm_set_depth",
@@ -95,6 +96,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_csr_pack_f32.restype = c_i32
     L.lpg_spmm_f32.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p]
     L.lpg_spmm_f32.restype = c_i32
+    L.lpg_spmm_f32_heavy.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p]
+    L.lpg_spmm_f32_heavy.restype = c_i32
     L.lpg_spmm_bf16.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p]
     L.lpg_spmm_bf16.restype = c_i32
     L.lpg_spmm_set_slice.argtypes = [c_i64]

@@ -166,6 +166,9 @@ def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=
                                    None if bh is None else bh.data_ptr(), logits.data_ptr(), logits.stride(0),
                                    ws.data_ptr(), _lib.stream_of(A1))
         TIMER.stop(tok)
+    if st == 3:  # a 32x32x16 x3 variant is selected: no fused heads there -- the FC, then a separate Linear
+        C = _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s, W2s)
+        return C, _fc_forward(C, heads[0], None, None, heads[1], False, arith="x3")
     _lib.check(st, "lpg_fc_x3_heads_f32")
     return C, logits
 

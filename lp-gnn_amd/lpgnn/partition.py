@@ -495,10 +495,11 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
     ex.start_broadcast_(right_new).finish()
     logits = None
     if heads is not None:
+        # halo rows are copies of other ranks' variables: their logits are the OWNERS' logits, broadcast
+        # (3 floats a row) rather than recomputed -- bitwise the owner's values, and no GEMM over the halo
         logit_r = torch.empty((right_new.shape[0], hr[0].shape[0]), dtype=torch.float32, device=left.device)
         logit_r[:n_own] = own[1]
-        if right_new.shape[0] > n_own:  # halo rows: copies of other ranks' outputs
-            logit_r[n_own:] = _fc.fc_forward(right_new[n_own:], hr[0], None, None, hr[1], False)
+        ex.start_broadcast_(logit_r).finish()
         logits = (logit_l, logit_r)
     ctx.padj, ctx.relu = padj, relu
     ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0

@@ -18,6 +18,7 @@ There is no CPU path: a CPU tensor raises.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -60,6 +61,16 @@ class CSR:
 
     def degrees(self) -> torch.Tensor:
         return self.rowptr[1:] - self.rowptr[:-1]
+
+    def heavy_rows(self, thresh: int):
+        """(int32 device tensor of the rows with more than `thresh` edges,
+        their count) -- computed once per CSR and threshold (one host sync at
+        the graph's first SpMM, none per layer)."""
+        cache = self.__dict__.setdefault("_heavy", {})
+        if thresh not in cache:
+            idx = torch.nonzero(self.degrees() > thresh).view(-1).to(torch.int32)
+            cache[thresh] = (idx, int(idx.numel()))
+        return cache[thresh]
 
 
 class BipartiteCSR:
@@ -159,6 +170,10 @@ class BipartiteCSR:
         return cls(CSR(a_rp, a_c, a_v, m, n), CSR(at_rp, at_c, at_v, n, m))
 
 
+# rows with more edges than this run as (row, 64-column) wave units (lpg_spmm_f32_heavy); 0 = off
+HEAVY_THRESH = int(os.environ.get("LPGNN_SPMM_HEAVY", "1024"))
+
+
 def spmm_forward(adj: CSR, x: torch.Tensor) -> torch.Tensor:
     """Y = adj @ x on the GPU (no autograd).  fp32 or bf16 storage."""
     if x.device.type != "cuda" or adj.device != x.device:
@@ -171,8 +186,13 @@ def spmm_forward(adj: CSR, x: torch.Tensor) -> torch.Tensor:
     Fd = x.shape[1]
     y = torch.empty((adj.n_rows, Fd), dtype=x.dtype, device=x.device)
     L = _lib.lib()
+    heavy = None
     if x.dtype == torch.float32:
         fn, name = L.lpg_spmm_f32, "lpg_spmm_f32"
+        if Fd >= 256 and HEAVY_THRESH > 0:
+            heavy = adj.heavy_rows(HEAVY_THRESH)
+            if heavy[1] == 0:
+                heavy = None
     elif x.dtype == torch.bfloat16:
         fn, name = L.lpg_spmm_bf16, "lpg_spmm_bf16"
     else:
@@ -180,7 +200,12 @@ def spmm_forward(adj: CSR, x: torch.Tensor) -> torch.Tensor:
     with torch.cuda.device(x.device):
         stream = _lib.stream_of(x)
         tok = TIMER.start(("spmm", adj.n_rows, adj.n_cols, Fd, str(x.dtype)))
-        st = fn(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), Fd, stream)
+        if heavy is None:
+            st = fn(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), Fd, stream)
+        else:  # degree-aware: rows above the threshold on 64-column waves (same per-element order)
+            name = "lpg_spmm_f32_heavy"
+            st = L.lpg_spmm_f32_heavy(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(),
+                                      y.stride(0), Fd, heavy[0].data_ptr(), heavy[1], HEAVY_THRESH, stream)
         TIMER.stop(tok)
     _lib.check(st, name)
     return y

@@ -73,9 +73,67 @@ def _worker(rank, world, port, out_dir, backend):
         assert abs(tot.item() - rloss) < 1e-3 * max(1.0, abs(rloss))
         for k, p in model.named_parameters():
             np.testing.assert_allclose(p.grad.cpu().numpy(), rgrads[k].numpy(), rtol=5e-3, atol=5e-5, err_msg=k)
+        _check_halo_logits_are_owners(plan, lv, world)
         open(os.path.join(out_dir, f"ok{rank}"), "w").write(str(tot.item()))
     finally:
         dist.destroy_process_group()
+
+
+def _check_halo_logits_are_owners(plan, lv, world):
+    """Every halo row's logits are bit for bit its owner's (broadcast, not recomputed)."""
+    mine = (plan.local_vars, plan.n_own, lv.numpy())
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    owner_row = {}
+    for r, (lvars, n_own, logits) in enumerate(every):
+        for j in range(n_own):
+            owner_row[int(lvars[j])] = logits[j]
+    halo = plan.local_vars[plan.n_own:]
+    got = lv.numpy()[plan.n_own:]
+    for k, v in enumerate(halo):
+        assert np.array_equal(got[k], owner_row[int(v)]), int(v)
+
+
+def _worker_dropout(rank, world, port, out_dir):
+    """The partitioned last layer + heads with training dropout: heads fused
+    into the FC epilogue vs a separate Linear, same dropout seeds -> same loss
+    and gradients (the single-GPU test_fused_heads_node_equals_separate_heads
+    on a partition)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lpgnn import GCN_FC, conv, partition as part
+
+        g = _graph()
+        plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
+        batch = part.make_local_batch(plan, g.x_s, g.x_t, g.y_s, g.y_t, device="cuda:0")
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=256, depth=4, dp=0.1).to("cuda:0").train()
+        out = {}
+        for fuse in (True, False):
+            conv.FUSE_HEAD_FWD = fuse
+            model.zero_grad()
+            torch.manual_seed(123)  # same dropout seeds
+            lc, lv = model(batch)
+            loss = part.balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.n_own)
+            loss.backward()
+            part.all_reduce_grads(model)
+            out[fuse] = (loss.item(), lv.detach()[:plan.n_own].clone(),
+                         {k: p.grad.clone() for k, p in model.named_parameters()})
+        conv.FUSE_HEAD_FWD = True
+        assert abs(out[True][0] - out[False][0]) < 1e-5
+        torch.testing.assert_close(out[True][1], out[False][1], rtol=1e-5, atol=1e-5)
+        for k, v in out[True][2].items():
+            torch.testing.assert_close(v, out[False][2][k], rtol=1e-4, atol=1e-6, msg=k)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_partitioned_fused_heads_with_dropout(tmp_path):
+    mp.spawn(_worker_dropout, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
 
 
 def test_two_ranks_one_gpu_gloo(tmp_path):

@@ -1,0 +1,77 @@
+"""The run_exp / validation driver (lpgnn.run, train.py:55-157, val.py:43-68)
+with the real GCN_FC on the HIP path: a 2-epoch run on synthetic .pk LPs
+(one of them above the edge threshold, so it trains through the k-hop
+NeighborLoader), checkpoint compatibility with the reference's key set,
+the per-epoch LR schedule, validation, and the 16-bit (--fp16) route."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_ref as O
+from tests.test_run import write_dataset
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(tmp_path, *extra):
+    from lpgnn import run
+
+    a = run.parse_args(["train", "--arch", "GCN_FC(8,8,hids=64,depth=3)", "--dataset", "synth", "--data_prefix",
+                        str(tmp_path / "data"), "--log_prefix", str(tmp_path / "runs"), "--epochs", "2",
+                        "--edge_num_thresh", "700", "--batch_size", "64", *extra])
+    return a
+
+
+def test_run_exp_two_epochs_checkpoint_and_validation(tmp_path):
+    from lpgnn import GCN_FC, run
+
+    # graphs of 600, 500, 800 (> threshold 700: NeighborLoader path) and 400 edges
+    write_dataset(str(tmp_path / "data" / "synth" / "highs-inp_tgt"), k=4)
+    args = _args(tmp_path)
+    ds = run.LPDataset(args.dataset_processed_prefix, thresh_num=args.edge_num_thresh, device=args.dev)
+    tr, va = run.split_train_val(ds)
+    assert [os.path.basename(tr.path(i)) for i in range(len(tr))] == ["lp2.pk", "lp3.pk"]  # seed-0 70/30 split
+    hist = run.run_exp(args)
+    assert hist["lr"] == [1e-3, 1e-4]
+    assert all(np.isfinite(hist["epoch_loss"]))
+    # lp2 (800 edges) went through the sampler in mini-batches of 64 seeds: more steps than graphs
+    assert hist["steps"] > 2 * 2
+    ck = torch.load(hist["checkpoint"], map_location="cpu", weights_only=True)
+    ref = O.init_state_dict(8, 8, 64, 3)
+    assert list(ck.keys()) == list(ref.keys()) and all(ck[k].shape == ref[k].shape for k in ref)
+    # --load_from + validation (full graph and k-hop every-neighbour inference)
+    vargs = _args(tmp_path, "--load_from", hist["checkpoint"])
+    model = run.make_model(vargs)
+    for k, v in ck.items():
+        assert torch.equal(model.state_dict()[k].cpu(), v)
+    _, acc, rows = run.validation(model, ds, vargs)
+    assert 0.0 <= acc <= 1.0 and len(rows) == 4
+    # --fp16: the bf16 compute path; logits close to the fp32 model's
+    fargs = _args(tmp_path, "--load_from", hist["checkpoint"], "--fp16", "1")
+    m16 = run.make_model(fargs)
+    assert m16.compute_dtype == torch.bfloat16
+    g = ds[0].to(args.dev)
+    with torch.no_grad():
+        a = torch.cat(model.eval()(g))
+        b = torch.cat(m16.eval()(g))
+    assert b.dtype == torch.float32 and (a - b).abs().mean().item() < 0.05
+
+
+def test_half_model_or_batch_is_refused():
+    """val.py:269 model.half() / batch_to(half=True): no fp16 kernels here --
+    a clear error instead of a silent fp32 run."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, batch_to, synth
+
+    g = synth.uniform_lp(50, 80, 400, seed=1)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda:0")
+    b = BipartiteBatch(x_s=torch.from_numpy(g.x_s), x_t=torch.from_numpy(g.x_t), y_s=torch.from_numpy(g.y_s),
+                       y_t=torch.from_numpy(g.y_t), edge_index=adj, s_bs=g.m, t_bs=g.n)
+    model = GCN_FC(8, 8, hids=32, depth=3).cuda().eval()
+    with pytest.raises(TypeError, match="float16"):
+        model(batch_to(b, "cuda:0", half=True))
+    b = batch_to(BipartiteBatch(x_s=torch.from_numpy(g.x_s), x_t=torch.from_numpy(g.x_t), y_s=torch.from_numpy(g.y_s),
+                                y_t=torch.from_numpy(g.y_t), edge_index=adj, s_bs=g.m, t_bs=g.n), "cuda:0")
+    with pytest.raises(TypeError, match="float16"):
+        model.half()(b)

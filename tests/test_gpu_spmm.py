@@ -241,3 +241,38 @@ def test_direct_bipartite_device_pack_equals_reference_chain():
         ca, cb = getattr(a.edge_index, o), getattr(b.edge_index, o)
         for f in ("rowptr", "col", "val"):
             assert torch.equal(getattr(ca, f), getattr(cb, f)), (o, f)
+
+
+@pytest.mark.parametrize("thresh", [0, 3, 64, 1024])
+@pytest.mark.parametrize("Fd,slice_cols", [(1024, 0), (1000, 0), (512, 512), (2048, 1024), (300, 0)])
+def test_degree_aware_heavy_rows_bitwise(thresh, Fd, slice_cols, monkeypatch):
+    """lpg_spmm_f32_heavy on a Zipf(1.5) skewed LP (rows up to thousands of
+    edges, many of degree 1, empty rows): rows above the threshold run as
+    64-column wave units, the rest as usual -- both directions bitwise the
+    torch_sparse spmm_cpu loop, for every threshold (0 = every non-empty row
+    heavy), ragged F and every slice width."""
+    from lpgnn import _lib, sparse, synth
+    from lpgnn.sparse import spmm_forward
+
+    monkeypatch.setattr(sparse, "HEAVY_THRESH", thresh)
+    g = synth.skewed_lp(3000, 5000, 60000, seed=11)
+    row = np.concatenate([g.row, np.full(4000, 7, np.int64)])  # row 7: a dense constraint (4000 extra edges)
+    col = np.concatenate([g.col, np.arange(1000, 5000, dtype=np.int64)])
+    key = np.unique(row * g.n + col)
+    row, col = key // g.n, key % g.n
+    val = np.random.default_rng(2).uniform(-1, 1, len(row)).astype(np.float32)
+    adj = _adj(row, col, val, g.m, g.n)
+    A, AT = _oracle_pair(row, col, val, g.m, g.n)
+    assert adj.fwd.degrees().max().item() > 4000
+    rng = np.random.default_rng(Fd)
+    L = _lib.lib()
+    try:
+        _lib.check(L.lpg_spmm_set_slice(slice_cols), "set_slice")
+        for csr, ref, n_src in ((adj.fwd, A, g.n), (adj.bwd, AT, g.m)):
+            X = rng.standard_normal((n_src, Fd)).astype(np.float32)
+            got = spmm_forward(csr, torch.from_numpy(X).to(DEV)).cpu().numpy()
+            assert np.array_equal(got, O.spmm_f32(*ref, X))
+            if thresh < 1024:
+                assert csr.heavy_rows(thresh)[1] > 0
+    finally:
+        L.lpg_spmm_set_slice(0)

@@ -161,6 +161,33 @@ def test_x3_fused_heads_match_separate_linear(M, N, K, hn, accum, drop):
     torch.testing.assert_close(lg, fc_forward(y0, Wh, None, None, bh, False), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("variant", [0, 5, 6, 9, 10, 11, 1, 2, 8])
+def test_x3_fused_heads_under_every_variant(variant):
+    """The fused-heads C equals lpg_fc_x3_f32's C under whatever x3 variant is
+    selected: the 16x16x32 variants share the heads kernel's MFMA shape and k
+    order (bitwise), the 32x32x16 ones make the heads path fall back to the FC
+    plus a separate Linear (again the variant's own C)."""
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward
+
+    g = torch.Generator().manual_seed(variant)
+    M, N, K = 1000, 1024, 256
+    A = torch.relu(torch.randn(M, K, generator=g)).to(DEV)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    Wh = (torch.randn(3, N, generator=g) * 0.1).to(DEV)
+    bh = torch.randn(3, generator=g).to(DEV)
+    L = _lib.lib()
+    try:
+        _lib.check(L.lpg_fc_x3_set_variant(variant), "set_variant")
+        y0 = fc_forward(A, W, None, None, b, True, arith="x3")
+        y, lg = fc_forward(A, W, None, None, b, True, arith="x3", heads=(Wh, bh))
+    finally:
+        L.lpg_fc_x3_set_variant(0)
+    assert torch.equal(y, y0)
+    torch.testing.assert_close(lg, fc_forward(y0, Wh, None, None, bh, False), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("relu", [False, True])
 def test_x3_accumulate(relu):
     """flags bit 1: C = act(A W^T + C + b), the addend read before the store."""
