@@ -272,7 +272,7 @@ def test_degree_aware_heavy_rows_bitwise(thresh, Fd, slice_cols, monkeypatch):
             X = rng.standard_normal((n_src, Fd)).astype(np.float32)
             got = spmm_forward(csr, torch.from_numpy(X).to(DEV)).cpu().numpy()
             assert np.array_equal(got, O.spmm_f32(*ref, X))
-            if thresh < 1024:
+            if thresh < csr.degrees().max().item():  # the heavy path actually ran in this direction
                 assert csr.heavy_rows(thresh)[1] > 0
     finally:
         L.lpg_spmm_set_slice(0)
