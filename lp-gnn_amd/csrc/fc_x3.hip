@@ -85,11 +85,20 @@ __device__ __forceinline__ unsigned pk_bf16(float x, float y) {  // v_cvt_pk_bf1
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x, y}, bf16x2));
 }
 
+// exact residual x - h as one v_sub_f32: kept out of the SLP vectorizer's reach, which paired
+// the two subtractions of a level into v_pk_add_f32 -- an issue-cost anti-lever beside MFMAs
+// (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
+__device__ __forceinline__ float sub_f32(float x, float h) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(h));
+  return r;
+}
+
 // one split level of a pair: the packed RNE bf16 terms; the exact residuals are left in x, y
 __device__ __forceinline__ unsigned split_lvl(float &x, float &y) {
   const unsigned p = pk_bf16(x, y);
-  x = x - __uint_as_float(p << 16);
-  y = y - __uint_as_float(p & 0xffff0000u);
+  x = sub_f32(x, __uint_as_float(p << 16));
+  y = sub_f32(y, __uint_as_float(p & 0xffff0000u));
   return p;
 }
 
@@ -639,6 +648,270 @@ lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
     hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, true, PROBE, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   else
     hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, false, PROBE, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+// 16 B per lane, buffer_load_dwordx4 ... lds into M0 = lds (lane-linear): the descriptor over
+// [p, p + n) is built from readfirstlane'd values, so it stays in SGPRs (a select between two
+// descriptors went to VGPRs and turned every load into a waterfall loop); the lane offset is
+// voff, the step soff (scalar); offsets at or past n read zeros
+__device__ __forceinline__ void dma16(uint64_t p, uint32_t n, unsigned char *lds, uint32_t voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(3))) void lds_v;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_v *)lds, 16, voff, soff, 0, 0);
+#endif
+}
+
+// ---- wide strips: fc_x3_wide (variants 12-15; the default) --------------------
+//
+// fc_fwd_x3_16 splits every A element once per block, so the split VALU per MFMA falls only as
+// the block's N width grows; and its stage() spent ~6 VALU per LDS-DMA piece on 64-bit address
+// arithmetic and phase selects (60 per k-tile, beside 88 of split).  fc_x3_wide: WM waves
+// stacked along M, each owning a 16 x BN strip (BN = 16 TN): one A fragment split per k-tile
+// feeds 6 TN MFMAs (TN = 16: 96).  Every DMA piece is a buffer_load ... lds through a
+// descriptor per operand and phase (wave-uniform SGPRs), the lane's offset fixed for the whole
+// loop and the k step in the scalar offset: no VALU per load, LDS destinations in M0 from SGPRs.
+// Rows/columns past the edge are clamped (their outputs are never stored).  Same MFMA shape,
+// k order and product sequence per output as fc_fwd_x3_16: the same C, bit for bit.
+// Requires lda1 == lda2, ldw1 == ldw2, ps1 == ps2 (one offset set for both k phases; the host
+// falls back to fc_fwd_x3_16 otherwise).
+template <int WM, int TM, int TN, int MINW, bool RELU, bool HEADS>
+__global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
+  constexpr int NW = WM;
+  constexpr int BM = WM * TM * 16, BN = TN * 16;
+  constexpr int A_BYTES = BM * BK * 4, WP_BYTES = BN * BK * 2;
+  constexpr int TILE_BYTES = A_BYTES + 3 * WP_BYTES;
+  // DMA pieces of 1 KiB (one wave instruction): A pieces (8 rows x 128 B) first, then the W
+  // pieces (16 rows x 64 B, plane by plane) -- piece q lands at q * 1 KiB of the tile image;
+  // wave w moves pieces w, w + NW, ... (the last round partial when NW does not divide PT)
+  constexpr int PA_T = BM / 8, PT = PA_T + 3 * (BN / 16), PPW = (PT + NW - 1) / NW;
+  static_assert(BM % 8 == 0 && BN % 16 == 0, "whole pieces");
+  static_assert(TN % 2 == 0, "W fragments are consumed in pairs");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
+
+  const int64_t nwg = a.mt * a.nt;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
+  const int64_t m0 = (wgid / a.nt) * BM;
+  const int64_t n0 = (wgid % a.nt) * BN;
+  const int64_t mrows = a.M - m0 < BM ? a.M - m0 : BM;  // rows of this block (>= 1)
+  const int64_t ncols = a.N - n0 < BN ? a.N - n0 : BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nk1 = (int)(a.K1 / BK);
+  const int nk = nk1 + (int)(a.K2 / BK);
+
+  // descriptors: A from row m0, W from column n0 (plane p at + p * ps); ranges cover exactly the
+  // bytes the block reads, so a stray offset reads zeros instead of faulting (dma16)
+  const int64_t kp1 = a.K1 > 0 ? a.K1 : BK, kp2 = a.K2 > 0 ? a.K2 : BK;
+  const uint64_t pa1 = (uint64_t)(a.A1 + m0 * a.lda1), pw1 = (uint64_t)(a.W1 + n0 * a.ldw1);
+  const uint64_t pa2 = a.A2 ? (uint64_t)(a.A2 + m0 * a.lda1) : pa1, pw2 = a.W2 ? (uint64_t)(a.W2 + n0 * a.ldw1) : pw1;
+  const uint32_t na1 = (uint32_t)(((mrows - 1) * a.lda1 + kp1) * 4), na2 = (uint32_t)(((mrows - 1) * a.lda1 + kp2) * 4);
+  const uint32_t nw1 = (uint32_t)((2 * a.ps1 + (ncols - 1) * a.ldw1 + kp1) * 2);
+  const uint32_t nw2 = (uint32_t)((2 * a.ps1 + (ncols - 1) * a.ldw1 + kp2) * 2);
+  uint32_t vo[PPW];
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) {
+    const int q = wave + NW * p;
+    if (q < PA_T) {
+      const int row = q * 8 + (lane >> 3);
+      const int64_t rc = row < mrows ? row : mrows - 1;  // rows past M feed outputs that are never stored
+      vo[p] = (uint32_t)((rc * a.lda1 + swzA(row, lane & 7) * 4) * 4);
+    } else {
+      const int qw = q < PT ? q - PA_T : 0, plane = qw / (BN / 16);
+      const int row = (qw % (BN / 16)) * 16 + (lane >> 2);
+      const int64_t rc = row < ncols ? row : ncols - 1;
+      vo[p] = (uint32_t)((plane * a.ps1 + rc * a.ldw1 + swzW(row, lane & 3) * 8) * 2);
+    }
+  }
+  auto stage = [&](int b, int t) {
+    const bool p2 = t >= nk1;
+    const int kk = p2 ? t - nk1 : t;
+    const uint64_t pa = p2 ? pa2 : pa1, pw = p2 ? pw2 : pw1;
+    const uint32_t na = p2 ? na2 : na1, nw = p2 ? nw2 : nw1;
+    unsigned char *base = smem + b * TILE_BYTES;
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) {
+      const int q = wave + NW * p;  // wave-uniform
+      if (PT % NW == 0 || q < PT) {
+        if (q < PA_T)
+          dma16(pa, na, base + q * 1024, vo[p], kk * (BK * 4));
+        else
+          dma16(pw, nw, base + q * 1024, vo[p], kk * (BK * 2));
+      }
+    }
+  };
+
+  f32x4 accH[TM][TN], accL[TM][TN];
+  const f32x4 zero = {};
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) accH[i][j] = accL[i][j] = zero;
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int rA0 = wave * TM * 16 + fr;
+
+  if (nk > 0) stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int b = 0;
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) stage(b ^ 1, t + 1);
+    const unsigned char *T = smem + b * TILE_BYTES;
+    Split3 av[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const unsigned char *ra = T + (rA0 + i * 16) * (BK * 4);
+      av[i] = split3(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16),
+                     *reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg + 1) * 16));
+    }
+    auto ldb = [&](int j, bf16x8(&bj)[3]) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bj[p] = *reinterpret_cast<const bf16x8 *>(T + A_BYTES + p * WP_BYTES + (j * 16 + fr) * (BK * 2) +
+                                                  swzW(j * 16 + fr, fg) * 16);
+    };
+    auto mfma6 = [&](int i, int j, const bf16x8(&bj)[3]) {
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i].l, bj[0], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i].m, bj[1], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i].h, bj[2], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i].m, bj[0], accL[i][j], 0, 0, 0);
+      accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i].h, bj[1], accL[i][j], 0, 0, 0);
+      accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i].h, bj[0], accH[i][j], 0, 0, 0);
+    };
+    // W fragments one pair ahead of the pair being multiplied
+    bf16x8 c0[3], c1[3];
+    ldb(0, c0);
+    ldb(1, c1);
+#pragma unroll
+    for (int j = 0; j < TN; j += 2) {
+      bf16x8 n0_[3], n1_[3];
+      if (j + 2 < TN) {
+        ldb(j + 2, n0_);
+        ldb(j + 3, n1_);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        mfma6(i, j, c0);
+        mfma6(i, j + 1, c1);
+      }
+      if (j + 2 < TN) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) c0[p] = n0_[p], c1[p] = n1_[p];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile t+1 landed; every wave done with tile t
+    asm volatile("" ::: "memory");
+    b ^= 1;
+  }
+
+  const int64_t mw = m0 + wave * TM * 16, nw = n0;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = accH[i][j] + accL[i][j];
+  if (a.accum) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int64_t col = nw + j * 16 + fr;
+      col = col < a.N ? col : a.N - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int64_t row = mw + i * 16 + 4 * fg + r;
+          row = row < a.M ? row : a.M - 1;
+          acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
+        }
+    }
+  }
+  float hs[HEADS ? 4 : 1][TM][4];  // fused heads: this lane's partial logits [head][i][r]
+  if constexpr (HEADS) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hs[c][i][r] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = nw + j * 16 + fr;
+    if (col >= a.N) continue;
+    const float bb = a.bias ? a.bias[col] : 0.f;
+    float hwv[HEADS ? 4 : 1];
+    if constexpr (HEADS) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) hwv[c] = c < a.hn ? a.hw[c * a.ldhw + col] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = mw + i * 16 + 4 * fg + r;
+        if (row >= a.M) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v = v + bb;
+        if (RELU) v = (v < 0.f) ? 0.f : v;
+        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        a.C[row * a.ldc + col] = v;
+        if constexpr (HEADS) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
+        }
+      }
+  }
+  if constexpr (HEADS) {  // sum over the 16 lanes (columns) of each row group, fixed DPP order; lane fr = 0 writes
+    const int64_t pidx = nw / BN;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hs[c][i][r] = c < a.hn ? sum16(hs[c][i][r]) : 0.f;
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = mw + i * 16 + 4 * fg + r;
+          if (row < a.M)
+            *reinterpret_cast<f32x4 *>(a.hpart + (pidx * a.M + row) * 4) =
+                f32x4{hs[0][i][r], hs[1][i][r], hs[2][i][r], hs[3][i][r]};
+        }
+    }
+  }
+}
+
+// whether fc_x3_wide can take these operands (one offset set for both phases, 32-bit offsets)
+bool wide_ok(const X3Args &a, int64_t BM, int64_t BN) {
+  if (a.K1 > 0 && a.K2 > 0 && (a.lda1 != a.lda2 || a.ldw1 != a.ldw2 || a.ps1 != a.ps2)) return false;
+  if (a.K1 == 0) return false;  // (the phase-1 operands carry the strides)
+  const int64_t K = a.K1 > a.K2 ? a.K1 : a.K2;
+  return (BM * a.lda1 + K) * 4 < ((int64_t)1 << 31) && (2 * a.ps1 + BN * a.ldw1 + K) * 2 < ((int64_t)1 << 31);
+}
+
+template <int WM, int TM, int TN, int MINW, bool HEADS = false>
+lpg_status launch_x3_wide(X3Args a, bool relu, hipStream_t s) {
+  constexpr int BM = WM * TM * 16, BN = TN * 16, NT = 64 * WM;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int64_t nwg = a.mt * a.nt;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, true, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, false, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -1213,10 +1486,22 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
     case 11:  // variant 10 with the n-tile-pair XCD map (N = 1024: 8 n-tiles)
       a.xmap = (a.N + 127) / 128 == 8;
       return launch_x3_16<4, 1, 2, 8>(a, relu, s);
+    case 12: if (wide_ok(a, 128, 256)) return launch_x3_wide<8, 1, 16, 2>(a, relu, s);  // 128 x 256, 8 waves
+      break;
+    case 13: if (wide_ok(a, 128, 128)) return launch_x3_wide<8, 1, 8, 4>(a, relu, s);  // 128 x 128, 8 waves, 2/CU
+      break;
+    case 14: if (wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);  // 128 x 128, 4 waves of 32 x 128
+      break;
+    case 15: if (wide_ok(a, 256, 128)) return launch_x3_wide<8, 2, 8, 2>(a, relu, s);  // 256 x 128, 8 waves of 32 x 128
+      break;
+    case 16: if (wide_ok(a, 256, 128)) return launch_x3_wide<16, 1, 8, 4>(a, relu, s);  // 256 x 128, 16 waves
+      break;
     case 99: return launch_x3_16<4, 2, 4, 4, true>(a, relu, s);  // timing probe: no A split (WRONG results)
-    default:  // (tools/exp_x3.py at the c2 shapes: 199-212 TF/s, 5-10 % over 5 / 6)
-      return launch_x3_16<4, 1, 2, 8>(a, relu, s);
+    default:  // = 14 (tools/exp_wide.py at the c2 shapes: 207-221 TF/s, +3-6 % over fc_fwd_x3_16 = variant 10)
+      if (wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);
+      break;
   }
+  return launch_x3_16<4, 1, 2, 8>(a, relu, s);  // a wide variant that cannot take these operands
 }
 
 extern "C" int64_t lpg_fc_x3_heads_workspace_bytes(int64_t M, int64_t N) {
@@ -1254,9 +1539,21 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   a.hpart = reinterpret_cast<float *>(workspace);
   a.xmap = g_x3_variant == 11 && (N + 127) / 128 == 8;
   hipStream_t s = as_stream(stream);
-  const lpg_status r = launch_x3_16<4, 1, 2, 8, false, true>(a, flags & 1, s);  // 32 x 128 wave tiles: N / 128 partials
+  // one partial per (BN-column tile, row): N / 128 for fc_fwd_x3_16, N / 256 for the 256-wide strips
+  int64_t bn = 128;
+  lpg_status r;
+  if (g_x3_variant == 12 && wide_ok(a, 128, 256)) {
+    bn = 256;
+    r = launch_x3_wide<8, 1, 16, 2, true>(a, flags & 1, s);
+  } else if (g_x3_variant == 13 && wide_ok(a, 128, 128)) {
+    r = launch_x3_wide<8, 1, 8, 4, true>(a, flags & 1, s);
+  } else if ((g_x3_variant == 0 || g_x3_variant == 14) && wide_ok(a, 128, 128)) {
+    r = launch_x3_wide<4, 2, 8, 2, true>(a, flags & 1, s);
+  } else {
+    r = launch_x3_16<4, 1, 2, 8, false, true>(a, flags & 1, s);  // 32 x 128 wave tiles: N / 128 partials
+  }
   if (r != LPG_OK) return r;
-  const int64_t nparts = (N + 127) / 128;
+  const int64_t nparts = (N + bn - 1) / bn;
   hipLaunchKernelGGL(heads_fold, dim3((unsigned)((M * hn + 255) / 256)), dim3(256), 0, s, M, nparts, hn,
                      a.hpart, hb, logits, ldl);
   LPG_HIP(hipGetLastError());
@@ -1268,7 +1565,7 @@ extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
     g_wgrad_m16 = v - 100;
     return LPG_OK;
   }
-  LPG_REQUIRE((v >= 0 && v <= 11) || v == 99, "lpg_fc_x3_set_variant: variant %d not in [0, 11]", v);
+  LPG_REQUIRE((v >= 0 && v <= 16) || v == 99, "lpg_fc_x3_set_variant: variant %d not in [0, 16]", v);
   g_x3_variant = v;
   return LPG_OK;
 }

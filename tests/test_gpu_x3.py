@@ -97,15 +97,49 @@ def test_x3_variants_identical():
     b = torch.randn(300, generator=g).to(DEV)
     L = _lib.lib()
     outs = {}
-    for v in range(12):
+    for v in range(17):
         assert L.lpg_fc_x3_set_variant(v) == 0
         outs[v] = fc_forward(A1, W1, A2, W2, b, True, arith="x3")
     L.lpg_fc_x3_set_variant(0)
     for v in (2, 3, 4, 8):  # 32x32x16
         assert torch.equal(outs[v], outs[1]), v
-    for v in (5, 6, 7, 9, 10, 11):  # 16x16x32 (the default)
-        assert torch.equal(outs[v], outs[0]), v
+    for v in (5, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16):  # 16x16x32 (the default; lda1 != lda2 here: the
+        assert torch.equal(outs[v], outs[0]), v          # wide variants fall back to fc_fwd_x3_16)
     torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K1,K2,accum,drop", [
+    (700, 300, 128, 128, False, 0.0),   # ragged M and N tiles, both k phases
+    (37, 1024, 256, 0, True, 0.0),      # fewer rows than one tile, accumulate
+    (5000, 1024, 1024, 1024, False, 0.1),
+    (1, 130, 64, 64, False, 0.0),
+])
+def test_x3_wide_variants_bitwise(M, N, K1, K2, accum, drop):
+    """fc_x3_wide (variants 12-16; the default 0 = 14): buffer_load ... lds staging and wide wave
+    strips, the same MFMA shape, k order and product sequence per output as fc_fwd_x3_16
+    (variant 10) -- bitwise the same C, incl. ragged edges (clamped rows/columns), dropout and
+    the accumulate flag's addend."""
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward
+
+    g = torch.Generator().manual_seed(M + N + K1)
+    A1 = torch.randn(M, K1, generator=g).to(DEV)
+    A2 = torch.randn(M, K2, generator=g).to(DEV) if K2 else None
+    W1 = (torch.randn(N, K1, generator=g) * 0.05).to(DEV)
+    W2 = (torch.randn(N, K2, generator=g) * 0.05).to(DEV) if K2 else None
+    b = torch.randn(N, generator=g).to(DEV)
+    P = torch.randn(M, N, generator=g).to(DEV) if accum else None
+    L = _lib.lib()
+    outs = {}
+    try:
+        for v in (10, 0, 12, 13, 14, 15, 16):
+            _lib.check(L.lpg_fc_x3_set_variant(v), "set_variant")
+            outs[v] = fc_forward(A1, W1, A2, W2, b, True, drop, 5, out=None if P is None else P.clone(),
+                                 accumulate=accum, arith="x3")
+    finally:
+        L.lpg_fc_x3_set_variant(0)
+    for v in (0, 12, 13, 14, 15, 16):
+        assert torch.equal(outs[v], outs[10]), v
 
 
 @pytest.mark.parametrize("M", [1024, 1100, 37])
@@ -161,7 +195,7 @@ def test_x3_fused_heads_match_separate_linear(M, N, K, hn, accum, drop):
     torch.testing.assert_close(lg, fc_forward(y0, Wh, None, None, bh, False), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 5, 6, 9, 10, 11, 1, 2, 8])
+@pytest.mark.parametrize("variant", [0, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 1, 2, 8])
 def test_x3_fused_heads_under_every_variant(variant):
     """The fused-heads C equals lpg_fc_x3_f32's C under whatever x3 variant is
     selected: the 16x16x32 variants share the heads kernel's MFMA shape and k

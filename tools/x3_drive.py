@@ -7,7 +7,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "lp-gnn_amd")]
 import torch  # noqa: E402
 
+from lpgnn import _lib  # noqa: E402
 from lpgnn.fc import fc_forward  # noqa: E402
+
+_lib.check(_lib.lib().lpg_fc_x3_set_variant(int(os.environ.get("LPG_X3V", "0"))), "set_variant")
 
 arith = sys.argv[1] if len(sys.argv) > 1 else "x3"
 M = 200_000
