@@ -207,16 +207,24 @@ lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int
                             int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream);
 
 /* Tile choice for lpg_fc_x3_f32 (tuning).  On 16x16x32 MFMAs: 0 = default =
- * 10, 5 / 6 / 7 = 128 x 128 / 256 x 128 / 128 x 64 tiles of 64 x 64 (or
+ * 14, 5 / 6 / 7 = 128 x 128 / 256 x 128 / 128 x 64 tiles of 64 x 64 (or
  * 64 x 32) wave tiles, 9 / 10 = 256 x 128 / 128 x 128 tiles of 32 x 128 wave
  * tiles (each A row split by one wave only), 11 = 10 with XCD pairs sharing
- * n-tile pairs when N spans 8 tiles (N = 1024); on
+ * n-tile pairs when N spans 8 tiles (N = 1024); the fc_x3_wide kernels
+ * (buffer_load ... lds staging with the k step in the scalar offset, wave
+ * strips along N): 12 = 128 x 256 of 16 x 256 strips, 13 = 128 x 128 of
+ * 16 x 128 (2 blocks/CU), 14 = 128 x 128 of 32 x 128 (the default), 15 =
+ * 256 x 128 of 32 x 128, 16 = 256 x 128 of 16 x 128 (16 waves) -- they need
+ * lda1 == lda2, ldw1 == ldw2, ps1 == ps2 and fall back to 10 otherwise; on
  * 32x32x16 MFMAs: 1 = 256 x 128, 2 = 128 x 256, 3 / 4 = 128 x 128 / 256 x 128
  * software-pipelined, 8 = 128 x 128.  Variants on the same MFMA shape give
  * identical bits (the two shapes differ in in-instruction summation).
- * 100 / 101 / 102 / 103: the weight-gradient kernel (32x32x16 / 16x16x32 /
- * cooperative 16x16x32 with one split per element, default 102 /
- * producer-consumer form of 102; 101, 102 and 103 give identical bits).
+ * 100 .. 105: the weight-gradient kernel (100 / 101 = 32x32x16 / 16x16x32
+ * with per-wave splits, 102 = cooperative 16x16x32 with one split per element
+ * and block, 103 = producer-consumer form of 102, 104 / 105 = 256 x 128 tiles
+ * with two plane buffers, the next chunk split under the current chunk's
+ * MFMAs, 105 (the default) interleaving the split column by column; 101 .. 105
+ * give identical bits).
  * 99: a timing probe without the activation split
  * (WRONG results, measurement only). */
 lpg_status lpg_fc_x3_set_variant(int32_t v);

@@ -1257,6 +1257,158 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3c(int64_t R, int64_t N, int64_
   }
 }
 
+// Wide, split-ahead variant of wgrad_x3c (lpg_fc_x3_set_variant(104); the default): a 256 (n) x
+// 128 (k) output tile per 512-thread block (8 waves of 64 x 64, 2 x 2 waves... 4 x 2), one block
+// per CU, and TWO plane buffers (2 x 72 KiB).  wgrad_x3c splits a chunk, barriers, then
+// multiplies: both waves of a SIMD are in the same phase, so the split VALU and the MFMAs never
+// overlap.  Here chunk c + 1 is split into the other buffer in the same iteration as chunk c's
+// MFMAs (the loop is unrolled by two so the buffers are compile-time distinct and the scheduler
+// may interleave them), its global loads issued one iteration earlier; one barrier per chunk.
+// Each G element is split once per 128 k-columns and each X element once per 256 n-columns
+// (wgrad_x3c: once per 128 each): 1.37 split VALU per MFMA instead of 1.83.  Loader tasks: waves
+// 0-3 take G (64 column groups x 4 row groups), waves 4-5 X (32 x 4), waves 6-7 only multiply.
+// Same chunk ranges (the host passes wgrad_x3c's split count) and the same six products per output
+// in the same order: bitwise wgrad_x3c's partials.
+template <bool SCHED>
+__global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
+                                                    int64_t ldg, const float *__restrict__ X, int64_t ldx,
+                                                    float *__restrict__ part, int64_t nt, int64_t kt,
+                                                    int64_t chunks_per_split) {
+  constexpr int GC = 256, XC = 128;               // tile columns of G (n) and X (k)
+  constexpr int GP = GC * 32 * 2, XP = XC * 32 * 2;  // one plane image: columns x 32 rows x bf16
+  constexpr int BUFB = 3 * GP + 3 * XP;           // one buffer: G planes, then X planes (72 KiB)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB];
+
+  const int64_t nwg = (int64_t)gridDim.x, xcd = (int64_t)blockIdx.x % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t bid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (int64_t)blockIdx.x / 8;
+  const int64_t tiles = nt * kt;
+  const int64_t s = bid / tiles, tile = bid % tiles;
+  const int64_t n0 = (tile / kt) * GC, k0 = (tile % kt) * XC;
+  const int64_t nchunks = (R + 31) / 32;
+  const int64_t c0 = s * chunks_per_split;
+  const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // loader task: operand, 4 columns cg*4 .. +3, rows rg*8 .. +7 of a chunk; waves 6-7 repeat waves
+  // 4-5's X tasks (identical bytes to the same LDS addresses): every wave runs the same branch-free
+  // body, so the scheduler can interleave the split with the MFMAs, and the SIMDs hosting waves 6-7
+  // carry no more split work than the others
+  const bool isg = wave < 4;
+  const int lt = isg ? tid : (tid - 256) & 127;
+  const int cg = lt & (isg ? 63 : 31), rg = isg ? (lt >> 6) & 3 : (lt >> 5) & 3;
+  const int64_t colb = isg ? n0 : k0, lim = isg ? N : K, ld = isg ? ldg : ldx;
+  int64_t col0 = colb + cg * 4;
+  col0 = col0 < lim ? col0 : lim - 4;  // N, K multiples of 4: columns past the edge are never stored
+  // descriptor from row c0 * 32, column colb (rows past R out of range: zeros, no branch)
+  const float *sbase = (isg ? G : X) + c0 * 32 * ld + colb;
+  const int64_t left = (R - c0 * 32) * ld * 4;
+  const uint32_t nbytes = (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff);
+  const int voff = (int)((col0 - colb) * 4 + rg * 8 * ld * 4);
+  const int pl = isg ? GP : XP;  // (wave-uniform)
+  const int opoff = isg ? 0 : 3 * GP;
+  f32x4 raw[8];
+  auto load = [&](int64_t c) {  // c clamped to the last chunk: a spare re-load at the end, no branch
+    c = c < c1 ? c : c1 - 1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) raw[e] = buf_load4(sbase, nbytes, voff, (int)(((c - c0) * 32 + e) * ld * 4));
+  };
+  auto split_col = [&](unsigned char *buf, int q) {  // column cg*4 + q: its 8 rows -> three bf16x8
+    unsigned char *img = buf + opoff;
+    const Split3 t = split3(f32x4{raw[0][q], raw[1][q], raw[2][q], raw[3][q]},
+                            f32x4{raw[4][q], raw[5][q], raw[6][q], raw[7][q]});
+    const int col = cg * 4 + q;
+    unsigned char *dst = img + col * 64 + swzW(col, rg) * 16;
+    *reinterpret_cast<bf16x8 *>(dst) = t.h;
+    *reinterpret_cast<bf16x8 *>(dst + pl) = t.m;
+    *reinterpret_cast<bf16x8 *>(dst + 2 * pl) = t.l;
+  };
+  auto split_store = [&](unsigned char *buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) split_col(buf, q);
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;  // 4 (n) x 2 (k) waves of 64 x 64
+  const int fr = lane & 15, fg = lane >> 4;
+  f32x4 accH[4][4], accL[4][4];
+  const f32x4 zero = {};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accH[i][j] = accL[i][j] = zero;
+  auto frag = [&](const unsigned char *im, int plane, int col, bf16x8(&f)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8 *>(im + p * plane + col * 64 + swzW(col, fg) * 16);
+  };
+  // multiply the chunk in buf; with `next`, split column i of the next chunk (raw) into it after
+  // fragment row i's 24 MFMAs (SCHED: in source order, so the VALU lands between MFMA groups)
+  auto multiply = [&](const unsigned char *buf, unsigned char *next) {
+    bf16x8 bv[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) frag(buf + 3 * GP, XP, wn * 64 + j * 16 + fr, bv[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (SCHED && next && i > 0) split_col(next, i - 1);
+      bf16x8 av[3];
+      frag(buf, GP, wm * 64 + i * 16 + fr, av);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], bv[j][0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][1], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][2], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][1], accL[i][j], 0, 0, 0);
+        accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][0], accH[i][j], 0, 0, 0);
+      }
+    }
+    if (next) {
+      if constexpr (SCHED)
+        split_col(next, 3);
+      else
+        split_store(next);
+    }
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  unsigned char *const B0 = smem, *const B1 = smem + BUFB;
+  // prologue: chunk c0 split into B0, chunk c0 + 1's loads in flight
+  load(c0);
+  split_store(B0);
+  load(c0 + 1);
+  sync();
+  // half-iteration (chunk c in one buffer, chunk c+1's loads landed or landing): multiply it, split
+  // c+1 into the other buffer, issue c+2's loads, barrier.  Past the end the split writes B0 with a
+  // spare chunk nobody reads.
+  int64_t c = c0;
+  for (; c + 1 < c1; c += 2) {
+    multiply(B0, B1);
+    load(c + 2);
+    sync();
+    multiply(B1, B0);
+    load(c + 3);
+    sync();
+  }
+  if (c < c1) multiply(B0, nullptr);  // odd count: the last chunk sits in B0
+
+  float *P = part + s * N * K;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t col = k0 + wn * 64 + j * 16 + fr;
+    if (col >= K) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = n0 + wm * 64 + i * 16 + 4 * fg + r;
+        if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
+      }
+  }
+}
+
 // Producer/consumer variant of wgrad_x3c: 8 waves, one block per CU.  Waves
 // 0-3 multiply (wgrad_x3c's 2 x 2 wave tiles of 64 x 64); waves 4-7 load and
 // split (wgrad_x3c's tasks) the NEXT chunk into the other of two plane buffers
@@ -1415,7 +1567,7 @@ int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
 int g_x3_variant = 0;
 // lpg_fc_x3_set_variant(100 + v): wgrad kernel (0 = 32x32x16, 1 = 16x16x32, 2 = cooperative,
 // 3 = producer/consumer)
-int g_wgrad_m16 = 2;
+int g_wgrad_m16 = 5;
 
 }  // namespace
 }  // namespace lpg
@@ -1561,7 +1713,7 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
 }
 
 extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
-  if (v >= 100 && v <= 103) {
+  if (v >= 100 && v <= 105) {
     g_wgrad_m16 = v - 100;
     return LPG_OK;
   }
@@ -1599,13 +1751,23 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   float *zrow = part + S * N * K;  // 128 zero floats after the partials (lpg_wgrad_x3_workspace_bytes)
   hipStream_t st = as_stream(stream);
   LPG_HIP(hipMemsetAsync(zrow, 0, 512, st));
-  if (g_wgrad_m16 == 3)
+  if (g_wgrad_m16 >= 4 && (cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31)) {
+    const int64_t ntw = (N + 255) / 256, ktw = (K + 127) / 128;  // 256 x 128 tiles, wgrad_x3c's split count
+    const int64_t nbw = S_used * ntw * ktw;
+    LPG_REQUIRE(nbw < (int64_t)1 << 31, "lpg_wgrad_x3_f32: grid too large");
+    if (g_wgrad_m16 == 5)
+      hipLaunchKernelGGL(wgrad_x3w<true>, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw,
+                         ktw, cps);
+    else
+      hipLaunchKernelGGL(wgrad_x3w<false>, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw,
+                         ktw, cps);
+  } else if (g_wgrad_m16 == 3)
     hipLaunchKernelGGL(wgrad_x3p, dim3((unsigned)nblk), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, zrow, nt, kt,
                        cps);
-  else if (g_wgrad_m16 == 2 && (cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31))
+  else if (g_wgrad_m16 >= 2 && (cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31))
     hipLaunchKernelGGL(wgrad_x3c<true>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
                        nt, kt, S_used, cps);
-  else if (g_wgrad_m16 == 2)
+  else if (g_wgrad_m16 >= 2)
     hipLaunchKernelGGL(wgrad_x3c<false>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part,
                        zrow, nt, kt, S_used, cps);
   else if (g_wgrad_m16)

@@ -176,6 +176,11 @@ def lib() -> ctypes.CDLL:
     for nm in ("lpg_scan_i64", "lpg_sample_count", "lpg_sample_fill", "lpg_sample_dedupe", "lpg_sample_assign",
                "lpg_sample_local_ids", "lpg_induced_count", "lpg_induced_fill", "lpg_sample_reset"):
         getattr(L, nm).restype = c_i32
+    # tuning knobs for A/B runs (bench.py, tools/): the x3 FC tile variant and the weight-gradient kernel
+    for env, off in (("LPGNN_X3_VARIANT", 0), ("LPGNN_WGRAD_VARIANT", 100)):
+        if os.environ.get(env):
+            if L.lpg_fc_x3_set_variant(int(os.environ[env]) + off) != 0:
+                raise RuntimeError(f"{env}={os.environ[env]}: {L.lpg_last_error().decode()}")
     _lib = L
     return L
 

@@ -303,10 +303,12 @@ def test_wgrad_x3_accuracy_vs_fp64(R, N, K):
     (3000, 128, 128),     # T = 9 (odd), shorter last split
     (70000, 128, 64),     # T = 35, many splits
     (4096, 1024, 1024),   # hidden-layer tile grid
+    (1000, 300, 200),     # N, K not multiples of the 256 x 128 tile
 ])
 def test_wgrad_x3_kernels_bitwise_equal(R, N, K):
-    """The producer/consumer weight-gradient kernel (variant 103) forms the
-    cooperative kernel's products in the same order: identical bits."""
+    """The producer/consumer (variant 103) and the wide split-ahead weight-gradient kernels (104,
+    105: 256 x 128 tiles, two plane buffers, the host passes the cooperative kernel's split
+    count) form the cooperative kernel's products in the same order: identical bits."""
     from lpgnn import _lib
     from lpgnn.fc import wgrad
 
@@ -316,15 +318,16 @@ def test_wgrad_x3_kernels_bitwise_equal(R, N, K):
     X = torch.randn(R, K, generator=g).relu().to(DEV)
     out = {}
     try:
-        for v in (102, 103):
+        for v in (102, 103, 104, 105):
             assert L.lpg_fc_x3_set_variant(v) == 0
             out[v] = wgrad(G, X, arith="x3")
     finally:
         L.lpg_fc_x3_set_variant(100 + _DEFAULT_WGRAD)
-    assert torch.equal(out[102], out[103])
+    for v in (103, 104, 105):
+        assert torch.equal(out[102], out[v]), v
 
 
-_DEFAULT_WGRAD = 2  # csrc/fc_x3.hip g_wgrad_m16
+_DEFAULT_WGRAD = 5  # csrc/fc_x3.hip g_wgrad_m16
 
 
 def test_wgrad_x3_strided_inputs():

@@ -29,8 +29,9 @@ for R in (100_000, 200_000):
     d = (wgrad(G, X, arith="x3") - G.t() @ X).abs().max().item()
     d16 = (wg(101)() - wg(100)()).abs().max().item()
     dc = (wg(102)() - wg(101)()).abs().max().item()
-    print(f"R={R} max|coop - m16| = {dc:.3e}  pc == coop bitwise: {torch.equal(wg(103)(), wg(102)())}")
-    t = timeit({"wgrad_x3_m32": wg(100), "wgrad_x3_m16": wg(101), "wgrad_x3_coop": wg(102), "wgrad_x3_pc": wg(103),
+    print(f"R={R} max|coop - m16| = {dc:.3e}  pc == coop bitwise: {torch.equal(wg(103)(), wg(102)())}  "
+          f"wide == coop: {torch.equal(wg(104)(), wg(102)())}  wide/sched == coop: {torch.equal(wg(105)(), wg(102)())}")
+    t = timeit({"wgrad_x3_coop": wg(102), "wgrad_x3_wide": wg(104), "wgrad_x3_wsched": wg(105),
                 "wgrad_torch": lambda: G.t() @ X,
                 "igrad_x3": lambda: input_grad(G, W, arith="x3"), "igrad_torch": lambda: G @ W})
     for k, ms in t.items():
