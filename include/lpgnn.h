@@ -280,10 +280,30 @@ lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int
                        const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
                        void *stream);
 /* Tile choice for lpg_fc_bf16 (tuning/benchmarks): 0 = default (128 x 128 below
- * 4096 rows, else 256 x 256 BK 64), 1 = 128 x 128, 2 = 256 x 256 with
- * BK 64 and 2 buffers, 3 = 256 x 256 with BK 32 and 3 buffers.  All give
- * identical bits. */
+ * 4096 rows, else 7), 1 = 128 x 128, 2 = 256 x 256 with BK 64 and 2 buffers,
+ * 3 = 256 x 256 with BK 32 and 3 buffers, 4 / 5 = 256 x 256 with
+ * buffer_load ... lds staging and the barrier mid-tile, 4 / 8 waves, 6 = 5
+ * with the fragment reads and DMA placed between the MFMAs, 7 = 6 with
+ * s_setprio 1 on waves 4-7, 8 = 4 placed (4-8 need lda1 == lda2 and
+ * ldw1 == ldw2, else 2).  All give identical bits.  100-104 select the
+ * lpg_wgrad_bf16 kernel (100 / 101 = 4 / 8 waves, 102 = 101 placed (the
+ * default), 103 = 102 + s_setprio, 104 = 100 placed; identical bits). */
 lpg_status lpg_fc_bf16_set_variant(int32_t v);
+
+/* bf16 weight gradient (c5 backward, reference train.py:128 loss.backward()
+ * through GraphConv's lin_rel / lin_root): dW[n, k] = sum_r G[r, n] X[r, k],
+ * G = dZ [R, N] and X = the layer input [R, K] as bf16 bit patterns
+ * (row-major, leading dimensions ldg / ldx; N, K, ldg, ldx multiples of 8,
+ * 16-byte aligned), fp32 accumulation on v_mfma_f32_16x16x32_bf16, dW fp32
+ * [N, K] (lddw a multiple of 4, 16-byte aligned) -- the fp32 master-weight
+ * gradient, never rounded to bf16.  Replaces torch's (G^T @ X).float() on
+ * hipBLASLt (a bf16-rounded product).  R is split into contiguous ranges
+ * whose partial products go to `workspace` (lpg_wgrad_bf16_workspace_bytes
+ * bytes, 16-byte aligned; 0 bytes = not needed) and are added in range
+ * order: deterministic. */
+int64_t lpg_wgrad_bf16_workspace_bytes(int64_t R, int64_t N, int64_t K);
+lpg_status lpg_wgrad_bf16(int64_t R, int64_t N, int64_t K, const uint16_t *G, int64_t ldg, const uint16_t *X,
+                          int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream);
 
 /* Backward of a Linear with 1 <= N <= 4 outputs (the heads lin_left /
  * lin_right, arch.py:175-176, 190; torch Linear backward):

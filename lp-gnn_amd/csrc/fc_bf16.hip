@@ -57,6 +57,86 @@ __device__ __forceinline__ uint16_t to_bf16_rne(float f) {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// Epilogue shared by the bf16 FC kernels: wave `wave` owns the FM*16 x FN*16
+// output block at (wrow0, wcol0); C/D map of 16x16x32: col = lane & 15, row =
+// 4 * (lane >> 4) + r.  `smem` must be free (every wave past its last tile read).
+template <int FM, int FN, bool RELU>
+__device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[FM][FN], unsigned char *smem,
+                                              int wave, int lane, int64_t wrow0, int64_t wcol0) {
+  constexpr int EP_PITCH = FN * 16 * 2 + 16;  // epilogue image row pitch (bytes, 16-B aligned)
+  const int fr = lane & 15, fq = lane >> 4;
+  if (a.N % 8 == 0 && a.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(a.C) & 15) == 0) {
+    // Through LDS (the staging buffers are free after the last barrier): each
+    // wave writes its FM*16 x FN*16 bf16 tile row-major (padded pitch), then
+    // stores it as 16-B chunks, 8 lanes per 128-B row segment -- one
+    // global_store_dwordx4 per 8 outputs instead of one 2-byte store each.
+    unsigned char *img = smem + wave * (FM * 16 * EP_PITCH);
+    constexpr int CPR = FN * 16 / 8;  // 16-B chunks per row
+    if (a.accum) {  // the addend tile, coalesced 16-B loads into the same image
+#pragma unroll
+      for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
+        const int q = it * 64 + lane;
+        const int lr = q / CPR, ch = q % CPR;
+        const int64_t row = wrow0 + lr < a.M ? wrow0 + lr : a.M - 1, col = wcol0 + ch * 8;
+        if (col < a.N)
+          *reinterpret_cast<uint4 *>(img + lr * EP_PITCH + ch * 16) =
+              *reinterpret_cast<const uint4 *>(a.C + row * a.ldc + col);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t col = wcol0 + j * 16 + fr;
+      const float bb = (a.bias && col < a.N) ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = i * 16 + fq * 4 + r;
+          float v = acc[i][j][r];
+          if (a.accum) v = v + bf16_to_f32(*reinterpret_cast<const uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2));
+          v = v + bb;
+          if (RELU) v = v < 0.f ? 0.f : v;
+          if (a.drop_thresh) v = drop_hash(a.seed, wrow0 + lr, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+          *reinterpret_cast<uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2) = to_bf16_rne(v);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
+      const int q = it * 64 + lane;
+      const int lr = q / CPR, ch = q % CPR;
+      const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
+      const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
+      if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int64_t col = wcol0 + j * 16 + fr;
+    if (col >= a.N) continue;
+    const float bb = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = wrow0 + i * 16 + fq * 4 + r;
+        if (row >= a.M) continue;
+        float v = acc[i][j][r];
+        if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
+        v = v + bb;
+        if (RELU) v = v < 0.f ? 0.f : v;
+        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        a.C[row * a.ldc + col] = to_bf16_rne(v);
+      }
+    }
+  }
+}
+
 // WM x WN waves, each owning FM x FN fragments of 16 x 16.
 template <int WM, int WN, int FM, int FN, bool RELU>
 __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
@@ -152,78 +232,7 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
     __syncthreads();  // the DMA of tile t+1 has landed (vmcnt(0)) and every wave is done reading tile t
   }
 
-  // Epilogue: C/D map of 16x16x32: col = lane & 15, row = 4 * (lane >> 4) + r.
-  const int64_t wrow0 = m0 + wm * FM * 16, wcol0 = n0 + wn * FN * 16;
-  if (a.N % 8 == 0 && a.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(a.C) & 15) == 0) {
-    // Through LDS (the staging buffers are free after the last barrier): each
-    // wave writes its FM*16 x FN*16 bf16 tile row-major (padded pitch), then
-    // stores it as 16-B chunks, 8 lanes per 128-B row segment -- one
-    // global_store_dwordx4 per 8 outputs instead of one 2-byte store each.
-    unsigned char *img = smem + wave * (FM * 16 * EP_PITCH);
-    constexpr int CPR = FN * 16 / 8;  // 16-B chunks per row
-    if (a.accum) {  // the addend tile, coalesced 16-B loads into the same image
-#pragma unroll
-      for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
-        const int q = it * 64 + lane;
-        const int lr = q / CPR, ch = q % CPR;
-        const int64_t row = wrow0 + lr < a.M ? wrow0 + lr : a.M - 1, col = wcol0 + ch * 8;
-        if (col < a.N)
-          *reinterpret_cast<uint4 *>(img + lr * EP_PITCH + ch * 16) =
-              *reinterpret_cast<const uint4 *>(a.C + row * a.ldc + col);
-      }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int64_t col = wcol0 + j * 16 + fr;
-      const float bb = (a.bias && col < a.N) ? a.bias[col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int lr = i * 16 + fq * 4 + r;
-          float v = acc[i][j][r];
-          if (a.accum) v = v + bf16_to_f32(*reinterpret_cast<const uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2));
-          v = v + bb;
-          if (RELU) v = v < 0.f ? 0.f : v;
-          if (a.drop_thresh) v = drop_hash(a.seed, wrow0 + lr, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-          *reinterpret_cast<uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2) = to_bf16_rne(v);
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
-      const int q = it * 64 + lane;
-      const int lr = q / CPR, ch = q % CPR;
-      const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
-      const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
-      if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
-    }
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int64_t col = wcol0 + j * 16 + fr;
-    if (col >= a.N) continue;
-    const float bb = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = wrow0 + i * 16 + fq * 4 + r;
-        if (row >= a.M) continue;
-        float v = acc[i][j][r];
-        if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
-        v = v + bb;
-        if (RELU) v = v < 0.f ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-        a.C[row * a.ldc + col] = to_bf16_rne(v);
-      }
-    }
-  }
+  epilogue_bf16<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
 }
 
 // Deeper pipeline, 256 x 256 tile (8 waves, 2 x 4, 8 x 4 fragments each):
@@ -361,6 +370,401 @@ __global__ __launch_bounds__(512) void fc_fwd_bf16_p3(FcB16Args a) {
   }
 }
 
+// ---- pipelined kernel with buffer_load ... lds staging (variants 4, 5) ------
+//
+// fc_bf16_p: same tile image, fragment order and epilogue as fc_fwd_bf16, two
+// changes in the k loop.
+// (1) Staging: every 1-KiB DMA piece is a buffer_load ... lds through one
+//     descriptor per operand and phase (wave-uniform SGPRs), the lane's offset
+//     (row + swizzled chunk) fixed for the whole loop and the k step in the
+//     scalar offset -- no 64-bit address arithmetic and no row clamps per load
+//     (rows past M / N are past the descriptor's range and read zeros).
+// (2) The barrier sits in the middle of a k-tile:  read F1 (second 32-k
+//     half of tile t)  ->  MFMAs of F0  ->  barrier  ->  DMA of tile t+2 into
+//     the buffer just released  ->  read F0 of tile t+1  ->  MFMAs of F1.
+//     Every fragment read is issued one 32-k step ahead of the MFMAs that
+//     consume it (two fragment register sets), and the DMA of a tile has the
+//     MFMAs of one whole tile to land.
+// Variant 4: 4 waves of 128 x 128 (8 x 8 fragments, 256 accumulators: one
+// wave per SIMD, half the LDS fragment bytes per MFMA of the 8-wave form);
+// variant 5: 8 waves of 128 x 64 as fc_fwd_bf16.  Requires lda1 == lda2 and
+// ldw1 == ldw2 (one offset set for both k phases); the host falls back to
+// fc_fwd_bf16 otherwise.
+template <int WM, int WN, int FM, int FN, bool RELU, bool SCHED, bool PRIO>
+__global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  constexpr int A_BYTES = BM * BK * 2, TILE_BYTES = A_BYTES + BN * BK * 2;
+  constexpr int PA = BM / 8, PT = PA + BN / 8, PPW = PT / NW;  // 1-KiB pieces: A, total, per wave
+  static_assert(PA % NW == 0 && PT % NW == 0, "whole pieces per wave");
+  constexpr int EP_BYTES = NW * FM * 16 * (FN * 16 * 2 + 16);
+  constexpr int SMEM = 2 * TILE_BYTES > EP_BYTES ? 2 * TILE_BYTES : EP_BYTES;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int64_t nwg = a.mt * a.nt;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
+  const int64_t m0 = (wgid / a.nt) * BM;
+  const int64_t n0 = (wgid % a.nt) * BN;
+  const int64_t mrows = a.M - m0 < BM ? a.M - m0 : BM;
+  const int64_t ncols = a.N - n0 < BN ? a.N - n0 : BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int nk1 = (int)(a.K1 / BK);
+  const int nk = nk1 + (int)(a.K2 / BK);
+
+  // descriptors from row m0 of A / row n0 of W; a range ends after the block's last row, so the
+  // offsets of rows past M (N) -- row * ld * 2 >= (rows - 1) * ld * 2 + K * 2 -- read zeros
+  const int64_t kp1 = a.K1 > 0 ? a.K1 : BK, kp2 = a.K2 > 0 ? a.K2 : BK;
+  const uint64_t pa1 = (uint64_t)(a.A1 + m0 * a.lda1), pw1 = (uint64_t)(a.W1 + n0 * a.ldw1);
+  const uint64_t pa2 = a.A2 ? (uint64_t)(a.A2 + m0 * a.lda1) : pa1, pw2 = a.W2 ? (uint64_t)(a.W2 + n0 * a.ldw1) : pw1;
+  const uint32_t na1 = (uint32_t)(((mrows - 1) * a.lda1 + kp1) * 2), na2 = (uint32_t)(((mrows - 1) * a.lda1 + kp2) * 2);
+  const uint32_t nw1 = (uint32_t)(((ncols - 1) * a.ldw1 + kp1) * 2), nw2 = (uint32_t)(((ncols - 1) * a.ldw1 + kp2) * 2);
+  // piece q = wave + NW p: rows 8 (q mod PA) .. +7 of A (q < PA) or W; lane i lands at row
+  // 8 q' + i / 8, physical chunk i % 8, so it fetches logical chunk swz(row, i % 8)
+  uint32_t vo[PPW];
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) {
+    const int q = wave + NW * p;
+    const int row = (q < PA ? q : q - PA) * 8 + (lane >> 3);
+    vo[p] = (uint32_t)((row * (q < PA ? a.lda1 : a.ldw1) + swz(row, lane & 7) * 8) * 2);
+  }
+  // t >= nk: no tile -- the same instructions with an empty range (zeros land in a buffer nobody
+  // reads again), so the loop body stays one basic block for the scheduler
+  auto stage = [&](int b, int t) {
+    const bool ok = t < nk;
+    t = ok ? t : nk - 1;
+    const bool p2 = t >= nk1;
+    const int kk = p2 ? t - nk1 : t;
+    unsigned char *base = smem + b * TILE_BYTES;
+    const uint32_t na = ok ? (p2 ? na2 : na1) : 0u, nw = ok ? (p2 ? nw2 : nw1) : 0u;
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) {
+      const int q = wave + NW * p;  // A pieces for p < PA / NW (compile-time per p)
+      if (p < PA / NW)
+        dma16(p2 ? pa2 : pa1, na, base + q * 1024, vo[p], kk * (BK * 2));
+      else
+        dma16(p2 ? pw2 : pw1, nw, base + q * 1024, vo[p], kk * (BK * 2));
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  auto rd = [&](int b, int s, bf16x8(&av)[FM], bf16x8(&bv)[FN]) {  // 32-k step s (0, 1) of buffer b
+    const unsigned char *As = smem + b * TILE_BYTES;
+    const unsigned char *Bs = As + A_BYTES;
+    const int chunk = s * 4 + fq;  // k = 32 s + 8 fq .. +7
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * FM * 16 + i * 16 + fr;
+      av[i] = *reinterpret_cast<const bf16x8 *>(As + row * 128 + swz(row, chunk) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * FN * 16 + j * 16 + fr;
+      bv[j] = *reinterpret_cast<const bf16x8 *>(Bs + row * 128 + swz(row, chunk) * 16);
+    }
+  };
+  auto mma = [&](const bf16x8(&av)[FM], const bf16x8(&bv)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+  };
+  auto barrier = [&]() {  // this wave's DMA landed and its fragment reads returned; then all waves
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+  if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the later-dispatched half (wave-uniform)
+  if (nk > 0) {
+    stage(0, 0);
+    barrier();
+    if (nk > 1) stage(1, 1);
+    rd(0, 0, a0, b0);
+  }
+  // the last tile is peeled: inside the loop every path has the same reads in flight, so the
+  // compiler's lgkmcnt waits before mma(a1, b1) only cover a1 / b1 (with a conditional barrier the
+  // join made them wait for most of the next tile's F0 reads too)
+  constexpr int NR = FM + FN, NM = FM * FN;
+  for (int t = 0; t + 1 < nk; ++t) {
+    const int b = t & 1;
+    rd(b, 1, a1, b1);
+    mma(a0, b0);
+    if constexpr (SCHED) {  // the F1 reads one per MFMA from the top, the rest MFMAs
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+    }
+    barrier();  // tile t + 1 landed everywhere; every wave is done reading buffer b
+    stage(b, t + 2);
+    rd(b ^ 1, 0, a0, b0);
+    mma(a1, b1);
+    if constexpr (SCHED) {  // DMA pieces, then the next tile's F0 reads, one per MFMA
+#pragma unroll
+      for (int k = 0; k < PPW; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      if constexpr (NM > PPW + NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - PPW - NR, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (nk > 0) {
+    rd((nk - 1) & 1, 1, a1, b1);
+    mma(a0, b0);
+    mma(a1, b1);
+  }
+  // the epilogue image reuses the tile buffers: the last (empty-range) DMA has landed, every wave
+  // is past its reads
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  epilogue_bf16<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+}
+
+// ---- weight gradient dW = G^T X in bf16 (fp32 out) ---------------------------
+//
+// dW[n, k] = sum_r G[r, n] X[r, k] (G = dZ [R, N], X = the layer input [R, K],
+// both bf16, row-major; dW fp32 [N, K], the torch Linear weight layout): the
+// lin_rel / lin_root weight gradients of the c5 bf16 model's backward
+// (reference train.py:128 loss.backward() through GraphConv's Linears).  Both
+// operands are r-major while the MFMA wants 8 consecutive r per lane, so the
+// tiles are staged row-major by LDS-DMA (G rows of 256 n, X rows of 256 k:
+// 512-B rows) and the fragments are read with ds_read_b64_tr_b16, the gfx950
+// transposing LDS read (per 16-lane group: 4 rows x 16 columns in, lane i gets
+// column i): two reads give a lane its 8 consecutive r of one column.  Image:
+// 32-B segment s of row r stored at s ^ f(r), f(r) = (r & 3) | ((r & 8) >> 1),
+// so the 8 rows one 32-lane half reads (r0 .. r0+3 and r0+8 .. r0+11) land on
+// 8 distinct bank groups (conflict-free); the DMA source addresses carry the
+// inverse map (the LDS destination stays lane-linear).  R-tiles of 64 rows,
+// two buffers, the fc_bf16_p pipeline (barrier mid-tile).  Output tile
+// 256 x 256; the 2048 x 2048 weights are only 64 tiles, so R is split into S
+// contiguous ranges (XCD-aware: one range's tiles run on one XCD and share its
+// rows in L2), partial tiles to a workspace, folded in range order:
+// deterministic, no atomics.  Each range's descriptor is rebased per R-tile,
+// so rows past the range (and past R) read zeros.
+struct WgB16Args {
+  int64_t R, N, K;
+  const uint16_t *G, *X;
+  int64_t ldg, ldx;
+  float *P;  // partials: range s at P + s * ps, [N, ldp]
+  int64_t ldp, ps;
+  int64_t nt, kt, S, rows_per_split;
+};
+
+constexpr int WG_BR = 64;  // rows per R-tile
+
+// dma16 as inline asm (the same buffer_load_dwordx4 ... lds, M0 = the LDS destination): hipcc
+// then does not track the DMA and inserts no s_waitcnt vmcnt before the ds_read_tr16 reads of the
+// OTHER stage buffer (it cannot tell the intrinsic's LDS address from the DMA's and waited for the
+// DMA just issued before every read that followed it); every DMA of wgrad_bf16 goes through here
+// (the kernel has no other M0 user), and its barriers wait vmcnt(0) themselves
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16_asm(uint64_t p, uint32_t n, unsigned char *lds, uint32_t voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(3))) unsigned char lds_u8;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
+  const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_u8 *)lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(rs)
+               : "memory", "m0");
+#endif
+}
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ int wg_f(int r) { return (r & 3) | ((r & 8) >> 1); }
+
+template <int WM, int WN, int FM, int FN, bool SCHED, bool PRIO>
+__global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
+  constexpr int NW = WM * WN;
+  constexpr int BN = WM * FM * 16, BKC = WN * FN * 16;  // output rows (n) x columns (k)
+  static_assert(BN == 256 && BKC == 256, "512-B image rows");
+  constexpr int ROWB = 512, G_BYTES = WG_BR * ROWB, TILE_BYTES = 2 * G_BYTES;
+  constexpr int PG = G_BYTES / 1024, PT = 2 * PG, PPW = PT / NW;  // pieces of 2 rows
+  static_assert(PG % NW == 0, "whole pieces per wave");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
+
+  const int64_t nwg = (int64_t)gridDim.x, bx = blockIdx.x;
+  const int64_t xcd = bx % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t bid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bx / 8;
+  const int64_t tiles = a.nt * a.kt;
+  const int64_t s = bid / tiles, tile = bid % tiles;
+  const int64_t n0 = (tile / a.kt) * BN, k0 = (tile % a.kt) * BKC;
+  const int64_t r0 = s * a.rows_per_split;
+  const int64_t r1 = r0 + a.rows_per_split < a.R ? r0 + a.rows_per_split : a.R;
+  const int nk = r1 > r0 ? (int)((r1 - r0 + WG_BR - 1) / WG_BR) : 0;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  // piece q = wave + NW p: rows 2 (q mod PG), +1 of G (q < PG) or X; lane i lands at row
+  // 2 q' + i / 32, physical 16-B chunk c = i % 32, logical chunk c ^ (f(row) << 1)
+  uint32_t vo[PPW];
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) {
+    const int q = wave + NW * p;
+    const int row = (q < PG ? q : q - PG) * 2 + (lane >> 5), c = lane & 31;
+    vo[p] = (uint32_t)((row * (q < PG ? a.ldg : a.ldx) + (c ^ (wg_f(row) << 1)) * 8) * 2);
+  }
+  auto stage = [&](int b, int t) {  // t >= nk: empty ranges (zeros into a buffer nobody reads again)
+    unsigned char *base = smem + b * TILE_BYTES;
+    const int64_t rt = r0 + (int64_t)t * WG_BR;
+    const int64_t left = r1 > rt ? r1 - rt : 0;
+    const int64_t gb = left * a.ldg * 2, xb = left * a.ldx * 2;
+    const uint32_t ng = (uint32_t)(gb < 0x7fffffff ? gb : 0x7fffffff), nx = (uint32_t)(xb < 0x7fffffff ? xb : 0x7fffffff);
+    const uint64_t pg = (uint64_t)(a.G + rt * a.ldg + n0), px = (uint64_t)(a.X + rt * a.ldx + k0);
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) {
+      const int q = wave + NW * p;
+      if (p < PG / NW)
+        dma16_asm(pg, ng, base + q * 1024, vo[p]);
+      else
+        dma16_asm(px, nx, base + q * 1024, vo[p]);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed fragment reads: lane 16g + 4qq + pp supplies row 32 s + 8 g + 4 h + qq, columns
+  // 16 c + 4 pp .. +3 of the 16-column block c; f(row) = qq | ((g & 1) << 2) for every s, h
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int fl = qq | ((g & 1) << 2);
+  const int lane_off = (8 * g + qq) * ROWB + 8 * pp;
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto tr2 = [&](const unsigned char *img, int off) {  // rows +0..3 and +4..7 -> 8 consecutive r
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + off + 4 * ROWB));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto rd = [&](int b, int st, bf16x8(&av)[FM], bf16x8(&bv)[FN]) {
+    // fl laundered per call: the 12 fragment addresses are recomputed (a few VALU) instead of
+    // being hoisted out of the loop as 12 more live VGPRs (which spilled)
+    int flv = fl;
+    asm volatile("" : "+v"(flv));
+    const unsigned char *Gs = smem + b * TILE_BYTES + st * 32 * ROWB + lane_off;
+    const unsigned char *Xs = Gs + G_BYTES;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) av[i] = tr2(Gs, ((wm * FM + i) ^ flv) * 32);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bv[j] = tr2(Xs, ((wn * FN + j) ^ flv) * 32);
+  };
+  auto mma = [&](const bf16x8(&av)[FM], const bf16x8(&bv)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+  if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (nk > 0) {
+    stage(0, 0);
+    barrier();
+    if (nk > 1) stage(1, 1);
+    rd(0, 0, a0, b0);
+  }
+  constexpr int NR = 2 * (FM + FN), NM = FM * FN;  // transposed reads (two per fragment), MFMAs
+  for (int t = 0; t + 1 < nk; ++t) {  // last tile peeled, as in fc_bf16_p
+    const int b = t & 1;
+    rd(b, 1, a1, b1);
+    mma(a0, b0);
+    if constexpr (SCHED) {
+#pragma unroll
+      for (int k = 0; k < NR && k < NM; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      if constexpr (NR < NM) __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+    }
+    barrier();
+    stage(b, t + 2);
+    rd(b ^ 1, 0, a0, b0);
+    mma(a1, b1);
+    if constexpr (SCHED) {
+#pragma unroll
+      for (int k = 0; k < PPW; ++k) {  // (the asm DMAs are not schedulable units: they keep their place)
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (PPW + k < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      if constexpr (NM > PPW + NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - PPW - NR, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (nk > 0) {
+    rd((nk - 1) & 1, 1, a1, b1);
+    mma(a0, b0);
+    mma(a1, b1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (empty) DMA lands before the wave ends
+
+  // D map: row (n) = 4 * (lane >> 4) + r, col (k) = lane & 15
+  float *P = a.P + s * a.ps;
+  const int fr = lane & 15;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int64_t col = k0 + wn * FN * 16 + j * 16 + fr;
+    if (col >= a.K) continue;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = n0 + wm * FM * 16 + i * 16 + 4 * g + r;
+        if (row < a.N) P[row * a.ldp + col] = acc[i][j][r];
+      }
+  }
+}
+
+// dW = sum_s part[s] in range order (s = 0 first): the deterministic fold of wgrad_bf16
+__global__ __launch_bounds__(256) void wgrad_bf16_fold(int64_t N, int64_t K, int64_t S, const float *__restrict__ part,
+                                                       float *__restrict__ dW, int64_t lddw) {
+  const int64_t kq = K / 4, tot = N * kq;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (int64_t)gridDim.x * 256) {
+    const int64_t n = i / kq, k = (i % kq) * 4;
+    f32x4 v = *reinterpret_cast<const f32x4 *>(part + n * K + k);
+    for (int64_t s = 1; s < S; ++s) v = v + *reinterpret_cast<const f32x4 *>(part + s * N * K + n * K + k);
+    *reinterpret_cast<f32x4 *>(dW + n * lddw + k) = v;
+  }
+}
+
 template <int WM, int WN, int FM, int FN>
 lpg_status launch_bf16(FcB16Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
@@ -389,7 +793,54 @@ lpg_status launch_bf16_p3(FcB16Args a, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
-int g_bf16_variant = 0;  // lpg_fc_bf16_set_variant: 0 = by size, 1 = 128 x 128, 2 = 256^2 2-buffer, 3 = 256^2 3-buffer
+template <int WM, int WN, int FM, int FN, bool SCHED = false, bool PRIO = false>
+lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int64_t nwg = a.mt * a.nt;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_bf16: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, true, SCHED, PRIO>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0,
+                       s, a);
+  else
+    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, false, SCHED, PRIO>), dim3((unsigned)nwg), dim3(64 * WM * WN),
+                       0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+// whether fc_bf16_p can take these operands: one offset set for both k phases, 32-bit offsets
+bool p_ok(const FcB16Args &a) {
+  if (a.K1 == 0) return false;
+  if (a.K2 > 0 && (a.lda1 != a.lda2 || a.ldw1 != a.ldw2)) return false;
+  const int64_t K = a.K1 > a.K2 ? a.K1 : a.K2;
+  return (256 * a.lda1 + K) * 2 < ((int64_t)1 << 31) && (256 * a.ldw1 + K) * 2 < ((int64_t)1 << 31);
+}
+
+// lpg_fc_bf16_set_variant: 0 = by size (128 x 128 below 4096 rows, else 7, else 2), 1 = 128 x 128,
+// 2 = 256^2 2-buffer, 3 = 256^2 3-buffer,
+// 4 / 5 = fc_bf16_p with 4 / 8 waves, 6 = 5 with the reads and DMA placed between the MFMAs
+// (sched_group_barrier), 7 = 6 + s_setprio 1 for waves 4-7, 8 = 4 placed; 100 / 101 = wgrad_bf16
+// with 4 / 8 waves, 102 / 103 = 101 placed / + prio, 104 = 100 placed (102 the default; measured
+// at the c5 shapes, profiles/r02_kbench_bf16.log: 7 1209-1212 TF/s vs hipBLASLt 1268 (2 1033);
+// 102 1172-1222 vs hipBLASLt's bf16-output GEMM 924-1004)
+int g_bf16_variant = 0;
+int g_wgrad_bf16_variant = 102;
+
+int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
+  const int64_t tiles = ((N + 255) / 256) * ((K + 255) / 256);
+  int64_t S = (512 + tiles / 2) / tiles;
+  const int64_t smax = (R + 511) / 512;
+  S = S < smax ? S : smax;
+  S = S < 1 ? 1 : S;
+  int64_t rows = (R + S - 1) / S;
+  rows = ((rows + WG_BR - 1) / WG_BR) * WG_BR;
+  rows = rows < WG_BR ? WG_BR : rows;
+  S = R > 0 ? (R + rows - 1) / rows : 1;
+  *S_out = S;
+  return rows;
+}
 
 }  // namespace
 }  // namespace lpg
@@ -421,12 +872,65 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
   const bool relu = flags & 1;
   if (g_bf16_variant == 1 || (g_bf16_variant == 0 && M < 4096))
     return launch_bf16<2, 2, 4, 4>(a, relu, s);  // 128 x 128
+  if (g_bf16_variant == 0 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true, true>(a, relu, s);  // = 7
   if (g_bf16_variant == 3) return launch_bf16_p3(a, relu, s);  // 256 x 256, BK 32, 3 buffers
+  if (g_bf16_variant == 4 && p_ok(a)) return launch_bf16_p<2, 2, 8, 8>(a, relu, s);  // 4 waves of 128 x 128
+  if (g_bf16_variant == 5 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4>(a, relu, s);  // 8 waves of 128 x 64
+  if (g_bf16_variant == 6 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true>(a, relu, s);  // + placed reads
+  if (g_bf16_variant == 7 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true, true>(a, relu, s);  // + prio
+  if (g_bf16_variant == 8 && p_ok(a)) return launch_bf16_p<2, 2, 8, 8, true>(a, relu, s);  // 4 waves, placed
   return launch_bf16<2, 4, 8, 4>(a, relu, s);    // 256 x 256, BK 64, 2 buffers
 }
 
 extern "C" lpg_status lpg_fc_bf16_set_variant(int32_t v) {
-  LPG_REQUIRE(v >= 0 && v <= 3, "lpg_fc_bf16_set_variant: variant %d not in [0, 3]", v);
-  g_bf16_variant = v;
+  LPG_REQUIRE((v >= 0 && v <= 8) || (v >= 100 && v <= 104),
+              "lpg_fc_bf16_set_variant: variant %d not in [0, 8] or [100, 104]", v);
+  if (v >= 100)
+    g_wgrad_bf16_variant = v;
+  else
+    g_bf16_variant = v;
+  return LPG_OK;
+}
+
+extern "C" int64_t lpg_wgrad_bf16_workspace_bytes(int64_t R, int64_t N, int64_t K) {
+  if (R < 0 || N <= 0 || K <= 0) return 0;
+  int64_t S;
+  wgrad_bf16_rows(R, N, K, &S);
+  return S > 1 ? S * N * K * 4 : 0;
+}
+
+extern "C" lpg_status lpg_wgrad_bf16(int64_t R, int64_t N, int64_t K, const uint16_t *G, int64_t ldg,
+                                     const uint16_t *X, int64_t ldx, float *dW, int64_t lddw, void *workspace,
+                                     void *stream) {
+  LPG_REQUIRE(R >= 0 && N >= 0 && K >= 0, "lpg_wgrad_bf16: negative size");
+  if (N == 0 || K == 0) return LPG_OK;
+  LPG_REQUIRE(N % 8 == 0 && K % 8 == 0 && ldg % 8 == 0 && ldx % 8 == 0 && ldg >= N && ldx >= K &&
+                  ldg < ((int64_t)1 << 24) && ldx < ((int64_t)1 << 24),
+              "lpg_wgrad_bf16: N, K, ldg, ldx must be multiples of 8 (ldg >= N, ldx >= K)");
+  LPG_REQUIRE(R == 0 || (G && X && aligned16(G) && aligned16(X)), "lpg_wgrad_bf16: G/X must be 16-byte aligned");
+  LPG_REQUIRE(dW && aligned16(dW) && lddw >= K && lddw % 4 == 0, "lpg_wgrad_bf16: bad dW/lddw");
+  int64_t S;
+  const int64_t rows = wgrad_bf16_rows(R, N, K, &S);
+  LPG_REQUIRE(S == 1 || (workspace && aligned16(workspace)), "lpg_wgrad_bf16: workspace required (16-B aligned)");
+  WgB16Args w{R, N, K, G, X, ldg, ldx, S > 1 ? static_cast<float *>(workspace) : dW, S > 1 ? K : lddw, N * K,
+              (N + 255) / 256, (K + 255) / 256, S, rows};
+  const int64_t nwg = w.nt * w.kt * S;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_wgrad_bf16: grid too large");
+  hipStream_t s = as_stream(stream);
+  switch (g_wgrad_bf16_variant) {
+    case 100: hipLaunchKernelGGL((wgrad_bf16<2, 2, 8, 8, false, false>), dim3((unsigned)nwg), dim3(256), 0, s, w); break;
+    case 101: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, false, false>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
+    case 102: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, true, false>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
+    case 103: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, true, true>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
+    default: hipLaunchKernelGGL((wgrad_bf16<2, 2, 8, 8, true, false>), dim3((unsigned)nwg), dim3(256), 0, s, w); break;
+  }
+  LPG_HIP(hipGetLastError());
+  if (S > 1) {
+    const int64_t tot = N * (K / 4);
+    const int64_t blocks = (tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096;
+    hipLaunchKernelGGL(wgrad_bf16_fold, dim3((unsigned)blocks), dim3(256), 0, s, N, K, S,
+                       static_cast<const float *>(workspace), dW, lddw);
+    LPG_HIP(hipGetLastError());
+  }
   return LPG_OK;
 }

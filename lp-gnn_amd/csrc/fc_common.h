@@ -27,6 +27,20 @@ __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int64_t row, int64_
   return lowbias32(hr ^ ((uint32_t)col * 0x9e3779b9u) ^ (uint32_t)(seed >> 32));
 }
 
+// 16 B per lane, buffer_load_dwordx4 ... lds into M0 = lds (lane-linear): the descriptor over
+// [p, p + n) is built from readfirstlane'd values, so it stays in SGPRs (a select between two
+// descriptors went to VGPRs and turned every load into a waterfall loop); the lane offset is
+// voff, the step soff (scalar); offsets at or past n read zeros
+__device__ __forceinline__ void dma16(uint64_t p, uint32_t n, unsigned char *lds, uint32_t voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(3))) void lds_v;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_v *)lds, 16, voff, soff, 0, 0);
+#endif
+}
+
 // Host-side dropout threshold / scale shared by the FC entry points.
 inline void dropout_params(float p, uint32_t *thresh, float *scale) {
   *thresh = 0u;

@@ -652,20 +652,6 @@ lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
-// 16 B per lane, buffer_load_dwordx4 ... lds into M0 = lds (lane-linear): the descriptor over
-// [p, p + n) is built from readfirstlane'd values, so it stays in SGPRs (a select between two
-// descriptors went to VGPRs and turned every load into a waterfall loop); the lane offset is
-// voff, the step soff (scalar); offsets at or past n read zeros
-__device__ __forceinline__ void dma16(uint64_t p, uint32_t n, unsigned char *lds, uint32_t voff, int soff) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  typedef __attribute__((address_space(3))) void lds_v;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_v *)lds, 16, voff, soff, 0, 0);
-#endif
-}
-
 // ---- wide strips: fc_x3_wide (variants 12-15; the default) --------------------
 //
 // fc_fwd_x3_16 splits every A element once per block, so the split VALU per MFMA falls only as

@@ -34,6 +34,8 @@ HEADER_SYMBOLS = (
     "lpg_fc_set_variant",
     "lpg_fc_bf16",
     "lpg_fc_bf16_set_variant",
+    "lpg_wgrad_bf16_workspace_bytes",
+    "lpg_wgrad_bf16",
     "lpg_split3_f32",
     "lpg_fc_x3_f32",
     "lpg_fc_x3_set_variant",
@@ -133,6 +135,10 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_bf16.restype = c_i32
     L.lpg_fc_bf16_set_variant.argtypes = [c_i32]
     L.lpg_fc_bf16_set_variant.restype = c_i32
+    L.lpg_wgrad_bf16_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
+    L.lpg_wgrad_bf16_workspace_bytes.restype = c_i64
+    L.lpg_wgrad_bf16.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p]
+    L.lpg_wgrad_bf16.restype = c_i32
     L.lpg_relu_dropout_bwd_f32.argtypes = [c_i64, c_p, c_p, ctypes.c_float, c_p, c_p]
     L.lpg_relu_dropout_bwd_f32.restype = c_i32
     L.lpg_relu_bwd_colsum_workspace_bytes.argtypes = [c_i64, c_i64]
@@ -180,6 +186,11 @@ def lib() -> ctypes.CDLL:
     for env, off in (("LPGNN_X3_VARIANT", 0), ("LPGNN_WGRAD_VARIANT", 100)):
         if os.environ.get(env):
             if L.lpg_fc_x3_set_variant(int(os.environ[env]) + off) != 0:
+                raise RuntimeError(f"{env}={os.environ[env]}: {L.lpg_last_error().decode()}")
+    # ... and the bf16 (c5) FC tile / weight-gradient kernel
+    for env, off in (("LPGNN_BF16_VARIANT", 0), ("LPGNN_WGRAD_BF16_VARIANT", 100)):
+        if os.environ.get(env):
+            if L.lpg_fc_bf16_set_variant(int(os.environ[env]) + off) != 0:
                 raise RuntimeError(f"{env}={os.environ[env]}: {L.lpg_last_error().decode()}")
     _lib = L
     return L

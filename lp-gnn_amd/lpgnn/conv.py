@@ -215,9 +215,10 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
     t_r, tsrc_r, relt_r = plan(AT, A, dz_r, left, w_rel_l2r, agg_r, need[0], need[3])
     t_l, tsrc_l, relt_l = plan(A, AT, dz_l, right, w_rel_r2l, agg_l, need[1], need[6])
 
-    # fp32: the x3 kernels (weight gradient G^T X, input gradient G W) unless LPGNN_FC_ARITH=fp32
-    wg = (lambda g, x: (g.t() @ x).float()) if bf16 else _fc.wgrad
-    ig = None if bf16 else _fc.input_grad
+    # fp32: the x3 kernels (weight gradient G^T X, input gradient G W) unless LPGNN_FC_ARITH=fp32;
+    # bf16: lpg_wgrad_bf16 (fp32 weight gradients) and lpg_fc_bf16 on the transposed weights
+    wg = _fc.wgrad_bf16 if bf16 else _fc.wgrad
+    ig = _fc.input_grad_bf16 if bf16 else _fc.input_grad
 
     def wgrads(dz, agg, x_dst, need_rel, need_root):
         if not (need_rel or need_root):
@@ -244,9 +245,6 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
 
     def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root):
         """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients)."""
-        if ig is None:
-            g = T @ w_rel if t_src else spmm_forward(St, dz @ w_rel)
-            return g.addmm_(dz_root, w_root)
         if t_src:  # both terms over the same rows: one two-part GEMM
             return ig(T, w_rel, dz_root, w_root)
         return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True)

@@ -14,10 +14,10 @@ arch.py:129-141 for one side (lpg_knowledge_f32).
 Forward numerics are bitwise reproducible (oracle/fc_ref.c).  Training-mode
 dropout (arch.py:186-187) is fused into the FC epilogue with a counter-based
 RNG seeded from torch's generator.  Backward: dZ = (Y > 0) ? dY/(1-p) : 0 in
-one pass (lpg_relu_dropout_bwd_f32); dA = dZ W, dW = dZ^T A, db = sum(dZ)
-as plain library GEMMs through torch on the same stream (hipBLASLt); the
-heads' backward (N = 3) runs in lpg_linear_small_bwd_f32.  Tolerance-level
-parity for gradients.
+one pass (lpg_relu_dropout_bwd_f32); dA = dZ W and dW = dZ^T A on the x3
+kernels (fp32) or lpg_fc_bf16 / lpg_wgrad_bf16 (bf16, c5), the library GEMMs
+only with LPGNN_FC_ARITH=fp32; db = sum(dZ); the heads' backward (N = 3)
+runs in lpg_linear_small_bwd_f32.  Tolerance-level parity for gradients.
 """
 from __future__ import annotations
 
@@ -243,7 +243,7 @@ def _prep_bf16(t: Tensor | None) -> Tensor | None:
 
 def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                     relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
-                    accumulate: bool = False) -> Tensor:
+                    accumulate: bool = False, key: str | None = None) -> Tensor:
     """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16);
     ``accumulate`` adds the bf16 addend held in ``out`` (overwritten)."""
     if A1.device.type != "cuda":
@@ -263,7 +263,7 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0)
     with torch.cuda.device(A1.device):
-        tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu-bf16" if relu else "lin-bf16"))
+        tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, key or ("relu-bf16" if relu else "lin-bf16")))
         st = L.lpg_fc_bf16(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
                            K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
                            None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
@@ -272,6 +272,44 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_bf16")
     return C
+
+
+def wgrad_bf16(G: Tensor, X: Tensor) -> Tensor:
+    """G^T X for bf16 G [R, N], X [R, K]: the fp32 weight gradient [N, K] of a
+    Linear in the c5 bf16 model (lpg_wgrad_bf16: fp32 accumulation, fp32 out,
+    deterministic split-R reduction)."""
+    if G.device.type != "cuda":
+        raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
+    G, X = G.to(torch.bfloat16), X.to(torch.bfloat16)
+    R, N, K = G.shape[0], G.shape[1], X.shape[1]
+    pad = lambda t, c: t if c % 8 == 0 else F.pad(t, (0, 8 - c % 8))
+    Gp, Xp = pad(G, N), pad(X, K)
+    if Gp.stride(1) != 1 or Gp.stride(0) % 8 or Gp.data_ptr() % 16:
+        Gp = Gp.contiguous()
+    if Xp.stride(1) != 1 or Xp.stride(0) % 8 or Xp.data_ptr() % 16:
+        Xp = Xp.contiguous()
+    Np, Kp = Gp.shape[1], Xp.shape[1]
+    L = _lib.lib()
+    dW = torch.empty((Np, Kp), dtype=torch.float32, device=G.device)
+    ws = torch.empty(max(16, L.lpg_wgrad_bf16_workspace_bytes(R, Np, Kp)), dtype=torch.uint8, device=G.device)
+    with torch.cuda.device(G.device):
+        tok = TIMER.start(("wgrad", R, N, K, "bf16"))
+        st = L.lpg_wgrad_bf16(R, Np, Kp, Gp.data_ptr(), Gp.stride(0), Xp.data_ptr(), Xp.stride(0), dW.data_ptr(),
+                              dW.stride(0), ws.data_ptr(), _lib.stream_of(G))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_wgrad_bf16")
+    return dW if (Np, Kp) == (N, K) else dW[:N, :K]
+
+
+def input_grad_bf16(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | None = None,
+                    out: Tensor | None = None, accumulate: bool = False) -> Tensor:
+    """G1 W1 [+ G2 W2] [+ out] in bf16 for Linear weights W [out, in]: the
+    c5 input gradient of lin_rel / lin_root on the bf16 FC kernel (lpg_fc_bf16
+    with the weights transposed; fp32 accumulation, one bf16 rounding)."""
+    t = lambda W: None if W is None else W.detach().t().to(torch.bfloat16).contiguous()
+    G1 = G1.to(torch.bfloat16)
+    G2 = None if G2 is None else G2.to(torch.bfloat16)
+    return fc_forward_bf16(G1, t(W1), G2, t(W2), None, False, out=out, accumulate=accumulate, key="igrad-bf16")
 
 
 def relu_dropout_bwd(g: Tensor, y: Tensor, scale: float) -> Tensor:
@@ -401,15 +439,15 @@ class _FC(torch.autograd.Function):
         A1, A2, W1, W2, C = ctx.saved_tensors
         need = ctx.needs_input_grad
         want_db = ctx.has_b and need[4]
-        if ctx.bf16:  # bf16 grads through hipBLASLt; weight/bias grads returned in fp32
+        if ctx.bf16:  # bf16 input grads on lpg_fc_bf16, fp32 weight grads on lpg_wgrad_bf16, fp32 bias grad
             if ctx.relu:
                 g, db = relu_bwd_colsum_bf16(gC, C, ctx.scale, want_db)
             else:
-                g, db = gC, (gC.float().sum(0) if want_db else None)
-            dA1 = g @ W1 if need[0] else None
-            dA2 = g @ W2 if ctx.has_a2 and need[1] else None
-            dW1 = (g.t() @ A1).float() if need[2] else None
-            dW2 = (g.t() @ A2).float() if ctx.has_a2 and need[3] else None
+                g, db = gC.to(torch.bfloat16), (gC.float().sum(0) if want_db else None)
+            dA1 = input_grad_bf16(g, W1) if need[0] else None
+            dA2 = input_grad_bf16(g, W2) if ctx.has_a2 and need[1] else None
+            dW1 = wgrad_bf16(g, A1) if need[2] else None
+            dW2 = wgrad_bf16(g, A2) if ctx.has_a2 and need[3] else None
             return dA1, dA2, dW1, dW2, db, None, None
         if ctx.relu:
             g, db = relu_bwd_colsum(gC, C, ctx.scale, want_db)  # ReLU + dropout bwd, bias grad fused
@@ -496,8 +534,8 @@ class _Linear(torch.autograd.Function):
         need = ctx.needs_input_grad
         if ctx.bf16:
             g = g.to(torch.bfloat16)
-            dx = g @ W if need[0] else None
-            dW = (g.t() @ x).float() if need[1] else None
+            dx = input_grad_bf16(g, W) if need[0] else None
+            dW = wgrad_bf16(g, x) if need[1] else None
             db = g.float().sum(0) if ctx.has_b and need[2] else None
             return dx, dW, db
         if W.shape[0] <= 4 and x.shape[1] % 4 == 0:

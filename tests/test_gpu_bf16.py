@@ -43,7 +43,7 @@ def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
     torch.testing.assert_close(got, ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("M,N,K,relu,bias", [
     (5000, 1024, 1024, True, True),  # re-associated left2right root part
     (129, 130, 64, False, True),     # N % 8 != 0: per-element epilogue
@@ -92,7 +92,7 @@ def test_fc_bf16_tile_variants_identical():
     L = _lib.lib()
     outs = []
     try:
-        for v in (1, 2, 3):
+        for v in (1, 2, 3, 4, 5, 6, 7, 8):
             L.lpg_fc_bf16_set_variant(v)
             outs.append(fc_forward_bf16(A1, W1, A2, W2, b, True, 0.2, seed=9))
     finally:
@@ -178,3 +178,98 @@ def test_relu_bwd_colsum_bf16(M, N):
         ref = want.double().sum(0)
         chain = 64 + (M + 63) // 64
         assert bool(((db.double() - ref).abs() <= chain * 2.0 ** -24 * want.double().abs().sum(0) + 1e-30).all())
+
+
+def _wgrad_bound(G, X):
+    """fp32-accumulation bound for G^T X over R rows: the MFMA sums 32 products per
+    instruction and the chain adds one instruction result per 32 rows, the fold one
+    range partial per range -- (R / 32 + 64) * 2^-24 * sum |g x| covers every order."""
+    R = G.shape[0]
+    return (R / 32 + 128) * 2.0 ** -24 * (G.double().abs().t() @ X.double().abs())
+
+
+@pytest.mark.parametrize("R,N,K", [
+    (0, 64, 64),            # no rows: zeros
+    (1, 8, 8),              # one row, narrow
+    (100, 264, 136),        # ragged tiles, one R-range
+    (4097, 256, 512),       # ragged last R-tile
+    (70001, 1024, 1024),    # several R-ranges + fold
+    (20000, 2048, 2048),    # c5 weight shape
+])
+def test_wgrad_bf16_vs_fp64(R, N, K):
+    """lpg_wgrad_bf16 (fp32 accumulation of exact bf16 x bf16 products) against
+    fp64 G^T X of the same bf16 operands; both kernel variants bitwise identical
+    and run-to-run identical."""
+    from lpgnn import _lib
+    from lpgnn.fc import wgrad_bf16
+
+    g = torch.Generator().manual_seed(R + N + K)
+    G = torch.randn(R, N, generator=g).to(BF)
+    X = torch.relu(torch.randn(R, K, generator=g)).to(BF)
+    Gd, Xd = G.to(DEV), X.to(DEV)
+    L = _lib.lib()
+    try:
+        outs = []
+        for v in (100, 101, 102, 103, 104, 100):
+            L.lpg_fc_bf16_set_variant(v)
+            outs.append(wgrad_bf16(Gd, Xd))
+    finally:
+        L.lpg_fc_bf16_set_variant(100)
+    assert outs[0].dtype == torch.float32 and outs[0].shape == (N, K)
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
+    ref = G.double().t() @ X.double()
+    err = (outs[0].cpu().double() - ref).abs()
+    assert bool((err <= _wgrad_bound(G, X) + 1e-30).all()), err.max().item()
+
+
+def test_wgrad_bf16_asymmetric():
+    """G = I (R = N) with an asymmetric X catches a transposed operand or D map:
+    dW = X exactly (each output is one product)."""
+    from lpgnn.fc import wgrad_bf16
+
+    R = 272
+    G = torch.eye(R, dtype=BF, device=DEV)
+    X = (torch.arange(R * 264, dtype=torch.float32, device=DEV).view(R, 264) % 61 - 30).to(BF)
+    assert torch.equal(wgrad_bf16(G, X), X.float())
+
+
+def test_wgrad_bf16_strided_operands():
+    """Column slices of wider tensors (leading dimension > N, K), as the layer's
+    [agg | x_dst] halves would be."""
+    from lpgnn.fc import wgrad_bf16
+
+    torch.manual_seed(3)
+    Gw = torch.randn(5000, 640, device=DEV).to(BF)
+    Xw = torch.randn(5000, 776, device=DEV).to(BF)
+    G, X = Gw[:, 128:512], Xw[:, 8:520]
+    got = wgrad_bf16(G, X)
+    ref = G.double().t() @ X.double()
+    assert bool(((got.double() - ref).abs() <= _wgrad_bound(G, X) + 1e-30).all())
+
+
+@pytest.mark.parametrize("M,N,Nout,two,acc", [
+    (1000, 2048, 2048, False, False),
+    (4099, 1024, 2048, True, False),   # the two-part form (T W_rel + dZ_root W_root)
+    (5000, 1024, 1024, False, True),   # accumulated onto an SpMM result
+    (300, 264, 136, True, True),
+])
+def test_input_grad_bf16(M, N, Nout, two, acc):
+    """G1 W1 [+ G2 W2] [+ P] on lpg_fc_bf16 with the transposed weights, within one
+    bf16 rounding of the fp32 product of the same bf16 operands."""
+    from lpgnn.fc import input_grad_bf16
+
+    g = torch.Generator().manual_seed(M + N)
+    G1 = torch.randn(M, Nout, generator=g).to(BF).to(DEV)
+    W1 = (torch.randn(Nout, N, generator=g) * 0.05).to(DEV)  # fp32 master weights
+    G2 = torch.randn(M, Nout, generator=g).to(BF).to(DEV) if two else None
+    W2 = (torch.randn(Nout, N, generator=g) * 0.05).to(DEV) if two else None
+    P = torch.randn(M, N, generator=g).to(BF).to(DEV) if acc else None
+    ref = G1.float() @ W1.to(BF).float()
+    if two:
+        ref = ref + G2.float() @ W2.to(BF).float()
+    if acc:
+        ref = ref + P.float()
+    got = input_grad_bf16(G1, W1, G2, W2, out=P, accumulate=acc)
+    assert got.dtype == BF and got.shape == (M, N)
+    torch.testing.assert_close(got.float(), ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)

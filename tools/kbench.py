@@ -5,6 +5,7 @@
 fc   : lpg_fc_f32 at the c2 shapes vs torch (hipBLASLt) linear+linear+add+relu
 fcpmc: only the two hidden-layer FC kernels (fp32 c2 and bf16 c5 shapes), for PMC passes
 bf16 : lpg_fc_bf16 at the c5 shape vs torch bf16 (hipBLASLt)
+bf16bwd: the c5 backward GEMMs (lpg_wgrad_bf16, lpg_fc_bf16 on transposed weights) vs torch
 load : graph load at c2 -- reference chain (to_undirected + MyToBipartite + device pack) vs direct pack
 spmm : lpg_spmm_f32 at c2, both directions, slice widths 256/512/1024
 bwd  : the FC backward GEMMs at c2 shapes through torch (hipBLASLt)
@@ -163,14 +164,61 @@ def bench_bf16(out):
             return fc_forward_bf16(B1, V1, B2, V2, b2, True)
         return f
     y0 = var(0)()
-    for v in (1, 2, 3):
+    for v in (1, 2, 3, 4, 5, 6, 7, 8):
         assert torch.equal(var(v)(), y0), f"bf16 variant {v} differs"
-    t = timeit({"lpg_fc_bf16 v0 (default)": var(0), "lpg_fc_bf16 v1 128x128": var(1),
-                "lpg_fc_bf16 v2 256x256 2buf": var(2), "lpg_fc_bf16 v3 256x256 3buf": var(3),
+    t = timeit({"lpg_fc_bf16 v2 256x256 2buf": var(2), "lpg_fc_bf16 v5 8-wave pipelined": var(5),
+                "lpg_fc_bf16 v6 v5 + placed": var(6), "lpg_fc_bf16 v7 v6 + prio": var(7),
+                "lpg_fc_bf16 v8 4-wave placed": var(8),
                 "torch_bf16_1gemm_relu": lambda: torch.relu(F.linear(Bc, Vc, b2.to(torch.bfloat16)))})
     L.lpg_fc_bf16_set_variant(0)
     for k, v in t.items():
         out[f"bf16 M={M} K=4096 {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * 4096 / v / 1e9)
+
+
+def bench_bf16bwd(out):
+    """c5 backward GEMMs: lpg_wgrad_bf16 (4 / 8 waves) vs torch (G^T X).float(); the input
+    gradient on lpg_fc_bf16 (transposed weights) vs torch G @ W."""
+    from lpgnn import _lib
+    from lpgnn.fc import input_grad_bf16, wgrad_bf16
+
+    L = _lib.lib()
+    BF = torch.bfloat16
+    for R in (100_000, 200_000):
+        G = torch.randn(R, 2048, device="cuda").to(BF)
+        X = torch.relu(torch.randn(R, 2048, device="cuda")).to(BF)
+        W = torch.randn(2048, 2048, device="cuda") * 0.02
+        Wb = W.to(BF)
+
+        def wv(v):
+            def f():
+                L.lpg_fc_bf16_set_variant(v)
+                return wgrad_bf16(G, X)
+            return f
+        a = wv(100)()
+        for v in (101, 102, 103, 104):
+            assert torch.equal(a, wv(v)()), f"wgrad variant {v} differs"
+        ref = (G.float().t() @ X.float())
+        print(f"R={R} wgrad max|ours - fp32 torch| = {(a - ref).abs().max().item():.3e}  "
+              f"max|torch bf16 - fp32| = {((G.t() @ X).float() - ref).abs().max().item():.3e}", flush=True)
+        del ref
+
+        def iv(v, two=False):
+            def f():
+                L.lpg_fc_bf16_set_variant(v)
+                return input_grad_bf16(G, W, G if two else None, W if two else None)
+            return f
+        t = timeit({"wgrad v100 4-wave": wv(100), "wgrad v101 8-wave": wv(101), "wgrad v102 placed": wv(102),
+                    "wgrad v103 placed+prio": wv(103), "wgrad v104 4-wave placed": wv(104),
+                    "wgrad torch (G^T X).float()": lambda: (G.t() @ X).float(),
+                    "igrad v5": iv(5), "igrad v6": iv(6), "igrad v7": iv(7), "igrad torch G @ W": lambda: G @ Wb,
+                    "igrad2 v5": iv(5, True), "igrad2 v6": iv(6, True), "igrad2 v7": iv(7, True),
+                    "igrad2 torch": lambda: torch.addmm(G @ Wb, G, Wb)}, rounds=5, iters=3)
+        L.lpg_fc_bf16_set_variant(0)
+        L.lpg_fc_bf16_set_variant(100)
+        for k, v in t.items():
+            fl = 2.0 * R * 2048 * 2048 * (2 if k.startswith("igrad2") else 1)
+            out[f"bf16bwd R={R} {k}"] = dict(ms=v, tflops=fl / v / 1e9)
+        del G, X
 
 
 def bench_load(out):
@@ -244,6 +292,7 @@ if __name__ == "__main__":
     out = {}
     for w in which:
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
+         "bf16bwd": bench_bf16bwd,
          "load": bench_load, "fcpi": bench_fcpi}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
