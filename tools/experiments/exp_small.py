@@ -3,7 +3,7 @@ ReLU mask, conv1 weight gradient, heads forward) -- A/B of builds via LPGNN_LIB.
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "lp-gnn_amd")]
 import torch  # noqa: E402
 

@@ -3,12 +3,12 @@ wide-strip kernels (variants 12-15).  Every variant's C must equal variant 0's
 bit for bit (same MFMA shape, k order and product sequence); prints ms and TF/s
 (fp32-equivalent: 2 M N K).
 
-  LPG_X3V=0,12,13,14,15 python tools/exp_wide.py
+  LPG_X3V=0,12,13,14,15 python tools/experiments/exp_wide.py
 """
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "lp-gnn_amd")]
 import torch  # noqa: E402
 

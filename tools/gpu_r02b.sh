@@ -15,6 +15,8 @@ for s in ${*:-tests kb}; do
     tests) run bf16tests 400 python -u -m pytest tests/test_gpu_bf16.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     kb) run kbench_bf16 400 python -u tools/kbench.py bf16 bf16bwd ;;
     c5) run bench_c5 600 python -u bench.py --config c5 --steps 10 --warmup 3 ;;
+    profc5) run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 -o run -- \
+              python bench.py --config c5 --steps 3 --warmup 2 --profile-only ;;
     c5parity) run c5parity 900 python -u -m pytest tests/test_gpu_c2_parity.py -k c5 -v -s -p no:cacheprovider --timeout 900 --timeout-method thread ;;
     *) echo "unknown stage $s"; exit 2 ;;
   esac
