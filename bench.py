@@ -302,11 +302,15 @@ def main():
                      "traffic_source": traffic_src},
         "fc_roofline": {"bound": "mfma", "achieved": fc_tf, "peak": fc_peak, "unit": "TFLOP/s",
                         "frac": fc_tf / fc_peak, "launches": sum(kern[k][0] for k in fc_keys),
-                        "kernel": ("lpg fc_fwd_bf16 (hidden GraphConv FC, fwd)" if args.bf16 else
+                        "kernel": ("lpg fc_bf16 + wgrad_bf16 (hidden-width GEMMs, fwd + bwd: FC forward, input "
+                                   "gradients on the FC kernel, weight gradients)" if args.bf16 else
                                    "lpg fc_fwd_x3 + wgrad_x3 (hidden-width GEMMs, fwd + bwd; fp32 via exact "
                                    "3-way bf16 split, peak = dense bf16 / 6)" if x3 else
                                    "lpg fc_fwd_f32 (hidden GraphConv FC, fwd)"),
-                        "fp32_mfma_peak_frac": None if args.bf16 else fc_tf / FP32_MFMA_PEAK_TFLOPS},
+                        "fp32_mfma_peak_frac": None if args.bf16 else fc_tf / FP32_MFMA_PEAK_TFLOPS,
+                        # the bf16 MFMA work these launches issue (x3: 6 bf16 products per fp32 product),
+                        # comparable with a plain bf16 GEMM's rate on this chip
+                        "bf16_mfma_equiv_tflops": fc_tf * (6 if x3 and not args.bf16 else 1)},
         "spmm_directions": {
             ("cons<-vars" if (k[1], k[2]) == (args.m, args.n) and not distributed else
              "vars<-cons" if (k[1], k[2]) == (args.n, args.m) and not distributed else f"{k[1]}x{k[2]}"):

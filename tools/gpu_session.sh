@@ -55,6 +55,14 @@ for s in $STAGES; do
       python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_spmm.json" \
         "$(python bench.py --print-workload)" || true
       ;;
+    pmc_c5)
+      step pmc_fetch_c5 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c5" -o run -- \
+        python "$ROOT/bench.py" --config c5 --steps 2 --warmup 1 --profile-only
+      step pmc_write_c5 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c5" -o run -- \
+        python "$ROOT/bench.py" --config c5 --steps 2 --warmup 1 --profile-only
+      python tools/pmc_summary.py "$OUT/pmc_fetch_c5" "$OUT/pmc_write_c5" "$OUT/pmc_spmm_c5.json" \
+        "$(python bench.py --config c5 --print-workload)" || true
+      ;;
     *) echo "unknown stage $s"; exit 2 ;;
   esac
 done
