@@ -368,6 +368,12 @@ lpg_status lpg_spmm_set_slice(int64_t cols_per_slice);
  * accumulation order does not change). */
 lpg_status lpg_spmm_set_depth(int64_t edges);
 
+/* Tuning knob for lpg_spmm_f32 (results bitwise identical): 1 (default) = a
+ * row chunk's last (n mod depth) edges are gathered together, predicated per
+ * edge; 0 = one dependent gather at a time (the round-1 form, kept for A/B
+ * runs).  The bf16 kernel always gathers its remainder one by one. */
+lpg_status lpg_spmm_set_remainder(int32_t batched);
+
 /* ---- k-hop neighbour sampling (NeighborLoader collate, train.py:111-116,
  * val.py:22-27; replaces torch_sparse 0.6.12 neighbor_sample) -------------
  * Graph = CSC of the homogeneous LP graph: colptr [N+1], row [E] (sources of

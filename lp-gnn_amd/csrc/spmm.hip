@@ -45,13 +45,17 @@ __device__ __forceinline__ void axpy4(float4 &acc, float v, const float4 &x) {
 // Heavy rows (degree > thresh; SpMM skew, e.g. a dense LP constraint): one block per heavy row
 // and column slice, its 4 waves on interleaved 64-column pieces (lane l of wave w holds columns
 // c0 + 256 q + 64 w + l, q < NV: one float per lane, every gather a contiguous 256 B), HU edges
-// gathered ahead.  The row's chain is split over 4x the waves of a (row, slice) wave, every
+// gathered ahead (HU = 32, the next 64-edge chunk's indices prefetched).  The row's chain is split over 4x the waves of a (row, slice) wave, every
 // element still summed over the row's edges in CSR order (bitwise the same result), so a
 // 6 000-edge row no longer sets the kernel's tail.
+// All (heavy row, slice) units sit at the head of plane 0 (longest rows first: the host passes the
+// rows by decreasing degree), so every long chain starts at the beginning of the launch instead of
+// when its slice's plane is dispatched; the same block ids in the other planes exit at once.
 struct HeavyRows {
-  const int32_t *rows;  // heavy row ids (rows with degree > thresh)
-  int64_t blocks;       // = number of heavy rows: the leading blocks of every y plane
+  const int32_t *rows;  // heavy row ids (rows with degree > thresh), longest first
+  int64_t blocks;       // = number of heavy rows
   int64_t thresh;       // the main waves skip rows with more edges than this
+  int64_t slices;       // column slices of the launch (set by the launcher)
 };
 
 template <int NV, int HU>
@@ -69,13 +73,20 @@ __device__ __forceinline__ void spmm_f32_heavy_row(int64_t row, int64_t c0, int 
   const float *Xs = X + cw;
   int64_t e = rowptr[row];
   const int64_t end = rowptr[row + 1];
+  // the next 64-edge chunk's (col, val) are fetched while this chunk's gathers are in flight
+  int cn = 0;
+  float vn = 0.f;
+  if (e + lane < end) {
+    cn = col[e + lane];
+    vn = val[e + lane];
+  }
   while (e < end) {
     const int n = (int)(end - e < 64 ? end - e : 64);
-    int cl = 0;
-    float vl = 0.f;
-    if (lane < n) {
-      cl = col[e + lane];
-      vl = val[e + lane];
+    const int cl = cn;
+    const float vl = vn;
+    if (e + 64 + lane < end) {
+      cn = col[e + 64 + lane];
+      vn = val[e + 64 + lane];
     }
     int j = 0;
     for (; j + HU <= n; j += HU) {
@@ -108,19 +119,24 @@ __device__ __forceinline__ void spmm_f32_heavy_row(int64_t row, int64_t c0, int 
 }
 
 // ---------------------------------------------------------------- fp32 wide
-template <int NV, int U, bool FULL>
+// REMB: the chunk's last n mod U edges are gathered together too (predicated per edge, wave-uniform)
+// instead of one dependent load at a time: a row of 20 edges costs 3 memory round trips, not 6,
+// and rows shorter than U (most rows of a skewed LP) one.  Same edges, same order: same bits.
+template <int NV, int U, bool FULL, bool REMB = true>
 __global__ __launch_bounds__(kBlock) void spmm_f32_rowwave(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
     float *__restrict__ Y, int64_t ldy, int64_t F, HeavyRows hv) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if ((int64_t)blockIdx.x < hv.blocks) {  // heavy rows first: dispatched at the head of each plane
-    spmm_f32_heavy_row<NV, 16>(hv.rows[blockIdx.x], (int64_t)blockIdx.y * (NV * 256), wave, rowptr, col, val, X,
-                               ldx, Y, ldy, F);
+  const int64_t hb = hv.blocks * hv.slices;
+  if ((int64_t)blockIdx.x < hb) {  // heavy (row, slice) units: all at the head of plane 0
+    if (blockIdx.y != 0) return;
+    const int64_t hr = (int64_t)blockIdx.x / hv.slices, sl = (int64_t)blockIdx.x % hv.slices;
+    spmm_f32_heavy_row<NV, 32>(hv.rows[hr], sl * (NV * 256), wave, rowptr, col, val, X, ldx, Y, ldy, F);
     return;
   }
-  const int64_t row = ((int64_t)blockIdx.x - hv.blocks) * kWavesPerBlock + wave;
+  const int64_t row = ((int64_t)blockIdx.x - hb) * kWavesPerBlock + wave;
   if (row >= n_rows) return;
   if (rowptr[row + 1] - rowptr[row] > hv.thresh) return;  // a heavy row: done by the units above
   const int64_t c0 = (int64_t)blockIdx.y * (NV * 256);
@@ -160,6 +176,28 @@ __global__ __launch_bounds__(kBlock) void spmm_f32_rowwave(
 #pragma unroll
         for (int q = 0; q < NV; ++q) axpy4(acc[q], v, xv[k][q]);
       }
+    }
+    if (REMB && j < n) {
+      const int rem = n - j;  // 1 .. U-1, wave-uniform
+      float4 xv[U][NV];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (k < rem) {
+          const float *xr = Xs + (int64_t)bcast_i(cl, j + k) * ldx;
+#pragma unroll
+          for (int q = 0; q < NV; ++q)
+            xv[k][q] = ok[q] ? *reinterpret_cast<const float4 *>(xr + q * 256) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (k < rem) {
+          const float v = bcast_f(vl, j + k);
+#pragma unroll
+          for (int q = 0; q < NV; ++q) axpy4(acc[q], v, xv[k][q]);
+        }
+      }
+      j = n;
     }
     for (; j < n; ++j) {
       const float *xr = Xs + (int64_t)bcast_i(cl, j) * ldx;
@@ -341,6 +379,8 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
 
 int64_t g_slice_cols = 0;  // lpg_spmm_set_slice; 0 = auto
 int g_depth = 0;           // lpg_spmm_set_depth: edges gathered ahead per wave (0 = auto)
+int g_remb = 1;            // lpg_spmm_set_remainder (fp32 rowwave): chunk remainder gathered together (1) or one
+                           // by one (the bf16 kernel keeps one by one: batched, it measured 7-55 % slower)
 
 lpg_status check_csr(const lpg_csr *A) {
   LPG_REQUIRE(A != nullptr, "lpg_spmm: A is NULL");
@@ -363,9 +403,17 @@ lpg_status launch_wide_f32(const lpg_csr *A, const float *X, int64_t ldx, float 
                            int64_t F, hipStream_t s, HeavyRows hv) {
   const int64_t W = NV * 256;
   const int64_t slices = (F + W - 1) / W;
-  const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock + hv.blocks;
+  hv.slices = slices;
+  const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock + hv.blocks * slices;
   LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_f32: grid too large");
   dim3 grid((unsigned)nblk, (unsigned)slices);
+  if (!g_remb) {  // the one-load-at-a-time remainder (A/B knob, lpg_spmm_set_remainder(0))
+    if (F % W == 0)
+      return launch(spmm_f32_rowwave<NV, U, true, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
+                    Y, ldy, F, hv);
+    return launch(spmm_f32_rowwave<NV, U, false, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
+                  Y, ldy, F, hv);
+  }
   if (F % W == 0)
     return launch(spmm_f32_rowwave<NV, U, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
                   Y, ldy, F, hv);
@@ -403,6 +451,12 @@ extern "C" lpg_status lpg_spmm_set_slice(int64_t cols) {
   LPG_REQUIRE(cols == 0 || cols == 256 || cols == 512 || cols == 1024,
               "lpg_spmm_set_slice: cols must be 0 (auto), 256, 512 or 1024, got %lld", (long long)cols);
   g_slice_cols = cols;
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_spmm_set_remainder(int32_t batched) {
+  LPG_REQUIRE(batched == 0 || batched == 1, "lpg_spmm_set_remainder: %d not in {0, 1}", batched);
+  g_remb = batched;
   return LPG_OK;
 }
 
@@ -444,7 +498,10 @@ static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, f
   // gathered at a time and stays resident in the 256 MiB Infinity Cache;
   // measured ~3 % faster than full-width rows at c2 (profiles/r01_kbench*).
   if (W == 0) W = 256;
-  const int U = g_depth == 0 ? 8 : g_depth;
+  // auto depth: 16 edges in flight for rows of >= 16 edges on average (c2 cons<-vars, degree 20: 0.947
+  // of the edge-gather roofline vs 0.913 at 8), else 8 (vars<-cons, degree 10: 0.938 vs 0.915; a
+  // skewed LP, whose light rows average 5 edges once its heavy rows are split off: 0.98 vs 0.89)
+  const int U = g_depth != 0 ? g_depth : (hv.blocks == 0 && A->nnz >= 16 * A->n_rows) ? 16 : 8;
   if (W == 256) {
     if (U == 16) return launch_wide_f32<1, 16>(A, X, ldx, Y, ldy, F, s, hv);
     if (U == 32) return launch_wide_f32<1, 32>(A, X, ldx, Y, ldy, F, s, hv);
@@ -459,7 +516,7 @@ static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, f
 
 extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
                                    int64_t F, void *stream) {
-  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX}, stream);
+  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, stream);
 }
 
 extern "C" lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
@@ -468,7 +525,7 @@ extern "C" lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64
   LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_f32_heavy: negative n_heavy / thresh");
   LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_f32_heavy: heavy_rows is NULL");
   LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_f32_heavy: more heavy rows than rows");
-  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX}, stream);
+  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1}, stream);
 }
 
 extern "C" lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,

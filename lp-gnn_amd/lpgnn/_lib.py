@@ -30,6 +30,7 @@ HEADER_SYMBOLS = (
     "lpg_spmm_bf16",
     "lpg_spmm_set_slice",
     "lpg_spmm_set_depth",
+    "lpg_spmm_set_remainder",
     "lpg_fc_f32",
     "lpg_fc_set_variant",
     "lpg_fc_bf16",
@@ -105,6 +106,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_spmm_set_slice.argtypes = [c_i64]
     L.lpg_spmm_set_slice.restype = c_i32
     L.lpg_spmm_set_depth.argtypes = [c_i64]
+    L.lpg_spmm_set_remainder.argtypes = [c_i32]
+    L.lpg_spmm_set_remainder.restype = c_i32
     L.lpg_spmm_set_depth.restype = c_i32
     L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
                              c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_p]

@@ -68,7 +68,10 @@ class CSR:
         the graph's first SpMM, none per layer)."""
         cache = self.__dict__.setdefault("_heavy", {})
         if thresh not in cache:
-            idx = torch.nonzero(self.degrees() > thresh).view(-1).to(torch.int32)
+            deg = self.degrees()
+            idx = torch.nonzero(deg > thresh).view(-1)
+            # longest rows first: their chains start at the head of the launch (lpg_spmm_f32_heavy)
+            idx = idx[torch.argsort(deg[idx], descending=True, stable=True)].to(torch.int32)
             cache[thresh] = (idx, int(idx.numel()))
         return cache[thresh]
 

@@ -276,3 +276,35 @@ def test_degree_aware_heavy_rows_bitwise(thresh, Fd, slice_cols, monkeypatch):
                 assert csr.heavy_rows(thresh)[1] > 0
     finally:
         L.lpg_spmm_set_slice(0)
+
+
+@pytest.mark.parametrize("depth", [8, 16, 32])
+@pytest.mark.parametrize("Fd,dt", [(1024, torch.float32), (300, torch.float32), (2048, torch.float32)])
+def test_batched_remainder_bitwise(depth, Fd, dt):
+    """lpg_spmm_set_remainder: the chunk remainder gathered together (default) or one
+    gather at a time give the same bits, equal to the oracle loop; degrees 0..150 so
+    every remainder length 0 .. depth-1 occurs, and rows cross the 64-edge chunks."""
+    from lpgnn import _lib
+    from lpgnn.sparse import spmm_forward
+
+    rng = np.random.default_rng(depth + Fd)
+    m, n = 700, 900
+    deg = rng.integers(0, 151, m)
+    row = np.repeat(np.arange(m), deg)
+    col = np.concatenate([rng.choice(n, d, replace=False) for d in deg]).astype(np.int64)
+    val = rng.uniform(-1, 1, len(row)).astype(np.float32)
+    adj = _adj(row, col, val, m, n)
+    X = torch.from_numpy(rng.standard_normal((n, Fd)).astype(np.float32)).to(dt)
+    L = _lib.lib()
+    outs = []
+    try:
+        L.lpg_spmm_set_depth(depth)
+        for rb in (1, 0):
+            L.lpg_spmm_set_remainder(rb)
+            outs.append(spmm_forward(adj.fwd, X.to(DEV)).cpu())
+    finally:
+        L.lpg_spmm_set_depth(0)
+        L.lpg_spmm_set_remainder(1)
+    assert torch.equal(outs[0], outs[1])
+    A, _ = _oracle_pair(row, col, val, m, n)
+    assert np.array_equal(outs[0].numpy(), O.spmm_f32(*A, X.numpy()))

@@ -113,20 +113,53 @@ def _spmm_graph(out, L, gname, g, spmm_forward, BipartiteCSR):
         X = torch.randn(K, 1024, device="cuda")
         fns = {}
         ref = spmm_forward(csr, X)
-        for sl, u in ((1024, 0), (512, 8), (512, 16), (256, 8), (256, 16), (256, 32)):
-            def f(sl=sl, u=u):
+        from lpgnn import sparse as S
+        h0 = S.HEAVY_THRESH
+        for sl, u, h, rb in ((256, 8, h0, 0), (256, 8, h0, 1), (256, 16, h0, 1), (256, 32, h0, 1), (512, 8, h0, 1),
+                             (256, 8, 0, 1), (256, 16, 0, 1), (256, 8, 256, 1)):
+            def f(sl=sl, u=u, h=h, rb=rb):
                 L.lpg_spmm_set_slice(sl)
                 L.lpg_spmm_set_depth(u)
+                L.lpg_spmm_set_remainder(rb)  # 1: a chunk's last n mod depth edges gathered together
+                S.HEAVY_THRESH = h  # degree-aware split: rows above h on (row, 64-column) waves; 0 = off
                 return spmm_forward(csr, X)
             assert torch.equal(f(), ref)
-            fns[f"slice{sl} depth{u}"] = f
+            fns[f"slice{sl} depth{u} heavy>{h} rem{'B' if rb else '1'}"] = f
         t = timeit(fns)
         L.lpg_spmm_set_slice(0)
         L.lpg_spmm_set_depth(0)
+        L.lpg_spmm_set_remainder(1)
+        S.HEAVY_THRESH = h0
         B = g.nnz * 1024 * 4 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 1024 * 4
         for k, v in t.items():
             out[f"spmm {gname} {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000,
                                                    max_deg=int(csr.degrees().max().item()))
+
+
+def bench_spmm16(out):
+    """bf16 SpMM at the c5 width (F = 2048), both directions, remainder batched or not."""
+    from lpgnn import BipartiteCSR, _lib, synth
+    from lpgnn.sparse import spmm_forward
+
+    L = _lib.lib()
+    for gname, g in (("uniform", synth.uniform_lp(100_000, 200_000, 2_000_000, seed=0)),
+                     ("skewed", synth.skewed_lp(100_000, 200_000, 2_000_000, seed=0))):
+        adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
+        for name, csr, K in (("cons<-vars", adj.fwd, g.n), ("vars<-cons", adj.bwd, g.m)):
+            X = torch.randn(K, 2048, device="cuda").to(torch.bfloat16)
+            ref = spmm_forward(csr, X)
+            fns = {}
+            for rb in (0, 1):
+                def f(rb=rb):
+                    L.lpg_spmm_set_remainder(rb)
+                    return spmm_forward(csr, X)
+                assert torch.equal(f(), ref)
+                fns[f"rem{'B' if rb else '1'} (bf16 ignores the knob)"] = f
+            t = timeit(fns)
+            L.lpg_spmm_set_remainder(1)
+            B = g.nnz * 2048 * 2 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 2048 * 2
+            for k, v in t.items():
+                out[f"spmm bf16 {gname} {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000)
 
 
 def bench_fcpmc(out):
@@ -292,7 +325,7 @@ if __name__ == "__main__":
     out = {}
     for w in which:
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
-         "bf16bwd": bench_bf16bwd,
+         "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
          "load": bench_load, "fcpi": bench_fcpi}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
