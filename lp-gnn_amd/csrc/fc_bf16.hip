@@ -24,11 +24,15 @@
 #include "common.h"
 #include "fc_common.h"
 
+#include <type_traits>
+
 namespace lpg {
 namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BK = 64;
 
@@ -85,23 +89,44 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    // the element loop with the addend / dropout choices made once (uniform branches per element
+    // cost more than the arithmetic), RNE to bf16 in pairs by v_cvt_pk_bf16_f32
+    auto body = [&](auto acc_c, auto drop_c) {
+      constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int64_t col = wcol0 + j * 16 + fr;
-      const float bb = (a.bias && col < a.N) ? a.bias[col] : 0.f;
+      for (int j = 0; j < FN; ++j) {
+        const int64_t col = wcol0 + j * 16 + fr;
+        const float bb = (a.bias && col < a.N) ? a.bias[col] : 0.f;
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
+        for (int i = 0; i < FM; ++i) {
+          float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int lr = i * 16 + fq * 4 + r;
-          float v = acc[i][j][r];
-          if (a.accum) v = v + bf16_to_f32(*reinterpret_cast<const uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2));
-          v = v + bb;
-          if (RELU) v = v < 0.f ? 0.f : v;
-          if (a.drop_thresh) v = drop_hash(a.seed, wrow0 + lr, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-          *reinterpret_cast<uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2) = to_bf16_rne(v);
+          for (int r = 0; r < 4; ++r) {
+            const int lr = i * 16 + fq * 4 + r;
+            v[r] = acc[i][j][r];
+            if constexpr (ACC)
+              v[r] = v[r] + bf16_to_f32(*reinterpret_cast<const uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2));
+            v[r] = v[r] + bb;
+            if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
+            if constexpr (DROP) v[r] = drop_hash(a.seed, wrow0 + lr, col) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const int lr = i * 16 + fq * 4 + r;
+            const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[r], v[r + 1]}, bf16x2));
+            *reinterpret_cast<uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2) = (uint16_t)pk;
+            *reinterpret_cast<uint16_t *>(img + (lr + 1) * EP_PITCH + (j * 16 + fr) * 2) = (uint16_t)(pk >> 16);
+          }
         }
       }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    const bool drop = RELU && a.drop_thresh;
+    if (a.accum) {
+      if (drop) body(T_{}, T_{}); else body(T_{}, F_{});
+    } else {
+      if (drop) body(F_{}, T_{}); else body(F_{}, F_{});
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

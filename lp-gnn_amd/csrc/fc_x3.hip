@@ -830,32 +830,44 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) hs[c][i][r] = 0.f;
   }
+  // the element loop with the bias / dropout choices made once (uniform branches per element cost
+  // more than the arithmetic)
+  auto body = [&](auto bias_c, auto drop_c) {
+    constexpr bool BIAS = decltype(bias_c)::value, DROP = decltype(drop_c)::value;
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int64_t col = nw + j * 16 + fr;
-    if (col >= a.N) continue;
-    const float bb = a.bias ? a.bias[col] : 0.f;
-    float hwv[HEADS ? 4 : 1];
-    if constexpr (HEADS) {
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = nw + j * 16 + fr;
+      if (col >= a.N) continue;
+      const float bb = BIAS ? a.bias[col] : 0.f;
+      float hwv[HEADS ? 4 : 1];
+      if constexpr (HEADS) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) hwv[c] = c < a.hn ? a.hw[c * a.ldhw + col] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = mw + i * 16 + 4 * fg + r;
-        if (row >= a.M) continue;
-        float v = acc[i][j][r];
-        if (a.bias) v = v + bb;
-        if (RELU) v = (v < 0.f) ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-        a.C[row * a.ldc + col] = v;
-        if constexpr (HEADS) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
-        }
+        for (int c = 0; c < 4; ++c) hwv[c] = c < a.hn ? a.hw[c * a.ldhw + col] : 0.f;
       }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = mw + i * 16 + 4 * fg + r;
+          if (row >= a.M) continue;
+          float v = acc[i][j][r];
+          if constexpr (BIAS) v = v + bb;
+          if (RELU) v = (v < 0.f) ? 0.f : v;
+          if constexpr (DROP) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+          a.C[row * a.ldc + col] = v;
+          if constexpr (HEADS) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
+          }
+        }
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (a.bias) {
+    if (a.drop_thresh) body(T_{}, T_{}); else body(T_{}, F_{});
+  } else {
+    if (a.drop_thresh) body(F_{}, T_{}); else body(F_{}, F_{});
   }
   if constexpr (HEADS) {  // sum over the 16 lanes (columns) of each row group, fixed DPP order; lane fr = 0 writes
     const int64_t pidx = nw / BN;

@@ -1,0 +1,20 @@
+#!/bin/bash
+# round-2 GPU session c: full GPU tests, then the c2 and c5 benches
+mkdir -p gpurun_out && export TMPDIR=/tmp
+run() {  # run <name> <timeout> <cmd...>: stops the session on a crash/abort/timeout (exit >= 2)
+  local name=$1 tmo=$2; shift 2
+  timeout -k 10 "$tmo" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -3 "gpurun_out/$name.log"
+  if [ $rc -ge 2 ]; then tail -30 "gpurun_out/$name.log"; exit $rc; fi
+}
+for s in ${*:-tests c2 c5}; do
+  case $s in
+    tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    c2) run bench_c2 600 python -u bench.py ;;
+    c5) run bench_c5 600 python -u bench.py --config c5 --steps 10 --warmup 3 ;;
+    kbf16) run kbench_bf16 400 python -u tools/kbench.py bf16 bf16bwd ;;
+    *) echo "unknown stage $s"; exit 2 ;;
+  esac
+done
