@@ -174,6 +174,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # LPGNN_DIST_BACKEND=gloo: a rehearsal of the N-rank path with several ranks sharing the visible
+    # GPU(s) (host-staged exchanges); the measured runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("LPGNN_DIST_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"LPGNN_DIST_BACKEND={backend}: nccl or gloo")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     distributed = world > 1 or args.partitioned
@@ -182,7 +189,10 @@ def main():
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        if backend == "gloo":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     import lpgnn
     from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
@@ -277,6 +287,8 @@ def main():
     achieved = bytes_total / (spmm_ms / 1e3) / 1e9 if spmm_ms > 0 else 0.0
     per_launch_bytes = bytes_total / max(launches, 1)
     traffic, traffic_src = load_pmc_traffic(workload)
+    if distributed and backend != "nccl":
+        workload += f" [rehearsal: {world} ranks over {backend} sharing {torch.cuda.device_count()} GPU(s)]"
     out = {
         "metric": "edges/sec bipartite SpMM (hid=1024, depth=3) at 1/2/4/8 MI355X; % HBM roofline",
         "value": value,

@@ -306,6 +306,12 @@ __global__ __launch_bounds__(kT) void linear_small_bwd_p1(int64_t M, int64_t K, 
   const int64_t r1 = r0 + kRowsLinear < M ? r0 + kRowsLinear : M;
   const int64_t tot = N * K + N + (MASK ? K : 0);
   float *pw = part + (int64_t)blockIdx.x * tot;  // [N][K], db[N], (MASK) dbY[K]
+  // db = sum_m G[m, c] in row order, accumulated beside the rows' other work by every thread (the
+  // same sums; thread 0 stores them) -- a separate loop after it was 128 dependent loads per block
+  float sg[N];
+#pragma unroll
+  for (int c = 0; c < N; ++c) sg[c] = 0.f;
+  bool first = true;
   for (int64_t k = (int64_t)threadIdx.x * 4; k < K; k += kT * 4) {
     float4 w[N], acc[N];
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -319,6 +325,7 @@ __global__ __launch_bounds__(kT) void linear_small_bwd_p1(int64_t M, int64_t K, 
 #pragma unroll
       for (int c = 0; c < N; ++c) {
         const float gc = G[m * ldg + c];
+        if (first) sg[c] = sg[c] + gc;
         d.x = d.x + gc * w[c].x; d.y = d.y + gc * w[c].y; d.z = d.z + gc * w[c].z; d.w = d.w + gc * w[c].w;
         acc[c].x = acc[c].x + gc * h.x; acc[c].y = acc[c].y + gc * h.y;
         acc[c].z = acc[c].z + gc * h.z; acc[c].w = acc[c].w + gc * h.w;
@@ -344,11 +351,16 @@ __global__ __launch_bounds__(kT) void linear_small_bwd_p1(int64_t M, int64_t K, 
 #pragma unroll
     for (int c = 0; c < N; ++c) *reinterpret_cast<float4 *>(pw + c * K + k) = acc[c];
     if (MASK) *reinterpret_cast<float4 *>(pw + N * K + N + k) = cs;
+    first = false;
   }
-  if (threadIdx.x < (unsigned)N) {
-    float sgc = 0.f;
-    for (int64_t m = r0; m < r1; ++m) sgc = sgc + G[m * ldg + threadIdx.x];
-    pw[N * K + threadIdx.x] = sgc;
+  if (threadIdx.x == 0) {
+    if (first) {  // (no column pass ran on this thread: K == 0)
+      for (int64_t m = r0; m < r1; ++m)
+#pragma unroll
+        for (int c = 0; c < N; ++c) sg[c] = sg[c] + G[m * ldg + c];
+    }
+#pragma unroll
+    for (int c = 0; c < N; ++c) pw[N * K + c] = sg[c];
   }
 }
 
