@@ -132,7 +132,9 @@ __global__ __launch_bounds__(kBlock) void spmm_f32_rowwave(
   const int64_t hb = hv.blocks * hv.slices;
   if ((int64_t)blockIdx.x < hb) {  // heavy (row, slice) units: all at the head of plane 0
     if (blockIdx.y != 0) return;
-    const int64_t hr = (int64_t)blockIdx.x / hv.slices, sl = (int64_t)blockIdx.x % hv.slices;
+    // 32-bit division (the 64-bit expansion uses v_fmamk_f32, which the no-FMA ISA guard rejects)
+    const uint32_t hs = (uint32_t)hv.slices, bxu = blockIdx.x;
+    const int64_t hr = bxu / hs, sl = bxu % hs;
     spmm_f32_heavy_row<NV, 32>(hv.rows[hr], sl * (NV * 256), wave, rowptr, col, val, X, ldx, Y, ldy, F);
     return;
   }
