@@ -220,6 +220,76 @@ __global__ __launch_bounds__(kBlock) void spmm_f32_rowwave(
     if (ok[q]) *reinterpret_cast<float4 *>(yr + q * 256) = acc[q];
 }
 
+// ------------------------------------------------------- fp32 narrow slices
+// For gathered tables far above the 256 MiB Infinity Cache (c4: a [4M, 1024] fp32 table is 16 GB, a
+// 256-column slice still 4 GB): one wave per (row, 64*CW-column slice), lane l holding columns
+// c0 + CW*l .. +CW-1 (CW = 2: 512 B per gather, CW = 1: 256 B), so a slice of the table is 2-4x
+// smaller than at 256 columns.  Same edge order, the chunk remainder gathered together: the same bits.
+template <int CW> struct VecF;
+template <> struct VecF<1> { typedef float T; };
+template <> struct VecF<2> { typedef float2 T; };
+
+__device__ __forceinline__ void axpyv(float &acc, float v, float x) { acc = acc + v * x; }
+__device__ __forceinline__ void axpyv(float2 &acc, float v, float2 x) {
+  acc.x = acc.x + v * x.x;
+  acc.y = acc.y + v * x.y;
+}
+__device__ __forceinline__ void zerov(float &a) { a = 0.f; }
+__device__ __forceinline__ void zerov(float2 &a) { a = make_float2(0.f, 0.f); }
+
+template <int CW, int U>
+__global__ __launch_bounds__(kBlock) void spmm_f32_rowslim(int64_t n_rows, const int64_t *__restrict__ rowptr,
+                                                           const int32_t *__restrict__ col,
+                                                           const float *__restrict__ val, const float *__restrict__ X,
+                                                           int64_t ldx, float *__restrict__ Y, int64_t ldy, int64_t F) {
+  typedef typename VecF<CW>::T V;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (row >= n_rows) return;
+  const int64_t c0 = (int64_t)blockIdx.y * (64 * CW);
+  const bool ok = c0 + lane * CW < F;
+  V acc;
+  zerov(acc);
+  const float *Xs = X + c0 + lane * CW;
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  while (e < end) {
+    const int n = (int)(end - e < 64 ? end - e : 64);
+    int cl = 0;
+    float vl = 0.f;
+    if (lane < n) {
+      cl = col[e + lane];
+      vl = val[e + lane];
+    }
+    int j = 0;
+    for (; j + U <= n; j += U) {
+      V xv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (ok) xv[k] = *reinterpret_cast<const V *>(Xs + (int64_t)bcast_i(cl, j + k) * ldx); else zerov(xv[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) axpyv(acc, bcast_f(vl, j + k), xv[k]);
+    }
+    if (j < n) {
+      const int rem = n - j;  // wave-uniform
+      V xv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (k < rem) {
+          if (ok) xv[k] = *reinterpret_cast<const V *>(Xs + (int64_t)bcast_i(cl, j + k) * ldx); else zerov(xv[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (k < rem) axpyv(acc, bcast_f(vl, j + k), xv[k]);
+    }
+    e += n;
+  }
+  if (ok) *reinterpret_cast<V *>(Y + row * ldy + c0 + lane * CW) = acc;
+}
+
 // -------------------------------------------------------------- fp32 narrow
 // F <= FW <= 64: FW lanes per row, 256/FW rows per block (conv1, F = 8).
 template <int FW, int U>
@@ -450,8 +520,8 @@ lpg_status launch_wide_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, ui
 using namespace lpg;
 
 extern "C" lpg_status lpg_spmm_set_slice(int64_t cols) {
-  LPG_REQUIRE(cols == 0 || cols == 256 || cols == 512 || cols == 1024,
-              "lpg_spmm_set_slice: cols must be 0 (auto), 256, 512 or 1024, got %lld", (long long)cols);
+  LPG_REQUIRE(cols == 0 || cols == 64 || cols == 128 || cols == 256 || cols == 512 || cols == 1024,
+              "lpg_spmm_set_slice: cols must be 0 (auto), 64, 128, 256, 512 or 1024, got %lld", (long long)cols);
   g_slice_cols = cols;
   return LPG_OK;
 }
@@ -499,11 +569,23 @@ static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, f
   // (blockIdx.y major), so only a quarter-width source table is being
   // gathered at a time and stays resident in the 256 MiB Infinity Cache;
   // measured ~3 % faster than full-width rows at c2 (profiles/r01_kbench*).
-  if (W == 0) W = 256;
+  // auto: 128-column slices (2 floats per lane, 512-B gathers; measured 0.95 / 0.99 of the edge-gather
+  // roofline at c2 vs 0.93 / 0.94 at 256, profiles/r02_kbench_spmm_big.log) unless heavy rows are split
+  // off, which the 256-column form does
+  if (W == 0) W = hv.blocks == 0 ? 128 : 256;
   // auto depth: 16 edges in flight for rows of >= 16 edges on average (c2 cons<-vars, degree 20: 0.947
   // of the edge-gather roofline vs 0.913 at 8), else 8 (vars<-cons, degree 10: 0.938 vs 0.915; a
   // skewed LP, whose light rows average 5 edges once its heavy rows are split off: 0.98 vs 0.89)
   const int U = g_depth != 0 ? g_depth : (hv.blocks == 0 && A->nnz >= 16 * A->n_rows) ? 16 : 8;
+  if ((W == 64 || W == 128) && hv.blocks == 0) {  // narrow slices (no heavy-row split in this form)
+    dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock), (unsigned)((F + W - 1) / W));
+    if (W == 128)
+      return U == 16 ? launch(spmm_f32_rowslim<2, 16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F)
+                     : launch(spmm_f32_rowslim<2, 8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    return U == 16 ? launch(spmm_f32_rowslim<1, 16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F)
+                   : launch(spmm_f32_rowslim<1, 8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+  }
+  if (W == 64 || W == 128) W = 256;
   if (W == 256) {
     if (U == 16) return launch_wide_f32<1, 16>(A, X, ldx, Y, ldy, F, s, hv);
     if (U == 32) return launch_wide_f32<1, 32>(A, X, ldx, Y, ldy, F, s, hv);

@@ -61,7 +61,7 @@ def test_widths_bitwise(Fd):
     assert np.array_equal(spmm_forward(adj.bwd, torch.from_numpy(Xc).to(DEV)).cpu().numpy(), O.spmm_f32(*AT, Xc))
 
 
-@pytest.mark.parametrize("slice_cols", [256, 512, 1024])
+@pytest.mark.parametrize("slice_cols", [64, 128, 256, 512, 1024])
 def test_slice_widths_bitwise(slice_cols):
     from lpgnn import _lib
     from lpgnn.sparse import spmm_forward

@@ -136,6 +136,39 @@ def _spmm_graph(out, L, gname, g, spmm_forward, BipartiteCSR):
                                                    max_deg=int(csr.degrees().max().item()))
 
 
+def bench_spmmbig(out):
+    """fp32 SpMM slice widths on graphs whose gathered table is far above the Infinity Cache: a c4
+    rank's share at N = 8 (250K x 500K, nnz 5M) and the whole c4 graph (2M x 4M, nnz 40M); c2 beside."""
+    from lpgnn import BipartiteCSR, _lib, synth
+    from lpgnn.sparse import spmm_forward
+
+    L = _lib.lib()
+    for gname, (m, n, nnz) in (("c2", (100_000, 200_000, 2_000_000)), ("c4/8", (250_000, 500_000, 5_000_000)),
+                               ("c4", (2_000_000, 4_000_000, 40_000_000))):
+        g = synth.uniform_lp(m, n, nnz, seed=0)
+        adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
+        del g
+        for name, csr, K in (("cons<-vars", adj.fwd, n), ("vars<-cons", adj.bwd, m)):
+            X = torch.randn(K, 1024, device="cuda")
+            ref = spmm_forward(csr, X)
+            fns = {}
+            for sl in (256, 128, 64):
+                def f(sl=sl):
+                    L.lpg_spmm_set_slice(sl)
+                    return spmm_forward(csr, X)
+                assert torch.equal(f(), ref)
+                fns[f"slice{sl}"] = f
+            t = timeit(fns, rounds=5, iters=3)
+            L.lpg_spmm_set_slice(0)
+            rows = csr.n_rows
+            B = nnz * 1024 * 4 + nnz * 8 + (rows + 1) * 8 + rows * 1024 * 4
+            for k, v in t.items():
+                out[f"spmm {gname} {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000)
+            del X, ref
+        del adj
+        torch.cuda.empty_cache()
+
+
 def bench_spmm16(out):
     """bf16 SpMM at the c5 width (F = 2048), both directions, remainder batched or not."""
     from lpgnn import BipartiteCSR, _lib, synth
@@ -326,6 +359,7 @@ if __name__ == "__main__":
     for w in which:
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
+         "spmmbig": bench_spmmbig,
          "load": bench_load, "fcpi": bench_fcpi}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
