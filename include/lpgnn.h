@@ -98,12 +98,13 @@ lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx,
 
 /* lpg_spmm_f32 with degree-aware scheduling for skewed rows: heavy_rows
  * (device int32 [n_heavy]) must list exactly the rows of A with more than
- * `thresh` edges (any order).  Those rows run as (row, 64-column) wave units
- * at the head of the grid instead of (row, 256-column) units, so a long
- * constraint row's sequential chain is spread over 4x the waves; every
- * element is still summed over its row's edges in CSR order -- the result
- * is bitwise lpg_spmm_f32's.  F < 256 and unaligned shapes ignore the list.
- * Same fwd/bwd use as lpg_spmm_f32 (torch_sparse spmm_sum / SPMMSum). */
+ * `thresh` edges (longest first is fastest).  Those rows run as (row,
+ * 64-column) wave units, all at the head of the launch, instead of (row,
+ * 128/256-column) units, so a long constraint row's sequential chain is
+ * spread over 4x the waves and starts first; every element is still summed
+ * over its row's edges in CSR order -- the result is bitwise lpg_spmm_f32's.
+ * F < 256 and unaligned shapes ignore the list.  Same fwd/bwd use as
+ * lpg_spmm_f32 (torch_sparse spmm_sum / SPMMSum). */
 lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64_t ldx,
                               float *Y, int64_t ldy, int64_t F,
                               const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
@@ -113,6 +114,12 @@ lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64_t ldx,
  * accumulated row is rounded to bf16 once (round-to-nearest-even). */
 lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
                          uint16_t *Y, int64_t ldy, int64_t F, void *stream);
+/* ... and its degree-aware form (heavy_rows as lpg_spmm_f32_heavy; the heavy
+ * units are (row, 128-column) waves); bitwise lpg_spmm_bf16's result. */
+lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx,
+                               uint16_t *Y, int64_t ldy, int64_t F,
+                               const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
+                               void *stream);
 
 /* ---- dense FC (replaces GraphConv's lin_rel + lin_root + ReLU) ----------- */
 

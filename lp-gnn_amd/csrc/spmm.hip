@@ -434,6 +434,129 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
   }
 }
 
+// bf16 heavy rows (degree > thresh): one block per (heavy row, 512-column piece), wave w on columns
+// c0 + 128 w + 2 l, +1 (4-B gathers, 256 B per wave-instruction), 32 gathers in flight and the next
+// 64-edge chunk's indices prefetched -- 4x the waves on one long row's chain, each element still
+// summed in CSR order (the same bits).
+__device__ __forceinline__ void spmm_bf16_heavy_row(int64_t row, int64_t c0, int wave,
+                                                    const int64_t *__restrict__ rowptr,
+                                                    const int32_t *__restrict__ col, const float *__restrict__ val,
+                                                    const uint16_t *__restrict__ X, int64_t ldx,
+                                                    uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
+  constexpr int HU = 32;
+  const int lane = threadIdx.x & 63;
+  const int64_t cw = c0 + wave * 128 + lane * 2;
+  const bool ok = cw < F;
+  float a0 = 0.f, a1 = 0.f;
+  const uint16_t *Xs = X + cw;
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  int cn = 0;
+  float vn = 0.f;
+  if (e + lane < end) {
+    cn = col[e + lane];
+    vn = val[e + lane];
+  }
+  while (e < end) {
+    const int n = (int)(end - e < 64 ? end - e : 64);
+    const int cl = cn;
+    const float vl = vn;
+    if (e + 64 + lane < end) {
+      cn = col[e + 64 + lane];
+      vn = val[e + 64 + lane];
+    }
+    for (int j = 0; j < n; j += HU) {
+      const int rem = n - j < HU ? n - j : HU;  // wave-uniform
+      uint32_t xv[HU];
+#pragma unroll
+      for (int k = 0; k < HU; ++k)
+        if (k < rem) xv[k] = ok ? *reinterpret_cast<const uint32_t *>(Xs + (int64_t)bcast_i(cl, j + k) * ldx) : 0u;
+#pragma unroll
+      for (int k = 0; k < HU; ++k)
+        if (k < rem) {
+          const float v = bcast_f(vl, j + k);
+          a0 = a0 + v * bf16_to_f32(xv[k] & 0xffffu);
+          a1 = a1 + v * bf16_to_f32(xv[k] >> 16);
+        }
+    }
+    e += n;
+  }
+  if (ok) *reinterpret_cast<uint32_t *>(Y + row * ldy + cw) = f32_to_bf16_rne(a0) | (f32_to_bf16_rne(a1) << 16);
+}
+
+// bf16 narrow slices: one wave per (row, 256-column slice), lane l holding columns c0 + 4l .. +3
+// (8-B gathers, 512 B per wave-instruction), fp32 accumulation, one RNE rounding -- the bf16 twin of
+// spmm_f32_rowslim (a slice of the c5 [200K, 2048] bf16 table is 102 MB instead of the whole 820 MB),
+// the chunk remainder gathered together.  Same edge order: the same bits as spmm_bf16_rowwave.
+template <int U>
+__global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, const int64_t *__restrict__ rowptr,
+                                                            const int32_t *__restrict__ col,
+                                                            const float *__restrict__ val,
+                                                            const uint16_t *__restrict__ X, int64_t ldx,
+                                                            uint16_t *__restrict__ Y, int64_t ldy, int64_t F,
+                                                            HeavyRows hv) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t hb = hv.blocks * hv.slices;  // heavy (row, 512-column piece) units: the head of plane 0
+  if ((int64_t)blockIdx.x < hb) {
+    if (blockIdx.y != 0) return;
+    const uint32_t hs = (uint32_t)hv.slices, bxu = blockIdx.x;
+    spmm_bf16_heavy_row(hv.rows[bxu / hs], (int64_t)(bxu % hs) * 512, wave, rowptr, col, val, X, ldx, Y, ldy, F);
+    return;
+  }
+  const int64_t row = ((int64_t)blockIdx.x - hb) * kWavesPerBlock + wave;
+  if (row >= n_rows) return;
+  if (rowptr[row + 1] - rowptr[row] > hv.thresh) return;  // a heavy row: done by the units above
+  const int64_t c0 = (int64_t)blockIdx.y * 256;
+  const bool ok = c0 + lane * 4 < F;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const uint16_t *Xs = X + c0 + lane * 4;
+  auto axpy = [&](float v, uint2 x) {
+    acc[0] = acc[0] + v * bf16_to_f32(x.x & 0xffffu);
+    acc[1] = acc[1] + v * bf16_to_f32(x.x >> 16);
+    acc[2] = acc[2] + v * bf16_to_f32(x.y & 0xffffu);
+    acc[3] = acc[3] + v * bf16_to_f32(x.y >> 16);
+  };
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  while (e < end) {
+    const int n = (int)(end - e < 64 ? end - e : 64);
+    int cl = 0;
+    float vl = 0.f;
+    if (lane < n) {
+      cl = col[e + lane];
+      vl = val[e + lane];
+    }
+    int j = 0;
+    for (; j + U <= n; j += U) {
+      uint2 xv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        xv[k] = ok ? *reinterpret_cast<const uint2 *>(Xs + (int64_t)bcast_i(cl, j + k) * ldx) : make_uint2(0, 0);
+#pragma unroll
+      for (int k = 0; k < U; ++k) axpy(bcast_f(vl, j + k), xv[k]);
+    }
+    if (j < n) {
+      const int rem = n - j;  // wave-uniform
+      uint2 xv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (k < rem)
+          xv[k] = ok ? *reinterpret_cast<const uint2 *>(Xs + (int64_t)bcast_i(cl, j + k) * ldx) : make_uint2(0, 0);
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (k < rem) axpy(bcast_f(vl, j + k), xv[k]);
+    }
+    e += n;
+  }
+  if (ok) {
+    uint2 o;
+    o.x = f32_to_bf16_rne(acc[0]) | (f32_to_bf16_rne(acc[1]) << 16);
+    o.y = f32_to_bf16_rne(acc[2]) | (f32_to_bf16_rne(acc[3]) << 16);
+    *reinterpret_cast<uint2 *>(Y + row * ldy + c0 + lane * 4) = o;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
@@ -612,8 +735,8 @@ extern "C" lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64
   return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1}, stream);
 }
 
-extern "C" lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,
-                                    int64_t ldy, int64_t F, void *stream) {
+static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
+                                 int64_t F, HeavyRows hv, void *stream) {
   lpg_status st = check_csr(A);
   if (st != LPG_OK) return st;
   LPG_REQUIRE(F >= 0, "lpg_spmm_bf16: F < 0");
@@ -627,7 +750,36 @@ extern "C" lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
     return launch(spmm_bf16_generic, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
-  if (F <= 512) return launch_wide_bf16<1, 8>(A, X, ldx, Y, ldy, F, s);
-  if (F <= 1024) return launch_wide_bf16<2, 8>(A, X, ldx, Y, ldy, F, s);
+  // slice width: lpg_spmm_set_slice (256 = spmm_bf16_rowslim, 512 / 1024 / 2048 = rowwave with 1 / 2 / 4
+  // 16-B pieces per lane); auto = 256 (c5: 0.92 / 0.97 of the edge-gather roofline vs 0.88 / 0.91 for
+  // whole 2048-column rows, profiles/r02_kbench_spmm16.log); heavy rows only split in the 256 form
+  const int64_t W = g_slice_cols == 0 || hv.blocks > 0 ? 256 : g_slice_cols;
+  if (W <= 256) {
+    hv.slices = (F + 511) / 512;
+    const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock + hv.blocks * hv.slices;
+    LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_bf16: grid too large");
+    dim3 grid((unsigned)nblk, (unsigned)((F + 255) / 256));
+    const int U = g_depth != 0 ? g_depth : (hv.blocks == 0 && A->nnz >= 16 * A->n_rows) ? 16 : 8;
+    if (U == 16)
+      return launch(spmm_bf16_rowslim<16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
+    return launch(spmm_bf16_rowslim<8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
+  }
+  if (W == 512 || F <= 512) return launch_wide_bf16<1, 8>(A, X, ldx, Y, ldy, F, s);
+  if (W == 1024 || F <= 1024) return launch_wide_bf16<2, 8>(A, X, ldx, Y, ldy, F, s);
   return launch_wide_bf16<4, 4>(A, X, ldx, Y, ldy, F, s);
+}
+
+extern "C" lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,
+                                    int64_t ldy, int64_t F, void *stream) {
+  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, stream);
+}
+
+extern "C" lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,
+                                          int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
+                                          int64_t thresh, void *stream) {
+  LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_bf16_heavy: negative n_heavy / thresh");
+  LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_bf16_heavy: heavy_rows is NULL");
+  LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_bf16_heavy: more heavy rows than rows");
+  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1},
+                        stream);
 }

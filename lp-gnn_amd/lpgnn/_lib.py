@@ -28,6 +28,7 @@ HEADER_SYMBOLS = (
     "lpg_spmm_f32",
     "lpg_spmm_f32_heavy",
     "lpg_spmm_bf16",
+    "lpg_spmm_bf16_heavy",
     "lpg_spmm_set_slice",
     "lpg_spmm_set_depth",
     "lpg_spmm_set_remainder",
@@ -103,6 +104,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_spmm_f32_heavy.restype = c_i32
     L.lpg_spmm_bf16.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p]
     L.lpg_spmm_bf16.restype = c_i32
+    L.lpg_spmm_bf16_heavy.argtypes = L.lpg_spmm_f32_heavy.argtypes
+    L.lpg_spmm_bf16_heavy.restype = c_i32
     L.lpg_spmm_set_slice.argtypes = [c_i64]
     L.lpg_spmm_set_slice.restype = c_i32
     L.lpg_spmm_set_depth.argtypes = [c_i64]

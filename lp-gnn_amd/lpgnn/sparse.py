@@ -198,6 +198,10 @@ def spmm_forward(adj: CSR, x: torch.Tensor) -> torch.Tensor:
                 heavy = None
     elif x.dtype == torch.bfloat16:
         fn, name = L.lpg_spmm_bf16, "lpg_spmm_bf16"
+        if Fd >= 256 and HEAVY_THRESH > 0:
+            heavy = adj.heavy_rows(HEAVY_THRESH)
+            if heavy[1] == 0:
+                heavy = None
     else:
         raise RuntimeError(f"lpgnn.spmm: unsupported dtype {x.dtype}")
     with torch.cuda.device(x.device):
@@ -205,10 +209,10 @@ def spmm_forward(adj: CSR, x: torch.Tensor) -> torch.Tensor:
         tok = TIMER.start(("spmm", adj.n_rows, adj.n_cols, Fd, str(x.dtype)))
         if heavy is None:
             st = fn(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), Fd, stream)
-        else:  # degree-aware: rows above the threshold on 64-column waves (same per-element order)
-            name = "lpg_spmm_f32_heavy"
-            st = L.lpg_spmm_f32_heavy(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(),
-                                      y.stride(0), Fd, heavy[0].data_ptr(), heavy[1], HEAVY_THRESH, stream)
+        else:  # degree-aware: rows above the threshold on narrow wave units (same per-element order)
+            name = "lpg_spmm_f32_heavy" if x.dtype == torch.float32 else "lpg_spmm_bf16_heavy"
+            st = getattr(L, name)(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(),
+                                  y.stride(0), Fd, heavy[0].data_ptr(), heavy[1], HEAVY_THRESH, stream)
         TIMER.stop(tok)
     _lib.check(st, name)
     return y

@@ -308,3 +308,55 @@ def test_batched_remainder_bitwise(depth, Fd, dt):
     assert torch.equal(outs[0], outs[1])
     A, _ = _oracle_pair(row, col, val, m, n)
     assert np.array_equal(outs[0].numpy(), O.spmm_f32(*A, X.numpy()))
+
+
+@pytest.mark.parametrize("slice_cols", [0, 256, 512, 1024])
+@pytest.mark.parametrize("Fd", [256, 1000, 2048])
+def test_bf16_slice_widths_bitwise(slice_cols, Fd):
+    """bf16 SpMM: the 256-column slice kernel (the default) and the 16-B-per-lane row
+    kernels give the oracle's bits for every slice width, degrees 0..150."""
+    from lpgnn import _lib
+    from lpgnn.sparse import spmm_forward
+
+    rng = np.random.default_rng(Fd + slice_cols)
+    m, n = 300, 500
+    deg = rng.integers(0, 151, m)
+    row = np.repeat(np.arange(m), deg)
+    col = np.concatenate([rng.choice(n, d, replace=False) for d in deg]).astype(np.int64)
+    val = rng.uniform(-1, 1, len(row)).astype(np.float32)
+    adj = _adj(row, col, val, m, n)
+    A, _ = _oracle_pair(row, col, val, m, n)
+    X = torch.randn(n, Fd).to(torch.bfloat16)
+    Xbits = X.view(torch.int16).numpy().view(np.uint16)
+    L = _lib.lib()
+    try:
+        assert L.lpg_spmm_set_slice(slice_cols) == 0
+        y = spmm_forward(adj.fwd, X.to(DEV)).cpu().view(torch.int16).numpy().view(np.uint16)
+    finally:
+        L.lpg_spmm_set_slice(0)
+    assert np.array_equal(y, O.spmm_bf16(*A, Xbits))
+
+
+@pytest.mark.parametrize("thresh", [0, 3, 64])
+@pytest.mark.parametrize("Fd", [512, 1000, 2048])
+def test_bf16_heavy_rows_bitwise(thresh, Fd, monkeypatch):
+    """bf16 degree-aware split (lpg_spmm_bf16_heavy): rows above the threshold on
+    (row, 128-column) wave units give the oracle's bits; a 2000-edge row crosses many
+    64-edge chunks and the 32-gather batches."""
+    from lpgnn import sparse as S
+    from lpgnn.sparse import spmm_forward
+
+    rng = np.random.default_rng(Fd + thresh)
+    m, n = 200, 2500
+    deg = rng.integers(0, 40, m)
+    deg[[3, 77, 150]] = [2000, 130, 65]
+    row = np.repeat(np.arange(m), deg)
+    col = np.concatenate([rng.choice(n, d, replace=False) for d in deg]).astype(np.int64)
+    val = rng.uniform(-1, 1, len(row)).astype(np.float32)
+    adj = _adj(row, col, val, m, n)
+    A, _ = _oracle_pair(row, col, val, m, n)
+    X = torch.randn(n, Fd).to(torch.bfloat16)
+    Xbits = X.view(torch.int16).numpy().view(np.uint16)
+    monkeypatch.setattr(S, "HEAVY_THRESH", thresh)
+    y = spmm_forward(adj.fwd, X.to(DEV)).cpu().view(torch.int16).numpy().view(np.uint16)
+    assert np.array_equal(y, O.spmm_bf16(*A, Xbits))

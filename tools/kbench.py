@@ -170,7 +170,7 @@ def bench_spmmbig(out):
 
 
 def bench_spmm16(out):
-    """bf16 SpMM at the c5 width (F = 2048), both directions, remainder batched or not."""
+    """bf16 SpMM at the c5 width (F = 2048), both directions, slice widths (256 = rowslim)."""
     from lpgnn import BipartiteCSR, _lib, synth
     from lpgnn.sparse import spmm_forward
 
@@ -180,16 +180,24 @@ def bench_spmm16(out):
         adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
         for name, csr, K in (("cons<-vars", adj.fwd, g.n), ("vars<-cons", adj.bwd, g.m)):
             X = torch.randn(K, 2048, device="cuda").to(torch.bfloat16)
+            L.lpg_spmm_set_slice(1024)  # the whole-row (round-1) form as the reference
+            from lpgnn import sparse as S0
+            hh, S0.HEAVY_THRESH = S0.HEAVY_THRESH, 0
             ref = spmm_forward(csr, X)
+            S0.HEAVY_THRESH = hh
             fns = {}
-            for rb in (0, 1):
-                def f(rb=rb):
-                    L.lpg_spmm_set_remainder(rb)
+            from lpgnn import sparse as S
+            h0 = S.HEAVY_THRESH
+            for sl, h in ((256, h0), (256, 0), (512, 0), (1024, 0)):
+                def f(sl=sl, h=h):
+                    L.lpg_spmm_set_slice(sl)
+                    S.HEAVY_THRESH = h
                     return spmm_forward(csr, X)
                 assert torch.equal(f(), ref)
-                fns[f"rem{'B' if rb else '1'} (bf16 ignores the knob)"] = f
+                fns[f"slice{sl} heavy>{h}"] = f
             t = timeit(fns)
-            L.lpg_spmm_set_remainder(1)
+            L.lpg_spmm_set_slice(0)
+            S.HEAVY_THRESH = h0
             B = g.nnz * 2048 * 2 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 2048 * 2
             for k, v in t.items():
                 out[f"spmm bf16 {gname} {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000)
