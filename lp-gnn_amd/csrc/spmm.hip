@@ -488,7 +488,9 @@ __device__ __forceinline__ void spmm_bf16_heavy_row(int64_t row, int64_t c0, int
 // (8-B gathers, 512 B per wave-instruction), fp32 accumulation, one RNE rounding -- the bf16 twin of
 // spmm_f32_rowslim (a slice of the c5 [200K, 2048] bf16 table is 102 MB instead of the whole 820 MB),
 // the chunk remainder gathered together.  Same edge order: the same bits as spmm_bf16_rowwave.
-template <int U>
+// HEAVY: the launch carries heavy-row units (instantiated only then: compiled in, the heavy body made
+// the light-row waves 7 % slower at c5 even with no heavy rows)
+template <int U, bool HEAVY>
 __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, const int64_t *__restrict__ rowptr,
                                                             const int32_t *__restrict__ col,
                                                             const float *__restrict__ val,
@@ -497,16 +499,18 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, cons
                                                             HeavyRows hv) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int64_t hb = hv.blocks * hv.slices;  // heavy (row, 512-column piece) units: the head of plane 0
-  if ((int64_t)blockIdx.x < hb) {
-    if (blockIdx.y != 0) return;
-    const uint32_t hs = (uint32_t)hv.slices, bxu = blockIdx.x;
-    spmm_bf16_heavy_row(hv.rows[bxu / hs], (int64_t)(bxu % hs) * 512, wave, rowptr, col, val, X, ldx, Y, ldy, F);
-    return;
+  const int64_t hb = HEAVY ? hv.blocks * hv.slices : 0;  // heavy (row, 512-column piece) units: head of plane 0
+  if constexpr (HEAVY) {
+    if ((int64_t)blockIdx.x < hb) {
+      if (blockIdx.y != 0) return;
+      const uint32_t hs = (uint32_t)hv.slices, bxu = blockIdx.x;
+      spmm_bf16_heavy_row(hv.rows[bxu / hs], (int64_t)(bxu % hs) * 512, wave, rowptr, col, val, X, ldx, Y, ldy, F);
+      return;
+    }
   }
   const int64_t row = ((int64_t)blockIdx.x - hb) * kWavesPerBlock + wave;
   if (row >= n_rows) return;
-  if (rowptr[row + 1] - rowptr[row] > hv.thresh) return;  // a heavy row: done by the units above
+  if (HEAVY && rowptr[row + 1] - rowptr[row] > hv.thresh) return;  // a heavy row: done by the units above
   const int64_t c0 = (int64_t)blockIdx.y * 256;
   const bool ok = c0 + lane * 4 < F;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -760,9 +764,11 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
     LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_bf16: grid too large");
     dim3 grid((unsigned)nblk, (unsigned)((F + 255) / 256));
     const int U = g_depth != 0 ? g_depth : (hv.blocks == 0 && A->nnz >= 16 * A->n_rows) ? 16 : 8;
+    if (hv.blocks > 0)
+      return launch(spmm_bf16_rowslim<8, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
     if (U == 16)
-      return launch(spmm_bf16_rowslim<16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
-    return launch(spmm_bf16_rowslim<8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
+      return launch(spmm_bf16_rowslim<16, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
+    return launch(spmm_bf16_rowslim<8, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
   }
   if (W == 512 || F <= 512) return launch_wide_bf16<1, 8>(A, X, ldx, Y, ldy, F, s);
   if (W == 1024 || F <= 1024) return launch_wide_bf16<2, 8>(A, X, ldx, Y, ldy, F, s);
