@@ -362,16 +362,91 @@ __device__ __forceinline__ void axpy8_bf16(float (&acc)[8], float v, const uint4
   }
 }
 
-// Lane l holds columns c0 + q*512 + 8l .. +7 (16 bytes) for q < NV.
-template <int NV, int U, bool FULL>
+// bf16 heavy rows (degree > thresh): one block per (heavy row, 512-column piece) at the head of plane 0
+// of a 512-column spmm_bf16_rowwave launch, wave w on columns
+// c0 + 128 w + 2 l, +1 (4-B gathers, 256 B per wave-instruction), 32 gathers in flight and the next
+// 64-edge chunk's indices prefetched -- 4x the waves on one long row's chain, each element still
+// summed in CSR order (the same bits).
+__device__ __forceinline__ void spmm_bf16_heavy_row(int64_t row, int64_t c0, int wave,
+                                                    const int64_t *__restrict__ rowptr,
+                                                    const int32_t *__restrict__ col, const float *__restrict__ val,
+                                                    const uint16_t *__restrict__ X, int64_t ldx,
+                                                    uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
+  constexpr int HU = 32;
+  const int lane = threadIdx.x & 63;
+  const int64_t cw = c0 + wave * 128 + lane * 2;
+  const bool ok = cw < F;
+  float a0 = 0.f, a1 = 0.f;
+  const uint16_t *Xs = X + cw;
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  int cn = 0;
+  float vn = 0.f;
+  if (e + lane < end) {
+    cn = col[e + lane];
+    vn = val[e + lane];
+  }
+  while (e < end) {
+    const int n = (int)(end - e < 64 ? end - e : 64);
+    const int cl = cn;
+    const float vl = vn;
+    if (e + 64 + lane < end) {
+      cn = col[e + 64 + lane];
+      vn = val[e + 64 + lane];
+    }
+    int j = 0;
+    for (; j + HU <= n; j += HU) {  // full batches: no predication (uniform branches around loads
+      uint32_t xv[HU];              // made the waitcnt pass serialise them)
+#pragma unroll
+      for (int k = 0; k < HU; ++k)
+        xv[k] = ok ? *reinterpret_cast<const uint32_t *>(Xs + (int64_t)bcast_i(cl, j + k) * ldx) : 0u;
+#pragma unroll
+      for (int k = 0; k < HU; ++k) {
+        const float v = bcast_f(vl, j + k);
+        a0 = a0 + v * bf16_to_f32(xv[k] & 0xffffu);
+        a1 = a1 + v * bf16_to_f32(xv[k] >> 16);
+      }
+    }
+    if (j < n) {
+      const int rem = n - j;  // wave-uniform, < HU
+      uint32_t xv[HU];
+#pragma unroll
+      for (int k = 0; k < HU; ++k)
+        if (k < rem) xv[k] = ok ? *reinterpret_cast<const uint32_t *>(Xs + (int64_t)bcast_i(cl, j + k) * ldx) : 0u;
+#pragma unroll
+      for (int k = 0; k < HU; ++k)
+        if (k < rem) {
+          const float v = bcast_f(vl, j + k);
+          a0 = a0 + v * bf16_to_f32(xv[k] & 0xffffu);
+          a1 = a1 + v * bf16_to_f32(xv[k] >> 16);
+        }
+    }
+    e += n;
+  }
+  if (ok) *reinterpret_cast<uint32_t *>(Y + row * ldy + cw) = f32_to_bf16_rne(a0) | (f32_to_bf16_rne(a1) << 16);
+}
+
+// Lane l holds columns c0 + q*512 + 8l .. +7 (16 bytes) for q < NV.  HEAVY (NV = 1): the launch's
+// leading blocks of plane 0 are heavy (row, 512-column) units, as in spmm_f32_rowwave.
+template <int NV, int U, bool FULL, bool HEAVY = false>
 __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
-    uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
+    uint16_t *__restrict__ Y, int64_t ldy, int64_t F, HeavyRows hv) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int64_t hb = HEAVY ? hv.blocks * hv.slices : 0;
+  if constexpr (HEAVY) {
+    if ((int64_t)blockIdx.x < hb) {
+      if (blockIdx.y != 0) return;
+      const uint32_t hs = (uint32_t)hv.slices, bxu = blockIdx.x;
+      spmm_bf16_heavy_row(hv.rows[bxu / hs], (int64_t)(bxu % hs) * 512, wave, rowptr, col, val, X, ldx, Y, ldy, F);
+      return;
+    }
+  }
+  const int64_t row = ((int64_t)blockIdx.x - hb) * kWavesPerBlock + wave;
   if (row >= n_rows) return;
+  if (HEAVY && rowptr[row + 1] - rowptr[row] > hv.thresh) return;  // a heavy row: done by the units above
   const int64_t c0 = (int64_t)blockIdx.y * (NV * 512);
   bool ok[NV];
 #pragma unroll
@@ -434,83 +509,20 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
   }
 }
 
-// bf16 heavy rows (degree > thresh): one block per (heavy row, 512-column piece), wave w on columns
-// c0 + 128 w + 2 l, +1 (4-B gathers, 256 B per wave-instruction), 32 gathers in flight and the next
-// 64-edge chunk's indices prefetched -- 4x the waves on one long row's chain, each element still
-// summed in CSR order (the same bits).
-__device__ __forceinline__ void spmm_bf16_heavy_row(int64_t row, int64_t c0, int wave,
-                                                    const int64_t *__restrict__ rowptr,
-                                                    const int32_t *__restrict__ col, const float *__restrict__ val,
-                                                    const uint16_t *__restrict__ X, int64_t ldx,
-                                                    uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
-  constexpr int HU = 32;
-  const int lane = threadIdx.x & 63;
-  const int64_t cw = c0 + wave * 128 + lane * 2;
-  const bool ok = cw < F;
-  float a0 = 0.f, a1 = 0.f;
-  const uint16_t *Xs = X + cw;
-  int64_t e = rowptr[row];
-  const int64_t end = rowptr[row + 1];
-  int cn = 0;
-  float vn = 0.f;
-  if (e + lane < end) {
-    cn = col[e + lane];
-    vn = val[e + lane];
-  }
-  while (e < end) {
-    const int n = (int)(end - e < 64 ? end - e : 64);
-    const int cl = cn;
-    const float vl = vn;
-    if (e + 64 + lane < end) {
-      cn = col[e + 64 + lane];
-      vn = val[e + 64 + lane];
-    }
-    for (int j = 0; j < n; j += HU) {
-      const int rem = n - j < HU ? n - j : HU;  // wave-uniform
-      uint32_t xv[HU];
-#pragma unroll
-      for (int k = 0; k < HU; ++k)
-        if (k < rem) xv[k] = ok ? *reinterpret_cast<const uint32_t *>(Xs + (int64_t)bcast_i(cl, j + k) * ldx) : 0u;
-#pragma unroll
-      for (int k = 0; k < HU; ++k)
-        if (k < rem) {
-          const float v = bcast_f(vl, j + k);
-          a0 = a0 + v * bf16_to_f32(xv[k] & 0xffffu);
-          a1 = a1 + v * bf16_to_f32(xv[k] >> 16);
-        }
-    }
-    e += n;
-  }
-  if (ok) *reinterpret_cast<uint32_t *>(Y + row * ldy + cw) = f32_to_bf16_rne(a0) | (f32_to_bf16_rne(a1) << 16);
-}
-
 // bf16 narrow slices: one wave per (row, 256-column slice), lane l holding columns c0 + 4l .. +3
 // (8-B gathers, 512 B per wave-instruction), fp32 accumulation, one RNE rounding -- the bf16 twin of
 // spmm_f32_rowslim (a slice of the c5 [200K, 2048] bf16 table is 102 MB instead of the whole 820 MB),
 // the chunk remainder gathered together.  Same edge order: the same bits as spmm_bf16_rowwave.
-// HEAVY: the launch carries heavy-row units (instantiated only then: compiled in, the heavy body made
-// the light-row waves 7 % slower at c5 even with no heavy rows)
-template <int U, bool HEAVY>
+template <int U>
 __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, const int64_t *__restrict__ rowptr,
                                                             const int32_t *__restrict__ col,
                                                             const float *__restrict__ val,
                                                             const uint16_t *__restrict__ X, int64_t ldx,
-                                                            uint16_t *__restrict__ Y, int64_t ldy, int64_t F,
-                                                            HeavyRows hv) {
+                                                            uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int64_t hb = HEAVY ? hv.blocks * hv.slices : 0;  // heavy (row, 512-column piece) units: head of plane 0
-  if constexpr (HEAVY) {
-    if ((int64_t)blockIdx.x < hb) {
-      if (blockIdx.y != 0) return;
-      const uint32_t hs = (uint32_t)hv.slices, bxu = blockIdx.x;
-      spmm_bf16_heavy_row(hv.rows[bxu / hs], (int64_t)(bxu % hs) * 512, wave, rowptr, col, val, X, ldx, Y, ldy, F);
-      return;
-    }
-  }
-  const int64_t row = ((int64_t)blockIdx.x - hb) * kWavesPerBlock + wave;
+  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave;
   if (row >= n_rows) return;
-  if (HEAVY && rowptr[row + 1] - rowptr[row] > hv.thresh) return;  // a heavy row: done by the units above
   const int64_t c0 = (int64_t)blockIdx.y * 256;
   const bool ok = c0 + lane * 4 < F;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -634,11 +646,26 @@ lpg_status launch_wide_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, ui
   const int64_t W = NV * 512;
   const int64_t slices = (F + W - 1) / W;
   dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock), (unsigned)slices);
+  const HeavyRows none{nullptr, 0, INT64_MAX, 1};
   if (F % W == 0)
     return launch(spmm_bf16_rowwave<NV, U, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
-                  Y, ldy, F);
+                  Y, ldy, F, none);
   return launch(spmm_bf16_rowwave<NV, U, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
-                Y, ldy, F);
+                Y, ldy, F, none);
+}
+
+// 512-column slices with the heavy rows split off (heavy units first in plane 0)
+lpg_status launch_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
+                             int64_t F, HeavyRows hv, hipStream_t s) {
+  hv.slices = (F + 511) / 512;
+  const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock + hv.blocks * hv.slices;
+  LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_bf16: grid too large");
+  dim3 grid((unsigned)nblk, (unsigned)hv.slices);
+  if (F % 512 == 0)
+    return launch(spmm_bf16_rowwave<1, 8, true, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y,
+                  ldy, F, hv);
+  return launch(spmm_bf16_rowwave<1, 8, false, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y,
+                ldy, F, hv);
 }
 
 }  // namespace
@@ -756,19 +783,17 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
   }
   // slice width: lpg_spmm_set_slice (256 = spmm_bf16_rowslim, 512 / 1024 / 2048 = rowwave with 1 / 2 / 4
   // 16-B pieces per lane); auto = 256 (c5: 0.92 / 0.97 of the edge-gather roofline vs 0.88 / 0.91 for
-  // whole 2048-column rows, profiles/r02_kbench_spmm16.log); heavy rows only split in the 256 form
-  const int64_t W = g_slice_cols == 0 || hv.blocks > 0 ? 256 : g_slice_cols;
+  // whole 2048-column rows, profiles/r02_kbench_spmm16.log); with heavy rows split off, 512-column slices
+// (spmm_bf16_rowwave<1, 8> + heavy units: a skewed LP's mostly one-edge rows want few, wide wave tasks)
+  if (hv.blocks > 0) return launch_bf16_heavy(A, X, ldx, Y, ldy, F, hv, s);
+  const int64_t W = g_slice_cols == 0 ? 256 : g_slice_cols;
   if (W <= 256) {
-    hv.slices = (F + 511) / 512;
-    const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock + hv.blocks * hv.slices;
+    const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
     LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_bf16: grid too large");
     dim3 grid((unsigned)nblk, (unsigned)((F + 255) / 256));
-    const int U = g_depth != 0 ? g_depth : (hv.blocks == 0 && A->nnz >= 16 * A->n_rows) ? 16 : 8;
-    if (hv.blocks > 0)
-      return launch(spmm_bf16_rowslim<8, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
-    if (U == 16)
-      return launch(spmm_bf16_rowslim<16, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
-    return launch(spmm_bf16_rowslim<8, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
+    const int U = g_depth != 0 ? g_depth : A->nnz >= 16 * A->n_rows ? 16 : 8;
+    if (U == 16) return launch(spmm_bf16_rowslim<16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    return launch(spmm_bf16_rowslim<8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
   if (W == 512 || F <= 512) return launch_wide_bf16<1, 8>(A, X, ldx, Y, ldy, F, s);
   if (W == 1024 || F <= 1024) return launch_wide_bf16<2, 8>(A, X, ldx, Y, ldy, F, s);
