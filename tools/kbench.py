@@ -249,6 +249,26 @@ def bench_bf16(out):
         out[f"bf16 M={M} K=4096 {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * 4096 / v / 1e9)
 
 
+def bench_fck(out):
+    """lpg_fc_bf16 (default variant) at M = 200K / 100K, N = 2048 for K = 1024 .. 8192 (one phase,
+    no epilogue options, and with ReLU + dropout + accumulate): per-block fixed cost vs the k loop."""
+    from lpgnn.fc import fc_forward_bf16
+
+    BF = torch.bfloat16
+    for M in (200_000, 100_000):
+        for K in (1024, 2048, 4096, 8192):
+            A = torch.randn(M, K, device="cuda").to(BF)
+            W = (torch.randn(2048, K, device="cuda") * 0.02).to(BF)
+            b = torch.randn(2048, device="cuda")
+            P = torch.randn(M, 2048, device="cuda").to(BF)
+            t = timeit({"plain": lambda: fc_forward_bf16(A, W, None, None, None, False),
+                        "relu+drop+acc": lambda: fc_forward_bf16(A, W, None, None, b, True, 0.1, 7, out=P.clone(),
+                                                                 accumulate=True)}, rounds=5, iters=3)
+            for k, v in t.items():
+                out[f"fcK M={M} K={K} {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * K / v / 1e9)
+            del A, W, P
+
+
 def bench_bf16bwd(out):
     """c5 backward GEMMs: lpg_wgrad_bf16 (4 / 8 waves) vs torch (G^T X).float(); the input
     gradient on lpg_fc_bf16 (transposed weights) vs torch G @ W."""
@@ -367,7 +387,7 @@ if __name__ == "__main__":
     for w in which:
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
-         "spmmbig": bench_spmmbig,
+         "spmmbig": bench_spmmbig, "fck": bench_fck,
          "load": bench_load, "fcpi": bench_fcpi}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
