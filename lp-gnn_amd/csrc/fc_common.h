@@ -27,6 +27,14 @@ __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int64_t row, int64_
   return lowbias32(hr ^ ((uint32_t)col * 0x9e3779b9u) ^ (uint32_t)(seed >> 32));
 }
 
+// drop_hash split into its row and column keys, for epilogues that hold a few rows and a few
+// columns per lane: drop_hash(seed, row, col) == drop_hash_k(drop_row_key(seed, row), drop_col_key(col))
+__device__ __forceinline__ uint32_t drop_row_key(uint64_t seed, int64_t row) {
+  return lowbias32((uint32_t)row ^ (uint32_t)seed) ^ (uint32_t)(seed >> 32);
+}
+__device__ __forceinline__ uint32_t drop_col_key(int64_t col) { return (uint32_t)col * 0x9e3779b9u; }
+__device__ __forceinline__ uint32_t drop_hash_k(uint32_t rk, uint32_t ck) { return lowbias32(rk ^ ck); }
+
 // 16 B per lane, buffer_load_dwordx4 ... lds into M0 = lds (lane-linear): the descriptor over
 // [p, p + n) is built from readfirstlane'd values, so it stays in SGPRs (a select between two
 // descriptors went to VGPRs and turned every load into a waterfall loop); the lane offset is

@@ -806,44 +806,106 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = accH[i][j] + accL[i][j];
-  if (a.accum) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      int64_t col = nw + j * 16 + fr;
-      col = col < a.N ? col : a.N - 1;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int64_t row = mw + i * 16 + 4 * fg + r;
-          row = row < a.M ? row : a.M - 1;
-          acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
-        }
-    }
-  }
-  float hs[HEADS ? 4 : 1][TM][4];  // fused heads: this lane's partial logits [head][i][r]
+  // fused heads (hn <= 3 here; the host routes hn = 4 to fc_fwd_x3_16): this lane's partial
+  // logits [head][i][r]
+  constexpr int HC = HEADS ? 3 : 1;
+  float hs[HC][TM][4];
   if constexpr (HEADS) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < HC; ++c)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) hs[c][i][r] = 0.f;
   }
-  // the element loop with the bias / dropout choices made once (uniform branches per element cost
-  // more than the arithmetic)
-  auto body = [&](auto bias_c, auto drop_c) {
-    constexpr bool BIAS = decltype(bias_c)::value, DROP = decltype(drop_c)::value;
+  auto head_w = [&](int64_t col, float(&hwv)[HC]) {  // loads from valid rows only, no branch
+    if constexpr (HEADS) {
+#pragma unroll
+      for (int c = 0; c < HC; ++c) {
+        const float w = a.hw[(c < a.hn ? c : a.hn - 1) * a.ldhw + col];
+        hwv[c] = c < a.hn ? w : 0.f;
+      }
+    }
+  };
+  if (mw + TM * 16 <= a.M && nw + BN <= a.N) {
+    // interior wave tile (wave-uniform): no per-element bounds, one C row pointer per (i, r) with
+    // the column step j * 16 as the store's immediate offset, the dropout row keys computed once
+    // per row (the per-element forms cost ~24 VALU incl. 6 v_mul_lo_u32 and a branch per output)
+    float *rp[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rp[i][r] = a.C + (mw + i * 16 + 4 * fg + r) * a.ldc + nw + fr;
+    if (a.accum) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + rp[i][r][j * 16];
+    }
+    auto body = [&](auto bias_c, auto drop_c) {
+      constexpr bool BIAS = decltype(bias_c)::value, DROP = decltype(drop_c)::value;
+      uint32_t rk[TM][4];
+      if constexpr (DROP) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rk[i][r] = drop_row_key(a.seed, mw + i * 16 + 4 * fg + r);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t col = nw + j * 16 + fr;
+        const float bb = BIAS ? a.bias[col] : 0.f;
+        const uint32_t ck = drop_col_key(col);
+        float hwv[HC];
+        head_w(col, hwv);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[i][j][r];
+            if constexpr (BIAS) v = v + bb;
+            if (RELU) v = (v < 0.f) ? 0.f : v;
+            if constexpr (DROP) v = drop_hash_k(rk[i][r], ck) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+            rp[i][r][j * 16] = v;
+            if constexpr (HEADS) {
+#pragma unroll
+              for (int c = 0; c < HC; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
+            }
+          }
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    if (a.bias) {
+      if (a.drop_thresh) body(T_{}, T_{}); else body(T_{}, F_{});
+    } else {
+      if (a.drop_thresh) body(F_{}, T_{}); else body(F_{}, F_{});
+    }
+  } else {  // edge wave tile: per-element bounds (same arithmetic, same bits)
+    if (a.accum) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int64_t col = nw + j * 16 + fr;
+        col = col < a.N ? col : a.N - 1;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            int64_t row = mw + i * 16 + 4 * fg + r;
+            row = row < a.M ? row : a.M - 1;
+            acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
+          }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int64_t col = nw + j * 16 + fr;
       if (col >= a.N) continue;
-      const float bb = BIAS ? a.bias[col] : 0.f;
-      float hwv[HEADS ? 4 : 1];
-      if constexpr (HEADS) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) hwv[c] = c < a.hn ? a.hw[c * a.ldhw + col] : 0.f;
-      }
+      const float bb = a.bias ? a.bias[col] : 0.f;
+      float hwv[HC];
+      head_w(col, hwv);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -851,32 +913,25 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
           const int64_t row = mw + i * 16 + 4 * fg + r;
           if (row >= a.M) continue;
           float v = acc[i][j][r];
-          if constexpr (BIAS) v = v + bb;
+          if (a.bias) v = v + bb;
           if (RELU) v = (v < 0.f) ? 0.f : v;
-          if constexpr (DROP) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+          if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
           a.C[row * a.ldc + col] = v;
           if constexpr (HEADS) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
+            for (int c = 0; c < HC; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
           }
         }
     }
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  if (a.bias) {
-    if (a.drop_thresh) body(T_{}, T_{}); else body(T_{}, F_{});
-  } else {
-    if (a.drop_thresh) body(F_{}, T_{}); else body(F_{}, F_{});
   }
   if constexpr (HEADS) {  // sum over the 16 lanes (columns) of each row group, fixed DPP order; lane fr = 0 writes
     const int64_t pidx = nw / BN;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < HC; ++c)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hs[c][i][r] = c < a.hn ? sum16(hs[c][i][r]) : 0.f;
+        for (int r = 0; r < 4; ++r) hs[c][i][r] = sum16(hs[c][i][r]);  // heads past hn sum zeros
     if (fr == 0) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -885,7 +940,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
           const int64_t row = mw + i * 16 + 4 * fg + r;
           if (row < a.M)
             *reinterpret_cast<f32x4 *>(a.hpart + (pidx * a.M + row) * 4) =
-                f32x4{hs[0][i][r], hs[1][i][r], hs[2][i][r], hs[3][i][r]};
+                f32x4{hs[0][i][r], hs[1][i][r], hs[2][i][r], 0.f};
         }
     }
   }
@@ -1692,12 +1747,13 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   // one partial per (BN-column tile, row): N / 128 for fc_fwd_x3_16, N / 256 for the 256-wide strips
   int64_t bn = 128;
   lpg_status r;
-  if (g_x3_variant == 12 && wide_ok(a, 128, 256)) {
+  const bool wide_heads = hn <= 3;  // fc_x3_wide carries three head slots
+  if (wide_heads && g_x3_variant == 12 && wide_ok(a, 128, 256)) {
     bn = 256;
     r = launch_x3_wide<8, 1, 16, 2, true>(a, flags & 1, s);
-  } else if (g_x3_variant == 13 && wide_ok(a, 128, 128)) {
+  } else if (wide_heads && g_x3_variant == 13 && wide_ok(a, 128, 128)) {
     r = launch_x3_wide<8, 1, 8, 4, true>(a, flags & 1, s);
-  } else if ((g_x3_variant == 0 || g_x3_variant == 14) && wide_ok(a, 128, 128)) {
+  } else if (wide_heads && (g_x3_variant == 0 || g_x3_variant == 14) && wide_ok(a, 128, 128)) {
     r = launch_x3_wide<4, 2, 8, 2, true>(a, flags & 1, s);
   } else {
     r = launch_x3_16<4, 1, 2, 8, false, true>(a, flags & 1, s);  // 32 x 128 wave tiles: N / 128 partials

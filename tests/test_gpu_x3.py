@@ -112,6 +112,7 @@ def test_x3_variants_identical():
     (700, 300, 128, 128, False, 0.0),   # ragged M and N tiles, both k phases
     (37, 1024, 256, 0, True, 0.0),      # fewer rows than one tile, accumulate
     (5000, 1024, 1024, 1024, False, 0.1),
+    (1000, 1024, 256, 0, True, 0.1),    # interior tiles (the unchecked epilogue), accumulate + dropout
     (1, 130, 64, 64, False, 0.0),
 ])
 def test_x3_wide_variants_bitwise(M, N, K1, K2, accum, drop):
@@ -167,6 +168,7 @@ def test_x3_xcd_pair_map_covers_every_tile(M):
     (1000, 1024, 1024, 3, False, 0.0),  # the last hidden layer + lin_left / lin_right
     (333, 200, 96, 3, True, 0.0),       # ragged 128-column tiles, accumulate (re-associated direction)
     (37, 130, 64, 1, False, 0.2),       # one head, dropout
+    (1000, 1024, 256, 3, True, 0.1),    # interior tiles: accumulate + dropout + heads (the c2 root FC)
     (5000, 1024, 2048, 4, False, 0.0),
 ])
 def test_x3_fused_heads_match_separate_linear(M, N, K, hn, accum, drop):

@@ -9,6 +9,7 @@ bf16bwd: the c5 backward GEMMs (lpg_wgrad_bf16, lpg_fc_bf16 on transposed weight
 load : graph load at c2 -- reference chain (to_undirected + MyToBipartite + device pack) vs direct pack
 spmm : lpg_spmm_f32 at c2, both directions, slice widths 256/512/1024
 bwd  : the FC backward GEMMs at c2 shapes through torch (hipBLASLt)
+x3epi: lpg_fc_x3 at the c2 shapes, one line per epilogue (plain / ReLU+dropout / +accumulate / +heads)
 """
 import json
 import os
@@ -269,6 +270,33 @@ def bench_fck(out):
             del A, W, P
 
 
+def bench_x3epi(out):
+    """lpg_fc_x3 at the c2 FC shapes with each epilogue: plain, ReLU + dropout (two phases) and
+    ReLU + dropout + accumulate (in place, no clone in the timed region), heads fused."""
+    from lpgnn.fc import fc_forward
+
+    for M, K1, K2, mode in ((200_000, 1024, 0, "lin"), (200_000, 1024, 0, "relu+drop+acc"),
+                            (200_000, 1024, 0, "relu+drop+acc+heads"),
+                            (100_000, 1024, 1024, "relu+drop"), (100_000, 1024, 0, "lin")):
+        A1 = torch.randn(M, K1, device="cuda")
+        A2 = torch.randn(M, K2, device="cuda") if K2 else None
+        W1 = torch.randn(1024, K1, device="cuda") * 0.03
+        W2 = torch.randn(1024, K2, device="cuda") * 0.03 if K2 else None
+        b = torch.randn(1024, device="cuda")
+        P = torch.randn(M, 1024, device="cuda")
+        hd = (torch.randn(3, 1024, device="cuda") * 0.03, torch.randn(3, device="cuda"))
+
+        def f(A1=A1, A2=A2, W1=W1, W2=W2, b=b, P=P, mode=mode):
+            if mode == "lin":
+                return fc_forward(A1, W1, A2, W2, None, False, arith="x3")
+            return fc_forward(A1, W1, A2, W2, b, True, 0.1, 7, out=P if "acc" in mode else None,
+                              accumulate="acc" in mode, arith="x3", heads=hd if "heads" in mode else None)
+        t = timeit({mode: f}, rounds=7, iters=4)
+        for k, v in t.items():
+            out[f"x3epi M={M} K={K1}+{K2} {k}"] = dict(ms=v, tflops=2.0 * M * 1024 * (K1 + K2) / v / 1e9)
+        del A1, A2, P
+
+
 def bench_bf16bwd(out):
     """c5 backward GEMMs: lpg_wgrad_bf16 (4 / 8 waves) vs torch (G^T X).float(); the input
     gradient on lpg_fc_bf16 (transposed weights) vs torch G @ W."""
@@ -387,7 +415,7 @@ if __name__ == "__main__":
     for w in which:
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
-         "spmmbig": bench_spmmbig, "fck": bench_fck,
+         "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi,
          "load": bench_load, "fcpi": bench_fcpi}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
