@@ -287,12 +287,14 @@ lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int
                        const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
                        void *stream);
 /* Tile choice for lpg_fc_bf16 (tuning/benchmarks): 0 = default (128 x 128 below
- * 4096 rows, else 7), 1 = 128 x 128, 2 = 256 x 256 with BK 64 and 2 buffers,
+ * 4096 rows, else 10), 1 = 128 x 128, 2 = 256 x 256 with BK 64 and 2 buffers,
  * 3 = 256 x 256 with BK 32 and 3 buffers, 4 / 5 = 256 x 256 with
  * buffer_load ... lds staging and the barrier mid-tile, 4 / 8 waves, 6 = 5
  * with the fragment reads and DMA placed between the MFMAs, 7 = 6 with
- * s_setprio 1 on waves 4-7, 8 = 4 placed (4-8 need lda1 == lda2 and
- * ldw1 == ldw2, else 2).  All give identical bits.  100-104 select the
+ * s_setprio 1 on waves 4-7, 8 = 4 placed, 9 = 7 with the MFMA issued as
+ * W x A^T (four consecutive output columns per lane) and a register epilogue,
+ * 10 = 9 through the LDS image (4-9 need lda1 == lda2 and ldw1 == ldw2,
+ * else 2).  All give identical bits.  100-104 select the
  * lpg_wgrad_bf16 kernel (100 / 101 = 4 / 8 waves, 102 = 101 placed (the
  * default), 103 = 102 + s_setprio, 104 = 100 placed; identical bits). */
 lpg_status lpg_fc_bf16_set_variant(int32_t v);

@@ -162,6 +162,189 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
   }
 }
 
+// Epilogue of the transposed-fragment form (fc_bf16_p with TRO: the MFMA is issued as W x A^T,
+// so the 16x16 C/D map puts output ROW 16 i + (lane & 15) on the lane and four CONSECUTIVE
+// columns 16 j + 4 (lane >> 4) + r in its registers): every lane packs its four outputs into one
+// 8-byte store (and loads a 4-wide addend the same way) -- no LDS image, no barrier, and the
+// dropout row key is computed once per fragment row.  Same arithmetic per element as
+// epilogue_bf16 (addend, + bias (0 without one), ReLU, dropout, RNE), so the same bits.
+template <int FM, int FN, bool RELU>
+__device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)[FM][FN], int lane, int64_t wrow0,
+                                                int64_t wcol0) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const int64_t c0 = wcol0 + 4 * fq;  // this lane's first column of fragment j = 0
+  if (wrow0 + FM * 16 <= a.M && wcol0 + FN * 16 <= a.N && a.ldc % 4 == 0 &&
+      (reinterpret_cast<uintptr_t>(a.C) & 7) == 0) {
+    uint16_t *const rp0 = a.C + (wrow0 + fr) * a.ldc + c0;  // fragment row i at + 16 i ldc (uniform step)
+    float bb[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bb[j][r] = a.bias ? a.bias[c0 + j * 16 + r] : 0.f;
+    auto body = [&](auto acc_c, auto drop_c) {
+      constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
+      constexpr int IH = FM / 2;  // addend loads in two halves of IH fragment rows (register budget)
+      uint32_t ck[FN][4];
+      if constexpr (DROP) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ck[j][r] = drop_col_key(c0 + j * 16 + r);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint2 ad[IH][FN];
+        if constexpr (ACC) {
+#pragma unroll
+          for (int ii = 0; ii < IH; ++ii)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              ad[ii][j] = *reinterpret_cast<const uint2 *>(rp0 + (h * IH + ii) * 16 * a.ldc + j * 16);
+        }
+#pragma unroll
+        for (int ii = 0; ii < IH; ++ii) {
+          const int i = h * IH + ii;
+          const uint32_t rk = DROP ? drop_row_key(a.seed, wrow0 + i * 16 + fr) : 0u;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[r] = acc[i][j][r];
+              if constexpr (ACC) {
+                const uint32_t w = r < 2 ? ad[ii][j].x : ad[ii][j].y;
+                v[r] = v[r] + __uint_as_float((r & 1) ? (w & 0xffff0000u) : (w << 16));
+              }
+              v[r] = v[r] + bb[j][r];
+              if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
+              if constexpr (DROP) v[r] = drop_hash_k(rk, ck[j][r]) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
+            }
+            const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2));
+            const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2));
+            *reinterpret_cast<uint2 *>(rp0 + i * 16 * a.ldc + j * 16) = uint2{lo, hi};
+          }
+        }
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    const bool drop = RELU && a.drop_thresh;
+    if (a.accum) {
+      if (drop) body(T_{}, T_{}); else body(T_{}, F_{});
+    } else {
+      if (drop) body(F_{}, T_{}); else body(F_{}, F_{});
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int64_t row = wrow0 + i * 16 + fr;
+    if (row >= a.M) continue;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t col = c0 + j * 16 + r;
+        if (col >= a.N) continue;
+        float v = acc[i][j][r];
+        if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
+        v = v + (a.bias ? a.bias[col] : 0.f);
+        if (RELU) v = v < 0.f ? 0.f : v;
+        if (RELU && a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        a.C[row * a.ldc + col] = to_bf16_rne(v);
+      }
+  }
+}
+
+// Transposed fragments through the LDS image (fc_bf16_p with TRO = 2): the lane's four
+// consecutive columns go to the image as one ds_write_b64 (ds_read_b64 for the addend) instead
+// of four 2-byte accesses, then the rows leave as 16-byte stores as in epilogue_bf16.  Image
+// pitch 144 B: the 64 lanes' 8-byte accesses of one (i, j) are bank-conflict free.
+template <int FM, int FN, bool RELU>
+__device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc)[FM][FN], unsigned char *smem,
+                                                 int wave, int lane, int64_t wrow0, int64_t wcol0) {
+  constexpr int EP_PITCH = FN * 16 * 2 + 16;
+  const int fr = lane & 15, fq = lane >> 4;
+  if (!(a.N % 8 == 0 && a.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(a.C) & 15) == 0)) {
+    epilogue_bf16_t<FM, FN, RELU>(a, acc, lane, wrow0, wcol0);  // its per-element path
+    return;
+  }
+  unsigned char *img = smem + wave * (FM * 16 * EP_PITCH);
+  constexpr int CPR = FN * 16 / 8;  // 16-B chunks per row
+  if (a.accum) {  // the addend tile, coalesced 16-B loads into the image
+#pragma unroll
+    for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
+      const int q = it * 64 + lane;
+      const int lr = q / CPR, ch = q % CPR;
+      const int64_t row = wrow0 + lr < a.M ? wrow0 + lr : a.M - 1, col = wcol0 + ch * 8;
+      if (col < a.N)
+        *reinterpret_cast<uint4 *>(img + lr * EP_PITCH + ch * 16) =
+            *reinterpret_cast<const uint4 *>(a.C + row * a.ldc + col);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  const int64_t c0 = wcol0 + 4 * fq;
+  float bb[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bb[j][r] = (a.bias && c0 + j * 16 + r < a.N) ? a.bias[c0 + j * 16 + r] : 0.f;
+  auto body = [&](auto acc_c, auto drop_c) {
+    constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
+    uint32_t ck[FN][4];
+    if constexpr (DROP) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ck[j][r] = drop_col_key(c0 + j * 16 + r);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const uint32_t rk = DROP ? drop_row_key(a.seed, wrow0 + i * 16 + fr) : 0u;
+      unsigned char *ip = img + (i * 16 + fr) * EP_PITCH + fq * 8;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        uint2 ad = {0u, 0u};
+        if constexpr (ACC) ad = *reinterpret_cast<const uint2 *>(ip + j * 32);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[i][j][r];
+          if constexpr (ACC) {
+            const uint32_t w = r < 2 ? ad.x : ad.y;
+            v[r] = v[r] + __uint_as_float((r & 1) ? (w & 0xffff0000u) : (w << 16));
+          }
+          v[r] = v[r] + bb[j][r];
+          if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
+          if constexpr (DROP) v[r] = drop_hash_k(rk, ck[j][r]) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
+        }
+        const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2));
+        const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2));
+        *reinterpret_cast<uint2 *>(ip + j * 32) = uint2{lo, hi};
+      }
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  const bool drop = RELU && a.drop_thresh;
+  if (a.accum) {
+    if (drop) body(T_{}, T_{}); else body(T_{}, F_{});
+  } else {
+    if (drop) body(F_{}, T_{}); else body(F_{}, F_{});
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
+    const int q = it * 64 + lane;
+    const int lr = q / CPR, ch = q % CPR;
+    const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
+    const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
+    if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+  }
+}
+
 // WM x WN waves, each owning FM x FN fragments of 16 x 16.
 template <int WM, int WN, int FM, int FN, bool RELU>
 __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
@@ -415,7 +598,7 @@ __global__ __launch_bounds__(512) void fc_fwd_bf16_p3(FcB16Args a) {
 // variant 5: 8 waves of 128 x 64 as fc_fwd_bf16.  Requires lda1 == lda2 and
 // ldw1 == ldw2 (one offset set for both k phases); the host falls back to
 // fc_fwd_bf16 otherwise.
-template <int WM, int WN, int FM, int FN, bool RELU, bool SCHED, bool PRIO>
+template <int WM, int WN, int FM, int FN, bool RELU, bool SCHED, bool PRIO, int TRO = 0>
 __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
@@ -499,10 +682,17 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
     }
   };
   auto mma = [&](const bf16x8(&av)[FM], const bf16x8(&bv)[FN]) {
+    if constexpr (TRO != 0) {  // W x A^T; consecutive MFMAs share their first operand, as below
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
   };
   auto barrier = [&]() {  // this wave's DMA landed and its fragment reads returned; then all waves
     __builtin_amdgcn_sched_barrier(0);
@@ -561,10 +751,17 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
     mma(a1, b1);
   }
   // the epilogue image reuses the tile buffers: the last (empty-range) DMA has landed, every wave
-  // is past its reads
+  // is past its reads (the transposed form writes straight from registers: no image, no barrier)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  epilogue_bf16<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+  if constexpr (TRO == 1) {
+    epilogue_bf16_t<FM, FN, RELU>(a, acc, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+  } else if constexpr (TRO == 2) {
+    __syncthreads();
+    epilogue_bf16_ti<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+  } else {
+    __syncthreads();
+    epilogue_bf16<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+  }
 }
 
 // ---- weight gradient dW = G^T X in bf16 (fp32 out) ---------------------------
@@ -818,7 +1015,7 @@ lpg_status launch_bf16_p3(FcB16Args a, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
-template <int WM, int WN, int FM, int FN, bool SCHED = false, bool PRIO = false>
+template <int WM, int WN, int FM, int FN, bool SCHED = false, bool PRIO = false, int TRO = 0>
 lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   a.mt = (a.M + BM - 1) / BM;
@@ -826,11 +1023,11 @@ lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_bf16: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, true, SCHED, PRIO>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0,
-                       s, a);
+    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, true, SCHED, PRIO, TRO>), dim3((unsigned)nwg),
+                       dim3(64 * WM * WN), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, false, SCHED, PRIO>), dim3((unsigned)nwg), dim3(64 * WM * WN),
-                       0, s, a);
+    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, false, SCHED, PRIO, TRO>), dim3((unsigned)nwg),
+                       dim3(64 * WM * WN), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -843,13 +1040,16 @@ bool p_ok(const FcB16Args &a) {
   return (256 * a.lda1 + K) * 2 < ((int64_t)1 << 31) && (256 * a.ldw1 + K) * 2 < ((int64_t)1 << 31);
 }
 
-// lpg_fc_bf16_set_variant: 0 = by size (128 x 128 below 4096 rows, else 7, else 2), 1 = 128 x 128,
+// lpg_fc_bf16_set_variant: 0 = by size (128 x 128 below 4096 rows, else 10, else 2), 1 = 128 x 128,
 // 2 = 256^2 2-buffer, 3 = 256^2 3-buffer,
 // 4 / 5 = fc_bf16_p with 4 / 8 waves, 6 = 5 with the reads and DMA placed between the MFMAs
-// (sched_group_barrier), 7 = 6 + s_setprio 1 for waves 4-7, 8 = 4 placed; 100 / 101 = wgrad_bf16
-// with 4 / 8 waves, 102 / 103 = 101 placed / + prio, 104 = 100 placed (102 the default; measured
-// at the c5 shapes, profiles/r02_kbench_bf16.log: 7 1209-1212 TF/s vs hipBLASLt 1268 (2 1033);
-// 102 1172-1222 vs hipBLASLt's bf16-output GEMM 924-1004)
+// (sched_group_barrier), 7 = 6 + s_setprio 1 for waves 4-7, 8 = 4 placed, 9 = 7 with transposed
+// fragments (W x A^T) and a register epilogue, 10 = 7 with transposed fragments through the LDS
+// image (8-byte LDS accesses); 100 / 101 = wgrad_bf16 with 4 / 8 waves, 102 / 103 = 101 placed /
+// + prio, 104 = 100 placed (102 the default; measured at the c5 shapes,
+// profiles/r02_kbench_bf16.log: 7 1209-1212 TF/s vs hipBLASLt 1268 (2 1033); 102 1172-1222 vs
+// hipBLASLt's bf16-output GEMM 924-1004; profiles/r02_kbench_fck10.log: 10 = 7 on plain
+// epilogues, ReLU + dropout + accumulate 1.745 -> 1.662 ms at M = 200K, K = 2048)
 int g_bf16_variant = 0;
 int g_wgrad_bf16_variant = 102;
 
@@ -897,19 +1097,23 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
   const bool relu = flags & 1;
   if (g_bf16_variant == 1 || (g_bf16_variant == 0 && M < 4096))
     return launch_bf16<2, 2, 4, 4>(a, relu, s);  // 128 x 128
-  if (g_bf16_variant == 0 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true, true>(a, relu, s);  // = 7
+  if (g_bf16_variant == 0 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true, true, 2>(a, relu, s);  // = 10
   if (g_bf16_variant == 3) return launch_bf16_p3(a, relu, s);  // 256 x 256, BK 32, 3 buffers
   if (g_bf16_variant == 4 && p_ok(a)) return launch_bf16_p<2, 2, 8, 8>(a, relu, s);  // 4 waves of 128 x 128
   if (g_bf16_variant == 5 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4>(a, relu, s);  // 8 waves of 128 x 64
   if (g_bf16_variant == 6 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true>(a, relu, s);  // + placed reads
   if (g_bf16_variant == 7 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true, true>(a, relu, s);  // + prio
   if (g_bf16_variant == 8 && p_ok(a)) return launch_bf16_p<2, 2, 8, 8, true>(a, relu, s);  // 4 waves, placed
+  if (g_bf16_variant == 9 && p_ok(a))  // 7 with transposed fragments: register epilogue, 8-byte stores
+    return launch_bf16_p<2, 4, 8, 4, true, true, 1>(a, relu, s);
+  if (g_bf16_variant == 10 && p_ok(a))  // 7 with transposed fragments through the image (8-byte LDS accesses)
+    return launch_bf16_p<2, 4, 8, 4, true, true, 2>(a, relu, s);
   return launch_bf16<2, 4, 8, 4>(a, relu, s);    // 256 x 256, BK 64, 2 buffers
 }
 
 extern "C" lpg_status lpg_fc_bf16_set_variant(int32_t v) {
-  LPG_REQUIRE((v >= 0 && v <= 8) || (v >= 100 && v <= 104),
-              "lpg_fc_bf16_set_variant: variant %d not in [0, 8] or [100, 104]", v);
+  LPG_REQUIRE((v >= 0 && v <= 10) || (v >= 100 && v <= 104),
+              "lpg_fc_bf16_set_variant: variant %d not in [0, 10] or [100, 104]", v);
   if (v >= 100)
     g_wgrad_bf16_variant = v;
   else

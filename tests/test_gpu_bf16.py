@@ -43,7 +43,7 @@ def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
     torch.testing.assert_close(got, ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("M,N,K,relu,bias", [
     (5000, 1024, 1024, True, True),  # re-associated left2right root part
     (129, 130, 64, False, True),     # N % 8 != 0: per-element epilogue
@@ -92,13 +92,44 @@ def test_fc_bf16_tile_variants_identical():
     L = _lib.lib()
     outs = []
     try:
-        for v in (1, 2, 3, 4, 5, 6, 7, 8):
+        for v in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
             L.lpg_fc_bf16_set_variant(v)
             outs.append(fc_forward_bf16(A1, W1, A2, W2, b, True, 0.2, seed=9))
     finally:
         L.lpg_fc_bf16_set_variant(0)
     for o in outs:
         assert torch.equal(o, outs[0])
+
+
+@pytest.mark.parametrize("M,N,relu,drop,bias", [
+    (5000, 1024, True, 0.1, True),    # interior tiles: the register epilogue's unchecked path
+    (4099, 1000, True, 0.3, False),   # ragged rows and columns
+    (3000, 512, False, 0.0, True),    # linear (the lin_rel GEMM of the re-associated direction)
+])
+def test_fc_bf16_transposed_fragments_identical(M, N, relu, drop, bias):
+    """Variants 9 / 10 issue the MFMA as W x A^T (transposed fragments; 9: register epilogue with
+    8-byte stores, 10: 8-byte accesses to the LDS image): the same bits as the LDS-image epilogue
+    of variant 7, with accumulate and dropout."""
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward_bf16
+
+    g = torch.Generator().manual_seed(M + N)
+    A = torch.randn(M, 256, generator=g).to(BF).to(DEV)
+    W = (torch.randn(N, 256, generator=g) * 0.05).to(BF).to(DEV)
+    P = torch.randn(M, N, generator=g).to(BF).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV) if bias else None
+    L = _lib.lib()
+    outs = []
+    try:
+        for v in (7, 9, 10):
+            L.lpg_fc_bf16_set_variant(v)
+            for acc in (False, True):
+                outs.append(fc_forward_bf16(A, W, None, None, b, relu, drop, seed=3, out=P.clone() if acc else None,
+                                            accumulate=acc))
+    finally:
+        L.lpg_fc_bf16_set_variant(0)
+    for k in (2, 4):
+        assert torch.equal(outs[0], outs[k]) and torch.equal(outs[1], outs[k + 1])
 
 
 def test_fc_bf16_asymmetric_identity():

@@ -239,11 +239,12 @@ def bench_bf16(out):
             return fc_forward_bf16(B1, V1, B2, V2, b2, True)
         return f
     y0 = var(0)()
-    for v in (1, 2, 3, 4, 5, 6, 7, 8):
+    for v in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
         assert torch.equal(var(v)(), y0), f"bf16 variant {v} differs"
     t = timeit({"lpg_fc_bf16 v2 256x256 2buf": var(2), "lpg_fc_bf16 v5 8-wave pipelined": var(5),
                 "lpg_fc_bf16 v6 v5 + placed": var(6), "lpg_fc_bf16 v7 v6 + prio": var(7),
-                "lpg_fc_bf16 v8 4-wave placed": var(8),
+                "lpg_fc_bf16 v8 4-wave placed": var(8), "lpg_fc_bf16 v9 v7 + transposed fragments": var(9),
+                "lpg_fc_bf16 v10 transposed via image": var(10),
                 "torch_bf16_1gemm_relu": lambda: torch.relu(F.linear(Bc, Vc, b2.to(torch.bfloat16)))})
     L.lpg_fc_bf16_set_variant(0)
     for k, v in t.items():
@@ -251,10 +252,13 @@ def bench_bf16(out):
 
 
 def bench_fck(out):
-    """lpg_fc_bf16 (default variant) at M = 200K / 100K, N = 2048 for K = 1024 .. 8192 (one phase,
-    no epilogue options, and with ReLU + dropout + accumulate): per-block fixed cost vs the k loop."""
+    """lpg_fc_bf16 variants 7 / 9 / 10 at M = 200K / 100K, N = 2048 for K = 1024 .. 8192 (one phase,
+    no epilogue options, and with ReLU + dropout + accumulate in place): per-block fixed cost vs
+    the k loop."""
+    from lpgnn import _lib
     from lpgnn.fc import fc_forward_bf16
 
+    L = _lib.lib()
     BF = torch.bfloat16
     for M in (200_000, 100_000):
         for K in (1024, 2048, 4096, 8192):
@@ -262,9 +266,17 @@ def bench_fck(out):
             W = (torch.randn(2048, K, device="cuda") * 0.02).to(BF)
             b = torch.randn(2048, device="cuda")
             P = torch.randn(M, 2048, device="cuda").to(BF)
-            t = timeit({"plain": lambda: fc_forward_bf16(A, W, None, None, None, False),
-                        "relu+drop+acc": lambda: fc_forward_bf16(A, W, None, None, b, True, 0.1, 7, out=P.clone(),
-                                                                 accumulate=True)}, rounds=5, iters=3)
+
+            def run(v, acc, A=A, W=W, b=b, P=P):
+                def f():
+                    L.lpg_fc_bf16_set_variant(v)
+                    if acc:
+                        return fc_forward_bf16(A, W, None, None, b, True, 0.1, 7, out=P, accumulate=True)
+                    return fc_forward_bf16(A, W, None, None, None, False)
+                return f
+            t = timeit({f"v{v} {'relu+drop+acc' if acc else 'plain'}": run(v, acc) for v in (7, 9, 10)
+                        for acc in (False, True)}, rounds=5, iters=3)
+            L.lpg_fc_bf16_set_variant(0)
             for k, v in t.items():
                 out[f"fcK M={M} K={K} {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * K / v / 1e9)
             del A, W, P
