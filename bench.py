@@ -307,7 +307,7 @@ def main():
                    "hid": args.hids, "depth": args.depth, "parallelism": parallelism},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("lpg spmm_bf16_rowwave" if args.bf16 else "lpg spmm_f32_rowslim / rowwave")
+                     "kernel": ("lpg spmm_bf16_rowslim / rowwave" if args.bf16 else "lpg spmm_f32_rowslim / rowwave")
                                + " (F=hid, both directions, fwd+bwd)",
                      "bytes_per_launch": per_launch_bytes,
                      "avg_launch_ms": spmm_ms / max(launches, 1), "launches": launches,

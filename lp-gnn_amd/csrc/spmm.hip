@@ -573,6 +573,42 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, cons
   }
 }
 
+// F <= FW <= 64, bf16: FW lanes per row, 256/FW rows per block (the c5 conv1 input, F = 8); the
+// same per-element sequence as spmm_bf16_generic (fp32 sum in edge order, one RNE at the end).
+template <int FW, int U>
+__global__ __launch_bounds__(kBlock) void spmm_bf16_narrow(
+    int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
+    uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
+  constexpr int RPB = kBlock / FW;
+  const int sub = threadIdx.x % FW;
+  const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / FW;
+  if (row >= n_rows) return;
+  const bool active = sub < F;
+  const uint16_t *Xs = X + sub;
+  float acc = 0.f;
+  int64_t e = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  for (; e + U <= end; e += U) {
+    int c[U];
+    float v[U], x[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      c[k] = col[e + k];
+      v[k] = val[e + k];
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) x[k] = active ? bf16_to_f32(Xs[(int64_t)c[k] * ldx]) : 0.f;
+#pragma unroll
+    for (int k = 0; k < U; ++k) acc = acc + v[k] * x[k];
+  }
+  for (; e < end; ++e) {
+    const float x = active ? bf16_to_f32(Xs[(int64_t)col[e] * ldx]) : 0.f;
+    acc = acc + val[e] * x;
+  }
+  if (active) Y[row * ldy + sub] = (uint16_t)f32_to_bf16_rne(acc);
+}
+
 __global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
@@ -777,6 +813,14 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
   LPG_REQUIRE(A->nnz == 0 || X != nullptr, "lpg_spmm_bf16: X is NULL");
   hipStream_t s = as_stream(stream);
   const bool vec = (F % 8 == 0) && (ldx % 8 == 0) && (ldy % 8 == 0) && aligned16(X) && aligned16(Y);
+  if (F <= 64) {  // narrow: FW lanes per row (any alignment)
+    const int FW = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
+    dim3 grid((unsigned)((A->n_rows + kBlock / FW - 1) / (kBlock / FW)));
+    if (FW == 8) return launch(spmm_bf16_narrow<8, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    if (FW == 16) return launch(spmm_bf16_narrow<16, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    if (FW == 32) return launch(spmm_bf16_narrow<32, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    return launch(spmm_bf16_narrow<64, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+  }
   if (!vec || F < 256) {
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
     return launch(spmm_bf16_generic, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);

@@ -129,8 +129,9 @@ def test_long_rows_cross_chunk_boundaries():
     assert np.array_equal(spmm_forward(adj.bwd, torch.from_numpy(Xc).to(DEV)).cpu().numpy(), O.spmm_f32(*AT, Xc))
 
 
-@pytest.mark.parametrize("Fd", [8, 40, 512, 1024, 2048, 2056])
+@pytest.mark.parametrize("Fd", [3, 8, 17, 40, 64, 100, 512, 1024, 2048, 2056])
 def test_bf16_bitwise(Fd):
+    """bf16 SpMM bitwise vs the oracle: narrow (F <= 64), generic, slice and wide-row paths."""
     from lpgnn.sparse import spmm_forward
 
     rng = np.random.default_rng(100 + Fd)
