@@ -818,7 +818,7 @@ __device__ __forceinline__ void dma16_asm(uint64_t p, uint32_t n, unsigned char 
 
 __device__ __forceinline__ int wg_f(int r) { return (r & 3) | ((r & 8) >> 1); }
 
-template <int WM, int WN, int FM, int FN, bool SCHED, bool PRIO>
+template <int WM, int WN, int FM, int FN, bool SCHED, bool PRIO, bool TRO = false>
 __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
   constexpr int NW = WM * WN;
   constexpr int BN = WM * FM * 16, BKC = WN * FN * 16;  // output rows (n) x columns (k)
@@ -899,10 +899,17 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
     for (int j = 0; j < FN; ++j) bv[j] = tr2(Xs, ((wn * FN + j) ^ flv) * 32);
   };
   auto mma = [&](const bf16x8(&av)[FM], const bf16x8(&bv)[FN]) {
+    if constexpr (TRO) {  // X^T G: four consecutive k (dW columns) per lane, for 16-byte stores
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
   };
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
@@ -958,9 +965,29 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (empty) DMA lands before the wave ends
 
-  // D map: row (n) = 4 * (lane >> 4) + r, col (k) = lane & 15
   float *P = a.P + s * a.ps;
   const int fr = lane & 15;
+  if constexpr (TRO) {  // D map: n = lane & 15, k = 4 * (lane >> 4) + r
+    const bool vec = a.ldp % 4 == 0 && (reinterpret_cast<uintptr_t>(P) & 15) == 0;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int64_t row = n0 + wm * FM * 16 + i * 16 + fr;
+      if (row >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t col = k0 + wn * FN * 16 + j * 16 + 4 * g;
+        if (vec && col + 3 < a.K) {
+          *reinterpret_cast<f32x4 *>(P + row * a.ldp + col) = acc[i][j];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (col + r < a.K) P[row * a.ldp + col + r] = acc[i][j][r];
+        }
+      }
+    }
+    return;
+  }
+  // D map: row (n) = 4 * (lane >> 4) + r, col (k) = lane & 15
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int64_t col = k0 + wn * FN * 16 + j * 16 + fr;
@@ -1112,8 +1139,8 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
 }
 
 extern "C" lpg_status lpg_fc_bf16_set_variant(int32_t v) {
-  LPG_REQUIRE((v >= 0 && v <= 10) || (v >= 100 && v <= 104),
-              "lpg_fc_bf16_set_variant: variant %d not in [0, 10] or [100, 104]", v);
+  LPG_REQUIRE((v >= 0 && v <= 10) || (v >= 100 && v <= 105),
+              "lpg_fc_bf16_set_variant: variant %d not in [0, 10] or [100, 105]", v);
   if (v >= 100)
     g_wgrad_bf16_variant = v;
   else
@@ -1151,6 +1178,7 @@ extern "C" lpg_status lpg_wgrad_bf16(int64_t R, int64_t N, int64_t K, const uint
     case 101: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, false, false>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
     case 102: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, true, false>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
     case 103: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, true, true>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
+    case 105: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, true, false, true>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
     default: hipLaunchKernelGGL((wgrad_bf16<2, 2, 8, 8, true, false>), dim3((unsigned)nwg), dim3(256), 0, s, w); break;
   }
   LPG_HIP(hipGetLastError());

@@ -241,7 +241,7 @@ def test_wgrad_bf16_vs_fp64(R, N, K):
     L = _lib.lib()
     try:
         outs = []
-        for v in (100, 101, 102, 103, 104, 100):
+        for v in (100, 101, 102, 103, 104, 105, 100):
             L.lpg_fc_bf16_set_variant(v)
             outs.append(wgrad_bf16(Gd, Xd))
     finally:

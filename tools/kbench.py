@@ -9,6 +9,7 @@ bf16bwd: the c5 backward GEMMs (lpg_wgrad_bf16, lpg_fc_bf16 on transposed weight
 load : graph load at c2 -- reference chain (to_undirected + MyToBipartite + device pack) vs direct pack
 spmm : lpg_spmm_f32 at c2, both directions, slice widths 256/512/1024
 bwd  : the FC backward GEMMs at c2 shapes through torch (hipBLASLt)
+wgk  : lpg_wgrad_bf16 vs R (per-launch fixed cost)
 x3epi: lpg_fc_x3 at the c2 shapes, one line per epilogue (plain / ReLU+dropout / +accumulate / +heads)
 """
 import json
@@ -282,6 +283,48 @@ def bench_fck(out):
             del A, W, P
 
 
+def bench_wgk(out):
+    """lpg_wgrad_bf16 (default variant) at N = K = 2048 for R = 25K .. 400K: the per-launch fixed
+    cost (prologue, partial-tile epilogue, fold) against the per-row slope."""
+    from lpgnn import _lib
+    from lpgnn.fc import wgrad_bf16
+
+    L = _lib.lib()
+    BF = torch.bfloat16
+    for R in (25_000, 50_000, 100_000, 200_000, 400_000):
+        G = torch.randn(R, 2048, device="cuda").to(BF)
+        X = torch.relu(torch.randn(R, 2048, device="cuda")).to(BF)
+
+        def run(v, G=G, X=X):
+            def f():
+                L.lpg_fc_bf16_set_variant(v)
+                return wgrad_bf16(G, X)
+            return f
+        assert torch.equal(run(102)(), run(105)())
+        t = timeit({f"v{v}": run(v) for v in (102, 105)}, rounds=5, iters=4)
+        L.lpg_fc_bf16_set_variant(102)
+        for k, v in t.items():
+            out[f"wgk R={R} {k}"] = dict(ms=v, tflops=2.0 * R * 2048 * 2048 / v / 1e9)
+        del G, X
+
+
+def bench_rbwd(out):
+    """lpg_relu_bwd_colsum_bf16 at the c5 shapes (200K / 100K x 2048) and lpg_relu_bwd_colsum_f32
+    at c2 (200K x 1024): GB/s of g + y read and dZ written."""
+    from lpgnn.fc import relu_bwd_colsum, relu_bwd_colsum_bf16
+
+    for M in (200_000, 100_000):
+        g = torch.randn(M, 2048, device="cuda").to(torch.bfloat16)
+        y = torch.randn(M, 2048, device="cuda").to(torch.bfloat16)
+        t = timeit({"bf16": lambda: relu_bwd_colsum_bf16(g, y, 1.1, True)}, rounds=7, iters=5)
+        out[f"rbwd bf16 M={M}"] = dict(ms=t["bf16"], gbs=3 * M * 2048 * 2 / t["bf16"] / 1e6)
+        del g, y
+    g = torch.randn(200_000, 1024, device="cuda")
+    y = torch.randn(200_000, 1024, device="cuda")
+    t = timeit({"f32": lambda: relu_bwd_colsum(g, y, 1.1, True)}, rounds=7, iters=5)
+    out["rbwd f32 M=200000"] = dict(ms=t["f32"], gbs=3 * 200_000 * 1024 * 4 / t["f32"] / 1e6)
+
+
 def bench_x3epi(out):
     """lpg_fc_x3 at the c2 FC shapes with each epilogue: plain, ReLU + dropout (two phases) and
     ReLU + dropout + accumulate (in place, no clone in the timed region), heads fused."""
@@ -427,7 +470,7 @@ if __name__ == "__main__":
     for w in which:
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
-         "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi,
+         "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi, "wgk": bench_wgk, "rbwd": bench_rbwd,
          "load": bench_load, "fcpi": bench_fcpi}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
