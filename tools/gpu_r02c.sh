@@ -16,6 +16,7 @@ for s in ${*:-tests c2 c5}; do
     c5) run bench_c5 600 python -u bench.py --config c5 --steps 10 --warmup 3 ;;
     kbf16) run kbench_bf16 400 python -u tools/kbench.py bf16 bf16bwd ;;
     mtests) run pytest_model 400 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_x3.py tests/test_gpu_partition.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    c4n1) run bench_c4_n1 900 python -u bench.py --config c4 --steps 5 --warmup 2 ;;
     rehearse2)  # the N = 2 c4 bench path end to end, 2 ranks sharing this box's GPU over gloo
       LPGNN_DIST_BACKEND=gloo run rehearse_c4_n2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29600 bench.py --gpus 2 --steps 3 --warmup 1 ;;
