@@ -20,6 +20,9 @@ for s in ${*:-tests c2 c5}; do
     rehearse2)  # the N = 2 c4 bench path end to end, 2 ranks sharing this box's GPU over gloo
       LPGNN_DIST_BACKEND=gloo run rehearse_c4_n2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29600 bench.py --gpus 2 --steps 3 --warmup 1 ;;
+    rehearse4)  # N = 4: four ranks sharing this box's GPU over gloo (three exchange peers per rank)
+      LPGNN_DIST_BACKEND=gloo run rehearse_c4_n4 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+        --master-addr 127.0.0.1 --master-port 29601 bench.py --gpus 4 --steps 2 --warmup 1 ;;
     *) echo "unknown stage $s"; exit 2 ;;
   esac
 done
