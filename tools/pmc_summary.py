@@ -42,7 +42,7 @@ def main(fetch_dir, write_dir, out, workload):
         wk = sum(w) / len(w)
         res[name[:200]] = dict(dispatches=len(f), fetch_kib_raw=fk, write_kib=wk,
                                hbm_bytes=(2 * fk + wk) * 1024.0)
-    spmm = [v for k, v in res.items() if "spmm_f32_rowwave" in k or "spmm_f32_rowslim" in k or "spmm_bf16_rowwave" in k]
+    spmm = [v for k, v in res.items() if any(s in k for s in ("spmm_f32_rowwave", "spmm_f32_rowslim", "spmm_bf16_rowwave", "spmm_bf16_rowslim"))]
     hbm = None
     if spmm:
         # the rowwave kernel runs only at F = hid in the bench step
