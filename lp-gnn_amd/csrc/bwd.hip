@@ -33,7 +33,10 @@ constexpr int kUnrollWgrad = LPG_WGRAD_UNROLL;
 #ifndef LPG_LINEAR_UNROLL
 #define LPG_LINEAR_UNROLL 4
 #endif
-constexpr int kRowsLinear = 128;
+#ifndef LPG_LINEAR_ROWS
+#define LPG_LINEAR_ROWS 128
+#endif
+constexpr int kRowsLinear = LPG_LINEAR_ROWS;
 constexpr int kUnrollLinear = LPG_LINEAR_UNROLL;
 constexpr int kMaxSmallK = 16;
 constexpr int kSmallNMax = 4;

@@ -321,7 +321,10 @@ __global__ __launch_bounds__(256) void relu_dropout_bwd_f32(int64_t n4, const fl
 // (pik), added into the +0 total in order -- bitwise identical.
 // Position i of a part's chain -> k: groups of 8, inside a group 0,4,1,5,2,6,3,7.
 __host__ __device__ constexpr int pik(int i) { return (i & ~7) + (i & 1) * 4 + ((i >> 1) & 3); }
-constexpr int kSmallKRows = 64;
+#ifndef LPG_SMALLK_ROWS
+#define LPG_SMALLK_ROWS 64
+#endif
+constexpr int kSmallKRows = LPG_SMALLK_ROWS;
 
 template <int K>
 __device__ __forceinline__ void load_row_k(float (&x)[K > 0 ? K : 1], const float *A, int64_t ld, int64_t m) {

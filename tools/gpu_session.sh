@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests -> smoke -> bench -> rocprofv3 kernel stats.
 # Usage (from the repo root, via gpurun):  bash tools/gpu_session.sh [stages...]
-# stages: tests smoke bench prof pmc bench_c5 prof_c5 kbench kbfc   (default: tests smoke bench prof)
+# stages: tests smoke bench prof pmc bench_c5 prof_c5 kbench kbfc mfma   (default: tests smoke bench prof)
 # Every GPU step has its own time limit; the script stops at the first step
 # that crashes, aborts or times out (exit >= 2 or signal), and continues past
 # a plain test failure (exit 1) so the bench still runs.
@@ -46,6 +46,7 @@ for s in $STAGES; do
         python "$ROOT/bench.py" --config c5 --steps 3 --warmup 2 --profile-only
       ;;
     kbench) step kbench 600 python tools/kbench.py ;;
+    mfma) step mfma_peak 120 tools/experiments/mfma_peak 3 ;;  # sustained bf16 MFMA rate (build: see the source)
     kbfc) step kbench_fc 600 python tools/kbench.py fc ;;
     pmc)
       step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \

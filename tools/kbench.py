@@ -464,6 +464,33 @@ def bench_fcpi(out):
         del A1, A2
 
 
+def bench_stream(out):
+    """The c2 step's streaming kernels at 100K / 200K x 1024 (GB/s of the bytes each must move):
+    heads + ReLU backward (read Y, write dZ), conv1 weight gradients from (g, y) (read both),
+    conv1 forward with ReLU + dropout (write C); torch copy_ / fill_ as the box's streaming rates."""
+    from lpgnn.fc import fc_forward, heads_relu_bwd, relu_wgrad_smallk
+
+    dev = "cuda"
+    for M in (100_000, 200_000):
+        g = torch.randn(M, 1024, device=dev)
+        y = torch.relu(torch.randn(M, 1024, device=dev))
+        G3 = torch.randn(M, 3, device=dev)
+        W3 = torch.randn(3, 1024, device=dev)
+        X8, X8b = torch.randn(M, 8, device=dev), torch.randn(M, 8, device=dev)
+        W8, W8b = torch.randn(1024, 8, device=dev), torch.randn(1024, 8, device=dev)
+        b = torch.randn(1024, device=dev)
+        dst = torch.empty_like(g)
+        nb = M * 1024 * 4
+        t = timeit({"heads_relu_bwd": lambda: heads_relu_bwd(G3, W3, y, 1.1, True),
+                    "relu_wgrad_smallk": lambda: relu_wgrad_smallk(g, y, 1.1, X8, X8b, True),
+                    "conv1_fwd": lambda: fc_forward(X8, W8, X8b, W8b, b, True, 0.1, 7),
+                    "torch_copy": lambda: dst.copy_(g), "torch_fill": lambda: dst.fill_(1.0)})
+        for k, v in t.items():
+            nbytes = nb * (1 if k in ("conv1_fwd", "torch_fill") else 2)
+            out[f"stream M={M} {k}"] = dict(ms=v, gbs=nbytes / v / 1e6)
+        del g, y, dst
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["fc", "spmm", "bwd"]
     out = {}
@@ -471,7 +498,7 @@ if __name__ == "__main__":
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
          "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi, "wgk": bench_wgk, "rbwd": bench_rbwd,
-         "load": bench_load, "fcpi": bench_fcpi}[w](out)
+         "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
