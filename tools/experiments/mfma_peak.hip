@@ -27,8 +27,8 @@ typedef __attribute__((__vector_size__(4 * sizeof(float)))) float f32x4;
   } while (0)
 
 // NACC independent accumulators per wave; `iters` rounds of NACC MFMAs.  NREAD > 0: every round
-// first reads NREAD B operands from LDS (ds_read_b128, the address stepping with the round), the
-// MFMAs cycling through them -- the operand traffic a GEMM's inner loop carries (the x3 FC reads
+// reads the NEXT round's NREAD B operands from LDS (ds_read_b128, the address stepping with the
+// round; in flight under this round's MFMAs), the MFMAs cycling through the current ones -- the operand traffic a GEMM's inner loop carries (the x3 FC reads
 // 0.29 fragments per MFMA, the bf16 FC 0.375)
 template <int NACC, int NREAD = 0>
 __global__ __launch_bounds__(256) void mfma_loop(const unsigned *__restrict__ seed, int iters, float *__restrict__ out,
@@ -47,7 +47,12 @@ __global__ __launch_bounds__(256) void mfma_loop(const unsigned *__restrict__ se
     b[i] = (__bf16)__uint_as_float(((rb & 0x807fffffu) | (0x7bu + (rb >> 29)) << 23));
   }
   f32x4 acc[NACC];
-  for (int j = 0; j < NACC; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // distinct starting values: identical chains (same operands, same start) would be merged by the compiler
+  for (int j = 0; j < NACC; ++j) {
+    f32x4 v;
+    for (int e = 0; e < 4; ++e) v[e] = __uint_as_float(0x3f800000u | (next() >> 9));
+    acc[j] = v;
+  }
   __shared__ bf16x8 lds[4][8][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if constexpr (NREAD > 0) {
@@ -62,13 +67,20 @@ __global__ __launch_bounds__(256) void mfma_loop(const unsigned *__restrict__ se
     __syncthreads();
   }
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  bf16x8 cur[NREAD > 0 ? NREAD : 1];
+  if constexpr (NREAD > 0) {
+#pragma unroll
+    for (int r = 0; r < NREAD; ++r) cur[r] = lds[wave][r & 7][lane];
+  }
   for (int it = 0; it < iters; ++it) {
-    if constexpr (NREAD > 0) {
-      bf16x8 bv[NREAD];
+    if constexpr (NREAD > 0) {  // next round's operands in flight under this round's MFMAs
+      bf16x8 nxt[NREAD];
 #pragma unroll
-      for (int r = 0; r < NREAD; ++r) bv[r] = lds[wave][(it + r) & 7][lane];
+      for (int r = 0; r < NREAD; ++r) nxt[r] = lds[wave][(it + 1 + r) & 7][lane];
 #pragma unroll
-      for (int j = 0; j < NACC; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv[j % NREAD], acc[j], 0, 0, 0);
+      for (int j = 0; j < NACC; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, cur[j % NREAD], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < NREAD; ++r) cur[r] = nxt[r];
     } else {
 #pragma unroll
       for (int j = 0; j < NACC; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
