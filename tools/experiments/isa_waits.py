@@ -2,7 +2,7 @@
 global loads, vmcnt waits, barriers, labels and branches (to check that
 loads stay in flight where a kernel means them to).
 
-usage: python tools/isa_waits.py file.s mangled_kernel_name_substring
+usage: python tools/experiments/isa_waits.py file.s mangled_kernel_name_substring
 """
 import re
 import sys

@@ -3,7 +3,7 @@ hidden-layer shape a few times -- a short program for rocprofv3 PMC passes."""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "lp-gnn_amd")]
 import torch  # noqa: E402
 

@@ -398,6 +398,32 @@ def bench_bf16bwd(out):
         del G, X
 
 
+def bench_tail(out):
+    """Wave-quantisation tail of the FC launches: time vs M around the c2 / c5 row counts
+    (x3: 128x128 tiles, 8 n-tiles, 512 block slots -> one round = 8192 rows; bf16: 256x256 tiles,
+    8 n-tiles, 256 slots -> one round = 8192 rows)."""
+    from lpgnn.fc import fc_forward, fc_forward_bf16
+
+    for arith, N, K, dt in (("x3", 1024, 1024, torch.float32), ("bf16", 2048, 2048, torch.bfloat16)):
+        Mmax = 114_688
+        A1 = torch.randn(Mmax, K, device="cuda").to(dt)
+        W1 = (torch.randn(N, K, device="cuda") * 0.03)
+        b = torch.randn(N, device="cuda")
+        if dt == torch.bfloat16:
+            W1 = W1.to(dt)
+        for M in (90_112, 98_304, 100_000, 102_400, 106_496, 114_688):
+            A = A1[:M]
+
+            def f(A=A):
+                if arith == "bf16":
+                    return fc_forward_bf16(A, W1, None, None, b, True)
+                return fc_forward(A, W1, None, None, b, True, arith="x3")
+            t = timeit({"f": f}, rounds=7, iters=4)["f"]
+            out[f"tail {arith} M={M} N={N} K={K}"] = dict(ms=t, us_per_krow=t * 1e6 / M,
+                                                          tflops=2.0 * M * N * K / t / 1e9)
+        del A1
+
+
 def bench_load(out):
     import time
 
@@ -498,7 +524,7 @@ if __name__ == "__main__":
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
          "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi, "wgk": bench_wgk, "rbwd": bench_rbwd,
-         "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream}[w](out)
+         "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream, "tail": bench_tail}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
