@@ -43,6 +43,7 @@
 #include "common.h"
 #include "fc_common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 #pragma clang fp contract(off)
@@ -1608,6 +1609,14 @@ __global__ __launch_bounds__(256) void wgrad_fold(int64_t N, int64_t K, int64_t 
 }
 
 int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
+  static const int64_t forced = [] {  // LPGNN_WGRAD_SPLITS: experiment knob (read once)
+    const char *e = getenv("LPGNN_WGRAD_SPLITS");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  if (forced > 0) {
+    const int64_t nch = (R + 31) / 32;
+    return forced < nch ? forced : (nch > 0 ? nch : 1);
+  }
   const int64_t tiles = ((N + WG_T - 1) / WG_T) * ((K + WG_T - 1) / WG_T);
   const int64_t nchunks = (R + 31) / 32;
   int64_t S = (2048 + tiles - 1) / tiles;  // aim at >= 2048 blocks (8 per CU)

@@ -422,6 +422,14 @@ def bench_tail(out):
             out[f"tail {arith} M={M} N={N} K={K}"] = dict(ms=t, us_per_krow=t * 1e6 / M,
                                                           tflops=2.0 * M * N * K / t / 1e9)
         del A1
+    from lpgnn.fc import wgrad
+    for R in (100_000, 200_000, 400_000):
+        G = torch.randn(R, 1024, device="cuda")
+        X = torch.randn(R, 1024, device="cuda")
+        t = timeit({"f": lambda G=G, X=X: wgrad(G, X, arith="x3")}, rounds=7, iters=4)["f"]
+        out[f"tail wgrad_x3 R={R} splits={os.environ.get('LPGNN_WGRAD_SPLITS', 'auto')}"] = dict(
+            ms=t, tflops=2.0 * R * 1024 * 1024 / t / 1e9)
+        del G, X
 
 
 def bench_load(out):
