@@ -257,6 +257,14 @@ lpg_status lpg_relu_bwd_colsum_f32(int64_t M, int64_t N, const float *g, int64_t
 lpg_status lpg_relu_bwd_colsum_bf16(int64_t M, int64_t N, const uint16_t *g, int64_t ldg, const uint16_t *y,
                                     int64_t ldy, float scale, uint16_t *out, int64_t ldo, float *db,
                                     void *workspace, void *stream);
+/* Column sums only (db[n] = sum_m g[m, n], fp32) of a bf16 dZ that already went
+ * through its ReLU / dropout backward -- the output of lpg_fc_bf16_relu_bwd.
+ * Same blocks and fold as lpg_relu_bwd_colsum_bf16, so the same db bits for the
+ * same dZ.  Replaces the bias-gradient half of that pass in the folded c5
+ * backward (torch's `db = dZ.sum(0)` of the Linear, arch.py:57-62 via
+ * train.py:128 loss.backward()).  Workspace: lpg_relu_bwd_colsum_workspace_bytes. */
+lpg_status lpg_colsum_bf16(int64_t M, int64_t N, const uint16_t *g, int64_t ldg, float *db, void *workspace,
+                           void *stream);
 
 /* Weight gradients of a GraphConv whose inputs are narrow (conv1: the 8 LP
  * features, arch.py:170): dW1 = dZ^T A1 [N, K1], dW2 = dZ^T A2 [N, K2], in the
@@ -298,6 +306,20 @@ lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int
  * lpg_wgrad_bf16 kernel (100 / 101 = 4 / 8 waves, 102 = 101 placed (the
  * default), 103 = 102 + s_setprio, 104 = 100 placed; identical bits). */
 lpg_status lpg_fc_bf16_set_variant(int32_t v);
+
+/* The input gradient of a GraphConv layer whose input is the previous layer's
+ * ReLU + dropout output Y, with that layer's ReLU/dropout backward folded into
+ * the store (c5 backward, train.py:128 through arch.py:185-188's
+ * conv -> dropout -> ReLU):
+ *   C = (Y > 0) ? bf16(bf16(A1 W1^T + A2 W2^T [+ C]) * scale) : 0
+ * bit for bit lpg_fc_bf16 (no bias, no ReLU) followed by
+ * lpg_relu_bwd_colsum_bf16(C, Y, scale) -- without that pass's read of C and
+ * write of dZ.  flags: only bit 1 (C holds a bf16 addend).  N, ldc, ldy
+ * multiples of 8, C and Y 16-byte aligned; other requirements as lpg_fc_bf16. */
+lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
+                                const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc, int32_t flags,
+                                const uint16_t *Y, int64_t ldy, float scale, void *stream);
 
 /* bf16 weight gradient (c5 backward, reference train.py:128 loss.backward()
  * through GraphConv's lin_rel / lin_root): dW[n, k] = sum_r G[r, n] X[r, k],

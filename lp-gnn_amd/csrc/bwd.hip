@@ -100,6 +100,9 @@ __device__ __forceinline__ uint32_t f32_to_bf16_rne(float f) {
   return u >> 16;
 }
 
+// MASK = false (lpg_colsum_bf16): g already is dZ (the folded form, lpg_fc_bf16_relu_bwd) --
+// only the column sums, same blocks and order, so the same db bits; y and out unused.
+template <bool MASK>
 __global__ __launch_bounds__(kT) void relu_bwd_colsum_bf16_p1(int64_t M, int64_t N, const uint16_t *__restrict__ g,
                                                               int64_t ldg, const uint16_t *__restrict__ y,
                                                               int64_t ldy, float scale, uint16_t *__restrict__ out,
@@ -116,28 +119,33 @@ __global__ __launch_bounds__(kT) void relu_bwd_colsum_bf16_p1(int64_t M, int64_t
         uint32_t o = 0;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-          const float yf = bf16_to_f32((yw[h] >> (16 * e)) & 0xffffu);
-          const uint32_t d = yf > 0.f ? f32_to_bf16_rne(bf16_to_f32((gw[h] >> (16 * e)) & 0xffffu) * scale) : 0u;
+          uint32_t d = (gw[h] >> (16 * e)) & 0xffffu;
+          if constexpr (MASK) {
+            const float yf = bf16_to_f32((yw[h] >> (16 * e)) & 0xffffu);
+            d = yf > 0.f ? f32_to_bf16_rne(bf16_to_f32(d) * scale) : 0u;
+          }
           s[2 * h + e] = s[2 * h + e] + bf16_to_f32(d);
           o |= d << (16 * e);
         }
         ow[h] = o;
       }
-      *reinterpret_cast<uint4 *>(out + m * ldo + c) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      if constexpr (MASK) *reinterpret_cast<uint4 *>(out + m * ldo + c) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
     };
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
     int64_t m = r0;
     for (; m + 4 <= r1; m += 4) {
       uint4 gv[4], yv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         gv[u] = *reinterpret_cast<const uint4 *>(g + (m + u) * ldg + c);
-        yv[u] = *reinterpret_cast<const uint4 *>(y + (m + u) * ldy + c);
+        yv[u] = MASK ? *reinterpret_cast<const uint4 *>(y + (m + u) * ldy + c) : z4;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) row(gv[u], yv[u], m + u);
     }
     for (; m < r1; ++m)
-      row(*reinterpret_cast<const uint4 *>(g + m * ldg + c), *reinterpret_cast<const uint4 *>(y + m * ldy + c), m);
+      row(*reinterpret_cast<const uint4 *>(g + m * ldg + c),
+          MASK ? *reinterpret_cast<const uint4 *>(y + m * ldy + c) : z4, m);
     if (part) {
       float *pp = part + (int64_t)blockIdx.x * N + c;
       *reinterpret_cast<float4 *>(pp) = make_float4(s[0], s[1], s[2], s[3]);
@@ -436,8 +444,8 @@ extern "C" lpg_status lpg_relu_bwd_colsum_bf16(int64_t M, int64_t N, const uint1
   hipStream_t s = as_stream(stream);
   const int64_t nblk = (M + kRowsColsum - 1) / kRowsColsum;
   float *part = db ? static_cast<float *>(workspace) : nullptr;
-  hipLaunchKernelGGL(relu_bwd_colsum_bf16_p1, dim3((unsigned)nblk), dim3(kT), 0, s, M, N, g, ldg, y, ldy, scale, out,
-                     ldo, part);
+  hipLaunchKernelGGL(relu_bwd_colsum_bf16_p1<true>, dim3((unsigned)nblk), dim3(kT), 0, s, M, N, g, ldg, y, ldy, scale,
+                     out, ldo, part);
   LPG_HIP(hipGetLastError());
   if (db) {
     const float *img;
@@ -445,6 +453,34 @@ extern "C" lpg_status lpg_relu_bwd_colsum_bf16(int64_t M, int64_t N, const uint1
     hipLaunchKernelGGL(sum_partials, dim3((unsigned)((N + kT - 1) / kT)), dim3(kT), 0, s, nrow, N, img, db);
     LPG_HIP(hipGetLastError());
   }
+  return LPG_OK;
+}
+
+// db = column sums of a bf16 dZ that already went through its ReLU / dropout backward (the
+// folded form, lpg_fc_bf16_relu_bwd): the blocks, partials and fold of lpg_relu_bwd_colsum_bf16,
+// so db is bitwise what that kernel returns for the same dZ.  Workspace:
+// lpg_relu_bwd_colsum_workspace_bytes(M, N).
+extern "C" lpg_status lpg_colsum_bf16(int64_t M, int64_t N, const uint16_t *g, int64_t ldg, float *db,
+                                      void *workspace, void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0, "lpg_colsum_bf16: negative size");
+  LPG_REQUIRE(db != nullptr || N == 0, "lpg_colsum_bf16: NULL db");
+  if (M == 0 || N == 0) {
+    if (N > 0) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, as_stream(stream)));
+    return LPG_OK;
+  }
+  LPG_REQUIRE(g && workspace && aligned16(workspace), "lpg_colsum_bf16: NULL pointer or unaligned workspace");
+  LPG_REQUIRE(N % 8 == 0 && ldg % 8 == 0 && aligned16(g),
+              "lpg_colsum_bf16: N / ldg must be multiples of 8, g 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int64_t nblk = (M + kRowsColsum - 1) / kRowsColsum;
+  float *part = static_cast<float *>(workspace);
+  hipLaunchKernelGGL(relu_bwd_colsum_bf16_p1<false>, dim3((unsigned)nblk), dim3(kT), 0, s, M, N, g, ldg,
+                     (const uint16_t *)nullptr, (int64_t)0, 1.f, (uint16_t *)nullptr, (int64_t)0, part);
+  LPG_HIP(hipGetLastError());
+  const float *img;
+  const int64_t nrow = fold(nblk, N, part, part + nblk * N, &img, s);
+  hipLaunchKernelGGL(sum_partials, dim3((unsigned)((N + kT - 1) / kT)), dim3(kT), 0, s, nrow, N, img, db);
+  LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
 

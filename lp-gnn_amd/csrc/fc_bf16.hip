@@ -48,6 +48,11 @@ struct FcB16Args {
   uint32_t drop_thresh;
   float drop_scale;
   int32_t accum;  // flags bit 1: C holds a bf16 addend, C = bf16(act(A1 W1^T + A2 W2^T + C + bias))
+  // lpg_fc_bf16_relu_bwd: the ReLU + dropout backward of the layer whose output is `my`, applied to
+  // the stored bf16 result: C = (my > 0) ? bf16(C * mscale) : 0 (nullptr: off)
+  const uint16_t *my;
+  int64_t ldy;
+  float mscale;
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
@@ -60,6 +65,26 @@ __device__ __forceinline__ uint16_t to_bf16_rne(float f) {
 }
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// The folded ReLU/dropout backward on 8 stored bf16 values: (y > 0) ? RNE(g * scale) : 0 per
+// element -- the arithmetic of lpg_relu_bwd_colsum_bf16 on the same bf16 g, so the same bits.
+__device__ __forceinline__ uint4 relu_bwd8(uint4 g, uint4 y, float scale) {
+  const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, yw[4] = {y.x, y.y, y.z, y.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float yf = __uint_as_float(((yw[h] >> (16 * e)) & 0xffffu) << 16);
+      const float gf = __uint_as_float(((gw[h] >> (16 * e)) & 0xffffu) << 16);
+      const uint32_t d = yf > 0.f ? (uint32_t)to_bf16_rne(gf * scale) : 0u;
+      w |= d << (16 * e);
+    }
+    o[h] = w;
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
 
 // Epilogue shared by the bf16 FC kernels: wave `wave` owns the FM*16 x FN*16
 // output block at (wrow0, wcol0); C/D map of 16x16x32: col = lane & 15, row =
@@ -135,8 +160,11 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
       const int q = it * 64 + lane;
       const int lr = q / CPR, ch = q % CPR;
       const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
-      const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
-      if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+      uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
+      if (row < a.M && col < a.N) {
+        if (a.my) v = relu_bwd8(v, *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col), a.mscale);
+        *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+      }
     }
     return;
   }
@@ -340,8 +368,11 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
     const int q = it * 64 + lane;
     const int lr = q / CPR, ch = q % CPR;
     const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
-    const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
-    if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+    uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
+    if (row < a.M && col < a.N) {
+      if (a.my) v = relu_bwd8(v, *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col), a.mscale);
+      *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+    }
   }
 }
 
@@ -1097,6 +1128,12 @@ int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
 }  // namespace
 }  // namespace lpg
 
+namespace lpg {
+namespace {
+lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant);
+}  // namespace
+}  // namespace lpg
+
 using namespace lpg;
 
 extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
@@ -1120,8 +1157,42 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
     a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);
     a.drop_scale = 1.f / (1.f - dropout_p);
   }
-  hipStream_t s = as_stream(stream);
-  const bool relu = flags & 1;
+  return fc_bf16_dispatch(a, flags & 1, as_stream(stream), g_bf16_variant);
+}
+
+// The input gradient of a layer whose input went through the previous layer's ReLU + dropout,
+// with that backward folded into the store: C = (Y > 0) ? bf16(bf16(G1 W1^T + G2 W2^T [+ C]) * scale) : 0
+// -- bit for bit lpg_fc_bf16 followed by lpg_relu_bwd_colsum_bf16(C, Y, scale) (whose bias column
+// sums the caller takes from lpg_colsum_bf16 on C).  Saves the separate pass's read of C and
+// write of dZ (c5: 2 x [rows, 2048] bf16 per layer input).
+extern "C" lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                           const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
+                                           int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
+                                           int32_t flags, const uint16_t *Y, int64_t ldy, float scale, void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_bf16_relu_bwd: negative size");
+  if (M == 0 || N == 0) return LPG_OK;
+  LPG_REQUIRE(C != nullptr && ldc >= N && Y != nullptr && ldy >= N, "lpg_fc_bf16_relu_bwd: bad C/ldc or Y/ldy");
+  LPG_REQUIRE(N % 8 == 0 && ldc % 8 == 0 && ldy % 8 == 0 && aligned16(C) && aligned16(Y),
+              "lpg_fc_bf16_relu_bwd: N, ldc, ldy must be multiples of 8, C and Y 16-byte aligned");
+  LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "lpg_fc_bf16_relu_bwd: K1, K2 must be multiples of %d", BK);
+  LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1), "lpg_fc_bf16_relu_bwd: bad A1/W1");
+  LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2), "lpg_fc_bf16_relu_bwd: bad A2/W2");
+  LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
+                  (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
+              "lpg_fc_bf16_relu_bwd: A/W must be 16-byte aligned with leading dimensions multiple of 8");
+  LPG_REQUIRE((flags & ~2) == 0, "lpg_fc_bf16_relu_bwd: only the accumulate flag (2) is accepted, got 0x%x", flags);
+  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, nullptr, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, 0, 0u, 1.f, (flags >> 1) & 1,
+              Y, ldy, scale};
+  // the fold lives in the LDS-image epilogues: variants without one (3, 9) take the default kernel
+  const int v = (g_bf16_variant == 3 || g_bf16_variant == 9) ? 0 : g_bf16_variant;
+  return fc_bf16_dispatch(a, false, as_stream(stream), v);
+}
+
+namespace lpg {
+namespace {
+lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant) {
+  const int64_t M = a.M;
+  const int g_bf16_variant = variant;
   if (g_bf16_variant == 1 || (g_bf16_variant == 0 && M < 4096))
     return launch_bf16<2, 2, 4, 4>(a, relu, s);  // 128 x 128
   if (g_bf16_variant == 0 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true, true, 2>(a, relu, s);  // = 10
@@ -1137,6 +1208,8 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
     return launch_bf16_p<2, 4, 8, 4, true, true, 2>(a, relu, s);
   return launch_bf16<2, 4, 8, 4>(a, relu, s);    // 256 x 256, BK 64, 2 buffers
 }
+}  // namespace
+}  // namespace lpg
 
 extern "C" lpg_status lpg_fc_bf16_set_variant(int32_t v) {
   LPG_REQUIRE((v >= 0 && v <= 10) || (v >= 100 && v <= 105),

@@ -36,6 +36,8 @@ HEADER_SYMBOLS = (
     "lpg_fc_set_variant",
     "lpg_fc_bf16",
     "lpg_fc_bf16_set_variant",
+    "lpg_fc_bf16_relu_bwd",
+    "lpg_colsum_bf16",
     "lpg_wgrad_bf16_workspace_bytes",
     "lpg_wgrad_bf16",
     "lpg_split3_f32",
@@ -116,6 +118,11 @@ def lib() -> ctypes.CDLL:
                              c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_p]
     L.lpg_fc_f32.restype = c_i32
     L.lpg_fc_bf16.argtypes = L.lpg_fc_f32.argtypes
+    L.lpg_fc_bf16_relu_bwd.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
+                                       c_p, c_i64, c_i32, c_p, c_i64, ctypes.c_float, c_p]
+    L.lpg_fc_bf16_relu_bwd.restype = c_i32
+    L.lpg_colsum_bf16.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p]
+    L.lpg_colsum_bf16.restype = c_i32
     L.lpg_split3_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_i64, c_p]
     L.lpg_split3_f32.restype = c_i32
     L.lpg_fc_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64,

@@ -113,14 +113,14 @@ class GraphConvTwoDirection(nn.Module):
         self.right2left = GraphConv((right_dim, left_dim), out_dim)
 
     def forward(self, left_feas, right_feas, edge_index: BipartiteCSR, edge_weight=None, relu: bool = False,
-                dropout: float = 0.0):
+                dropout: float = 0.0, fold_in: bool = False):
         # edge_index is A (m x n, rows = cons).  arch.py:71-74: l2r = A^T, r2l = A.
         if edge_weight is None and isinstance(edge_index, BipartiteCSR) and \
                 getattr(edge_index, "partitioned_conv", None) is None:
             # one autograd node for both directions (lpgnn.conv): same forward,
             # fused gradient sums and the cheaper association in backward
             return _conv.two_direction(left_feas, right_feas, edge_index, self.left2right, self.right2left,
-                                       relu, dropout)
+                                       relu, dropout, fold_in)
         tdc = getattr(edge_index, "two_direction_conv", None)  # row-partitioned multi-GPU adjacency
         if tdc is not None and edge_weight is None:
             out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout)
@@ -201,7 +201,9 @@ class GCN_FC(GCNBase):
             # dropout (x * mask / (1-p), a non-negative scale), so the ReLU is
             # fused into the FC and dropout follows it (inside the conv, so a
             # partitioned run drops each variable once, at its owner).
-            left, right = conv(left, right, edge_index, relu=True, dropout=dp)
+            # fold_in: the previous layer's outputs feed only this layer (bf16: its ReLU/dropout
+            # backward runs in this layer's input-gradient stores)
+            left, right = conv(left, right, edge_index, relu=True, dropout=dp, fold_in=True)
         out = None
         if fuse_heads:  # last layer + heads (arch.py:184-190) as one node: one backward pass over its output
             last = layers[-1]

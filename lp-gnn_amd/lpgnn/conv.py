@@ -53,6 +53,9 @@ _OVERLAP = os.environ.get("LPGNN_OVERLAP", "0") == "1"
 REASSOCIATE = os.environ.get("LPGNN_REASSOC", "1") == "1"
 # LPGNN_FUSE_HEAD_FWD=0: the heads' forward as its own Linear kernels instead of in the last layer's FC epilogue
 FUSE_HEAD_FWD = os.environ.get("LPGNN_FUSE_HEAD_FWD", "1") == "1"
+# LPGNN_FOLD_RELU_BWD=0: in the bf16 (c5) model, keep the previous layer's ReLU/dropout backward as
+# its own pass (relu_bwd_colsum_bf16) instead of folding it into this layer's input-gradient store
+FOLD_RELU_BWD = os.environ.get("LPGNN_FOLD_RELU_BWD", "1") == "1"
 _SIDE = {}
 
 
@@ -141,15 +144,23 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
 
 class _TwoDirection(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+    def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
+                prev=None):
+        """``prev``: the backward node of the layer that produced (left, right) with ReLU (bf16), whose
+        outputs feed only this layer -- its ReLU/dropout backward is then folded into this layer's
+        input-gradient stores (lpg_fc_bf16_relu_bwd) and it takes dZ as given (column sums only)."""
         left_new, right_new, saved, _ = _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r,
                                                       w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
+        ctx.in_scale = None
+        if prev is not None:
+            ctx.in_scale = prev.scale
+            prev.out_folded = True
         ctx.save_for_backward(*saved)
         return left_new, right_new
 
     @staticmethod
     def backward(ctx, g_left, g_right):
-        return _backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right)
+        return _backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None,)
 
 
 def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
@@ -164,6 +175,9 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
     def mask(g, y, want_db):
         if g is None:
             g = torch.zeros_like(y)
+        if getattr(ctx, "out_folded", False):  # the next layer's input-gradient store applied our ReLU backward
+            g = g.to(dt).contiguous()
+            return g, (_fc.colsum_bf16(g) if want_db else None)
         if not ctx.relu:
             g = g.to(dt).contiguous()
             return g, (g.float().sum(0) if want_db else None)
@@ -243,17 +257,21 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
     if relt_l:
         dw_rel_r2l = wg(t_l, right)
 
-    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root):
-        """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients)."""
+    in_scale = getattr(ctx, "in_scale", None) if bf16 else None
+
+    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in):
+        """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients);
+        with a folded previous layer, through its ReLU/dropout backward (x_in = its output)."""
+        kw = {} if in_scale is None else {"mask": (x_in, in_scale)}
         if t_src:  # both terms over the same rows: one two-part GEMM
-            return ig(T, w_rel, dz_root, w_root)
-        return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True)
+            return ig(T, w_rel, dz_root, w_root, **kw)
+        return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True, **kw)
 
     g_l = g_r = None
     if need[1]:  # right = src of right2left (S = A), dst of left2right
-        g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r)
+        g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r, right)
     if need[0]:  # left = src of left2right (S = A^T), dst of right2left
-        g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l)
+        g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l, left)
     return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 
@@ -305,8 +323,17 @@ def two_direction_heads(left: Tensor, right: Tensor, adj: BipartiteCSR, left2rig
 
 
 def two_direction(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, relu: bool = False,
-                  dropout: float = 0.0):
-    """GraphConvTwoDirection.forward (arch.py:65-81) through one autograd node."""
+                  dropout: float = 0.0, fold_in: bool = False):
+    """GraphConvTwoDirection.forward (arch.py:65-81) through one autograd node.  ``fold_in``: the
+    caller guarantees (left, right) feed nothing but this layer (GCN_FC's layer chain) -- if they
+    are a bf16 ReLU layer's outputs, that layer's ReLU/dropout backward is folded into this one's
+    input-gradient stores."""
+    prev = None
+    if fold_in and FOLD_RELU_BWD and left.dtype == torch.bfloat16 and torch.is_grad_enabled():
+        g = left.grad_fn
+        if g is not None and g is right.grad_fn and isinstance(g, _TwoDirection._backward_cls) and \
+                getattr(g, "relu", False) and getattr(g, "bf16", False):
+            prev = g
     return _TwoDirection.apply(left, right, adj, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                left2right.lin_root.weight, right2left.lin_rel.weight, right2left.lin_rel.bias,
-                               right2left.lin_root.weight, bool(relu), float(dropout))
+                               right2left.lin_root.weight, bool(relu), float(dropout), prev)

@@ -243,9 +243,13 @@ def _prep_bf16(t: Tensor | None) -> Tensor | None:
 
 def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                     relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
-                    accumulate: bool = False, key: str | None = None) -> Tensor:
+                    accumulate: bool = False, key: str | None = None, mask=None) -> Tensor:
     """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16);
-    ``accumulate`` adds the bf16 addend held in ``out`` (overwritten)."""
+    ``accumulate`` adds the bf16 addend held in ``out`` (overwritten).
+    ``mask`` = (Y, scale): an input gradient with the previous layer's ReLU/dropout backward
+    folded into the store, C = (Y > 0) ? bf16(C * scale) : 0 (lpg_fc_bf16_relu_bwd; no bias /
+    ReLU / dropout of its own) -- the bits of this call without ``mask`` followed by
+    relu_bwd_colsum_bf16(C, Y, scale)."""
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -262,6 +266,25 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0)
+    if mask is not None:
+        Y, scale = mask
+        if relu or bias is not None or dropout_p > 0:
+            raise RuntimeError("lpgnn bf16 FC: the folded ReLU backward takes no bias / ReLU / dropout")
+        if (Y.shape != (M, N) or Y.dtype != torch.bfloat16 or Y.device != A1.device or Y.stride(1) != 1
+                or Y.stride(0) % 8 or Y.data_ptr() % 16 or N % 8 or C.stride(0) % 8 or C.data_ptr() % 16):
+            # layouts the folded store does not take: the same bits in two passes
+            C = fc_forward_bf16(A1, W1, A2, W2, None, False, out=out, accumulate=accumulate, key=key)
+            return relu_bwd_colsum_bf16(C, Y, scale, False)[0]
+        with torch.cuda.device(A1.device):
+            tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, key or "lin-bf16-relubwd"))
+            st = L.lpg_fc_bf16_relu_bwd(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
+                                        K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
+                                        None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
+                                        C.data_ptr(), C.stride(0), flags, Y.data_ptr(), Y.stride(0), float(scale),
+                                        _lib.stream_of(A1))
+            TIMER.stop(tok)
+        _lib.check(st, "lpg_fc_bf16_relu_bwd")
+        return C
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, key or ("relu-bf16" if relu else "lin-bf16")))
         st = L.lpg_fc_bf16(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
@@ -302,14 +325,17 @@ def wgrad_bf16(G: Tensor, X: Tensor) -> Tensor:
 
 
 def input_grad_bf16(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | None = None,
-                    out: Tensor | None = None, accumulate: bool = False) -> Tensor:
+                    out: Tensor | None = None, accumulate: bool = False, mask=None) -> Tensor:
     """G1 W1 [+ G2 W2] [+ out] in bf16 for Linear weights W [out, in]: the
     c5 input gradient of lin_rel / lin_root on the bf16 FC kernel (lpg_fc_bf16
-    with the weights transposed; fp32 accumulation, one bf16 rounding)."""
+    with the weights transposed; fp32 accumulation, one bf16 rounding).
+    ``mask`` = (Y, scale): the previous layer's ReLU/dropout backward folded into the store
+    (fc_forward_bf16)."""
     t = lambda W: None if W is None else W.detach().t().to(torch.bfloat16).contiguous()
     G1 = G1.to(torch.bfloat16)
     G2 = None if G2 is None else G2.to(torch.bfloat16)
-    return fc_forward_bf16(G1, t(W1), G2, t(W2), None, False, out=out, accumulate=accumulate, key="igrad-bf16")
+    return fc_forward_bf16(G1, t(W1), G2, t(W2), None, False, out=out, accumulate=accumulate, key="igrad-bf16",
+                           mask=mask)
 
 
 def relu_dropout_bwd(g: Tensor, y: Tensor, scale: float) -> Tensor:
@@ -368,6 +394,23 @@ def relu_bwd_colsum_bf16(g: Tensor, y: Tensor, scale: float, want_db: bool):
                                         None if ws is None else ws.data_ptr(), _lib.stream_of(g))
     _lib.check(st, "lpg_relu_bwd_colsum_bf16")
     return out, db
+
+
+def colsum_bf16(g: Tensor) -> Tensor:
+    """db = g.sum(0) in fp32 for a bf16 dZ that already went through its ReLU/dropout backward
+    (lpg_colsum_bf16: the blocks and fold of relu_bwd_colsum_bf16, so the same bits)."""
+    M, N = g.shape
+    if g.dtype != torch.bfloat16 or N % 8 or g.stride(1) != 1 or g.stride(0) % 8 or g.data_ptr() % 16:
+        g = g.to(torch.bfloat16).contiguous()
+        if N % 8:
+            return g.float().sum(0)
+    L = _lib.lib()
+    db = torch.empty(N, dtype=torch.float32, device=g.device)
+    ws = _workspace(L.lpg_relu_bwd_colsum_workspace_bytes(M, N), g.device)
+    with torch.cuda.device(g.device):
+        st = L.lpg_colsum_bf16(M, N, g.data_ptr(), g.stride(0), db.data_ptr(), ws.data_ptr(), _lib.stream_of(g))
+    _lib.check(st, "lpg_colsum_bf16")
+    return db
 
 
 def wgrad_smallk(dz: Tensor, A1: Tensor, A2: Tensor | None):

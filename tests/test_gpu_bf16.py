@@ -304,3 +304,90 @@ def test_input_grad_bf16(M, N, Nout, two, acc):
     got = input_grad_bf16(G1, W1, G2, W2, out=P, accumulate=acc)
     assert got.dtype == BF and got.shape == (M, N)
     torch.testing.assert_close(got.float(), ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
+
+
+@pytest.mark.parametrize("M,N,Nin,two,acc,variant", [
+    (1000, 2048, 2048, False, True, 0),    # 128 x 128 kernel (M < 4096), accumulate form
+    (1000, 256, 512, True, False, 0),      # two-part form
+    (5003, 2048, 2048, True, False, 0),    # variant 10 (transposed fragments, LDS image)
+    (5003, 1024, 2048, False, True, 0),    # accumulate on variant 10, ragged last tile
+    (5003, 1032, 512, False, True, 7),     # untransposed image epilogue, ragged columns
+    (5003, 512, 512, True, False, 9),      # register-epilogue variant: routed to the default kernel
+    (5003, 512, 512, False, True, 3),      # BK 32 kernel: routed to the default kernel
+])
+def test_fc_bf16_relu_bwd_folded_bitwise(M, N, Nin, two, acc, variant):
+    """lpg_fc_bf16_relu_bwd = input_grad_bf16 then relu_bwd_colsum_bf16 (the separate pass), bit
+    for bit, for the accumulate and two-part forms the c5 backward uses; lpg_colsum_bf16 on the
+    folded dZ = the separate pass's bias gradient, bit for bit."""
+    from lpgnn import _lib
+    from lpgnn.fc import colsum_bf16, input_grad_bf16, relu_bwd_colsum_bf16
+
+    L = _lib.lib()
+    torch.manual_seed(M + N + variant)
+    G1 = torch.randn(M, N, device=DEV).to(BF)
+    W1 = torch.randn(N, Nin, device=DEV) * 0.03  # Linear [out = N, in = Nin]: dX = G W
+    G2 = torch.randn(M, N, device=DEV).to(BF) if two else None
+    W2 = torch.randn(N, Nin, device=DEV) * 0.03 if two else None
+    Y = torch.relu(torch.randn(M, Nin, device=DEV)).to(BF)
+    add = torch.randn(M, Nin, device=DEV).to(BF) if acc else None
+    try:
+        _lib.check(L.lpg_fc_bf16_set_variant(variant), "set_variant")
+        for scale in (1.0, 1.0 / 0.9):
+            ref = input_grad_bf16(G1, W1, G2, W2, out=None if add is None else add.clone(), accumulate=acc)
+            want, db_want = relu_bwd_colsum_bf16(ref, Y, scale, True)
+            got = input_grad_bf16(G1, W1, G2, W2, out=None if add is None else add.clone(), accumulate=acc,
+                                  mask=(Y, scale))
+            assert torch.equal(got, want)
+            assert torch.equal(colsum_bf16(got), db_want)
+    finally:
+        L.lpg_fc_bf16_set_variant(0)
+
+
+def test_fc_bf16_relu_bwd_rejects_bias_and_bad_layouts():
+    from lpgnn import _lib
+    from lpgnn.fc import fc_forward_bf16, relu_bwd_colsum_bf16
+
+    A = torch.randn(64, 128, device=DEV).to(BF)
+    W = (torch.randn(24, 128, device=DEV) * 0.05).to(BF)
+    Y = torch.relu(torch.randn(64, 24, device=DEV)).to(BF)
+    with pytest.raises(RuntimeError):
+        fc_forward_bf16(A, W, None, None, torch.zeros(24, device=DEV), False, mask=(Y, 1.0))
+    # a column count the folded store does not take (N % 8 != 0 after the output view): two passes, same bits
+    W20 = W[:20].contiguous()
+    Y20 = Y[:, :20]
+    got = fc_forward_bf16(A, W20, None, None, None, False, mask=(Y20, 1.25))
+    want = relu_bwd_colsum_bf16(fc_forward_bf16(A, W20, None, None, None, False), Y20, 1.25, False)[0]
+    assert torch.equal(got, want)
+    L = _lib.lib()
+    C = torch.empty(64, 24, dtype=BF, device=DEV)
+    st = L.lpg_fc_bf16_relu_bwd(64, 24, 128, A.data_ptr(), 128, W.data_ptr(), 128, 0, None, 0, None, 0,
+                                C.data_ptr(), 24, 1, Y.data_ptr(), 24, 1.0, None)  # ReLU flag: refused
+    assert st != 0
+
+
+def test_gcn_fc_bf16_folded_relu_bwd_identical(monkeypatch):
+    """The c5 model's backward with each layer's ReLU/dropout backward folded into the next layer's
+    input-gradient stores gives the same loss and the same gradient bits as the separate passes
+    (training dropout, same dropout seeds)."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, conv, synth
+    from lpgnn.train import balanced
+
+    g = synth.uniform_lp(1500, 5200, 30000, seed=5)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                           y_s=torch.from_numpy(g.y_s).to(DEV), y_t=torch.from_numpy(g.y_t).to(DEV),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=256, depth=5, dp=0.1, compute_dtype="bf16").to(DEV).train()
+    out = {}
+    for fold in (True, False):
+        monkeypatch.setattr(conv, "FOLD_RELU_BWD", fold)
+        model.zero_grad()
+        torch.manual_seed(321)  # same dropout seeds
+        lc, lv = model(batch)
+        loss = balanced(lc, lv, batch.y_s, batch.y_t)
+        loss.backward()
+        out[fold] = (loss.item(), {k: p.grad.clone() for k, p in model.named_parameters()})
+    assert out[True][0] == out[False][0]
+    for k, v in out[True][1].items():
+        assert torch.equal(v, out[False][1][k]), k
