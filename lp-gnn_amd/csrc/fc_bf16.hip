@@ -86,6 +86,22 @@ __device__ __forceinline__ uint4 relu_bwd8(uint4 g, uint4 y, float scale) {
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// The mask rows (Y) of a wave's store loop, issued together after the accumulators are in the
+// image: one memory latency per epilogue instead of one per 16-B chunk (a dependent load inside
+// the store loop cost ~0.3 ms per c5 launch).  Out-of-range chunks read as zeros (never stored).
+template <int SIT, int CPR>
+__device__ __forceinline__ void load_mask_rows(const FcB16Args &a, int lane, int64_t wrow0, int64_t wcol0,
+                                               uint4 (&yv)[SIT]) {
+#pragma unroll
+  for (int it = 0; it < SIT; ++it) {
+    const int q = it * 64 + lane;
+    const int lr = q / CPR, ch = q % CPR;
+    const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
+    yv[it] = (row < a.M && col < a.N) ? *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col)
+                                      : make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 // Epilogue shared by the bf16 FC kernels: wave `wave` owns the FM*16 x FN*16
 // output block at (wrow0, wcol0); C/D map of 16x16x32: col = lane & 15, row =
 // 4 * (lane >> 4) + r.  `smem` must be free (every wave past its last tile read).
@@ -153,16 +169,19 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
     } else {
       if (drop) body(F_{}, T_{}); else body(F_{}, F_{});
     }
+    constexpr int SIT = FM * 16 * CPR / 64;
+    uint4 yv[SIT];
+    if (a.my) load_mask_rows<SIT, CPR>(a, lane, wrow0, wcol0, yv);  // all in flight before the first use
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
+    for (int it = 0; it < SIT; ++it) {
       const int q = it * 64 + lane;
       const int lr = q / CPR, ch = q % CPR;
       const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
       uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
       if (row < a.M && col < a.N) {
-        if (a.my) v = relu_bwd8(v, *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col), a.mscale);
+        if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
         *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
       }
     }
@@ -361,16 +380,19 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
   } else {
     if (drop) body(F_{}, T_{}); else body(F_{}, F_{});
   }
+  constexpr int SIT = FM * 16 * CPR / 64;
+  uint4 yv[SIT];
+  if (a.my) load_mask_rows<SIT, CPR>(a, lane, wrow0, wcol0, yv);  // all in flight before the first use
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
+  for (int it = 0; it < SIT; ++it) {
     const int q = it * 64 + lane;
     const int lr = q / CPR, ch = q % CPR;
     const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
     uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
     if (row < a.M && col < a.N) {
-      if (a.my) v = relu_bwd8(v, *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col), a.mscale);
+      if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
       *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
     }
   }
