@@ -307,6 +307,12 @@ lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int
  * default), 103 = 102 + s_setprio, 104 = 100 placed; identical bits). */
 lpg_status lpg_fc_bf16_set_variant(int32_t v);
 
+/* dst[c, r] = src[r, c] for bf16 [R, C] (R, C, lds, ldd multiples of 8, 16-byte
+ * aligned): the transposed weights the c5 input gradients multiply by
+ * (dX = dZ W of a Linear, arch.py:57-62 through train.py:128). */
+lpg_status lpg_transpose_bf16(int64_t R, int64_t C, const uint16_t *src, int64_t lds, uint16_t *dst, int64_t ldd,
+                              void *stream);
+
 /* The input gradient of a GraphConv layer whose input is the previous layer's
  * ReLU + dropout output Y, with that layer's ReLU/dropout backward folded into
  * the store (c5 backward, train.py:128 through arch.py:185-188's

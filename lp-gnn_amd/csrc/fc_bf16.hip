@@ -1153,6 +1153,35 @@ int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
 namespace lpg {
 namespace {
 lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant);
+
+// dst[c, r] = src[r, c] for bf16 through a 64 x 64 LDS tile, 16-byte global accesses both ways
+// (the input gradients' W^T; torch's strided copy ran these at ~0.5 TB/s).  R, C multiples of 8.
+__global__ __launch_bounds__(256) void transpose_bf16(int64_t R, int64_t C, const uint16_t *__restrict__ src,
+                                                      int64_t lds, uint16_t *__restrict__ dst, int64_t ldd) {
+  constexpr int P = 64 + 8;  // tile pitch (elements): 144-B rows, 16-B aligned
+  __shared__ __attribute__((aligned(16))) uint16_t t[64 * P];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + 256 * k, row = q >> 3, ch = q & 7;
+    const int64_t r = r0 + row, c = c0 + ch * 8;
+    const uint4 v = (r < R && c < C) ? *reinterpret_cast<const uint4 *>(src + r * lds + c) : make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4 *>(t + row * P + ch * 8) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + 256 * k, col = q >> 3, rch = q & 7;
+    const int64_t c = c0 + col, r = r0 + rch * 8;
+    if (c < C && r < R) {
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        w[e] = (uint32_t)t[(rch * 8 + 2 * e) * P + col] | ((uint32_t)t[(rch * 8 + 2 * e + 1) * P + col] << 16);
+      *reinterpret_cast<uint4 *>(dst + c * ldd + r) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
 }  // namespace
 }  // namespace lpg
 
@@ -1232,6 +1261,20 @@ lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant) 
 }
 }  // namespace
 }  // namespace lpg
+
+extern "C" lpg_status lpg_transpose_bf16(int64_t R, int64_t C, const uint16_t *src, int64_t lds, uint16_t *dst,
+                                         int64_t ldd, void *stream) {
+  LPG_REQUIRE(R >= 0 && C >= 0, "lpg_transpose_bf16: negative size");
+  if (R == 0 || C == 0) return LPG_OK;
+  LPG_REQUIRE(src && dst && R % 8 == 0 && C % 8 == 0 && lds >= C && ldd >= R && lds % 8 == 0 && ldd % 8 == 0 &&
+                  aligned16(src) && aligned16(dst),
+              "lpg_transpose_bf16: R, C, lds, ldd must be multiples of 8 (lds >= C, ldd >= R), buffers 16-byte aligned");
+  const dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
+  LPG_REQUIRE((R + 63) / 64 < 65536, "lpg_transpose_bf16: too many rows");
+  hipLaunchKernelGGL(transpose_bf16, grid, dim3(256), 0, as_stream(stream), R, C, src, lds, dst, ldd);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
 
 extern "C" lpg_status lpg_fc_bf16_set_variant(int32_t v) {
   LPG_REQUIRE((v >= 0 && v <= 10) || (v >= 100 && v <= 105),

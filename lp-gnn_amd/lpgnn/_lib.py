@@ -38,6 +38,7 @@ HEADER_SYMBOLS = (
     "lpg_fc_bf16_set_variant",
     "lpg_fc_bf16_relu_bwd",
     "lpg_colsum_bf16",
+    "lpg_transpose_bf16",
     "lpg_wgrad_bf16_workspace_bytes",
     "lpg_wgrad_bf16",
     "lpg_split3_f32",
@@ -123,6 +124,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_bf16_relu_bwd.restype = c_i32
     L.lpg_colsum_bf16.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p]
     L.lpg_colsum_bf16.restype = c_i32
+    L.lpg_transpose_bf16.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p]
+    L.lpg_transpose_bf16.restype = c_i32
     L.lpg_split3_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_i64, c_p]
     L.lpg_split3_f32.restype = c_i32
     L.lpg_fc_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64,

@@ -331,7 +331,7 @@ def input_grad_bf16(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor
     with the weights transposed; fp32 accumulation, one bf16 rounding).
     ``mask`` = (Y, scale): the previous layer's ReLU/dropout backward folded into the store
     (fc_forward_bf16)."""
-    t = lambda W: None if W is None else W.detach().t().to(torch.bfloat16).contiguous()
+    t = lambda W: None if W is None else transpose_bf16(W.detach().to(torch.bfloat16))
     G1 = G1.to(torch.bfloat16)
     G2 = None if G2 is None else G2.to(torch.bfloat16)
     return fc_forward_bf16(G1, t(W1), G2, t(W2), None, False, out=out, accumulate=accumulate, key="igrad-bf16",
@@ -394,6 +394,18 @@ def relu_bwd_colsum_bf16(g: Tensor, y: Tensor, scale: float, want_db: bool):
                                         None if ws is None else ws.data_ptr(), _lib.stream_of(g))
     _lib.check(st, "lpg_relu_bwd_colsum_bf16")
     return out, db
+
+
+def transpose_bf16(W: Tensor) -> Tensor:
+    """W^T as a contiguous bf16 tensor (lpg_transpose_bf16; shapes it does not take: torch)."""
+    R, C = W.shape
+    if W.dtype != torch.bfloat16 or R % 8 or C % 8 or W.stride(1) != 1 or W.stride(0) % 8 or W.data_ptr() % 16:
+        return W.t().to(torch.bfloat16).contiguous()
+    out = torch.empty((C, R), dtype=torch.bfloat16, device=W.device)
+    with torch.cuda.device(W.device):
+        st = _lib.lib().lpg_transpose_bf16(R, C, W.data_ptr(), W.stride(0), out.data_ptr(), R, _lib.stream_of(W))
+    _lib.check(st, "lpg_transpose_bf16")
+    return out
 
 
 def colsum_bf16(g: Tensor) -> Tensor:

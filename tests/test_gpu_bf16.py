@@ -391,3 +391,13 @@ def test_gcn_fc_bf16_folded_relu_bwd_identical(monkeypatch):
     assert out[True][0] == out[False][0]
     for k, v in out[True][1].items():
         assert torch.equal(v, out[False][1][k]), k
+
+
+@pytest.mark.parametrize("R,C", [(8, 8), (2048, 2048), (72, 136), (1000, 8), (2048, 24)])
+def test_transpose_bf16(R, C):
+    from lpgnn.fc import transpose_bf16
+
+    W = torch.randn(R, C, device=DEV).to(BF)
+    assert torch.equal(transpose_bf16(W), W.t().contiguous())
+    big = torch.randn(R, C + 16, device=DEV).to(BF)[:, 8:8 + C]  # strided source rows
+    assert torch.equal(transpose_bf16(big), big.t().contiguous())

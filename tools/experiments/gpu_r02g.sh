@@ -1,0 +1,17 @@
+#!/bin/bash
+# c2 bench first (cold), bf16 transpose tests, c5 bench with the bf16 transpose kernel, c5 profile
+set -u
+mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 300 python bench.py > gpurun_out/bench_c2a.log 2>&1 || exit $?
+grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_c2a.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_bf16.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_bf16.log 2>&1 || { tail -30 gpurun_out/pytest_bf16.log; exit 1; }
+tail -2 gpurun_out/pytest_bf16.log
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --config c5 --steps 10 --warmup 3 > gpurun_out/bench_c5_t$i.log 2>&1 || exit $?
+  grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_c5_t$i.log
+done
+timeout -k 10 300 python bench.py > gpurun_out/bench_c2b.log 2>&1 || exit $?
+grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_c2b.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 -o run -- python bench.py --config c5 --steps 3 --warmup 2 --profile-only > gpurun_out/prof_c5.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --profile-only > gpurun_out/prof_c2.log 2>&1 || exit $?
+echo done
