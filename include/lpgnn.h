@@ -378,6 +378,14 @@ lpg_status lpg_fc_set_variant(int32_t variant);
  * NULL (unit weights).  Deterministic fixed-order reduction through
  * `workspace` (lpg_weighted_ce_workspace_bytes(M)).  An out-of-range label
  * makes the loss NaN. */
+/* Class counts of the balanced loss's weights (utils.py:286-299
+ * labels_to_balanced_weights, which counts by torch.unique): counts[c] =
+ * #{i : y[i] == c} for c = 0, 1, 2 (int64; other values are not counted),
+ * exact, no atomics, no host sync.  Workspace:
+ * lpg_class_counts_workspace_bytes(M). */
+int64_t lpg_class_counts_workspace_bytes(int64_t M);
+lpg_status lpg_class_counts3(int64_t M, const int64_t *y, int64_t *counts, void *workspace, void *stream);
+
 int64_t lpg_weighted_ce_workspace_bytes(int64_t M);
 lpg_status lpg_weighted_ce_fwd_f32(int64_t M, int64_t C, const float *x, int64_t ldx, const int64_t *y,
                                    const float *w, float coef, float *loss, float *wsum, void *workspace,

@@ -170,3 +170,61 @@ extern "C" lpg_status lpg_weighted_ce_bwd_f32(int64_t M, int64_t C, const float 
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
+
+namespace lpg {
+namespace {
+constexpr int kCntBlocks = 256;
+
+// Per-class label counts (3 classes): one partial triple per block, summed by one block in
+// block order -- integers, so the result is exact; no atomics.
+__global__ __launch_bounds__(256) void class_counts_p1(int64_t M, const int64_t *__restrict__ y,
+                                                       int64_t *__restrict__ part) {
+  __shared__ int64_t red[3][256];
+  int64_t c0 = 0, c1 = 0, c2 = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < M; i += (int64_t)gridDim.x * 256) {
+    const int64_t v = y[i];
+    c0 += v == 0;
+    c1 += v == 1;
+    c2 += v == 2;
+  }
+  red[0][threadIdx.x] = c0;
+  red[1][threadIdx.x] = c1;
+  red[2][threadIdx.x] = c2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int c = 0; c < 3; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) part[blockIdx.x * 3 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(64) void class_counts_p2(int nblk, const int64_t *__restrict__ part,
+                                                      int64_t *__restrict__ counts) {
+  if (threadIdx.x < 3) {
+    int64_t s = 0;
+    for (int b = 0; b < nblk; ++b) s += part[b * 3 + threadIdx.x];
+    counts[threadIdx.x] = s;
+  }
+}
+}  // namespace
+}  // namespace lpg
+
+extern "C" int64_t lpg_class_counts_workspace_bytes(int64_t M) {
+  (void)M;
+  return (int64_t)kCntBlocks * 3 * (int64_t)sizeof(int64_t);
+}
+
+extern "C" lpg_status lpg_class_counts3(int64_t M, const int64_t *y, int64_t *counts, void *workspace, void *stream) {
+  LPG_REQUIRE(M >= 0, "lpg_class_counts3: negative size");
+  LPG_REQUIRE(counts && workspace && (M == 0 || y), "lpg_class_counts3: NULL pointer");
+  hipStream_t s = as_stream(stream);
+  const int64_t want = (M + 256 * 8 - 1) / (256 * 8);
+  const int nblk = (int)(want < 1 ? 1 : (want > kCntBlocks ? kCntBlocks : want));
+  int64_t *part = static_cast<int64_t *>(workspace);
+  hipLaunchKernelGGL(class_counts_p1, dim3(nblk), dim3(256), 0, s, M, y, part);
+  LPG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(class_counts_p2, dim3(1), dim3(64), 0, s, nblk, part, counts);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}

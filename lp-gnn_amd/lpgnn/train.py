@@ -13,12 +13,27 @@ def labels_to_balanced_weights(labels, merge_lu=True):
     exactly two classes are present, w0 = w2 = mean(w0, w2).
 
     Restated without torch.unique / len(lbl) (which force a device->host
-    sync every step): class counts by a compare-and-sum
-    (a scatter-add onto three bins serialises its atomics: 41 us per call at
-    200 K labels), the same N / count_c division, branch choices as tensor
-    selects -- bitwise the reference's result (tests/test_gpu_model.py)."""
+    sync every step): class counts on the device
+    (lpg_class_counts3; a scatter-add onto three bins serialises its atomics:
+    41 us per call at 200 K labels), the same N / count_c division, branch
+    choices as tensor selects -- bitwise the reference's result
+    (tests/test_gpu_model.py)."""
     labels = labels.view(-1)
-    cnt = (labels.unsqueeze(1) == torch.arange(3, device=labels.device)).sum(0)
+    if labels.device.type == "cuda" and labels.dtype == torch.int64:
+        from . import _lib
+
+        labels = labels.contiguous()
+        L = _lib.lib()
+        cnt = torch.empty(3, dtype=torch.int64, device=labels.device)
+        ws = torch.empty(L.lpg_class_counts_workspace_bytes(labels.numel()) // 8, dtype=torch.int64,
+                         device=labels.device)
+        with torch.cuda.device(labels.device):
+            st = L.lpg_class_counts3(labels.numel(), labels.data_ptr(), cnt.data_ptr(), ws.data_ptr(),
+                                     _lib.stream_of(labels))
+        _lib.check(st, "lpg_class_counts3")
+    else:  # host-side callers (data preparation, CPU tests of the formula)
+        cnt = torch.zeros(3, dtype=torch.int64, device=labels.device)
+        cnt.scatter_add_(0, labels, torch.ones_like(labels))
     present = cnt > 0
     wei = cnt.sum() / cnt
     res = torch.where(present, wei, torch.zeros((), dtype=wei.dtype, device=labels.device))

@@ -181,7 +181,8 @@ def test_training_step_runs_and_matches_oracle_grads(arith, hids, monkeypatch):
 
 
 @pytest.mark.parametrize("labels", [[0, 1, 2, 1, 1, 0], [1, 1, 2, 2, 2], [0, 0, 0], [1, 1], [2, 1, 2],
-                                    [0, 2, 0, 2, 0], list(np.random.default_rng(0).integers(0, 3, 50000))])
+                                    [0, 2, 0, 2, 0], list(np.random.default_rng(0).integers(0, 3, 50000)),
+                                    list(np.random.default_rng(1).integers(0, 3, 600_000))])
 @pytest.mark.parametrize("merge", [True, False])
 def test_balanced_weights_sync_free_equal_reference(labels, merge):
     """The sync-free class weights == the reference formula (oracle
