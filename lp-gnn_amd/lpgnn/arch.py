@@ -217,8 +217,9 @@ class GCN_FC(GCNBase):
         if out is not None:
             left, right = out
         else:
-            left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias)
-            right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias)
+            # both heads fold the last layer's ReLU/dropout backward (bf16) or neither does
+            left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias, fold_in=True)
+            right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias, fold_in=True)
         return add_knowledge(left.float(), right.float(), x_left, x_right)
 
 

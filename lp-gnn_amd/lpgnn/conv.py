@@ -322,6 +322,16 @@ def two_direction_heads(left: Tensor, right: Tensor, adj: BipartiteCSR, left2rig
                                     lin_left.bias, lin_right.weight, lin_right.bias)
 
 
+def foldable_producer(x: Tensor):
+    """The backward node of the bf16 ReLU layer (_TwoDirection) that produced x, whose ReLU/dropout
+    backward a consumer may fold into its input-gradient stores, or None."""
+    g = x.grad_fn
+    if FOLD_RELU_BWD and g is not None and isinstance(g, _TwoDirection._backward_cls) and \
+            getattr(g, "relu", False) and getattr(g, "bf16", False):
+        return g
+    return None
+
+
 def two_direction(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, relu: bool = False,
                   dropout: float = 0.0, fold_in: bool = False):
     """GraphConvTwoDirection.forward (arch.py:65-81) through one autograd node.  ``fold_in``: the
@@ -329,11 +339,9 @@ def two_direction(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, ri
     are a bf16 ReLU layer's outputs, that layer's ReLU/dropout backward is folded into this one's
     input-gradient stores."""
     prev = None
-    if fold_in and FOLD_RELU_BWD and left.dtype == torch.bfloat16 and torch.is_grad_enabled():
-        g = left.grad_fn
-        if g is not None and g is right.grad_fn and isinstance(g, _TwoDirection._backward_cls) and \
-                getattr(g, "relu", False) and getattr(g, "bf16", False):
-            prev = g
+    if fold_in and left.dtype == torch.bfloat16 and torch.is_grad_enabled():
+        prev = foldable_producer(left)
+        prev = prev if prev is not None and prev is right.grad_fn else None
     return _TwoDirection.apply(left, right, adj, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                left2right.lin_root.weight, right2left.lin_rel.weight, right2left.lin_rel.bias,
                                right2left.lin_root.weight, bool(relu), float(dropout), prev)

@@ -573,9 +573,13 @@ class _Linear(torch.autograd.Function):
     """torch.nn.Linear on lpg_fc_f32; few-output backward on the HIP kernel."""
 
     @staticmethod
-    def forward(ctx, x, W, b):
+    def forward(ctx, x, W, b, prev=None):
         ctx.has_b = b is not None
         ctx.bf16 = x.dtype == torch.bfloat16
+        ctx.in_scale = None
+        if prev is not None:  # x = a bf16 ReLU layer's output feeding only this Linear: fold its backward
+            ctx.in_scale = prev.scale
+            prev.out_folded = True
         if ctx.bf16:
             W = W.to(torch.bfloat16)
             ctx.save_for_backward(x, W)
@@ -589,22 +593,30 @@ class _Linear(torch.autograd.Function):
         need = ctx.needs_input_grad
         if ctx.bf16:
             g = g.to(torch.bfloat16)
-            dx = input_grad_bf16(g, W) if need[0] else None
+            mask = None if ctx.in_scale is None else (x, ctx.in_scale)
+            dx = input_grad_bf16(g, W, mask=mask) if need[0] else None
             dW = wgrad_bf16(g, x) if need[1] else None
             db = g.float().sum(0) if ctx.has_b and need[2] else None
-            return dx, dW, db
+            return dx, dW, db, None
         if W.shape[0] <= 4 and x.shape[1] % 4 == 0:
             dx, dW, db = linear_small_bwd(g, W, x, need[0])
-            return dx, dW if need[1] else None, db if (ctx.has_b and need[2]) else None
+            return dx, dW if need[1] else None, db if (ctx.has_b and need[2]) else None, None
         dx = g @ W if need[0] else None
         dW = g.t() @ x if need[1] else None
         db = g.sum(0) if ctx.has_b and need[2] else None
-        return dx, dW, db
+        return dx, dW, db, None
 
 
-def linear(x: Tensor, weight: Tensor, bias) -> Tensor:
-    """torch.nn.Linear.forward on lpg_fc_f32 (heads, arch.py:190)."""
-    return _Linear.apply(x, weight, bias)
+def linear(x: Tensor, weight: Tensor, bias, fold_in: bool = False) -> Tensor:
+    """torch.nn.Linear.forward on lpg_fc_f32 (heads, arch.py:190).  ``fold_in`` (GCN_FC's heads,
+    bf16): the caller guarantees both outputs of the producing layer feed only its heads, so that
+    layer's ReLU/dropout backward is folded into the heads' input-gradient stores."""
+    prev = None
+    if fold_in and x.dtype == torch.bfloat16 and torch.is_grad_enabled():
+        from . import conv as _conv
+
+        prev = _conv.foldable_producer(x)
+    return _Linear.apply(x, weight, bias, prev)
 
 
 class _Knowledge(torch.autograd.Function):

@@ -110,7 +110,7 @@ def _worker(rank, world, port, out_dir, mode="global"):
 
         part._local_spmm = _cpu_local_spmm
         fc.graph_conv_fc = _cpu_graph_conv_fc
-        fc.linear = lambda x, w, b: F.linear(x, w, b)
+        fc.linear = lambda x, w, b, fold_in=False: F.linear(x, w, b)
         fc.knowledge = _cpu_knowledge
 
         if mode == "c4":  # each rank generates and plans only its own blocks
