@@ -199,13 +199,18 @@ __global__ __launch_bounds__(256) void class_counts_p1(int64_t M, const int64_t 
   if (threadIdx.x < 3) part[blockIdx.x * 3 + threadIdx.x] = red[threadIdx.x][0];
 }
 
-__global__ __launch_bounds__(64) void class_counts_p2(int nblk, const int64_t *__restrict__ part,
-                                                      int64_t *__restrict__ counts) {
-  if (threadIdx.x < 3) {
-    int64_t s = 0;
-    for (int b = 0; b < nblk; ++b) s += part[b * 3 + threadIdx.x];
-    counts[threadIdx.x] = s;
+__global__ __launch_bounds__(256) void class_counts_p2(int nblk, const int64_t *__restrict__ part,
+                                                       int64_t *__restrict__ counts) {
+  __shared__ int64_t red[3][256];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) red[c][threadIdx.x] = (int)threadIdx.x < nblk ? part[threadIdx.x * 3 + c] : 0;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int c = 0; c < 3; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + w];
+    __syncthreads();
   }
+  if (threadIdx.x < 3) counts[threadIdx.x] = red[threadIdx.x][0];
 }
 }  // namespace
 }  // namespace lpg
@@ -224,7 +229,7 @@ extern "C" lpg_status lpg_class_counts3(int64_t M, const int64_t *y, int64_t *co
   int64_t *part = static_cast<int64_t *>(workspace);
   hipLaunchKernelGGL(class_counts_p1, dim3(nblk), dim3(256), 0, s, M, y, part);
   LPG_HIP(hipGetLastError());
-  hipLaunchKernelGGL(class_counts_p2, dim3(1), dim3(64), 0, s, nblk, part, counts);
+  hipLaunchKernelGGL(class_counts_p2, dim3(1), dim3(256), 0, s, nblk, part, counts);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
