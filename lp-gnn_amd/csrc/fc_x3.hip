@@ -1813,8 +1813,9 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   float *part = reinterpret_cast<float *>(workspace);
   float *zrow = part + S * N * K;  // 128 zero floats after the partials (lpg_wgrad_x3_workspace_bytes)
   hipStream_t st = as_stream(stream);
-  LPG_HIP(hipMemsetAsync(zrow, 0, 512, st));
-  if (g_wgrad_m16 >= 4 && (cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31)) {
+  const bool wide = g_wgrad_m16 >= 4 && (cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31);
+  if (!wide) LPG_HIP(hipMemsetAsync(zrow, 0, 512, st));  // the zero row only the older kernels read
+  if (wide) {
     const int64_t ntw = (N + 255) / 256, ktw = (K + 127) / 128;  // 256 x 128 tiles, wgrad_x3c's split count
     const int64_t nbw = S_used * ntw * ktw;
     LPG_REQUIRE(nbw < (int64_t)1 << 31, "lpg_wgrad_x3_f32: grid too large");
