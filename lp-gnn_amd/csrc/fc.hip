@@ -37,6 +37,8 @@
 #include "common.h"
 #include "fc_common.h"
 
+#include <type_traits>
+
 #pragma clang fp contract(off)
 
 namespace lpg {
@@ -368,35 +370,63 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
 #pragma unroll
     for (int k = 0; k < K2; ++k) wp2[jp][k] = f32x2{w2[2 * jp][k], w2[2 * jp + 1][k]};
   }
-  for (int64_t m = r0; m < r1; ++m) {
-    const float *xr = sx + (m - r0) * KT;
-    float o[4];
-    // columns in pairs: one v_pk_fma_f32 advances two independent chains
-    // (a true fma per element -- the same bits as the scalar chains)
+  // the row loop with the addend / bias / dropout choices made once per launch (uniform branches
+  // per element cost more than the arithmetic of this write-bound kernel); the dropout column keys
+  // once per thread, the row key once per row -- the same mask bits as drop_hash(seed, row, col)
+  auto rows = [&](auto acc_c, auto bias_c, auto drop_c) {
+    constexpr bool ACC = decltype(acc_c)::value, BIAS = decltype(bias_c)::value, DROP = decltype(drop_c)::value;
+    uint32_t ck[4];
+    if constexpr (DROP) {
 #pragma unroll
-    for (int j = 0; j < 4; j += 2) {
-      // each part (<= 16 k) is one numerics block: its own chain from +0, then added to the total
-      f32x2 p1 = {0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < (K1 + 7) / 8 * 8; ++i) {
-        const int k = pik(i);
-        if (k < K1) p1 = __builtin_elementwise_fma(f32x2{xr[k], xr[k]}, wp1[j / 2][k], p1);
-      }
-      f32x2 t = f32x2{0.f, 0.f} + p1;
-      if (K2 > 0) {
-        f32x2 p2 = {0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < (K2 + 7) / 8 * 8; ++i) {
-          const int k = pik(i);
-          if (k < K2) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[j / 2][k], p2);
-        }
-        t = t + p2;
-      }
-      if (a.accum) t = t + f32x2{a.C[m * a.ldc + c + j], a.C[m * a.ldc + c + j + 1]};
-      o[j] = epilogue(a, t[0], b[j], m, c + j, RELU);
-      o[j + 1] = epilogue(a, t[1], b[j + 1], m, c + j + 1, RELU);
+      for (int j = 0; j < 4; ++j) ck[j] = drop_col_key(c + j);
     }
-    *reinterpret_cast<float4 *>(a.C + m * a.ldc + c) = make_float4(o[0], o[1], o[2], o[3]);
+    for (int64_t m = r0; m < r1; ++m) {
+      const float *xr = sx + (m - r0) * KT;
+      const uint32_t rk = DROP ? drop_row_key(a.seed, m) : 0u;
+      float o[4];
+      // columns in pairs: one v_pk_fma_f32 advances two independent chains
+      // (a true fma per element -- the same bits as the scalar chains)
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        // each part (<= 16 k) is one numerics block: its own chain from +0, then added to the total
+        f32x2 p1 = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < (K1 + 7) / 8 * 8; ++i) {
+          const int k = pik(i);
+          if (k < K1) p1 = __builtin_elementwise_fma(f32x2{xr[k], xr[k]}, wp1[j / 2][k], p1);
+        }
+        f32x2 t = f32x2{0.f, 0.f} + p1;
+        if (K2 > 0) {
+          f32x2 p2 = {0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < (K2 + 7) / 8 * 8; ++i) {
+            const int k = pik(i);
+            if (k < K2) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[j / 2][k], p2);
+          }
+          t = t + p2;
+        }
+        if constexpr (ACC) t = t + f32x2{a.C[m * a.ldc + c + j], a.C[m * a.ldc + c + j + 1]};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          float v = t[e];
+          if constexpr (BIAS) v = v + b[j + e];
+          if (RELU) v = (v < 0.f) ? 0.f : v;
+          if constexpr (DROP) v = drop_hash_k(rk, ck[j + e]) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+          o[j + e] = v;
+        }
+      }
+      *reinterpret_cast<float4 *>(a.C + m * a.ldc + c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  const bool acc = a.accum, bias = a.bias != nullptr, drop = a.drop_thresh != 0;
+  if (acc) {
+    if (bias) { if (drop) rows(T_{}, T_{}, T_{}); else rows(T_{}, T_{}, F_{}); }
+    else { if (drop) rows(T_{}, F_{}, T_{}); else rows(T_{}, F_{}, F_{}); }
+  } else {
+    if (bias) { if (drop) rows(F_{}, T_{}, T_{}); else rows(F_{}, T_{}, F_{}); }
+    else { if (drop) rows(F_{}, F_{}, T_{}); else rows(F_{}, F_{}, F_{}); }
   }
 }
 

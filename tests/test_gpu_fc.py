@@ -98,21 +98,26 @@ def test_fc_accumulate_bitwise(M, N, K, relu, bias, variant):
     assert np.array_equal(got, want.numpy())
 
 
-@pytest.mark.parametrize("p", [0.0, 0.25])
-def test_fc_smallk_equals_tiled_path(p):
+@pytest.mark.parametrize("p,bias,acc", [(0.0, True, False), (0.25, True, False), (0.0, False, False),
+                                        (0.25, False, True), (0.0, True, True)])
+def test_fc_smallk_equals_tiled_path(p, bias, acc):
     """The narrow-input kernel (K1 + K2 <= 16) and the MFMA tile kernel give
     the same bits, dropout mask included: zero-padding K1 to 20 moves the
-    same chain onto the tiled path (fma(0, 0, p) = p)."""
+    same chain onto the tiled path (fma(0, 0, p) = p).  Every epilogue form
+    (bias or not, dropout or not, accumulate or not)."""
     from lpgnn.fc import fc_forward
 
     torch.manual_seed(5)
     M, N = 2050, 1024
     A1, A2 = torch.randn(M, 8, device=DEV), torch.randn(M, 8, device=DEV)
     W1, W2 = torch.randn(N, 8, device=DEV) * 0.3, torch.randn(N, 8, device=DEV) * 0.3
-    b = torch.randn(N, device=DEV) * 0.1
+    b = torch.randn(N, device=DEV) * 0.1 if bias else None
+    P = torch.randn(M, N, device=DEV)
     pad = lambda x: torch.cat([x, torch.zeros(x.shape[0], 12, device=DEV)], 1).contiguous()
-    small = fc_forward(A1, W1, A2, W2, b, True, p, seed=77)
-    tiled = fc_forward(pad(A1), pad(W1), A2, W2, b, True, p, seed=77)
+    kw = dict(out=P.clone(), accumulate=True) if acc else {}
+    small = fc_forward(A1, W1, A2, W2, b, True, p, seed=77, **kw)
+    kw = dict(out=P.clone(), accumulate=True) if acc else {}
+    tiled = fc_forward(pad(A1), pad(W1), A2, W2, b, True, p, seed=77, arith="fp32", **kw)
     assert torch.equal(small, tiled)
 
 
