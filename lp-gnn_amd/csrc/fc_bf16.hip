@@ -337,6 +337,17 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
   for (int j = 0; j < FN; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) bb[j][r] = (a.bias && c0 + j * 16 + r < a.N) ? a.bias[c0 + j * 16 + r] : 0.f;
+  // the folded ReLU backward's mask rows, issued as the accumulators drain into the image (after
+  // fragment row i, the VGPRs of acc[i] take the next loads): their latency runs under the image writes
+  constexpr int SIT = FM * 16 * CPR / 64, SPI = (SIT + FM - 1) / FM;
+  uint4 yv[SIT];
+  auto load_y = [&](int it) {
+    const int q = it * 64 + lane;
+    const int lr = q / CPR, ch = q % CPR;
+    const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
+    yv[it] = (row < a.M && col < a.N) ? *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col)
+                                      : make_uint4(0u, 0u, 0u, 0u);
+  };
   auto body = [&](auto acc_c, auto drop_c) {
     constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
     uint32_t ck[FN][4];
@@ -370,6 +381,11 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
         const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2));
         *reinterpret_cast<uint2 *>(ip + j * 32) = uint2{lo, hi};
       }
+      if (a.my) {
+#pragma unroll
+        for (int u = 0; u < SPI; ++u)
+          if (i * SPI + u < SIT) load_y(i * SPI + u);
+      }
     }
   };
   using T_ = std::true_type;
@@ -380,21 +396,32 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
   } else {
     if (drop) body(F_{}, T_{}); else body(F_{}, F_{});
   }
-  constexpr int SIT = FM * 16 * CPR / 64;
-  uint4 yv[SIT];
-  if (a.my) load_mask_rows<SIT, CPR>(a, lane, wrow0, wcol0, yv);  // all in flight before the first use
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (a.my) {  // masked: every chunk formed first (one wait for the mask rows), then the stores back to back
+    uint4 v[SIT];
+#pragma unroll
+    for (int it = 0; it < SIT; ++it) {
+      const int q = it * 64 + lane;
+      const int lr = q / CPR, ch = q % CPR;
+      v[it] = relu_bwd8(*reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16), yv[it], a.mscale);
+    }
+#pragma unroll
+    for (int it = 0; it < SIT; ++it) {
+      const int q = it * 64 + lane;
+      const int lr = q / CPR, ch = q % CPR;
+      const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
+      if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v[it];
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < SIT; ++it) {
     const int q = it * 64 + lane;
     const int lr = q / CPR, ch = q % CPR;
     const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
-    uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
-    if (row < a.M && col < a.N) {
-      if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
-      *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
-    }
+    const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
+    if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
   }
 }
 
