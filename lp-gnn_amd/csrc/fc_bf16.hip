@@ -68,17 +68,20 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 
 // The folded ReLU/dropout backward on 8 stored bf16 values: (y > 0) ? RNE(g * scale) : 0 per
 // element -- the arithmetic of lpg_relu_bwd_colsum_bf16 on the same bf16 g, so the same bits.
-// Pairs on the packed datapath: one v_pk_mul_f32 and one v_cvt_pk_bf16_f32 (round to nearest even,
-// the software RNE's bits for every non-NaN value) per two elements.
 __device__ __forceinline__ uint4 relu_bwd8(uint4 g, uint4 y, float scale) {
   const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, yw[4] = {y.x, y.y, y.z, y.w};
   uint32_t o[4];
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
-    const f32x2 gf = {__uint_as_float(gw[h] << 16), __uint_as_float(gw[h] & 0xffff0000u)};
-    const float y0 = __uint_as_float(yw[h] << 16), y1 = __uint_as_float(yw[h] & 0xffff0000u);
-    const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(gf * f32x2{scale, scale}, bf16x2));
-    o[h] = (y0 > 0.f ? (pk & 0xffffu) : 0u) | (y1 > 0.f ? (pk & 0xffff0000u) : 0u);
+    uint32_t w = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float yf = __uint_as_float(((yw[h] >> (16 * e)) & 0xffffu) << 16);
+      const float gf = __uint_as_float(((gw[h] >> (16 * e)) & 0xffffu) << 16);
+      const uint32_t d = yf > 0.f ? (uint32_t)to_bf16_rne(gf * scale) : 0u;
+      w |= d << (16 * e);
+    }
+    o[h] = w;
   }
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
