@@ -95,6 +95,17 @@ lpg_status lpg_csr_pack_f32(const int64_t *row, const int64_t *col, const float 
  * the other orientation (torch_sparse SPMMSum::backward). */
 lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx,
                         float *Y, int64_t ldy, int64_t F, void *stream);
+/* lpg_spmm_f32[_heavy] with explicit per-call tuning (benchmarks / tests; no
+ * global state): heavy_rows / n_heavy / thresh as lpg_spmm_f32_heavy (NULL, 0,
+ * 0 = none); slice_cols = columns of F one wave task covers (0 = auto, or 64,
+ * 128, 256, 512, 1024; the slices run plane by plane, so a narrower slice
+ * keeps the gathered source slice resident in the 256 MiB Infinity Cache),
+ * depth = edges gathered ahead per wave (0 = auto, 8, 16, 32).  Every choice
+ * gives bitwise lpg_spmm_f32's result (the per-element summation order is
+ * always the row's CSR order). */
+lpg_status lpg_spmm_f32_tuned(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                              const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh, int64_t slice_cols,
+                              int32_t depth, void *stream);
 
 /* lpg_spmm_f32 with degree-aware scheduling for skewed rows: heavy_rows
  * (device int32 [n_heavy]) must list exactly the rows of A with more than
@@ -114,6 +125,11 @@ lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64_t ldx,
  * accumulated row is rounded to bf16 once (round-to-nearest-even). */
 lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,
                          uint16_t *Y, int64_t ldy, int64_t F, void *stream);
+/* ... with per-call tuning as lpg_spmm_f32_tuned (slice_cols 0 = auto = 256,
+ * 256, 512, 1024; depth for the 256-column form); bitwise lpg_spmm_bf16's. */
+lpg_status lpg_spmm_bf16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy, int64_t F,
+                               const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh, int64_t slice_cols,
+                               int32_t depth, void *stream);
 /* ... and its degree-aware form (heavy_rows as lpg_spmm_f32_heavy; the heavy
  * units are (row, 128-column) waves); bitwise lpg_spmm_bf16's result. */
 lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx,
@@ -122,6 +138,18 @@ lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx,
                                void *stream);
 
 /* ---- dense FC (replaces GraphConv's lin_rel + lin_root + ReLU) ----------- */
+
+/* FC flags (lpg_fc_f32, lpg_fc_x3_f32, lpg_fc_x3_heads_f32, lpg_fc_bf16,
+ * lpg_fc_bf16_relu_bwd): bit 0 = ReLU (+ fused dropout), bit 1 = accumulate,
+ * bits 8-11 = kernel choice, 0 = by shape.  Every kernel choice of one entry
+ * computes the same bits (the tests compare them); the choice exists so that
+ * benchmarks and tests can pick a kernel per call, without global state.
+ *   lpg_fc_x3_f32 / _heads: 1 = fc_fwd_x3_16 (global_load_lds staging);
+ *   lpg_fc_bf16 / _relu_bwd: 1 = 128 x 128 tiles, 2 = 256 x 256 tiles,
+ *     3 = the pipelined 256 x 256 kernel (the default from 4096 rows). */
+#define LPG_FC_RELU 1
+#define LPG_FC_ACCUMULATE 2
+#define LPG_FC_KERNEL(k) ((int32_t)(k) << 8)
 
 /* C[m, n] = act( sum_{k<K1} A1[m,k] W1[n,k] + sum_{k<K2} A2[m,k] W2[n,k] + bias[n] )
  *
@@ -213,29 +241,6 @@ int64_t lpg_wgrad_x3_workspace_bytes(int64_t R, int64_t N, int64_t K);
 lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
                             int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream);
 
-/* Tile choice for lpg_fc_x3_f32 (tuning).  On 16x16x32 MFMAs: 0 = default =
- * 14, 5 / 6 / 7 = 128 x 128 / 256 x 128 / 128 x 64 tiles of 64 x 64 (or
- * 64 x 32) wave tiles, 9 / 10 = 256 x 128 / 128 x 128 tiles of 32 x 128 wave
- * tiles (each A row split by one wave only), 11 = 10 with XCD pairs sharing
- * n-tile pairs when N spans 8 tiles (N = 1024); the fc_x3_wide kernels
- * (buffer_load ... lds staging with the k step in the scalar offset, wave
- * strips along N): 12 = 128 x 256 of 16 x 256 strips, 13 = 128 x 128 of
- * 16 x 128 (2 blocks/CU), 14 = 128 x 128 of 32 x 128 (the default), 15 =
- * 256 x 128 of 32 x 128, 16 = 256 x 128 of 16 x 128 (16 waves) -- they need
- * lda1 == lda2, ldw1 == ldw2, ps1 == ps2 and fall back to 10 otherwise; on
- * 32x32x16 MFMAs: 1 = 256 x 128, 2 = 128 x 256, 3 / 4 = 128 x 128 / 256 x 128
- * software-pipelined, 8 = 128 x 128.  Variants on the same MFMA shape give
- * identical bits (the two shapes differ in in-instruction summation).
- * 100 .. 105: the weight-gradient kernel (100 / 101 = 32x32x16 / 16x16x32
- * with per-wave splits, 102 = cooperative 16x16x32 with one split per element
- * and block, 103 = producer-consumer form of 102, 104 / 105 = 256 x 128 tiles
- * with two plane buffers, the next chunk split under the current chunk's
- * MFMAs, 105 (the default) interleaving the split column by column; 101 .. 105
- * give identical bits).
- * 99: a timing probe without the activation split
- * (WRONG results, measurement only). */
-lpg_status lpg_fc_x3_set_variant(int32_t v);
-
 /* Backward of ReLU (+ fused dropout): out[i] = y[i] > 0 ? g[i] * scale : 0,
  * y = the stored lpg_fc_f32 output, scale = 1/(1-p) (1 without dropout).
  * n a multiple of 4, buffers 16-byte aligned; out may alias g. */
@@ -294,19 +299,6 @@ lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int
                        int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
                        const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
                        void *stream);
-/* Tile choice for lpg_fc_bf16 (tuning/benchmarks): 0 = default (128 x 128 below
- * 4096 rows, else 10), 1 = 128 x 128, 2 = 256 x 256 with BK 64 and 2 buffers,
- * 3 = 256 x 256 with BK 32 and 3 buffers, 4 / 5 = 256 x 256 with
- * buffer_load ... lds staging and the barrier mid-tile, 4 / 8 waves, 6 = 5
- * with the fragment reads and DMA placed between the MFMAs, 7 = 6 with
- * s_setprio 1 on waves 4-7, 8 = 4 placed, 9 = 7 with the MFMA issued as
- * W x A^T (four consecutive output columns per lane) and a register epilogue,
- * 10 = 9 through the LDS image (4-9 need lda1 == lda2 and ldw1 == ldw2,
- * else 2).  All give identical bits.  100-104 select the
- * lpg_wgrad_bf16 kernel (100 / 101 = 4 / 8 waves, 102 = 101 placed (the
- * default), 103 = 102 + s_setprio, 104 = 100 placed; identical bits). */
-lpg_status lpg_fc_bf16_set_variant(int32_t v);
-
 /* dst[c, r] = src[r, c] for bf16 [R, C] (R, C, lds, ldd multiples of 8, 16-byte
  * aligned): the transposed weights the c5 input gradients multiply by
  * (dX = dZ W of a Linear, arch.py:57-62 through train.py:128). */
@@ -320,7 +312,7 @@ lpg_status lpg_transpose_bf16(int64_t R, int64_t C, const uint16_t *src, int64_t
  *   C = (Y > 0) ? bf16(bf16(A1 W1^T + A2 W2^T [+ C]) * scale) : 0
  * bit for bit lpg_fc_bf16 (no bias, no ReLU) followed by
  * lpg_relu_bwd_colsum_bf16(C, Y, scale) -- without that pass's read of C and
- * write of dZ.  flags: only bit 1 (C holds a bf16 addend).  N, ldc, ldy
+ * write of dZ.  flags: bit 1 (C holds a bf16 addend) and the kernel choice.  N, ldc, ldy
  * multiples of 8, C and Y 16-byte aligned; other requirements as lpg_fc_bf16. */
 lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
                                 const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
@@ -363,13 +355,6 @@ lpg_status lpg_heads_relu_bwd_f32(int64_t M, int64_t K, int64_t N, const float *
                                   const float *Y, int64_t ldy, float scale, float *dZ, int64_t lddz, float *dW,
                                   float *db, float *dbY, void *workspace, void *stream);
 
-/* Tuning knob for lpg_fc_f32 (process-global, default 0): tiled-kernel
- * variant, 0 = 128x128 tile, 2-stage LDS-DMA ring (2 blocks/CU), 1 = the same
- * with a 3-stage ring (1 block/CU), 2 = 64-deep k-tiles (K1, K2 multiples of
- * 64, else variant 0), 3 = 128x256 (8 waves), 4 = 256x128 (8 waves).  Every
- * variant produces bitwise identical results (same chain order). */
-lpg_status lpg_fc_set_variant(int32_t variant);
-
 /* ---- balanced loss (train.py:39-46) ---------------------------------------- */
 
 /* nn.CrossEntropyLoss(weight=w)(x, y) * coef (mean reduction, ignore_index
@@ -402,22 +387,6 @@ lpg_status lpg_weighted_ce_bwd_f32(int64_t M, int64_t C, const float *x, int64_t
  * Bitwise torch-CPU F.normalize semantics (norm = sqrt(fma(x2,x2,fma(x1,x1,x0*x0)))). */
 lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t ldl, const float *feas, int64_t ldf,
                              int64_t feas_cols, float bound, float *out, int64_t ldo, void *stream);
-
-/* Tuning knob for lpg_spmm_f32 (process-global, default 0 = auto):
- * columns per slice of F processed by one wave (multiple of 256, or 0).
- * Smaller slices keep the gathered source slice resident in the 256 MiB
- * Infinity Cache; see DESIGN.md. */
-lpg_status lpg_spmm_set_slice(int64_t cols_per_slice);
-/* Tuning knob: edges gathered ahead per wave in the wide fp32 kernel (8, 16,
- * 32; 0 = auto).  Results are bitwise identical for every setting (the
- * accumulation order does not change). */
-lpg_status lpg_spmm_set_depth(int64_t edges);
-
-/* Tuning knob for lpg_spmm_f32 (results bitwise identical): 1 (default) = a
- * row chunk's last (n mod depth) edges are gathered together, predicated per
- * edge; 0 = one dependent gather at a time (the round-1 form, kept for A/B
- * runs).  The bf16 kernel always gathers its remainder one by one. */
-lpg_status lpg_spmm_set_remainder(int32_t batched);
 
 /* ---- k-hop neighbour sampling (NeighborLoader collate, train.py:111-116,
  * val.py:22-27; replaces torch_sparse 0.6.12 neighbor_sample) -------------

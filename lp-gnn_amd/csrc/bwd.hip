@@ -14,6 +14,7 @@
 // kFold segment sums (many blocks, coalesced), then a short final pass --
 // so results are deterministic run to run, with no atomics.
 #include "common.h"
+#include "fc_common.h"
 
 #pragma clang fp contract(off)
 
@@ -93,12 +94,6 @@ __global__ __launch_bounds__(kT) void relu_bwd_colsum_p1(int64_t M, int64_t N, c
 // torch's bf16 `g * scale` gives; db sums the rounded dZ in fp32.
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
 
-__device__ __forceinline__ uint32_t f32_to_bf16_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
-}
 
 // MASK = false (lpg_colsum_bf16): g already is dZ (the folded form, lpg_fc_bf16_relu_bwd) --
 // only the column sums, same blocks and order, so the same db bits; y and out unused.
@@ -116,17 +111,9 @@ __global__ __launch_bounds__(kT) void relu_bwd_colsum_bf16_p1(int64_t M, int64_t
       uint32_t ow[4];
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
-        uint32_t o = 0;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          uint32_t d = (gw[h] >> (16 * e)) & 0xffffu;
-          if constexpr (MASK) {
-            const float yf = bf16_to_f32((yw[h] >> (16 * e)) & 0xffffu);
-            d = yf > 0.f ? f32_to_bf16_rne(bf16_to_f32(d) * scale) : 0u;
-          }
-          s[2 * h + e] = s[2 * h + e] + bf16_to_f32(d);
-          o |= d << (16 * e);
-        }
+        const uint32_t o = MASK ? relu_bwd_pk_bf16(gw[h], yw[h], scale) : gw[h];  // fc_common.h
+        s[2 * h] = s[2 * h] + bf16_to_f32(o & 0xffffu);
+        s[2 * h + 1] = s[2 * h + 1] + bf16_to_f32(o >> 16);
         ow[h] = o;
       }
       if constexpr (MASK) *reinterpret_cast<uint4 *>(out + m * ldo + c) = make_uint4(ow[0], ow[1], ow[2], ow[3]);

@@ -454,8 +454,6 @@ bool try_smallk(const FcArgs &a, bool relu, hipStream_t s, lpg_status *st) {
   return false;
 }
 
-int g_fc_variant = 0;  // lpg_fc_set_variant; 0 = default tile
-
 }  // namespace
 }  // namespace lpg
 
@@ -489,15 +487,9 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
   LPG_REQUIRE(K1 % 32 == 0 && K2 % 32 == 0,
               "lpg_fc_f32: K1, K2 must be multiples of 32 (zero-pad) unless 4 <= K1, K1 + K2 <= 16 and N %% 4 == 0");
   if (N <= 32) return launch_fc<4, 1, 1, 1, 32, 2>(a, relu, s);  // heads (N = 3): 128 x 32 tiles
-  switch (g_fc_variant) {
-    case 1: return launch_fc<2, 2, 2, 2, 32, 3>(a, relu, s);  // 3-stage ring, 96 KiB: 1 block / CU
-    case 2:
-      if (K1 % 64 == 0 && K2 % 64 == 0) return launch_fc<2, 2, 2, 2, 64, 2>(a, relu, s);  // BK 64, 128 KiB
-      return launch_fc<2, 2, 2, 2, 32, 2>(a, relu, s);
-    case 3: return launch_fc<2, 4, 2, 2, 32, 2>(a, relu, s);  // 128 x 256, 8 waves, 96 KiB
-    case 4: return launch_fc<4, 2, 2, 2, 32, 2>(a, relu, s);  // 256 x 128, 8 waves, 96 KiB
-    default: return launch_fc<2, 2, 2, 2, 32, 2>(a, relu, s);  // 128 x 128, 64 KiB: 2 blocks / CU
-  }
+  // 128 x 128, 64 KiB: 2 blocks / CU.  (A 3-stage ring, BK = 64, 128 x 256 and 256 x 128 tiles of
+  // the same kernel gave the same bits and ran 4-20 % slower; they are not shipped.)
+  return launch_fc<2, 2, 2, 2, 32, 2>(a, relu, s);
 }
 
 extern "C" lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const float *y, float scale, float *out,
@@ -514,12 +506,6 @@ extern "C" lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const 
                      reinterpret_cast<const float4 *>(g), reinterpret_cast<const float4 *>(y), scale,
                      reinterpret_cast<float4 *>(out));
   LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
-extern "C" lpg_status lpg_fc_set_variant(int32_t v) {
-  LPG_REQUIRE(v >= 0 && v <= 4, "lpg_fc_set_variant: variant %d not in [0, 4]", v);
-  g_fc_variant = v;
   return LPG_OK;
 }
 

@@ -66,24 +66,11 @@ __device__ __forceinline__ uint16_t to_bf16_rne(float f) {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-// The folded ReLU/dropout backward on 8 stored bf16 values: (y > 0) ? RNE(g * scale) : 0 per
-// element -- the arithmetic of lpg_relu_bwd_colsum_bf16 on the same bf16 g, so the same bits.
+// The folded ReLU/dropout backward on 8 stored bf16 values: relu_bwd_pk_bf16 (fc_common.h) per
+// pair -- the arithmetic and instructions of lpg_relu_bwd_colsum_bf16, so the same bits.
 __device__ __forceinline__ uint4 relu_bwd8(uint4 g, uint4 y, float scale) {
-  const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, yw[4] = {y.x, y.y, y.z, y.w};
-  uint32_t o[4];
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const float yf = __uint_as_float(((yw[h] >> (16 * e)) & 0xffffu) << 16);
-      const float gf = __uint_as_float(((gw[h] >> (16 * e)) & 0xffffu) << 16);
-      const uint32_t d = yf > 0.f ? (uint32_t)to_bf16_rne(gf * scale) : 0u;
-      w |= d << (16 * e);
-    }
-    o[h] = w;
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
+  return make_uint4(relu_bwd_pk_bf16(g.x, y.x, scale), relu_bwd_pk_bf16(g.y, y.y, scale),
+                    relu_bwd_pk_bf16(g.z, y.z, scale), relu_bwd_pk_bf16(g.w, y.w, scale));
 }
 
 // The mask rows (Y) of a wave's store loop, issued together after the accumulators are in the
@@ -523,145 +510,10 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
   epilogue_bf16<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
 }
 
-// Deeper pipeline, 256 x 256 tile (8 waves, 2 x 4, 8 x 4 fragments each):
-// BK = 32 (64-B rows), THREE LDS buffers of 32 KiB, the DMA of tile t+2 issued
-// while tile t feeds the MFMAs and tile t+1 still in flight across the
-// barrier.  A raw s_barrier with a counted vmcnt (this wave's 4 pieces of the
-// newest tile may stay outstanding) replaces __syncthreads(), whose fence
-// would wait for every DMA (vmcnt(0)).  LDS image per 64-B row: 4 16-B
-// chunks, chunk c stored at c ^ ((row >> 2) & 3) (16 consecutive rows of one
-// fragment read then cover all 16 bank groups).
-__device__ __forceinline__ int swz32(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
-
-template <bool RELU>
-__global__ __launch_bounds__(512) void fc_fwd_bf16_p3(FcB16Args a) {
-  constexpr int WM = 2, WN = 4, FM = 8, FN = 4, NW = 8, BKP = 32;
-  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;        // 256 x 256
-  constexpr int ROWB = BKP * 2;                               // 64-B rows
-  constexpr int TILE_BYTES = (BM + BN) * ROWB;                // 32 KiB
-  constexpr int PA = BM * ROWB / 1024 / NW, PB = BN * ROWB / 1024 / NW;  // 2 + 2 pieces per wave
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[3 * TILE_BYTES];
-
-  const int64_t nwg = a.mt * a.nt;
-  const int64_t bid = blockIdx.x;
-  const int64_t xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
-  const int64_t wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
-  const int64_t m0 = (wgid / a.nt) * BM;
-  const int64_t n0 = (wgid % a.nt) * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int nk1 = (int)(a.K1 / BKP);
-  const int nk = nk1 + (int)(a.K2 / BKP);
-
-  // piece = 16 rows x 64 B; lane i -> row 16*piece + i/4, physical chunk i%4
-  auto stage = [&](int b, int t) {
-    const bool p2 = t >= nk1;
-    const uint16_t *A = p2 ? a.A2 : a.A1;
-    const uint16_t *W = p2 ? a.W2 : a.W1;
-    const int64_t lda = p2 ? a.lda2 : a.lda1, ldw = p2 ? a.ldw2 : a.ldw1;
-    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BKP;
-    unsigned char *base = smem + b * TILE_BYTES;
-    typedef __attribute__((address_space(3))) unsigned char lds_t;
-#pragma unroll
-    for (int p = 0; p < PA; ++p) {
-      const int piece = wave + NW * p;
-      const int row = piece * 16 + (lane >> 2);
-      int64_t gr = m0 + row;
-      gr = gr < a.M ? gr : a.M - 1;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(A + gr * lda + k0 + swz32(row, lane & 3) * 8),
-                                       (lds_t *)(base + piece * 1024), 16, 0, 0);
-    }
-#pragma unroll
-    for (int p = 0; p < PB; ++p) {
-      const int piece = wave + NW * p;
-      const int row = piece * 16 + (lane >> 2);
-      int64_t gn = n0 + row;
-      gn = gn < a.N ? gn : a.N - 1;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(W + gn * ldw + k0 + swz32(row, lane & 3) * 8),
-                                       (lds_t *)(base + BM * ROWB + piece * 1024), 16, 0, 0);
-    }
-  };
-  auto barrier_keep_newest = [&]() {  // this wave's DMA of all but the newest tile has landed
-    asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  auto barrier_all = [&]() {
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  static_assert(PA + PB == 4, "vmcnt(4) above counts this wave's pieces of one tile");
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fq = lane >> 4;
-
-  if (nk > 0) stage(0, 0);
-  if (nk > 1) {
-    stage(1, 1);
-    barrier_keep_newest();
-  } else {
-    barrier_all();
-  }
-  int b = 0;
-  for (int t = 0; t < nk; ++t) {
-    const bool more = t + 2 < nk;
-    if (more) stage(b == 0 ? 2 : b - 1, t + 2);  // buffer (t + 2) % 3: read last in iteration t - 1
-    const unsigned char *As = smem + b * TILE_BYTES;
-    const unsigned char *Bs = As + BM * ROWB;
-    bf16x8 av[FM], bv[FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int row = wm * FM * 16 + i * 16 + fr;
-      av[i] = *reinterpret_cast<const bf16x8 *>(As + row * ROWB + swz32(row, fq) * 16);
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int row = wn * FN * 16 + j * 16 + fr;
-      bv[j] = *reinterpret_cast<const bf16x8 *>(Bs + row * ROWB + swz32(row, fq) * 16);
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
-    if (more)
-      barrier_keep_newest();  // tile t+1 landed, t+2 may still be in flight
-    else
-      barrier_all();
-    b = b == 2 ? 0 : b + 1;
-  }
-
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int64_t col = n0 + wn * FN * 16 + j * 16 + fr;
-    if (col >= a.N) continue;
-    const float bb = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * FM * 16 + i * 16 + fq * 4 + r;
-        if (row >= a.M) continue;
-        float v = acc[i][j][r];
-        if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
-        if (a.bias) v = v + bb;
-        if (RELU) v = v < 0.f ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-        a.C[row * a.ldc + col] = to_bf16_rne(v);
-      }
-    }
-  }
-}
-
-// ---- pipelined kernel with buffer_load ... lds staging (variants 4, 5) ------
+// ---- pipelined kernel with buffer_load ... lds staging (the default) -------
 //
-// fc_bf16_p: same tile image, fragment order and epilogue as fc_fwd_bf16, two
-// changes in the k loop.
+// fc_bf16_p: same tile image as fc_fwd_bf16 (8 waves of 128 x 64), three
+// changes in the k loop and one in the epilogue.
 // (1) Staging: every 1-KiB DMA piece is a buffer_load ... lds through one
 //     descriptor per operand and phase (wave-uniform SGPRs), the lane's offset
 //     (row + swizzled chunk) fixed for the whole loop and the k step in the
@@ -673,13 +525,19 @@ __global__ __launch_bounds__(512) void fc_fwd_bf16_p3(FcB16Args a) {
 //     Every fragment read is issued one 32-k step ahead of the MFMAs that
 //     consume it (two fragment register sets), and the DMA of a tile has the
 //     MFMAs of one whole tile to land.
-// Variant 4: 4 waves of 128 x 128 (8 x 8 fragments, 256 accumulators: one
-// wave per SIMD, half the LDS fragment bytes per MFMA of the 8-wave form);
-// variant 5: 8 waves of 128 x 64 as fc_fwd_bf16.  Requires lda1 == lda2 and
-// ldw1 == ldw2 (one offset set for both k phases); the host falls back to
-// fc_fwd_bf16 otherwise.
-template <int WM, int WN, int FM, int FN, bool RELU, bool SCHED, bool PRIO, int TRO = 0>
+// (3) The reads and DMA pieces are placed one per MFMA (sched_group_barrier)
+//     and waves 4-7 run at s_setprio 1.
+// (4) Transposed fragments: the MFMA is issued as W x A^T, so the 16x16 C/D
+//     map puts one output row on the lane and four consecutive columns in its
+//     registers (epilogue_bf16_ti: 8-byte LDS image accesses).  Bitwise the
+//     untransposed kernel (the MFMA sums the same exact products).
+// Requires lda1 == lda2 and ldw1 == ldw2 (one offset set for both k phases);
+// the host falls back to fc_fwd_bf16 otherwise.  (A 4-wave 128 x 128-per-wave
+// form -- 256 accumulators, one wave per SIMD -- measured 670-790 TF/s and
+// spilled; it is gone, see the spill rule in the header.)
+template <int WM, int WN, int FM, int FN, bool RELU>
 __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
+  constexpr bool SCHED = true, PRIO = true;
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   constexpr int A_BYTES = BM * BK * 2, TILE_BYTES = A_BYTES + BN * BK * 2;
@@ -761,18 +619,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
       bv[j] = *reinterpret_cast<const bf16x8 *>(Bs + row * 128 + swz(row, chunk) * 16);
     }
   };
-  auto mma = [&](const bf16x8(&av)[FM], const bf16x8(&bv)[FN]) {
-    if constexpr (TRO != 0) {  // W x A^T; consecutive MFMAs share their first operand, as below
+  auto mma = [&](const bf16x8(&av)[FM], const bf16x8(&bv)[FN]) {  // W x A^T (transposed fragments)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int i = 0; i < FM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
-    }
+      for (int i = 0; i < FM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
   };
   auto barrier = [&]() {  // this wave's DMA landed and its fragment reads returned; then all waves
     __builtin_amdgcn_sched_barrier(0);
@@ -831,17 +682,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
     mma(a1, b1);
   }
   // the epilogue image reuses the tile buffers: the last (empty-range) DMA has landed, every wave
-  // is past its reads (the transposed form writes straight from registers: no image, no barrier)
+  // is past its reads
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (TRO == 1) {
-    epilogue_bf16_t<FM, FN, RELU>(a, acc, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
-  } else if constexpr (TRO == 2) {
-    __syncthreads();
-    epilogue_bf16_ti<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
-  } else {
-    __syncthreads();
-    epilogue_bf16<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
-  }
+  __syncthreads();
+  epilogue_bf16_ti<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
 }
 
 // ---- weight gradient dW = G^T X in bf16 (fp32 out) ---------------------------
@@ -898,8 +742,9 @@ __device__ __forceinline__ void dma16_asm(uint64_t p, uint32_t n, unsigned char 
 
 __device__ __forceinline__ int wg_f(int r) { return (r & 3) | ((r & 8) >> 1); }
 
-template <int WM, int WN, int FM, int FN, bool SCHED, bool PRIO, bool TRO = false>
+template <int WM, int WN, int FM, int FN>
 __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
+  constexpr bool SCHED = true;
   constexpr int NW = WM * WN;
   constexpr int BN = WM * FM * 16, BKC = WN * FN * 16;  // output rows (n) x columns (k)
   static_assert(BN == 256 && BKC == 256, "512-B image rows");
@@ -935,7 +780,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
     unsigned char *base = smem + b * TILE_BYTES;
     const int64_t rt = r0 + (int64_t)t * WG_BR;
     const int64_t left = r1 > rt ? r1 - rt : 0;
-    const int64_t gb = left * a.ldg * 2, xb = left * a.ldx * 2;
+    // the ranges end at the last row's last column of the tile (not n0 / k0 elements past it), so
+    // a ragged column tile reads nothing past the end of G / X (its lanes past N / K read zeros)
+    const int64_t gw = a.N - n0 < 256 ? a.N - n0 : 256, xw = a.K - k0 < 256 ? a.K - k0 : 256;
+    const int64_t gb = left > 0 ? ((left - 1) * a.ldg + gw) * 2 : 0, xb = left > 0 ? ((left - 1) * a.ldx + xw) * 2 : 0;
     const uint32_t ng = (uint32_t)(gb < 0x7fffffff ? gb : 0x7fffffff), nx = (uint32_t)(xb < 0x7fffffff ? xb : 0x7fffffff);
     const uint64_t pg = (uint64_t)(a.G + rt * a.ldg + n0), px = (uint64_t)(a.X + rt * a.ldx + k0);
 #pragma unroll
@@ -979,17 +827,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
     for (int j = 0; j < FN; ++j) bv[j] = tr2(Xs, ((wn * FN + j) ^ flv) * 32);
   };
   auto mma = [&](const bf16x8(&av)[FM], const bf16x8(&bv)[FN]) {
-    if constexpr (TRO) {  // X^T G: four consecutive k (dW columns) per lane, for 16-byte stores
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int i = 0; i < FM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
-    }
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
   };
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
@@ -1000,7 +841,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
   };
 
   bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
-  if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   if (nk > 0) {
     stage(0, 0);
     barrier();
@@ -1047,26 +887,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_bf16(WgB16Args a) {
 
   float *P = a.P + s * a.ps;
   const int fr = lane & 15;
-  if constexpr (TRO) {  // D map: n = lane & 15, k = 4 * (lane >> 4) + r
-    const bool vec = a.ldp % 4 == 0 && (reinterpret_cast<uintptr_t>(P) & 15) == 0;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int64_t row = n0 + wm * FM * 16 + i * 16 + fr;
-      if (row >= a.N) continue;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int64_t col = k0 + wn * FN * 16 + j * 16 + 4 * g;
-        if (vec && col + 3 < a.K) {
-          *reinterpret_cast<f32x4 *>(P + row * a.ldp + col) = acc[i][j];
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (col + r < a.K) P[row * a.ldp + col + r] = acc[i][j][r];
-        }
-      }
-    }
-    return;
-  }
   // D map: row (n) = 4 * (lane >> 4) + r, col (k) = lane & 15
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
@@ -1109,20 +929,7 @@ lpg_status launch_bf16(FcB16Args a, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
-lpg_status launch_bf16_p3(FcB16Args a, bool relu, hipStream_t s) {
-  a.mt = (a.M + 255) / 256;
-  a.nt = (a.N + 255) / 256;
-  const int64_t nwg = a.mt * a.nt;
-  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_bf16: grid too large");
-  if (relu)
-    hipLaunchKernelGGL(fc_fwd_bf16_p3<true>, dim3((unsigned)nwg), dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL(fc_fwd_bf16_p3<false>, dim3((unsigned)nwg), dim3(512), 0, s, a);
-  LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
-template <int WM, int WN, int FM, int FN, bool SCHED = false, bool PRIO = false, int TRO = 0>
+template <int WM, int WN, int FM, int FN>
 lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   a.mt = (a.M + BM - 1) / BM;
@@ -1130,11 +937,9 @@ lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_bf16: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, true, SCHED, PRIO, TRO>), dim3((unsigned)nwg),
-                       dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, true>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, false, SCHED, PRIO, TRO>), dim3((unsigned)nwg),
-                       dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, false>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -1147,18 +952,13 @@ bool p_ok(const FcB16Args &a) {
   return (256 * a.lda1 + K) * 2 < ((int64_t)1 << 31) && (256 * a.ldw1 + K) * 2 < ((int64_t)1 << 31);
 }
 
-// lpg_fc_bf16_set_variant: 0 = by size (128 x 128 below 4096 rows, else 10, else 2), 1 = 128 x 128,
-// 2 = 256^2 2-buffer, 3 = 256^2 3-buffer,
-// 4 / 5 = fc_bf16_p with 4 / 8 waves, 6 = 5 with the reads and DMA placed between the MFMAs
-// (sched_group_barrier), 7 = 6 + s_setprio 1 for waves 4-7, 8 = 4 placed, 9 = 7 with transposed
-// fragments (W x A^T) and a register epilogue, 10 = 7 with transposed fragments through the LDS
-// image (8-byte LDS accesses); 100 / 101 = wgrad_bf16 with 4 / 8 waves, 102 / 103 = 101 placed /
-// + prio, 104 = 100 placed (102 the default; measured at the c5 shapes,
-// profiles/r02_kbench_bf16.log: 7 1209-1212 TF/s vs hipBLASLt 1268 (2 1033); 102 1172-1222 vs
-// hipBLASLt's bf16-output GEMM 924-1004; profiles/r02_kbench_fck10.log: 10 = 7 on plain
-// epilogues, ReLU + dropout + accumulate 1.745 -> 1.662 ms at M = 200K, K = 2048)
-int g_bf16_variant = 0;
-int g_wgrad_bf16_variant = 102;
+// Kernel choice, per call in flags bits 8-11 (LPG_FC_KERNEL(k), include/lpgnn.h): 0 = by shape
+// (128 x 128 below 4096 rows, else the pipelined kernel when p_ok, else 256 x 256), 1 = fc_fwd_bf16
+// 128 x 128 (4 waves), 2 = fc_fwd_bf16 256 x 256 (8 waves), 3 = fc_bf16_p (falls back to 2 when
+// !p_ok).  Every choice computes the same bits.  Measured at the c5 shapes
+// (profiles/r02_kbench_bf16.log, r02_kbench_fck10.log): fc_bf16_p 1212-1300 TF/s vs hipBLASLt
+// 1248-1268, fc_fwd_bf16 256^2 1033; wgrad_bf16 1172-1222 vs hipBLASLt's bf16-output GEMM 924-1004.
+constexpr int kKernels = 3;
 
 int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
   const int64_t tiles = ((N + 255) / 256) * ((K + 255) / 256);
@@ -1227,7 +1027,8 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
   LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
                   (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
               "lpg_fc_bf16: A/W must be 16-byte aligned with leading dimensions multiple of 8");
-  LPG_REQUIRE((flags & ~3) == 0, "lpg_fc_bf16: unknown flags 0x%x", flags);
+  const int kernel = (flags >> 8) & 15;
+  LPG_REQUIRE((flags & ~0xf03) == 0 && kernel <= kKernels, "lpg_fc_bf16: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_bf16: dropout_p %g not in [0, 1)", (double)dropout_p);
   FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1};
   if (dropout_p > 0.f) {
@@ -1235,7 +1036,7 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
     a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);
     a.drop_scale = 1.f / (1.f - dropout_p);
   }
-  return fc_bf16_dispatch(a, flags & 1, as_stream(stream), g_bf16_variant);
+  return fc_bf16_dispatch(a, flags & 1, as_stream(stream), kernel);
 }
 
 // The input gradient of a layer whose input went through the previous layer's ReLU + dropout,
@@ -1258,33 +1059,20 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, con
   LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
                   (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
               "lpg_fc_bf16_relu_bwd: A/W must be 16-byte aligned with leading dimensions multiple of 8");
-  LPG_REQUIRE((flags & ~2) == 0, "lpg_fc_bf16_relu_bwd: only the accumulate flag (2) is accepted, got 0x%x", flags);
+  const int kernel = (flags >> 8) & 15;
+  LPG_REQUIRE((flags & ~0xf02) == 0 && kernel <= kKernels,
+              "lpg_fc_bf16_relu_bwd: only the accumulate flag (2) and a kernel choice are accepted, got 0x%x", flags);
   FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, nullptr, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, 0, 0u, 1.f, (flags >> 1) & 1,
               Y, ldy, scale};
-  // the fold lives in the LDS-image epilogues: variants without one (3, 9) take the default kernel
-  const int v = (g_bf16_variant == 3 || g_bf16_variant == 9) ? 0 : g_bf16_variant;
-  return fc_bf16_dispatch(a, false, as_stream(stream), v);
+  return fc_bf16_dispatch(a, false, as_stream(stream), kernel);  // (every kernel's epilogue takes the fold)
 }
 
 namespace lpg {
 namespace {
-lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant) {
-  const int64_t M = a.M;
-  const int g_bf16_variant = variant;
-  if (g_bf16_variant == 1 || (g_bf16_variant == 0 && M < 4096))
-    return launch_bf16<2, 2, 4, 4>(a, relu, s);  // 128 x 128
-  if (g_bf16_variant == 0 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true, true, 2>(a, relu, s);  // = 10
-  if (g_bf16_variant == 3) return launch_bf16_p3(a, relu, s);  // 256 x 256, BK 32, 3 buffers
-  if (g_bf16_variant == 4 && p_ok(a)) return launch_bf16_p<2, 2, 8, 8>(a, relu, s);  // 4 waves of 128 x 128
-  if (g_bf16_variant == 5 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4>(a, relu, s);  // 8 waves of 128 x 64
-  if (g_bf16_variant == 6 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true>(a, relu, s);  // + placed reads
-  if (g_bf16_variant == 7 && p_ok(a)) return launch_bf16_p<2, 4, 8, 4, true, true>(a, relu, s);  // + prio
-  if (g_bf16_variant == 8 && p_ok(a)) return launch_bf16_p<2, 2, 8, 8, true>(a, relu, s);  // 4 waves, placed
-  if (g_bf16_variant == 9 && p_ok(a))  // 7 with transposed fragments: register epilogue, 8-byte stores
-    return launch_bf16_p<2, 4, 8, 4, true, true, 1>(a, relu, s);
-  if (g_bf16_variant == 10 && p_ok(a))  // 7 with transposed fragments through the image (8-byte LDS accesses)
-    return launch_bf16_p<2, 4, 8, 4, true, true, 2>(a, relu, s);
-  return launch_bf16<2, 4, 8, 4>(a, relu, s);    // 256 x 256, BK 64, 2 buffers
+lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
+  if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<2, 2, 4, 4>(a, relu, s);  // 128 x 128
+  if ((kernel == 0 || kernel == 3) && p_ok(a)) return launch_bf16_p<2, 4, 8, 4>(a, relu, s);
+  return launch_bf16<2, 4, 8, 4>(a, relu, s);  // 256 x 256, BK 64, 2 buffers
 }
 }  // namespace
 }  // namespace lpg
@@ -1300,16 +1088,6 @@ extern "C" lpg_status lpg_transpose_bf16(int64_t R, int64_t C, const uint16_t *s
   LPG_REQUIRE((R + 63) / 64 < 65536, "lpg_transpose_bf16: too many rows");
   hipLaunchKernelGGL(transpose_bf16, grid, dim3(256), 0, as_stream(stream), R, C, src, lds, dst, ldd);
   LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
-extern "C" lpg_status lpg_fc_bf16_set_variant(int32_t v) {
-  LPG_REQUIRE((v >= 0 && v <= 10) || (v >= 100 && v <= 105),
-              "lpg_fc_bf16_set_variant: variant %d not in [0, 10] or [100, 105]", v);
-  if (v >= 100)
-    g_wgrad_bf16_variant = v;
-  else
-    g_bf16_variant = v;
   return LPG_OK;
 }
 
@@ -1338,14 +1116,7 @@ extern "C" lpg_status lpg_wgrad_bf16(int64_t R, int64_t N, int64_t K, const uint
   const int64_t nwg = w.nt * w.kt * S;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_wgrad_bf16: grid too large");
   hipStream_t s = as_stream(stream);
-  switch (g_wgrad_bf16_variant) {
-    case 100: hipLaunchKernelGGL((wgrad_bf16<2, 2, 8, 8, false, false>), dim3((unsigned)nwg), dim3(256), 0, s, w); break;
-    case 101: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, false, false>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
-    case 102: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, true, false>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
-    case 103: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, true, true>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
-    case 105: hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4, true, false, true>), dim3((unsigned)nwg), dim3(512), 0, s, w); break;
-    default: hipLaunchKernelGGL((wgrad_bf16<2, 2, 8, 8, true, false>), dim3((unsigned)nwg), dim3(256), 0, s, w); break;
-  }
+  hipLaunchKernelGGL((wgrad_bf16<2, 4, 8, 4>), dim3((unsigned)nwg), dim3(512), 0, s, w);
   LPG_HIP(hipGetLastError());
   if (S > 1) {
     const int64_t tot = N * (K / 4);

@@ -49,6 +49,19 @@ __device__ __forceinline__ void dma16(uint64_t p, uint32_t n, unsigned char *lds
 #endif
 }
 
+// The ReLU/dropout backward of two packed bf16 values (element 0 in the low half):
+// (y > 0) ? RNE_bf16(g * scale) : 0 per element, on the packed datapath -- one v_pk_mul_f32 and one
+// v_cvt_pk_bf16_f32 per pair.  Shared by lpg_relu_bwd_colsum_bf16 (bwd.hip) and the folded form in
+// the bf16 FC epilogue (fc_bf16.hip), so the two give the same bits for every input, NaN included.
+typedef float lpg_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 lpg_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t relu_bwd_pk_bf16(uint32_t g, uint32_t y, float scale) {
+  const lpg_f32x2 gf = {__uint_as_float(g << 16), __uint_as_float(g & 0xffff0000u)};
+  const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(gf * lpg_f32x2{scale, scale}, lpg_bf16x2));
+  const float y0 = __uint_as_float(y << 16), y1 = __uint_as_float(y & 0xffff0000u);
+  return (y0 > 0.f ? (pk & 0xffffu) : 0u) | (y1 > 0.f ? (pk & 0xffff0000u) : 0u);
+}
+
 // Host-side dropout threshold / scale shared by the FC entry points.
 inline void dropout_params(float p, uint32_t *thresh, float *scale) {
   *thresh = 0u;

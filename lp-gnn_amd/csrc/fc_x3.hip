@@ -29,11 +29,11 @@
 // Operands: A (activations) fp32 as in lpg_fc_f32, split in registers by the
 // lane that feeds it to the MFMA; W pre-split once per call (lpg_split3_f32:
 // three bf16 planes, weights are small) so only A costs VALU in the k loop.
-// Two kernel families.  fc_fwd_x3 (variants 1-4, 8): 4 waves (2 x 2),
-// 128 x 128 output tile, each wave 2 x 2 fragments of 32 x 32 from
-// v_mfma_f32_32x32x16_bf16 (accH + accL: 128 VGPRs).  fc_fwd_x3_16 (the
-// default, variant 0 = <4,1,2,8>, and 5-7, 9, 10): v_mfma_f32_16x16x32_bf16
-// fragments, which hold a higher clock under DVFS on gfx950.  Both:  k-tiles of BK = 32 staged by LDS-DMA
+// Two kernels, both on v_mfma_f32_16x16x32_bf16 (which holds a higher clock
+// under DVFS on gfx950 than 32x32x16) with 128 x 128 output tiles of four
+// 32 x 128 wave strips: fc_x3_wide (the default: buffer_load ... lds staging)
+// and fc_fwd_x3_16 (global_load_lds staging; takes operands fc_x3_wide cannot,
+// and is the per-call alternative LPG_FC_KERNEL(1)).  Both:  k-tiles of BK = 32 staged by LDS-DMA
 // (global_load_lds) into a 2-stage ring: A as 128-B fp32 rows (16-B chunk c of
 // row r at c ^ ((r >> 1) & 7)), each W plane as 64-B bf16 rows (chunk c at
 // c ^ ((r >> 2) & 3)); both make the ds_read_b128 fragment reads
@@ -73,7 +73,6 @@ struct X3Args {
   uint32_t drop_thresh;
   float drop_scale;
   int32_t accum;
-  int32_t xmap;  // fc_fwd_x3_16 block -> tile map: 0 = m-major per XCD, 1 = n-tile pairs per XCD pair
   // fused heads (fc_fwd_x3_16 only): hw [hn][ldhw] fp32; per-(wave column tile, row) partial logits
   // to hpart [N / (TN * 16)][M][4]
   const float *hw;
@@ -157,248 +156,19 @@ __device__ __forceinline__ float sum16(float v) {
 __device__ __forceinline__ int swzA(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }  // 128-B rows
 __device__ __forceinline__ int swzW(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }  // 64-B rows
 
-template <int WM, int WN, int TM, int TN, bool PIPE, bool RELU>
-__global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3(X3Args a) {
-  constexpr int NW = WM * WN;
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  constexpr int A_BYTES = BM * BK * 4, WP_BYTES = BN * BK * 2;  // A image, one W plane image
-  constexpr int TILE_BYTES = A_BYTES + 3 * WP_BYTES;
-  constexpr int PA = BM / 8 / NW;            // A pieces (8 rows x 128 B) per wave
-  constexpr int PB = 3 * (BN / 16) / NW;     // W pieces (16 rows x 64 B, all planes) per wave
-  static_assert(BM % (8 * NW) == 0 && (3 * BN / 16) % NW == 0, "tile rows must split into whole pieces per wave");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
-
-  const int64_t nwg = a.mt * a.nt;
-  const int64_t bid = blockIdx.x;
-  const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
-  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
-  const int64_t m0 = (wgid / a.nt) * BM;
-  const int64_t n0 = (wgid % a.nt) * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int nk1 = (int)(a.K1 / BK);
-  const int nk = nk1 + (int)(a.K2 / BK);
-
-  const float *srcA1[PA], *srcA2[PA];
-  const uint16_t *srcW1[PB], *srcW2[PB];
-#pragma unroll
-  for (int p = 0; p < PA; ++p) {
-    const int row = (wave + NW * p) * 8 + (lane >> 3);
-    int64_t gr = m0 + row;
-    gr = gr < a.M ? gr : a.M - 1;  // rows past M feed outputs that are never stored
-    const int off = swzA(row, lane & 7) * 4;
-    srcA1[p] = a.A1 + gr * a.lda1 + off;
-    srcA2[p] = a.A2 + gr * a.lda2 + off;
-  }
-#pragma unroll
-  for (int p = 0; p < PB; ++p) {
-    const int q = wave + NW * p, plane = q / (BN / 16);
-    const int row = (q % (BN / 16)) * 16 + (lane >> 2);
-    int64_t gn = n0 + row;
-    gn = gn < a.N ? gn : a.N - 1;
-    const int off = swzW(row, lane & 3) * 8;
-    srcW1[p] = a.W1 + plane * a.ps1 + gn * a.ldw1 + off;
-    srcW2[p] = a.W2 + plane * a.ps2 + gn * a.ldw2 + off;
-  }
-  auto stage = [&](int b, int t) {
-    typedef __attribute__((address_space(3))) unsigned char lds_t;
-    unsigned char *base = smem + b * TILE_BYTES;
-    const bool p2 = t >= nk1;
-    const int64_t k0 = (int64_t)(p2 ? t - nk1 : t) * BK;
-#pragma unroll
-    for (int p = 0; p < PA; ++p)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcA2[p] : srcA1[p]) + k0),
-                                       (lds_t *)(base + (wave + NW * p) * 1024), 16, 0, 0);
-#pragma unroll
-    for (int p = 0; p < PB; ++p)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>((p2 ? srcW2[p] : srcW1[p]) + k0),
-                                       (lds_t *)(base + A_BYTES + (wave + NW * p) * 1024), 16, 0, 0);
-  };
-
-  f32x16 accH[TM][TN], accL[TM][TN];
-  const f32x16 zero = {};
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) accH[i][j] = accL[i][j] = zero;
-
-  const int fr = lane & 31, fk = lane >> 5;
-  const int rA0 = wm * TM * 32 + fr, rB0 = wn * TN * 32 + fr;
-
-  // operand reads of one 16-k substep (s) of the tile image T
-  struct RawA {
-    f32x4 v[TM][2];
-  };
-  struct OpB {
-    bf16x8 v[TN][3];
-  };
-  auto ldA = [&](const unsigned char *T, int s) {
-    RawA r;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        r.v[i][h] = *reinterpret_cast<const f32x4 *>(T + (rA0 + i * 32) * (BK * 4) +
-                                                     swzA(rA0 + i * 32, 4 * s + 2 * fk + h) * 16);
-    return r;
-  };
-  auto ldB = [&](const unsigned char *T, int s) {
-    OpB r;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        r.v[j][p] = *reinterpret_cast<const bf16x8 *>(T + A_BYTES + p * WP_BYTES + (rB0 + j * 32) * (BK * 2) +
-                                                      swzW(rB0 + j * 32, 2 * s + fk) * 16);
-    return r;
-  };
-  auto mfma_row = [&](int i, const Split3 &av, const OpB &bv) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.l, bv.v[j][0], accL[i][j], 0, 0, 0);
-      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv.v[j][1], accL[i][j], 0, 0, 0);
-      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.v[j][2], accL[i][j], 0, 0, 0);
-      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv.v[j][0], accL[i][j], 0, 0, 0);
-      accL[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.v[j][1], accL[i][j], 0, 0, 0);
-      accH[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.v[j][0], accH[i][j], 0, 0, 0);
-    }
-  };
-
-  if (!PIPE) {
-    if (nk > 0) stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    int b = 0;
-    for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk) stage(b ^ 1, t + 1);
-      const unsigned char *T = smem + b * TILE_BYTES;
-#pragma unroll
-      for (int s = 0; s < BK / 16; ++s) {  // lane half fk feeds k = 16 s + 8 fk + 0..7 of one 32x32x16 MFMA
-        const RawA ra = ldA(T, s);
-        const OpB bv = ldB(T, s);
-        Split3 av[TM];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) av[i] = split3(ra.v[i][0], ra.v[i][1]);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) mfma_row(i, av[i], bv);
-      }
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // tile t+1 landed; every wave done with tile t
-      asm volatile("" ::: "memory");
-      b ^= 1;
-    }
-  } else {
-    // Software-pipelined: a substep's operands are read one substep ahead, and
-    // each A fragment is split while the previous fragment's MFMAs run.  The
-    // DMA of tile t+2 goes into tile t's buffer right after the barrier that
-    // follows every wave's last read of tile t (issued during substep 0), so
-    // each DMA has a whole tile of MFMAs to land.
-    if (nk > 0) stage(0, 0);
-    if (nk > 1) {
-      stage(1, 1);
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(PA + PB) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    RawA ra = ldA(smem, 0);
-    for (int t = 0; t < nk; ++t) {
-      const int b = t & 1;
-      const unsigned char *T = smem + b * TILE_BYTES;
-      // substep 0 of tile t; prefetch substep 1's A
-      {
-        const OpB bv = ldB(T, 0);
-        const Split3 a0 = split3(ra.v[0][0], ra.v[0][1]);
-        const RawA nra = ldA(T, 1);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const Split3 ai = i == 0 ? a0 : split3(ra.v[i][0], ra.v[i][1]);
-          mfma_row(i, ai, bv);
-        }
-        ra = nra;
-      }
-      // substep 1; prefetch substep 0's A of tile t+1
-      {
-        const OpB bv = ldB(T, 1);
-        const Split3 a0 = split3(ra.v[0][0], ra.v[0][1]);
-        RawA nra = ra;
-        if (t + 1 < nk) {
-          asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();  // tile t+1 landed; every wave's reads of tile t are done
-          asm volatile("" ::: "memory");
-          if (t + 2 < nk) stage(b, t + 2);
-          nra = ldA(smem + (b ^ 1) * TILE_BYTES, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const Split3 ai = i == 0 ? a0 : split3(ra.v[i][0], ra.v[i][1]);
-          mfma_row(i, ai, bv);
-        }
-        ra = nra;
-      }
-    }
-  }
-
-  // Epilogue.  32x32 MFMA output map: col = lane & 31, row = 4 (lane >> 5) + (r & 3) + 8 (r >> 2).
-  // With the accumulate flag every C load is issued before the first store.
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = accH[i][j] + accL[i][j];
-  const int64_t mw = m0 + wm * TM * 32, nw = n0 + wn * TN * 32;
-  if (a.accum) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      int64_t col = nw + j * 32 + (lane & 31);
-      col = col < a.N ? col : a.N - 1;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          int64_t row = mw + i * 32 + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2);
-          row = row < a.M ? row : a.M - 1;
-          acc[i][j][r] = acc[i][j][r] + a.C[row * a.ldc + col];
-        }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int64_t col = nw + j * 32 + (lane & 31);
-    if (col >= a.N) continue;
-    const float bb = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int64_t rbase = mw + i * 32 + 4 * (lane >> 5);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row >= a.M) continue;
-        float v = acc[i][j][r];
-        if (a.bias) v = v + bb;
-        if (RELU) v = (v < 0.f) ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-        a.C[row * a.ldc + col] = v;
-      }
-    }
-  }
-}
-
 // The same GEMM on v_mfma_f32_16x16x32_bf16 (MI355X_MICROARCH.md 'DVFS
 // give-back' item 7: on random operands the chip holds a higher clock on this
 // shape, ~1.12-1.15x the FLOP/s of 32x32x16 at equal cycles per FLOP).  One
 // MFMA consumes a whole BK = 32 k-tile: lane group g = lane >> 4 feeds
 // k = 8g .. 8g+7 (A: two 16-B chunks of its row, W: chunk g of each plane);
-// the LDS images and swizzles are those of fc_fwd_x3 (16 consecutive rows at
-// one logical chunk land in 16 distinct bank slots).  Each wave owns
+// LDS images: A as 128-B fp32 rows (16-B chunk c of row r at c ^ ((r >> 1) & 7)),
+// each W plane as 64-B bf16 rows (chunk c at c ^ ((r >> 2) & 3)): 16 consecutive
+// rows at one logical chunk land in 16 distinct bank slots.  Each wave owns
 // (TM x TN) fragments of 16 x 16; output map col = lane & 15,
 // row = 4 (lane >> 4) + r.
 // HEADS: the fused-heads epilogue (lpg_fc_x3_heads_f32) is compiled only into the instantiations that
 // use it, so the plain FC and input-gradient GEMMs carry none of its registers.
-template <int WM, int WN, int TM, int TN, bool RELU, bool PROBE = false, bool HEADS = false>
+template <int WM, int WN, int TM, int TN, bool RELU, bool HEADS = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
@@ -412,17 +182,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
   const int64_t nwg = a.mt * a.nt;
   const int64_t bid = blockIdx.x;
   const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
-  int64_t m0, n0;
-  if (a.xmap) {  // nt == 8: XCDs x and x + 4 share n-tiles 2(x%4), +1 (their W planes stay in L2)
-    // and split the m-tiles: the pair's 2 * mt tiles in (m, n) order, first mt on x, rest on x + 4
-    const int64_t t = (xcd >> 2) * a.mt + bid / 8;
-    m0 = (t >> 1) * BM;
-    n0 = ((xcd & 3) * 2 + (t & 1)) * BN;
-  } else {
-    const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
-    m0 = (wgid / a.nt) * BM;
-    n0 = (wgid % a.nt) * BN;
-  }
+  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
+  const int64_t m0 = (wgid / a.nt) * BM;
+  const int64_t n0 = (wgid % a.nt) * BN;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -499,16 +261,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
     };
     auto lda = [&](int i) {
       const unsigned char *ra = T + (rA0 + i * 16) * (BK * 4);
-      Split3 av;
-      if constexpr (PROBE) {  // timing probe only (wrong results): A's bytes reinterpreted, no split VALU
-        av.h = *reinterpret_cast<const bf16x8 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16);
-        av.m = *reinterpret_cast<const bf16x8 *>(ra + swzA(rA0 + i * 16, 2 * fg + 1) * 16);
-        av.l = av.h;
-      } else {
-        av = split3(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16),
+      return split3(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16),
                     *reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg + 1) * 16));
-      }
-      return av;
     };
     if constexpr (TN <= 4) {
       bf16x8 bv[TN][3];
@@ -638,7 +392,7 @@ __global__ __launch_bounds__(256) void heads_fold(int64_t M, int64_t nparts, int
   logits[m * ldl + c] = v;
 }
 
-template <int WM, int WN, int TM, int TN, bool PROBE = false, bool HEADS = false>
+template <int WM, int WN, int TM, int TN, bool HEADS = false>
 lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16, NT = 64 * WM * WN;
   a.mt = (a.M + BM - 1) / BM;
@@ -646,14 +400,14 @@ lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, true, PROBE, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, true, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, false, PROBE, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_x3_16<WM, WN, TM, TN, false, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
 
-// ---- wide strips: fc_x3_wide (variants 12-15; the default) --------------------
+// ---- wide strips: fc_x3_wide (the default) -------------------------------------
 //
 // fc_fwd_x3_16 splits every A element once per block, so the split VALU per MFMA falls only as
 // the block's N width grows; and its stage() spent ~6 VALU per LDS-DMA piece on 64-bit address
@@ -807,43 +561,39 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = accH[i][j] + accL[i][j];
-  // fused heads (hn <= 3 here; the host routes hn = 4 to fc_fwd_x3_16): this lane's partial
-  // logits [head][i][r]
+  // fused heads (hn <= 3 here; the host routes hn = 4 to fc_fwd_x3_16): the store loops also put
+  // each output into a per-wave LDS image (the tile buffers are free: every wave passed the last
+  // k-tile's barrier), and a second pass reads them back column block by column block into this
+  // lane's partial logits -- the same values in the same order as accumulating them in the store
+  // loop, without 24 partial sums live beside the 64 outputs (that form spilled)
   constexpr int HC = HEADS ? 3 : 1;
-  float hs[HC][TM][4];
-  if constexpr (HEADS) {
-#pragma unroll
-    for (int c = 0; c < HC; ++c)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hs[c][i][r] = 0.f;
-  }
-  auto head_w = [&](int64_t col, float(&hwv)[HC]) {  // loads from valid rows only, no branch
-    if constexpr (HEADS) {
-#pragma unroll
-      for (int c = 0; c < HC; ++c) {
-        const float w = a.hw[(c < a.hn ? c : a.hn - 1) * a.ldhw + col];
-        hwv[c] = c < a.hn ? w : 0.f;
-      }
-    }
+  constexpr int HP = BN + 4;  // image row pitch (floats): rows 4 fg apart land 16 banks apart
+  static_assert(!HEADS || NW * TM * 16 * HP * 4 <= 2 * TILE_BYTES, "heads image fits the tile buffers");
+  float *const himg = reinterpret_cast<float *>(smem) + wave * (TM * 16 * HP) + 4 * fg * HP + fr;
+  auto hput = [&](int i, int r, int j, float v) {
+    if constexpr (HEADS) himg[(i * 16 + r) * HP + j * 16] = v;
   };
   if (mw + TM * 16 <= a.M && nw + BN <= a.N) {
-    // interior wave tile (wave-uniform): no per-element bounds, one C row pointer per (i, r) with
-    // the column step j * 16 as the store's immediate offset, the dropout row keys computed once
-    // per row (the per-element forms cost ~24 VALU incl. 6 v_mul_lo_u32 and a branch per output)
-    float *rp[TM][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rp[i][r] = a.C + (mw + i * 16 + 4 * fg + r) * a.ldc + nw + fr;
+    // interior wave tile (wave-uniform): no per-element bounds; element (i, r, j) lives at the
+    // wave-uniform row base C + (mw + 16 i + r) ldc + nw (SGPRs) plus ONE per-lane offset
+    // 4 fg ldc + fr (the same for every i, r, j) plus the column step j * 16 as the immediate offset
+    // (a per-(i, r) 64-bit row pointer took 16 VGPRs, and the fused heads' epilogue spilled);
+    // the dropout row keys are computed once per row (the per-element forms cost ~24 VALU incl.
+    // 6 v_mul_lo_u32 and a branch per output)
+    const int64_t loff = 4 * fg * a.ldc + fr;
+    auto rp = [&](int i, int r) -> float * {
+      const uint64_t rb = (uint64_t)(a.C + (mw + i * 16 + r) * a.ldc + nw);
+      const uint64_t u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32)) << 32) |
+                         __builtin_amdgcn_readfirstlane((uint32_t)rb);
+      return reinterpret_cast<float *>(u) + loff;
+    };
     if (a.accum) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + rp[i][r][j * 16];
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + rp(i, r)[j * 16];
     }
     auto body = [&](auto bias_c, auto drop_c) {
       constexpr bool BIAS = decltype(bias_c)::value, DROP = decltype(drop_c)::value;
@@ -859,8 +609,6 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
         const int64_t col = nw + j * 16 + fr;
         const float bb = BIAS ? a.bias[col] : 0.f;
         const uint32_t ck = drop_col_key(col);
-        float hwv[HC];
-        head_w(col, hwv);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -869,11 +617,8 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
             if constexpr (BIAS) v = v + bb;
             if (RELU) v = (v < 0.f) ? 0.f : v;
             if constexpr (DROP) v = drop_hash_k(rk[i][r], ck) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-            rp[i][r][j * 16] = v;
-            if constexpr (HEADS) {
-#pragma unroll
-              for (int c = 0; c < HC; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
-            }
+            rp(i, r)[j * 16] = v;
+            hput(i, r, j, v);
           }
       }
     };
@@ -905,8 +650,6 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
       const int64_t col = nw + j * 16 + fr;
       if (col >= a.N) continue;
       const float bb = a.bias ? a.bias[col] : 0.f;
-      float hwv[HC];
-      head_w(col, hwv);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -918,14 +661,40 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
           if (RELU) v = (v < 0.f) ? 0.f : v;
           if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
           a.C[row * a.ldc + col] = v;
-          if constexpr (HEADS) {
-#pragma unroll
-            for (int c = 0; c < HC; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
-          }
+          hput(i, r, j, v);
         }
     }
   }
-  if constexpr (HEADS) {  // sum over the 16 lanes (columns) of each row group, fixed DPP order; lane fr = 0 writes
+  if constexpr (HEADS) {
+    // this lane's partial logits [head][i][r] over its columns j * 16 + fr (columns past N and heads
+    // past hn get zero weights; image entries never written belong to rows / columns never stored)
+    float hs[HC][TM][4];
+#pragma unroll
+    for (int c = 0; c < HC; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hs[c][i][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = nw + j * 16 + fr;
+      const bool cok = col < a.N;
+      float hwv[HC];
+#pragma unroll
+      for (int c = 0; c < HC; ++c) {
+        const float w = a.hw[(c < a.hn ? c : a.hn - 1) * a.ldhw + (cok ? col : a.N - 1)];
+        hwv[c] = (c < a.hn && cok) ? w : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = cok ? himg[(i * 16 + r) * HP + j * 16] : 0.f;
+#pragma unroll
+          for (int c = 0; c < HC; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
+        }
+    }
+    // sum over the 16 lanes (columns) of each row group, fixed DPP order; lane fr = 0 writes
     const int64_t pidx = nw / BN;
 #pragma unroll
     for (int c = 0; c < HC; ++c)
@@ -970,21 +739,6 @@ lpg_status launch_x3_wide(X3Args a, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
-template <int WM, int WN, int TM, int TN, bool PIPE = false>
-lpg_status launch_x3(X3Args a, bool relu, hipStream_t s) {
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
-  a.mt = (a.M + BM - 1) / BM;
-  a.nt = (a.N + BN - 1) / BN;
-  const int64_t nwg = a.mt * a.nt;
-  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
-  if (relu)
-    hipLaunchKernelGGL((fc_fwd_x3<WM, WN, TM, TN, PIPE, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
-  else
-    hipLaunchKernelGGL((fc_fwd_x3<WM, WN, TM, TN, PIPE, false>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
-  LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
 // ---- weight gradient dW = G^T X on the same arithmetic -----------------------
 //
 // dW[n, k] = sum_r G[r, n] X[r, k] (G = dZ [R, N], X = the layer input [R, K]:
@@ -1002,176 +756,6 @@ lpg_status launch_x3(X3Args a, bool relu, hipStream_t s) {
 // from a zeroed 512-B row at the end of the workspace.
 constexpr int WG_T = 128;  // output tile (n and k)
 
-__device__ __forceinline__ Split3 split3_8(const float (&v)[8]) {
-  return split3(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]});
-}
-
-// M16: v_mfma_f32_16x16x32_bf16 (one MFMA per 32-row chunk, wave tile 4 x 4
-// fragments of 16 x 16; lane group g = lane >> 4 feeds rows 8g .. 8g+7).  Its
-// ds_read_b32 halves hold rows r and r + 8 at the same columns, so the image
-// XORs the 16-B chunk index with 4 on rows whose bit 3 is set (applied on the
-// DMA source address): the two rows land 16 banks apart.
-template <bool M16>
-__global__ __launch_bounds__(256, 2) void wgrad_x3(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
-                                                   int64_t ldg, const float *__restrict__ X, int64_t ldx,
-                                                   float *__restrict__ part, const float *__restrict__ zrow,
-                                                   int64_t nt, int64_t kt, int64_t S, int64_t chunks_per_split) {
-  constexpr int OP_BYTES = 32 * WG_T * 4;  // one operand's k-tile image: 32 rows x 512 B
-  constexpr int TILE_BYTES = 2 * OP_BYTES;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
-  auto swz = [](int row) { return M16 ? ((row >> 3) & 1) * 4 : 0; };  // 16-B chunk XOR of a row
-
-  // block -> (split s, output tile); consecutive blocks share s (same rows of G and X in L2)
-  // XCD-aware remap (blocks go round-robin to the 8 XCDs): each XCD walks a contiguous range of
-  // (split, tile) ids, so the tiles of one R range run on one XCD and share its rows of G and X
-  // in that XCD's L2 (round-robin spread them over all 8 L2s: 4x the bytes fetched past L2)
-  const int64_t nwg = (int64_t)gridDim.x, xcd = (int64_t)blockIdx.x % 8, q8 = nwg / 8, rr = nwg % 8;
-  const int64_t bid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (int64_t)blockIdx.x / 8;
-  const int64_t tiles = nt * kt;
-  const int64_t s = bid / tiles, tile = bid % tiles;
-  const int64_t n0 = (tile / kt) * WG_T, k0 = (tile % kt) * WG_T;
-  const int64_t nchunks = (R + 31) / 32;
-  const int64_t c0 = s * chunks_per_split;
-  const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-
-  // DMA: piece = 2 rows x 512 B; wave w moves pieces w, w+4, w+8, w+12 of G and of X
-  const float *srcG[4], *srcX[4], *srcZ;
-  int prow[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int piece = wave + 4 * p;
-    prow[p] = piece * 2 + (lane >> 5);
-    const int ch = (lane & 31) ^ swz(prow[p]);
-    int64_t gn = n0 + ch * 4, gk = k0 + ch * 4;
-    gn = gn < N ? gn : N - 4;  // N, K multiples of 4: columns past the edge feed outputs never stored
-    gk = gk < K ? gk : K - 4;
-    srcG[p] = G + gn;
-    srcX[p] = X + gk;
-  }
-  srcZ = zrow + (lane & 31) * 4;
-  auto stage = [&](int b, int64_t c) {
-    typedef __attribute__((address_space(3))) unsigned char lds_t;
-    unsigned char *base = smem + b * TILE_BYTES;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int64_t r = c * 32 + prow[p];
-      const bool in = r < R;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(in ? srcG[p] + r * ldg : srcZ),
-                                       (lds_t *)(base + (wave + 4 * p) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(in ? srcX[p] + r * ldx : srcZ),
-                                       (lds_t *)(base + OP_BYTES + (wave + 4 * p) * 1024), 16, 0, 0);
-    }
-  };
-  // the lane's 8 values of column col, rows r0 .. r0+7, from an operand image
-  auto read8 = [&](const unsigned char *img, int col, int r0, float (&v)[8]) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int r = r0 + e;
-      v[e] = *reinterpret_cast<const float *>(img + r * (WG_T * 4) + (((col >> 2) ^ swz(r)) * 4 + (col & 3)) * 4);
-    }
-  };
-
-  constexpr int FT = M16 ? 4 : 2;  // fragments per wave and dimension
-  typedef typename std::conditional<M16, f32x4, f32x16>::type acc_t;
-  acc_t accH[FT][FT], accL[FT][FT];
-  const acc_t zero = {};
-#pragma unroll
-  for (int i = 0; i < FT; ++i)
-#pragma unroll
-    for (int j = 0; j < FT; ++j) accH[i][j] = accL[i][j] = zero;
-  auto mfma6 = [&](acc_t &h, acc_t &l, const Split3 &av, const Split3 &bv) {
-    if constexpr (M16) {
-      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.l, bv.h, l, 0, 0, 0);
-      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bv.m, l, 0, 0, 0);
-      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv.l, l, 0, 0, 0);
-      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.m, bv.h, l, 0, 0, 0);
-      l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv.m, l, 0, 0, 0);
-      h = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.h, bv.h, h, 0, 0, 0);
-    } else {
-      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.l, bv.h, l, 0, 0, 0);
-      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv.m, l, 0, 0, 0);
-      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.l, l, 0, 0, 0);
-      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.m, bv.h, l, 0, 0, 0);
-      l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.m, l, 0, 0, 0);
-      h = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av.h, bv.h, h, 0, 0, 0);
-    }
-  };
-
-  // 32x32x16: lane (fr = lane & 31, fk = lane >> 5) feeds rows 16 ss + 8 fk .. +7 of substep ss;
-  // 16x16x32: lane (fr = lane & 15, g = lane >> 4) feeds rows 8 g .. +7 of the whole chunk
-  auto body = [&](const unsigned char *T) {
-    constexpr int FW = M16 ? 16 : 32;  // fragment width
-    const int fr = lane & (FW - 1);
-#pragma unroll
-    for (int ss = 0; ss < (M16 ? 1 : 2); ++ss) {
-      const int r0 = M16 ? 8 * (lane >> 4) : 16 * ss + 8 * (lane >> 5);
-      Split3 bv[FT];
-#pragma unroll
-      for (int j = 0; j < FT; ++j) {
-        float v[8];
-        read8(T + OP_BYTES, wn * 64 + j * FW + fr, r0, v);
-        bv[j] = split3_8(v);
-      }
-      // one A fragment's split live at a time (register pressure: 128 accumulators)
-#pragma unroll
-      for (int i = 0; i < FT; ++i) {
-        float v[8];
-        read8(T, wm * 64 + i * FW + fr, r0, v);
-        const Split3 av = split3_8(v);
-#pragma unroll
-        for (int j = 0; j < FT; ++j) mfma6(accH[i][j], accL[i][j], av, bv[j]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-
-  if (c0 < c1) stage(0, c0);
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  int b = 0;
-  for (int64_t c = c0; c < c1; ++c) {
-    if (c + 1 < c1) stage(b ^ 1, c + 1);
-    body(smem + b * TILE_BYTES);
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    b ^= 1;
-  }
-
-  // partial tile -> part[s] ([N, K] row-major).  32x32 output map: col = lane & 31,
-  // row = 4 (lane >> 5) + (r & 3) + 8 (r >> 2); 16x16: col = lane & 15, row = 4 (lane >> 4) + r
-  float *P = part + s * N * K;
-#pragma unroll
-  for (int j = 0; j < FT; ++j) {
-    const int64_t col = k0 + wn * 64 + j * (M16 ? 16 : 32) + (lane & (M16 ? 15 : 31));
-    if (col >= K) continue;
-#pragma unroll
-    for (int i = 0; i < FT; ++i) {
-#pragma unroll
-      for (int r = 0; r < (M16 ? 4 : 16); ++r) {
-        const int64_t row = M16 ? n0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r
-                                : n0 + wm * 64 + i * 32 + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2);
-        if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
-      }
-    }
-  }
-}
-
-// Cooperative variant: every element of a chunk is split ONCE per block.
-// Threads 0-127 take G, 128-255 take X; a thread loads 8 consecutive rows x 4
-// columns (8 global float4 loads straight to registers, issued one chunk
-// ahead, under the previous chunk's MFMAs), splits each column's 8 values
-// into three bf16x8 (k = the 8 rows) and writes them with ds_write_b128 into
-// plane images laid out for the MFMA: [column][32 rows] bf16, 64-B rows,
-// chunk c at c ^ ((col >> 2) & 3) (the fc kernel's W-plane image, read
-// conflict-free by 16 consecutive columns).  Then 4 waves (2 x 2, 64 x 64
-// each, 16x16x32) read b128 fragments.  One plane buffer (48 KiB), two
-// barriers per chunk.  Per lane and chunk: 32 splits (vs 64 when each wave
-// splits what it reads) and 24 ds_read_b128 (vs 64 ds_read_b32).
 // 16-B raw buffer load (v# in SGPRs: base and size wave-uniform): offsets at or past `nbytes`
 // return zeros, with no branch and no compare in the kernel
 __device__ __forceinline__ f32x4 buf_load4(const float *base, uint32_t nbytes, int voff, int soff) {
@@ -1184,145 +768,20 @@ __device__ __forceinline__ f32x4 buf_load4(const float *base, uint32_t nbytes, i
 #endif
 }
 
-// BUF: loads through a buffer descriptor over the block's R range (wave-uniform base, per-lane
-// offsets fixed for the whole loop, the chunk/row step as the scalar offset, rows past R out of
-// range = zeros): no per-load 64-bit address arithmetic or bounds compare (the host picks it
-// when the range's byte offsets fit 31 bits)
-template <bool BUF>
-__global__ __launch_bounds__(256, 2) void wgrad_x3c(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
-                                                    int64_t ldg, const float *__restrict__ X, int64_t ldx,
-                                                    float *__restrict__ part, const float *__restrict__ zrow,
-                                                    int64_t nt, int64_t kt, int64_t S, int64_t chunks_per_split) {
-  constexpr int PLANE = WG_T * 32 * 2;  // one plane image: 128 columns x 32 rows x bf16 = 8 KiB
-  constexpr int OPB = 3 * PLANE;        // one operand's three planes
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * OPB];
-
-  // XCD-aware remap (blocks go round-robin to the 8 XCDs): each XCD walks a contiguous range of
-  // (split, tile) ids, so the tiles of one R range run on one XCD and share its rows of G and X
-  // in that XCD's L2 (round-robin spread them over all 8 L2s: 4x the bytes fetched past L2)
-  const int64_t nwg = (int64_t)gridDim.x, xcd = (int64_t)blockIdx.x % 8, q8 = nwg / 8, rr = nwg % 8;
-  const int64_t bid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (int64_t)blockIdx.x / 8;
-  const int64_t tiles = nt * kt;
-  const int64_t s = bid / tiles, tile = bid % tiles;
-  const int64_t n0 = (tile / kt) * WG_T, k0 = (tile % kt) * WG_T;
-  const int64_t nchunks = (R + 31) / 32;
-  const int64_t c0 = s * chunks_per_split;
-  const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // load/split task: operand (G or X; waves 0-1 / 2-3, so wave-uniform), 4 columns cg*4 .. +3,
-  // rows rg*8 .. +7 of the chunk
-  const int op = __builtin_amdgcn_readfirstlane(tid >> 7), cg = tid & 31, rg = (tid >> 5) & 3;
-  const float *base;
-  int64_t ld, col0;
-  const int64_t colb = op ? k0 : n0;
-  {
-    const int64_t lim = op ? K : N;
-    col0 = colb + cg * 4;
-    col0 = col0 < lim ? col0 : lim - 4;  // N, K multiples of 4: columns past the edge are never stored
-    base = (op ? X : G) + col0;
-    ld = op ? ldx : ldg;
-  }
-  // BUF: descriptor from row c0 * 32, column colb of the operand
-  const float *sbase = (op ? X : G) + c0 * 32 * ld + colb;
-  const int64_t left = (R - c0 * 32) * ld * 4;
-  const uint32_t nbytes = (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff);
-  const int voff = (int)((col0 - colb) * 4 + rg * 8 * ld * 4);
-  unsigned char *img = smem + op * OPB;
-  f32x4 raw[8];
-  auto load = [&](int64_t c) {  // rows past R read zeros: no branch, every load stays in flight
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if constexpr (BUF) {
-        raw[e] = buf_load4(sbase, nbytes, voff, (int)(((c - c0) * 32 + e) * ld * 4));
-      } else {
-        const int64_t r = c * 32 + rg * 8 + e;
-        raw[e] = *reinterpret_cast<const f32x4 *>(r < R ? base + r * ld : zrow + cg * 4);
-      }
-    }
-  };
-  auto split_store = [&]() {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {  // column cg*4 + q: its 8 rows -> three bf16x8
-      const Split3 t = split3(f32x4{raw[0][q], raw[1][q], raw[2][q], raw[3][q]},
-                              f32x4{raw[4][q], raw[5][q], raw[6][q], raw[7][q]});
-      const int col = cg * 4 + q;
-      unsigned char *dst = img + col * 64 + swzW(col, rg) * 16;
-      *reinterpret_cast<bf16x8 *>(dst) = t.h;
-      *reinterpret_cast<bf16x8 *>(dst + PLANE) = t.m;
-      *reinterpret_cast<bf16x8 *>(dst + 2 * PLANE) = t.l;
-    }
-  };
-
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fg = lane >> 4;
-  f32x4 accH[4][4], accL[4][4];
-  const f32x4 zero = {};
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) accH[i][j] = accL[i][j] = zero;
-  auto frag = [&](const unsigned char *im, int col, bf16x8 (&f)[3]) {
-#pragma unroll
-    for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8 *>(im + p * PLANE + col * 64 + swzW(col, fg) * 16);
-  };
-
-  if (c0 < c1) load(c0);
-  for (int64_t c = c0; c < c1; ++c) {
-    split_store();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // planes of chunk c visible
-    asm volatile("" ::: "memory");
-    if (c + 1 < c1) load(c + 1);   // in flight under this chunk's MFMAs
-    bf16x8 bv[4][3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) frag(smem + OPB, wn * 64 + j * 16 + fr, bv[j]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf16x8 av[3];
-      frag(smem, wm * 64 + i * 16 + fr, av);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], bv[j][0], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][1], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][2], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][0], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][1], accL[i][j], 0, 0, 0);
-        accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][0], accH[i][j], 0, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's fragment reads of chunk c done before the next planes
-    asm volatile("" ::: "memory");
-  }
-
-  float *P = part + s * N * K;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t col = k0 + wn * 64 + j * 16 + fr;
-    if (col >= K) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = n0 + wm * 64 + i * 16 + 4 * fg + r;
-        if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
-      }
-  }
-}
-
-// Wide, split-ahead variant of wgrad_x3c (lpg_fc_x3_set_variant(104); the default): a 256 (n) x
-// 128 (k) output tile per 512-thread block (8 waves of 64 x 64, 2 x 2 waves... 4 x 2), one block
-// per CU, and TWO plane buffers (2 x 72 KiB).  wgrad_x3c splits a chunk, barriers, then
-// multiplies: both waves of a SIMD are in the same phase, so the split VALU and the MFMAs never
-// overlap.  Here chunk c + 1 is split into the other buffer in the same iteration as chunk c's
+// The weight-gradient kernel: each thread loads 8 consecutive rows x 4 columns of G or X (float4
+// per row through a buffer descriptor over the block's R range: rows past R read zeros, no
+// branch), splits each column's 8 values into three bf16x8 (k = the 8 rows) and writes them with
+// ds_write_b128 into plane images laid out for the MFMA ([column][32 rows] bf16, 64-B rows, chunk
+// c at c ^ ((col >> 2) & 3): the fc kernel's W-plane image, read conflict-free by 16 consecutive
+// columns); 8 waves (4 x 2, 64 x 64 each, 16x16x32) read b128 fragments.  A 256 (n) x 128 (k)
+// output tile per 512-thread block, one block per CU, and TWO plane buffers (2 x 72 KiB).  A
+// split-then-multiply form (round 1's cooperative kernel) keeps both waves of a SIMD in the same
+// phase, so the split VALU and the MFMAs never overlap.  Here chunk c + 1 is split into the other buffer in the same iteration as chunk c's
 // MFMAs (the loop is unrolled by two so the buffers are compile-time distinct and the scheduler
 // may interleave them), its global loads issued one iteration earlier; one barrier per chunk.
 // Each G element is split once per 128 k-columns and each X element once per 256 n-columns
-// (wgrad_x3c: once per 128 each): 1.37 split VALU per MFMA instead of 1.83.  Loader tasks: waves
+// (128 x 128 tiles: once per 128 each): 1.37 split VALU per MFMA instead of 1.83.  Loader tasks: waves
 // 0-3 take G (64 column groups x 4 row groups), waves 4-5 X (32 x 4), waves 6-7 only multiply.
-// Same chunk ranges (the host passes wgrad_x3c's split count) and the same six products per output
-// in the same order: bitwise wgrad_x3c's partials.
 template <bool SCHED>
 __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
                                                     int64_t ldg, const float *__restrict__ X, int64_t ldx,
@@ -1463,133 +922,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
   }
 }
 
-// Producer/consumer variant of wgrad_x3c: 8 waves, one block per CU.  Waves
-// 0-3 multiply (wgrad_x3c's 2 x 2 wave tiles of 64 x 64); waves 4-7 load and
-// split (wgrad_x3c's tasks) the NEXT chunk into the other of two plane buffers
-// (2 x 48 KiB).  Every SIMD then holds one multiplying and one splitting wave
-// (SIMD partners are waves w and w + 4): the split VALU issues under the
-// partner's MFMAs instead of in a phase of its own, and one barrier per chunk
-// separates the buffers.  Each producer's global loads for the next chunk
-// are in flight across the barrier.  Same products in the same order as wgrad_x3c: bitwise the same
-// partials.
-__global__ __launch_bounds__(512, 1) void wgrad_x3p(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
-                                                    int64_t ldg, const float *__restrict__ X, int64_t ldx,
-                                                    float *__restrict__ part, const float *__restrict__ zrow,
-                                                    int64_t nt, int64_t kt, int64_t chunks_per_split) {
-  constexpr int PLANE = WG_T * 32 * 2;
-  constexpr int OPB = 3 * PLANE;
-  constexpr int BUF = 2 * OPB;  // G planes, then X planes: 48 KiB
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
-
-  const int64_t nwg = (int64_t)gridDim.x, xcd = (int64_t)blockIdx.x % 8, q8 = nwg / 8, rr = nwg % 8;
-  const int64_t bid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (int64_t)blockIdx.x / 8;
-  const int64_t tiles = nt * kt;
-  const int64_t s = bid / tiles, tile = bid % tiles;
-  const int64_t n0 = (tile / kt) * WG_T, k0 = (tile % kt) * WG_T;
-  const int64_t nchunks = (R + 31) / 32;
-  const int64_t c0 = s * chunks_per_split;
-  const int64_t c1 = c0 + chunks_per_split < nchunks ? c0 + chunks_per_split : nchunks;
-  const int T = (int)(c1 - c0);  // >= 1 (the host sizes the splits so)
-
-  const int tid = threadIdx.x, wave = tid >> 6;
-  if (wave >= 4) {  // ---- producers
-    const int pt = tid - 256;
-    const int op = pt >> 7, cg = pt & 31, rg = (pt >> 5) & 3;
-    const int64_t lim = op ? K : N;
-    int64_t col0 = (op ? k0 : n0) + cg * 4;
-    col0 = col0 < lim ? col0 : lim - 4;  // N, K multiples of 4: columns past the edge are never stored
-    const float *base = (op ? X : G) + col0;
-    const int64_t ld = op ? ldx : ldg;
-    f32x4 raw[8];
-    auto load = [&](int64_t c) {  // rows past R read the zero row (no branch)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int64_t r = c * 32 + rg * 8 + e;
-        raw[e] = *reinterpret_cast<const f32x4 *>(r < R ? base + r * ld : zrow + cg * 4);
-      }
-    };
-    // iteration t: chunk t into buffer t & 1 (the consumers multiply chunk t - 1 meanwhile), then
-    // the loads of chunk t + 1 (the last iteration re-reads chunk T - 1, unused), in flight under
-    // the next iteration's barrier wait
-    load(c0);
-    for (int t = 0; t <= T; ++t) {
-      if (t < T) {
-        unsigned char *img = smem + (t & 1) * BUF + op * OPB;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const Split3 sp = split3(f32x4{raw[0][q], raw[1][q], raw[2][q], raw[3][q]},
-                                   f32x4{raw[4][q], raw[5][q], raw[6][q], raw[7][q]});
-          const int col = cg * 4 + q;
-          unsigned char *dst = img + col * 64 + swzW(col, rg) * 16;
-          *reinterpret_cast<bf16x8 *>(dst) = sp.h;
-          *reinterpret_cast<bf16x8 *>(dst + PLANE) = sp.m;
-          *reinterpret_cast<bf16x8 *>(dst + 2 * PLANE) = sp.l;
-        }
-        load(c0 + (t + 1 < T ? t + 1 : T - 1));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    return;
-  }
-
-  // ---- consumers
-  const int lane = tid & 63, wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fg = lane >> 4;
-  f32x4 accH[4][4], accL[4][4];
-  const f32x4 zero = {};
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) accH[i][j] = accL[i][j] = zero;
-  auto frag = [&](const unsigned char *im, int col, bf16x8 (&f)[3]) {
-#pragma unroll
-    for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8 *>(im + p * PLANE + col * 64 + swzW(col, fg) * 16);
-  };
-  auto multiply = [&](int b) {
-    const unsigned char *buf = smem + b * BUF;
-    bf16x8 bv[4][3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) frag(buf + OPB, wn * 64 + j * 16 + fr, bv[j]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf16x8 av[3];
-      frag(buf, wm * 64 + i * 16 + fr, av);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], bv[j][0], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][1], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][2], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[j][0], accL[i][j], 0, 0, 0);
-        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][1], accL[i][j], 0, 0, 0);
-        accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][0], accH[i][j], 0, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  // the producers' barrier sequence: T + 1 barriers
-  for (int t = 0; t <= T; ++t) {
-    if (t >= 1) multiply((t - 1) & 1);  // chunk t - 1
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-
-  float *P = part + s * N * K;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t col = k0 + wn * 64 + j * 16 + fr;
-    if (col >= K) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = n0 + wm * 64 + i * 16 + 4 * fg + r;
-        if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
-      }
-  }
-}
-
 // dW[n, k] = sum_s part[s][n, k], s ascending (fixed order), float4 per thread
 __global__ __launch_bounds__(256) void wgrad_fold(int64_t N, int64_t K, int64_t S, const float *__restrict__ part,
                                                   float *__restrict__ dW, int64_t lddw) {
@@ -1626,10 +958,11 @@ int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
   return S < 1 ? 1 : S;
 }
 
-int g_x3_variant = 0;
-// lpg_fc_x3_set_variant(100 + v): wgrad kernel (0 = 32x32x16, 1 = 16x16x32, 2 = cooperative,
-// 3 = producer/consumer)
-int g_wgrad_m16 = 5;
+// FC kernel choice, per call in flags bits 8-11 (LPG_FC_KERNEL(k), include/lpgnn.h): 0 = fc_x3_wide
+// <4,2,8,2> when wide_ok (else 1), 1 = fc_fwd_x3_16 <4,1,2,8>.  Same MFMA shape, k order and product
+// sequence per output: the same C, bit for bit.  (tools/experiments/exp_wide.py at the c2 shapes:
+// 207-221 TF/s for the wide form, +3-6 % over fc_fwd_x3_16.)
+constexpr int kX3Kernels = 1;
 
 }  // namespace
 }  // namespace lpg
@@ -1665,7 +998,7 @@ static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int
                   (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
               "lpg_fc_x3_f32: A rows must be 16-byte aligned (lda multiple of 4), W planes 16-byte aligned "
               "(ldw and plane stride multiples of 8)");
-  LPG_REQUIRE((flags & ~3) == 0, "lpg_fc_x3_f32: unknown flags 0x%x", flags);
+  LPG_REQUIRE((flags & ~0xf03) == 0 && ((flags >> 8) & 15) <= kX3Kernels, "lpg_fc_x3_f32: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_x3_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
   *out = X3Args{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, ps1, ps2, C, ldc, 0, 0, seed, 0u, 1.f,
                 (flags >> 1) & 1};
@@ -1686,36 +1019,8 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
   if (st != LPG_OK) return st;
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
-  switch (g_x3_variant) {
-    case 1: return launch_x3<4, 2, 2, 2>(a, relu, s);  // 256 x 128, 8 waves
-    case 2: return launch_x3<2, 4, 2, 2>(a, relu, s);  // 128 x 256, 8 waves
-    case 3: return launch_x3<2, 2, 2, 2, true>(a, relu, s);  // 128 x 128, software-pipelined
-    case 4: return launch_x3<4, 2, 2, 2, true>(a, relu, s);  // 256 x 128, software-pipelined
-    case 5: return launch_x3_16<2, 2, 4, 4>(a, relu, s);  // 128 x 128, 16x16x32 MFMA
-    case 6: return launch_x3_16<4, 2, 4, 4>(a, relu, s);  // 256 x 128, 16x16x32 MFMA
-    case 7: return launch_x3_16<2, 2, 4, 2>(a, relu, s);  // 128 x 64, 16x16x32 MFMA
-    case 8: return launch_x3<2, 2, 2, 2>(a, relu, s);  // 128 x 128, 4 waves
-    case 9: return launch_x3_16<8, 1, 2, 8>(a, relu, s);   // 256 x 128, 8 waves of 32 x 128 (A split once)
-    case 10: return launch_x3_16<4, 1, 2, 8>(a, relu, s);  // 128 x 128, 4 waves of 32 x 128
-    case 11:  // variant 10 with the n-tile-pair XCD map (N = 1024: 8 n-tiles)
-      a.xmap = (a.N + 127) / 128 == 8;
-      return launch_x3_16<4, 1, 2, 8>(a, relu, s);
-    case 12: if (wide_ok(a, 128, 256)) return launch_x3_wide<8, 1, 16, 2>(a, relu, s);  // 128 x 256, 8 waves
-      break;
-    case 13: if (wide_ok(a, 128, 128)) return launch_x3_wide<8, 1, 8, 4>(a, relu, s);  // 128 x 128, 8 waves, 2/CU
-      break;
-    case 14: if (wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);  // 128 x 128, 4 waves of 32 x 128
-      break;
-    case 15: if (wide_ok(a, 256, 128)) return launch_x3_wide<8, 2, 8, 2>(a, relu, s);  // 256 x 128, 8 waves of 32 x 128
-      break;
-    case 16: if (wide_ok(a, 256, 128)) return launch_x3_wide<16, 1, 8, 4>(a, relu, s);  // 256 x 128, 16 waves
-      break;
-    case 99: return launch_x3_16<4, 2, 4, 4, true>(a, relu, s);  // timing probe: no A split (WRONG results)
-    default:  // = 14 (tools/exp_wide.py at the c2 shapes: 207-221 TF/s, +3-6 % over fc_fwd_x3_16 = variant 10)
-      if (wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);
-      break;
-  }
-  return launch_x3_16<4, 1, 2, 8>(a, relu, s);  // a wide variant that cannot take these operands
+  if (((flags >> 8) & 15) == 0 && wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);
+  return launch_x3_16<4, 1, 2, 8>(a, relu, s);
 }
 
 extern "C" int64_t lpg_fc_x3_heads_workspace_bytes(int64_t M, int64_t N) {
@@ -1735,14 +1040,6 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   LPG_REQUIRE(hn >= 1 && hn <= 4, "lpg_fc_x3_heads_f32: %d heads outputs not in [1, 4]", (int)hn);
   LPG_REQUIRE(hw && ldhw >= N && logits && ldl >= hn, "lpg_fc_x3_heads_f32: bad head weight / logits");
   LPG_REQUIRE(workspace && aligned16(workspace), "lpg_fc_x3_heads_f32: workspace missing or not 16-byte aligned");
-  // the heads epilogue lives in the 16x16x32 kernel <4,1,2,8> (variants 0, 10, 11); its C equals
-  // lpg_fc_x3_f32's bit for bit under every 16x16x32 variant (one MFMA shape, one k order), not
-  // under the 32x32x16 ones: those report "unsupported" and the caller runs FC + a separate Linear
-  if (g_x3_variant == 1 || g_x3_variant == 2 || g_x3_variant == 3 || g_x3_variant == 4 || g_x3_variant == 8 ||
-      g_x3_variant == 99) {
-    set_error("lpg_fc_x3_heads_f32: x3 variant %d (32x32x16 MFMA / probe) has no fused heads", (int)g_x3_variant);
-    return LPG_ERR_UNSUPPORTED;
-  }
   X3Args a;
   const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
                                 dropout_p, seed, &a);
@@ -1751,37 +1048,19 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   a.ldhw = ldhw;
   a.hn = hn;
   a.hpart = reinterpret_cast<float *>(workspace);
-  a.xmap = g_x3_variant == 11 && (N + 127) / 128 == 8;
   hipStream_t s = as_stream(stream);
-  // one partial per (BN-column tile, row): N / 128 for fc_fwd_x3_16, N / 256 for the 256-wide strips
-  int64_t bn = 128;
+  // one partial per (128-column tile, row); fc_x3_wide carries three head slots, so hn = 4 (and the
+  // per-call alternative) takes fc_fwd_x3_16 -- the same C, bit for bit
   lpg_status r;
-  const bool wide_heads = hn <= 3;  // fc_x3_wide carries three head slots
-  if (wide_heads && g_x3_variant == 12 && wide_ok(a, 128, 256)) {
-    bn = 256;
-    r = launch_x3_wide<8, 1, 16, 2, true>(a, flags & 1, s);
-  } else if (wide_heads && g_x3_variant == 13 && wide_ok(a, 128, 128)) {
-    r = launch_x3_wide<8, 1, 8, 4, true>(a, flags & 1, s);
-  } else if (wide_heads && (g_x3_variant == 0 || g_x3_variant == 14) && wide_ok(a, 128, 128)) {
+  if (hn <= 3 && ((flags >> 8) & 15) == 0 && wide_ok(a, 128, 128))
     r = launch_x3_wide<4, 2, 8, 2, true>(a, flags & 1, s);
-  } else {
-    r = launch_x3_16<4, 1, 2, 8, false, true>(a, flags & 1, s);  // 32 x 128 wave tiles: N / 128 partials
-  }
+  else
+    r = launch_x3_16<4, 1, 2, 8, true>(a, flags & 1, s);
   if (r != LPG_OK) return r;
-  const int64_t nparts = (N + bn - 1) / bn;
+  const int64_t nparts = (N + 127) / 128;
   hipLaunchKernelGGL(heads_fold, dim3((unsigned)((M * hn + 255) / 256)), dim3(256), 0, s, M, nparts, hn,
                      a.hpart, hb, logits, ldl);
   LPG_HIP(hipGetLastError());
-  return LPG_OK;
-}
-
-extern "C" lpg_status lpg_fc_x3_set_variant(int32_t v) {
-  if (v >= 100 && v <= 105) {
-    g_wgrad_m16 = v - 100;
-    return LPG_OK;
-  }
-  LPG_REQUIRE((v >= 0 && v <= 16) || v == 99, "lpg_fc_x3_set_variant: variant %d not in [0, 16]", v);
-  g_x3_variant = v;
   return LPG_OK;
 }
 
@@ -1803,43 +1082,22 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   LPG_REQUIRE(N % 4 == 0 && K % 4 == 0 && ldg >= N && ldx >= K && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) &&
                   aligned16(X) && aligned16(workspace),
               "lpg_wgrad_x3_f32: N, K and leading dimensions must be multiples of 4 floats, buffers 16-byte aligned");
-  const int64_t nt = (N + WG_T - 1) / WG_T, kt = (K + WG_T - 1) / WG_T;
   const int64_t S = wgrad_splits(R, N, K);
   const int64_t nchunks = (R + 31) / 32;
   const int64_t cps = (nchunks + S - 1) / S;
   const int64_t S_used = (nchunks + cps - 1) / cps;
-  const int64_t nblk = S_used * nt * kt;
-  LPG_REQUIRE(nblk < (int64_t)1 << 31, "lpg_wgrad_x3_f32: grid too large");
   float *part = reinterpret_cast<float *>(workspace);
-  float *zrow = part + S * N * K;  // 128 zero floats after the partials (lpg_wgrad_x3_workspace_bytes)
   hipStream_t st = as_stream(stream);
-  const bool wide = g_wgrad_m16 >= 4 && (cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31);
-  if (!wide) LPG_HIP(hipMemsetAsync(zrow, 0, 512, st));  // the zero row only the older kernels read
-  if (wide) {
-    const int64_t ntw = (N + 255) / 256, ktw = (K + 127) / 128;  // 256 x 128 tiles, wgrad_x3c's split count
-    const int64_t nbw = S_used * ntw * ktw;
-    LPG_REQUIRE(nbw < (int64_t)1 << 31, "lpg_wgrad_x3_f32: grid too large");
-    if (g_wgrad_m16 == 5)
-      hipLaunchKernelGGL(wgrad_x3w<true>, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw,
-                         ktw, cps);
-    else
-      hipLaunchKernelGGL(wgrad_x3w<false>, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw,
-                         ktw, cps);
-  } else if (g_wgrad_m16 == 3)
-    hipLaunchKernelGGL(wgrad_x3p, dim3((unsigned)nblk), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, zrow, nt, kt,
-                       cps);
-  else if (g_wgrad_m16 >= 2 && (cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31))
-    hipLaunchKernelGGL(wgrad_x3c<true>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
-                       nt, kt, S_used, cps);
-  else if (g_wgrad_m16 >= 2)
-    hipLaunchKernelGGL(wgrad_x3c<false>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part,
-                       zrow, nt, kt, S_used, cps);
-  else if (g_wgrad_m16)
-    hipLaunchKernelGGL(wgrad_x3<true>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
-                       nt, kt, S_used, cps);
-  else
-    hipLaunchKernelGGL(wgrad_x3<false>, dim3((unsigned)nblk), dim3(256), 0, st, R, N, K, G, ldg, X, ldx, part, zrow,
-                       nt, kt, S_used, cps);
+  // one R range's byte offsets must fit the buffer descriptors' 31 bits (a range of R / S rows: at
+  // S <= 64 that is R * ld beyond 3e10 elements, 137 GB per operand)
+  LPG_REQUIRE((cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31),
+              "lpg_wgrad_x3_f32: an R range of %lld rows x %lld floats exceeds 2 GiB", (long long)(cps * 32),
+              (long long)(ldg > ldx ? ldg : ldx));
+  const int64_t ntw = (N + 255) / 256, ktw = (K + 127) / 128;  // 256 x 128 tiles
+  const int64_t nbw = S_used * ntw * ktw;
+  LPG_REQUIRE(nbw < (int64_t)1 << 31, "lpg_wgrad_x3_f32: grid too large");
+  hipLaunchKernelGGL(wgrad_x3w<true>, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw, ktw,
+                     cps);
   LPG_HIP(hipGetLastError());
   const int64_t n4 = N * (K / 4);
   hipLaunchKernelGGL(wgrad_fold, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, N, K, S_used, part, dW, lddw);

@@ -624,10 +624,18 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
   }
 }
 
-int64_t g_slice_cols = 0;  // lpg_spmm_set_slice; 0 = auto
-int g_depth = 0;           // lpg_spmm_set_depth: edges gathered ahead per wave (0 = auto)
-int g_remb = 1;            // lpg_spmm_set_remainder (fp32 rowwave): chunk remainder gathered together (1) or one
-                           // by one (the bf16 kernel keeps one by one: batched, it measured 7-55 % slower)
+// Tuning is per call (lpg_spmm_*_tuned): slice width and gather depth; every choice gives the same
+// bits.  (The fp32 rowwave kernel gathers a chunk's remainder together; the bf16 kernel keeps one
+// by one: batched, it measured 7-55 % slower.)
+lpg_status check_tuning(int64_t slice_cols, int32_t depth) {
+  LPG_REQUIRE(slice_cols == 0 || slice_cols == 64 || slice_cols == 128 || slice_cols == 256 || slice_cols == 512 ||
+                  slice_cols == 1024,
+              "lpg_spmm_*_tuned: slice_cols must be 0 (auto), 64, 128, 256, 512 or 1024, got %lld",
+              (long long)slice_cols);
+  LPG_REQUIRE(depth == 0 || depth == 8 || depth == 16 || depth == 32, "lpg_spmm_*_tuned: depth %d not in {0, 8, 16, 32}",
+              (int)depth);
+  return LPG_OK;
+}
 
 lpg_status check_csr(const lpg_csr *A) {
   LPG_REQUIRE(A != nullptr, "lpg_spmm: A is NULL");
@@ -654,13 +662,6 @@ lpg_status launch_wide_f32(const lpg_csr *A, const float *X, int64_t ldx, float 
   const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock + hv.blocks * slices;
   LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_f32: grid too large");
   dim3 grid((unsigned)nblk, (unsigned)slices);
-  if (!g_remb) {  // the one-load-at-a-time remainder (A/B knob, lpg_spmm_set_remainder(0))
-    if (F % W == 0)
-      return launch(spmm_f32_rowwave<NV, U, true, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
-                    Y, ldy, F, hv);
-    return launch(spmm_f32_rowwave<NV, U, false, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
-                  Y, ldy, F, hv);
-  }
   if (F % W == 0)
     return launch(spmm_f32_rowwave<NV, U, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
                   Y, ldy, F, hv);
@@ -709,29 +710,11 @@ lpg_status launch_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx, u
 
 using namespace lpg;
 
-extern "C" lpg_status lpg_spmm_set_slice(int64_t cols) {
-  LPG_REQUIRE(cols == 0 || cols == 64 || cols == 128 || cols == 256 || cols == 512 || cols == 1024,
-              "lpg_spmm_set_slice: cols must be 0 (auto), 64, 128, 256, 512 or 1024, got %lld", (long long)cols);
-  g_slice_cols = cols;
-  return LPG_OK;
-}
-
-extern "C" lpg_status lpg_spmm_set_remainder(int32_t batched) {
-  LPG_REQUIRE(batched == 0 || batched == 1, "lpg_spmm_set_remainder: %d not in {0, 1}", batched);
-  g_remb = batched;
-  return LPG_OK;
-}
-
-extern "C" lpg_status lpg_spmm_set_depth(int64_t edges) {
-  LPG_REQUIRE(edges == 0 || edges == 8 || edges == 16 || edges == 32,
-              "lpg_spmm_set_depth: %lld not in {0, 8, 16, 32}", (long long)edges);
-  g_depth = (int)edges;
-  return LPG_OK;
-}
-
 static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
-                                HeavyRows hv, void *stream) {
+                                HeavyRows hv, int64_t slice_cols, int32_t depth, void *stream) {
   lpg_status st = check_csr(A);
+  if (st != LPG_OK) return st;
+  st = check_tuning(slice_cols, depth);
   if (st != LPG_OK) return st;
   LPG_REQUIRE(F >= 0, "lpg_spmm_f32: F < 0");
   LPG_REQUIRE(ldx >= F && ldy >= F, "lpg_spmm_f32: ldx/ldy smaller than F");
@@ -754,7 +737,7 @@ static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, f
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
     return launch(spmm_f32_generic, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
-  int64_t W = g_slice_cols;
+  int64_t W = slice_cols;
   // auto: 256-column slices (one float4 per lane).  Slices run in order
   // (blockIdx.y major), so only a quarter-width source table is being
   // gathered at a time and stays resident in the 256 MiB Infinity Cache;
@@ -766,7 +749,7 @@ static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, f
   // auto depth: 16 edges in flight for rows of >= 16 edges on average (c2 cons<-vars, degree 20: 0.947
   // of the edge-gather roofline vs 0.913 at 8), else 8 (vars<-cons, degree 10: 0.938 vs 0.915; a
   // skewed LP, whose light rows average 5 edges once its heavy rows are split off: 0.98 vs 0.89)
-  const int U = g_depth != 0 ? g_depth : (hv.blocks == 0 && A->nnz >= 16 * A->n_rows) ? 16 : 8;
+  const int U = depth != 0 ? depth : (hv.blocks == 0 && A->nnz >= 16 * A->n_rows) ? 16 : 8;
   if ((W == 64 || W == 128) && hv.blocks == 0) {  // narrow slices (no heavy-row split in this form)
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock), (unsigned)((F + W - 1) / W));
     if (W == 128)
@@ -790,7 +773,17 @@ static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, f
 
 extern "C" lpg_status lpg_spmm_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
                                    int64_t F, void *stream) {
-  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, stream);
+  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, 0, 0, stream);
+}
+
+extern "C" lpg_status lpg_spmm_f32_tuned(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                                         int64_t F, const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
+                                         int64_t slice_cols, int32_t depth, void *stream) {
+  LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_f32_tuned: negative n_heavy / thresh");
+  LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_f32_tuned: heavy_rows is NULL");
+  LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_f32_tuned: more heavy rows than rows");
+  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1},
+                       slice_cols, depth, stream);
 }
 
 extern "C" lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
@@ -799,12 +792,15 @@ extern "C" lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64
   LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_f32_heavy: negative n_heavy / thresh");
   LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_f32_heavy: heavy_rows is NULL");
   LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_f32_heavy: more heavy rows than rows");
-  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1}, stream);
+  return spmm_f32_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1}, 0, 0,
+                       stream);
 }
 
 static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
-                                 int64_t F, HeavyRows hv, void *stream) {
+                                 int64_t F, HeavyRows hv, int64_t slice_cols, int32_t depth, void *stream) {
   lpg_status st = check_csr(A);
+  if (st != LPG_OK) return st;
+  st = check_tuning(slice_cols, depth);
   if (st != LPG_OK) return st;
   LPG_REQUIRE(F >= 0, "lpg_spmm_bf16: F < 0");
   LPG_REQUIRE(ldx >= F && ldy >= F, "lpg_spmm_bf16: ldx/ldy smaller than F");
@@ -825,17 +821,17 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
     return launch(spmm_bf16_generic, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
-  // slice width: lpg_spmm_set_slice (256 = spmm_bf16_rowslim, 512 / 1024 / 2048 = rowwave with 1 / 2 / 4
+  // slice width: slice_cols (256 = spmm_bf16_rowslim, 512 / 1024 / 2048 = rowwave with 1 / 2 / 4
   // 16-B pieces per lane); auto = 256 (c5: 0.92 / 0.97 of the edge-gather roofline vs 0.88 / 0.91 for
   // whole 2048-column rows, profiles/r02_kbench_spmm16.log); with heavy rows split off, 512-column slices
 // (spmm_bf16_rowwave<1, 8> + heavy units: a skewed LP's mostly one-edge rows want few, wide wave tasks)
   if (hv.blocks > 0) return launch_bf16_heavy(A, X, ldx, Y, ldy, F, hv, s);
-  const int64_t W = g_slice_cols == 0 ? 256 : g_slice_cols;
+  const int64_t W = slice_cols == 0 ? 256 : slice_cols;
   if (W <= 256) {
     const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
     LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_bf16: grid too large");
     dim3 grid((unsigned)nblk, (unsigned)((F + 255) / 256));
-    const int U = g_depth != 0 ? g_depth : A->nnz >= 16 * A->n_rows ? 16 : 8;
+    const int U = depth != 0 ? depth : A->nnz >= 16 * A->n_rows ? 16 : 8;
     if (U == 16) return launch(spmm_bf16_rowslim<16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
     return launch(spmm_bf16_rowslim<8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
@@ -846,7 +842,17 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
 
 extern "C" lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,
                                     int64_t ldy, int64_t F, void *stream) {
-  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, stream);
+  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, 0, 0, stream);
+}
+
+extern "C" lpg_status lpg_spmm_bf16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
+                                          int64_t F, const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
+                                          int64_t slice_cols, int32_t depth, void *stream) {
+  LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_bf16_tuned: negative n_heavy / thresh");
+  LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_bf16_tuned: heavy_rows is NULL");
+  LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_bf16_tuned: more heavy rows than rows");
+  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1},
+                        slice_cols, depth, stream);
 }
 
 extern "C" lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,
@@ -855,6 +861,6 @@ extern "C" lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, i
   LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_bf16_heavy: negative n_heavy / thresh");
   LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_bf16_heavy: heavy_rows is NULL");
   LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_bf16_heavy: more heavy rows than rows");
-  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1},
+  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1}, 0, 0,
                         stream);
 }

@@ -29,13 +29,10 @@ HEADER_SYMBOLS = (
     "lpg_spmm_f32_heavy",
     "lpg_spmm_bf16",
     "lpg_spmm_bf16_heavy",
-    "lpg_spmm_set_slice",
-    "lpg_spmm_set_depth",
-    "lpg_spmm_set_remainder",
+    "lpg_spmm_f32_tuned",
+    "lpg_spmm_bf16_tuned",
     "lpg_fc_f32",
-    "lpg_fc_set_variant",
     "lpg_fc_bf16",
-    "lpg_fc_bf16_set_variant",
     "lpg_fc_bf16_relu_bwd",
     "lpg_colsum_bf16",
     "lpg_transpose_bf16",
@@ -43,7 +40,6 @@ HEADER_SYMBOLS = (
     "lpg_wgrad_bf16",
     "lpg_split3_f32",
     "lpg_fc_x3_f32",
-    "lpg_fc_x3_set_variant",
     "lpg_fc_x3_heads_workspace_bytes",
     "lpg_fc_x3_heads_f32",
     "lpg_wgrad_x3_workspace_bytes",
@@ -111,12 +107,11 @@ def lib() -> ctypes.CDLL:
     L.lpg_spmm_bf16.restype = c_i32
     L.lpg_spmm_bf16_heavy.argtypes = L.lpg_spmm_f32_heavy.argtypes
     L.lpg_spmm_bf16_heavy.restype = c_i32
-    L.lpg_spmm_set_slice.argtypes = [c_i64]
-    L.lpg_spmm_set_slice.restype = c_i32
-    L.lpg_spmm_set_depth.argtypes = [c_i64]
-    L.lpg_spmm_set_remainder.argtypes = [c_i32]
-    L.lpg_spmm_set_remainder.restype = c_i32
-    L.lpg_spmm_set_depth.restype = c_i32
+    L.lpg_spmm_f32_tuned.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64,
+                                     c_i32, c_p]
+    L.lpg_spmm_f32_tuned.restype = c_i32
+    L.lpg_spmm_bf16_tuned.argtypes = L.lpg_spmm_f32_tuned.argtypes
+    L.lpg_spmm_bf16_tuned.restype = c_i32
     L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
                              c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_p]
     L.lpg_fc_f32.restype = c_i32
@@ -141,7 +136,6 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_x3_heads_workspace_bytes.restype = c_i64
     L.lpg_fc_x3_heads_f32.argtypes = L.lpg_fc_x3_f32.argtypes[:-1] + [c_i32, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p]
     L.lpg_fc_x3_heads_f32.restype = c_i32
-    L.lpg_fc_x3_set_variant.argtypes = [c_i32]
     L.lpg_wgrad_x3_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
     L.lpg_wgrad_x3_workspace_bytes.restype = c_i64
     L.lpg_wgrad_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p]
@@ -153,10 +147,7 @@ def lib() -> ctypes.CDLL:
     L.lpg_weighted_ce_bwd_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, ctypes.c_float, c_p, c_i64,
                                           c_p]
     L.lpg_weighted_ce_bwd_f32.restype = c_i32
-    L.lpg_fc_x3_set_variant.restype = c_i32
     L.lpg_fc_bf16.restype = c_i32
-    L.lpg_fc_bf16_set_variant.argtypes = [c_i32]
-    L.lpg_fc_bf16_set_variant.restype = c_i32
     L.lpg_wgrad_bf16_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
     L.lpg_wgrad_bf16_workspace_bytes.restype = c_i64
     L.lpg_wgrad_bf16.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p]
@@ -186,8 +177,6 @@ def lib() -> ctypes.CDLL:
     L.lpg_heads_relu_bwd_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, ctypes.c_float, c_p, c_i64,
                                          c_p, c_p, c_p, c_p, c_p]
     L.lpg_heads_relu_bwd_f32.restype = c_i32
-    L.lpg_fc_set_variant.argtypes = [c_i32]
-    L.lpg_fc_set_variant.restype = c_i32
     L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_i64, ctypes.c_float, c_p, c_i64, c_p]
     L.lpg_knowledge_f32.restype = c_i32
     L.lpg_scan_i64_workspace_bytes.argtypes = [c_i64]
@@ -204,18 +193,16 @@ def lib() -> ctypes.CDLL:
     for nm in ("lpg_scan_i64", "lpg_sample_count", "lpg_sample_fill", "lpg_sample_dedupe", "lpg_sample_assign",
                "lpg_sample_local_ids", "lpg_induced_count", "lpg_induced_fill", "lpg_sample_reset"):
         getattr(L, nm).restype = c_i32
-    # tuning knobs for A/B runs (bench.py, tools/): the x3 FC tile variant and the weight-gradient kernel
-    for env, off in (("LPGNN_X3_VARIANT", 0), ("LPGNN_WGRAD_VARIANT", 100)):
-        if os.environ.get(env):
-            if L.lpg_fc_x3_set_variant(int(os.environ[env]) + off) != 0:
-                raise RuntimeError(f"{env}={os.environ[env]}: {L.lpg_last_error().decode()}")
-    # ... and the bf16 (c5) FC tile / weight-gradient kernel
-    for env, off in (("LPGNN_BF16_VARIANT", 0), ("LPGNN_WGRAD_BF16_VARIANT", 100)):
-        if os.environ.get(env):
-            if L.lpg_fc_bf16_set_variant(int(os.environ[env]) + off) != 0:
-                raise RuntimeError(f"{env}={os.environ[env]}: {L.lpg_last_error().decode()}")
     _lib = L
     return L
+
+
+FC_RELU, FC_ACCUMULATE = 1, 2
+
+
+def fc_kernel(k: int) -> int:
+    """LPG_FC_KERNEL(k): the per-call kernel choice in an FC entry's flags (include/lpgnn.h)."""
+    return int(k) << 8
 
 
 def check(status: int, what: str) -> None:

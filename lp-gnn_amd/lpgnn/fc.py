@@ -57,26 +57,27 @@ _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless th
 
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
-               accumulate: bool = False, arith: str | None = None, heads=None):
+               accumulate: bool = False, arith: str | None = None, heads=None, kernel: int = 0):
     """act(A1 W1^T + A2 W2^T [+ out] + bias) through lpg_fc_f32; with
     ``accumulate`` the caller's ``out`` holds the addend and is overwritten.
     ``arith`` ("fp32" | "x3", default ``ARITH``) picks the tiled kernel's arithmetic.
     ``heads`` = (Wh [<= 4, N], bh or None): also return the logits C Wh^T + bh
     -- fused into the x3 kernel's epilogue (lpg_fc_x3_heads_f32), else the
-    separate Linear on C (the fp32 contract's own kernel)."""
+    separate Linear on C (the fp32 contract's own kernel).  ``kernel``: the x3 entries' per-call
+    kernel choice (LPG_FC_KERNEL, include/lpgnn.h; 0 = by shape; every choice gives the same bits)."""
     if heads is not None:
         M, N = A1.shape[0], W1.shape[0]
         k4 = lambda k: -(-k // 4) * 4
         small = 4 <= k4(A1.shape[1]) and k4(A1.shape[1]) + (0 if A2 is None else k4(A2.shape[1])) <= 16
         if (arith or ARITH) == "x3" and not small and N > 32 and heads[0].shape[0] <= 4:
-            return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, heads)
-        C = _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith)
+            return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, heads, kernel)
+        C = _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel)
         return C, _fc_forward(C, heads[0], None, None, heads[1], False, arith=arith)
-    return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith)
+    return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel)
 
 
 def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, accumulate=False, arith=None,
-                heads=None):
+                heads=None, kernel=0):
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -103,7 +104,8 @@ def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, acc
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0)
     if (arith or ARITH) == "x3" and not small and N > 32:
-        return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, heads=heads)
+        return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags | _lib.fc_kernel(kernel), dropout_p, seed, relu,
+                      heads=heads)
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
         st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
@@ -166,9 +168,6 @@ def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=
                                    None if bh is None else bh.data_ptr(), logits.data_ptr(), logits.stride(0),
                                    ws.data_ptr(), _lib.stream_of(A1))
         TIMER.stop(tok)
-    if st == 3:  # a 32x32x16 x3 variant is selected: no fused heads there -- the FC, then a separate Linear
-        C = _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s, W2s)
-        return C, _fc_forward(C, heads[0], None, None, heads[1], False, arith="x3")
     _lib.check(st, "lpg_fc_x3_heads_f32")
     return C, logits
 
@@ -243,13 +242,14 @@ def _prep_bf16(t: Tensor | None) -> Tensor | None:
 
 def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                     relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
-                    accumulate: bool = False, key: str | None = None, mask=None) -> Tensor:
+                    accumulate: bool = False, key: str | None = None, mask=None, kernel: int = 0) -> Tensor:
     """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16);
     ``accumulate`` adds the bf16 addend held in ``out`` (overwritten).
     ``mask`` = (Y, scale): an input gradient with the previous layer's ReLU/dropout backward
     folded into the store, C = (Y > 0) ? bf16(C * scale) : 0 (lpg_fc_bf16_relu_bwd; no bias /
     ReLU / dropout of its own) -- the bits of this call without ``mask`` followed by
-    relu_bwd_colsum_bf16(C, Y, scale)."""
+    relu_bwd_colsum_bf16(C, Y, scale).  ``kernel``: the per-call kernel choice (LPG_FC_KERNEL,
+    include/lpgnn.h; 0 = by shape, 1 = 128 x 128, 2 = 256 x 256, 3 = pipelined; the same bits)."""
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -265,7 +265,7 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
         C = torch.empty((M, N), dtype=torch.bfloat16, device=A1.device)
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
-    flags = (1 if relu else 0) | (2 if accumulate else 0)
+    flags = (1 if relu else 0) | (2 if accumulate else 0) | _lib.fc_kernel(kernel)
     if mask is not None:
         Y, scale = mask
         if relu or bias is not None or dropout_p > 0:
@@ -273,7 +273,7 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
         if (Y.shape != (M, N) or Y.dtype != torch.bfloat16 or Y.device != A1.device or Y.stride(1) != 1
                 or Y.stride(0) % 8 or Y.data_ptr() % 16 or N % 8 or C.stride(0) % 8 or C.data_ptr() % 16):
             # layouts the folded store does not take: the same bits in two passes
-            C = fc_forward_bf16(A1, W1, A2, W2, None, False, out=out, accumulate=accumulate, key=key)
+            C = fc_forward_bf16(A1, W1, A2, W2, None, False, out=out, accumulate=accumulate, key=key, kernel=kernel)
             return relu_bwd_colsum_bf16(C, Y, scale, False)[0]
         with torch.cuda.device(A1.device):
             tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, key or "lin-bf16-relubwd"))
@@ -325,7 +325,7 @@ def wgrad_bf16(G: Tensor, X: Tensor) -> Tensor:
 
 
 def input_grad_bf16(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | None = None,
-                    out: Tensor | None = None, accumulate: bool = False, mask=None) -> Tensor:
+                    out: Tensor | None = None, accumulate: bool = False, mask=None, kernel: int = 0) -> Tensor:
     """G1 W1 [+ G2 W2] [+ out] in bf16 for Linear weights W [out, in]: the
     c5 input gradient of lin_rel / lin_root on the bf16 FC kernel (lpg_fc_bf16
     with the weights transposed; fp32 accumulation, one bf16 rounding).
@@ -335,7 +335,7 @@ def input_grad_bf16(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor
     G1 = G1.to(torch.bfloat16)
     G2 = None if G2 is None else G2.to(torch.bfloat16)
     return fc_forward_bf16(G1, t(W1), G2, t(W2), None, False, out=out, accumulate=accumulate, key="igrad-bf16",
-                           mask=mask)
+                           mask=mask, kernel=kernel)
 
 
 def relu_dropout_bwd(g: Tensor, y: Tensor, scale: float) -> Tensor:

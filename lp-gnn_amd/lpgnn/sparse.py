@@ -177,8 +177,9 @@ class BipartiteCSR:
 HEAVY_THRESH = int(os.environ.get("LPGNN_SPMM_HEAVY", "1024"))
 
 
-def spmm_forward(adj: CSR, x: torch.Tensor) -> torch.Tensor:
-    """Y = adj @ x on the GPU (no autograd).  fp32 or bf16 storage."""
+def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0) -> torch.Tensor:
+    """Y = adj @ x on the GPU (no autograd).  fp32 or bf16 storage.  ``slice_cols`` / ``depth``: the
+    per-call tuning of lpg_spmm_*_tuned (0 = auto; every choice gives the same bits)."""
     if x.device.type != "cuda" or adj.device != x.device:
         raise RuntimeError(f"lpgnn.spmm: x ({x.device}) and adj ({adj.device}) must be on the same HIP device; "
                            "there is no CPU path")
@@ -189,30 +190,23 @@ def spmm_forward(adj: CSR, x: torch.Tensor) -> torch.Tensor:
     Fd = x.shape[1]
     y = torch.empty((adj.n_rows, Fd), dtype=x.dtype, device=x.device)
     L = _lib.lib()
-    heavy = None
     if x.dtype == torch.float32:
-        fn, name = L.lpg_spmm_f32, "lpg_spmm_f32"
-        if Fd >= 256 and HEAVY_THRESH > 0:
-            heavy = adj.heavy_rows(HEAVY_THRESH)
-            if heavy[1] == 0:
-                heavy = None
+        name = "lpg_spmm_f32_tuned"
     elif x.dtype == torch.bfloat16:
-        fn, name = L.lpg_spmm_bf16, "lpg_spmm_bf16"
-        if Fd >= 256 and HEAVY_THRESH > 0:
-            heavy = adj.heavy_rows(HEAVY_THRESH)
-            if heavy[1] == 0:
-                heavy = None
+        name = "lpg_spmm_bf16_tuned"
     else:
         raise RuntimeError(f"lpgnn.spmm: unsupported dtype {x.dtype}")
+    heavy = None
+    if Fd >= 256 and HEAVY_THRESH > 0:  # degree-aware: rows above the threshold on narrow wave units
+        heavy = adj.heavy_rows(HEAVY_THRESH)
+        if heavy[1] == 0:
+            heavy = None
     with torch.cuda.device(x.device):
         stream = _lib.stream_of(x)
         tok = TIMER.start(("spmm", adj.n_rows, adj.n_cols, Fd, str(x.dtype)))
-        if heavy is None:
-            st = fn(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), Fd, stream)
-        else:  # degree-aware: rows above the threshold on narrow wave units (same per-element order)
-            name = "lpg_spmm_f32_heavy" if x.dtype == torch.float32 else "lpg_spmm_bf16_heavy"
-            st = getattr(L, name)(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(),
-                                  y.stride(0), Fd, heavy[0].data_ptr(), heavy[1], HEAVY_THRESH, stream)
+        st = getattr(L, name)(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), Fd,
+                              None if heavy is None else heavy[0].data_ptr(), 0 if heavy is None else heavy[1],
+                              HEAVY_THRESH if heavy is not None else 0, int(slice_cols), int(depth), stream)
         TIMER.stop(tok)
     _lib.check(st, name)
     return y

@@ -83,10 +83,18 @@ def test_status_and_error_string():
     from lpgnn import _lib
 
     L = _lib.lib()
-    st = L.lpg_spmm_set_slice(300)
+    empty = _lib.LpgCsr(0, 0, 0, None, None, None)  # valid and empty: the tuning check runs, no device work
+    st = L.lpg_spmm_f32_tuned(ctypes.byref(empty), None, 0, None, 0, 0, None, 0, 0, 300, 0, None)
     assert st == 1
-    assert b"slice" in L.lpg_last_error()
-    assert L.lpg_spmm_set_slice(0) == 0
+    assert b"slice_cols" in L.lpg_last_error()
+    assert L.lpg_spmm_f32_tuned(ctypes.byref(empty), None, 0, None, 0, 0, None, 0, 0, 128, 16, None) == 0
+    assert L.lpg_spmm_f32_tuned(ctypes.byref(empty), None, 0, None, 0, 0, None, 0, 0, 0, 7, None) == 1
+    # an FC kernel choice past the entry's range is rejected before any launch (the pointers are
+    # never dereferenced: the flags check precedes every device call)
+    fake = 1 << 20
+    assert L.lpg_fc_bf16(1, 8, 64, fake, 64, fake, 64, 0, None, 0, None, 0, None, fake, 8, _lib.fc_kernel(9), 0.0, 0,
+                         None) == 1
+    assert b"flags" in L.lpg_last_error()
     # NULL CSR -> invalid argument, no device work
     assert L.lpg_spmm_f32(None, None, 0, None, 0, 0, None) == 1
     assert L.lpg_csr_pack_workspace_bytes(-1, 0, 0) == -1
@@ -124,3 +132,19 @@ def test_fc_rejects_unpadded_k_on_the_tiled_path():
     fake = 1 << 20  # 16-byte aligned, never dereferenced: validation fails first
     st = L.lpg_fc_f32(10, 64, 40, fake, 40, fake, 40, 0, None, 0, None, 0, None, fake, 64, 0, 0.0, 0, None)
     assert st == 1 and b"multiples of 32" in L.lpg_last_error()
+
+
+def test_no_shipped_kernel_uses_scratch():
+    """The spill rule: no kernel of ours in the shipped library uses scratch.  A
+    register-spilling bf16 FC tile once gave wrong bits -- hipcc's spill code dropped the last
+    dword of a partially reused accumulator tuple -- so spilling kernels are not shipped at all."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_resources as KR
+    from lpgnn import _lib
+
+    rows = KR.kernels(_lib.LIB_PATH)
+    ours = [(n, s) for n, _, s in rows if KR.is_ours(n)]
+    assert len(ours) > 50, len(ours)
+    assert [n for n, s in ours if s] == []

@@ -43,16 +43,45 @@ def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
     torch.testing.assert_close(got, ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+# per-call kernel choices of lpg_fc_bf16 (LPG_FC_KERNEL, include/lpgnn.h): 1 = 128 x 128,
+# 2 = 256 x 256, 3 = the pipelined transposed-fragment kernel (the default from 4096 rows)
+KERNELS = (1, 2, 3)
+
+
+def _f64_ulp_check(out, A, W, P, b, relu, A2=None, W2=None):
+    """Every output within one bf16 ulp of the fp64 value of the same bf16 operands (one RNE
+    rounding of an fp32-accumulated sum; a wrong register or a stale load is off by far more)."""
+    ref = A.double() @ W.double().t()
+    if A2 is not None:
+        ref = ref + A2.double() @ W2.double().t()
+    if P is not None:
+        ref = ref + P.double()
+    if b is not None:
+        ref = ref + b.double()
+    if relu:
+        ref = ref.clamp_min(0)
+    err = (out.double() - ref).abs()
+    bound = ref.abs() * 2.0 ** -7 + 1e-5
+    bad = (err > bound).nonzero()
+    assert bad.shape[0] == 0, (f"{bad.shape[0]} outputs off by more than one bf16 ulp, first (row, col) "
+                               f"{bad[:6].tolist()}, max err {err.max().item():.3g}")
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("M,N,K,relu,bias", [
     (5000, 1024, 1024, True, True),  # re-associated left2right root part
-    (129, 130, 64, False, True),     # N % 8 != 0: per-element epilogue
+    (129, 130, 64, False, True),     # N % 8 != 0: per-element epilogue, one k-tile
+    (129, 136, 64, False, True),     # one k-tile, LDS-image epilogue
+    (300, 130, 128, False, True),    # two k-tiles, several row tiles
     (4099, 264, 128, True, False),   # ragged 256 x 256 tiles
 ])
-def test_fc_bf16_accumulate(M, N, K, relu, bias, variant):
-    """Accumulate flag: C = bf16(act(A W^T + C + b)) in place; every tile
-    variant gives the same bits, within one bf16 rounding of fp32."""
-    from lpgnn import _lib
+def test_fc_bf16_accumulate(M, N, K, relu, bias, kernel):
+    """Accumulate flag: C = bf16(act(A W^T + C + b)) in place; every kernel gives the bits of the
+    default choice AND each output is within one bf16 ulp of the fp64 result of the same bf16
+    operands.  The second check is the one that caught a miscompiled spilling kernel (a 4-wave,
+    256-accumulator tile whose spill code dropped the last dword of an accumulator tuple: rows
+    4i + 3 of one 16-column fragment were off by O(1)); comparing kernels with each other alone
+    cannot tell which one is wrong."""
     from lpgnn.fc import fc_forward_bf16
 
     g = torch.Generator().manual_seed(M + N + K)
@@ -60,57 +89,40 @@ def test_fc_bf16_accumulate(M, N, K, relu, bias, variant):
     W = (torch.randn(N, K, generator=g) * 0.05).to(BF).to(DEV)
     P = torch.randn(M, N, generator=g).to(BF).to(DEV)
     b = (torch.randn(N, generator=g) * 0.1).to(DEV) if bias else None
-    L = _lib.lib()
     outs = []
-    try:
-        for v in (variant, 0):
-            L.lpg_fc_bf16_set_variant(v)
-            out = P.clone()
-            got = fc_forward_bf16(A, W, None, None, b, relu, out=out, accumulate=True)
-            assert got.data_ptr() == out.data_ptr()
-            outs.append(got)
-    finally:
-        L.lpg_fc_bf16_set_variant(0)
+    for k in (kernel, 0):
+        out = P.clone()
+        got = fc_forward_bf16(A, W, None, None, b, relu, out=out, accumulate=True, kernel=k)
+        assert got.data_ptr() == out.data_ptr()
+        outs.append(got)
     assert torch.equal(outs[0], outs[1])
-    ref = A.float() @ W.float().t() + P.float()
-    if bias:
-        ref = ref + b
-    if relu:
-        ref = torch.relu(ref)
-    torch.testing.assert_close(outs[0].float(), ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
+    _f64_ulp_check(outs[0].cpu(), A.cpu(), W.cpu(), P.cpu(), None if b is None else b.cpu(), relu)
 
 
-def test_fc_bf16_tile_variants_identical():
-    """Both tilings run the same per-output MFMA chain order: identical bits."""
-    from lpgnn import _lib
+def test_fc_bf16_kernels_identical():
+    """Every kernel runs the same per-output MFMA chain order: identical bits (ReLU + dropout,
+    two k phases), each within one bf16 ulp of fp64."""
     from lpgnn.fc import fc_forward_bf16
 
     torch.manual_seed(1)
     A1, A2 = (torch.randn(5000, 256, device=DEV).to(BF) for _ in range(2))
     W1, W2 = ((torch.randn(384, 256, device=DEV) * 0.05).to(BF) for _ in range(2))
     b = torch.randn(384, device=DEV)
-    L = _lib.lib()
-    outs = []
-    try:
-        for v in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
-            L.lpg_fc_bf16_set_variant(v)
-            outs.append(fc_forward_bf16(A1, W1, A2, W2, b, True, 0.2, seed=9))
-    finally:
-        L.lpg_fc_bf16_set_variant(0)
+    outs = [fc_forward_bf16(A1, W1, A2, W2, b, True, 0.2, seed=9, kernel=k) for k in KERNELS]
     for o in outs:
         assert torch.equal(o, outs[0])
+    outs = [fc_forward_bf16(A1, W1, A2, W2, b, True, kernel=k) for k in KERNELS]
+    _f64_ulp_check(outs[0].cpu(), A1.cpu(), W1.cpu(), None, b.cpu(), True, A2.cpu(), W2.cpu())
 
 
 @pytest.mark.parametrize("M,N,relu,drop,bias", [
-    (5000, 1024, True, 0.1, True),    # interior tiles: the register epilogue's unchecked path
+    (5000, 1024, True, 0.1, True),    # interior tiles
     (4099, 1000, True, 0.3, False),   # ragged rows and columns
     (3000, 512, False, 0.0, True),    # linear (the lin_rel GEMM of the re-associated direction)
 ])
 def test_fc_bf16_transposed_fragments_identical(M, N, relu, drop, bias):
-    """Variants 9 / 10 issue the MFMA as W x A^T (transposed fragments; 9: register epilogue with
-    8-byte stores, 10: 8-byte accesses to the LDS image): the same bits as the LDS-image epilogue
-    of variant 7, with accumulate and dropout."""
-    from lpgnn import _lib
+    """The pipelined kernel issues the MFMA as W x A^T (transposed fragments, 8-byte accesses to
+    the LDS image): the same bits as the untransposed 256 x 256 kernel, with accumulate and dropout."""
     from lpgnn.fc import fc_forward_bf16
 
     g = torch.Generator().manual_seed(M + N)
@@ -118,18 +130,12 @@ def test_fc_bf16_transposed_fragments_identical(M, N, relu, drop, bias):
     W = (torch.randn(N, 256, generator=g) * 0.05).to(BF).to(DEV)
     P = torch.randn(M, N, generator=g).to(BF).to(DEV)
     b = (torch.randn(N, generator=g) * 0.1).to(DEV) if bias else None
-    L = _lib.lib()
     outs = []
-    try:
-        for v in (7, 9, 10):
-            L.lpg_fc_bf16_set_variant(v)
-            for acc in (False, True):
-                outs.append(fc_forward_bf16(A, W, None, None, b, relu, drop, seed=3, out=P.clone() if acc else None,
-                                            accumulate=acc))
-    finally:
-        L.lpg_fc_bf16_set_variant(0)
-    for k in (2, 4):
-        assert torch.equal(outs[0], outs[k]) and torch.equal(outs[1], outs[k + 1])
+    for k in (2, 3):
+        for acc in (False, True):
+            outs.append(fc_forward_bf16(A, W, None, None, b, relu, drop, seed=3, out=P.clone() if acc else None,
+                                        accumulate=acc, kernel=k))
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
 
 
 def test_fc_bf16_asymmetric_identity():
@@ -229,23 +235,14 @@ def _wgrad_bound(G, X):
 ])
 def test_wgrad_bf16_vs_fp64(R, N, K):
     """lpg_wgrad_bf16 (fp32 accumulation of exact bf16 x bf16 products) against
-    fp64 G^T X of the same bf16 operands; both kernel variants bitwise identical
-    and run-to-run identical."""
-    from lpgnn import _lib
+    fp64 G^T X of the same bf16 operands; run-to-run identical."""
     from lpgnn.fc import wgrad_bf16
 
     g = torch.Generator().manual_seed(R + N + K)
     G = torch.randn(R, N, generator=g).to(BF)
     X = torch.relu(torch.randn(R, K, generator=g)).to(BF)
     Gd, Xd = G.to(DEV), X.to(DEV)
-    L = _lib.lib()
-    try:
-        outs = []
-        for v in (100, 101, 102, 103, 104, 105, 100):
-            L.lpg_fc_bf16_set_variant(v)
-            outs.append(wgrad_bf16(Gd, Xd))
-    finally:
-        L.lpg_fc_bf16_set_variant(100)
+    outs = [wgrad_bf16(Gd, Xd) for _ in range(2)]
     assert outs[0].dtype == torch.float32 and outs[0].shape == (N, K)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
@@ -306,41 +303,36 @@ def test_input_grad_bf16(M, N, Nout, two, acc):
     torch.testing.assert_close(got.float(), ref.to(BF).float(), rtol=2 ** -7, atol=2e-3)
 
 
-@pytest.mark.parametrize("M,N,Nin,two,acc,variant", [
+@pytest.mark.parametrize("M,N,Nin,two,acc,kernel", [
     (1000, 2048, 2048, False, True, 0),    # 128 x 128 kernel (M < 4096), accumulate form
     (1000, 256, 512, True, False, 0),      # two-part form
-    (5003, 2048, 2048, True, False, 0),    # variant 10 (transposed fragments, LDS image)
-    (5003, 1024, 2048, False, True, 0),    # accumulate on variant 10, ragged last tile
-    (5003, 1032, 512, False, True, 7),     # untransposed image epilogue, ragged columns
-    (5003, 512, 512, True, False, 9),      # register-epilogue variant: routed to the default kernel
-    (5003, 512, 512, False, True, 3),      # BK 32 kernel: routed to the default kernel
+    (5003, 2048, 2048, True, False, 0),    # pipelined kernel (transposed fragments, LDS image)
+    (5003, 1024, 2048, False, True, 0),    # accumulate on the pipelined kernel, ragged last tile
+    (5003, 1032, 512, False, True, 2),     # untransposed image epilogue, ragged columns
+    (5003, 512, 512, True, False, 1),      # 128 x 128 kernel above 4096 rows
 ])
-def test_fc_bf16_relu_bwd_folded_bitwise(M, N, Nin, two, acc, variant):
+def test_fc_bf16_relu_bwd_folded_bitwise(M, N, Nin, two, acc, kernel):
     """lpg_fc_bf16_relu_bwd = input_grad_bf16 then relu_bwd_colsum_bf16 (the separate pass), bit
     for bit, for the accumulate and two-part forms the c5 backward uses; lpg_colsum_bf16 on the
     folded dZ = the separate pass's bias gradient, bit for bit."""
     from lpgnn import _lib
     from lpgnn.fc import colsum_bf16, input_grad_bf16, relu_bwd_colsum_bf16
 
-    L = _lib.lib()
-    torch.manual_seed(M + N + variant)
+    torch.manual_seed(M + N + kernel)
     G1 = torch.randn(M, N, device=DEV).to(BF)
     W1 = torch.randn(N, Nin, device=DEV) * 0.03  # Linear [out = N, in = Nin]: dX = G W
     G2 = torch.randn(M, N, device=DEV).to(BF) if two else None
     W2 = torch.randn(N, Nin, device=DEV) * 0.03 if two else None
     Y = torch.relu(torch.randn(M, Nin, device=DEV)).to(BF)
     add = torch.randn(M, Nin, device=DEV).to(BF) if acc else None
-    try:
-        _lib.check(L.lpg_fc_bf16_set_variant(variant), "set_variant")
-        for scale in (1.0, 1.0 / 0.9):
-            ref = input_grad_bf16(G1, W1, G2, W2, out=None if add is None else add.clone(), accumulate=acc)
-            want, db_want = relu_bwd_colsum_bf16(ref, Y, scale, True)
-            got = input_grad_bf16(G1, W1, G2, W2, out=None if add is None else add.clone(), accumulate=acc,
-                                  mask=(Y, scale))
-            assert torch.equal(got, want)
-            assert torch.equal(colsum_bf16(got), db_want)
-    finally:
-        L.lpg_fc_bf16_set_variant(0)
+    for scale in (1.0, 1.0 / 0.9):
+        ref = input_grad_bf16(G1, W1, G2, W2, out=None if add is None else add.clone(), accumulate=acc,
+                              kernel=kernel)
+        want, db_want = relu_bwd_colsum_bf16(ref, Y, scale, True)
+        got = input_grad_bf16(G1, W1, G2, W2, out=None if add is None else add.clone(), accumulate=acc,
+                              mask=(Y, scale), kernel=kernel)
+        assert torch.equal(got, want)
+        assert torch.equal(colsum_bf16(got), db_want)
 
 
 def test_fc_bf16_relu_bwd_rejects_bias_and_bad_layouts():

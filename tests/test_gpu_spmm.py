@@ -72,12 +72,7 @@ def test_slice_widths_bitwise(slice_cols):
     adj = _adj(row, col, val, m, n)
     A, _ = _oracle_pair(row, col, val, m, n)
     Xv = rng.standard_normal((n, Fd)).astype(np.float32)
-    L = _lib.lib()
-    try:
-        assert L.lpg_spmm_set_slice(slice_cols) == 0
-        y = spmm_forward(adj.fwd, torch.from_numpy(Xv).to(DEV)).cpu().numpy()
-    finally:
-        L.lpg_spmm_set_slice(0)
+    y = spmm_forward(adj.fwd, torch.from_numpy(Xv).to(DEV), slice_cols=slice_cols).cpu().numpy()
     assert np.array_equal(y, O.spmm_f32(*A, Xv))
 
 
@@ -266,26 +261,20 @@ def test_degree_aware_heavy_rows_bitwise(thresh, Fd, slice_cols, monkeypatch):
     A, AT = _oracle_pair(row, col, val, g.m, g.n)
     assert adj.fwd.degrees().max().item() > 4000
     rng = np.random.default_rng(Fd)
-    L = _lib.lib()
-    try:
-        _lib.check(L.lpg_spmm_set_slice(slice_cols), "set_slice")
-        for csr, ref, n_src in ((adj.fwd, A, g.n), (adj.bwd, AT, g.m)):
-            X = rng.standard_normal((n_src, Fd)).astype(np.float32)
-            got = spmm_forward(csr, torch.from_numpy(X).to(DEV)).cpu().numpy()
-            assert np.array_equal(got, O.spmm_f32(*ref, X))
-            if thresh < csr.degrees().max().item():  # the heavy path actually ran in this direction
-                assert csr.heavy_rows(thresh)[1] > 0
-    finally:
-        L.lpg_spmm_set_slice(0)
+    for csr, ref, n_src in ((adj.fwd, A, g.n), (adj.bwd, AT, g.m)):
+        X = rng.standard_normal((n_src, Fd)).astype(np.float32)
+        got = spmm_forward(csr, torch.from_numpy(X).to(DEV), slice_cols=slice_cols).cpu().numpy()
+        assert np.array_equal(got, O.spmm_f32(*ref, X))
+        if thresh < csr.degrees().max().item():  # the heavy path actually ran in this direction
+            assert csr.heavy_rows(thresh)[1] > 0
 
 
 @pytest.mark.parametrize("depth", [8, 16, 32])
 @pytest.mark.parametrize("Fd,dt", [(1024, torch.float32), (300, torch.float32), (2048, torch.float32)])
-def test_batched_remainder_bitwise(depth, Fd, dt):
-    """lpg_spmm_set_remainder: the chunk remainder gathered together (default) or one
-    gather at a time give the same bits, equal to the oracle loop; degrees 0..150 so
-    every remainder length 0 .. depth-1 occurs, and rows cross the 64-edge chunks."""
-    from lpgnn import _lib
+def test_gather_depth_bitwise(depth, Fd, dt):
+    """Every gather depth (edges in flight per wave; a chunk's remainder gathered together,
+    predicated per edge) gives the oracle loop's bits, for 128- and 256-column slices; degrees
+    0..150 so every remainder length 0 .. depth-1 occurs, and rows cross the 64-edge chunks."""
     from lpgnn.sparse import spmm_forward
 
     rng = np.random.default_rng(depth + Fd)
@@ -296,16 +285,7 @@ def test_batched_remainder_bitwise(depth, Fd, dt):
     val = rng.uniform(-1, 1, len(row)).astype(np.float32)
     adj = _adj(row, col, val, m, n)
     X = torch.from_numpy(rng.standard_normal((n, Fd)).astype(np.float32)).to(dt)
-    L = _lib.lib()
-    outs = []
-    try:
-        L.lpg_spmm_set_depth(depth)
-        for rb in (1, 0):
-            L.lpg_spmm_set_remainder(rb)
-            outs.append(spmm_forward(adj.fwd, X.to(DEV)).cpu())
-    finally:
-        L.lpg_spmm_set_depth(0)
-        L.lpg_spmm_set_remainder(1)
+    outs = [spmm_forward(adj.fwd, X.to(DEV), slice_cols=sl, depth=depth).cpu() for sl in (0, 256)]
     assert torch.equal(outs[0], outs[1])
     A, _ = _oracle_pair(row, col, val, m, n)
     assert np.array_equal(outs[0].numpy(), O.spmm_f32(*A, X.numpy()))
@@ -329,12 +309,7 @@ def test_bf16_slice_widths_bitwise(slice_cols, Fd):
     A, _ = _oracle_pair(row, col, val, m, n)
     X = torch.randn(n, Fd).to(torch.bfloat16)
     Xbits = X.view(torch.int16).numpy().view(np.uint16)
-    L = _lib.lib()
-    try:
-        assert L.lpg_spmm_set_slice(slice_cols) == 0
-        y = spmm_forward(adj.fwd, X.to(DEV)).cpu().view(torch.int16).numpy().view(np.uint16)
-    finally:
-        L.lpg_spmm_set_slice(0)
+    y = spmm_forward(adj.fwd, X.to(DEV), slice_cols=slice_cols).cpu().view(torch.int16).numpy().view(np.uint16)
     assert np.array_equal(y, O.spmm_bf16(*A, Xbits))
 
 

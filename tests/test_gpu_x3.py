@@ -84,28 +84,17 @@ def test_x3_accuracy_vs_fp64(M, N, K1, K2, relu, bias):
     assert err.mean().item() <= 4 * e32.mean().item() + 1e-12
 
 
-def test_x3_variants_identical():
-    """Tile variants on the same MFMA shape give identical bits; the two MFMA
-    shapes (32x32x16, 16x16x32: different in-instruction summation) agree to
-    fp32 rounding."""
-    from lpgnn import _lib
+def test_x3_kernels_identical_when_strides_differ():
+    """lda1 != lda2: the default falls back to fc_fwd_x3_16 (the wide kernel needs one offset set
+    for both k phases) -- the same bits as choosing it explicitly (LPG_FC_KERNEL(1))."""
     from lpgnn.fc import fc_forward
 
     g = torch.Generator().manual_seed(5)
     A1, A2 = torch.randn(700, 256, generator=g).to(DEV), torch.randn(700, 128, generator=g).to(DEV)
     W1, W2 = torch.randn(300, 256, generator=g).to(DEV), torch.randn(300, 128, generator=g).to(DEV)
     b = torch.randn(300, generator=g).to(DEV)
-    L = _lib.lib()
-    outs = {}
-    for v in range(17):
-        assert L.lpg_fc_x3_set_variant(v) == 0
-        outs[v] = fc_forward(A1, W1, A2, W2, b, True, arith="x3")
-    L.lpg_fc_x3_set_variant(0)
-    for v in (2, 3, 4, 8):  # 32x32x16
-        assert torch.equal(outs[v], outs[1]), v
-    for v in (5, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16):  # 16x16x32 (the default; lda1 != lda2 here: the
-        assert torch.equal(outs[v], outs[0]), v          # wide variants fall back to fc_fwd_x3_16)
-    torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-5)
+    outs = [fc_forward(A1, W1, A2, W2, b, True, arith="x3", kernel=k) for k in (0, 1)]
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("M,N,K1,K2,accum,drop", [
@@ -116,11 +105,9 @@ def test_x3_variants_identical():
     (1, 130, 64, 64, False, 0.0),
 ])
 def test_x3_wide_variants_bitwise(M, N, K1, K2, accum, drop):
-    """fc_x3_wide (variants 12-16; the default 0 = 14): buffer_load ... lds staging and wide wave
-    strips, the same MFMA shape, k order and product sequence per output as fc_fwd_x3_16
-    (variant 10) -- bitwise the same C, incl. ragged edges (clamped rows/columns), dropout and
-    the accumulate flag's addend."""
-    from lpgnn import _lib
+    """fc_x3_wide (the default): buffer_load ... lds staging and wide wave strips, the same MFMA
+    shape, k order and product sequence per output as fc_fwd_x3_16 (LPG_FC_KERNEL(1)) -- bitwise
+    the same C, incl. ragged edges (clamped rows/columns), dropout and the accumulate flag's addend."""
     from lpgnn.fc import fc_forward
 
     g = torch.Generator().manual_seed(M + N + K1)
@@ -130,38 +117,9 @@ def test_x3_wide_variants_bitwise(M, N, K1, K2, accum, drop):
     W2 = (torch.randn(N, K2, generator=g) * 0.05).to(DEV) if K2 else None
     b = torch.randn(N, generator=g).to(DEV)
     P = torch.randn(M, N, generator=g).to(DEV) if accum else None
-    L = _lib.lib()
-    outs = {}
-    try:
-        for v in (10, 0, 12, 13, 14, 15, 16):
-            _lib.check(L.lpg_fc_x3_set_variant(v), "set_variant")
-            outs[v] = fc_forward(A1, W1, A2, W2, b, True, drop, 5, out=None if P is None else P.clone(),
-                                 accumulate=accum, arith="x3")
-    finally:
-        L.lpg_fc_x3_set_variant(0)
-    for v in (0, 12, 13, 14, 15, 16):
-        assert torch.equal(outs[v], outs[10]), v
-
-
-@pytest.mark.parametrize("M", [1024, 1100, 37])
-def test_x3_xcd_pair_map_covers_every_tile(M):
-    """Variant 11 (N = 1024: XCD pairs share n-tile pairs, odd m-tile counts split mid-pair) computes
-    every tile once: identical bits to the default map."""
-    from lpgnn import _lib
-    from lpgnn.fc import fc_forward
-
-    g = torch.Generator().manual_seed(M)
-    A1, W1 = torch.randn(M, 256, generator=g).to(DEV), torch.randn(1024, 256, generator=g).to(DEV)
-    b = torch.randn(1024, generator=g).to(DEV)
-    L = _lib.lib()
-    outs = {}
-    try:
-        for v in (0, 11):
-            assert L.lpg_fc_x3_set_variant(v) == 0
-            outs[v] = fc_forward(A1, W1, None, None, b, True, arith="x3")
-    finally:
-        L.lpg_fc_x3_set_variant(0)
-    assert torch.equal(outs[0], outs[11])
+    outs = [fc_forward(A1, W1, A2, W2, b, True, drop, 5, out=None if P is None else P.clone(), accumulate=accum,
+                       arith="x3", kernel=k) for k in (1, 0)]
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("M,N,K,hn,accum,drop", [
@@ -197,31 +155,27 @@ def test_x3_fused_heads_match_separate_linear(M, N, K, hn, accum, drop):
     torch.testing.assert_close(lg, fc_forward(y0, Wh, None, None, bh, False), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 1, 2, 8])
-def test_x3_fused_heads_under_every_variant(variant):
-    """The fused-heads C equals lpg_fc_x3_f32's C under whatever x3 variant is
-    selected: the 16x16x32 variants share the heads kernel's MFMA shape and k
-    order (bitwise), the 32x32x16 ones make the heads path fall back to the FC
-    plus a separate Linear (again the variant's own C)."""
-    from lpgnn import _lib
+@pytest.mark.parametrize("kernel", [0, 1])
+@pytest.mark.parametrize("M", [1000, 997])
+def test_x3_fused_heads_under_every_kernel(kernel, M):
+    """The fused-heads C equals lpg_fc_x3_f32's C under either kernel (one MFMA shape, one k
+    order: bitwise), and the two kernels' logits agree bitwise too (the wide kernel reads its
+    outputs back from an LDS image in the order the other accumulates them in registers)."""
     from lpgnn.fc import fc_forward
 
-    g = torch.Generator().manual_seed(variant)
-    M, N, K = 1000, 1024, 256
+    g = torch.Generator().manual_seed(M)
+    N, K = 1024, 256
     A = torch.relu(torch.randn(M, K, generator=g)).to(DEV)
     W = (torch.randn(N, K, generator=g) * 0.05).to(DEV)
     b = torch.randn(N, generator=g).to(DEV)
     Wh = (torch.randn(3, N, generator=g) * 0.1).to(DEV)
     bh = torch.randn(3, generator=g).to(DEV)
-    L = _lib.lib()
-    try:
-        _lib.check(L.lpg_fc_x3_set_variant(variant), "set_variant")
-        y0 = fc_forward(A, W, None, None, b, True, arith="x3")
-        y, lg = fc_forward(A, W, None, None, b, True, arith="x3", heads=(Wh, bh))
-    finally:
-        L.lpg_fc_x3_set_variant(0)
+    y0 = fc_forward(A, W, None, None, b, True, arith="x3", kernel=kernel)
+    y, lg = fc_forward(A, W, None, None, b, True, arith="x3", heads=(Wh, bh), kernel=kernel)
     assert torch.equal(y, y0)
     torch.testing.assert_close(lg, fc_forward(y0, Wh, None, None, bh, False), rtol=1e-5, atol=1e-5)
+    _, lg_other = fc_forward(A, W, None, None, b, True, arith="x3", heads=(Wh, bh), kernel=1 - kernel)
+    assert torch.equal(lg, lg_other)
 
 
 @pytest.mark.parametrize("relu", [False, True])
@@ -281,6 +235,9 @@ def test_x3_rejects_bad_shapes():
     (37, 132, 260),       # ragged output tiles, a single partial chunk
     (0, 64, 64),          # no rows: zeros
     (70000, 128, 64),     # many R splits
+    (20, 64, 64),         # one partial chunk per split (T = 1)
+    (3000, 128, 128),     # T = 9 (odd: the last chunk in the first plane buffer), shorter last split
+    (1000, 300, 200),     # N, K not multiples of the 256 x 128 tile
 ])
 def test_wgrad_x3_accuracy_vs_fp64(R, N, K):
     from lpgnn.fc import wgrad
@@ -296,40 +253,6 @@ def test_wgrad_x3_accuracy_vs_fp64(R, N, K):
     assert (err <= bound).all(), f"max err/bound {(err / bound).max().item():.3f}"
     again = wgrad(G.to(DEV), X.to(DEV), arith="x3").cpu().double()
     assert torch.equal(got, again)  # fixed-order split reduction: run-to-run identical
-
-
-@pytest.mark.parametrize("R,N,K", [
-    (20, 64, 64),         # one partial chunk per split (T = 1)
-    (37, 132, 260),       # ragged tiles, T = 2
-    (1000, 256, 128),     # T = 8
-    (3000, 128, 128),     # T = 9 (odd), shorter last split
-    (70000, 128, 64),     # T = 35, many splits
-    (4096, 1024, 1024),   # hidden-layer tile grid
-    (1000, 300, 200),     # N, K not multiples of the 256 x 128 tile
-])
-def test_wgrad_x3_kernels_bitwise_equal(R, N, K):
-    """The producer/consumer (variant 103) and the wide split-ahead weight-gradient kernels (104,
-    105: 256 x 128 tiles, two plane buffers, the host passes the cooperative kernel's split
-    count) form the cooperative kernel's products in the same order: identical bits."""
-    from lpgnn import _lib
-    from lpgnn.fc import wgrad
-
-    L = _lib.lib()
-    g = torch.Generator().manual_seed(R * 7 + K)
-    G = torch.randn(R, N, generator=g).to(DEV)
-    X = torch.randn(R, K, generator=g).relu().to(DEV)
-    out = {}
-    try:
-        for v in (102, 103, 104, 105):
-            assert L.lpg_fc_x3_set_variant(v) == 0
-            out[v] = wgrad(G, X, arith="x3")
-    finally:
-        L.lpg_fc_x3_set_variant(100 + _DEFAULT_WGRAD)
-    for v in (103, 104, 105):
-        assert torch.equal(out[102], out[v]), v
-
-
-_DEFAULT_WGRAD = 5  # csrc/fc_x3.hip g_wgrad_m16
 
 
 def test_wgrad_x3_strided_inputs():

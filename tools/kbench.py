@@ -43,6 +43,7 @@ def timeit(fns, rounds=7, iters=5):
 
 
 def bench_fc(out):
+    """The exact-fp32 FC (LPGNN_FC_ARITH=fp32's kernel) and the default x3 FC at the c2 shapes vs torch."""
     from lpgnn.fc import fc_forward
 
     dev = "cuda"
@@ -53,27 +54,13 @@ def bench_fc(out):
         W2 = torch.randn(1024, K, device=dev) * 0.03
         b = torch.randn(1024, device=dev)
         flops = 2.0 * M * 1024 * 2 * K
-        from lpgnn import _lib
-        L = _lib.lib()
-
-        def var(v):
-            def f():
-                L.lpg_fc_set_variant(v)
-                return fc_forward(A1, W1, A2, W2, b, True)
-            return f
-        y0 = var(0)()
-        for v in range(1, 9):
-            assert torch.equal(var(v)(), y0), f"variant {v} differs"
         t = timeit({
-            **{f"lpg_fc_f32 v{v}": var(v) for v in range(9)},
+            "lpg_fc_f32": lambda: fc_forward(A1, W1, A2, W2, b, True, arith="fp32"),
+            "lpg_fc_x3_f32": lambda: fc_forward(A1, W1, A2, W2, b, True, arith="x3"),
             "torch_2gemm_add_relu": lambda: torch.relu(F.linear(A1, W1, b) + F.linear(A2, W2)),
-            "torch_1gemm_K2048": lambda: F.linear(torch.cat([A1, A2], 1) if False else A1, torch.cat([W1], 1), b),
         })
-        L.lpg_fc_set_variant(0)
         for k, v in t.items():
-            f = flops if k != "torch_1gemm_K2048" else flops / 2
-            out[f"fc M={M} K={2*K} {k}"] = dict(ms=v, tflops=f / v / 1e9)
-        # heads and conv1
+            out[f"fc M={M} K={2*K} {k}"] = dict(ms=v, tflops=flops / v / 1e9)
         H = torch.randn(M, 1024, device=dev)
         Wh = torch.randn(3, 1024, device=dev)
         bh = torch.randn(3, device=dev)
@@ -117,20 +104,14 @@ def _spmm_graph(out, L, gname, g, spmm_forward, BipartiteCSR):
         ref = spmm_forward(csr, X)
         from lpgnn import sparse as S
         h0 = S.HEAVY_THRESH
-        for sl, u, h, rb in ((256, 8, h0, 0), (256, 8, h0, 1), (256, 16, h0, 1), (256, 32, h0, 1), (512, 8, h0, 1),
-                             (256, 8, 0, 1), (256, 16, 0, 1), (256, 8, 256, 1)):
-            def f(sl=sl, u=u, h=h, rb=rb):
-                L.lpg_spmm_set_slice(sl)
-                L.lpg_spmm_set_depth(u)
-                L.lpg_spmm_set_remainder(rb)  # 1: a chunk's last n mod depth edges gathered together
+        for sl, u, h in ((0, 0, h0), (128, 8, h0), (128, 16, h0), (256, 8, h0), (256, 16, h0), (256, 32, h0),
+                         (512, 8, h0), (256, 8, 0), (256, 8, 256)):
+            def f(sl=sl, u=u, h=h):
                 S.HEAVY_THRESH = h  # degree-aware split: rows above h on (row, 64-column) waves; 0 = off
-                return spmm_forward(csr, X)
+                return spmm_forward(csr, X, slice_cols=sl, depth=u)
             assert torch.equal(f(), ref)
-            fns[f"slice{sl} depth{u} heavy>{h} rem{'B' if rb else '1'}"] = f
+            fns[f"slice{sl} depth{u} heavy>{h}"] = f
         t = timeit(fns)
-        L.lpg_spmm_set_slice(0)
-        L.lpg_spmm_set_depth(0)
-        L.lpg_spmm_set_remainder(1)
         S.HEAVY_THRESH = h0
         B = g.nnz * 1024 * 4 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 1024 * 4
         for k, v in t.items():
@@ -156,12 +137,10 @@ def bench_spmmbig(out):
             fns = {}
             for sl in (256, 128, 64):
                 def f(sl=sl):
-                    L.lpg_spmm_set_slice(sl)
-                    return spmm_forward(csr, X)
+                    return spmm_forward(csr, X, slice_cols=sl)
                 assert torch.equal(f(), ref)
                 fns[f"slice{sl}"] = f
             t = timeit(fns, rounds=5, iters=3)
-            L.lpg_spmm_set_slice(0)
             rows = csr.n_rows
             B = nnz * 1024 * 4 + nnz * 8 + (rows + 1) * 8 + rows * 1024 * 4
             for k, v in t.items():
@@ -182,23 +161,20 @@ def bench_spmm16(out):
         adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
         for name, csr, K in (("cons<-vars", adj.fwd, g.n), ("vars<-cons", adj.bwd, g.m)):
             X = torch.randn(K, 2048, device="cuda").to(torch.bfloat16)
-            L.lpg_spmm_set_slice(1024)  # the whole-row (round-1) form as the reference
             from lpgnn import sparse as S0
             hh, S0.HEAVY_THRESH = S0.HEAVY_THRESH, 0
-            ref = spmm_forward(csr, X)
+            ref = spmm_forward(csr, X, slice_cols=1024)  # the whole-row (round-1) form as the reference
             S0.HEAVY_THRESH = hh
             fns = {}
             from lpgnn import sparse as S
             h0 = S.HEAVY_THRESH
             for sl, h in ((256, h0), (256, 0), (512, 0), (1024, 0)):
                 def f(sl=sl, h=h):
-                    L.lpg_spmm_set_slice(sl)
                     S.HEAVY_THRESH = h
-                    return spmm_forward(csr, X)
+                    return spmm_forward(csr, X, slice_cols=sl)
                 assert torch.equal(f(), ref)
                 fns[f"slice{sl} heavy>{h}"] = f
             t = timeit(fns)
-            L.lpg_spmm_set_slice(0)
             S.HEAVY_THRESH = h0
             B = g.nnz * 2048 * 2 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 2048 * 2
             for k, v in t.items():
@@ -231,35 +207,23 @@ def bench_bf16(out):
     b2 = torch.randn(2048, device="cuda")
     Bc = torch.cat([B1, B2], 1)
     Vc = torch.cat([V1, V2], 1)
-    from lpgnn import _lib
-    L = _lib.lib()
 
-    def var(v):
-        def f():
-            L.lpg_fc_bf16_set_variant(v)
-            return fc_forward_bf16(B1, V1, B2, V2, b2, True)
-        return f
-    y0 = var(0)()
-    for v in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
-        assert torch.equal(var(v)(), y0), f"bf16 variant {v} differs"
-    t = timeit({"lpg_fc_bf16 v2 256x256 2buf": var(2), "lpg_fc_bf16 v5 8-wave pipelined": var(5),
-                "lpg_fc_bf16 v6 v5 + placed": var(6), "lpg_fc_bf16 v7 v6 + prio": var(7),
-                "lpg_fc_bf16 v8 4-wave placed": var(8), "lpg_fc_bf16 v9 v7 + transposed fragments": var(9),
-                "lpg_fc_bf16 v10 transposed via image": var(10),
+    def ker(k):
+        return lambda: fc_forward_bf16(B1, V1, B2, V2, b2, True, kernel=k)
+    y0 = ker(0)()
+    for k in (1, 2, 3):
+        assert torch.equal(ker(k)(), y0), f"bf16 kernel {k} differs"
+    t = timeit({"lpg_fc_bf16 k2 256x256 2buf": ker(2), "lpg_fc_bf16 k3 pipelined (default)": ker(3),
                 "torch_bf16_1gemm_relu": lambda: torch.relu(F.linear(Bc, Vc, b2.to(torch.bfloat16)))})
-    L.lpg_fc_bf16_set_variant(0)
     for k, v in t.items():
         out[f"bf16 M={M} K=4096 {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * 4096 / v / 1e9)
 
 
 def bench_fck(out):
-    """lpg_fc_bf16 variants 7 / 9 / 10 at M = 200K / 100K, N = 2048 for K = 1024 .. 8192 (one phase,
-    no epilogue options, and with ReLU + dropout + accumulate in place): per-block fixed cost vs
-    the k loop."""
-    from lpgnn import _lib
+    """lpg_fc_bf16 (default kernel) at M = 200K / 100K, N = 2048 for K = 1024 .. 8192 (one phase, no
+    epilogue options, and with ReLU + dropout + accumulate in place): per-block fixed cost vs the k loop."""
     from lpgnn.fc import fc_forward_bf16
 
-    L = _lib.lib()
     BF = torch.bfloat16
     for M in (200_000, 100_000):
         for K in (1024, 2048, 4096, 8192):
@@ -268,41 +232,28 @@ def bench_fck(out):
             b = torch.randn(2048, device="cuda")
             P = torch.randn(M, 2048, device="cuda").to(BF)
 
-            def run(v, acc, A=A, W=W, b=b, P=P):
+            def run(acc, A=A, W=W, b=b, P=P):
                 def f():
-                    L.lpg_fc_bf16_set_variant(v)
                     if acc:
                         return fc_forward_bf16(A, W, None, None, b, True, 0.1, 7, out=P, accumulate=True)
                     return fc_forward_bf16(A, W, None, None, None, False)
                 return f
-            t = timeit({f"v{v} {'relu+drop+acc' if acc else 'plain'}": run(v, acc) for v in (7, 10)
-                        for acc in (False, True)}, rounds=5, iters=3)
-            L.lpg_fc_bf16_set_variant(0)
+            t = timeit({("relu+drop+acc" if acc else "plain"): run(acc) for acc in (False, True)}, rounds=5, iters=3)
             for k, v in t.items():
                 out[f"fcK M={M} K={K} {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * K / v / 1e9)
             del A, W, P
 
 
 def bench_wgk(out):
-    """lpg_wgrad_bf16 (default variant) at N = K = 2048 for R = 25K .. 400K: the per-launch fixed
-    cost (prologue, partial-tile epilogue, fold) against the per-row slope."""
-    from lpgnn import _lib
+    """lpg_wgrad_bf16 at N = K = 2048 for R = 25K .. 400K: the per-launch fixed cost (prologue,
+    partial-tile epilogue, fold) against the per-row slope."""
     from lpgnn.fc import wgrad_bf16
 
-    L = _lib.lib()
     BF = torch.bfloat16
     for R in (25_000, 50_000, 100_000, 200_000, 400_000):
         G = torch.randn(R, 2048, device="cuda").to(BF)
         X = torch.relu(torch.randn(R, 2048, device="cuda")).to(BF)
-
-        def run(v, G=G, X=X):
-            def f():
-                L.lpg_fc_bf16_set_variant(v)
-                return wgrad_bf16(G, X)
-            return f
-        assert torch.equal(run(102)(), run(105)())
-        t = timeit({f"v{v}": run(v) for v in (102, 105)}, rounds=5, iters=4)
-        L.lpg_fc_bf16_set_variant(102)
+        t = timeit({"wgrad_bf16": lambda G=G, X=X: wgrad_bf16(G, X)}, rounds=5, iters=4)
         for k, v in t.items():
             out[f"wgk R={R} {k}"] = dict(ms=v, tflops=2.0 * R * 2048 * 2048 / v / 1e9)
         del G, X
@@ -353,45 +304,26 @@ def bench_x3epi(out):
 
 
 def bench_bf16bwd(out):
-    """c5 backward GEMMs: lpg_wgrad_bf16 (4 / 8 waves) vs torch (G^T X).float(); the input
-    gradient on lpg_fc_bf16 (transposed weights) vs torch G @ W."""
-    from lpgnn import _lib
+    """c5 backward GEMMs: lpg_wgrad_bf16 vs torch (G^T X).float(); the input gradient on
+    lpg_fc_bf16 (transposed weights) vs torch G @ W."""
     from lpgnn.fc import input_grad_bf16, wgrad_bf16
 
-    L = _lib.lib()
     BF = torch.bfloat16
     for R in (100_000, 200_000):
         G = torch.randn(R, 2048, device="cuda").to(BF)
         X = torch.relu(torch.randn(R, 2048, device="cuda")).to(BF)
         W = torch.randn(2048, 2048, device="cuda") * 0.02
         Wb = W.to(BF)
-
-        def wv(v):
-            def f():
-                L.lpg_fc_bf16_set_variant(v)
-                return wgrad_bf16(G, X)
-            return f
-        a = wv(100)()
-        for v in (101, 102, 103, 104):
-            assert torch.equal(a, wv(v)()), f"wgrad variant {v} differs"
+        a = wgrad_bf16(G, X)
         ref = (G.float().t() @ X.float())
         print(f"R={R} wgrad max|ours - fp32 torch| = {(a - ref).abs().max().item():.3e}  "
               f"max|torch bf16 - fp32| = {((G.t() @ X).float() - ref).abs().max().item():.3e}", flush=True)
         del ref
-
-        def iv(v, two=False):
-            def f():
-                L.lpg_fc_bf16_set_variant(v)
-                return input_grad_bf16(G, W, G if two else None, W if two else None)
-            return f
-        t = timeit({"wgrad v100 4-wave": wv(100), "wgrad v101 8-wave": wv(101), "wgrad v102 placed": wv(102),
-                    "wgrad v103 placed+prio": wv(103), "wgrad v104 4-wave placed": wv(104),
+        t = timeit({"wgrad": lambda: wgrad_bf16(G, X),
                     "wgrad torch (G^T X).float()": lambda: (G.t() @ X).float(),
-                    "igrad v5": iv(5), "igrad v6": iv(6), "igrad v7": iv(7), "igrad torch G @ W": lambda: G @ Wb,
-                    "igrad2 v5": iv(5, True), "igrad2 v6": iv(6, True), "igrad2 v7": iv(7, True),
+                    "igrad": lambda: input_grad_bf16(G, W), "igrad torch G @ W": lambda: G @ Wb,
+                    "igrad2": lambda: input_grad_bf16(G, W, G, W),
                     "igrad2 torch": lambda: torch.addmm(G @ Wb, G, Wb)}, rounds=5, iters=3)
-        L.lpg_fc_bf16_set_variant(0)
-        L.lpg_fc_bf16_set_variant(100)
         for k, v in t.items():
             fl = 2.0 * R * 2048 * 2048 * (2 if k.startswith("igrad2") else 1)
             out[f"bf16bwd R={R} {k}"] = dict(ms=v, tflops=fl / v / 1e9)
@@ -461,13 +393,11 @@ def bench_load(out):
 
 
 def bench_fcpi(out):
-    """FC kernel variants at the c2 hidden-layer shapes vs hipBLASLt (torch)."""
-    from lpgnn import _lib
+    """The x3 FC kernels (default wide, LPG_FC_KERNEL(1)) and the exact-fp32 kernel at the c2
+    hidden-layer shapes vs hipBLASLt (torch)."""
     from lpgnn.fc import fc_forward
 
-    L = _lib.lib()
     dev = "cuda"
-    variants = [int(v) for v in os.environ.get("LPG_FCV", "0,1,2,3,4").split(",")]
     for M, K1, K2 in ((200_000, 1024, 1024), (200_000, 1024, 0), (100_000, 1024, 0)):
         A1 = torch.randn(M, K1, device=dev).relu_()
         A2 = torch.randn(M, K2, device=dev).relu_() if K2 else None
@@ -475,24 +405,15 @@ def bench_fcpi(out):
         W2 = torch.randn(1024, K2, device=dev) * 0.03 if K2 else None
         b = torch.randn(1024, device=dev)
         flops = 2.0 * M * 1024 * (K1 + K2)
-
-        def var(v):
-            def f():
-                L.lpg_fc_set_variant(v)
-                return fc_forward(A1, W1, A2, W2, b, True)
-            return f
-        ys = {v: var(v)() for v in variants}
-        ref = ys[variants[0]]
-        for v, y in ys.items():
-            d = (y - ref).abs().max().item()
-            out[f"fcpi M={M} K={K1}+{K2} v{v} maxdiff"] = dict(d=d)
-        fns = {f"v{v}": var(v) for v in variants}
+        fns = {"x3 wide": lambda: fc_forward(A1, W1, A2, W2, b, True, arith="x3"),
+               "x3 k1": lambda: fc_forward(A1, W1, A2, W2, b, True, arith="x3", kernel=1),
+               "fp32": lambda: fc_forward(A1, W1, A2, W2, b, True, arith="fp32")}
+        assert torch.equal(fns["x3 wide"](), fns["x3 k1"]())
         if K2:
             fns["torch"] = lambda: torch.relu(torch.addmm(b, A1, W1.t()).addmm_(A2, W2.t()))
         else:
             fns["torch"] = lambda: torch.relu(torch.addmm(b, A1, W1.t()))
         t = timeit(fns)
-        L.lpg_fc_set_variant(0)
         for k, v in t.items():
             out[f"fcpi M={M} K={K1}+{K2} {k}"] = dict(ms=v, tflops=flops / v / 1e9)
         del A1, A2
