@@ -4,6 +4,12 @@ SpMM kernel and the oracle CPU path timed beside it.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
 
+With --gpus N > 1 and no RANK / WORLD_SIZE in the environment, bench.py launches the N ranks
+itself (one child process per GPU, started before this process touches the GPU; rank 0 prints
+the JSON line) -- the same line as under ``torch.distributed.run --nproc-per-node N``.
+``--share-gpu`` makes the N ranks share the visible GPU(s) over gloo (a rehearsal on a 1-GPU
+box; the measured runs use RCCL, one rank per GPU).
+
 A step = one GCN_FC(8, 8, hids=1024, depth=3) training iteration of
 train.py:117-129 on the synthetic c2 graph (100K cons x 200K vars, nnz 2M,
 BASELINE.json configs[1]): forward (2 SpMM at F=8 + 2 at F=1024, FC stacks,
@@ -62,6 +68,12 @@ def parse():
     ap.add_argument("--print-workload", action="store_true", help="print the N=1 workload string and exit")
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned RCCL path even at N=1 (the N>1 code path)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="self-launched N>1: ranks share the visible GPU(s) over gloo (rehearsal, not a measurement)")
+    ap.add_argument("--rho-sweep", default="0,0.02,0.1,1.0",
+                    help="c4 at N>1: rho values whose partition boundary counts go into the JSON ('' = off)")
+    ap.add_argument("--inference", action="store_true",
+                    help="time eval-mode forward + inference_gnn (the reference's timed path) instead of training")
     args = ap.parse_args()
     if args.config is None:
         args.config = "c2" if args.gpus == 1 else "c4"
@@ -164,11 +176,57 @@ def workload_name(args) -> str:
             f"GCN_FC(8,8,hids={args.hids},depth={args.depth}{dt}) fwd+bwd+Adam")
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks as child processes (this process never
+    initialises the GPU and never execs), forward their output, return the first failing exit
+    status (0 if all ranks succeed).  If one rank fails the others are stopped."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if args.share_gpu:
+            env["LPGNN_DIST_BACKEND"] = "gloo"
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:  # a failed rank: stop the others (they would wait in a collective)
+                        os.killpg(q.pid, signal.SIGTERM)
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for q in procs:
+            os.killpg(q.pid, signal.SIGTERM)
+        raise
+    return rc
+
+
 def main():
     args = parse()
     if args.print_workload:
         print(workload_name(args))
         return
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -256,6 +314,9 @@ def main():
         exch = {"per_rank": gathered,
                 "note": "standalone F=hid owner-reduce / halo-broadcast of [n_local, F] fp32 rows (median ms, "
                         "barrier + sync around each); in the step they run async under independent compute"}
+        if args.config == "c4" and world > 1 and args.rho_sweep:  # after the timed region
+            exch["rho_sweep"] = partition.rho_sweep(args, rank, world,
+                                                    [float(r) for r in args.rho_sweep.split(",")], args.hids)
 
     # hid-width SpMM launches (the metric's kernel) measured on their stream
     hid_keys = [k for k in kern if k[0] == "spmm" and k[3] == args.hids]

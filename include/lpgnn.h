@@ -167,7 +167,10 @@ lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  * element (m, n) is kept iff a counter-based hash of (seed, m, n) (two
  * rounds of the 32-bit lowbias32 mix) is >= dropout_p * 2^32, and kept
  * values are scaled by 1 / (1 - dropout_p).  The mask is never stored: the
- * kept set is exactly where the output is > 0.
+ * kept set is exactly where the output is > 0.  The hash keys row m as
+ * row_offset + m: a caller computing a slice of a larger node set (the row
+ * partition, lpgnn/partition.py) passes the slice's first global node id, so
+ * every node's mask is the one a single-GPU run would draw.
  * Row-major fp32, leading dimensions in floats; A/W leading dimensions
  * multiples of 4, A/W 16-byte aligned; K1 and K2 multiples of 32 (zero-pad:
  * padded k are exact no-ops), except for the narrow-input kernel (4 <= K1,
@@ -184,7 +187,7 @@ lpg_status lpg_fc_f32(int64_t M, int64_t N,
                       int64_t K1, const float *A1, int64_t lda1, const float *W1, int64_t ldw1,
                       int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2,
                       const float *bias, float *C, int64_t ldc, int32_t flags,
-                      float dropout_p, uint64_t seed, void *stream);
+                      float dropout_p, uint64_t seed, int64_t row_offset, void *stream);
 
 /* fp32 FC on the bf16 matrix cores (same operation and epilogue as
  * lpg_fc_f32; also the input-gradient GEMMs dZ W of its backward, with W
@@ -204,7 +207,7 @@ lpg_status lpg_fc_x3_f32(int64_t M, int64_t N,
                          int64_t K1, const float *A1, int64_t lda1, const uint16_t *W1, int64_t ldw1, int64_t ps1,
                          int64_t K2, const float *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2,
                          const float *bias, float *C, int64_t ldc, int32_t flags,
-                         float dropout_p, uint64_t seed, void *stream);
+                         float dropout_p, uint64_t seed, int64_t row_offset, void *stream);
 
 /* The exact three-way bf16 split of an fp32 matrix for lpg_fc_x3_f32:
  * plane p of dst ([rows, cols], leading dimension ldd, plane p at
@@ -227,7 +230,7 @@ lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1
                                const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
                                int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
                                float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                               int32_t hn, const float *hw, int64_t ldhw, const float *hb, float *logits,
+                               int64_t row_offset, int32_t hn, const float *hw, int64_t ldhw, const float *hb, float *logits,
                                int64_t ldl, void *workspace, void *stream);
 
 /* Weight gradient on the same arithmetic: dW[n, k] = sum_r G[r, n] X[r, k]
@@ -298,7 +301,7 @@ lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const float *g, int64
 lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1, const uint16_t *W1,
                        int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
                        const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                       void *stream);
+                       int64_t row_offset, void *stream);
 /* dst[c, r] = src[r, c] for bf16 [R, C] (R, C, lds, ldd multiples of 8, 16-byte
  * aligned): the transposed weights the c5 input gradients multiply by
  * (dX = dZ W of a Linear, arch.py:57-62 through train.py:128). */

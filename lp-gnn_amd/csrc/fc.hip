@@ -65,12 +65,14 @@ struct FcArgs {
   // flags bit 1: C holds an addend on entry, C = act(A1 W1^T + A2 W2^T + C + bias);
   // each element is read and rewritten by the lane that owns it
   int32_t accum;
+  // the dropout key of row m is row_off + m (the global node id when C holds a slice of the rows)
+  int64_t row_off;
 };
 
 __device__ __forceinline__ float epilogue(const FcArgs &a, float v, float b, int64_t row, int64_t col, bool relu) {
   if (a.bias) v = v + b;
   if (relu) v = (v < 0.f) ? 0.f : v;
-  if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+  if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
   return v;
 }
 
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
     }
     for (int64_t m = r0; m < r1; ++m) {
       const float *xr = sx + (m - r0) * KT;
-      const uint32_t rk = DROP ? drop_row_key(a.seed, m) : 0u;
+      const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + m) : 0u;
       float o[4];
       // columns in pairs: one v_pk_fma_f32 advances two independent chains
       // (a true fma per element -- the same bits as the scalar chains)
@@ -462,7 +464,8 @@ using namespace lpg;
 extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1, const float *W1,
                                  int64_t ldw1, int64_t K2, const float *A2, int64_t lda2, const float *W2,
                                  int64_t ldw2, const float *bias, float *C, int64_t ldc, int32_t flags,
-                                 float dropout_p, uint64_t seed, void *stream) {
+                                 float dropout_p, uint64_t seed, int64_t row_offset,
+                                 void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_f32: negative size");
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_f32: bad C/ldc");
@@ -474,7 +477,8 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
               "lpg_fc_f32: A/W must be 16-byte aligned");
   LPG_REQUIRE((flags & ~3) == 0, "lpg_fc_f32: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
-  FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1};
+  FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1,
+           row_offset};
   if (dropout_p > 0.f) {
     const double th = (double)dropout_p * 4294967296.0;
     a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);

@@ -53,6 +53,7 @@ struct FcB16Args {
   const uint16_t *my;
   int64_t ldy;
   float mscale;
+  int64_t row_off;  // the dropout key of row m is row_off + m
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
@@ -136,7 +137,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
               v[r] = v[r] + bf16_to_f32(*reinterpret_cast<const uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2));
             v[r] = v[r] + bb;
             if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
-            if constexpr (DROP) v[r] = drop_hash(a.seed, wrow0 + lr, col) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
+            if constexpr (DROP) v[r] = drop_hash(a.seed, a.row_off + wrow0 + lr, col) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
           }
 #pragma unroll
           for (int r = 0; r < 4; r += 2) {
@@ -189,7 +190,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
         if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
         v = v + bb;
         if (RELU) v = v < 0.f ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         a.C[row * a.ldc + col] = to_bf16_rne(v);
       }
     }
@@ -238,7 +239,7 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
 #pragma unroll
         for (int ii = 0; ii < IH; ++ii) {
           const int i = h * IH + ii;
-          const uint32_t rk = DROP ? drop_row_key(a.seed, wrow0 + i * 16 + fr) : 0u;
+          const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + wrow0 + i * 16 + fr) : 0u;
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
             float v[4];
@@ -284,7 +285,7 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
         if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
         v = v + (a.bias ? a.bias[col] : 0.f);
         if (RELU) v = v < 0.f ? 0.f : v;
-        if (RELU && a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        if (RELU && a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         a.C[row * a.ldc + col] = to_bf16_rne(v);
       }
   }
@@ -346,7 +347,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const uint32_t rk = DROP ? drop_row_key(a.seed, wrow0 + i * 16 + fr) : 0u;
+      const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + wrow0 + i * 16 + fr) : 0u;
       unsigned char *ip = img + (i * 16 + fr) * EP_PITCH + fq * 8;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -1017,7 +1018,8 @@ using namespace lpg;
 extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
                                   const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
                                   const uint16_t *W2, int64_t ldw2, const float *bias, uint16_t *C, int64_t ldc,
-                                  int32_t flags, float dropout_p, uint64_t seed, void *stream) {
+                                  int32_t flags, float dropout_p, uint64_t seed, int64_t row_offset,
+                                  void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_bf16: negative size");
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_bf16: bad C/ldc");
@@ -1030,7 +1032,8 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
   const int kernel = (flags >> 8) & 15;
   LPG_REQUIRE((flags & ~0xf03) == 0 && kernel <= kKernels, "lpg_fc_bf16: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_bf16: dropout_p %g not in [0, 1)", (double)dropout_p);
-  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1};
+  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1,
+              nullptr, 0, 1.f, row_offset};
   if (dropout_p > 0.f) {
     const double th = (double)dropout_p * 4294967296.0;
     a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);

@@ -79,6 +79,7 @@ struct X3Args {
   int64_t ldhw;
   int32_t hn;
   float *hpart;
+  int64_t row_off;  // the dropout key of row m is row_off + m (the global node id of a row slice)
 };
 
 __device__ __forceinline__ unsigned pk_bf16(float x, float y) {  // v_cvt_pk_bf16_f32: RNE, x in the low half
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
         float v = acc[i][j][r];
         if (a.bias) v = v + bb;
         if (RELU) v = (v < 0.f) ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         a.C[row * a.ldc + col] = v;
         if constexpr (HEADS) {
 #pragma unroll
@@ -574,19 +575,11 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
     if constexpr (HEADS) himg[(i * 16 + r) * HP + j * 16] = v;
   };
   if (mw + TM * 16 <= a.M && nw + BN <= a.N) {
-    // interior wave tile (wave-uniform): no per-element bounds; element (i, r, j) lives at the
-    // wave-uniform row base C + (mw + 16 i + r) ldc + nw (SGPRs) plus ONE per-lane offset
-    // 4 fg ldc + fr (the same for every i, r, j) plus the column step j * 16 as the immediate offset
-    // (a per-(i, r) 64-bit row pointer took 16 VGPRs, and the fused heads' epilogue spilled);
-    // the dropout row keys are computed once per row (the per-element forms cost ~24 VALU incl.
-    // 6 v_mul_lo_u32 and a branch per output)
-    const int64_t loff = 4 * fg * a.ldc + fr;
-    auto rp = [&](int i, int r) -> float * {
-      const uint64_t rb = (uint64_t)(a.C + (mw + i * 16 + r) * a.ldc + nw);
-      const uint64_t u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32)) << 32) |
-                         __builtin_amdgcn_readfirstlane((uint32_t)rb);
-      return reinterpret_cast<float *>(u) + loff;
-    };
+    // interior wave tile (wave-uniform): no per-element bounds, one C row pointer per (i, r) with
+    // the column step j * 16 as the store's immediate offset, the dropout row keys computed once
+    // per row (the per-element forms cost ~24 VALU incl. 6 v_mul_lo_u32 and a branch per output)
+    float *const c0 = a.C + (mw + 4 * fg) * a.ldc + nw + fr;
+    auto rp = [&](int i, int r) -> float * { return c0 + (i * 16 + r) * a.ldc; };
     if (a.accum) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -602,7 +595,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) rk[i][r] = drop_row_key(a.seed, mw + i * 16 + 4 * fg + r);
+          for (int r = 0; r < 4; ++r) rk[i][r] = drop_row_key(a.seed, a.row_off + mw + i * 16 + 4 * fg + r);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -659,7 +652,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
           float v = acc[i][j][r];
           if (a.bias) v = v + bb;
           if (RELU) v = (v < 0.f) ? 0.f : v;
-          if (a.drop_thresh) v = drop_hash(a.seed, row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+          if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
           a.C[row * a.ldc + col] = v;
           hput(i, r, j, v);
         }
@@ -988,7 +981,7 @@ static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int
                           const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
                           int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
                           float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                          X3Args *out) {
+                          int64_t row_offset, X3Args *out) {
   LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_x3_f32: bad C/ldc");
   LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "lpg_fc_x3_f32: K1, K2 must be multiples of %d (zero-pad)", BK);
   LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1 && ps1 >= N * ldw1), "lpg_fc_x3_f32: bad A1/W1");
@@ -1003,6 +996,7 @@ static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int
   *out = X3Args{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, ps1, ps2, C, ldc, 0, 0, seed, 0u, 1.f,
                 (flags >> 1) & 1};
   dropout_params(dropout_p, &out->drop_thresh, &out->drop_scale);
+  out->row_off = row_offset;
   return LPG_OK;
 }
 
@@ -1010,12 +1004,12 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
                                     const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
                                     int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
                                     float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                                    void *stream) {
+                                    int64_t row_offset, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_f32: negative size");
   if (M == 0 || N == 0) return LPG_OK;
   X3Args a;
   const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
-                                dropout_p, seed, &a);
+                                dropout_p, seed, row_offset, &a);
   if (st != LPG_OK) return st;
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
@@ -1032,7 +1026,8 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
                                           const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
                                           int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2,
                                           const float *bias, float *C, int64_t ldc, int32_t flags, float dropout_p,
-                                          uint64_t seed, int32_t hn, const float *hw, int64_t ldhw, const float *hb,
+                                          uint64_t seed, int64_t row_offset, int32_t hn, const float *hw,
+                                          int64_t ldhw, const float *hb,
                                           float *logits, int64_t ldl, void *workspace, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_heads_f32: negative size");
   if (M == 0) return LPG_OK;
@@ -1042,7 +1037,7 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   LPG_REQUIRE(workspace && aligned16(workspace), "lpg_fc_x3_heads_f32: workspace missing or not 16-byte aligned");
   X3Args a;
   const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
-                                dropout_p, seed, &a);
+                                dropout_p, seed, row_offset, &a);
   if (st != LPG_OK) return st;
   a.hw = hw;
   a.ldhw = ldhw;

@@ -113,7 +113,7 @@ def lib() -> ctypes.CDLL:
     L.lpg_spmm_bf16_tuned.argtypes = L.lpg_spmm_f32_tuned.argtypes
     L.lpg_spmm_bf16_tuned.restype = c_i32
     L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
-                             c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_p]
+                             c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_i64, c_p]
     L.lpg_fc_f32.restype = c_i32
     L.lpg_fc_bf16.argtypes = L.lpg_fc_f32.argtypes
     L.lpg_fc_bf16_relu_bwd.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
@@ -130,7 +130,7 @@ def lib() -> ctypes.CDLL:
     L.lpg_split3_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_i64, c_p]
     L.lpg_split3_f32.restype = c_i32
     L.lpg_fc_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
-                                c_i64, c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_p]
+                                c_i64, c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_i64, c_p]
     L.lpg_fc_x3_f32.restype = c_i32
     L.lpg_fc_x3_heads_workspace_bytes.argtypes = [c_i64, c_i64]
     L.lpg_fc_x3_heads_workspace_bytes.restype = c_i64

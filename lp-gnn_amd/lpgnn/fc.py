@@ -57,27 +57,33 @@ _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless th
 
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
-               accumulate: bool = False, arith: str | None = None, heads=None, kernel: int = 0):
+               accumulate: bool = False, arith: str | None = None, heads=None, kernel: int = 0,
+               row_offset: int = 0):
     """act(A1 W1^T + A2 W2^T [+ out] + bias) through lpg_fc_f32; with
     ``accumulate`` the caller's ``out`` holds the addend and is overwritten.
     ``arith`` ("fp32" | "x3", default ``ARITH``) picks the tiled kernel's arithmetic.
     ``heads`` = (Wh [<= 4, N], bh or None): also return the logits C Wh^T + bh
     -- fused into the x3 kernel's epilogue (lpg_fc_x3_heads_f32), else the
     separate Linear on C (the fp32 contract's own kernel).  ``kernel``: the x3 entries' per-call
-    kernel choice (LPG_FC_KERNEL, include/lpgnn.h; 0 = by shape; every choice gives the same bits)."""
+    kernel choice (LPG_FC_KERNEL, include/lpgnn.h; 0 = by shape; every choice gives the same bits).
+    ``row_offset``: the dropout mask keys row m as row_offset + m (the global node id of the first
+    row when this call computes a slice of a node set: the row partition)."""
     if heads is not None:
         M, N = A1.shape[0], W1.shape[0]
         k4 = lambda k: -(-k // 4) * 4
         small = 4 <= k4(A1.shape[1]) and k4(A1.shape[1]) + (0 if A2 is None else k4(A2.shape[1])) <= 16
         if (arith or ARITH) == "x3" and not small and N > 32 and heads[0].shape[0] <= 4:
-            return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, heads, kernel)
-        C = _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel)
+            return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, heads, kernel,
+                               row_offset)
+        C = _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel,
+                        row_offset=row_offset)
         return C, _fc_forward(C, heads[0], None, None, heads[1], False, arith=arith)
-    return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel)
+    return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel,
+                       row_offset=row_offset)
 
 
 def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, accumulate=False, arith=None,
-                heads=None, kernel=0):
+                heads=None, kernel=0, row_offset=0):
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -105,14 +111,14 @@ def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, acc
     flags = (1 if relu else 0) | (2 if accumulate else 0)
     if (arith or ARITH) == "x3" and not small and N > 32:
         return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags | _lib.fc_kernel(kernel), dropout_p, seed, relu,
-                      heads=heads)
+                      heads=heads, row_offset=row_offset)
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
         st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
                           K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
                           None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
                           None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags,
-                          float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
+                          float(dropout_p), int(seed) & (2**64 - 1), int(row_offset), _lib.stream_of(A1))
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_f32")
     return C
@@ -138,7 +144,8 @@ def split3(W: Tensor, transpose: bool = False) -> Tensor:
     return out
 
 
-def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=None, W2s=None, heads=None):
+def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=None, W2s=None, heads=None,
+           row_offset=0):
     """lpg_fc_x3_f32 on fp32 A and pre-split W (split here unless given); with
     ``heads`` = (Wh, bh) lpg_fc_x3_heads_f32, returning (C, logits)."""
     W1s = split3(W1) if W1s is None else W1s
@@ -148,7 +155,7 @@ def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=
             None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
             None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0, W2s.stride(0) if K2 else 0,
             None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags, float(dropout_p),
-            int(seed) & (2**64 - 1))
+            int(seed) & (2**64 - 1), int(row_offset))
     key = ("fc", M, N, A1.shape[1] + K2, ("relu" if relu else "lin") + "-x3")
     with torch.cuda.device(A1.device):
         if heads is None:
@@ -242,7 +249,8 @@ def _prep_bf16(t: Tensor | None) -> Tensor | None:
 
 def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                     relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
-                    accumulate: bool = False, key: str | None = None, mask=None, kernel: int = 0) -> Tensor:
+                    accumulate: bool = False, key: str | None = None, mask=None, kernel: int = 0,
+                    row_offset: int = 0) -> Tensor:
     """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16);
     ``accumulate`` adds the bf16 addend held in ``out`` (overwritten).
     ``mask`` = (Y, scale): an input gradient with the previous layer's ReLU/dropout backward
@@ -291,7 +299,7 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
                            K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
                            None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
                            None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags,
-                           float(dropout_p), int(seed) & (2**64 - 1), _lib.stream_of(A1))
+                           float(dropout_p), int(seed) & (2**64 - 1), int(row_offset), _lib.stream_of(A1))
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_bf16")
     return C

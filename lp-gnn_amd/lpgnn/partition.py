@@ -209,7 +209,12 @@ def plan_partition_blocks(spec, world: int, rank: int, group=None, edges=None) -
     if world > 1:
         got, recv_counts = _a2a_ids(halo, send_counts, group)
         recv_idx = got - v_lo
-        nb_glob = torch.tensor([float(np.unique(got).shape[0])])
+        # boundary = touched by >= 2 ranks (plan_partition's rule): an owned variable a remote rank
+        # touches counts if this rank's rows touch it too or a second remote rank does
+        rv, rc = np.unique(got, return_counts=True)
+        mine = np.unique(col[(col >= v_lo) & (col < v_hi)])
+        nb_loc = int(((rc >= 2) | np.isin(rv, mine, assume_unique=True)).sum())
+        nb_glob = torch.tensor([nb_loc], dtype=torch.int64)
         if dist.get_backend(group) != "gloo":
             nb_glob = nb_glob.cuda()
         dist.all_reduce(nb_glob, group=group)
@@ -294,6 +299,15 @@ class Exchange:
     def __init__(self, plan: PartitionPlan, device, group=None):
         self.n_own, self.n_local = plan.n_own, plan.n_local
         self.m, self.n = plan.m, plan.n  # global sizes: rank-independent layout decisions
+        # dropout keys (the FC's row_offset): the constraint rows are the block [row_lo, row_hi); the
+        # owned variables are keyed by their global ids when they form one contiguous range (every
+        # block plan: the bench and c4 paths), so each node draws the mask a single-GPU run draws.
+        # A general plan's owned set need not be contiguous: it keys owned row i as owned[0] + i
+        # (masks stay independent per node within a rank, not equal to the one-GPU masks).
+        self.cons_key0 = int(plan.row_lo)
+        own = plan.owned
+        self.var_key0 = int(own[0]) if own.shape[0] else 0
+        self.var_keys_global = bool(own.shape[0] == 0 or int(own[-1]) - int(own[0]) + 1 == own.shape[0])
         self.send_idx = torch.from_numpy(plan.send_idx).to(device)
         self.recv_idx = torch.from_numpy(plan.recv_idx).to(device)
         self.send_counts, self.recv_counts = list(plan.send_counts), list(plan.recv_counts)
@@ -480,18 +494,19 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
     red = ex.start_reduce(agg_r, inplace=True)  # halo partials -> owners, in flight ...
     agg_l = spmm_forward(A, right)              # ... under the purely local constraint side
     hl, hr = heads if heads is not None else (None, None)
-    left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l, heads=hl)
+    left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l, heads=hl,
+                              row_offset=ex.cons_key0)
     if hl is not None:
         left_new, logit_l = left_new
     red.finish()                                # owners' rows of agg_r now hold the full sums
     if ra:  # lin_root + bias + ReLU accumulated onto the owners' sums, in place
         right_new, agg_r = agg_r, None
         own = _fc.fc_forward(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
-                             out=right_new[:n_own], accumulate=True, heads=hr)
+                             out=right_new[:n_own], accumulate=True, heads=hr, row_offset=ex.var_key0)
     else:
         right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
         own = _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
-                             out=right_new[:n_own], heads=hr)
+                             out=right_new[:n_own], heads=hr, row_offset=ex.var_key0)
     ex.start_broadcast_(right_new).finish()
     logits = None
     if heads is not None:
@@ -853,6 +868,33 @@ def build_bench_job(args, rank: int, world: int, device) -> BenchJob:
     wl = (f"{kind} {spec.m}x{spec.n} nnz={spec.nnz} ({spec.blocks} row blocks, rho={spec.rho}) row-partitioned "
           f"over {world} GPU(s), GCN_FC(8,8,hids={args.hids},depth={args.depth}) fwd+bwd+Adam")
     return BenchJob(step, plan.nnz_local, wl, plan, batch, spec)
+
+
+def rho_sweep(args, rank: int, world: int, rhos, F: int) -> list:
+    """SURVEY.md §8d/§8e's locality sweep for the bench graph: for each rho (the fraction of a
+    block's edges on other blocks' variables) this rank generates and plans its own blocks again
+    and the ranks pool their boundary counts.  Per rho: boundary variables (touched by >= 2
+    ranks), halo rows per rank, rows each rank sends + receives in one exchange, and the MiB that
+    moves per exchange at width F (fp32) on the busiest rank -- the plan, not a timing."""
+    import copy
+
+    out = []
+    for rho in rhos:
+        a = copy.copy(args)
+        a.rho = float(rho)
+        spec = bench_spec(a, world)
+        plan = plan_partition_blocks(spec, world, rank)
+        mine = [int(plan.halo.shape[0]), int(plan.n_own), int(sum(plan.send_counts)), int(sum(plan.recv_counts)),
+                sum(1 for c in plan.send_counts if c) + sum(1 for c in plan.recv_counts if c)]
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        rows = [h[2] + h[3] for h in every]
+        out.append({"rho": float(rho), "boundary_vars_global": plan.n_boundary_global,
+                    "halo_rows_per_rank": [h[0] for h in every], "owned_vars_per_rank": [h[1] for h in every],
+                    "exchange_rows_per_rank": rows, "peers_max": max(h[4] for h in every),
+                    "mib_per_exchange_max": max(rows) * F * 4 / 2 ** 20})
+        del plan
+    return out
 
 
 def time_exchange(ex: Exchange, F: int, device, reps: int = 5) -> dict:

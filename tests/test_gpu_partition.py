@@ -123,7 +123,10 @@ def _worker_dropout(rank, world, port, out_dir):
                          {k: p.grad.clone() for k, p in model.named_parameters()})
         conv.FUSE_HEAD_FWD = True
         assert abs(out[True][0] - out[False][0]) < 1e-5
-        torch.testing.assert_close(out[True][1], out[False][1], rtol=1e-5, atol=1e-5)
+        # the logits after add_knowledge: the fused heads sum each row in a different order than the
+        # separate Linear (equal to fp32 rounding, test_x3_fused_heads_match_separate_linear), and
+        # normalize()'s 10/|h| amplifies that where |h| is small -- the north star's 1e-4 bar
+        torch.testing.assert_close(out[True][1], out[False][1], rtol=0, atol=1e-4)
         for k, v in out[True][2].items():
             torch.testing.assert_close(v, out[False][2][k], rtol=1e-4, atol=1e-6, msg=k)
         open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
@@ -162,3 +165,93 @@ def test_bench_partitioned_path_runs():
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
     assert d["value"] > 0 and d["config"]["parallelism"].startswith("rowpart")
+
+
+# ------------------------------------------------- c4 (BASELINE.json configs[3]) on the HIP path
+def _c4_small():
+    from lpgnn import synth
+
+    return synth.c4_spec(scale=50, seed=3)  # 40K x 80K, nnz 800K: the c4 generator at 1/50 size
+
+
+def _worker_c4(rank, world, port, out_dir, mode):
+    """c4's generator and its rank-local planner, HIP kernels on every rank (ranks share the GPU,
+    gloo), against mode "oracle": the single-graph oracle evaluation (MKL fp32, the reference's
+    arithmetic; dropout 0), or mode "dropout": the single-GPU HIP model in train mode with
+    dropout 0.1 and the same seeds -- identical masks because the FC epilogues key dropout on
+    global node ids (constraint row_lo + i, owned variables by their global ids)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, partition as part
+        from lpgnn.train import balanced
+        from oracle import model_ref as O
+
+        dev = "cuda:0"
+        spec = _c4_small()
+        plan = part.plan_partition_blocks(spec, world, rank)
+        assert plan.owned[-1] - plan.owned[0] + 1 == plan.n_own  # block plans: contiguous owners
+        batch = part.make_block_batch(spec, plan, device=dev)
+        dp = 0.1 if mode == "dropout" else 0.0
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=256, depth=3, dp=dp).to(dev).train()
+        sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        torch.manual_seed(7)
+        lc, lv = model(batch)
+        loss = part.balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.var_owned)
+        loss.backward()
+        part.all_reduce_grads(model)
+        tot = loss.detach().clone()
+        part._all_reduce_(tot)
+        lc, lv = lc.detach().cpu(), lv.detach().cpu()
+        grads = {k: p.grad.detach().cpu() for k, p in model.named_parameters()}
+        g = spec.full()
+        if mode == "oracle":
+            A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
+            AT = O.csr_transpose(*A, g.m, g.n)
+            params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in sd0.items()}
+            rc, rv = O.gcn_fc_forward(params, torch.from_numpy(g.x_s), torch.from_numpy(g.x_t), A, AT, 3)
+            rloss = O.balanced(rc, rv, torch.from_numpy(g.y_s), torch.from_numpy(g.y_t))
+            rloss.backward()
+            rgrads = {k: params[k].grad for k in grads}
+            rc, rv, rloss = rc.detach(), rv.detach(), rloss.item()
+        else:
+            adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
+            b = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(dev), x_t=torch.from_numpy(g.x_t).to(dev),
+                               y_s=torch.from_numpy(g.y_s).to(dev), y_t=torch.from_numpy(g.y_t).to(dev),
+                               edge_index=adj, s_bs=g.m, t_bs=g.n)
+            ref = GCN_FC(8, 8, hids=256, depth=3, dp=dp).to(dev).train()
+            ref.load_state_dict(sd0)
+            torch.manual_seed(7)  # the same dropout seeds as the partitioned forward
+            rc, rv = ref(b)
+            rl = balanced(rc, rv, b.y_s, b.y_t)
+            rl.backward()
+            rgrads = {k: p.grad.detach().cpu() for k, p in ref.named_parameters()}
+            rc, rv, rloss = rc.detach().cpu(), rv.detach().cpu(), rl.item()
+        # owned AND halo rows (halo = the owners' values), the north star's 1e-4 on the logits
+        np.testing.assert_allclose(lc.numpy(), rc.numpy()[plan.row_lo:plan.row_hi], atol=1e-4)
+        np.testing.assert_allclose(lv.numpy(), rv.numpy()[plan.local_vars], atol=1e-4)
+        assert abs(tot.item() - rloss) < 1e-4 * max(1.0, abs(rloss)), (tot.item(), rloss)
+        for k, v in grads.items():
+            np.testing.assert_allclose(v.numpy(), rgrads[k].numpy(), rtol=2e-3, atol=2e-5, err_msg=k)
+        _check_halo_logits_are_owners(plan, lv, world)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write(str(tot.item()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_c4_reduced_two_ranks_hip_vs_oracle(tmp_path):
+    """c4 at 1/50 size through the HIP partitioned path (2 ranks): owned and halo logits, the
+    loss and every gradient against the single-graph oracle (not against the HIP single-GPU run)."""
+    mp.spawn(_worker_c4, args=(2, _free_port(), str(tmp_path), "oracle"), nprocs=2, join=True)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+
+
+@pytest.mark.timeout(600)
+def test_c4_reduced_dropout_two_ranks_equal_one_gpu(tmp_path):
+    """Train mode with dropout 0.1: N = 2 equals the one-GPU model within fp32 tolerance -- the
+    dropout masks are keyed on global node ids, so both draw the same mask for every node."""
+    mp.spawn(_worker_c4, args=(2, _free_port(), str(tmp_path), "dropout"), nprocs=2, join=True)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()

@@ -172,7 +172,7 @@ def _check_block_plan(plan, g, spec, world, rank):
     bounds = np.arange(world + 1, dtype=np.int64) * per * spec.mb
     ref = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank, bounds=bounds,
                               owner=part.block_owner(spec, world))
-    for f in ("row_lo", "row_hi", "send_counts", "recv_counts"):
+    for f in ("row_lo", "row_hi", "send_counts", "recv_counts", "n_boundary_global"):
         assert getattr(plan, f) == getattr(ref, f), f
     for f in ("owned", "halo", "e_row", "e_gcol", "e_col", "e_val", "send_idx", "recv_idx"):
         assert np.array_equal(getattr(plan, f), getattr(ref, f)), f
@@ -208,3 +208,37 @@ def test_c4_reduced_two_ranks_match_single_graph(tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), "c4"), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"ok{r}").exists()
+
+
+def _worker_rho(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from types import SimpleNamespace
+
+        import lpgnn.partition as part
+
+        args = SimpleNamespace(config="c4", m=40_000, n=80_000, nnz=800_000, rho=0.02)
+        sw = part.rho_sweep(args, rank, world, [0.0, 0.02, 0.1, 1.0], 1024)
+        assert [s["rho"] for s in sw] == [0.0, 0.02, 0.1, 1.0]
+        assert sw[0]["boundary_vars_global"] == 0 and sw[0]["halo_rows_per_rank"] == [0] * world
+        assert sw[0]["exchange_rows_per_rank"] == [0] * world
+        b = [s["boundary_vars_global"] for s in sw]
+        assert b[0] < b[1] < b[2] < b[3], b
+        for s in sw:  # every rank reports the same pooled numbers; owned variables tile [0, n)
+            assert sum(s["owned_vars_per_rank"]) == args.n
+        # the sweep's plan at the bench rho is the bench's own plan
+        spec = part.bench_spec(args, world)
+        plan = part.plan_partition_blocks(spec, world, rank)
+        assert sw[1]["halo_rows_per_rank"][rank] == plan.halo.shape[0]
+        assert sw[1]["boundary_vars_global"] == plan.n_boundary_global
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rho_sweep_boundary_counts(tmp_path):
+    """bench.py's c4 rho sweep: no boundary at rho = 0, growing with rho, pooled
+    identically on every rank, equal to the bench's own plan at the bench rho."""
+    mp.spawn(_worker_rho, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
