@@ -214,22 +214,23 @@ def process_raw(raw):
     return [A.row, A.col, A.data, c_feas, v_feas, y_s, y_t, ncons + nvars]
 
 
-def load_processed(path, device="cpu", thresh_num=np.inf):
+def load_processed(path, device="cpu", thresh_num=np.inf, record=None):
     """LPDataset.get (dataset.py:229-264) + MyToBipartite (268-332) for one
-    processed file -> a BipartiteBatch with the dual CSR packed on `device`."""
+    processed file -> a BipartiteBatch with the dual CSR packed on `device`.
+    ``record``: the file's already-decoded msgpack record (no second read)."""
     from .data import MyToBipartite, lp_to_unipartite
 
-    row, col, A_data, c_feas, v_feas, y_s, y_t, nnodes = msgpack_load(path)
+    row, col, A_data, c_feas, v_feas, y_s, y_t, nnodes = msgpack_load(path) if record is None else record
     data = lp_to_unipartite(row, col, A_data, c_feas, v_feas, y_s, y_t, processed_path=str(path))
     assert data.num_nodes == int(nnodes)
     return MyToBipartite(dev=device, thresh_num=thresh_num)(data)
 
 
-def load_bipartite(path, device="cpu"):
+def load_bipartite(path, device="cpu", record=None):
     """load_processed without the to_undirected / split round trip: the .pk
     record straight to a BipartiteBatch (data.bipartite_from_lp)."""
     from .data import bipartite_from_lp
 
-    row, col, A_data, c_feas, v_feas, y_s, y_t, nnodes = msgpack_load(path)
+    row, col, A_data, c_feas, v_feas, y_s, y_t, nnodes = msgpack_load(path) if record is None else record
     assert int(nnodes) == np.asarray(c_feas).shape[0] + np.asarray(v_feas).shape[0]
     return bipartite_from_lp(row, col, A_data, c_feas, v_feas, y_s, y_t, device, processed_path=str(path))

@@ -23,10 +23,12 @@ What is different, and why:
 * accuracy per step is computed on the device (val.accuracy_device, no host
   sync); the host sklearn path is used only by ``validation``;
 * ``--fp16 1`` (utils.py:770; val.py:269 ``model.half()``) selects the
-  16-bit inference path of this build, which is bf16 (same storage width,
-  fp32 exponent range; the bf16 MFMA kernels of the c5 configuration).  A
-  model or batch converted to torch.float16 by hand is rejected by
-  GCN_FC.forward instead of being silently promoted;
+  16-bit inference path of this build for VALIDATION only, as in the
+  reference (train.py never converts the model): bf16 (same storage width,
+  fp32 exponent range; the bf16 MFMA kernels of the c5 configuration).
+  Training stays fp32 with the flag set.  A model or batch converted to
+  torch.float16 by hand is rejected by GCN_FC.forward instead of being
+  silently promoted;
 * ``--replicas`` (torch.distributed initialised, world > 1): data parallel
   over graphs ("many small LPs: replicas only").  Every rank
   walks the same shuffled epoch order and takes every world-th graph; the
@@ -66,6 +68,7 @@ class LPDataset:
         self.raw_dir = os.path.join(self.root, "raw")
         self._files = self._file_names()
         self._indices = list(range(len(self._files))) if indices is None else list(indices)
+        self._nnz = {}  # file index -> edge count, learned on first load (shared by subsets)
 
     def _file_names(self):
         """dataset.py:160-168: the longer listing of raw/ and processed/,
@@ -102,21 +105,28 @@ class LPDataset:
         return os.path.join(self.processed_dir, self._files[self._indices[i]])
 
     def nnz(self, i: int) -> int:
+        """Edge count of graph i (the file is read once; the count is cached)."""
         from . import lpio
 
-        return int(np.asarray(lpio.msgpack_load(self.path(i))[0]).shape[0])
+        f = self._indices[i]
+        if f not in self._nnz:
+            self._nnz[f] = int(np.asarray(lpio.msgpack_load(self.path(i))[0]).shape[0])
+        return self._nnz[f]
 
     def __getitem__(self, idx):
         if isinstance(idx, (list, tuple, np.ndarray)):
             return LPDataset._subset(self, [self._indices[int(i)] for i in idx])
         from . import lpio
 
-        p = self.path(int(idx))
+        i = int(idx)
+        p = self.path(i)
+        rec = lpio.msgpack_load(p)  # one read and decode per graph and epoch
+        self._nnz[self._indices[i]] = int(np.asarray(rec[0]).shape[0])
         # above the threshold the reference keeps the homogeneous graph (dataset.py:280-281);
         # the direct loader packs the dual CSR on the device without the undirected round trip
-        if self.direct and self.nnz(int(idx)) <= self.thresh_num:
-            return lpio.load_bipartite(p, device=self.device)
-        return lpio.load_processed(p, device=self.device, thresh_num=self.thresh_num)
+        if self.direct and self._nnz[self._indices[i]] <= self.thresh_num:
+            return lpio.load_bipartite(p, device=self.device, record=rec)
+        return lpio.load_processed(p, device=self.device, thresh_num=self.thresh_num, record=rec)
 
     @staticmethod
     def _subset(ds, indices):
@@ -217,12 +227,13 @@ def parse_args(argv=None):
 
 
 # ------------------------------------------------------------------- model
-def make_model(args):
-    """eval(args.arch) (train.py:79) + --load_from (train.py:80) + --fp16 (val.py:269)."""
+def make_model(args, for_eval: bool = False):
+    """eval(args.arch) (train.py:79) + --load_from (train.py:80); --fp16 (val.py:269) only for an
+    evaluation model (``for_eval``): the reference's train.py trains in fp32 whatever the flag."""
     from .arch import build_model
 
     model = build_model(args.arch)
-    if args.fp16:
+    if args.fp16 and for_eval:
         model.set_compute_dtype(torch.bfloat16)
     if str(args.load_from).lower() != "none":
         model.load(args.load_from)
@@ -350,10 +361,16 @@ def validation(model, ds, args):
 def main(argv=None):
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(message)s")
     args = parse_args(argv)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1 and not args.replicas:
+        # under a launcher without --replicas every rank would train the full schedule and write
+        # args.json / mdl.pth into the same directory: refuse instead
+        raise SystemExit(f"WORLD_SIZE={world_env}: pass --replicas 1 for data-parallel training over graphs "
+                         "(or run one process)")
     if args.replicas:
         import torch.distributed as dist
 
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
+        if world_env > 1 and not dist.is_initialized():
             backend = "nccl" if torch.cuda.is_available() else "gloo"
             dist.init_process_group(backend)
             if torch.cuda.is_available():
@@ -366,7 +383,7 @@ def main(argv=None):
     ds = LPDataset(args.dataset_processed_prefix, thresh_num=args.edge_num_thresh, device=args.dev)
     _, val_ds = split_train_val(ds, args.seed)
     eval_ds = ds if args.split == "trainval" else val_ds
-    model = make_model(args)
+    model = make_model(args, for_eval=True)
     _, avg_acc, rows = validation(model, eval_ds, args)
     print(json.dumps({"avg_acc": avg_acc, "graphs": rows}))
     return 0

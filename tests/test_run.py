@@ -181,3 +181,40 @@ def test_data_parallel_replicas_gloo(tmp_path):
     opt.step()
     for k, v in model.state_dict().items():
         torch.testing.assert_close(p0[k], v, rtol=1e-6, atol=1e-7, msg=k)
+
+
+def test_fp16_flag_is_validation_only(tmp_path):
+    """--fp16 (utils.py:770) changes only the evaluation model (val.py:269 model.half(); here bf16):
+    train.py trains in fp32 whatever the flag, and so does run_exp's model."""
+    from lpgnn import run
+
+    a = _args(tmp_path, "--fp16", "1", "--arch", "GCN_FC(8,8,hids=16,depth=3)")
+    assert run.make_model(a).compute_dtype == torch.float32
+    assert run.make_model(a, for_eval=True).compute_dtype == torch.bfloat16
+    b = _args(tmp_path, "--arch", "GCN_FC(8,8,hids=16,depth=3)")
+    assert run.make_model(b, for_eval=True).compute_dtype == torch.float32
+
+
+def test_dataset_reads_each_graph_once(tmp_path, monkeypatch):
+    """LPDataset decodes a .pk file once per __getitem__ (the nnz threshold test reuses the record)."""
+    from lpgnn import lpio, run
+
+    root = write_dataset(str(tmp_path / "data"))
+    ds = run.LPDataset(root)
+    calls = []
+    real = lpio.msgpack_load
+    monkeypatch.setattr(lpio, "msgpack_load", lambda p: calls.append(p) or real(p))
+    g = ds[1]
+    assert len(calls) == 1 and hasattr(g, "x_s")
+    assert ds.nnz(1) == g.edge_index.nnz() and len(calls) == 1
+
+
+def test_world_size_without_replicas_is_refused(tmp_path, monkeypatch):
+    """Under a launcher (WORLD_SIZE > 1) without --replicas every rank would train the whole
+    schedule into the same log directory: main() refuses."""
+    from lpgnn import run
+
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit, match="--replicas"):
+        run.main(["train", "--dataset", "synth", "--data_prefix", str(tmp_path / "d"), "--log_prefix",
+                  str(tmp_path / "r")])
