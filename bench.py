@@ -139,6 +139,32 @@ def cpu_baseline(g, hids, depth, steps):
     return dt, threads
 
 
+def cpu_inference(g, hids, depth, steps, bf16=False):
+    """The oracle's eval-mode forward (C spmm_cpu loop + torch CPU GEMMs, fp32: the reference's
+    CPU arithmetic) + inference_gnn (val.py:106-124) on this host, `steps` graphs after one
+    untimed warm-up -- the reference's timed inference path (scripts/pred_basis.py:113-118)."""
+    from oracle import model_ref as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = min(threads, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
+    AT = O.csr_transpose(*A, g.m, g.n)
+    sd = O.init_state_dict(8, 8, hids, depth)
+    x_s, x_t = torch.from_numpy(g.x_s), torch.from_numpy(g.x_t)
+
+    def infer():
+        with torch.no_grad():
+            lc, lv = O.gcn_fc_forward(sd, x_s, x_t, A, AT, depth)
+            return O.inference_gnn(torch.cat((lc, lv)), g.m)
+
+    infer()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        infer()
+    return (time.perf_counter() - t0) / steps, threads
+
+
 def cpu_spmm(g, F, reps=3):
     """SURVEY.md §8d's two CPU SpMM numbers at F = hid, per direction (median of
     `reps`): (1) the oracle's C restatement of torch_sparse spmm_cpu (OpenMP,
@@ -177,8 +203,9 @@ def cpu_spmm(g, F, reps=3):
 def workload_name(args) -> str:
     dt = ", bf16" if args.bf16 else ""
     kind = "synthetic block LP (8 row blocks, rho=%g)" % args.rho if args.config == "c4" else "synthetic LP"
+    what = "eval forward + inference_gnn" if getattr(args, "inference", False) else "fwd+bwd+Adam"
     return (f"{args.config}: {kind} {args.m}x{args.n} nnz={args.nnz}, "
-            f"GCN_FC(8,8,hids={args.hids},depth={args.depth}{dt}) fwd+bwd+Adam")
+            f"GCN_FC(8,8,hids={args.hids},depth={args.depth}{dt}) {what}")
 
 
 def _free_port() -> int:
@@ -232,6 +259,8 @@ def main():
         return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
+    if args.inference and (args.gpus > 1 or args.partitioned):
+        raise SystemExit("--inference times the one-GPU eval path (the reference's scripts/pred_basis.py)")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -277,8 +306,21 @@ def main():
         torch.manual_seed(0)
         model = GCN_FC(8, 8, hids=args.hids, depth=args.depth,
                        compute_dtype=torch.bfloat16 if args.bf16 else torch.float32).to(dev)
-        opt, _ = make_optimizer(model)
-        step = lambda: train_step(model, batch, opt)
+        if args.inference:
+            # the reference's timed path (scripts/pred_basis.py:113-118, 169-173): eval-mode
+            # model(batch) + inference_gnn on the concatenated logits (val.py:106-124, with its
+            # invariant checks), one graph per step
+            from lpgnn.val import inference_gnn
+
+            model.eval()
+
+            def step():
+                with torch.no_grad():
+                    lc, lv = model(batch)
+                    return inference_gnn(torch.cat((lc, lv), 0), g.m)
+        else:
+            opt, _ = make_optimizer(model)
+            step = lambda: train_step(model, batch, opt)
         local_nnz = g.nnz
         workload = workload_name(args)
         parallelism = "single"
@@ -406,7 +448,18 @@ def main():
     }
     if exch is not None:
         out["exchange"] = exch
-    if rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None and args.config == "c2":
+    if args.inference:
+        out["mode"] = "inference: eval-mode model(batch) + inference_gnn (scripts/pred_basis.py:113-118)"
+        out["ms_per_graph"] = out["ms_per_step"]
+    if (rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None
+            and args.inference):
+        cdt, threads = cpu_inference(g, args.hids, args.depth, args.cpu_steps)
+        out["cpu_baseline"] = {"value": edges_local / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
+                               "sample": f"{args.cpu_steps} eval forward(s) + inference_gnn of the same "
+                                         f"{args.config} graph after one untimed warm-up: oracle C spmm_cpu loop "
+                                         f"(OpenMP) + torch CPU GEMMs in fp32, {cdt:.2f} s/graph",
+                               "s_per_step": cdt}
+    elif rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None and args.config == "c2":
         cdt, threads = cpu_baseline(g, args.hids, args.depth, args.cpu_steps)
         out["cpu_baseline"] = {"value": edges_local / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
                                "sample": f"{args.cpu_steps} full fwd+bwd+Adam step(s) of the same c2 workload after one "

@@ -214,39 +214,57 @@ def test_c2_training_step_grads_vs_oracle_autograd(arith, monkeypatch):
 
 # c5 tolerance: bf16 activations (8-bit significand, relative rounding 2^-9) through 6 layers;
 # the knowledge-normalised logits live in [-20, 10].
-# Round-2 measurement: mean 0.032, p99 0.18, argmax agreement 0.9976.  A node whose raw head output
-# |h| is small is amplified by add_knowledge's 10/|h| (the same effect as the c2 test's, at bf16's
-# 2^-9 instead of fp32's 2^-24), so even a top-2 gap of 1.0 can flip there: a rate, not all-equal.
-C5_MEAN, C5_P99, C5_ARGMAX, C5_ARGMAX_CLEAR = 0.05, 0.25, 0.995, 0.999
+# Round-2 measurement: mean 0.032, p99 0.18, argmax agreement 0.9976.  Argmax flips are explained
+# node by node with the c2 test's method: a node whose raw head output |h| is small is amplified by
+# add_knowledge's 10 h / |h| (Lipschitz constant 10 * 2 / |h|), so a bf16-sized head difference can
+# move its logits by more than a top-2 gap of 1 -- and only there.
+C5_MEAN, C5_P99, C5_ARGMAX = 0.05, 0.25, 0.995
+C5_HEAD_REL = 0.02        # relative Frobenius error of the heads h (before add_knowledge)
+C5_CLEAR_FLIPS_MAX = 30   # argmax flips where MKL's top-2 gap > 1 (round 2: ~3 of 300 000)
 
 
 def test_c5_bf16_logits_and_step_vs_fp32_oracle(monkeypatch):
     """BASELINE configs[4] at its full size: GCN_FC(8,8,hids=2048,depth=6) in
     bf16 on the c2 graph vs the oracle's fp32 MKL evaluation (logits: mean
-    |d| <= 0.05, p99 <= 0.25, argmax agreement >= 99.5 % overall and
-    >= 99.9 % where MKL's top-2 gap exceeds 1.0), then one training step: finite fp32
+    |d| <= 0.05, p99 <= 0.25, argmax agreement >= 99.5 % overall; the heads
+    within 2 % relative; EVERY argmax flip where MKL's top-2 gap exceeds 1.0
+    explained by add_knowledge's amplification of that node's own head
+    difference, and their number bounded), then one training step: finite fp32
     master-weight gradients with cosine >= 0.95 to the oracle's autograd."""
     from lpgnn.train import balanced
 
     r32 = _oracle(2048, 6, torch.float32, True)
     model = _model(2048, 6, dtype=torch.bfloat16, dp=0.0)
     batch = _batch()
-    model.eval()
-    with torch.no_grad():
-        got = torch.cat(model(batch)).cpu().double()
-    ref = r32["logits"].double()
+    got, heads = _hip_eval_with_heads(model, batch, monkeypatch)
+    ref, ref_h = r32["logits"].double(), r32["heads"].double()
     d = (got - ref).abs().flatten()
     agree = (got.argmax(-1) == ref.argmax(-1)).double().mean().item()
-    top2 = ref.topk(2, dim=-1).values
-    clear = (top2[:, 0] - top2[:, 1]) > 1.0
+    dh_rel = ((heads - ref_h).norm() / ref_h.norm()).item()
     print(f"c5 bf16 vs fp32 MKL: mean |d| {d.mean():.3e}, p99 {torch.quantile(d[:1 << 24], 0.99):.3e}, "
-          f"max {d.max():.3e}; argmax agreement {agree:.5f}")
+          f"max {d.max():.3e}; argmax agreement {agree:.5f}; heads rel. error {dh_rel:.3e}, "
+          f"max |dh| {(heads - ref_h).abs().max():.3e}")
     assert torch.isfinite(got).all()
     assert d.mean().item() <= C5_MEAN and torch.quantile(d[:1 << 24], 0.99).item() <= C5_P99
     assert agree >= C5_ARGMAX
-    agree_clear = (got.argmax(-1)[clear] == ref.argmax(-1)[clear]).double().mean().item()
-    print(f"c5: argmax agreement where MKL's top-2 gap > 1: {agree_clear:.5f} over {int(clear.sum())} nodes")
-    assert agree_clear >= C5_ARGMAX_CLEAR
+    assert dh_rel <= C5_HEAD_REL
+    # every flip where MKL's top-2 gap exceeds 1: the node's logit change is within the
+    # normalisation's Lipschitz bound of its own head change, 10 * 2 |dh| / |h| -- so it is a
+    # small-|h| node (a flip needs |d| >= gap / 2, hence |h| <= 40 |dh| / gap)
+    top2 = ref.topk(2, dim=-1).values
+    gap = top2[:, 0] - top2[:, 1]
+    clear = gap > 1.0
+    flip = clear & (got.argmax(-1) != ref.argmax(-1))
+    dn = (got - ref).abs().max(-1).values
+    hn = ref_h.norm(dim=-1)
+    lip = 10 * 2 * (heads - ref_h).norm(dim=-1) / hn * (1 + 1e-3) + 1e-3
+    idx = flip.nonzero().flatten()
+    print(f"c5: argmax flips where MKL's top-2 gap > 1: {int(flip.sum())} of {int(clear.sum())} nodes"
+          + "".join(f"; node {int(i)}: gap {gap[i]:.3f} |d| {dn[i]:.3f} |h| {hn[i]:.3e} |dh| "
+                    f"{(heads[i] - ref_h[i]).norm():.3e} bound {lip[i]:.3f}" for i in idx[:8]))
+    assert int(flip.sum()) <= C5_CLEAR_FLIPS_MAX
+    assert bool((dn[flip] <= lip[flip]).all()), "an argmax flip not explained by add_knowledge's amplification"
+    assert bool((hn[flip] <= 40 * (heads - ref_h).norm(dim=-1)[flip] / gap[flip] * (1 + 1e-3) + 1e-6).all())
     model.train()
     lc, lv = model(batch)
     loss = balanced(lc, lv, batch.y_s, batch.y_t)
