@@ -297,7 +297,11 @@ lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const float *g, int64
  * v_mfma_f32_16x16x32_bf16, fp32 bias, same epilogue (ReLU, fused dropout
  * with the same mask function), C stored as bf16 (round to nearest even).
  * flags as lpg_fc_f32 (bit 1: C holds a bf16 addend, added in fp32 before
- * the bias). */
+ * the bias).  Narrow inputs (conv1's LP features: 4 <= K1, K1 + K2 <= 16,
+ * multiples of 4, N and ldc multiples of 4, C 8-byte aligned; no padding)
+ * run a streaming kernel: one fp32 fma chain per output over the exact
+ * bf16 products, the same epilogue -- equal to the MFMA kernel on the padded
+ * operands up to fp32 summation order. */
 lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1, const uint16_t *W1,
                        int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
                        const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
@@ -357,6 +361,42 @@ lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float
 lpg_status lpg_heads_relu_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W,
                                   const float *Y, int64_t ldy, float scale, float *dZ, int64_t lddz, float *dW,
                                   float *db, float *dbY, void *workspace, void *stream);
+
+/* bf16 twin of lpg_relu_wgrad_smallk_f32 (c5 conv1, arch.py:170 through
+ * train.py:128): g, y, A1, A2 bf16 bit patterns; dW1, dW2, db fp32.  y == NULL:
+ * g already is dZ (the next layer's input gradient folded this layer's ReLU /
+ * dropout backward into its store, lpg_fc_bf16_relu_bwd); else dZ = (y > 0) ?
+ * RNE_bf16(g * scale) : 0 on the fly (the bits of lpg_relu_bwd_colsum_bf16).
+ * One read of the gradient gives dW1, dW2 and db (db may be NULL).  N, ldg,
+ * ldy multiples of 4, g / y 8-byte aligned; workspace
+ * lpg_wgrad_smallk_workspace_bytes(M, N, K1 + K2), 16-byte aligned. */
+lpg_status lpg_relu_wgrad_smallk_bf16(int64_t M, int64_t N, const uint16_t *g, int64_t ldg, const uint16_t *y,
+                                      int64_t ldy, float scale, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                      int64_t K2, const uint16_t *A2, int64_t lda2, float *dW1, float *dW2, float *db,
+                                      void *workspace, void *stream);
+
+/* The heads' forward in bf16 (lin_left / lin_right of the c5 model,
+ * arch.py:175-176, 190): out[m, c] = RNE_bf16(sum_k H[m, k] W[c, k] + bias[c])
+ * for 1 <= N <= 4, 8 <= K <= 2048 (K, ldh multiples of 8; H bf16 and W fp32
+ * holding the bf16 weights, both 16-byte aligned; bias fp32 or NULL; out bf16
+ * [M, N], leading dimension ldo).  One streaming pass over H; the MFMA FC on N
+ * zero-padded to 64 sums the same exact products in another order. */
+lpg_status lpg_linear_small_fwd_bf16(int64_t M, int64_t K, int64_t N, const uint16_t *H, int64_t ldh, const float *W,
+                                     const float *bias, uint16_t *out, int64_t ldo, void *stream);
+
+/* The heads' backward in bf16, one pass over the layer output H [M, K] (bf16):
+ *   dH[m, k] = RNE_bf16(sum_c G[m, c] W[c, k]); with mask != 0 through the
+ *              producing layer's ReLU/dropout backward, (H > 0) ? RNE_bf16(dH * scale) : 0
+ *              (the layer's dZ, bitwise lpg_fc_bf16 + lpg_relu_bwd_colsum_bf16's rule);
+ *   dW = G^T H (fp32 [N, K]), db = sum_m G[m, :]  (db may be NULL),
+ *   dbY[k] = sum_m dH[m, k] when dbY != NULL: bitwise lpg_colsum_bf16 on the stored dH.
+ * G [M, N] fp32 (ldg >= N), W [N, K] fp32 contiguous (the bf16 weights), 1 <= N <= 4;
+ * K, ldh, lddh multiples of 8, W / H / dH 16-byte aligned; workspace
+ * lpg_heads_bwd_bf16_workspace_bytes(M, K, N), 16-byte aligned. */
+int64_t lpg_heads_bwd_bf16_workspace_bytes(int64_t M, int64_t K, int64_t N);
+lpg_status lpg_heads_bwd_bf16(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W,
+                              const uint16_t *H, int64_t ldh, int32_t mask, float scale, uint16_t *dH, int64_t lddh,
+                              float *dW, float *db, float *dbY, void *workspace, void *stream);
 
 /* ---- balanced loss (train.py:39-46) ---------------------------------------- */
 

@@ -7,14 +7,15 @@
 //   lpg_relu_wgrad_smallk_f32 the same from (g, y) with the ReLU/dropout backward and db fused (dZ never stored)
 //   lpg_linear_small_bwd_f32  the heads' backward (N = 3 outputs): dH = G W, dW = G^T H, db = sum G
 //
-// All are row-block kernels: a block owns R consecutive rows and all columns
-// (256 threads x float4 = 1024 columns per pass, rows unrolled by 4 so each
-// thread keeps 4+ loads in flight), and writes one row of per-block partial
-// sums.  The partials are then added in a fixed order -- a fold into
-// kFold segment sums (many blocks, coalesced), then a short final pass --
-// so results are deterministic run to run, with no atomics.
+// plus the c5 (bf16) twins and the bf16 heads' forward.  Row-block kernels: a block owns a range
+// of rows and 16 B of columns per thread, streams its rows with the next group's loads issued
+// before the current group's arithmetic, and writes one row of per-block partial sums.  The
+// partials are then added in a fixed order -- a fold into kFold segment sums (many blocks,
+// coalesced), then a short final pass -- so results are deterministic run to run, with no atomics.
 #include "common.h"
 #include "fc_common.h"
+
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -23,22 +24,7 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int kRowsColsum = 64;
-#ifndef LPG_WGRAD_ROWS
-#define LPG_WGRAD_ROWS 256
-#endif
-#ifndef LPG_WGRAD_UNROLL
-#define LPG_WGRAD_UNROLL 8  // rows of dZ (or g, y) in flight per thread; 4 -> 8 measured 0.61 -> 0.36 ms at 200K rows
-#endif
-constexpr int kRowsWgrad = LPG_WGRAD_ROWS;
-constexpr int kUnrollWgrad = LPG_WGRAD_UNROLL;
-#ifndef LPG_LINEAR_UNROLL
-#define LPG_LINEAR_UNROLL 4
-#endif
-#ifndef LPG_LINEAR_ROWS
-#define LPG_LINEAR_ROWS 128
-#endif
-constexpr int kRowsLinear = LPG_LINEAR_ROWS;
-constexpr int kUnrollLinear = LPG_LINEAR_UNROLL;
+constexpr int kRowsLinear = 128;  // heads_bwd_p1 rows per block (two 64-row column-sum chunks)
 constexpr int kMaxSmallK = 16;
 constexpr int kSmallNMax = 4;
 constexpr int64_t kFold = 64;
@@ -93,6 +79,9 @@ __global__ __launch_bounds__(kT) void relu_bwd_colsum_p1(int64_t M, int64_t N, c
 // loads), 2048 per pass; dZ = RNE(bf16)(g * scale) where y > 0, the value
 // torch's bf16 `g * scale` gives; db sums the rounded dZ in fp32.
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {  // RNE, v_cvt_pk_bf16_f32
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(lpg_f32x2{lo, hi}, lpg_bf16x2));
+}
 
 
 // MASK = false (lpg_colsum_bf16): g already is dZ (the folded form, lpg_fc_bf16_relu_bwd) --
@@ -198,71 +187,168 @@ int64_t fold(int64_t nblk, int64_t n, const float *part, float *seg, const float
 
 int64_t fold_floats(int64_t nblk, int64_t n) { return (nblk + (nblk > 2 * kFold ? kFold : 0)) * n; }
 
-// part[b][k][n] = sum over the block's rows of A[m][k] * dZ[m][n], k < K = K1 + K2.
-// The block's [A1 | A2] rows are staged once into LDS ([row][KP], zero-padded
-// to KP = K rounded up to 4) and read back as broadcast b128 loads.  (Weight
-// gradients carry no bitwise contract: fused multiply-adds, checked against
-// fp64 within the summation bound.)  With MASK the kernel reads the output
-// gradient g and the stored output y instead of dZ and applies the ReLU /
-// dropout backward on the fly, dZ = (y > 0) ? g * scale : 0, adding a K-th
-// partial row for the bias gradient -- conv1 (whose inputs need no gradient)
-// never materialises dZ.
-template <int K, bool MASK>
-__global__ __launch_bounds__(kT) void wgrad_smallk_p1(int64_t M, int64_t N, const float *__restrict__ dz,
-                                                      int64_t ldz, const float *__restrict__ y, int64_t ldy,
-                                                      float scale, int K1, const float *__restrict__ A1,
-                                                      int64_t lda1, const float *__restrict__ A2, int64_t lda2,
-                                                      float *__restrict__ part) {
-  constexpr int KP = (K + 3) / 4 * 4;
-  constexpr int KR = K + (MASK ? 1 : 0);  // partial rows per block
-  __shared__ float4 sa[kRowsWgrad * KP / 4];
-  const int64_t r0 = (int64_t)blockIdx.x * kRowsWgrad;
-  const int64_t r1 = r0 + kRowsWgrad < M ? r0 + kRowsWgrad : M;
-  float *sf = reinterpret_cast<float *>(sa);
-  for (int i = threadIdx.x; i < kRowsWgrad * KP; i += kT) {
-    const int r = i / KP, k = i % KP;
-    const int64_t m = r0 + r;
-    float v = 0.f;
-    if (m < r1 && k < K) v = k < K1 ? A1[m * lda1 + k] : A2[m * lda2 + (k - K1)];
-    sf[i] = v;
-  }
-  __syncthreads();
-  for (int64_t c = (int64_t)threadIdx.x * 4; c < N; c += kT * 4) {
-    float4 acc[KR];
-#pragma unroll
-    for (int k = 0; k < KR; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto row = [&](int r, float4 z) {
-      float a[KP];
-#pragma unroll
-      for (int q = 0; q < KP / 4; ++q) {
-        const float4 v = sa[r * (KP / 4) + q];
-        a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        acc[k].x = __builtin_fmaf(a[k], z.x, acc[k].x); acc[k].y = __builtin_fmaf(a[k], z.y, acc[k].y);
-        acc[k].z = __builtin_fmaf(a[k], z.z, acc[k].z); acc[k].w = __builtin_fmaf(a[k], z.w, acc[k].w);
-      }
-      if (MASK) add4(acc[KR - 1], z);
-    };
-    auto load_z = [&](int64_t m) {
-      const float4 g = *reinterpret_cast<const float4 *>(dz + m * ldz + c);
-      if (!MASK) return g;
-      return relu_scale(g, *reinterpret_cast<const float4 *>(y + m * ldy + c), scale);
-    };
-    const int nr = (int)(r1 - r0);
-    int r = 0;
-    for (; r + kUnrollWgrad <= nr; r += kUnrollWgrad) {
-      float4 z[kUnrollWgrad];
-#pragma unroll
-      for (int u = 0; u < kUnrollWgrad; ++u) z[u] = load_z(r0 + r + u);
-#pragma unroll
-      for (int u = 0; u < kUnrollWgrad; ++u) row(r + u, z[u]);
+// Weight gradients of a narrow-input FC (conv1: K = K1 + K2 <= 16 LP features):
+//   part[s][k][n] = sum over block s's rows m of A[m][k] * dZ[m][n]   (k < K),
+//   part[s][K][n] = sum_m dZ[m][n]                                    (the bias gradient row)
+// dZ = the stored gradient, or with MASK (y > 0) ? g * scale : 0 from the output gradient g and the
+// stored output y (bf16: relu_bwd_pk_bf16, the bits of relu_bwd_colsum_bf16 and of the folded
+// store).  Grid (column groups of 1024 = 256 threads x 4 columns, S row ranges): block s owns rows
+// [s M / S, (s + 1) M / S) -- every resident block the same share, the partial image [S][K + 1][N]
+// independent of M -- walked in 64-row chunks whose [A1 | A2] rows are staged in LDS as fp32
+// (double-buffered; the next chunk's values are loaded into registers a chunk ahead).  The
+// gradient rows stream in groups of U, the next group's loads issued before the current group's
+// FMAs (>= 128 B per lane in flight; hipcc otherwise interleaved them with the arithmetic and kept
+// two loads in flight, 1.8 TB/s for bf16), accumulated as column pairs on v_pk_fma_f32.  (Weight
+// gradients carry no bitwise contract: fma chains per block, folded in block order, checked against
+// fp64 within the summation bound.)
+constexpr int kChunk = 64;
+
+template <bool BF> using G4 = typename std::conditional<BF, uint2, float4>::type;  // 4 gradient values
+
+template <bool BF, bool MASK>
+__device__ __forceinline__ void grad_pairs(G4<BF> g, G4<BF> y, float scale, lpg_f32x2 &z01, lpg_f32x2 &z23) {
+  if constexpr (BF) {
+    uint32_t a = g.x, b = g.y;
+    if constexpr (MASK) {
+      a = relu_bwd_pk_bf16(a, y.x, scale);
+      b = relu_bwd_pk_bf16(b, y.y, scale);
     }
-    for (; r < nr; ++r) row(r, load_z(r0 + r));
-    float *pb = part + (int64_t)blockIdx.x * KR * N;
+    z01 = lpg_f32x2{__uint_as_float(a << 16), __uint_as_float(a & 0xffff0000u)};
+    z23 = lpg_f32x2{__uint_as_float(b << 16), __uint_as_float(b & 0xffff0000u)};
+  } else {
+    if constexpr (MASK) g = relu_scale(g, y, scale);
+    z01 = lpg_f32x2{g.x, g.y};
+    z23 = lpg_f32x2{g.z, g.w};
+  }
+}
+
+template <int K, bool MASK, bool BF>
+__global__ __launch_bounds__(kT) void wgrad_smallk_p1(int64_t M, int64_t N, const void *__restrict__ dzv, int64_t ldz,
+                                                      const void *__restrict__ yv, int64_t ldy, float scale, int K1,
+                                                      const void *__restrict__ A1v, int64_t lda1,
+                                                      const void *__restrict__ A2v, int64_t lda2, int64_t S,
+                                                      float *__restrict__ part) {
+  using E = typename std::conditional<BF, uint16_t, float>::type;
+  constexpr int KP = (K + 3) / 4 * 4;
+  constexpr int KR = K + 1;
+  constexpr int U = 128 / ((BF ? 8 : 16) * (MASK ? 2 : 1));  // rows per group: 128 B per lane in flight
+  constexpr int AE = kChunk * KP / kT;                        // staged A values per thread per chunk
+  static_assert(kChunk % (2 * U) == 0 && kChunk * KP % kT == 0, "chunk shape");
+  __shared__ float4 sa[2][kChunk * KP / 4];
+  const E *dz = static_cast<const E *>(dzv), *y = static_cast<const E *>(yv);
+  const E *A1 = static_cast<const E *>(A1v), *A2 = static_cast<const E *>(A2v);
+  const int64_t c = (int64_t)blockIdx.x * (kT * 4) + threadIdx.x * 4;
+  const bool col_ok = c < N;
+  const int64_t cl = col_ok ? c : N - 4;  // lanes past N load an in-range column (never accumulated)
+  const int64_t sb = blockIdx.y;
+  const int64_t rb = sb * M / S, re = (sb + 1) * M / S;
+  if (re <= rb) {  // (block-uniform: no barrier is skipped by part of a block)
+    if (col_ok)
+      for (int k = 0; k < KR; ++k) *reinterpret_cast<float4 *>(part + (sb * KR + k) * N + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const int nch = (int)((re - rb + kChunk - 1) / kChunk);
+  const int nfull = (int)((re - rb) / kChunk);
+
+  // the next chunk's A values, raw (converted / zeroed when stored, so nothing waits for these
+  // loads before the chunk boundary); addresses clamped in range, branchless
+  E areg[AE];
+  bool aok[AE];
+  auto load_a = [&](int64_t r0) {
 #pragma unroll
-    for (int k = 0; k < KR; ++k) *reinterpret_cast<float4 *>(pb + k * N + c) = acc[k];
+    for (int j = 0; j < AE; ++j) {
+      const int i = threadIdx.x + kT * j, r = i / KP, k = i % KP;
+      const int64_t m = r0 + r < re ? r0 + r : re - 1;
+      const int kk = k < K ? k : K - 1;
+      areg[j] = kk < K1 ? A1[m * lda1 + kk] : A2[m * lda2 + (kk - K1)];
+      aok[j] = r0 + r < re && k < K;
+    }
+  };
+  auto store_a = [&](int buf) {
+    float *sf = reinterpret_cast<float *>(sa[buf]);
+#pragma unroll
+    for (int j = 0; j < AE; ++j) {
+      float v;
+      if constexpr (BF) v = bf16_to_f32(areg[j]); else v = areg[j];
+      sf[threadIdx.x + kT * j] = aok[j] ? v : 0.f;
+    }
+  };
+  // gradient rows in two register buffers: group g + 1 loads while group g is multiplied (a copy
+  // from one buffer into the other made hipcc wait for the loads before the copy)
+  G4<BF> gA[U], yA[U], gB[U], yB[U];
+  auto issue = [&](G4<BF>(&gb)[U], G4<BF>(&yb)[U], int64_t m0) {  // rows past re: clamped, never used
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t m = m0 + u < re ? m0 + u : re - 1;
+      gb[u] = *reinterpret_cast<const G4<BF> *>(dz + m * ldz + cl);
+      if constexpr (MASK) yb[u] = *reinterpret_cast<const G4<BF> *>(y + m * ldy + cl);
+    }
+  };
+  lpg_f32x2 acc[KR][2];
+#pragma unroll
+  for (int k = 0; k < KR; ++k) acc[k][0] = acc[k][1] = lpg_f32x2{0.f, 0.f};
+  auto row = [&](G4<BF> gv, G4<BF> yv, const float4 *ar) {
+    float a[KP];
+#pragma unroll
+    for (int q = 0; q < KP / 4; ++q) {
+      const float4 v = ar[q];
+      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+    }
+    lpg_f32x2 z01, z23;
+    grad_pairs<BF, MASK>(gv, yv, scale, z01, z23);
+    if (!col_ok) z01 = z23 = lpg_f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      acc[k][0] = __builtin_elementwise_fma(lpg_f32x2{a[k], a[k]}, z01, acc[k][0]);
+      acc[k][1] = __builtin_elementwise_fma(lpg_f32x2{a[k], a[k]}, z23, acc[k][1]);
+    }
+    acc[K][0] = acc[K][0] + z01;
+    acc[K][1] = acc[K][1] + z23;
+  };
+  auto group = [&](const G4<BF>(&gb)[U], const G4<BF>(&yb)[U], const float4 *sab, int rl) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) row(gb[u], yb[u], sab + (rl + u) * (KP / 4));
+  };
+
+  load_a(rb);
+  store_a(0);
+  issue(gA, yA, rb);
+  __syncthreads();
+  if (nch > 1) load_a(rb + kChunk);
+  // whole 64-row chunks: branch-free, one group always in flight
+  for (int ch = 0; ch < nfull; ++ch) {
+    const float4 *sab = sa[ch & 1];
+    const int64_t cb = rb + (int64_t)ch * kChunk;
+    for (int j = 0; j < kChunk / (2 * U); ++j) {
+      issue(gB, yB, cb + (2 * j + 1) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      group(gA, yA, sab, 2 * j * U);
+      issue(gA, yA, cb + (2 * j + 2) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      group(gB, yB, sab, (2 * j + 1) * U);
+    }
+    if (ch + 1 < nch) {  // the next chunk's A (loaded a chunk ago) into the other buffer
+      store_a((ch + 1) & 1);
+      lds_barrier();  // (not __syncthreads: its fence would drain the gradient loads in flight)
+      if (ch + 2 < nch) load_a(cb + 2 * kChunk);
+    }
+  }
+  // the partial last chunk: row by row (gA holds its first group)
+  if (nfull < nch) {
+    const float4 *sab = sa[nfull & 1];
+    const int64_t cb = rb + (int64_t)nfull * kChunk;
+    for (int64_t m0 = cb; m0 < re; m0 += U) {
+      if (m0 != cb) issue(gA, yA, m0);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (m0 + u < re) row(gA[u], yA[u], sab + (int)(m0 - cb + u) * (KP / 4));
+    }
+  }
+  if (col_ok) {
+    float *pb = part + sb * KR * N + c;
+#pragma unroll
+    for (int k = 0; k < KR; ++k)
+      *reinterpret_cast<float4 *>(pb + k * N) = make_float4(acc[k][0][0], acc[k][0][1], acc[k][1][0], acc[k][1][1]);
   }
 }
 
@@ -285,77 +371,168 @@ __global__ __launch_bounds__(kT) void wgrad_smallk_p2(int64_t nrow, int64_t N, i
   }
 }
 
-// Backward of a Linear with few outputs (the heads, N = 3, arch.py:190):
-//   dH[m, k] = sum_c G[m, c] W[c, k]        (written if dH != NULL)
-//   dW[c, k] = sum_m G[m, c] H[m, k],  db[c] = sum_m G[m, c]
-// Pass 1 streams H once, writes dH and the block's partial [dW | db] row.
-// MASK (lpg_heads_relu_bwd_f32): H is the output Y of the previous layer's
-// ReLU (+ dropout), and the gradient leaves already through that layer's
-// ReLU/dropout backward: dH[m, k] = Y[m, k] > 0 ? scale * sum_c G W : 0 (the
-// layer's dZ), plus its bias gradient dbY[k] = sum_m dH[m, k] as K more
-// partial columns -- the pass relu_bwd_colsum would make over dH and Y again.
-template <int N, bool MASK>
-__global__ __launch_bounds__(kT) void linear_small_bwd_p1(int64_t M, int64_t K, const float *__restrict__ G,
-                                                          int64_t ldg, const float *__restrict__ W,
-                                                          const float *__restrict__ H, int64_t ldh,
-                                                          float *__restrict__ dH, int64_t lddh, float scale,
-                                                          float *__restrict__ part) {
-  const int64_t r0 = (int64_t)blockIdx.x * kRowsLinear;
-  const int64_t r1 = r0 + kRowsLinear < M ? r0 + kRowsLinear : M;
-  const int64_t tot = N * K + N + (MASK ? K : 0);
-  float *pw = part + (int64_t)blockIdx.x * tot;  // [N][K], db[N], (MASK) dbY[K]
-  // db = sum_m G[m, c] in row order, accumulated beside the rows' other work by every thread (the
-  // same sums; thread 0 stores them) -- a separate loop after it was 128 dependent loads per block
-  float sg[N];
+// Backward of a Linear with few outputs (the heads lin_left / lin_right, N = 3, arch.py:190) over
+// its input H [M, K] (fp32, or bf16 for the c5 model), G / W fp32:
+//   dH[m, k] = sum_c G[m, c] W[c, k]        (written if dH != NULL; bf16: RNE)
+//   dW[c, k] = sum_m G[m, c] H[m, k],  db[c] = sum_m G[m, c]     (per-block partials [N K + N])
+// MASK (the fused heads + ReLU backward): H is the output Y of the previous layer's ReLU (+
+// dropout) and dH leaves through that layer's ReLU/dropout backward -- the layer's dZ:
+// fp32 (Y > 0) ? scale * dH : 0, bf16 relu_bwd_pk_bf16(RNE(dH), Y, scale) -- the bits of the
+// separate relu_bwd_colsum pass over the plain dH.  party != NULL: the column sums of the stored
+// dH per 64-row chunk in row order into the partial image [ceil(M / 64)][K] of relu_bwd_colsum
+// (chunk j = rows [64 j, 64 j + 64)), so the same fold gives the same bits as that pass's db.
+// A block owns 128 rows (2 chunks) and 16 B of columns per thread (fp32 4, bf16 8); its G rows are
+// staged in LDS once (the per-row G loads were scalar loads, each waited for before its row:
+// 4.4 TB/s), the H rows stream in groups of 8 with the next group's loads issued before the current
+// group's arithmetic.
+template <bool BF> using H16 = typename std::conditional<BF, uint4, float4>::type;
+
+template <int N, bool MASK, bool BF, bool STORE>
+__global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const float *__restrict__ G, int64_t ldg,
+                                                   const float *__restrict__ W, const void *__restrict__ Hv,
+                                                   int64_t ldh, void *__restrict__ dHv, int64_t lddh, float scale,
+                                                   float *__restrict__ part, float *__restrict__ party) {
+  using E = typename std::conditional<BF, uint16_t, float>::type;
+  constexpr int EPT = BF ? 8 : 4;  // columns per thread
+  constexpr int P = EPT / 2;       // column pairs
+  constexpr int U = 8;             // rows per group (128 B per lane in flight)
+  constexpr int RB = kRowsLinear;  // rows per block
+  constexpr int CH = kRowsColsum;  // column-sum chunk
+  static_assert(RB % CH == 0 && CH % (2 * U) == 0, "block shape");
+  __shared__ float4 sg4[RB];
+  const E *H = static_cast<const E *>(Hv);
+  E *dH = static_cast<E *>(dHv);
+  const int64_t r0 = (int64_t)blockIdx.x * RB;
+  const int64_t r1 = r0 + RB < M ? r0 + RB : M;
+  if (threadIdx.x < RB) {
+    const int64_t m = r0 + threadIdx.x;
+    float gv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (m < r1) {
 #pragma unroll
-  for (int c = 0; c < N; ++c) sg[c] = 0.f;
-  bool first = true;
-  for (int64_t k = (int64_t)threadIdx.x * 4; k < K; k += kT * 4) {
-    float4 w[N], acc[N];
-    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int c = 0; c < N; ++c) gv[c] = G[m * ldg + c];
+    }
+    sg4[threadIdx.x] = make_float4(gv[0], gv[1], gv[2], gv[3]);
+  }
+  __syncthreads();
+  const int64_t tot = N * K + N;
+  float *pw = part + (int64_t)blockIdx.x * tot;  // [N][K], db[N]
+  const int nfull = (int)((r1 - r0) / CH), nch = (int)((r1 - r0 + CH - 1) / CH);
+  for (int64_t k = (int64_t)threadIdx.x * EPT; k < K; k += kT * EPT) {
+    lpg_f32x2 w[N][P], acc[N][P], cs[P];
 #pragma unroll
     for (int c = 0; c < N; ++c) {
-      w[c] = *reinterpret_cast<const float4 *>(W + c * K + k);
-      acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < P; q += 2) {
+        const float4 wv = *reinterpret_cast<const float4 *>(W + c * K + k + 2 * q);
+        w[c][q] = lpg_f32x2{wv.x, wv.y};
+        w[c][q + 1] = lpg_f32x2{wv.z, wv.w};
+      }
+#pragma unroll
+      for (int q = 0; q < P; ++q) acc[c][q] = lpg_f32x2{0.f, 0.f};
     }
-    auto row = [&](int64_t m, float4 h) {
-      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < P; ++q) cs[q] = lpg_f32x2{0.f, 0.f};
+    H16<BF> hA[U], hB[U];  // two register buffers: group g + 1 loading while group g is processed
+    auto issue = [&](H16<BF>(&hb)[U], int64_t m0) {  // rows past r1: clamped, never used
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t m = m0 + u < r1 ? m0 + u : r1 - 1;
+        hb[u] = *reinterpret_cast<const H16<BF> *>(H + m * ldh + k);
+      }
+    };
+    auto row = [&](H16<BF> hv, int64_t m) {
+      lpg_f32x2 h[P];
+      uint32_t hw[4] = {0u, 0u, 0u, 0u};
+      if constexpr (BF) {
+        hw[0] = hv.x; hw[1] = hv.y; hw[2] = hv.z; hw[3] = hv.w;
+#pragma unroll
+        for (int q = 0; q < P; ++q) h[q] = lpg_f32x2{__uint_as_float(hw[q] << 16), __uint_as_float(hw[q] & 0xffff0000u)};
+      } else {
+        h[0] = lpg_f32x2{hv.x, hv.y};
+        h[1] = lpg_f32x2{hv.z, hv.w};
+      }
+      const float4 g4 = sg4[m - r0];
+      const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+      lpg_f32x2 d[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) d[q] = lpg_f32x2{0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < N; ++c) {
-        const float gc = G[m * ldg + c];
-        if (first) sg[c] = sg[c] + gc;
-        d.x = d.x + gc * w[c].x; d.y = d.y + gc * w[c].y; d.z = d.z + gc * w[c].z; d.w = d.w + gc * w[c].w;
-        acc[c].x = acc[c].x + gc * h.x; acc[c].y = acc[c].y + gc * h.y;
-        acc[c].z = acc[c].z + gc * h.z; acc[c].w = acc[c].w + gc * h.w;
+        const lpg_f32x2 gc = {gv[c], gv[c]};
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          d[q] = __builtin_elementwise_fma(gc, w[c][q], d[q]);
+          acc[c][q] = __builtin_elementwise_fma(gc, h[q], acc[c][q]);
+        }
       }
-      if (MASK) {
-        d.x = h.x > 0.f ? d.x * scale : 0.f;
-        d.y = h.y > 0.f ? d.y * scale : 0.f;
-        d.z = h.z > 0.f ? d.z * scale : 0.f;
-        d.w = h.w > 0.f ? d.w * scale : 0.f;
-        cs.x = cs.x + d.x; cs.y = cs.y + d.y; cs.z = cs.z + d.z; cs.w = cs.w + d.w;
+      if constexpr (BF) {
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          o[q] = pk_bf16(d[q][0], d[q][1]);
+          if (MASK) o[q] = relu_bwd_pk_bf16(o[q], hw[q], scale);
+          cs[q] = cs[q] + lpg_f32x2{__uint_as_float(o[q] << 16), __uint_as_float(o[q] & 0xffff0000u)};
+        }
+        if (STORE) *reinterpret_cast<uint4 *>(dH + m * lddh + k) = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {
+        float o[4] = {d[0][0], d[0][1], d[1][0], d[1][1]};
+        const float hv4[4] = {h[0][0], h[0][1], h[1][0], h[1][1]};
+        if (MASK) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = hv4[e] > 0.f ? o[e] * scale : 0.f;
+        }
+        cs[0] = cs[0] + lpg_f32x2{o[0], o[1]};
+        cs[1] = cs[1] + lpg_f32x2{o[2], o[3]};
+        if (STORE) *reinterpret_cast<float4 *>(dH + m * lddh + k) = make_float4(o[0], o[1], o[2], o[3]);
       }
-      if (dH) *reinterpret_cast<float4 *>(dH + m * lddh + k) = d;
     };
-    int64_t m = r0;
-    for (; m + kUnrollLinear <= r1; m += kUnrollLinear) {
-      float4 h[kUnrollLinear];
+    auto flush = [&](int ch) {  // the chunk's column sums into relu_bwd_colsum's partial image
+      if (party) {
+        float *py = party + (r0 / CH + ch) * K + k;
 #pragma unroll
-      for (int u = 0; u < kUnrollLinear; ++u) h[u] = *reinterpret_cast<const float4 *>(H + (m + u) * ldh + k);
+        for (int q = 0; q < P; q += 2)
+          *reinterpret_cast<float4 *>(py + 2 * q) = make_float4(cs[q][0], cs[q][1], cs[q + 1][0], cs[q + 1][1]);
+      }
 #pragma unroll
-      for (int u = 0; u < kUnrollLinear; ++u) row(m + u, h[u]);
+      for (int q = 0; q < P; ++q) cs[q] = lpg_f32x2{0.f, 0.f};
+    };
+    issue(hA, r0);
+    for (int ch = 0; ch < nfull; ++ch) {  // whole chunks: branch-free, one group always in flight
+      const int64_t cb = r0 + (int64_t)ch * CH;
+      for (int j = 0; j < CH / (2 * U); ++j) {
+        issue(hB, cb + (2 * j + 1) * U);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) row(hA[u], cb + 2 * j * U + u);
+        issue(hA, cb + (2 * j + 2) * U);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) row(hB[u], cb + (2 * j + 1) * U + u);
+      }
+      flush(ch);
     }
-    for (; m < r1; ++m) row(m, *reinterpret_cast<const float4 *>(H + m * ldh + k));
+    if (nfull < nch) {  // the partial last chunk, row by row (hA holds its first group)
+      const int64_t cb = r0 + (int64_t)nfull * CH;
+      for (int64_t m0 = cb; m0 < r1; m0 += U) {
+        if (m0 != cb) issue(hA, m0);
 #pragma unroll
-    for (int c = 0; c < N; ++c) *reinterpret_cast<float4 *>(pw + c * K + k) = acc[c];
-    if (MASK) *reinterpret_cast<float4 *>(pw + N * K + N + k) = cs;
-    first = false;
+        for (int u = 0; u < U; ++u)
+          if (m0 + u < r1) row(hA[u], m0 + u);
+      }
+      flush(nfull);
+    }
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+#pragma unroll
+      for (int q = 0; q < P; q += 2)
+        *reinterpret_cast<float4 *>(pw + c * K + k + 2 * q) =
+            make_float4(acc[c][q][0], acc[c][q][1], acc[c][q + 1][0], acc[c][q + 1][1]);
   }
-  if (threadIdx.x == 0) {
-    if (first) {  // (no column pass ran on this thread: K == 0)
-      for (int64_t m = r0; m < r1; ++m)
-#pragma unroll
-        for (int c = 0; c < N; ++c) sg[c] = sg[c] + G[m * ldg + c];
+  if (threadIdx.x == 0) {  // db = sum_m G[m, c] in row order
+    float sg[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t m = r0; m < r1; ++m) {
+      const float4 g4 = sg4[m - r0];
+      sg[0] = sg[0] + g4.x; sg[1] = sg[1] + g4.y; sg[2] = sg[2] + g4.z; sg[3] = sg[3] + g4.w;
     }
 #pragma unroll
     for (int c = 0; c < N; ++c) pw[N * K + c] = sg[c];
@@ -374,6 +551,84 @@ __global__ __launch_bounds__(kT) void linear_small_bwd_p2(int64_t nrow, int64_t 
     if (db) db[i - (int64_t)N * K] = s;
   } else if (dbY) {
     dbY[i - (int64_t)N * K - N] = s;
+  }
+}
+
+// ---- bf16 (c5) narrow kernels: conv1's weight gradients and the heads (N = 3) ----------------
+
+
+// The heads' forward in bf16 (c5): out[m, c] = RNE_bf16(sum_k H[m, k] W[c, k] + b[c]) for N <= 4,
+// one streaming pass over H.  A wave takes RW rows at a time; lane l holds the 8-column chunks
+// l, l + 64, ... (KC of them; their weights stay in registers), sums its products per (row, c),
+// then a butterfly over the 64 lanes.  The MFMA kernel on N padded to 64 (0.36 ms per c5 step)
+// sums the same exact bf16 x bf16 products in another order: tolerance, not bits.
+constexpr int kRowsPerWaveFwd = 4;
+
+template <int N, int KC>
+__global__ __launch_bounds__(256) void linear_small_fwd_bf16(int64_t M, int64_t K, const uint16_t *__restrict__ H,
+                                                             int64_t ldh, const float *__restrict__ W,
+                                                             const float *__restrict__ bias,
+                                                             uint16_t *__restrict__ out, int64_t ldo) {
+  constexpr int RW = kRowsPerWaveFwd;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwave = (int64_t)gridDim.x * 4;
+  float w[KC][N][8];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    const int64_t k = (int64_t)kc * 512 + lane * 8;
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0;
+      if (k < K) {
+        w0 = *reinterpret_cast<const float4 *>(W + c * K + k);
+        w1 = *reinterpret_cast<const float4 *>(W + c * K + k + 4);
+      }
+      w[kc][c][0] = w0.x; w[kc][c][1] = w0.y; w[kc][c][2] = w0.z; w[kc][c][3] = w0.w;
+      w[kc][c][4] = w1.x; w[kc][c][5] = w1.y; w[kc][c][6] = w1.z; w[kc][c][7] = w1.w;
+    }
+  }
+  float b[N];
+#pragma unroll
+  for (int c = 0; c < N; ++c) b[c] = bias ? bias[c] : 0.f;
+  for (int64_t m0 = wave * RW; m0 < M; m0 += nwave * RW) {
+    uint4 hv[RW][KC];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int64_t m = m0 + r < M ? m0 + r : M - 1;  // clamped rows are never stored
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const int64_t k = (int64_t)kc * 512 + lane * 8;
+        hv[r][kc] = k < K ? *reinterpret_cast<const uint4 *>(H + m * ldh + k) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    float p[RW][N];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+#pragma unroll
+      for (int c = 0; c < N; ++c) p[r][c] = 0.f;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const uint32_t hw[4] = {hv[r][kc].x, hv[r][kc].y, hv[r][kc].z, hv[r][kc].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float h0 = bf16_to_f32(hw[e] & 0xffffu), h1 = bf16_to_f32(hw[e] >> 16);
+#pragma unroll
+          for (int c = 0; c < N; ++c)
+            p[r][c] = __builtin_fmaf(h1, w[kc][c][2 * e + 1], __builtin_fmaf(h0, w[kc][c][2 * e], p[r][c]));
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1)
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int c = 0; c < N; ++c) p[r][c] = p[r][c] + __shfl_xor(p[r][c], s, 64);
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int c = 0; c < N; ++c)
+        if (lane == r * N + c && m0 + r < M) out[(m0 + r) * ldo + c] = (uint16_t)pk_bf16(p[r][c] + b[c], 0.f);
   }
 }
 
@@ -471,25 +726,33 @@ extern "C" lpg_status lpg_colsum_bf16(int64_t M, int64_t N, const uint16_t *g, i
   return LPG_OK;
 }
 
-extern "C" int64_t lpg_wgrad_smallk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
-  if (M < 0 || N < 0 || K < 0) return -1;
-  return fold_floats((M + kRowsWgrad - 1) / kRowsWgrad, (K + 1) * N) * (int64_t)sizeof(float);
-}
-
 namespace lpg {
 namespace {
 
-lpg_status wgrad_smallk(int64_t M, int64_t N, const float *dz, int64_t ldz, const float *y, int64_t ldy, float scale,
-                        int64_t K1, const float *A1, int64_t lda1, int64_t K2, const float *A2, int64_t lda2,
+// wgrad_smallk_p1's row ranges: the resident blocks shared by the column groups, at least one
+// chunk of rows each and at most kWgSplits (the partial image [S][K + 1][N]; the workspace is
+// sized for the most a launch can use)
+constexpr int64_t kWgSplits = 512;
+int64_t wgrad_smallk_splits(int64_t M) {
+  const int64_t s = (M + kChunk - 1) / kChunk;
+  return s < 1 ? 1 : (s > kWgSplits ? kWgSplits : s);
+}
+
+template <bool BF>
+lpg_status wgrad_smallk(int64_t M, int64_t N, const void *dz, int64_t ldz, const void *y, int64_t ldy, float scale,
+                        int64_t K1, const void *A1, int64_t lda1, int64_t K2, const void *A2, int64_t lda2,
                         float *dW1, float *dW2, float *db, void *workspace, void *stream, const char *name) {
   const int64_t K = K1 + K2;
   const bool mask = y != nullptr;
+  const uintptr_t al = BF ? 7 : 15;  // 4 gradient values per load: 8 B (bf16) / 16 B (fp32)
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0 && K >= 1 && K <= kMaxSmallK, "%s: need 1 <= K1 + K2 <= %d",
               name, kMaxSmallK);
   LPG_REQUIRE(dz && workspace && (K1 == 0 || A1) && (K2 == 0 || A2), "%s: NULL pointer", name);
-  LPG_REQUIRE(N % 4 == 0 && ldz % 4 == 0 && aligned16(dz) && aligned16(workspace) &&
-                  (!mask || (ldy % 4 == 0 && aligned16(y))),
-              "%s: N / leading dims multiples of 4, gradient / output / workspace 16-byte aligned", name);
+  LPG_REQUIRE((K1 == 0 || lda1 >= K1) && (K2 == 0 || lda2 >= K2), "%s: bad lda", name);
+  LPG_REQUIRE(N % 4 == 0 && ldz % 4 == 0 && (reinterpret_cast<uintptr_t>(dz) & al) == 0 && aligned16(workspace) &&
+                  (!mask || (ldy % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & al) == 0)),
+              "%s: N / leading dims multiples of 4, gradient / output aligned to 4 elements, workspace 16-byte aligned",
+              name);
   hipStream_t s = as_stream(stream);
   if (M == 0 || N == 0) {
     if (dW1 && N * K1) LPG_HIP(hipMemsetAsync(dW1, 0, sizeof(float) * N * K1, s));
@@ -497,20 +760,27 @@ lpg_status wgrad_smallk(int64_t M, int64_t N, const float *dz, int64_t ldz, cons
     if (db && N) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, s));
     return LPG_OK;
   }
-  const int64_t nblk = (M + kRowsWgrad - 1) / kRowsWgrad;
-  const int64_t KR = K + (mask ? 1 : 0);
+  const int64_t KR = K + 1;
   float *part = static_cast<float *>(workspace);
   const int k1 = (int)K1;
-  const dim3 grid((unsigned)nblk), block(kT);
+  const int64_t ncg = (N + kT * 4 - 1) / (kT * 4);
+  LPG_REQUIRE(ncg < 65536, "%s: N too large", name);
+  auto splits = [&](auto kern) {
+    const int64_t r = resident_blocks(kern, kT) / ncg, smax = wgrad_smallk_splits(M);
+    return r < 1 ? (int64_t)1 : (r < smax ? r : smax);
+  };
+  int64_t S = 1;
   switch (K * 2 + (mask ? 1 : 0)) {
-#define LPG_WG(KK)                                                                                                  \
-  case 2 * KK:                                                                                                      \
-    hipLaunchKernelGGL((wgrad_smallk_p1<KK, false>), grid, block, 0, s, M, N, dz, ldz, y, ldy, scale, k1, A1, lda1, \
-                       A2, lda2, part);                                                                             \
-    break;                                                                                                          \
-  case 2 * KK + 1:                                                                                                  \
-    hipLaunchKernelGGL((wgrad_smallk_p1<KK, true>), grid, block, 0, s, M, N, dz, ldz, y, ldy, scale, k1, A1, lda1,  \
-                       A2, lda2, part);                                                                             \
+#define LPG_WG(KK)                                                                                      \
+  case 2 * KK:                                                                                          \
+    S = splits(wgrad_smallk_p1<KK, false, BF>);                                                         \
+    hipLaunchKernelGGL((wgrad_smallk_p1<KK, false, BF>), dim3((unsigned)ncg, (unsigned)S), dim3(kT), 0, s, M, N, \
+                       dz, ldz, y, ldy, scale, k1, A1, lda1, A2, lda2, S, part);                       \
+    break;                                                                                              \
+  case 2 * KK + 1:                                                                                      \
+    S = splits(wgrad_smallk_p1<KK, true, BF>);                                                          \
+    hipLaunchKernelGGL((wgrad_smallk_p1<KK, true, BF>), dim3((unsigned)ncg, (unsigned)S), dim3(kT), 0, s, M, N,  \
+                       dz, ldz, y, ldy, scale, k1, A1, lda1, A2, lda2, S, part);                       \
     break;
     LPG_WG(1) LPG_WG(2) LPG_WG(3) LPG_WG(4) LPG_WG(5) LPG_WG(6) LPG_WG(7) LPG_WG(8)
     LPG_WG(9) LPG_WG(10) LPG_WG(11) LPG_WG(12) LPG_WG(13) LPG_WG(14) LPG_WG(15) LPG_WG(16)
@@ -518,21 +788,92 @@ lpg_status wgrad_smallk(int64_t M, int64_t N, const float *dz, int64_t ldz, cons
   }
   LPG_HIP(hipGetLastError());
   const float *img;
-  const int64_t nrow = fold(nblk, KR * N, part, part + nblk * KR * N, &img, s);
+  const int64_t nrow = fold(S, KR * N, part, part + S * KR * N, &img, s);
   hipLaunchKernelGGL(wgrad_smallk_p2, dim3((unsigned)((KR * N + kT - 1) / kT)), dim3(kT), 0, s, nrow, N, (int)K,
                      (int)KR, k1, img, dW1, dW2, db);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
 
+int64_t heads_bwd_floats(int64_t M, int64_t K, int64_t N) {
+  const int64_t nblk = (M + kRowsLinear - 1) / kRowsLinear, nchunk = (M + kRowsColsum - 1) / kRowsColsum;
+  return fold_floats(nblk, N * K + N) + fold_floats(nchunk, K);
+}
+
+// The heads' backward (heads_bwd_p1) for both dtypes: dW / db through the [nblk][N K + N] image,
+// dbY through relu_bwd_colsum's [ceil(M / 64)][K] image and its fold + final pass.
+template <bool BF>
+lpg_status heads_bwd(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W, const void *H,
+                     int64_t ldh, void *dH, int64_t lddh, float scale, float *dW, float *db, float *dbY, bool mask,
+                     void *workspace, void *stream, const char *what) {
+  constexpr int EPT = BF ? 8 : 4;
+  LPG_REQUIRE(M >= 0 && K >= 0 && N >= 1 && N <= kSmallNMax, "%s: need 1 <= N <= %d", what, kSmallNMax);
+  LPG_REQUIRE(K % EPT == 0 && ldh % EPT == 0 && (dH == nullptr || lddh % EPT == 0) && ldg >= N,
+              "%s: K and leading dims must be multiples of %d", what, EPT);
+  LPG_REQUIRE(G && W && H && workspace && (dH || !mask), "%s: NULL pointer", what);
+  LPG_REQUIRE(aligned16(W) && aligned16(H) && (dH == nullptr || aligned16(dH)) && aligned16(workspace),
+              "%s: W/H/dH/workspace must be 16-byte aligned", what);
+  hipStream_t s = as_stream(stream);
+  const int64_t nblk = (M + kRowsLinear - 1) / kRowsLinear, nchunk = (M + kRowsColsum - 1) / kRowsColsum;
+  if (nblk == 0 || K == 0) {
+    if (dW && N * K) LPG_HIP(hipMemsetAsync(dW, 0, sizeof(float) * N * K, s));
+    if (dbY && K) LPG_HIP(hipMemsetAsync(dbY, 0, sizeof(float) * K, s));
+    if (nblk == 0) {
+      if (db) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, s));
+      return LPG_OK;
+    }
+  }
+  LPG_REQUIRE(nblk < ((int64_t)1 << 31), "%s: too many rows", what);
+  const int64_t tot = N * K + N;
+  float *part = static_cast<float *>(workspace);
+  float *party = part + fold_floats(nblk, tot);
+  float *py = dbY ? party : nullptr;
+  const dim3 grid((unsigned)nblk), block(kT);
+#define LPG_HB(NN)                                                                                                \
+  if (mask)                                                                                                       \
+    hipLaunchKernelGGL((heads_bwd_p1<NN, true, BF, true>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh,   \
+                       scale, part, py);                                                                          \
+  else if (dH)                                                                                                    \
+    hipLaunchKernelGGL((heads_bwd_p1<NN, false, BF, true>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh,  \
+                       scale, part, py);                                                                          \
+  else                                                                                                            \
+    hipLaunchKernelGGL((heads_bwd_p1<NN, false, BF, false>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh, \
+                       scale, part, py);
+  switch (N) {
+    case 1: LPG_HB(1) break;
+    case 2: LPG_HB(2) break;
+    case 3: LPG_HB(3) break;
+    default: LPG_HB(4)
+  }
+#undef LPG_HB
+  LPG_HIP(hipGetLastError());
+  const float *img;
+  const int64_t nrow = fold(nblk, tot, part, part + nblk * tot, &img, s);
+  hipLaunchKernelGGL(linear_small_bwd_p2, dim3((unsigned)((tot + kT - 1) / kT)), dim3(kT), 0, s, nrow, K, (int)N, tot,
+                     img, dW, db, (float *)nullptr);
+  LPG_HIP(hipGetLastError());
+  if (dbY && K) {  // the fold and final pass of relu_bwd_colsum over the same 64-row partials
+    const float *imy;
+    const int64_t nry = fold(nchunk, K, party, party + nchunk * K, &imy, s);
+    hipLaunchKernelGGL(sum_partials, dim3((unsigned)((K + kT - 1) / kT)), dim3(kT), 0, s, nry, K, imy, dbY);
+    LPG_HIP(hipGetLastError());
+  }
+  return LPG_OK;
+}
+
 }  // namespace
 }  // namespace lpg
+
+extern "C" int64_t lpg_wgrad_smallk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  if (M < 0 || N < 0 || K < 0) return -1;
+  return fold_floats(wgrad_smallk_splits(M), (K + 1) * N) * (int64_t)sizeof(float);
+}
 
 extern "C" lpg_status lpg_wgrad_smallk_f32(int64_t M, int64_t N, const float *dz, int64_t ldz, int64_t K1,
                                            const float *A1, int64_t lda1, int64_t K2, const float *A2, int64_t lda2,
                                            float *dW1, float *dW2, void *workspace, void *stream) {
-  return wgrad_smallk(M, N, dz, ldz, nullptr, 0, 1.f, K1, A1, lda1, K2, A2, lda2, dW1, dW2, nullptr, workspace,
-                      stream, "lpg_wgrad_smallk_f32");
+  return wgrad_smallk<false>(M, N, dz, ldz, nullptr, 0, 1.f, K1, A1, lda1, K2, A2, lda2, dW1, dW2, nullptr, workspace,
+                             stream, "lpg_wgrad_smallk_f32");
 }
 
 extern "C" lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const float *g, int64_t ldg, const float *y,
@@ -540,68 +881,32 @@ extern "C" lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const floa
                                                 int64_t K2, const float *A2, int64_t lda2, float *dW1, float *dW2,
                                                 float *db, void *workspace, void *stream) {
   LPG_REQUIRE(y != nullptr, "lpg_relu_wgrad_smallk_f32: NULL output");
-  return wgrad_smallk(M, N, g, ldg, y, ldy, scale, K1, A1, lda1, K2, A2, lda2, dW1, dW2, db, workspace, stream,
-                      "lpg_relu_wgrad_smallk_f32");
+  return wgrad_smallk<false>(M, N, g, ldg, y, ldy, scale, K1, A1, lda1, K2, A2, lda2, dW1, dW2, db, workspace, stream,
+                             "lpg_relu_wgrad_smallk_f32");
 }
 
-namespace lpg {
-namespace {
-
-lpg_status linear_small_bwd(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W,
-                            const float *H, int64_t ldh, float *dH, int64_t lddh, float scale, float *dW, float *db,
-                            float *dbY, bool mask, void *workspace, void *stream, const char *what) {
-  LPG_REQUIRE(M >= 0 && K >= 0 && N >= 1 && N <= kSmallNMax, "%s: need 1 <= N <= %d", what, kSmallNMax);
-  LPG_REQUIRE(K % 4 == 0 && ldh % 4 == 0 && (dH == nullptr || lddh % 4 == 0),
-              "%s: K and leading dims must be multiples of 4", what);
-  LPG_REQUIRE(G && W && H && workspace, "%s: NULL pointer", what);
-  LPG_REQUIRE(aligned16(W) && aligned16(H) && (dH == nullptr || aligned16(dH)) && aligned16(workspace),
-              "%s: W/H/dH/workspace must be 16-byte aligned", what);
-  hipStream_t s = as_stream(stream);
-  const int64_t nblk = (M + kRowsLinear - 1) / kRowsLinear;
-  if (nblk == 0) {
-    if (dW) LPG_HIP(hipMemsetAsync(dW, 0, sizeof(float) * N * K, s));
-    if (db) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, s));
-    if (dbY) LPG_HIP(hipMemsetAsync(dbY, 0, sizeof(float) * K, s));
-    return LPG_OK;
-  }
-  float *part = static_cast<float *>(workspace);
-  const dim3 grid((unsigned)nblk), block(kT);
-#define LPG_LSB(NN)                                                                                               \
-  if (mask)                                                                                                       \
-    hipLaunchKernelGGL((linear_small_bwd_p1<NN, true>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh,     \
-                       scale, part);                                                                              \
-  else                                                                                                            \
-    hipLaunchKernelGGL((linear_small_bwd_p1<NN, false>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh,    \
-                       scale, part);
-  switch (N) {
-    case 1: LPG_LSB(1) break;
-    case 2: LPG_LSB(2) break;
-    case 3: LPG_LSB(3) break;
-    default: LPG_LSB(4)
-  }
-#undef LPG_LSB
-  LPG_HIP(hipGetLastError());
-  const int64_t tot = N * K + N + (mask ? K : 0);
-  const float *img;
-  const int64_t nrow = fold(nblk, tot, part, part + nblk * tot, &img, s);
-  hipLaunchKernelGGL(linear_small_bwd_p2, dim3((unsigned)((tot + kT - 1) / kT)), dim3(kT), 0, s, nrow, K, (int)N, tot,
-                     img, dW, db, dbY);
-  LPG_HIP(hipGetLastError());
-  return LPG_OK;
+// conv1's weight gradients in bf16 from one read of the gradient: dW1 = dZ^T A1, dW2 = dZ^T A2,
+// db = sum_m dZ (fp32 out).  y == NULL: g already is dZ (the folded ReLU backward of the next
+// layer's input gradient); else dZ = (y > 0) ? RNE_bf16(g * scale) : 0 on the fly (never stored).
+// Workspace: lpg_wgrad_smallk_workspace_bytes(M, N, K1 + K2).
+extern "C" lpg_status lpg_relu_wgrad_smallk_bf16(int64_t M, int64_t N, const uint16_t *g, int64_t ldg,
+                                                 const uint16_t *y, int64_t ldy, float scale, int64_t K1,
+                                                 const uint16_t *A1, int64_t lda1, int64_t K2, const uint16_t *A2,
+                                                 int64_t lda2, float *dW1, float *dW2, float *db, void *workspace,
+                                                 void *stream) {
+  return wgrad_smallk<true>(M, N, g, ldg, y, ldy, scale, K1, A1, lda1, K2, A2, lda2, dW1, dW2, db, workspace, stream,
+                            "lpg_relu_wgrad_smallk_bf16");
 }
-
-}  // namespace
-}  // namespace lpg
 
 extern "C" int64_t lpg_linear_small_bwd_workspace_bytes(int64_t M, int64_t K, int64_t N) {
   if (M < 0 || K < 0 || N < 0) return -1;
-  return fold_floats((M + kRowsLinear - 1) / kRowsLinear, N * K + N + K) * (int64_t)sizeof(float);
+  return heads_bwd_floats(M, K, N) * (int64_t)sizeof(float);
 }
 
 extern "C" lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
                                                const float *W, const float *H, int64_t ldh, float *dH, int64_t lddh,
                                                float *dW, float *db, void *workspace, void *stream) {
-  return linear_small_bwd(M, K, N, G, ldg, W, H, ldh, dH, lddh, 1.f, dW, db, nullptr, false, workspace, stream,
+  return heads_bwd<false>(M, K, N, G, ldg, W, H, ldh, dH, lddh, 1.f, dW, db, nullptr, false, workspace, stream,
                           "lpg_linear_small_bwd_f32");
 }
 
@@ -610,6 +915,61 @@ extern "C" lpg_status lpg_heads_relu_bwd_f32(int64_t M, int64_t K, int64_t N, co
                                              int64_t lddz, float *dW, float *db, float *dbY, void *workspace,
                                              void *stream) {
   LPG_REQUIRE(dZ != nullptr, "lpg_heads_relu_bwd_f32: NULL dZ");
-  return linear_small_bwd(M, K, N, G, ldg, W, Y, ldy, dZ, lddz, scale, dW, db, dbY, true, workspace, stream,
+  return heads_bwd<false>(M, K, N, G, ldg, W, Y, ldy, dZ, lddz, scale, dW, db, dbY, true, workspace, stream,
                           "lpg_heads_relu_bwd_f32");
+}
+
+extern "C" int64_t lpg_heads_bwd_bf16_workspace_bytes(int64_t M, int64_t K, int64_t N) {
+  if (M < 0 || K < 0 || N < 0) return -1;
+  return heads_bwd_floats(M, K, N) * (int64_t)sizeof(float);
+}
+
+// The heads' backward in bf16 (G [M, N] and W [N, K] fp32 holding the bf16 model's values, H the
+// layer output [M, K] bf16): dH (bf16; mask != 0: through the layer's ReLU/dropout backward, the
+// layer's dZ), dW, db, and (dbY != NULL) the column sums of the stored dH -- bitwise
+// lpg_colsum_bf16 on it.  Workspace: lpg_heads_bwd_bf16_workspace_bytes(M, K, N).
+extern "C" lpg_status lpg_heads_bwd_bf16(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W,
+                                         const uint16_t *H, int64_t ldh, int32_t mask, float scale, uint16_t *dH,
+                                         int64_t lddh, float *dW, float *db, float *dbY, void *workspace,
+                                         void *stream) {
+  LPG_REQUIRE(dH != nullptr, "lpg_heads_bwd_bf16: NULL dH");
+  return heads_bwd<true>(M, K, N, G, ldg, W, H, ldh, dH, lddh, scale, dW, db, dbY, mask != 0, workspace, stream,
+                         "lpg_heads_bwd_bf16");
+}
+
+// The heads' forward in bf16: out[m, c] = RNE_bf16(sum_k H[m, k] W[c, k] + bias[c]), N <= 4,
+// K <= 2048 (W fp32 holding the bf16 model's values; out bf16 [M, N] with leading dim ldo).
+extern "C" lpg_status lpg_linear_small_fwd_bf16(int64_t M, int64_t K, int64_t N, const uint16_t *H, int64_t ldh,
+                                                const float *W, const float *bias, uint16_t *out, int64_t ldo,
+                                                void *stream) {
+  const char *what = "lpg_linear_small_fwd_bf16";
+  LPG_REQUIRE(M >= 0 && K >= 8 && K <= 2048 && K % 8 == 0 && N >= 1 && N <= kSmallNMax,
+              "%s: need 1 <= N <= %d and 8 <= K <= 2048, K %% 8 == 0", what, kSmallNMax);
+  if (M == 0) return LPG_OK;
+  LPG_REQUIRE(H && W && out && ldh >= K && ldh % 8 == 0 && ldo >= N && aligned16(H) && aligned16(W),
+              "%s: bad H/W/out (H, W 16-byte aligned, ldh a multiple of 8)", what);
+  const int64_t waves = (M + kRowsPerWaveFwd - 1) / kRowsPerWaveFwd;
+  int64_t blocks = (waves + 3) / 4;
+  blocks = blocks < 4096 ? blocks : 4096;
+  const int kc = (int)((K + 511) / 512);
+  hipStream_t s = as_stream(stream);
+#define LPG_LF(NN, KC) \
+  hipLaunchKernelGGL((linear_small_fwd_bf16<NN, KC>), dim3((unsigned)blocks), dim3(256), 0, s, M, K, H, ldh, W, bias, out, ldo)
+#define LPG_LFN(NN)          \
+  switch (kc) {              \
+    case 1: LPG_LF(NN, 1); break; \
+    case 2: LPG_LF(NN, 2); break; \
+    case 3: LPG_LF(NN, 3); break; \
+    default: LPG_LF(NN, 4);  \
+  }
+  switch (N) {
+    case 1: LPG_LFN(1) break;
+    case 2: LPG_LFN(2) break;
+    case 3: LPG_LFN(3) break;
+    default: LPG_LFN(4)
+  }
+#undef LPG_LFN
+#undef LPG_LF
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
 }

@@ -34,4 +34,27 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 
 inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Compute units of the current device (cached per device id).
+inline int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// Workgroups of `kernel` (block of `threads`) that stay resident on the whole device at once:
+// the grid of a persistent (row-range) kernel, so that no tail round follows.
+template <typename K>
+inline int64_t resident_blocks(K kernel, int threads) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  return (int64_t)per_cu * device_cus();
+}
+
 }  // namespace lpg

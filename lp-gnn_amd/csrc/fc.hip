@@ -340,29 +340,42 @@ __device__ __forceinline__ void load_row_k(float (&x)[K > 0 ? K : 1], const floa
 }
 
 template <int K1, int K2, bool RELU>
-__global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
+__global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
   static_assert(K1 % 4 == 0 && K2 % 4 == 0 && K1 >= 4, "small-K kernel: K1, K2 multiples of 4");
   constexpr int KT = K1 + K2;
-  // the block's rows of [A1 | A2] staged once in LDS (coalesced), so the row
-  // loop never waits on a global load; every lane then reads the same row
-  // values (LDS broadcast)
-  __shared__ __attribute__((aligned(16))) float sx[kSmallKRows * KT];
-  const int64_t r0 = (int64_t)blockIdx.x * kSmallKRows;
-  const int64_t r1 = r0 + kSmallKRows < a.M ? r0 + kSmallKRows : a.M;
-  for (int i = threadIdx.x; i < kSmallKRows * KT; i += 256) {
-    const int r = i / KT, k = i % KT;
-    const int64_t m = r0 + r < r1 ? r0 + r : r1 - 1;  // rows past r1 are never stored
-    sx[i] = k < K1 ? a.A1[m * a.lda1 + k] : a.A2[m * a.lda2 + (k - K1)];
-  }
-  __syncthreads();
-  const int64_t c = (int64_t)blockIdx.y * 1024 + (int64_t)threadIdx.x * 4;
-  if (c >= a.N) return;
+  constexpr int AE = kSmallKRows * KT / 256;  // staged values per thread per chunk
+  // Block (column group, s) owns rows [s M / S, (s + 1) M / S) (the grid is about what stays
+  // resident, so there is no tail round), walked in chunks of kSmallKRows rows whose [A1 | A2]
+  // rows are staged in LDS (double-buffered; the next chunk's values are loaded a chunk ahead,
+  // every load of a chunk in flight together -- one at a time the staging cost a memory latency
+  // per value); every lane then reads the same row values (LDS broadcast)
+  __shared__ __attribute__((aligned(16))) float sx[2][kSmallKRows * KT];
+  const int64_t sb = blockIdx.y;
+  const int64_t rb = sb * a.M / S, re = (sb + 1) * a.M / S;
+  if (re <= rb) return;  // (block-uniform)
+  const int nch = (int)((re - rb + kSmallKRows - 1) / kSmallKRows);
+  float xr_next[AE];
+  auto load_x = [&](int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < AE; ++j) {
+      const int i = threadIdx.x + 256 * j, r = i / KT, k = i % KT;
+      const int64_t m = r0 + r < re ? r0 + r : re - 1;  // rows past re are never stored
+      xr_next[j] = k < K1 ? a.A1[m * a.lda1 + k] : a.A2[m * a.lda2 + (k - K1)];
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < AE; ++j) sx[buf][threadIdx.x + 256 * j] = xr_next[j];
+  };
+  const int64_t c = (int64_t)blockIdx.x * 1024 + (int64_t)threadIdx.x * 4;
+  const bool col_ok = c < a.N;
+  const int64_t cc = col_ok ? c : 0;  // (lanes past N compute column 0 and store nothing)
   float w1[4][K1], w2[4][K2 > 0 ? K2 : 1], b[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    load_row_k<K1>(w1[j], a.W1, a.ldw1, c + j);
-    load_row_k<K2>(w2[j], a.W2, a.ldw2, c + j);
-    b[j] = a.bias ? a.bias[c + j] : 0.f;
+    load_row_k<K1>(w1[j], a.W1, a.ldw1, cc + j);
+    load_row_k<K2>(w2[j], a.W2, a.ldw2, cc + j);
+    b[j] = a.bias ? a.bias[cc + j] : 0.f;
   }
   f32x2 wp1[2][K1], wp2[2][K2 > 0 ? K2 : 1];  // column pairs (0,1), (2,3), packed once
 #pragma unroll
@@ -372,6 +385,10 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
 #pragma unroll
     for (int k = 0; k < K2; ++k) wp2[jp][k] = f32x2{w2[2 * jp][k], w2[2 * jp + 1][k]};
   }
+  load_x(rb);
+  store_x(0);
+  __syncthreads();
+  if (nch > 1) load_x(rb + kSmallKRows);
   // the row loop with the addend / bias / dropout choices made once per launch (uniform branches
   // per element cost more than the arithmetic of this write-bound kernel); the dropout column keys
   // once per thread, the row key once per row -- the same mask bits as drop_hash(seed, row, col)
@@ -382,42 +399,54 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) ck[j] = drop_col_key(c + j);
     }
-    for (int64_t m = r0; m < r1; ++m) {
-      const float *xr = sx + (m - r0) * KT;
-      const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + m) : 0u;
-      float o[4];
-      // columns in pairs: one v_pk_fma_f32 advances two independent chains
-      // (a true fma per element -- the same bits as the scalar chains)
+    for (int ch = 0; ch < nch; ++ch) {
+      const int64_t r0 = rb + (int64_t)ch * kSmallKRows;
+      const int64_t r1 = r0 + kSmallKRows < re ? r0 + kSmallKRows : re;
+      const float *xb = sx[ch & 1];
+      if (col_ok) {
+        for (int64_t m = r0; m < r1; ++m) {
+          const float *xr = xb + (m - r0) * KT;
+          const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + m) : 0u;
+          float o[4];
+          // columns in pairs: one v_pk_fma_f32 advances two independent chains
+          // (a true fma per element -- the same bits as the scalar chains)
 #pragma unroll
-      for (int j = 0; j < 4; j += 2) {
-        // each part (<= 16 k) is one numerics block: its own chain from +0, then added to the total
-        f32x2 p1 = {0.f, 0.f};
+          for (int j = 0; j < 4; j += 2) {
+            // each part (<= 16 k) is one numerics block: its own chain from +0, then added to the total
+            f32x2 p1 = {0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < (K1 + 7) / 8 * 8; ++i) {
-          const int k = pik(i);
-          if (k < K1) p1 = __builtin_elementwise_fma(f32x2{xr[k], xr[k]}, wp1[j / 2][k], p1);
-        }
-        f32x2 t = f32x2{0.f, 0.f} + p1;
-        if (K2 > 0) {
-          f32x2 p2 = {0.f, 0.f};
+            for (int i = 0; i < (K1 + 7) / 8 * 8; ++i) {
+              const int k = pik(i);
+              if (k < K1) p1 = __builtin_elementwise_fma(f32x2{xr[k], xr[k]}, wp1[j / 2][k], p1);
+            }
+            f32x2 t = f32x2{0.f, 0.f} + p1;
+            if (K2 > 0) {
+              f32x2 p2 = {0.f, 0.f};
 #pragma unroll
-          for (int i = 0; i < (K2 + 7) / 8 * 8; ++i) {
-            const int k = pik(i);
-            if (k < K2) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[j / 2][k], p2);
+              for (int i = 0; i < (K2 + 7) / 8 * 8; ++i) {
+                const int k = pik(i);
+                if (k < K2) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[j / 2][k], p2);
+              }
+              t = t + p2;
+            }
+            if constexpr (ACC) t = t + f32x2{a.C[m * a.ldc + c + j], a.C[m * a.ldc + c + j + 1]};
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              float v = t[e];
+              if constexpr (BIAS) v = v + b[j + e];
+              if (RELU) v = (v < 0.f) ? 0.f : v;
+              if constexpr (DROP) v = drop_hash_k(rk, ck[j + e]) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+              o[j + e] = v;
+            }
           }
-          t = t + p2;
-        }
-        if constexpr (ACC) t = t + f32x2{a.C[m * a.ldc + c + j], a.C[m * a.ldc + c + j + 1]};
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          float v = t[e];
-          if constexpr (BIAS) v = v + b[j + e];
-          if (RELU) v = (v < 0.f) ? 0.f : v;
-          if constexpr (DROP) v = drop_hash_k(rk, ck[j + e]) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-          o[j + e] = v;
+          *reinterpret_cast<float4 *>(a.C + m * a.ldc + c) = make_float4(o[0], o[1], o[2], o[3]);
         }
       }
-      *reinterpret_cast<float4 *>(a.C + m * a.ldc + c) = make_float4(o[0], o[1], o[2], o[3]);
+      if (ch + 1 < nch) {  // the next chunk's rows (loaded a chunk ago) into the other buffer
+        store_x((ch + 1) & 1);
+        lds_barrier();  // (not __syncthreads: its fence would wait for the stores in flight)
+        if (ch + 2 < nch) load_x(r0 + 2 * kSmallKRows);
+      }
     }
   };
   using T_ = std::true_type;
@@ -432,13 +461,22 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a) {
   }
 }
 
+// row ranges of the small-K kernels: the blocks that stay resident, shared by the column
+// groups, at least one chunk of rows each
+inline int64_t smallk_splits(int64_t M, int64_t ncg, int64_t resident) {
+  int64_t s = resident / (ncg > 0 ? ncg : 1);
+  const int64_t chunks = (M + kSmallKRows - 1) / kSmallKRows;
+  s = s < chunks ? s : chunks;
+  return s < 1 ? 1 : s;
+}
+
 template <int K1, int K2>
 lpg_status launch_smallk(const FcArgs &a, bool relu, hipStream_t s) {
-  const dim3 grid((unsigned)((a.M + kSmallKRows - 1) / kSmallKRows), (unsigned)((a.N + 1023) / 1024));
-  if (relu)
-    hipLaunchKernelGGL((fc_smallk_f32<K1, K2, true>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((fc_smallk_f32<K1, K2, false>), grid, dim3(256), 0, s, a);
+  const int64_t ncg = (a.N + 1023) / 1024;
+  auto kern = relu ? fc_smallk_f32<K1, K2, true> : fc_smallk_f32<K1, K2, false>;
+  const int64_t S = smallk_splits(a.M, ncg, resident_blocks(kern, 256));
+  const dim3 grid((unsigned)ncg, (unsigned)S);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, a, S);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -446,7 +484,7 @@ lpg_status launch_smallk(const FcArgs &a, bool relu, hipStream_t s) {
 // K1, K2 multiples of 4, 4 <= K1, K1 + K2 <= 16; returns false if not covered
 bool try_smallk(const FcArgs &a, bool relu, hipStream_t s, lpg_status *st) {
   if (a.K1 < 4 || a.K1 + a.K2 > 16 || a.N % 4 || a.ldc % 4 || !aligned16(a.C)) return false;
-  if (a.M >= ((int64_t)1 << 31) * kSmallKRows) return false;
+  if ((a.N + 1023) / 1024 >= 65536) return false;
   switch (a.K1 * 100 + a.K2) {
 #define LPG_SK(X, Y) case X * 100 + Y: *st = launch_smallk<X, Y>(a, relu, s); return true;
     LPG_SK(4, 0) LPG_SK(4, 4) LPG_SK(4, 8) LPG_SK(4, 12) LPG_SK(8, 0) LPG_SK(8, 4) LPG_SK(8, 8)

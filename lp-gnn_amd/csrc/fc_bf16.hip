@@ -1010,6 +1010,150 @@ __global__ __launch_bounds__(256) void transpose_bf16(int64_t R, int64_t C, cons
     }
   }
 }
+
+// conv1 in bf16 (c5): K1 + K2 <= 16 LP features, so the launch is the [M, N] bf16 output write
+// (the MFMA kernel ran it on K zero-padded to 64 + 64: 0.44 ms per c5 step).  The block's rows of
+// [A1 | A2] are staged once in LDS as fp32, a thread's 4 columns of weights live in registers as
+// column pairs (v_pk_fma_f32); each output is one fp32 fma chain over the exact bf16 x bf16 products
+// of the A1 part, the A2 part's chain added to it, then epilogue_bf16's order: + addend, + bias,
+// ReLU, dropout (the shared mask hash, row key row_off + m), RNE to bf16.  The MFMA kernel sums the
+// same exact products in its own order, so the two agree to fp32 summation order (tolerance).
+constexpr int kSmallKRowsB = 64;
+
+template <int K1, int K2, bool RELU>
+__global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
+  static_assert(K1 % 4 == 0 && K2 % 4 == 0 && K1 >= 4, "small-K kernel: K1, K2 multiples of 4");
+  constexpr int KT = K1 + K2;
+  constexpr int AE = kSmallKRowsB * KT / 256;  // staged values per thread per chunk
+  // rows [s M / S, (s + 1) M / S) per block (a resident grid: no tail round), in chunks whose rows
+  // are staged double-buffered, a chunk ahead, every load of a chunk in flight together
+  __shared__ __attribute__((aligned(16))) float sx[2][kSmallKRowsB * KT];
+  const int64_t sb = blockIdx.y;
+  const int64_t rb = sb * a.M / S, re = (sb + 1) * a.M / S;
+  if (re <= rb) return;  // (block-uniform)
+  const int nch = (int)((re - rb + kSmallKRowsB - 1) / kSmallKRowsB);
+  uint32_t xr_next[AE];  // raw: converted when stored, so nothing waits for the loads before then
+  auto load_x = [&](int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < AE; ++j) {
+      const int i = threadIdx.x + 256 * j, r = i / KT, k = i % KT;
+      const int64_t m = r0 + r < re ? r0 + r : re - 1;  // rows past re are never stored
+      xr_next[j] = k < K1 ? a.A1[m * a.lda1 + k] : a.A2[m * a.lda2 + (k - K1)];
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < AE; ++j) sx[buf][threadIdx.x + 256 * j] = bf16_to_f32(xr_next[j]);
+  };
+  const int64_t c = (int64_t)blockIdx.x * 1024 + (int64_t)threadIdx.x * 4;
+  const bool col_ok = c < a.N;
+  const int64_t cc = col_ok ? c : 0;  // (lanes past N compute column 0 and store nothing)
+  f32x2 wp1[2][K1], wp2[2][K2 > 0 ? K2 : 1], bp[2];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+      wp1[jp][k] = f32x2{bf16_to_f32(a.W1[(cc + 2 * jp) * a.ldw1 + k]), bf16_to_f32(a.W1[(cc + 2 * jp + 1) * a.ldw1 + k])};
+#pragma unroll
+    for (int k = 0; k < K2; ++k)
+      wp2[jp][k] = f32x2{bf16_to_f32(a.W2[(cc + 2 * jp) * a.ldw2 + k]), bf16_to_f32(a.W2[(cc + 2 * jp + 1) * a.ldw2 + k])};
+    bp[jp] = a.bias ? f32x2{a.bias[cc + 2 * jp], a.bias[cc + 2 * jp + 1]} : f32x2{0.f, 0.f};
+  }
+  load_x(rb);
+  store_x(0);
+  __syncthreads();
+  if (nch > 1) load_x(rb + kSmallKRowsB);
+  auto rows = [&](auto acc_c, auto drop_c) {
+    constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
+    uint32_t ck[4];
+    if constexpr (DROP) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ck[j] = drop_col_key(c + j);
+    }
+    for (int ch = 0; ch < nch; ++ch) {
+      const int64_t r0 = rb + (int64_t)ch * kSmallKRowsB;
+      const int64_t r1 = r0 + kSmallKRowsB < re ? r0 + kSmallKRowsB : re;
+      const float *xb = sx[ch & 1];
+      if (col_ok) {
+        for (int64_t m = r0; m < r1; ++m) {
+          const float *xr = xb + (m - r0) * KT;
+          uint2 add = make_uint2(0u, 0u);
+          if constexpr (ACC) add = *reinterpret_cast<const uint2 *>(a.C + m * a.ldc + c);
+          const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + m) : 0u;
+          uint32_t out[2];
+#pragma unroll
+          for (int jp = 0; jp < 2; ++jp) {
+            f32x2 t = {0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < K1; ++k) t = __builtin_elementwise_fma(f32x2{xr[k], xr[k]}, wp1[jp][k], t);
+            if constexpr (K2 > 0) {
+              f32x2 p2 = {0.f, 0.f};
+#pragma unroll
+              for (int k = 0; k < K2; ++k) p2 = __builtin_elementwise_fma(f32x2{xr[K1 + k], xr[K1 + k]}, wp2[jp][k], p2);
+              t = t + p2;
+            }
+            if constexpr (ACC) {
+              const uint32_t w = jp ? add.y : add.x;
+              t = t + f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+            }
+            t = t + bp[jp];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              float v = t[e];
+              if (RELU) v = v < 0.f ? 0.f : v;
+              if constexpr (DROP) v = drop_hash_k(rk, ck[2 * jp + e]) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+              t[e] = v;
+            }
+            out[jp] = __builtin_bit_cast(uint32_t, __builtin_convertvector(t, bf16x2));
+          }
+          *reinterpret_cast<uint2 *>(a.C + m * a.ldc + c) = make_uint2(out[0], out[1]);
+        }
+      }
+      if (ch + 1 < nch) {  // the next chunk's rows (loaded a chunk ago) into the other buffer
+        store_x((ch + 1) & 1);
+        lds_barrier();  // (not __syncthreads: its fence would wait for the stores in flight)
+        if (ch + 2 < nch) load_x(r0 + 2 * kSmallKRowsB);
+      }
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  const bool drop = RELU && a.drop_thresh;
+  if (a.accum) {
+    if (drop) rows(T_{}, T_{}); else rows(T_{}, F_{});
+  } else {
+    if (drop) rows(F_{}, T_{}); else rows(F_{}, F_{});
+  }
+}
+
+template <int K1, int K2>
+lpg_status launch_smallk_bf16(const FcB16Args &a, bool relu, hipStream_t s) {
+  const int64_t ncg = (a.N + 1023) / 1024, chunks = (a.M + kSmallKRowsB - 1) / kSmallKRowsB;
+  auto kern = relu ? fc_smallk_bf16<K1, K2, true> : fc_smallk_bf16<K1, K2, false>;
+  int64_t S = resident_blocks(kern, 256) / ncg;  // the resident blocks, shared by the column groups
+  S = S < chunks ? S : chunks;
+  S = S < 1 ? 1 : S;
+  const dim3 grid((unsigned)ncg, (unsigned)S);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, a, S);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+// The small-K shapes (4 <= K1, K1 + K2 <= 16, multiples of 4; N, ldc multiples of 4, C 8-byte
+// aligned); false if not covered
+bool try_smallk_bf16(const FcB16Args &a, bool relu, hipStream_t s, lpg_status *st) {
+  if (a.K1 < 4 || a.K1 + a.K2 > 16 || a.K1 % 4 || a.K2 % 4 || a.N % 4 || a.ldc % 4 ||
+      (reinterpret_cast<uintptr_t>(a.C) & 7))
+    return false;
+  if ((a.N + 1023) / 1024 >= 65536) return false;
+  switch (a.K1 * 100 + a.K2) {
+#define LPG_SKB(X, Y) case X * 100 + Y: *st = launch_smallk_bf16<X, Y>(a, relu, s); return true;
+    LPG_SKB(4, 0) LPG_SKB(4, 4) LPG_SKB(4, 8) LPG_SKB(4, 12) LPG_SKB(8, 0) LPG_SKB(8, 4) LPG_SKB(8, 8)
+    LPG_SKB(12, 0) LPG_SKB(12, 4) LPG_SKB(16, 0)
+#undef LPG_SKB
+  }
+  return false;
+}
 }  // namespace
 }  // namespace lpg
 
@@ -1023,22 +1167,22 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_bf16: negative size");
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_bf16: bad C/ldc");
-  LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "lpg_fc_bf16: K1, K2 must be multiples of %d (pad the features)", BK);
   LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1), "lpg_fc_bf16: bad A1/W1");
   LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2), "lpg_fc_bf16: bad A2/W2");
-  LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
-                  (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
-              "lpg_fc_bf16: A/W must be 16-byte aligned with leading dimensions multiple of 8");
   const int kernel = (flags >> 8) & 15;
   LPG_REQUIRE((flags & ~0xf03) == 0 && kernel <= kKernels, "lpg_fc_bf16: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_bf16: dropout_p %g not in [0, 1)", (double)dropout_p);
   FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1,
               nullptr, 0, 1.f, row_offset};
-  if (dropout_p > 0.f) {
-    const double th = (double)dropout_p * 4294967296.0;
-    a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);
-    a.drop_scale = 1.f / (1.f - dropout_p);
-  }
+  dropout_params(dropout_p, &a.drop_thresh, &a.drop_scale);
+  lpg_status st;
+  if (try_smallk_bf16(a, flags & 1, as_stream(stream), &st)) return st;  // conv1: narrow LP features
+  LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0,
+              "lpg_fc_bf16: K1, K2 must be multiples of %d (zero-pad) unless 4 <= K1, K1 + K2 <= 16 (multiples of 4) "
+              "and N, ldc are multiples of 4", BK);
+  LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
+                  (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
+              "lpg_fc_bf16: A/W must be 16-byte aligned with leading dimensions multiple of 8");
   return fc_bf16_dispatch(a, flags & 1, as_stream(stream), kernel);
 }
 

@@ -62,6 +62,12 @@ __device__ __forceinline__ uint32_t relu_bwd_pk_bf16(uint32_t g, uint32_t y, flo
   return (y0 > 0.f ? (pk & 0xffffu) : 0u) | (y1 > 0.f ? (pk & 0xffff0000u) : 0u);
 }
 
+// A workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, then
+// s_barrier.  __syncthreads() also carries a release fence, i.e. s_waitcnt vmcnt(0): every
+// global load and store the wave has in flight -- a streaming kernel that stages rows in LDS
+// drained its prefetched loads (and its stores) at each such barrier.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Host-side dropout threshold / scale shared by the FC entry points.
 inline void dropout_params(float p, uint32_t *thresh, float *scale) {
   *thresh = 0u;

@@ -177,7 +177,11 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
             g = torch.zeros_like(y)
         if getattr(ctx, "out_folded", False):  # the next layer's input-gradient store applied our ReLU backward
             g = g.to(dt).contiguous()
-            return g, (_fc.colsum_bf16(g) if want_db else None)
+            if not want_db:
+                return g, None
+            # the bf16 heads' backward already summed these columns (fc.heads_bwd_bf16: the bits of colsum_bf16)
+            pre = (getattr(ctx, "folded_colsum", None) or {}).pop(y.data_ptr(), None)
+            return g, (pre[1] if pre is not None and pre[0] == g.data_ptr() else _fc.colsum_bf16(g))
         if not ctx.relu:
             g = g.to(dt).contiguous()
             return g, (g.float().sum(0) if want_db else None)
@@ -185,17 +189,21 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
             return _fc.relu_bwd_colsum_bf16(g, y, ctx.scale, want_db)
         return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
 
-    small = (dz is None and not bf16 and ctx.relu and agg_r is not None and agg_l is not None
+    small = (dz is None and ctx.relu and agg_r is not None and agg_l is not None
              and agg_r.shape[1] + right.shape[1] <= 16 and agg_l.shape[1] + left.shape[1] <= 16
-             and right_new.shape[1] % 4 == 0)
+             and right_new.shape[1] % 4 == 0 and left_new.shape[1] % 4 == 0)
     if small and not (need[0] or need[1]):
-        # conv1: the inputs are features -- weight and bias gradients straight from (g, y)
+        # conv1: the inputs are features -- weight and bias gradients straight from (g, y); bf16: from
+        # dZ itself when the next layer's input-gradient store already applied the ReLU backward
         g_r0 = torch.zeros_like(right_new) if g_right is None else g_right
         g_l0 = torch.zeros_like(left_new) if g_left is None else g_left
-        dw_rel_l2r, dw_root_l2r, db_l2r = _fc.relu_wgrad_smallk(g_r0, right_new, ctx.scale, agg_r, right,
-                                                                ctx.has_b[0] and need[4])
-        dw_rel_r2l, dw_root_r2l, db_r2l = _fc.relu_wgrad_smallk(g_l0, left_new, ctx.scale, agg_l, left,
-                                                                ctx.has_b[1] and need[7])
+        if bf16:
+            folded = getattr(ctx, "out_folded", False)
+            wk = lambda g, y, a, x, wb: _fc.relu_wgrad_smallk_bf16(g, None if folded else y, ctx.scale, a, x, wb)
+        else:
+            wk = lambda g, y, a, x, wb: _fc.relu_wgrad_smallk(g, y, ctx.scale, a, x, wb)
+        dw_rel_l2r, dw_root_l2r, db_l2r = wk(g_r0, right_new, agg_r, right, ctx.has_b[0] and need[4])
+        dw_rel_r2l, dw_root_r2l, db_r2l = wk(g_l0, left_new, agg_l, left, ctx.has_b[1] and need[7])
         keep = lambda t, i: t if need[i] else None
         return (None, None, None, keep(dw_rel_l2r, 3), db_l2r, keep(dw_root_l2r, 5), keep(dw_rel_r2l, 6), db_r2l,
                 keep(dw_root_r2l, 8), None, None)

@@ -261,7 +261,18 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
-    A1, W1, A2, W2 = _prep_bf16(A1), _prep_bf16(W1), _prep_bf16(A2), _prep_bf16(W2)
+    k1, k2 = A1.shape[1], (0 if A2 is None else A2.shape[1])
+    # conv1 (narrow LP features): the streaming small-K kernel takes the operands unpadded
+    small = (mask is None and 4 <= k1 and k1 + k2 <= 16 and k1 % 4 == 0 and k2 % 4 == 0 and N % 4 == 0
+             and (out is None or (out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0)))
+    if small:
+        A1, W1 = A1.contiguous(), W1.contiguous()
+        A2 = None if A2 is None else A2.contiguous()
+        W2 = None if W2 is None else W2.contiguous()
+        if any(t is not None and t.dtype != torch.bfloat16 for t in (A1, W1, A2, W2)):
+            raise RuntimeError("lpgnn bf16 FC: bf16 operands expected")
+    else:
+        A1, W1, A2, W2 = _prep_bf16(A1), _prep_bf16(W1), _prep_bf16(A2), _prep_bf16(W2)
     bias = None if bias is None else bias.float().contiguous()
     if out is not None:
         if out.shape != (M, N) or out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.device != A1.device:
@@ -473,6 +484,84 @@ def relu_wgrad_smallk(g: Tensor, y: Tensor, scale: float, A1: Tensor, A2: Tensor
     return dW1, dW2, db
 
 
+def relu_wgrad_smallk_bf16(g: Tensor, y: Tensor | None, scale: float, A1: Tensor, A2: Tensor | None, want_db: bool):
+    """bf16 twin of relu_wgrad_smallk (c5 conv1, lpg_relu_wgrad_smallk_bf16): (dW1, dW2, db) fp32 from one
+    read of the gradient.  ``y`` None: g already is dZ (the next layer folded this layer's ReLU /
+    dropout backward into its input-gradient store); else dZ = (y > 0) ? bf16(g * scale) : 0 on the fly."""
+    M, N = g.shape
+    g = g.to(torch.bfloat16).contiguous()
+    y = None if y is None else y.contiguous()
+    A1 = A1.to(torch.bfloat16).contiguous()
+    A2 = None if A2 is None else A2.to(torch.bfloat16).contiguous()
+    K1, K2 = A1.shape[1], (0 if A2 is None else A2.shape[1])
+    L = _lib.lib()
+    ws = _workspace(L.lpg_wgrad_smallk_workspace_bytes(M, N, K1 + K2), g.device)
+    dW1 = torch.empty((N, K1), dtype=torch.float32, device=g.device)
+    dW2 = torch.empty((N, K2), dtype=torch.float32, device=g.device) if K2 else None
+    db = torch.empty(N, dtype=torch.float32, device=g.device) if want_db else None
+    with torch.cuda.device(g.device):
+        tok = TIMER.start(("wgrad_smallk", M, N, K1 + K2, "bf16"))
+        st = L.lpg_relu_wgrad_smallk_bf16(M, N, g.data_ptr(), g.stride(0), None if y is None else y.data_ptr(),
+                                          0 if y is None else y.stride(0), float(scale), K1, A1.data_ptr(), max(K1, 1),
+                                          K2, None if A2 is None else A2.data_ptr(), max(K2, 1), dW1.data_ptr(),
+                                          None if dW2 is None else dW2.data_ptr(), None if db is None else db.data_ptr(),
+                                          ws.data_ptr(), _lib.stream_of(g))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_relu_wgrad_smallk_bf16")
+    return dW1, dW2, db
+
+
+def _small_heads_bf16(x: Tensor, W: Tensor) -> bool:
+    """The bf16 heads' streaming kernels take this Linear (N <= 4 outputs, K <= 2048)."""
+    K = x.shape[1]
+    return (x.dtype == torch.bfloat16 and W.shape[0] <= 4 and 8 <= K <= 2048 and K % 8 == 0 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0)
+
+
+def linear_small_fwd_bf16(x: Tensor, W: Tensor, b: Tensor | None) -> Tensor:
+    """The bf16 heads' forward (lpg_linear_small_fwd_bf16): bf16 [M, N] = RNE(x W^T + b), W rounded to
+    bf16 first (the c5 model's weights), fp32 sums."""
+    M, K = x.shape
+    N = W.shape[0]
+    Wf = W.detach().to(torch.bfloat16).float().contiguous()
+    b = None if b is None else b.detach().float().contiguous()
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    with torch.cuda.device(x.device):
+        tok = TIMER.start(("heads_fwd", M, N, K, "bf16"))
+        st = _lib.lib().lpg_linear_small_fwd_bf16(M, K, N, x.data_ptr(), x.stride(0), Wf.data_ptr(),
+                                                  None if b is None else b.data_ptr(), out.data_ptr(), N,
+                                                  _lib.stream_of(x))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_linear_small_fwd_bf16")
+    return out
+
+
+def heads_bwd_bf16(G: Tensor, W: Tensor, Y: Tensor, scale: float | None, want_dby: bool):
+    """(dH, dW, db, dbY) of the bf16 heads in one pass over their input Y (lpg_heads_bwd_bf16).
+    ``scale`` not None: dH goes through the producing layer's ReLU/dropout backward (the layer's dZ,
+    the bits of the separate relu_bwd_colsum_bf16 pass), and dbY = its column sums (the bits of
+    colsum_bf16 on dH)."""
+    M, K = Y.shape
+    N = W.shape[0]
+    Gf = G.float().contiguous()
+    Wf = W.detach().to(torch.bfloat16).float().contiguous()
+    L = _lib.lib()
+    ws = _workspace(L.lpg_heads_bwd_bf16_workspace_bytes(M, K, N), Y.device)
+    dH = torch.empty((M, K), dtype=torch.bfloat16, device=Y.device)
+    dW = torch.empty((N, K), dtype=torch.float32, device=Y.device)
+    db = torch.empty(N, dtype=torch.float32, device=Y.device)
+    dbY = torch.empty(K, dtype=torch.float32, device=Y.device) if want_dby else None
+    with torch.cuda.device(Y.device):
+        tok = TIMER.start(("heads_bwd", M, N, K, "bf16"))
+        st = L.lpg_heads_bwd_bf16(M, K, N, Gf.data_ptr(), Gf.stride(0), Wf.data_ptr(), Y.data_ptr(), Y.stride(0),
+                                  0 if scale is None else 1, 1.0 if scale is None else float(scale), dH.data_ptr(), K,
+                                  dW.data_ptr(), db.data_ptr(), None if dbY is None else dbY.data_ptr(), ws.data_ptr(),
+                                  _lib.stream_of(Y))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_heads_bwd_bf16")
+    return dH, dW, db, dbY
+
+
 def _new_seed() -> int:
     """A dropout seed from torch's default generator (torch.manual_seed reproducible)."""
     return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
@@ -585,12 +674,17 @@ class _Linear(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.bf16 = x.dtype == torch.bfloat16
         ctx.in_scale = None
+        ctx.small, ctx.prev = False, None
         if prev is not None:  # x = a bf16 ReLU layer's output feeding only this Linear: fold its backward
             ctx.in_scale = prev.scale
             prev.out_folded = True
         if ctx.bf16:
             W = W.to(torch.bfloat16)
             ctx.save_for_backward(x, W)
+            ctx.small = _small_heads_bf16(x, W)
+            ctx.prev = prev
+            if ctx.small:  # the heads (N = 3): one streaming pass over x
+                return linear_small_fwd_bf16(x, W, b)
             return fc_forward_bf16(x, W, None, None, b, False)
         ctx.save_for_backward(x, W)
         return fc_forward(x, W, None, None, b, False)
@@ -599,6 +693,16 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, g):
         x, W = ctx.saved_tensors
         need = ctx.needs_input_grad
+        if ctx.bf16 and ctx.small:
+            # one pass over x: dx (through the producing layer's ReLU/dropout backward when folded),
+            # dW, db, and that layer's bias column sums, handed to its backward node (conv.py)
+            dx, dW, db, dby = heads_bwd_bf16(g.to(torch.bfloat16), W, x, ctx.in_scale, ctx.in_scale is not None)
+            if ctx.prev is not None and dby is not None:
+                if getattr(ctx.prev, "folded_colsum", None) is None:
+                    ctx.prev.folded_colsum = {}
+                ctx.prev.folded_colsum[x.data_ptr()] = (dx.data_ptr(), dby)
+            ctx.prev = None
+            return (dx if need[0] else None), (dW if need[1] else None), (db if ctx.has_b and need[2] else None), None
         if ctx.bf16:
             g = g.to(torch.bfloat16)
             mask = None if ctx.in_scale is None else (x, ctx.in_scale)

@@ -885,7 +885,8 @@ def rho_sweep(args, rank: int, world: int, rhos, F: int) -> list:
         spec = bench_spec(a, world)
         plan = plan_partition_blocks(spec, world, rank)
         mine = [int(plan.halo.shape[0]), int(plan.n_own), int(sum(plan.send_counts)), int(sum(plan.recv_counts)),
-                sum(1 for c in plan.send_counts if c) + sum(1 for c in plan.recv_counts if c)]
+                len({r for r, c in enumerate(plan.send_counts) if c and r != rank} |
+                    {r for r, c in enumerate(plan.recv_counts) if c and r != rank})]  # distinct peer ranks
         every = [None] * world
         dist.all_gather_object(every, mine)
         rows = [h[2] + h[3] for h in every]

@@ -420,12 +420,15 @@ def bench_fcpi(out):
 
 
 def bench_stream(out):
-    """The c2 step's streaming kernels at 100K / 200K x 1024 (GB/s of the bytes each must move):
-    heads + ReLU backward (read Y, write dZ), conv1 weight gradients from (g, y) (read both),
-    conv1 forward with ReLU + dropout (write C); torch copy_ / fill_ as the box's streaming rates."""
-    from lpgnn.fc import fc_forward, heads_relu_bwd, relu_wgrad_smallk
+    """The c2 / c5 steps' streaming kernels at 100K / 200K rows (GB/s of the bytes each must move):
+    heads + ReLU backward (read Y, write dZ), conv1 weight gradients from (g, y) or from dZ (read
+    both / one), conv1 forward with ReLU + dropout (write C), the bf16 heads' forward (read Y);
+    fp32 at F = 1024 (c2), bf16 at F = 2048 (c5); torch copy_ / fill_ as the box's streaming rates."""
+    from lpgnn.fc import (fc_forward, fc_forward_bf16, heads_bwd_bf16, heads_relu_bwd, linear_small_fwd_bf16,
+                          relu_wgrad_smallk, relu_wgrad_smallk_bf16)
 
     dev = "cuda"
+    BF = torch.bfloat16
     for M in (100_000, 200_000):
         g = torch.randn(M, 1024, device=dev)
         y = torch.relu(torch.randn(M, 1024, device=dev))
@@ -444,6 +447,24 @@ def bench_stream(out):
             nbytes = nb * (1 if k in ("conv1_fwd", "torch_fill") else 2)
             out[f"stream M={M} {k}"] = dict(ms=v, gbs=nbytes / v / 1e6)
         del g, y, dst
+        # c5 (bf16, F = 2048): the same bytes per row
+        gb = torch.randn(M, 2048, device=dev).to(BF)
+        yb = torch.relu(torch.randn(M, 2048, device=dev)).to(BF)
+        Gb = torch.randn(M, 3, device=dev).to(BF)
+        W3b = torch.randn(3, 2048, device=dev)
+        X8h, X8bh = X8.to(BF), X8b.to(BF)
+        W8h, W8bh = torch.randn(2048, 8, device=dev).to(BF), torch.randn(2048, 8, device=dev).to(BF)
+        b2 = torch.randn(2048, device=dev)
+        nb = M * 2048 * 2
+        t = timeit({"bf16 heads_bwd(mask)": lambda: heads_bwd_bf16(Gb, W3b, yb, 1.1, True),
+                    "bf16 relu_wgrad_smallk(g,y)": lambda: relu_wgrad_smallk_bf16(gb, yb, 1.1, X8h, X8bh, True),
+                    "bf16 wgrad_smallk(dZ)": lambda: relu_wgrad_smallk_bf16(gb, None, 1.0, X8h, X8bh, True),
+                    "bf16 conv1_fwd": lambda: fc_forward_bf16(X8h, W8h, X8bh, W8bh, b2, True, 0.1, 7),
+                    "bf16 heads_fwd": lambda: linear_small_fwd_bf16(yb, W3b, b2[:3])})
+        for k, v in t.items():
+            nbytes = nb * (2 if ("heads_bwd" in k or "(g,y)" in k) else 1)
+            out[f"stream M={M} {k}"] = dict(ms=v, gbs=nbytes / v / 1e6)
+        del gb, yb
 
 
 if __name__ == "__main__":
