@@ -24,6 +24,12 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int kRowsColsum = 64;
+#ifndef LPG_HEADS_U_F32
+#define LPG_HEADS_U_F32 8
+#endif
+#ifndef LPG_HEADS_U_BF16
+#define LPG_HEADS_U_BF16 8
+#endif
 constexpr int kRowsLinear = 128;  // heads_bwd_p1 rows per block (two 64-row column-sum chunks)
 constexpr int kMaxSmallK = 16;
 constexpr int kSmallNMax = 4;
@@ -395,7 +401,7 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
   using E = typename std::conditional<BF, uint16_t, float>::type;
   constexpr int EPT = BF ? 8 : 4;  // columns per thread
   constexpr int P = EPT / 2;       // column pairs
-  constexpr int U = 8;             // rows per group (128 B per lane in flight)
+  constexpr int U = BF ? LPG_HEADS_U_BF16 : LPG_HEADS_U_F32;  // rows per group (8: 128 B per lane in flight)
   constexpr int RB = kRowsLinear;  // rows per block
   constexpr int CH = kRowsColsum;  // column-sum chunk
   static_assert(RB % CH == 0 && CH % (2 * U) == 0, "block shape");

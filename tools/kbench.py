@@ -244,6 +244,23 @@ def bench_fck(out):
             del A, W, P
 
 
+def bench_fckern(out):
+    """lpg_fc_bf16's per-call kernel choices (LPG_FC_KERNEL: 1 = 128 x 128 tiles, 4 waves, 2 blocks
+    per CU; 2 = 256 x 256; 3 = the pipelined 256 x 256 default) at the c5 shapes, ReLU + dropout."""
+    from lpgnn.fc import fc_forward_bf16
+
+    BF = torch.bfloat16
+    for M, K in ((200_000, 2048), (100_000, 4096), (200_000, 4096)):
+        A = torch.randn(M, K, device="cuda").to(BF)
+        W = (torch.randn(2048, K, device="cuda") * 0.02).to(BF)
+        b = torch.randn(2048, device="cuda")
+        fns = {f"kernel={k}": (lambda k=k: fc_forward_bf16(A, W, None, None, b, True, 0.1, 7, kernel=k)) for k in (1, 2, 3)}
+        t = timeit(fns, rounds=5, iters=3)
+        for k, v in t.items():
+            out[f"fckern M={M} K={K} {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * K / v / 1e9)
+        del A, W
+
+
 def bench_wgk(out):
     """lpg_wgrad_bf16 at N = K = 2048 for R = 25K .. 400K: the per-launch fixed cost (prologue,
     partial-tile epilogue, fold) against the per-row slope."""
@@ -474,7 +491,7 @@ if __name__ == "__main__":
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
          "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi, "wgk": bench_wgk, "rbwd": bench_rbwd,
-         "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream, "tail": bench_tail}[w](out)
+         "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream, "tail": bench_tail, "fckern": bench_fckern}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
