@@ -261,6 +261,31 @@ def bench_fckern(out):
         del A, W
 
 
+def bench_epidrop(out):
+    """What each epilogue option costs in the hidden-layer GEMMs: the c5 bf16 FC (M = 200K, N = 2048,
+    K = 2048) and the c2 x3 FC (M = 200K, N = 1024, K = 1024) with plain / bias+ReLU / +dropout /
+    +accumulate epilogues."""
+    from lpgnn.fc import fc_forward, fc_forward_bf16
+
+    BF = torch.bfloat16
+    M = 200_000
+    for name, N, K, dt in (("bf16", 2048, 2048, BF), ("x3", 1024, 1024, torch.float32)):
+        A = torch.randn(M, K, device="cuda").to(dt)
+        W = (torch.randn(N, K, device="cuda") * 0.02).to(dt)
+        b = torch.randn(N, device="cuda")
+        P = torch.randn(M, N, device="cuda").to(dt)
+        fwd = fc_forward_bf16 if name == "bf16" else (lambda *a, **k: fc_forward(*a, arith="x3", **k))
+        fns = {"plain": lambda: fwd(A, W, None, None, None, False),
+               "bias+relu": lambda: fwd(A, W, None, None, b, True),
+               "bias+relu+drop": lambda: fwd(A, W, None, None, b, True, 0.1, 7),
+               "bias+relu+acc": lambda: fwd(A, W, None, None, b, True, out=P, accumulate=True),
+               "bias+relu+drop+acc": lambda: fwd(A, W, None, None, b, True, 0.1, 7, out=P, accumulate=True)}
+        t = timeit(fns, rounds=5, iters=3)
+        for k, v in t.items():
+            out[f"epidrop {name} M={M} N={N} K={K} {k}"] = dict(ms=v, tflops=2.0 * M * N * K / v / 1e9)
+        del A, W, P
+
+
 def bench_wgk(out):
     """lpg_wgrad_bf16 at N = K = 2048 for R = 25K .. 400K: the per-launch fixed cost (prologue,
     partial-tile epilogue, fold) against the per-row slope."""
@@ -491,7 +516,8 @@ if __name__ == "__main__":
         {"fc": bench_fc, "spmm": bench_spmm, "bwd": bench_bwd, "fcpmc": bench_fcpmc, "bf16": bench_bf16,
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
          "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi, "wgk": bench_wgk, "rbwd": bench_rbwd,
-         "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream, "tail": bench_tail, "fckern": bench_fckern}[w](out)
+         "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream, "tail": bench_tail, "fckern": bench_fckern,
+         "epidrop": bench_epidrop}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
