@@ -48,9 +48,11 @@ def test_run_exp_two_epochs_checkpoint_and_validation(tmp_path):
         assert torch.equal(model.state_dict()[k].cpu(), v)
     _, acc, rows = run.validation(model, ds, vargs)
     assert 0.0 <= acc <= 1.0 and len(rows) == 4
-    # --fp16: the bf16 compute path; logits close to the fp32 model's
+    # --fp16: the bf16 compute path for evaluation (val.py:269); training stays fp32 whatever the
+    # flag (the reference's train.py never reads it); logits close to the fp32 model's
     fargs = _args(tmp_path, "--load_from", hist["checkpoint"], "--fp16", "1")
-    m16 = run.make_model(fargs)
+    assert run.make_model(fargs).compute_dtype == torch.float32
+    m16 = run.make_model(fargs, for_eval=True)
     assert m16.compute_dtype == torch.bfloat16
     g = ds[0].to(args.dev)
     with torch.no_grad():
