@@ -536,6 +536,22 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
 // the host falls back to fc_fwd_bf16 otherwise.  (A 4-wave 128 x 128-per-wave
 // form -- 256 accumulators, one wave per SIMD -- measured 670-790 TF/s and
 // spilled; it is gone, see the spill rule in the header.)
+#ifdef LPG_PHASE_PROBE
+// experiments build only (tools/experiments/phase_probe.py): per-block phase timestamps of
+// fc_bf16_p -- start, first tile landed, k loop done, epilogue done -- as s_memrealtime (100 MHz)
+// and s_memtime (core clock), written by lane 0 of wave 0 with vector stores
+__device__ uint64_t *lpg_probe_buf;
+#define LPG_PROBE(i)                                                                               \
+  do {                                                                                             \
+    if (lpg_probe_buf && tid == 0) {                                                               \
+      lpg_probe_buf[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                      \
+      lpg_probe_buf[blockIdx.x * 8 + 4 + (i)] = __builtin_amdgcn_s_memtime();                      \
+    }                                                                                              \
+  } while (0)
+#else
+#define LPG_PROBE(i) do { } while (0)
+#endif
+
 template <int WM, int WN, int FM, int FN, bool RELU>
 __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
   constexpr bool SCHED = true, PRIO = true;
@@ -562,6 +578,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
   const int wm = wave / WN, wn = wave % WN;
   const int nk1 = (int)(a.K1 / BK);
   const int nk = nk1 + (int)(a.K2 / BK);
+  LPG_PROBE(0);
 
   // descriptors from row m0 of A / row n0 of W; a range ends after the block's last row, so the
   // offsets of rows past M (N) -- row * ld * 2 >= (rows - 1) * ld * 2 + K * 2 -- read zeros
@@ -639,6 +656,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
   if (nk > 0) {
     stage(0, 0);
     barrier();
+    LPG_PROBE(1);
     if (nk > 1) stage(1, 1);
     rd(0, 0, a0, b0);
   }
@@ -686,7 +704,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
   // is past its reads
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  LPG_PROBE(2);
   epilogue_bf16_ti<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+#ifdef LPG_PHASE_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (probe build: the epilogue's stores done)
+  LPG_PROBE(3);
+#endif
 }
 
 // ---- weight gradient dW = G^T X in bf16 (fp32 out) ---------------------------
@@ -1158,6 +1181,13 @@ bool try_smallk_bf16(const FcB16Args &a, bool relu, hipStream_t s, lpg_status *s
 }  // namespace lpg
 
 using namespace lpg;
+
+#ifdef LPG_PHASE_PROBE
+extern "C" lpg_status lpg_debug_set_probe(void *p) {
+  LPG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(lpg_probe_buf), &p, sizeof(p)));
+  return LPG_OK;
+}
+#endif
 
 extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
                                   const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
