@@ -48,13 +48,28 @@ inline int device_cus() {
 }
 
 // Workgroups of `kernel` (block of `threads`) that stay resident on the whole device at once:
-// the grid of a persistent (row-range) kernel, so that no tail round follows.
+// the grid of a persistent (row-range) kernel, so that no tail round follows.  The occupancy query
+// runs once per (kernel, block size, device) and host thread (a thread-local cache: no locks).
 template <typename K>
 inline int64_t resident_blocks(K kernel, int threads) {
+  struct Entry {
+    const void *k;
+    int threads, dev;
+    int64_t blocks;
+  };
+  thread_local Entry cache[32];
+  thread_local int used = 0;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  const void *key = reinterpret_cast<const void *>(kernel);
+  for (int i = 0; i < used; ++i)
+    if (cache[i].k == key && cache[i].threads == threads && cache[i].dev == dev) return cache[i].blocks;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
     per_cu = 1;
-  return (int64_t)per_cu * device_cus();
+  const int64_t blocks = (int64_t)per_cu * device_cus();
+  if (used < 32) cache[used++] = Entry{key, threads, dev, blocks};
+  return blocks;
 }
 
 }  // namespace lpg
