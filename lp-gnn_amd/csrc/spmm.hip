@@ -746,10 +746,10 @@ static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, f
   // roofline at c2 vs 0.93 / 0.94 at 256, profiles/r02_kbench_spmm_big.log) unless heavy rows are split
   // off, which the 256-column form does
   if (W == 0) W = hv.blocks == 0 ? 128 : 256;
-  // auto depth: 16 edges in flight for rows of >= 16 edges on average (c2 cons<-vars, degree 20: 0.947
-  // of the edge-gather roofline vs 0.913 at 8), else 8 (vars<-cons, degree 10: 0.938 vs 0.915; a
-  // skewed LP, whose light rows average 5 edges once its heavy rows are split off: 0.98 vs 0.89)
-  const int U = depth != 0 ? depth : (hv.blocks == 0 && A->nnz >= 16 * A->n_rows) ? 16 : 8;
+  // auto depth: 8 edges in flight per batch (round 3, profiles/r03_kbench_spmmdepth.log, same box:
+  // c2 cons<-vars 0.975 at 8 vs 0.967 at 16, vars<-cons 0.980 vs 0.927; depth 32 0.52-0.71; round 2
+  // had measured 16 ahead for cons<-vars, 0.947 vs 0.913; the heavy-row split already used 8)
+  const int U = depth != 0 ? depth : 8;
   if ((W == 64 || W == 128) && hv.blocks == 0) {  // narrow slices (no heavy-row split in this form)
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock), (unsigned)((F + W - 1) / W));
     if (W == 128)
@@ -831,7 +831,9 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
     const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
     LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_bf16: grid too large");
     dim3 grid((unsigned)nblk, (unsigned)((F + 255) / 256));
-    const int U = depth != 0 ? depth : A->nnz >= 16 * A->n_rows ? 16 : 8;
+    // auto depth 8 (c5 cons<-vars 0.970 of the edge-gather roofline at 8 vs 0.903 at 16, vars<-cons
+    // 0.970 vs 0.807: profiles/r03_kbench_spmmdepth.log)
+    const int U = depth != 0 ? depth : 8;
     if (U == 16) return launch(spmm_bf16_rowslim<16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
     return launch(spmm_bf16_rowslim<8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }

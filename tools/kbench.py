@@ -286,6 +286,29 @@ def bench_epidrop(out):
         del A, W, P
 
 
+def bench_spmmdepth(out):
+    """The c2 / c5 SpMMs (uniform 100K x 200K, nnz 2M) at gather depth 8 / 16 / 32, default slices."""
+    from lpgnn import BipartiteCSR, synth
+    from lpgnn.sparse import spmm_forward
+
+    g = synth.uniform_lp(100_000, 200_000, 2_000_000, seed=0)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
+    for dt, F in ((torch.float32, 1024), (torch.bfloat16, 2048)):
+        for name, csr, K in (("cons<-vars", adj.fwd, g.n), ("vars<-cons", adj.bwd, g.m)):
+            X = torch.randn(K, F, device="cuda").to(dt)
+            ref = spmm_forward(csr, X)
+            fns = {}
+            for d in (8, 16, 32):
+                f = (lambda d=d: spmm_forward(csr, X, depth=d))
+                assert torch.equal(f(), ref)
+                fns[f"depth{d}"] = f
+            t = timeit(fns)
+            esz = 2 if dt == torch.bfloat16 else 4
+            B = g.nnz * F * esz + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * F * esz
+            for k, v in t.items():
+                out[f"spmm {dt} {name} {k}"] = dict(ms=v, frac=B / v / 1e6 / 8000)
+
+
 def bench_wgk(out):
     """lpg_wgrad_bf16 at N = K = 2048 for R = 25K .. 400K: the per-launch fixed cost (prologue,
     partial-tile epilogue, fold) against the per-row slope."""
@@ -517,7 +540,7 @@ if __name__ == "__main__":
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
          "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi, "wgk": bench_wgk, "rbwd": bench_rbwd,
          "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream, "tail": bench_tail, "fckern": bench_fckern,
-         "epidrop": bench_epidrop}[w](out)
+         "epidrop": bench_epidrop, "spmmdepth": bench_spmmdepth}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
