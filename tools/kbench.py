@@ -287,7 +287,7 @@ def bench_epidrop(out):
 
 
 def bench_spmmdepth(out):
-    """The c2 / c5 SpMMs (uniform 100K x 200K, nnz 2M) at gather depth 8 / 16 / 32, default slices."""
+    """The c2 / c5 SpMMs (uniform 100K x 200K, nnz 2M) at gather depth 8 / 16 and each slice width."""
     from lpgnn import BipartiteCSR, synth
     from lpgnn.sparse import spmm_forward
 
@@ -298,15 +298,40 @@ def bench_spmmdepth(out):
             X = torch.randn(K, F, device="cuda").to(dt)
             ref = spmm_forward(csr, X)
             fns = {}
-            for d in (8, 16, 32):
-                f = (lambda d=d: spmm_forward(csr, X, depth=d))
-                assert torch.equal(f(), ref)
-                fns[f"depth{d}"] = f
+            slices = (64, 128, 256) if dt == torch.float32 else (256, 512)
+            for d in (8, 16):
+                for sl in slices:
+                    f = (lambda d=d, sl=sl: spmm_forward(csr, X, slice_cols=sl, depth=d))
+                    assert torch.equal(f(), ref)
+                    fns[f"depth{d} slice{sl}"] = f
             t = timeit(fns)
             esz = 2 if dt == torch.bfloat16 else 4
             B = g.nnz * F * esz + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * F * esz
             for k, v in t.items():
                 out[f"spmm {dt} {name} {k}"] = dict(ms=v, frac=B / v / 1e6 / 8000)
+
+
+def bench_x3kern(out):
+    """lpg_fc_x3_f32's per-call kernel choice (0 = the wide 128 x 128 kernel, 1 = the 16-row strip
+    kernel) at the c2 FC shapes, plain and ReLU + dropout + accumulate."""
+    from lpgnn.fc import fc_forward
+
+    for M, K1, K2 in ((200_000, 1024, 0), (100_000, 1024, 1024), (100_000, 1024, 0)):
+        A1 = torch.randn(M, K1, device="cuda")
+        A2 = torch.randn(M, K2, device="cuda") if K2 else None
+        W1 = torch.randn(1024, K1, device="cuda") * 0.03
+        W2 = torch.randn(1024, K2, device="cuda") * 0.03 if K2 else None
+        b = torch.randn(1024, device="cuda")
+        P = torch.randn(M, 1024, device="cuda")
+        fns = {}
+        for k in (0, 1):
+            fns[f"kernel={k} plain"] = (lambda k=k: fc_forward(A1, W1, A2, W2, None, False, arith="x3", kernel=k))
+            fns[f"kernel={k} relu+drop+acc"] = (lambda k=k: fc_forward(A1, W1, A2, W2, b, True, 0.1, 7, out=P,
+                                                                       accumulate=True, arith="x3", kernel=k))
+        t = timeit(fns, rounds=5, iters=3)
+        for name, v in t.items():
+            out[f"x3kern M={M} K={K1}+{K2} {name}"] = dict(ms=v, tflops=2.0 * M * 1024 * (K1 + K2) / v / 1e9)
+        del A1, A2, P
 
 
 def bench_wgk(out):
@@ -540,7 +565,7 @@ if __name__ == "__main__":
          "bf16bwd": bench_bf16bwd, "spmm16": bench_spmm16,
          "spmmbig": bench_spmmbig, "fck": bench_fck, "x3epi": bench_x3epi, "wgk": bench_wgk, "rbwd": bench_rbwd,
          "load": bench_load, "fcpi": bench_fcpi, "stream": bench_stream, "tail": bench_tail, "fckern": bench_fckern,
-         "epidrop": bench_epidrop, "spmmdepth": bench_spmmdepth}[w](out)
+         "epidrop": bench_epidrop, "spmmdepth": bench_spmmdepth, "x3kern": bench_x3kern}[w](out)
         torch.cuda.empty_cache()
     for k, v in out.items():
         print(f"{k:45s} " + " ".join(f"{a}={b:.4g}" for a, b in v.items() if b is not None))
