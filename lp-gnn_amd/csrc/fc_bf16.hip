@@ -1246,9 +1246,41 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, con
 
 namespace lpg {
 namespace {
+// rows [r, M) of a as their own call: operands, output, mask rows and dropout keys offset by r
+FcB16Args rows_from(const FcB16Args &a, int64_t r) {
+  FcB16Args t = a;
+  t.M = a.M - r;
+  t.A1 = a.A1 ? a.A1 + r * a.lda1 : nullptr;
+  t.A2 = a.A2 ? a.A2 + r * a.lda2 : nullptr;
+  t.C = a.C + r * a.ldc;
+  t.my = a.my ? a.my + r * a.ldy : nullptr;
+  t.row_off = a.row_off + r;
+  return t;
+}
+
 lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
   if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<2, 2, 4, 4>(a, relu, s);  // 128 x 128
-  if ((kernel == 0 || kernel == 3) && p_ok(a)) return launch_bf16_p<2, 4, 8, 4>(a, relu, s);
+  if ((kernel == 0 || kernel == 3) && p_ok(a)) {
+    if (kernel == 0) {
+      // The last round of 256 x 256 tiles (one block per CU) is usually partial: c5's 200 K rows are 24
+      // rounds + 41 % of one, 100 K rows 12 + 21 %, and the CUs without a tile idle for a whole block
+      // time.  Those rows run as a second launch on 128 x 128 tiles (4 x the blocks, 2 per CU) -- the
+      // same per-element arithmetic, so the same bits (kernels are interchangeable, LPG_FC_KERNEL).
+      const int64_t nt = (a.N + 255) / 256;
+      const int64_t per_round = (int64_t)(device_cus() / (nt > 0 ? nt : 1)) * 256;
+      if (per_round >= 256) {
+        const int64_t full = a.M / per_round * per_round, tail = a.M - full;
+        if (full > 0 && tail > 0 && 2 * tail <= per_round) {
+          FcB16Args h = a;
+          h.M = full;
+          const lpg_status st = launch_bf16_p<2, 4, 8, 4>(h, relu, s);
+          if (st != LPG_OK) return st;
+          return launch_bf16<2, 2, 4, 4>(rows_from(a, full), relu, s);
+        }
+      }
+    }
+    return launch_bf16_p<2, 4, 8, 4>(a, relu, s);
+  }
   return launch_bf16<2, 4, 8, 4>(a, relu, s);  // 256 x 256, BK 64, 2 buffers
 }
 }  // namespace

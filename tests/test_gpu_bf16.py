@@ -115,6 +115,34 @@ def test_fc_bf16_kernels_identical():
     _f64_ulp_check(outs[0].cpu(), A1.cpu(), W1.cpu(), None, b.cpu(), True, A2.cpu(), W2.cpu())
 
 
+def test_fc_bf16_tail_split_identical():
+    """The default choice runs the partial last round of 256 x 256 tiles as a second launch on
+    128 x 128 tiles (rows offset, dropout keys offset); with enough rows for a full round plus a small
+    tail that path runs, and it gives the bits of the single pipelined launch (kernel 3): ReLU +
+    dropout, accumulate, and the folded ReLU backward."""
+    from lpgnn.fc import fc_forward_bf16
+
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    N = 2048
+    per_round = (cus // (N // 256)) * 256
+    M = per_round + per_round // 3 + 77  # a full round + a third of one, ragged
+    torch.manual_seed(4)
+    A1 = torch.randn(M, 128, device=DEV).to(BF)
+    W1 = (torch.randn(N, 128, device=DEV) * 0.05).to(BF)
+    b = torch.randn(N, device=DEV)
+    got = fc_forward_bf16(A1, W1, None, None, b, True, 0.2, seed=3, row_offset=11, kernel=0)
+    want = fc_forward_bf16(A1, W1, None, None, b, True, 0.2, seed=3, row_offset=11, kernel=3)
+    assert torch.equal(got, want)
+    P = torch.randn(M, N, device=DEV).to(BF)
+    got = fc_forward_bf16(A1, W1, None, None, b, True, 0.1, seed=5, out=P.clone(), accumulate=True, kernel=0)
+    want = fc_forward_bf16(A1, W1, None, None, b, True, 0.1, seed=5, out=P.clone(), accumulate=True, kernel=3)
+    assert torch.equal(got, want)
+    Y = torch.relu(torch.randn(M, N, device=DEV)).to(BF)
+    got = fc_forward_bf16(A1, W1, None, None, None, False, mask=(Y, 1.25), kernel=0)
+    want = fc_forward_bf16(A1, W1, None, None, None, False, mask=(Y, 1.25), kernel=3)
+    assert torch.equal(got, want)
+
+
 @pytest.mark.parametrize("M,N,relu,drop,bias", [
     (5000, 1024, True, 0.1, True),    # interior tiles
     (4099, 1000, True, 0.3, False),   # ragged rows and columns

@@ -254,7 +254,7 @@ def bench_fckern(out):
         A = torch.randn(M, K, device="cuda").to(BF)
         W = (torch.randn(2048, K, device="cuda") * 0.02).to(BF)
         b = torch.randn(2048, device="cuda")
-        fns = {f"kernel={k}": (lambda k=k: fc_forward_bf16(A, W, None, None, b, True, 0.1, 7, kernel=k)) for k in (1, 2, 3)}
+        fns = {f"kernel={k}": (lambda k=k: fc_forward_bf16(A, W, None, None, b, True, 0.1, 7, kernel=k)) for k in (0, 1, 2, 3)}
         t = timeit(fns, rounds=5, iters=3)
         for k, v in t.items():
             out[f"fckern M={M} K={K} {k}"] = dict(ms=v, tflops=2.0 * M * 2048 * K / v / 1e9)
