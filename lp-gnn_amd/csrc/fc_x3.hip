@@ -749,33 +749,35 @@ lpg_status launch_x3_wide(X3Args a, bool relu, hipStream_t s) {
 // from a zeroed 512-B row at the end of the workspace.
 constexpr int WG_T = 128;  // output tile (n and k)
 
-// 16-B raw buffer load (v# in SGPRs: base and size wave-uniform): offsets at or past `nbytes`
-// return zeros, with no branch and no compare in the kernel
-__device__ __forceinline__ f32x4 buf_load4(const float *base, uint32_t nbytes, int voff, int soff) {
+// 4-B raw buffer load (v# in SGPRs: base and size wave-uniform): offsets at or past `nbytes` return
+// zeros, with no branch and no compare in the kernel
+__device__ __forceinline__ float buf_load1(const float *base, uint32_t nbytes, int voff, int soff) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), (short)0, (int)nbytes, 0x00020000);
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
 #else
-  return f32x4{};
+  return 0.f;
 #endif
 }
 
-// The weight-gradient kernel: each thread loads 8 consecutive rows x 4 columns of G or X (float4
-// per row through a buffer descriptor over the block's R range: rows past R read zeros, no
-// branch), splits each column's 8 values into three bf16x8 (k = the 8 rows) and writes them with
-// ds_write_b128 into plane images laid out for the MFMA ([column][32 rows] bf16, 64-B rows, chunk
-// c at c ^ ((col >> 2) & 3): the fc kernel's W-plane image, read conflict-free by 16 consecutive
-// columns); 8 waves (4 x 2, 64 x 64 each, 16x16x32) read b128 fragments.  A 256 (n) x 128 (k)
-// output tile per 512-thread block, one block per CU, and TWO plane buffers (2 x 72 KiB).  A
-// split-then-multiply form (round 1's cooperative kernel) keeps both waves of a SIMD in the same
-// phase, so the split VALU and the MFMAs never overlap.  Here chunk c + 1 is split into the other buffer in the same iteration as chunk c's
-// MFMAs (the loop is unrolled by two so the buffers are compile-time distinct and the scheduler
-// may interleave them), its global loads issued one iteration earlier; one barrier per chunk.
-// Each G element is split once per 128 k-columns and each X element once per 256 n-columns
-// (128 x 128 tiles: once per 128 each): 1.37 split VALU per MFMA instead of 1.83.  Loader tasks: waves
-// 0-3 take G (64 column groups x 4 row groups), waves 4-5 X (32 x 4), waves 6-7 only multiply.
-template <bool SCHED>
+// The weight-gradient kernel: each thread loads three columns' 8 consecutive rows of G or X (one
+// dword per row through a buffer descriptor over the block's R range: rows past R read zeros, no
+// branch; a wave's 64 lanes read 256 contiguous bytes of a row), splits each column's 8 values into
+// three bf16x8 (k = the 8 rows) and writes them with ds_write_b128 into plane images laid out for
+// the MFMA ([column][32 rows] bf16, 64-B rows, chunk c at c ^ ((col >> 2) & 3): the fc kernel's
+// W-plane image, read conflict-free by 16 consecutive columns); 8 waves (4 x 2, 64 x 64 each,
+// 16x16x32) read b128 fragments.  A 256 (n) x 128 (k) output tile per 512-thread block, one block
+// per CU, and TWO plane buffers (2 x 72 KiB).  A split-then-multiply form (round 1's cooperative
+// kernel) keeps both waves of a SIMD in the same phase, so the split VALU and the MFMAs never
+// overlap.  Here chunk c + 1 is split into the other buffer in the same iteration as chunk c's
+// MFMAs, one unit after each fragment row (the loop is unrolled by two so the buffers are
+// compile-time distinct), and each unit's chunk c + 2 loads go out right behind its split; one
+// barrier per chunk.  Each G element is split once per 128 k-columns and each X element once per
+// 256 n-columns: 1.375 split VALU per MFMA, the same for every wave.  (Round 2's loader gave waves
+// 0-3 G and waves 4-7 X with 6-7 repeating 4-5's work, 1.83 per MFMA on every SIMD, and issued a
+// chunk's loads one fragment row before their use: 189 / 211 TF/s at R = 100 / 200 K against 197 /
+// 218 for the balanced tasks, profiles/r03_wgrad_bal.log.)
 __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
                                                     int64_t ldg, const float *__restrict__ X, int64_t ldx,
                                                     float *__restrict__ part, int64_t nt, int64_t kt,
@@ -796,42 +798,43 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // loader task: operand, 4 columns cg*4 .. +3, rows rg*8 .. +7 of a chunk; waves 6-7 repeat waves
-  // 4-5's X tasks (identical bytes to the same LDS addresses): every wave runs the same branch-free
-  // body, so the scheduler can interleave the split with the MFMAs, and the SIMDs hosting waves 6-7
-  // carry no more split work than the others
-  const bool isg = wave < 4;
-  const int lt = isg ? tid : (tid - 256) & 127;
-  const int cg = lt & (isg ? 63 : 31), rg = isg ? (lt >> 6) & 3 : (lt >> 5) & 3;
-  const int64_t colb = isg ? n0 : k0, lim = isg ? N : K, ld = isg ? ldg : ldx;
-  int64_t col0 = colb + cg * 4;
-  col0 = col0 < lim ? col0 : lim - 4;  // N, K multiples of 4: columns past the edge are never stored
-  // descriptor from row c0 * 32, column colb (rows past R out of range: zeros, no branch)
-  const float *sbase = (isg ? G : X) + c0 * 32 * ld + colb;
-  const int64_t left = (R - c0 * 32) * ld * 4;
-  const uint32_t nbytes = (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff);
-  const int voff = (int)((col0 - colb) * 4 + rg * 8 * ld * 4);
-  const int pl = isg ? GP : XP;  // (wave-uniform)
-  const int opoff = isg ? 0 : 3 * GP;
-  f32x4 raw[8];
-  auto load = [&](int64_t c) {  // c clamped to the last chunk: a spare re-load at the end, no branch
+  // loader tasks, the same for every thread (so every SIMD carries the same split VALU, whichever
+  // waves it hosts): three split units of 8 rows (rg * 8 .. + 7, rg = tid >> 7) per chunk -- unit 0
+  // G column gc, unit 1 G column 128 + gc, unit 2 X column gc (gc = tid & 127): 24 elements per
+  // lane, every G and X element split once per block and chunk (G once per 128 k-columns, X once
+  // per 256 n-columns).  Each unit has its own 8 registers: its next chunk's loads are issued as
+  // soon as it has been split, a whole multiply ahead of their use.
+  const int gc = tid & 127, rg = tid >> 7;
+  // columns past the edge are clamped (their outputs are never stored)
+  const int64_t col_u[3] = {n0 + gc < N ? n0 + gc : N - 1, n0 + 128 + gc < N ? n0 + 128 + gc : N - 1,
+                            k0 + gc < K ? k0 + gc : K - 1};
+  // descriptors from row c0 * 32 (rows past R out of range: zeros, no branch)
+  const float *gbase = G + c0 * 32 * ldg + n0, *xbase = X + c0 * 32 * ldx + k0;
+  const int64_t gleft = (R - c0 * 32) * ldg * 4, xleft = (R - c0 * 32) * ldx * 4;
+  const uint32_t gbytes = (uint32_t)(gleft < 0x7fffffff ? gleft : 0x7fffffff);
+  const uint32_t xbytes = (uint32_t)(xleft < 0x7fffffff ? xleft : 0x7fffffff);
+  float raw[3][8];
+  auto load_unit = [&](int u, int64_t c) {  // c clamped to the last chunk: a spare re-load at the end, no branch
     c = c < c1 ? c : c1 - 1;
+    const bool isg = u < 2;
+    const int64_t ld = isg ? ldg : ldx;
+    const int voff = (int)((col_u[u] - (isg ? n0 : k0)) * 4 + rg * 8 * ld * 4);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) raw[e] = buf_load4(sbase, nbytes, voff, (int)(((c - c0) * 32 + e) * ld * 4));
+    for (int e = 0; e < 8; ++e)
+      raw[u][e] = buf_load1(isg ? gbase : xbase, isg ? gbytes : xbytes, voff, (int)(((c - c0) * 32 + e) * ld * 4));
   };
-  auto split_col = [&](unsigned char *buf, int q) {  // column cg*4 + q: its 8 rows -> three bf16x8
-    unsigned char *img = buf + opoff;
-    const Split3 t = split3(f32x4{raw[0][q], raw[1][q], raw[2][q], raw[3][q]},
-                            f32x4{raw[4][q], raw[5][q], raw[6][q], raw[7][q]});
-    const int col = cg * 4 + q;
-    unsigned char *dst = img + col * 64 + swzW(col, rg) * 16;
+  auto load = [&](int64_t c) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) load_unit(u, c);
+  };
+  auto split_col = [&](unsigned char *buf, int u) {  // unit u's 8 rows -> three bf16x8
+    const Split3 t = split3(f32x4{raw[u][0], raw[u][1], raw[u][2], raw[u][3]},
+                            f32x4{raw[u][4], raw[u][5], raw[u][6], raw[u][7]});
+    const int col = u == 1 ? 128 + gc : gc, pl = u < 2 ? GP : XP;
+    unsigned char *dst = buf + (u < 2 ? 0 : 3 * GP) + col * 64 + swzW(col, rg) * 16;
     *reinterpret_cast<bf16x8 *>(dst) = t.h;
     *reinterpret_cast<bf16x8 *>(dst + pl) = t.m;
     *reinterpret_cast<bf16x8 *>(dst + 2 * pl) = t.l;
-  };
-  auto split_store = [&](unsigned char *buf) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) split_col(buf, q);
   };
 
   const int wm = wave >> 1, wn = wave & 1;  // 4 (n) x 2 (k) waves of 64 x 64
@@ -846,15 +849,25 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
 #pragma unroll
     for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8 *>(im + p * plane + col * 64 + swzW(col, fg) * 16);
   };
-  // multiply the chunk in buf; with `next`, split column i of the next chunk (raw) into it after
-  // fragment row i's 24 MFMAs (SCHED: in source order, so the VALU lands between MFMA groups)
-  auto multiply = [&](const unsigned char *buf, unsigned char *next) {
+  // multiply the chunk in buf; with `next`, split unit i - 1 of the next chunk (raw) into it after
+  // fragment row i - 1's 24 MFMAs and issue that unit's loads of chunk `cload` (in source order, so
+  // the VALU lands between MFMA groups)
+  // (`split` a std::integral_constant: a runtime `next != nullptr` test -- hipcc cannot prove an LDS
+  // pointer non-null -- put a branch around every split, and at each join the waitcnt pass assumed
+  // the path without the other units' loads and waited for all of them)
+  auto multiply = [&](const unsigned char *buf, unsigned char *next, int64_t cload, auto split) {
     bf16x8 bv[4][3];
 #pragma unroll
     for (int j = 0; j < 4; ++j) frag(buf + 3 * GP, XP, wn * 64 + j * 16 + fr, bv[j]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (SCHED && next && i > 0) split_col(next, i - 1);
+      if (decltype(split)::value && i > 0) {
+        split_col(next, i - 1);
+        // the unit's registers are free only once its split has read them: a load hoisted above
+        // the split made hipcc copy the in-flight values out first, and wait for every load to do so
+        __builtin_amdgcn_sched_barrier(0);
+        load_unit(i - 1, cload);
+      }
       bf16x8 av[3];
       frag(buf, GP, wm * 64 + i * 16 + fr, av);
 #pragma unroll
@@ -867,12 +880,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
         accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][0], accH[i][j], 0, 0, 0);
       }
     }
-    if (next) {
-      if constexpr (SCHED)
-        split_col(next, 3);
-      else
-        split_store(next);
-    }
   };
   auto sync = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -883,22 +890,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
   unsigned char *const B0 = smem, *const B1 = smem + BUFB;
   // prologue: chunk c0 split into B0, chunk c0 + 1's loads in flight
   load(c0);
-  split_store(B0);
+#pragma unroll
+  for (int u = 0; u < 3; ++u) split_col(B0, u);
   load(c0 + 1);
   sync();
   // half-iteration (chunk c in one buffer, chunk c+1's loads landed or landing): multiply it, split
-  // c+1 into the other buffer, issue c+2's loads, barrier.  Past the end the split writes B0 with a
-  // spare chunk nobody reads.
+  // c+1 into the other buffer unit by unit, each unit's c+2 loads issued behind its split, barrier.
+  // Past the end the split writes B0 with a spare chunk nobody reads.
   int64_t c = c0;
   for (; c + 1 < c1; c += 2) {
-    multiply(B0, B1);
-    load(c + 2);
+    multiply(B0, B1, c + 2, std::true_type{});
     sync();
-    multiply(B1, B0);
-    load(c + 3);
+    multiply(B1, B0, c + 3, std::true_type{});
     sync();
   }
-  if (c < c1) multiply(B0, nullptr);  // odd count: the last chunk sits in B0
+  if (c < c1) multiply(B0, nullptr, 0, std::false_type{});  // odd count: the last chunk sits in B0
 
   float *P = part + s * N * K;
 #pragma unroll
@@ -1091,7 +1097,7 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   const int64_t ntw = (N + 255) / 256, ktw = (K + 127) / 128;  // 256 x 128 tiles
   const int64_t nbw = S_used * ntw * ktw;
   LPG_REQUIRE(nbw < (int64_t)1 << 31, "lpg_wgrad_x3_f32: grid too large");
-  hipLaunchKernelGGL(wgrad_x3w<true>, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw, ktw,
+  hipLaunchKernelGGL(wgrad_x3w, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw, ktw,
                      cps);
   LPG_HIP(hipGetLastError());
   const int64_t n4 = N * (K / 4);
