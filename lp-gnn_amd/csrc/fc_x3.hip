@@ -42,6 +42,7 @@
 // n-tiles, so the A panel is re-read from that XCD's L2).
 #include "common.h"
 #include "fc_common.h"
+#include "x3_split.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -50,13 +51,6 @@
 
 namespace lpg {
 namespace {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;
 
@@ -81,44 +75,6 @@ struct X3Args {
   float *hpart;
   int64_t row_off;  // the dropout key of row m is row_off + m (the global node id of a row slice)
 };
-
-__device__ __forceinline__ unsigned pk_bf16(float x, float y) {  // v_cvt_pk_bf16_f32: RNE, x in the low half
-  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x, y}, bf16x2));
-}
-
-// exact residual x - h as one v_sub_f32: kept out of the SLP vectorizer's reach, which paired
-// the two subtractions of a level into v_pk_add_f32 -- an issue-cost anti-lever beside MFMAs
-// (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
-__device__ __forceinline__ float sub_f32(float x, float h) {
-  float r;
-  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(h));
-  return r;
-}
-
-// one split level of a pair: the packed RNE bf16 terms; the exact residuals are left in x, y
-__device__ __forceinline__ unsigned split_lvl(float &x, float &y) {
-  const unsigned p = pk_bf16(x, y);
-  x = sub_f32(x, __uint_as_float(p << 16));
-  y = sub_f32(y, __uint_as_float(p & 0xffff0000u));
-  return p;
-}
-
-struct Split3 {
-  bf16x8 h, m, l;
-};
-
-// 8 consecutive k (lo = k 0..3, hi = k 4..7) -> the three bf16x8 MFMA operands
-__device__ __forceinline__ Split3 split3(f32x4 lo, f32x4 hi) {
-  u32x4 H, Mi, L;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float x = i < 2 ? lo[2 * i] : hi[2 * i - 4], y = i < 2 ? lo[2 * i + 1] : hi[2 * i - 3];
-    H[i] = split_lvl(x, y);
-    Mi[i] = split_lvl(x, y);
-    L[i] = pk_bf16(x, y);
-  }
-  return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, Mi), __builtin_bit_cast(bf16x8, L)};
-}
 
 // dst plane p [rows, cols] (ldd) = term p of src (transposed: src is [cols, rows]).
 // One thread per output pair (2 consecutive columns).
@@ -749,18 +705,6 @@ lpg_status launch_x3_wide(X3Args a, bool relu, hipStream_t s) {
 // from a zeroed 512-B row at the end of the workspace.
 constexpr int WG_T = 128;  // output tile (n and k)
 
-// 4-B raw buffer load (v# in SGPRs: base and size wave-uniform): offsets at or past `nbytes` return
-// zeros, with no branch and no compare in the kernel
-__device__ __forceinline__ float buf_load1(const float *base, uint32_t nbytes, int voff, int soff) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), (short)0, (int)nbytes, 0x00020000);
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
-#else
-  return 0.f;
-#endif
-}
-
 // The weight-gradient kernel: each thread loads three columns' 8 consecutive rows of G or X (one
 // dword per row through a buffer descriptor over the block's R range: rows past R read zeros, no
 // branch; a wave's 64 lanes read 256 contiguous bytes of a row), splits each column's 8 values into
@@ -1083,12 +1027,12 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   LPG_REQUIRE(N % 4 == 0 && K % 4 == 0 && ldg >= N && ldx >= K && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) &&
                   aligned16(X) && aligned16(workspace),
               "lpg_wgrad_x3_f32: N, K and leading dimensions must be multiples of 4 floats, buffers 16-byte aligned");
+  float *part = reinterpret_cast<float *>(workspace);
+  hipStream_t st = as_stream(stream);
   const int64_t S = wgrad_splits(R, N, K);
   const int64_t nchunks = (R + 31) / 32;
   const int64_t cps = (nchunks + S - 1) / S;
   const int64_t S_used = (nchunks + cps - 1) / cps;
-  float *part = reinterpret_cast<float *>(workspace);
-  hipStream_t st = as_stream(stream);
   // one R range's byte offsets must fit the buffer descriptors' 31 bits (a range of R / S rows: at
   // S <= 64 that is R * ld beyond 3e10 elements, 137 GB per operand)
   LPG_REQUIRE((cps * 32 + 40) * (ldg > ldx ? ldg : ldx) * 4 < ((int64_t)1 << 31),
