@@ -423,6 +423,19 @@ lpg_status lpg_weighted_ce_bwd_f32(int64_t M, int64_t C, const float *x, int64_t
                                    const float *w, const float *wsum, const float *gout, float coef,
                                    float *dx, int64_t lddx, void *stream);
 
+/* ---- basis labels (inference_gnn, val.py:106-124) -------------------------- */
+
+/* labels[i] for i < total from logits [total, 3] (stride ldl): P = softmax(logits) with NaN -> 0;
+ * the m nodes with the largest P[:, 1] get 1 (of the nodes equal to the m-th largest value, the
+ * lowest indices; torch.topk leaves that choice open), every other node argmax(P[i,0], P[i,2])
+ * (0 on a tie).  Replaces the softmax / topk / argmax chain of val.py:106-118 (the reference's
+ * timed post-processing, scripts/pred_basis.py:117).  0 <= m <= total.  Exact radix select on the
+ * float bits, no host sync, deterministic.  Workspace: lpg_basis_labels_workspace_bytes(total),
+ * 16-byte aligned. */
+int64_t lpg_basis_labels_workspace_bytes(int64_t total);
+lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float *logits, int64_t ldl, int64_t *labels,
+                                void *workspace, void *stream);
+
 /* add_knowledge for one side (arch.py:129-141): out = normalize(logit) * 10,
  * then out[:,0] -= bound where feas[:, cols-3] != 0 (infinite lower bound)
  * and out[:,2] -= bound where feas[:, cols-1] != 0 (infinite upper bound).

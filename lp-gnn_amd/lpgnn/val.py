@@ -17,18 +17,52 @@ from .arch import arch_depth
 @torch.no_grad()
 def inference_gnn(logits, m, check: bool = True, **kwargs):
     """val.py:106-124.  ``check=False`` skips the two invariant asserts
-    (val.py:119-122), the only host syncs, for per-step use on the device."""
+    (val.py:119-122), the only host sync, for per-step use on the device.
+    On a HIP device the whole chain (softmax, NaN -> 0, top-m of P[:, 1],
+    argmax over {0, 2}) is one lpg_basis_labels_f32 call (exact radix select;
+    of the nodes tied at the m-th largest P[:, 1] the lowest indices are
+    basic, a choice torch.topk leaves open); on the host, the reference's
+    torch ops."""
     n = logits.shape[0] - m
-    pr = F.softmax(logits.float(), dim=-1)
-    pr = pr.clone()
-    pr[torch.isnan(pr)] = 0
-    _, topk_idx = pr[:, 1].topk(m)
-    pr[:, 1] = pr.min() - 1
-    pr[topk_idx, 1] = pr.max() + 1
-    pred = pr.argmax(-1)
+    if logits.is_cuda and logits.dim() == 2 and logits.shape[1] == 3:
+        pred = _basis_labels_device(logits.float(), m)
+    else:
+        pr = F.softmax(logits.float(), dim=-1)
+        pr = pr.clone()
+        pr[torch.isnan(pr)] = 0
+        _, topk_idx = pr[:, 1].topk(m)
+        pr[:, 1] = pr.min() - 1
+        pr[topk_idx, 1] = pr.max() + 1
+        pred = pr.argmax(-1)
     if check:
-        assert (pred == 1).sum().item() == m
-        assert (pred[m:m + n] == 1).sum().item() == ((pred[:m] == 0) | (pred[:m] == 2)).sum().item()
+        basic = pred == 1
+        outer = (pred[:m] == 0) | (pred[:m] == 2)
+        got = torch.stack((basic.sum(), basic[m:m + n].sum(), outer.sum())).tolist()  # one host sync
+        assert got[0] == m
+        assert got[1] == got[2]
+    return pred
+
+
+def _basis_labels_device(logits, m):
+    from . import _lib
+
+    total = logits.shape[0]
+    if logits.stride(1) != 1:
+        logits = logits.contiguous()
+    if not 0 <= m <= total:
+        raise RuntimeError(f"inference_gnn: m = {m} outside [0, {total}] (topk)")
+    L = _lib.lib()
+    pred = torch.empty(total, dtype=torch.int64, device=logits.device)
+    ws = torch.empty((max(16, L.lpg_basis_labels_workspace_bytes(total)) + 15) // 16 * 4, dtype=torch.float32,
+                     device=logits.device)
+    from .timing import TIMER
+
+    with torch.cuda.device(logits.device):
+        tok = TIMER.start(("basis_labels", total, 3, m, "f32"))
+        st = L.lpg_basis_labels_f32(total, m, logits.data_ptr(), logits.stride(0), pred.data_ptr(), ws.data_ptr(),
+                                    _lib.stream_of(logits))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_basis_labels_f32")
     return pred
 
 
