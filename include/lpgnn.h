@@ -149,6 +149,9 @@ lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  *     3 = the pipelined 256 x 256 kernel (the default from 4096 rows). */
 #define LPG_FC_RELU 1
 #define LPG_FC_ACCUMULATE 2
+#define LPG_FC_HEADS_ONLY 4 /* lpg_fc_x3_heads_f32 only: C is not written (the logits are the only output;
+                             * with LPG_FC_ACCUMULATE C still supplies the addend, else C may be NULL):
+                             * the no-grad forward of the last layer, whose output feeds only the heads */
 #define LPG_FC_KERNEL(k) ((int32_t)(k) << 8)
 
 /* C[m, n] = act( sum_{k<K1} A1[m,k] W1[n,k] + sum_{k<K2} A2[m,k] W2[n,k] + bias[n] )

@@ -74,6 +74,7 @@ struct X3Args {
   int32_t hn;
   float *hpart;
   int64_t row_off;  // the dropout key of row m is row_off + m (the global node id of a row slice)
+  int32_t store;    // 0: C is not written (LPG_FC_HEADS_ONLY: the logits are the only output)
 };
 
 // dst plane p [rows, cols] (ldd) = term p of src (transposed: src is [cols, rows]).
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
         if (a.bias) v = v + bb;
         if (RELU) v = (v < 0.f) ? 0.f : v;
         if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-        a.C[row * a.ldc + col] = v;
+        if (a.store) a.C[row * a.ldc + col] = v;
         if constexpr (HEADS) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) hs[c][i][r] = hs[c][i][r] + v * hwv[c];
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
             if constexpr (BIAS) v = v + bb;
             if (RELU) v = (v < 0.f) ? 0.f : v;
             if constexpr (DROP) v = drop_hash_k(rk[i][r], ck) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-            rp(i, r)[j * 16] = v;
+            if (!HEADS || a.store) rp(i, r)[j * 16] = v;
             hput(i, r, j, v);
           }
       }
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
           if (a.bias) v = v + bb;
           if (RELU) v = (v < 0.f) ? 0.f : v;
           if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-          a.C[row * a.ldc + col] = v;
+          if (!HEADS || a.store) a.C[row * a.ldc + col] = v;
           hput(i, r, j, v);
         }
     }
@@ -932,7 +933,8 @@ static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int
                           int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
                           float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
                           int64_t row_offset, X3Args *out) {
-  LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_x3_f32: bad C/ldc");
+  const bool heads_only = flags & LPG_FC_HEADS_ONLY;
+  LPG_REQUIRE((C != nullptr || (heads_only && !(flags & LPG_FC_ACCUMULATE))) && ldc >= N, "lpg_fc_x3_f32: bad C/ldc");
   LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "lpg_fc_x3_f32: K1, K2 must be multiples of %d (zero-pad)", BK);
   LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1 && ps1 >= N * ldw1), "lpg_fc_x3_f32: bad A1/W1");
   LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2 && ps2 >= N * ldw2), "lpg_fc_x3_f32: bad A2/W2");
@@ -941,12 +943,13 @@ static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int
                   (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
               "lpg_fc_x3_f32: A rows must be 16-byte aligned (lda multiple of 4), W planes 16-byte aligned "
               "(ldw and plane stride multiples of 8)");
-  LPG_REQUIRE((flags & ~0xf03) == 0 && ((flags >> 8) & 15) <= kX3Kernels, "lpg_fc_x3_f32: unknown flags 0x%x", flags);
+  LPG_REQUIRE((flags & ~0xf07) == 0 && ((flags >> 8) & 15) <= kX3Kernels, "lpg_fc_x3_f32: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_x3_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
   *out = X3Args{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, ps1, ps2, C, ldc, 0, 0, seed, 0u, 1.f,
                 (flags >> 1) & 1};
   dropout_params(dropout_p, &out->drop_thresh, &out->drop_scale);
   out->row_off = row_offset;
+  out->store = heads_only ? 0 : 1;
   return LPG_OK;
 }
 
@@ -957,6 +960,7 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
                                     int64_t row_offset, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_f32: negative size");
   if (M == 0 || N == 0) return LPG_OK;
+  LPG_REQUIRE(!(flags & LPG_FC_HEADS_ONLY), "lpg_fc_x3_f32: LPG_FC_HEADS_ONLY needs the heads entry");
   X3Args a;
   const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
                                 dropout_p, seed, row_offset, &a);

@@ -86,7 +86,7 @@ def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
 
 
 def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                  heads=None):
+                  heads=None, heads_only=False):
     """The layer's forward (both directions); records on ctx what the backward
     needs and returns (left_new, right_new, tensors to save, logits).  With
     heads = ((Wh_l, bh_l), (Wh_r, bh_r)) the heads run in the FC epilogues
@@ -105,6 +105,10 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out)
 
     hd = heads if heads is not None and not bf16 else (None, None)
+    # no-grad (eval) forward of the heads layer: its output feeds only the heads, so the fused kernels
+    # skip storing it (LPG_FC_HEADS_ONLY); the returned layer outputs then hold no values.  (Decided by
+    # the caller: inside an autograd.Function's forward grad mode is always off.)
+    ho = heads is not None and heads_only
 
     def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None, head=None):
         """(output, aggregate kept for the backward, logits of `head` or None)."""
@@ -113,12 +117,12 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
             y = spmm_forward(S, fc(x_src, w_rel, None, None, None, False))
             if head is not None:
                 y, lg = _fc.fc_forward(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True,
-                                       heads=head)
+                                       heads=head, heads_only=ho)
                 return y, None, lg
             return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None, None
         agg = spmm_forward(S, x_src) if agg is None else agg
         if head is not None:
-            y, lg = _fc.fc_forward(agg, w_rel, x_dst, w_root, b, relu, dropout, seed, heads=head)
+            y, lg = _fc.fc_forward(agg, w_rel, x_dst, w_root, b, relu, dropout, seed, heads=head, heads_only=ho)
             return y, agg, lg
         return _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, dropout, seed, bf16), agg, None
 
@@ -292,11 +296,11 @@ class _TwoDirectionHeads(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                wh_l, bh_l, wh_r, bh_r):
+                wh_l, bh_l, wh_r, bh_r, heads_only=False):
         # the heads fused into the layer's FC epilogues (x3 arithmetic), else their own Linear kernels
         left_new, right_new, saved, logits = _forward_core(
             ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-            heads=((wh_l, bh_l), (wh_r, bh_r)) if FUSE_HEAD_FWD else None)
+            heads=((wh_l, bh_l), (wh_r, bh_r)) if FUSE_HEAD_FWD else None, heads_only=heads_only)
         if logits is None:
             logits = (_fc.fc_forward(left_new, wh_l, None, None, bh_l, False),
                       _fc.fc_forward(right_new, wh_r, None, None, bh_r, False))
@@ -317,17 +321,22 @@ class _TwoDirectionHeads(torch.autograd.Function):
         core = _backward_core(ctx, saved, need, None, None, dz=(dz_l, db_r2l, dz_r, db_l2r))
         keep = lambda t, i, has=True: t if (need[i] and has) else None
         return (*core, keep(dwh_l, 11), keep(dbh_l, 12, ctx.heads_b[0]), keep(dwh_r, 13),
-                keep(dbh_r, 14, ctx.heads_b[1]))
+                keep(dbh_r, 14, ctx.heads_b[1]), None)
 
 
 def two_direction_heads(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, lin_left, lin_right,
                         dropout: float = 0.0):
     """GraphConvTwoDirection (ReLU, dropout) followed by the heads lin_left /
     lin_right (arch.py:184-190) through one autograd node: (logit_l, logit_r)."""
+    ts = (left, right, left2right.lin_rel.weight, left2right.lin_rel.bias, left2right.lin_root.weight,
+          right2left.lin_rel.weight, right2left.lin_rel.bias, right2left.lin_root.weight, lin_left.weight,
+          lin_left.bias, lin_right.weight, lin_right.bias)
+    # nothing will differentiate through this call: the layer output (which feeds only the heads) is not needed
+    heads_only = not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts))
     return _TwoDirectionHeads.apply(left, right, adj, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                     left2right.lin_root.weight, right2left.lin_rel.weight, right2left.lin_rel.bias,
                                     right2left.lin_root.weight, True, float(dropout), lin_left.weight,
-                                    lin_left.bias, lin_right.weight, lin_right.bias)
+                                    lin_left.bias, lin_right.weight, lin_right.bias, heads_only)
 
 
 def foldable_producer(x: Tensor):

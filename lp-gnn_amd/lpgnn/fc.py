@@ -58,7 +58,7 @@ _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless th
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
                accumulate: bool = False, arith: str | None = None, heads=None, kernel: int = 0,
-               row_offset: int = 0):
+               row_offset: int = 0, heads_only: bool = False):
     """act(A1 W1^T + A2 W2^T [+ out] + bias) through lpg_fc_f32; with
     ``accumulate`` the caller's ``out`` holds the addend and is overwritten.
     ``arith`` ("fp32" | "x3", default ``ARITH``) picks the tiled kernel's arithmetic.
@@ -67,14 +67,16 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
     separate Linear on C (the fp32 contract's own kernel).  ``kernel``: the x3 entries' per-call
     kernel choice (LPG_FC_KERNEL, include/lpgnn.h; 0 = by shape; every choice gives the same bits).
     ``row_offset``: the dropout mask keys row m as row_offset + m (the global node id of the first
-    row when this call computes a slice of a node set: the row partition)."""
+    row when this call computes a slice of a node set: the row partition).
+    ``heads_only`` (with ``heads``): C is not needed -- the fused x3 kernel then does not write it
+    (LPG_FC_HEADS_ONLY) and the returned C holds no values (the no-grad forward of the last layer)."""
     if heads is not None:
         M, N = A1.shape[0], W1.shape[0]
         k4 = lambda k: -(-k // 4) * 4
         small = 4 <= k4(A1.shape[1]) and k4(A1.shape[1]) + (0 if A2 is None else k4(A2.shape[1])) <= 16
         if (arith or ARITH) == "x3" and not small and N > 32 and heads[0].shape[0] <= 4:
             return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, heads, kernel,
-                               row_offset)
+                               row_offset, heads_only)
         C = _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel,
                         row_offset=row_offset)
         return C, _fc_forward(C, heads[0], None, None, heads[1], False, arith=arith)
@@ -83,7 +85,7 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
 
 
 def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, accumulate=False, arith=None,
-                heads=None, kernel=0, row_offset=0):
+                heads=None, kernel=0, row_offset=0, heads_only=False):
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -110,6 +112,8 @@ def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, acc
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0)
     if (arith or ARITH) == "x3" and not small and N > 32:
+        if heads is not None and heads_only:
+            flags |= 4  # LPG_FC_HEADS_ONLY
         return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags | _lib.fc_kernel(kernel), dropout_p, seed, relu,
                       heads=heads, row_offset=row_offset)
     with torch.cuda.device(A1.device):

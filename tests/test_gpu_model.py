@@ -234,3 +234,26 @@ def test_fused_heads_node_equals_separate_heads(monkeypatch):
     assert abs(out[True][0] - out[False][0]) < 1e-6
     for k, v in out[True][1].items():
         torch.testing.assert_close(v, out[False][1][k], rtol=1e-4, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("m,n", [(900, 1700), (5000, 2300)])
+def test_no_grad_heads_only_forward_equals_grad_forward(m, n):
+    """Eval forward under no_grad: the last layer's fused x3 kernels skip storing the layer output
+    (LPG_FC_HEADS_ONLY, it feeds only the heads) -- the logits are bitwise those of the same forward
+    with autograd on (which stores it), in both directions (the re-associated one accumulates onto
+    the SpMM output)."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+
+    g = synth.uniform_lp(m, n, 12 * m, seed=11)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                           y_s=torch.from_numpy(g.y_s).to(DEV), y_t=torch.from_numpy(g.y_t).to(DEV),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=256, depth=3).to(DEV).eval()
+    with torch.no_grad():
+        lc0, lv0 = model(batch)
+    with torch.enable_grad():
+        lc1, lv1 = model(batch)
+    assert lc1.requires_grad
+    assert torch.equal(lc0, lc1.detach()) and torch.equal(lv0, lv1.detach())
