@@ -10,8 +10,9 @@
 // same counts whatever the order).  Every block of a pass re-derives the previous passes' bin
 // choice from the merged histogram (a 4096-bin suffix scan, a few microseconds), block 0 records it
 // for the later kernels.  Nodes above the threshold value are basic; of the nodes equal to it, the
-// lowest indices are taken (torch.topk leaves that choice unspecified).  Five launches, no host
-// synchronisation, deterministic.
+// lowest indices are taken (torch.topk leaves that choice unspecified: per-block tie counts, a
+// one-block scan, a ballot prefix inside the block).  Six launches, no host synchronisation,
+// deterministic.
 #include "common.h"
 
 namespace lpg {
@@ -171,6 +172,30 @@ __global__ __launch_bounds__(kBT) void basis_ties(int64_t total, Ws w) {
   if (threadIdx.x == 0) w.ties[blockIdx.x] = cnt;
 }
 
+// ties[b] -> the number of threshold ties in the blocks before b (exclusive prefix, in place): one
+// block, each thread a contiguous run of blocks
+__global__ __launch_bounds__(1024) void basis_tie_scan(int64_t nb, Ws w) {
+  __shared__ int64_t sc[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (nb + 1023) / 1024, b0 = t * per, b1 = b0 + per < nb ? b0 + per : nb;
+  int64_t local = 0;
+  for (int64_t b = b0; b < b1; ++b) local += w.ties[b];
+  sc[t] = local;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int64_t v = t >= o ? sc[t - o] : 0;
+    __syncthreads();
+    sc[t] += v;
+    __syncthreads();
+  }
+  int64_t run = sc[t] - local;
+  for (int64_t b = b0; b < b1; ++b) {
+    const uint32_t c = w.ties[b];
+    w.ties[b] = (uint32_t)run;  // < 2^31 nodes per call (host check)
+    run += c;
+  }
+}
+
 // labels: 1 above the threshold and for the first need_eq keys equal to it (by node index), else the
 // argmax over {0, 2}.  With `select` false (m = 0) no node is basic.
 __global__ __launch_bounds__(kBT) void basis_labels(int64_t total, int32_t select, Ws w, int64_t *__restrict__ out) {
@@ -179,22 +204,12 @@ __global__ __launch_bounds__(kBT) void basis_labels(int64_t total, int32_t selec
   const int64_t need_eq = select ? w.st->need_eq : 0;
   const uint32_t k = i < total ? w.keys[i] : 0u;
   const bool eq = select && i < total && k == thr;
-  // ties of the blocks before this one
-  __shared__ int64_t part[kBT];
   __shared__ uint32_t wcnt[kBT / 64];
-  int64_t before = 0;
-  if (select)
-    for (int64_t b = threadIdx.x; b < (int64_t)blockIdx.x; b += kBT) before += w.ties[b];
-  part[threadIdx.x] = before;
   const uint64_t bal = __ballot(eq);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) wcnt[wv] = (uint32_t)__popcll(bal);
   __syncthreads();
-  for (int o = kBT / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
-    __syncthreads();
-  }
-  int64_t rank = part[0] + (int64_t)__popcll(bal & ((1ull << lane) - 1ull));
+  int64_t rank = (select ? (int64_t)w.ties[blockIdx.x] : 0) + (int64_t)__popcll(bal & ((1ull << lane) - 1ull));
   for (int v = 0; v < wv; ++v) rank += wcnt[v];
   if (i < total) out[i] = (select && (k > thr || (eq && rank < need_eq))) ? 1 : (int64_t)w.side[i];
 }
@@ -213,7 +228,7 @@ extern "C" lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float
   if (total == 0) return LPG_OK;
   LPG_REQUIRE(logits && labels && workspace && ldl >= 3, "lpg_basis_labels_f32: NULL pointer or ldl < 3");
   LPG_REQUIRE(aligned16(workspace), "lpg_basis_labels_f32: workspace not 16-byte aligned");
-  LPG_REQUIRE(total < ((int64_t)1 << 31) * kBT, "lpg_basis_labels_f32: too many nodes");
+  LPG_REQUIRE(total < ((int64_t)1 << 31), "lpg_basis_labels_f32: too many nodes");
   hipStream_t s = as_stream(stream);
   const Ws w = carve(workspace, total);
   const unsigned nb = (unsigned)((total + kBT - 1) / kBT);
@@ -223,6 +238,7 @@ extern "C" lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float
     hipLaunchKernelGGL(basis_pass2, dim3(nb), dim3(kBT), 0, s, total, m, w);
     hipLaunchKernelGGL(basis_pass3, dim3(nb), dim3(kBT), 0, s, total, w);
     hipLaunchKernelGGL(basis_ties, dim3(nb), dim3(kBT), 0, s, total, w);
+    hipLaunchKernelGGL(basis_tie_scan, dim3(1), dim3(1024), 0, s, (int64_t)nb, w);
   }
   hipLaunchKernelGGL(basis_labels, dim3(nb), dim3(kBT), 0, s, total, (int32_t)(m > 0), w, labels);
   LPG_HIP(hipGetLastError());

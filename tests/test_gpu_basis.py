@@ -66,9 +66,9 @@ def test_basis_labels_ties_lowest_index_and_invariants():
     above the m-th largest P[:, 1] plus the lowest-index nodes equal to it."""
     g = torch.Generator().manual_seed(3)
     pool = torch.randn(40, 3, generator=g) * 2
-    idx = torch.randint(0, 40, (50_000,), generator=g)
+    idx = torch.randint(0, 40, (400_000,), generator=g)  # 1563 blocks: the tie scan runs >1 block per thread
     logits = pool[idx]
-    m = 17_321
+    m = 137_321
     dev = _device_labels(logits, m)
     p1 = torch.softmax(logits.to(DEV), dim=-1)[:, 1].cpu()
     # the device's own P[:, 1] order: recompute the keys the kernel selected on
