@@ -42,6 +42,7 @@ for s in $STAGES; do
       ;;
     bench_c5) step bench_c5 900 python bench.py --config c5 --steps 10 --warmup 3 ;;
     bench_inf) step bench_inf 600 python bench.py --inference ;;
+    bench_c4) step bench_c4 900 python bench.py --config c4 --steps 5 --warmup 2 --cpu-steps 0 ;;
     prof_c5)
       step prof_c5 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run -- \
         python "$ROOT/bench.py" --config c5 --steps 3 --warmup 2 --profile-only
