@@ -46,9 +46,10 @@ from .sparse import BipartiteCSR, CSR, spmm_forward
 _GEMM_FLOPS = 160e12  # in-step rates used only to pick the cheaper association
 _SPMM_BYTES = 7e12
 # LPGNN_OVERLAP=1: run the HBM-bound SpMMs that are independent of the current FC / GEMM on a
-# second stream beside it.  Measured on c2: ~1 ms (2.6 %) more whole-step throughput, but the
-# overlapped SpMM launches then share CUs and HBM with the FC and each takes ~2x longer, which
-# hides the kernel's own roofline fraction in the bench -- off by default.
+# second stream beside it.  Measured on c2: ~1 ms (2.6 %) more whole-step throughput in round 1; at
+# the round-3 kernels 20.88-21.09 against 21.05-21.08 ms (noise), while the overlapped SpMM launches
+# share CUs and HBM with the FC and read 0.85 of the roofline instead of 0.98 -- off by default
+# (DESIGN.md §6, §9).
 _OVERLAP = os.environ.get("LPGNN_OVERLAP", "0") == "1"
 REASSOCIATE = os.environ.get("LPGNN_REASSOC", "1") == "1"
 # LPGNN_FUSE_HEAD_FWD=0: the heads' forward as its own Linear kernels instead of in the last layer's FC epilogue
