@@ -1,0 +1,21 @@
+"""x3 FC at the verdict's K = 2048 shape (M = 200 K, K = 1024 + 1024, N = 1024, ReLU), a few
+launches, for rocprofv3 --pmc passes (past-L2 bytes, MFMA busy, clock)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "lp-gnn_amd")]
+import torch  # noqa: E402
+
+from lpgnn.fc import fc_forward  # noqa: E402
+
+torch.manual_seed(0)
+A1 = torch.randn(200_000, 1024, device="cuda")
+A2 = torch.randn(200_000, 1024, device="cuda")
+W1 = torch.randn(1024, 1024, device="cuda") * 0.03
+W2 = torch.randn(1024, 1024, device="cuda") * 0.03
+b = torch.randn(1024, device="cuda")
+for _ in range(4):
+    fc_forward(A1, W1, A2, W2, b, True, arith="x3")
+torch.cuda.synchronize()
+print("done")
