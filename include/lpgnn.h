@@ -416,6 +416,14 @@ lpg_status lpg_heads_bwd_bf16(int64_t M, int64_t K, int64_t N, const float *G, i
  * lpg_class_counts_workspace_bytes(M). */
 int64_t lpg_class_counts_workspace_bytes(int64_t M);
 lpg_status lpg_class_counts3(int64_t M, const int64_t *y, int64_t *counts, void *workspace, void *stream);
+/* The balanced loss's class weights themselves (utils.py:286-299 labels_to_balanced_weights, on the
+ * device, no host sync): weights[c] = N / count_c (float32 operands, correctly rounded) for the
+ * present classes of y (labels 0, 1, 2), 0 otherwise; with merge_lu and other than exactly two
+ * classes present, weights[0] = weights[2] = (weights[0] + weights[2]) / 2.  The counting pass of
+ * lpg_class_counts3 plus the formula in its fold (one launch fewer than ~13 elementwise ops).
+ * Workspace: lpg_class_counts_workspace_bytes(M). */
+lpg_status lpg_balanced_weights3(int64_t M, const int64_t *y, int32_t merge_lu, float *weights, void *workspace,
+                                 void *stream);
 
 int64_t lpg_weighted_ce_workspace_bytes(int64_t M);
 lpg_status lpg_weighted_ce_fwd_f32(int64_t M, int64_t C, const float *x, int64_t ldx, const int64_t *y,

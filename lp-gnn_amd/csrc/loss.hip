@@ -200,7 +200,8 @@ __global__ __launch_bounds__(256) void class_counts_p1(int64_t M, const int64_t 
 }
 
 __global__ __launch_bounds__(256) void class_counts_p2(int nblk, const int64_t *__restrict__ part,
-                                                       int64_t *__restrict__ counts) {
+                                                       int64_t *__restrict__ counts, float *__restrict__ weights,
+                                                       int32_t merge_lu) {
   __shared__ int64_t red[3][256];
 #pragma unroll
   for (int c = 0; c < 3; ++c) red[c][threadIdx.x] = (int)threadIdx.x < nblk ? part[threadIdx.x * 3 + c] : 0;
@@ -210,7 +211,18 @@ __global__ __launch_bounds__(256) void class_counts_p2(int nblk, const int64_t *
       for (int c = 0; c < 3; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x < 3) counts[threadIdx.x] = red[threadIdx.x][0];
+  if (threadIdx.x < 3 && counts) counts[threadIdx.x] = red[threadIdx.x][0];
+  if (threadIdx.x == 0 && weights) {
+    // labels_to_balanced_weights (utils.py:286-299): w[c] = N / count_c (int64 true division, i.e.
+    // float32 operands, correctly rounded) for present classes, 0 otherwise; unless exactly two
+    // classes are present, w0 = w2 = (w0 + w2) / 2 (merge_lu)
+    const int64_t c0 = red[0][0], c1 = red[1][0], c2 = red[2][0];
+    const float n = (float)(c0 + c1 + c2);
+    float w0 = c0 > 0 ? n / (float)c0 : 0.f, w2 = c2 > 0 ? n / (float)c2 : 0.f;
+    const float w1 = c1 > 0 ? n / (float)c1 : 0.f;
+    if (merge_lu && (c0 > 0) + (c1 > 0) + (c2 > 0) != 2) w0 = w2 = (w0 + w2) / 2.f;
+    weights[0] = w0, weights[1] = w1, weights[2] = w2;
+  }
 }
 }  // namespace
 }  // namespace lpg
@@ -229,7 +241,23 @@ extern "C" lpg_status lpg_class_counts3(int64_t M, const int64_t *y, int64_t *co
   int64_t *part = static_cast<int64_t *>(workspace);
   hipLaunchKernelGGL(class_counts_p1, dim3(nblk), dim3(256), 0, s, M, y, part);
   LPG_HIP(hipGetLastError());
-  hipLaunchKernelGGL(class_counts_p2, dim3(1), dim3(256), 0, s, nblk, part, counts);
+  hipLaunchKernelGGL(class_counts_p2, dim3(1), dim3(256), 0, s, nblk, part, counts, (float *)nullptr, 0);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_balanced_weights3(int64_t M, const int64_t *y, int32_t merge_lu, float *weights,
+                                            void *workspace, void *stream) {
+  LPG_REQUIRE(M >= 0, "lpg_balanced_weights3: negative size");
+  LPG_REQUIRE(weights && workspace && (M == 0 || y), "lpg_balanced_weights3: NULL pointer");
+  hipStream_t s = as_stream(stream);
+  const int64_t want = (M + 256 * 8 - 1) / (256 * 8);
+  const int nblk = (int)(want < 1 ? 1 : (want > kCntBlocks ? kCntBlocks : want));
+  int64_t *part = static_cast<int64_t *>(workspace);
+  hipLaunchKernelGGL(class_counts_p1, dim3(nblk), dim3(256), 0, s, M, y, part);
+  LPG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(class_counts_p2, dim3(1), dim3(256), 0, s, nblk, part, (int64_t *)nullptr, weights,
+                     merge_lu ? 1 : 0);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }

@@ -47,6 +47,7 @@ HEADER_SYMBOLS = (
     "lpg_weighted_ce_workspace_bytes",
     "lpg_class_counts_workspace_bytes",
     "lpg_class_counts3",
+    "lpg_balanced_weights3",
     "lpg_basis_labels_workspace_bytes",
     "lpg_basis_labels_f32",
     "lpg_weighted_ce_fwd_f32",
@@ -131,6 +132,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_class_counts_workspace_bytes.restype = c_i64
     L.lpg_class_counts3.argtypes = [c_i64, c_p, c_p, c_p, c_p]
     L.lpg_class_counts3.restype = c_i32
+    L.lpg_balanced_weights3.argtypes = [c_i64, c_p, c_i32, c_p, c_p, c_p]
+    L.lpg_balanced_weights3.restype = c_i32
     L.lpg_basis_labels_workspace_bytes.argtypes = [c_i64]
     L.lpg_basis_labels_workspace_bytes.restype = c_i64
     L.lpg_basis_labels_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p]

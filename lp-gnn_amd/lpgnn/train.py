@@ -13,27 +13,30 @@ def labels_to_balanced_weights(labels, merge_lu=True):
     exactly two classes are present, w0 = w2 = mean(w0, w2).
 
     Restated without torch.unique / len(lbl) (which force a device->host
-    sync every step): class counts on the device
-    (lpg_class_counts3; a scatter-add onto three bins serialises its atomics:
-    41 us per call at 200 K labels), the same N / count_c division, branch
-    choices as tensor selects -- bitwise the reference's result
+    sync every step).  On a HIP device one call,
+    lpg_balanced_weights3: the class counts (a scatter-add onto three bins
+    serialises its atomics: 41 us per call at 200 K labels) and the formula
+    in the counts' fold (instead of ~13 elementwise launches); on the host
+    the tensor form below.  Both bitwise the reference's result
     (tests/test_gpu_model.py)."""
     labels = labels.view(-1)
     if labels.device.type == "cuda" and labels.dtype == torch.int64:
+        # counts and the formula below in one device pass (lpg_balanced_weights3), the same bits
         from . import _lib
 
         labels = labels.contiguous()
         L = _lib.lib()
-        cnt = torch.empty(3, dtype=torch.int64, device=labels.device)
+        res = torch.empty(3, dtype=torch.float32, device=labels.device)
         ws = torch.empty(L.lpg_class_counts_workspace_bytes(labels.numel()) // 8, dtype=torch.int64,
                          device=labels.device)
         with torch.cuda.device(labels.device):
-            st = L.lpg_class_counts3(labels.numel(), labels.data_ptr(), cnt.data_ptr(), ws.data_ptr(),
-                                     _lib.stream_of(labels))
-        _lib.check(st, "lpg_class_counts3")
-    else:  # host-side callers (data preparation, CPU tests of the formula)
-        cnt = torch.zeros(3, dtype=torch.int64, device=labels.device)
-        cnt.scatter_add_(0, labels, torch.ones_like(labels))
+            st = L.lpg_balanced_weights3(labels.numel(), labels.data_ptr(), 1 if merge_lu else 0, res.data_ptr(),
+                                         ws.data_ptr(), _lib.stream_of(labels))
+        _lib.check(st, "lpg_balanced_weights3")
+        return res
+    # host-side callers (data preparation, CPU tests of the formula)
+    cnt = torch.zeros(3, dtype=torch.int64, device=labels.device)
+    cnt.scatter_add_(0, labels, torch.ones_like(labels))
     present = cnt > 0
     wei = cnt.sum() / cnt
     res = torch.where(present, wei, torch.zeros((), dtype=wei.dtype, device=labels.device))

@@ -180,7 +180,8 @@ def test_training_step_runs_and_matches_oracle_grads(arith, hids, monkeypatch):
     assert torch.isfinite(L).item()
 
 
-@pytest.mark.parametrize("labels", [[0, 1, 2, 1, 1, 0], [1, 1, 2, 2, 2], [0, 0, 0], [1, 1], [2, 1, 2],
+@pytest.mark.parametrize("labels", [[0, 1, 2, 1, 1, 0], [1, 1, 2, 2, 2], [0, 0, 0], [1, 1], [2, 1, 2], [1], [2],
+                                    [2, 2, 2, 0], [0, 1],
                                     [0, 2, 0, 2, 0], list(np.random.default_rng(0).integers(0, 3, 50000)),
                                     list(np.random.default_rng(1).integers(0, 3, 600_000))])
 @pytest.mark.parametrize("merge", [True, False])
