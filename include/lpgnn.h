@@ -454,6 +454,11 @@ lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float *logits, i
  * Bitwise torch-CPU F.normalize semantics (norm = sqrt(fma(x2,x2,fma(x1,x1,x0*x0)))). */
 lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t ldl, const float *feas, int64_t ldf,
                              int64_t feas_cols, float bound, float *out, int64_t ldo, void *stream);
+/* Its backward (autograd of F.normalize(x) * 10, arch.py:134-135; the bound subtractions pass g
+ * through): dx = 10 (g / d - x (x . g) / d^3) where |x| > 1e-12, else 10 g / d (d = max(|x|, 1e-12)),
+ * logit / g / dx [M, 3] with row strides ldl / ldg / lddx.  One pass instead of torch's ~12 kernels. */
+lpg_status lpg_knowledge_bwd_f32(int64_t M, const float *logit, int64_t ldl, const float *g, int64_t ldg, float *dx,
+                                 int64_t lddx, void *stream);
 
 /* ---- k-hop neighbour sampling (NeighborLoader collate, train.py:111-116,
  * val.py:22-27; replaces torch_sparse 0.6.12 neighbor_sample) -------------

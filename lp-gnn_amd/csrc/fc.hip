@@ -301,6 +301,25 @@ __global__ __launch_bounds__(256) void knowledge_f32(int64_t M, const float *__r
   out[m * ldo + 2] = y2;
 }
 
+// backward of y = normalize(x) * 10 (the mask subtractions have unit derivative), torch autograd's
+// formula for F.normalize (arch.py:134-135):
+//   dx = 10 (g / d - x (x . g) / d^3) where n > 1e-12, else 10 g / d   (d = max(n, 1e-12))
+__global__ __launch_bounds__(256) void knowledge_bwd_f32(int64_t M, const float *__restrict__ logit, int64_t ldl,
+                                                         const float *__restrict__ g, int64_t ldg,
+                                                         float *__restrict__ dx, int64_t lddx) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const float x[3] = {logit[m * ldl], logit[m * ldl + 1], logit[m * ldl + 2]};
+  const float gv[3] = {g[m * ldg], g[m * ldg + 1], g[m * ldg + 2]};
+  const float nrm = sqrtf(__builtin_fmaf(x[2], x[2], __builtin_fmaf(x[1], x[1], x[0] * x[0])));
+  const float d = nrm < 1e-12f ? 1e-12f : nrm;
+  const float xg = x[0] * gv[0] + x[1] * gv[1] + x[2] * gv[2];
+  const float d3 = d * d * d;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    dx[m * lddx + c] = nrm > 1e-12f ? 10.f * (gv[c] / d - x[c] * xg / d3) : 10.f * gv[c] / d;
+}
+
 // dZ = (Y > 0) ? g * scale : 0 -- backward of ReLU followed by dropout
 // (Y is the stored post-dropout output, so Y > 0 <=> kept and ReLU-active).
 __global__ __launch_bounds__(256) void relu_dropout_bwd_f32(int64_t n4, const float4 *__restrict__ g,
@@ -547,6 +566,18 @@ extern "C" lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const 
   hipLaunchKernelGGL(relu_dropout_bwd_f32, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), n4,
                      reinterpret_cast<const float4 *>(g), reinterpret_cast<const float4 *>(y), scale,
                      reinterpret_cast<float4 *>(out));
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_knowledge_bwd_f32(int64_t M, const float *logit, int64_t ldl, const float *g, int64_t ldg,
+                                            float *dx, int64_t lddx, void *stream) {
+  LPG_REQUIRE(M >= 0, "lpg_knowledge_bwd_f32: M < 0");
+  if (M == 0) return LPG_OK;
+  LPG_REQUIRE(logit && g && dx, "lpg_knowledge_bwd_f32: NULL pointer");
+  LPG_REQUIRE(ldl >= 3 && ldg >= 3 && lddx >= 3, "lpg_knowledge_bwd_f32: bad shapes");
+  hipLaunchKernelGGL(knowledge_bwd_f32, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, as_stream(stream), M, logit,
+                     ldl, g, ldg, dx, lddx);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }

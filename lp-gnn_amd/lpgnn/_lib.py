@@ -67,6 +67,7 @@ HEADER_SYMBOLS = (
     "lpg_heads_bwd_bf16_workspace_bytes",
     "lpg_heads_bwd_bf16",
     "lpg_knowledge_f32",
+    "lpg_knowledge_bwd_f32",
     "lpg_scan_i64_workspace_bytes",
     "lpg_scan_i64",
     "lpg_sample_count",
@@ -201,6 +202,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_heads_bwd_bf16.restype = c_i32
     L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_i64, ctypes.c_float, c_p, c_i64, c_p]
     L.lpg_knowledge_f32.restype = c_i32
+    L.lpg_knowledge_bwd_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p]
+    L.lpg_knowledge_bwd_f32.restype = c_i32
     L.lpg_scan_i64_workspace_bytes.argtypes = [c_i64]
     L.lpg_scan_i64_workspace_bytes.restype = c_i64
     L.lpg_scan_i64.argtypes = [c_p, c_i64, c_p, c_p, c_i64, c_p]

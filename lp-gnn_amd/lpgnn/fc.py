@@ -754,12 +754,14 @@ class _Knowledge(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        """autograd of F.normalize(x) * 10 in one pass (lpg_knowledge_bwd_f32)."""
         (x,) = ctx.saved_tensors
-        n = torch.linalg.vector_norm(x, dim=1, keepdim=True)
-        d = n.clamp_min(1e-12)
-        xg = (x * g).sum(1, keepdim=True)
-        big = n > 1e-12
-        dx = torch.where(big, 10.0 * (g / d - x * xg / (d * d * d)), 10.0 * g / d)
+        g = g.contiguous().float()
+        dx = torch.empty_like(x)
+        with torch.cuda.device(x.device):
+            st = _lib.lib().lpg_knowledge_bwd_f32(x.shape[0], x.data_ptr(), x.stride(0), g.data_ptr(), g.stride(0),
+                                                  dx.data_ptr(), dx.stride(0), _lib.stream_of(x))
+        _lib.check(st, "lpg_knowledge_bwd_f32")
         return dx, None, None
 
 
