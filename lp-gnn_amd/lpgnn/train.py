@@ -171,7 +171,10 @@ def train_step(model, batch, opt, loss="balanced", check_nan=True):
     the seed nodes, loss, backward, optimizer step.  Returns the loss tensor
     (no host sync unless check_nan)."""
     logit_cons, logit_vars = model(batch)
-    logit_cons, logit_vars = logit_cons[:batch.s_bs], logit_vars[:batch.t_bs]
+    # the seed-node slices (train.py:122-123); a slice that covers the whole tensor is skipped: its
+    # autograd node would allocate a zero gradient and copy into it every step for the same values
+    seed = lambda t, k: t if k == t.shape[0] else t[:k]
+    logit_cons, logit_vars = seed(logit_cons, batch.s_bs), seed(logit_vars, batch.t_bs)
     y_s, y_t = batch.y_s[:batch.s_bs], batch.y_t[:batch.t_bs]
     L = LOSSES[loss](logit_cons, logit_vars, y_s, y_t)
     if check_nan:
