@@ -421,3 +421,18 @@ def test_transpose_bf16(R, C):
     assert torch.equal(transpose_bf16(W), W.t().contiguous())
     big = torch.randn(R, C + 16, device=DEV).to(BF)[:, 8:8 + C]  # strided source rows
     assert torch.equal(transpose_bf16(big), big.t().contiguous())
+
+
+@pytest.mark.parametrize("M,N", [(1, 8), (7, 16), (63, 16), (65, 256), (1000, 2048), (4099, 1032), (70001, 256)])
+def test_colsum_bf16_bitwise_masked_pass(M, N):
+    """lpg_colsum_bf16 (read-only column sums, double-buffered rows) == the bias gradient of
+    relu_bwd_colsum_bf16 with every element kept and scale 1 (the same blocks, row order and fold),
+    incl. ragged last blocks."""
+    from lpgnn.fc import colsum_bf16, relu_bwd_colsum_bf16
+
+    torch.manual_seed(M * 7 + N)
+    g = torch.randn(M, N, device=DEV).to(BF)
+    y = torch.ones(M, N, device=DEV, dtype=BF)
+    out, db = relu_bwd_colsum_bf16(g, y, 1.0, True)
+    assert torch.equal(out, g)
+    assert torch.equal(colsum_bf16(g), db)
