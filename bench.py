@@ -4,34 +4,37 @@ SpMM kernel and the oracle CPU path timed beside it.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
 
+One workload family at every N (the line the driver turns into a scaling curve):
+
+* headline ``value`` -- c2 WEAK scaling (BASELINE.json configs[1] per GPU).  A step = one
+  GCN_FC(8, 8, hids=1024, depth=3) training iteration of train.py:117-129: forward (2 SpMM at F=8
+  + 2 at F=1024, FC stacks, heads, add_knowledge), balanced loss, backward (2 SpMM at F=1024 + FC
+  grads), Adam.  N=1: the synthetic c2 graph (100K cons x 200K vars, nnz 2M) on one GPU.  N>1: N
+  c2-sized row blocks of one block LP (each block's edges leave its variable range with
+  probability rho = 0.02), constraint-row partitioned, one block per rank (lpgnn.partition:
+  owner reduce / halo broadcast of boundary-variable rows over RCCL).  value = (hid-width SpMM
+  edge traversals of all ranks in the timed steps) / (max-over-ranks time).
+* sub-record ``c4`` -- BASELINE.json configs[3] (2M x 4M, nnz 40M, fixed) at the same N: the whole
+  graph on one GPU at N=1, row-partitioned over the N ranks at N>1 (STRONG scaling), with the
+  locality (rho) sweep of the partition at N>1.
+* sub-record ``inference`` (N=1) -- the reference's own timed path (scripts/pred_basis.py:157-176):
+  eval-mode model(batch) + inference_gnn on c2, ms/graph, with the oracle's CPU inference beside it.
+
 With --gpus N > 1 and no RANK / WORLD_SIZE in the environment, bench.py launches the N ranks
 itself (one child process per GPU, started before this process touches the GPU; rank 0 prints
 the JSON line) -- the same line as under ``torch.distributed.run --nproc-per-node N``.
 ``--share-gpu`` makes the N ranks share the visible GPU(s) over gloo (a rehearsal on a 1-GPU
 box; the measured runs use RCCL, one rank per GPU).
 
-A step = one GCN_FC(8, 8, hids=1024, depth=3) training iteration of
-train.py:117-129 on the synthetic c2 graph (100K cons x 200K vars, nnz 2M,
-BASELINE.json configs[1]): forward (2 SpMM at F=8 + 2 at F=1024, FC stacks,
-heads, add_knowledge), balanced loss, backward (2 SpMM at F=1024 + FC
-grads), Adam step.  value = (hid-width SpMM edge traversals in the step) /
-step time, whole job.
-
-N>1 defaults to ``--config c4`` (BASELINE.json configs[3]): the fixed
-2M cons x 4M vars, nnz 40M block LP, constraint-row partitioned over the N
-ranks (one process per GPU, torchrun) -- STRONG scaling; each rank generates
-and plans only its own row blocks (lpgnn.partition.plan_partition_blocks),
-boundary-variable rows are reduced to their owners and broadcast back over
-RCCL.  ``--config c2`` with N>1 is the weak-scaling variant (N c2-sized
-blocks).  ``--config c4`` at N=1 runs the whole c4 graph on one GPU.
-
-``--config c5`` runs BASELINE.json configs[4] instead (same graph,
-GCN_FC hids=2048 depth=6, bf16 activations / SpMM storage / MFMA FC, fp32
-master weights) -- the MFMA-utilisation stress line, not the headline.
+``--config c4`` times c4 as the headline instead, ``--config c5`` BASELINE.json configs[4]
+(same graph, GCN_FC hids=2048 depth=6, bf16 activations / SpMM storage / MFMA FC, fp32 master
+weights; one GPU) -- the MFMA-utilisation stress line, not the headline.  ``--inference`` times
+the eval path as the headline (``--fp16``: the reference's model.half() mode, val.py:269).
 """
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import sys
@@ -44,17 +47,18 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+METRIC = "edges/sec bipartite SpMM (hid=1024, depth=3) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense (MI355X_MICROARCH.md; the 5 PF figure is 2:1 sparse)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense (MI355X_MICROARCH.md; the 5 PF figure is 2:1 sparse); fp16 the same
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=("c2", "c4", "c5"), default=None,
-                    help="c2 = headline fp32 hid 1024 depth 3 (default at N=1); c4 = 2M x 4M nnz 40M "
-                         "row-partitioned, strong scaling (default at N>1); c5 = bf16 hid 2048 depth 6")
+    ap.add_argument("--config", choices=("c2", "c4", "c5"), default="c2",
+                    help="c2 = headline fp32 hid 1024 depth 3, weak scaling over N (default); c4 = 2M x 4M nnz 40M "
+                         "(whole graph at N=1, row-partitioned at N>1: strong scaling); c5 = bf16 hid 2048 depth 6")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--m", type=int, default=None)
@@ -64,8 +68,8 @@ def parse():
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--rho", type=float, default=0.02, help="boundary edge fraction for N>1 partitions")
     ap.add_argument("--cpu-steps", type=int, default=1, help="oracle CPU steps for cpu_baseline (0 = skip)")
-    ap.add_argument("--profile-only", action="store_true", help="no CPU baseline, no JSON extras (rocprof runs)")
-    ap.add_argument("--print-workload", action="store_true", help="print the N=1 workload string and exit")
+    ap.add_argument("--profile-only", action="store_true", help="no CPU baseline, no sub-records (rocprof runs)")
+    ap.add_argument("--print-workload", action="store_true", help="print the workload string and exit")
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned RCCL path even at N=1 (the N>1 code path)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -74,15 +78,29 @@ def parse():
                     help="c4 at N>1: rho values whose partition boundary counts go into the JSON ('' = off)")
     ap.add_argument("--inference", action="store_true",
                     help="time eval-mode forward + inference_gnn (the reference's timed path) instead of training")
-    args = ap.parse_args()
-    if args.config is None:
-        args.config = "c2" if args.gpus == 1 else "c4"
+    ap.add_argument("--fp16", action="store_true",
+                    help="with --inference: the reference's --fp16 mode (model.half(), batch_to(half=True))")
+    ap.add_argument("--sub", default="c4,inference",
+                    help="sub-records after the headline ('' = none): c4 (configs[3] at the same N), "
+                         "inference (N=1: the reference's timed eval path on c2)")
+    ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--c4-warmup", type=int, default=2)
+    ap.add_argument("--c4-scale", type=int, default=1, help="c4 sub-record at 1/scale size (rehearsals)")
+    ap.add_argument("--inf-steps", type=int, default=20)
+    args = ap.parse_args(argv)
+    fill(args)
+    return args
+
+
+def fill(args):
     from lpgnn.synth import CONFIGS
 
     for k, v in CONFIGS[args.config].items():
         if getattr(args, k) is None:
             setattr(args, k, v)
     args.bf16 = args.config == "c5"
+    if args.fp16 and not args.inference:
+        raise SystemExit("--fp16 is the reference's inference mode (val.py:269, pred_basis.py:146): use --inference")
     return args
 
 
@@ -93,9 +111,10 @@ def spmm_bytes(n_rows: int, nnz: int, F: int, s: int = 4) -> int:
     return nnz * F * s + nnz * 8 + (n_rows + 1) * 8 + n_rows * F * s
 
 
-def load_pmc_traffic(workload: str):
+def load_pmc_traffic(key: str):
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
-    PMC summary (profiles/*pmc*.json, produced by tools/pmc_summary.py)."""
+    PMC summary (profiles/*pmc*.json, produced by tools/pmc_summary.py), matched
+    on its ``workload`` key (the N=1 workload string, or a rank-share key)."""
     import glob
 
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
@@ -103,9 +122,19 @@ def load_pmc_traffic(workload: str):
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+        if d.get("workload") == key and d.get("hbm_bytes_per_launch"):
             return d["hbm_bytes_per_launch"], os.path.basename(path)
     return None, None
+
+
+def rank_share_key(family: str, world: int, rank: int = 0) -> str:
+    """The PMC key of one rank's share of a partitioned workload (tools/pmc_rank_share.py)."""
+    return f"{family} rank share: rank {rank} of {world}, F=1024 SpMM both directions"
+
+
+def _threads():
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return min(threads, len(os.sched_getaffinity(0)))
 
 
 def cpu_baseline(g, hids, depth, steps):
@@ -113,8 +142,7 @@ def cpu_baseline(g, hids, depth, steps):
     timed on this host for `steps` full fwd+bwd steps of the same workload."""
     from oracle import model_ref as O
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    threads = min(threads, len(os.sched_getaffinity(0)))
+    threads = _threads()
     torch.set_num_threads(threads)
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
@@ -139,14 +167,14 @@ def cpu_baseline(g, hids, depth, steps):
     return dt, threads
 
 
-def cpu_inference(g, hids, depth, steps, bf16=False):
+def cpu_inference(g, hids, depth, steps, fp16=False):
     """The oracle's eval-mode forward (C spmm_cpu loop + torch CPU GEMMs, fp32: the reference's
-    CPU arithmetic) + inference_gnn (val.py:106-124) on this host, `steps` graphs after one
-    untimed warm-up -- the reference's timed inference path (scripts/pred_basis.py:113-118)."""
+    CPU arithmetic; ``fp16``: the same with every stored tensor rounded to fp16, the oracle of the
+    --fp16 mode) + inference_gnn (val.py:106-124) on this host, `steps` graphs after one untimed
+    warm-up -- the reference's timed inference path (scripts/pred_basis.py:113-118)."""
     from oracle import model_ref as O
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    threads = min(threads, len(os.sched_getaffinity(0)))
+    threads = _threads()
     torch.set_num_threads(threads)
     A = O.csr_from_coo(g.row, g.col, g.val, g.m, g.n)
     AT = O.csr_transpose(*A, g.m, g.n)
@@ -155,8 +183,11 @@ def cpu_inference(g, hids, depth, steps, bf16=False):
 
     def infer():
         with torch.no_grad():
-            lc, lv = O.gcn_fc_forward(sd, x_s, x_t, A, AT, depth)
-            return O.inference_gnn(torch.cat((lc, lv)), g.m)
+            if fp16:
+                lc, lv = O.gcn_fc_forward_fp16(sd, x_s, x_t, A, AT, depth)
+            else:
+                lc, lv = O.gcn_fc_forward(sd, x_s, x_t, A, AT, depth)
+            return O.inference_gnn(torch.cat((lc.float(), lv.float())), g.m)
 
     infer()
     t0 = time.perf_counter()
@@ -201,7 +232,8 @@ def cpu_spmm(g, F, reps=3):
 
 
 def workload_name(args) -> str:
-    dt = ", bf16" if args.bf16 else ""
+    """The one-GPU workload string (also the PMC key of the N=1 line)."""
+    dt = ", bf16" if args.bf16 else (", fp16" if getattr(args, "fp16", False) else "")
     kind = "synthetic block LP (8 row blocks, rho=%g)" % args.rho if args.config == "c4" else "synthetic LP"
     what = "eval forward + inference_gnn" if getattr(args, "inference", False) else "fwd+bwd+Adam"
     return (f"{args.config}: {kind} {args.m}x{args.n} nnz={args.nnz}, "
@@ -252,6 +284,257 @@ def self_launch(args) -> int:
     return rc
 
 
+# ------------------------------------------------------------------- measurement
+class Ctx:
+    """Per-process run context: rank, world, device, backend, whether a process group is up."""
+
+    def __init__(self, rank, world, dev, backend, distributed):
+        self.rank, self.world, self.dev, self.backend, self.distributed = rank, world, dev, backend, distributed
+
+    def sync(self):
+        torch.cuda.synchronize()
+        if self.distributed:
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+
+    def gather(self, obj):
+        if not self.distributed:
+            return [obj]
+        out = [None] * self.world
+        torch.distributed.all_gather_object(out, obj)
+        return out
+
+
+def timed(ctx, step, steps, warmup):
+    """W untimed warm-up steps, then exactly K steps bracketed by a barrier + device sync on both
+    sides; the hot-path kernels' HIP events recorded on their launch stream (lpgnn.timing).
+    Returns (this rank's seconds, {key: (launches, ms)}, {key: [ms per launch]})."""
+    from lpgnn.timing import TIMER
+
+    for _ in range(warmup):
+        step()
+    ctx.sync()
+    TIMER.reset()
+    TIMER.enabled = True
+    tw0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.sync()
+    dt = time.perf_counter() - t0
+    if os.environ.get("LPGNN_TRACE_WINDOW"):  # the timed region on the profiler's clock (tools/trace_timeline.py)
+        print(f"TRACE_WINDOW rank={ctx.rank} boottime_ns={tw0} {time.clock_gettime_ns(time.CLOCK_BOOTTIME)}",
+              file=sys.stderr, flush=True)
+    TIMER.enabled = False
+    kern, per_launch = TIMER.summary(), TIMER.launches()
+    TIMER.reset()
+    return dt, kern, per_launch
+
+
+def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_key, single_dirs=None, fp16=False,
+           training=True):
+    """value, ms_per_step, the SpMM roofline and the hidden-width GEMM roofline of one timed run,
+    aggregated over the ranks (collective: every rank calls it).
+
+    value = sum over ranks of the hid-width SpMM edge traversals / the max-over-ranks wall time.
+    roofline.achieved = per-GPU GB/s = (sum over ranks of the algorithmic bytes of the F=hid SpMM
+    launches) / (N x the slowest rank's summed SpMM kernel time); at N=1 bytes / time of the one GPU.
+    roofline.per_rank keeps every rank's own fraction."""
+    hid_keys = [k for k in kern if k[0] == "spmm" and k[3] == hids]
+    launches = sum(kern[k][0] for k in hid_keys)
+    spmm_ms = sum(kern[k][1] for k in hid_keys)
+    bytes_total = sum(kern[k][0] * spmm_bytes(k[1], local_nnz, k[3], esz) for k in hid_keys)
+    # dense GEMMs of hidden width on the hand-written kernels (FC forward + x3 input and weight
+    # gradients; K >= hid): MFMA utilisation.  x3 = fp32 through the exact three-way bf16 split,
+    # 6 bf16 MFMA products per fp32 product, so its MFMA-bound peak is the dense bf16 peak / 6.
+    fc_keys = [k for k in kern if k[0] in ("fc", "wgrad") and k[3] >= hids and k[2] >= 64]
+    x3 = any(str(k[4]).endswith("x3") for k in fc_keys)
+    half = esz == 2
+    fc_flops = sum(kern[k][0] * 2.0 * k[1] * k[2] * k[3] for k in fc_keys)
+    fc_ms = sum(kern[k][1] for k in fc_keys)
+    fc_launches = sum(kern[k][0] for k in fc_keys)
+    mine = dict(dt=dt, edges=launches * local_nnz, bytes=bytes_total, spmm_ms=spmm_ms, launches=launches,
+                fc_flops=fc_flops, fc_ms=fc_ms)
+    every = ctx.gather(mine)
+    dt_max = max(r["dt"] for r in every)
+    world = len(every)
+    value = sum(r["edges"] for r in every) / dt_max
+    t_max = max(r["spmm_ms"] for r in every)
+    b_sum = sum(r["bytes"] for r in every)
+    achieved = b_sum / (world * t_max / 1e3) / 1e9 if t_max > 0 else 0.0
+    traffic, traffic_src = load_pmc_traffic(traffic_key)
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": ("lpg spmm_%s_rowslim / rowwave" % ("f16" if fp16 else "bf16" if half else "f32"))
+                      + " (F=hid, both directions%s)" % (", fwd+bwd" if training else ", eval forward"),
+            "bytes_per_launch": b_sum / max(1, sum(r["launches"] for r in every)),
+            "avg_launch_ms": sum(r["spmm_ms"] for r in every) / max(1, sum(r["launches"] for r in every)),
+            "launches": sum(r["launches"] for r in every), "traffic_source": traffic_src, "traffic_key": traffic_key}
+    if world > 1:
+        roof["aggregation"] = ("per-GPU: sum of all ranks' algorithmic bytes / (N x the slowest rank's SpMM "
+                               "kernel time); traffic = the PMC of rank 0's share on one GPU")
+        roof["achieved_all_gpus"] = b_sum / (t_max / 1e3) / 1e9 if t_max > 0 else 0.0
+        roof["peak_all_gpus"] = HBM_PEAK_GBS * world
+        roof["per_rank"] = [{"frac": (r["bytes"] / (r["spmm_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS) if r["spmm_ms"] else 0.0,
+                             "avg_launch_ms": r["spmm_ms"] / max(1, r["launches"]), "launches": r["launches"],
+                             "bytes_per_launch": r["bytes"] / max(1, r["launches"])} for r in every]
+    fc_tf_all = sum(r["fc_flops"] for r in every) / (max(r["fc_ms"] for r in every) * world / 1e3) / 1e12 \
+        if any(r["fc_ms"] for r in every) else 0.0
+    fc_peak = BF16_MFMA_PEAK_TFLOPS if half else (BF16_MFMA_PEAK_TFLOPS / 6 if x3 else FP32_MFMA_PEAK_TFLOPS)
+    fc = {"bound": "mfma", "achieved": fc_tf_all, "peak": fc_peak, "unit": "TFLOP/s", "frac": fc_tf_all / fc_peak,
+          "launches": fc_launches,
+          "kernel": ("lpg fc_f16 (hidden-width FC forward on v_mfma_f32_16x16x32_f16)" if fp16 else
+                     "lpg fc_bf16 + wgrad_bf16 (hidden-width GEMMs, fwd + bwd: FC forward, input "
+                     "gradients on the FC kernel, weight gradients)" if half else
+                     "lpg fc_fwd_x3 + wgrad_x3 (hidden-width GEMMs, fwd + bwd; fp32 via exact "
+                     "3-way bf16 split, peak = dense bf16 / 6)" if x3 else
+                     "lpg fc_fwd_f32 (hidden GraphConv FC, fwd)"),
+          "fp32_mfma_peak_frac": None if half else fc_tf_all / FP32_MFMA_PEAK_TFLOPS,
+          # the bf16 MFMA work these launches issue (x3: 6 bf16 products per fp32 product),
+          # comparable with a plain bf16 GEMM's rate on this chip
+          "bf16_mfma_equiv_tflops": fc_tf_all * (6 if x3 and not half else 1)}
+    dirs = {}
+    for k, v in per_launch.items():
+        if k[0] != "spmm" or k[3] != hids:
+            continue
+        name = (single_dirs or {}).get((k[1], k[2]), f"{k[1]}x{k[2]}")
+        med = float(np.median(v))
+        dirs[name] = {"median_ms": med, "launches": len(v), "edges_per_s": local_nnz / (med / 1e3),
+                      "roofline_frac": spmm_bytes(k[1], local_nnz, k[3], esz) / (med / 1e3) / 1e9 / HBM_PEAK_GBS}
+    return {"value": value, "ms_per_step": dt_max / max(1, steps) * 1e3, "roofline": roof, "fc_roofline": fc,
+            "spmm_directions": dirs,
+            "spmm_edges_per_s_kernel": launches * local_nnz / (spmm_ms / 1e3) if spmm_ms > 0 else None,
+            "spmm_ms_per_step": spmm_ms / max(1, steps),
+            "kernels": {f"{k[0]}[{k[1]}x{k[2]},F={k[3]},{k[4]}]": {"launches": v[0], "ms": v[1]}
+                        for k, v in sorted(kern.items())}}
+
+
+# ------------------------------------------------------------------------ jobs
+def one_gpu_job(args, dev, inference=False, fp16=False):
+    """The one-GPU workload of args.config: (step, graph, local nnz).  c2/c5: the uniform c2 graph;
+    c4: the whole block LP (lpgnn.partition.bench_spec at one rank)."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.train import make_optimizer, train_step
+
+    if args.config == "c4":
+        from lpgnn.partition import bench_spec
+
+        g = bench_spec(args, 1).full()
+    else:
+        g = synth.uniform_lp(args.m, args.n, args.nnz, seed=0)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(dev), x_t=torch.from_numpy(g.x_t).to(dev),
+                           y_s=torch.from_numpy(g.y_s).to(dev), y_t=torch.from_numpy(g.y_t).to(dev),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=args.hids, depth=args.depth,
+                   compute_dtype=torch.bfloat16 if args.bf16 else torch.float32).to(dev)
+    if inference:
+        # the reference's timed path (scripts/pred_basis.py:113-118, 169-173): eval-mode
+        # model(batch) + inference_gnn on the concatenated logits (val.py:106-124, with its
+        # invariant checks), one graph per step; --fp16: model.half() + batch_to(half=True)
+        from lpgnn.data import batch_to
+        from lpgnn.val import inference_gnn
+
+        if fp16:
+            model.half()
+            batch = batch_to(batch, dev, half=True)
+        model.eval()
+
+        def step():
+            with torch.no_grad():
+                lc, lv = model(batch)
+                return inference_gnn(torch.cat((lc, lv), 0), g.m)
+    else:
+        opt, _ = make_optimizer(model)
+        step = lambda: train_step(model, batch, opt)  # noqa: E731
+    return step, g, g.nnz
+
+
+def c4_args(args):
+    a = copy.copy(args)
+    a.config, a.m, a.n, a.nnz, a.hids, a.depth = "c4", None, None, None, None, None
+    a.inference, a.fp16 = False, False
+    fill(a)
+    if args.c4_scale > 1:
+        a.m, a.n, a.nnz = a.m // args.c4_scale, a.n // args.c4_scale, a.nnz // args.c4_scale
+    return a
+
+
+def run_config(ctx, a, steps, warmup, family):
+    """Time args `a`'s training workload at the current N: one GPU (N=1, not --partitioned) or this
+    rank's share of the row partition.  Returns (record, graph or None)."""
+    from lpgnn import partition
+
+    part = ctx.distributed
+    if not part:
+        step, g, local_nnz = one_gpu_job(a, ctx.dev)
+        workload = workload_name(a)
+        dirs = {(a.m, a.n): "cons<-vars", (a.n, a.m): "vars<-cons"}
+        key = workload
+    else:
+        job = partition.build_bench_job(a, ctx.rank, ctx.world, ctx.dev)
+        step, g, local_nnz, workload = job.step, None, job.local_nnz, job.workload
+        dirs = None
+        key = rank_share_key(family, ctx.world) if ctx.world > 1 else workload
+    dt, kern, per_launch = timed(ctx, step, steps, warmup)
+    rec = report(ctx, dt, kern, per_launch, steps=steps, hids=a.hids, local_nnz=local_nnz,
+                 esz=2 if a.bf16 else 4, traffic_key=key, single_dirs=dirs)
+    rec["workload"] = workload
+    rec["config"] = {"workload": workload, "n_cons": a.m * (ctx.world if part and a.config != "c4" else 1),
+                     "n_vars": a.n * (ctx.world if part and a.config != "c4" else 1),
+                     "nnz": a.nnz * (ctx.world if part and a.config != "c4" else 1),
+                     "hid": a.hids, "depth": a.depth,
+                     "parallelism": f"rowpart{ctx.world}" if part else "single"}
+    if part:
+        if a.config == "c4":
+            rec["config"]["n_cons"], rec["config"]["n_vars"], rec["config"]["nnz"] = \
+                job.spec.m, job.spec.n, job.spec.nnz
+        exch = partition.time_exchange(job.batch.edge_index.ex, a.hids, ctx.dev)
+        exch.update(halo_rows=int(job.plan.halo.shape[0]), owned_vars=job.plan.n_own,
+                    boundary_vars_global=job.plan.n_boundary_global)
+        rec["exchange"] = {"per_rank": ctx.gather(exch),
+                           "note": "standalone F=hid owner-reduce / halo-broadcast of [n_local, F] fp32 rows "
+                                   "(median ms, barrier + sync around each); in the step they run async under "
+                                   "independent compute"}
+        if a.config == "c4" and ctx.world > 1 and a.rho_sweep:  # after the timed region
+            rec["exchange"]["rho_sweep"] = partition.rho_sweep(a, ctx.rank, ctx.world,
+                                                               [float(r) for r in a.rho_sweep.split(",")], a.hids)
+        del job
+    del step
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return rec, g
+
+
+def run_inference(ctx, a, steps, warmup, fp16, with_cpu):
+    """The reference's timed eval path on one GPU (N=1): eval forward + inference_gnn per graph."""
+    step, g, nnz = one_gpu_job(a, ctx.dev, inference=True, fp16=fp16)
+    dt, kern, per_launch = timed(ctx, step, steps, warmup)
+    wl = workload_name(a)
+    rec = report(ctx, dt, kern, per_launch, steps=steps, hids=a.hids, local_nnz=nnz,
+                 esz=2 if (a.bf16 or fp16) else 4, traffic_key=wl,
+                 single_dirs={(a.m, a.n): "cons<-vars", (a.n, a.m): "vars<-cons"}, fp16=fp16, training=False)
+    rec["ms_per_graph"] = dt / steps * 1e3
+    rec["ms_per_step"] = rec["ms_per_graph"]
+    rec["workload"] = wl
+    rec["mode"] = ("inference: eval-mode model(batch) + inference_gnn (scripts/pred_basis.py:113-118)"
+                   + ("; --fp16: model.half() + batch_to(half=True) (val.py:269, utils.py:909-915)" if fp16 else ""))
+    if with_cpu and a.cpu_steps > 0:
+        cdt, threads = cpu_inference(g, a.hids, a.depth, a.cpu_steps, fp16=fp16)
+        rec["cpu_baseline"] = {"value": rec["value"] * dt / steps / cdt, "unit": "edges/s", "cores": threads,
+                               "kind": "port", "s_per_graph": cdt,
+                               "sample": f"{a.cpu_steps} eval forward(s) + inference_gnn of the same "
+                                         f"{a.config} graph after one untimed warm-up: oracle C spmm_cpu loop "
+                                         f"(OpenMP) + torch CPU GEMMs in fp32"
+                                         + (" with fp16-rounded storage" if fp16 else "")
+                                         + f", {cdt:.2f} s/graph"}
+    del step
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return rec, g
+
+
 def main():
     args = parse()
     if args.print_workload:
@@ -261,6 +544,8 @@ def main():
         sys.exit(self_launch(args))
     if args.inference and (args.gpus > 1 or args.partitioned):
         raise SystemExit("--inference times the one-GPU eval path (the reference's scripts/pred_basis.py)")
+    if args.config == "c5" and (args.gpus > 1 or args.partitioned):
+        raise SystemExit("c5 (bf16, configs[4]) is a one-GPU configuration")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -285,187 +570,64 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
             dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+    ctx = Ctx(rank, world, dev, backend if distributed else "none", distributed)
 
     import lpgnn
-    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
-    from lpgnn.timing import TIMER
-    from lpgnn.train import make_optimizer, train_step
 
-    exch = None
-    if not distributed:
-        if args.config == "c4":  # the whole c4 graph on one GPU
-            from lpgnn.partition import bench_spec
-
-            g = bench_spec(args, 1).full()
-        else:
-            g = synth.uniform_lp(args.m, args.n, args.nnz, seed=0)
-        adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
-        batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(dev), x_t=torch.from_numpy(g.x_t).to(dev),
-                               y_s=torch.from_numpy(g.y_s).to(dev), y_t=torch.from_numpy(g.y_t).to(dev),
-                               edge_index=adj, s_bs=g.m, t_bs=g.n)
-        torch.manual_seed(0)
-        model = GCN_FC(8, 8, hids=args.hids, depth=args.depth,
-                       compute_dtype=torch.bfloat16 if args.bf16 else torch.float32).to(dev)
-        if args.inference:
-            # the reference's timed path (scripts/pred_basis.py:113-118, 169-173): eval-mode
-            # model(batch) + inference_gnn on the concatenated logits (val.py:106-124, with its
-            # invariant checks), one graph per step
-            from lpgnn.val import inference_gnn
-
-            model.eval()
-
-            def step():
-                with torch.no_grad():
-                    lc, lv = model(batch)
-                    return inference_gnn(torch.cat((lc, lv), 0), g.m)
-        else:
-            opt, _ = make_optimizer(model)
-            step = lambda: train_step(model, batch, opt)
-        local_nnz = g.nnz
-        workload = workload_name(args)
-        parallelism = "single"
+    subs = [s for s in args.sub.split(",") if s] if not args.profile_only else []
+    g = None
+    if args.inference:
+        head, g = run_inference(ctx, args, args.steps, args.warmup, args.fp16, with_cpu=False)
+        family = args.config
     else:
-        from lpgnn import partition
-
-        job = partition.build_bench_job(args, rank, world, dev)
-        step, local_nnz, g = job.step, job.local_nnz, None
-        workload = job.workload
-        parallelism = f"rowpart{world}"
-        spec = job.spec
-
-    def sync():
-        torch.cuda.synchronize()
-        if distributed:
-            torch.distributed.barrier()
-            torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    sync()
-    TIMER.reset()
-    TIMER.enabled = True
-    tw0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    dt = time.perf_counter() - t0
-    if os.environ.get("LPGNN_TRACE_WINDOW"):  # the timed region on the profiler's clock (tools/trace_timeline.py)
-        print(f"TRACE_WINDOW rank={rank} boottime_ns={tw0} {time.clock_gettime_ns(time.CLOCK_BOOTTIME)}",
-              file=sys.stderr, flush=True)
-    TIMER.enabled = False
-    kern = TIMER.summary()
-    per_launch = TIMER.launches()
-    if distributed:  # the boundary exchange on its own, after the timed steps
-        exch = partition.time_exchange(job.batch.edge_index.ex, args.hids, dev)
-        exch.update(halo_rows=int(job.plan.halo.shape[0]), owned_vars=job.plan.n_own,
-                    boundary_vars_global=job.plan.n_boundary_global)
-        gathered = [None] * world
-        torch.distributed.all_gather_object(gathered, exch)
-        exch = {"per_rank": gathered,
-                "note": "standalone F=hid owner-reduce / halo-broadcast of [n_local, F] fp32 rows (median ms, "
-                        "barrier + sync around each); in the step they run async under independent compute"}
-        if args.config == "c4" and world > 1 and args.rho_sweep:  # after the timed region
-            exch["rho_sweep"] = partition.rho_sweep(args, rank, world,
-                                                    [float(r) for r in args.rho_sweep.split(",")], args.hids)
-
-    # hid-width SpMM launches (the metric's kernel) measured on their stream
-    hid_keys = [k for k in kern if k[0] == "spmm" and k[3] == args.hids]
-    launches = sum(kern[k][0] for k in hid_keys)
-    spmm_ms = sum(kern[k][1] for k in hid_keys)
-    nnz_of = lambda k: local_nnz  # every launch traverses the local graph's edges once
-    esz = 2 if args.bf16 else 4
-    bytes_total = sum(kern[k][0] * spmm_bytes(k[1], nnz_of(k), k[3], esz) for k in hid_keys)
-    # dense GEMMs of hidden width on the hand-written kernels (FC forward + x3 input and weight
-    # gradients; K >= hid): MFMA utilisation.  x3 = fp32 through the exact three-way bf16 split,
-    # 6 bf16 MFMA products per fp32 product, so its MFMA-bound peak is the dense bf16 peak / 6.
-    fc_keys = [k for k in kern if k[0] in ("fc", "wgrad") and k[3] >= args.hids and k[2] >= 64]
-    x3 = any(str(k[4]).endswith("x3") for k in fc_keys)
-    fc_flops = sum(kern[k][0] * 2.0 * k[1] * k[2] * k[3] for k in fc_keys)
-    fc_ms = sum(kern[k][1] for k in fc_keys)
-    fc_peak = BF16_MFMA_PEAK_TFLOPS if args.bf16 else (BF16_MFMA_PEAK_TFLOPS / 6 if x3 else FP32_MFMA_PEAK_TFLOPS)
-    fc_tf = fc_flops / (fc_ms / 1e3) / 1e12 if fc_ms > 0 else 0.0
-    edges_local = launches * local_nnz / args.steps  # per step
-    t = torch.tensor([dt], device=dev)
-    e = torch.tensor([edges_local], device=dev, dtype=torch.float64)
-    if distributed:
-        import torch.distributed as dist
-
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(e, op=dist.ReduceOp.SUM)
-    dt_max = t.item()
-    value = e.item() * args.steps / dt_max
-
-    achieved = bytes_total / (spmm_ms / 1e3) / 1e9 if spmm_ms > 0 else 0.0
-    per_launch_bytes = bytes_total / max(launches, 1)
-    traffic, traffic_src = load_pmc_traffic(workload)
+        family = f"{args.config} weak scaling (rho={args.rho})" if args.config != "c4" else f"c4 (rho={args.rho})"
+        head, g = run_config(ctx, args, args.steps, args.warmup, family)
+    workload = head.pop("workload")
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "local_rank": local, "device": str(dev), "name": props.name,
+          "pci": "%04x:%02x:%02x" % (getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", 0),
+                                     getattr(props, "pci_device_id", 0)),
+          "uuid": str(getattr(props, "uuid", ""))}
+    ranks = ctx.gather(me)
     if distributed and backend != "nccl":
         workload += f" [rehearsal: {world} ranks over {backend} sharing {torch.cuda.device_count()} GPU(s)]"
+    cfg = head.pop("config", None) or {"workload": workload, "n_cons": args.m, "n_vars": args.n, "nnz": args.nnz,
+                                       "hid": args.hids, "depth": args.depth, "parallelism": "single"}
+    cfg["workload"] = workload
     out = {
-        "metric": "edges/sec bipartite SpMM (hid=1024, depth=3) at 1/2/4/8 MI355X; % HBM roofline",
-        "value": value,
+        "metric": METRIC,
+        "value": head.pop("value"),
         "unit": "edges/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": dt_max / args.steps * 1e3,
+        "ms_per_step": head.pop("ms_per_step"),
         "higher_is_better": True,
         "scaling": "strong" if args.config == "c4" else "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if args.bf16 else "fp32",
-        "data": "synthetic (seeded uniform LP graph, LP feature layout; random-init GCN_FC weights)",
-        "config": {"workload": workload, "n_cons": spec.m if distributed else args.m,
-                   "n_vars": spec.n if distributed else args.n, "nnz": spec.nnz if distributed else args.nnz,
-                   "hid": args.hids, "depth": args.depth, "parallelism": parallelism},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("lpg spmm_bf16_rowslim / rowwave" if args.bf16 else "lpg spmm_f32_rowslim / rowwave")
-                               + " (F=hid, both directions, fwd+bwd)",
-                     "bytes_per_launch": per_launch_bytes,
-                     "avg_launch_ms": spmm_ms / max(launches, 1), "launches": launches,
-                     "traffic_source": traffic_src},
-        "fc_roofline": {"bound": "mfma", "achieved": fc_tf, "peak": fc_peak, "unit": "TFLOP/s",
-                        "frac": fc_tf / fc_peak, "launches": sum(kern[k][0] for k in fc_keys),
-                        "kernel": ("lpg fc_bf16 + wgrad_bf16 (hidden-width GEMMs, fwd + bwd: FC forward, input "
-                                   "gradients on the FC kernel, weight gradients)" if args.bf16 else
-                                   "lpg fc_fwd_x3 + wgrad_x3 (hidden-width GEMMs, fwd + bwd; fp32 via exact "
-                                   "3-way bf16 split, peak = dense bf16 / 6)" if x3 else
-                                   "lpg fc_fwd_f32 (hidden GraphConv FC, fwd)"),
-                        "fp32_mfma_peak_frac": None if args.bf16 else fc_tf / FP32_MFMA_PEAK_TFLOPS,
-                        # the bf16 MFMA work these launches issue (x3: 6 bf16 products per fp32 product),
-                        # comparable with a plain bf16 GEMM's rate on this chip
-                        "bf16_mfma_equiv_tflops": fc_tf * (6 if x3 and not args.bf16 else 1)},
-        "spmm_directions": {
-            ("cons<-vars" if (k[1], k[2]) == (args.m, args.n) and not distributed else
-             "vars<-cons" if (k[1], k[2]) == (args.n, args.m) and not distributed else f"{k[1]}x{k[2]}"):
-            {"median_ms": float(np.median(v)), "launches": len(v),
-             "edges_per_s": local_nnz / (float(np.median(v)) / 1e3),
-             "roofline_frac": spmm_bytes(k[1], local_nnz, k[3], esz) / (float(np.median(v)) / 1e3) / 1e9
-             / HBM_PEAK_GBS}
-            for k, v in per_launch.items() if k[0] == "spmm" and k[3] == args.hids},
-        "spmm_edges_per_s_kernel": launches * local_nnz / (spmm_ms / 1e3) if spmm_ms > 0 else None,
-        "spmm_ms_per_step": spmm_ms / args.steps,
-        "kernels": {f"{k[0]}[{k[1]}x{k[2]},F={k[3]},{k[4]}]": {"launches": v[0], "ms": v[1]}
-                    for k, v in sorted(kern.items())},
-        "library": lpgnn.library_path(),
-        "max_hbm_allocated_gb": torch.cuda.max_memory_allocated(dev) / 1e9,
+        "dtype": "bf16" if args.bf16 else ("fp16" if args.fp16 else "fp32"),
+        "data": "synthetic (seeded uniform / block LP graphs, LP feature layout; random-init GCN_FC weights)",
+        "config": cfg,
+        "dist": {"backend": ctx.backend, "world_size": world, "ranks": ranks,
+                 "launcher": "torchrun / self-launched children" if distributed else "single process"},
     }
-    if exch is not None:
-        out["exchange"] = exch
-    if args.inference:
-        out["mode"] = "inference: eval-mode model(batch) + inference_gnn (scripts/pred_basis.py:113-118)"
-        out["ms_per_graph"] = out["ms_per_step"]
-    if (rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None
-            and args.inference):
-        cdt, threads = cpu_inference(g, args.hids, args.depth, args.cpu_steps)
-        out["cpu_baseline"] = {"value": edges_local / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
+    out.update(head)
+    out["library"] = lpgnn.library_path()
+    out["max_hbm_allocated_gb"] = torch.cuda.max_memory_allocated(dev) / 1e9
+    main_cpu = rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None
+    if main_cpu and args.inference:
+        cdt, threads = cpu_inference(g, args.hids, args.depth, args.cpu_steps, fp16=args.fp16)
+        out["cpu_baseline"] = {"value": out["value"] * out["ms_per_step"] / 1e3 / cdt, "unit": "edges/s",
+                               "cores": threads, "kind": "port", "s_per_step": cdt,
                                "sample": f"{args.cpu_steps} eval forward(s) + inference_gnn of the same "
                                          f"{args.config} graph after one untimed warm-up: oracle C spmm_cpu loop "
-                                         f"(OpenMP) + torch CPU GEMMs in fp32, {cdt:.2f} s/graph",
-                               "s_per_step": cdt}
-    elif rank == 0 and world == 1 and args.cpu_steps > 0 and not args.profile_only and g is not None and args.config == "c2":
+                                         f"(OpenMP) + torch CPU GEMMs in fp32"
+                                         + (" with fp16-rounded storage" if args.fp16 else "")
+                                         + f", {cdt:.2f} s/graph"}
+    elif main_cpu and args.config == "c2":
         cdt, threads = cpu_baseline(g, args.hids, args.depth, args.cpu_steps)
-        out["cpu_baseline"] = {"value": edges_local / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
+        edges_step = out["value"] * out["ms_per_step"] / 1e3
+        out["cpu_baseline"] = {"value": edges_step / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
                                "sample": f"{args.cpu_steps} full fwd+bwd+Adam step(s) of the same c2 workload after one "
                                          f"untimed warm-up step: "
                                          f"oracle C spmm_cpu loop (OpenMP) + torch CPU GEMMs, "
@@ -473,6 +635,27 @@ def main():
                                "s_per_step": cdt}
         out["cpu_spmm"] = dict(cpu_spmm(g, args.hids), threads=threads,
                                note="F=hid SpMM alone on the host, median of 3 (SURVEY.md 8d CPU numbers)")
+    del g
+    if args.inference:
+        out["mode"] = head.get("mode")
+        out["ms_per_graph"] = out["ms_per_step"]
+    # ---- sub-records: the same N, after the headline (its memory released) ----
+    if "c4" in subs and not args.inference and args.config != "c4":
+        a4 = c4_args(args)
+        rec, _ = run_config(ctx, a4, args.c4_steps, args.c4_warmup, f"c4 (rho={a4.rho})")
+        rec["scaling"] = "strong"
+        rec["steps"], rec["warmup"] = args.c4_steps, args.c4_warmup
+        rec["note"] = ("BASELINE.json configs[3] at this N: the whole graph on one GPU at N=1, constraint-row "
+                       "partitioned over the N ranks at N>1 (fixed total work); value = all ranks' F=hid SpMM "
+                       "edges / max-over-ranks time")
+        if distributed and backend != "nccl":
+            rec["workload"] += " [rehearsal over gloo]"
+        out["c4"] = rec
+    if "inference" in subs and not args.inference and world == 1 and not args.partitioned and args.config == "c2":
+        a_inf = copy.copy(args)
+        a_inf.inference = True
+        rec, _ = run_inference(ctx, a_inf, args.inf_steps, 3, False, with_cpu=rank == 0)
+        out["inference"] = rec
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

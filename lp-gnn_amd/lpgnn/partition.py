@@ -184,7 +184,7 @@ def _a2a_ids(send: np.ndarray, send_counts: list, group) -> tuple:
     return out.cpu().numpy(), recv_counts
 
 
-def plan_partition_blocks(spec, world: int, rank: int, group=None, edges=None) -> PartitionPlan:
+def plan_partition_blocks(spec, world: int, rank: int, group=None, edges=None, exchange: bool = True) -> PartitionPlan:
     """The plan of `rank` for a synth.BlockLP, built from the rank's OWN rows
     only (no global edge list): rank r holds row blocks [r*B/P, (r+1)*B/P)
     and owns the variables of the same blocks' variable ranges; its halo is
@@ -192,7 +192,8 @@ def plan_partition_blocks(spec, world: int, rank: int, group=None, edges=None) -
     variables with one all_to_all of id lists (the only O(halo) setup
     traffic).  Equal to plan_partition(global graph, bounds, block_owner)
     field for field (tests/test_partition.py).  `edges`: the rank's
-    (row, col, val) if already generated."""
+    (row, col, val) if already generated.  ``exchange=False``: no process group -- the local
+    CSR fields only (the receive lists stay empty, n_boundary_global = -1; tools/pmc_rank_share.py)."""
     per = _block_owner_ranges(spec.blocks, world)
     b0, b1 = rank * per, (rank + 1) * per
     row, col, val = edges if edges is not None else spec.rows(b0, b1)[:3]
@@ -206,7 +207,9 @@ def plan_partition_blocks(spec, world: int, rank: int, group=None, edges=None) -
     h_owner = (halo // spec.nb) // per
     send_counts = np.bincount(h_owner, minlength=world).tolist()
     send_idx = np.arange(owned.shape[0], local_vars.shape[0], dtype=np.int64)
-    if world > 1:
+    if world > 1 and not exchange:
+        recv_idx, recv_counts, n_boundary = np.empty(0, np.int64), [0] * world, -1
+    elif world > 1:
         got, recv_counts = _a2a_ids(halo, send_counts, group)
         recv_idx = got - v_lo
         # boundary = touched by >= 2 ranks (plan_partition's rule): an owned variable a remote rank

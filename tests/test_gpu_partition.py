@@ -159,22 +159,53 @@ def test_bench_partitioned_path_runs():
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
                LOCAL_RANK="0")
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--partitioned", "--steps", "2",
-                          "--warmup", "1", "--m", "20000", "--n", "40000", "--nnz", "400000", "--cpu-steps", "0"],
+                          "--warmup", "1", "--m", "20000", "--n", "40000", "--nnz", "400000", "--cpu-steps", "0",
+                          "--sub", ""],
                          capture_output=True, text=True, env=env, timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
     assert d["value"] > 0 and d["config"]["parallelism"].startswith("rowpart")
+    assert d["dist"]["backend"] == "nccl" and d["dist"]["world_size"] == 1
+
+
+@pytest.mark.timeout(900)
+def test_bench_two_ranks_share_gpu_line():
+    """`bench.py --gpus 2 --share-gpu` (self-launched gloo rehearsal) at reduced sizes: one JSON line
+    with the headline on the c2 weak-scaling family, the c4 sub-record at the same N (strong), the
+    roofline aggregated over both ranks, and the backend / world / per-rank devices recorded."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--share-gpu", "--steps", "2",
+                          "--warmup", "1", "--m", "10000", "--n", "20000", "--nnz", "200000", "--c4-scale", "40",
+                          "--c4-steps", "2", "--c4-warmup", "1", "--rho-sweep", "0,0.02"],
+                         capture_output=True, text=True, env=env, timeout=840)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
+    assert d["config"]["parallelism"] == "rowpart2" and d["config"]["n_cons"] == 20000
+    assert "c2 weak scaling" in d["config"]["workload"]
+    assert d["dist"]["backend"] == "gloo" and d["dist"]["world_size"] == 2 and len(d["dist"]["ranks"]) == 2
+    r = d["roofline"]
+    assert len(r["per_rank"]) == 2 and 0 < r["frac"] and r["peak_all_gpus"] == 2 * r["peak"]
+    c4 = d["c4"]
+    assert c4["scaling"] == "strong" and c4["config"]["parallelism"] == "rowpart2" and c4["value"] > 0
+    assert c4["config"]["nnz"] == 40_000_000 // 40
+    assert [s["rho"] for s in c4["exchange"]["rho_sweep"]] == [0.0, 0.02]
 
 
 # ------------------------------------------------- c4 (BASELINE.json configs[3]) on the HIP path
-def _c4_small():
+def _c4_small(scale=50):
     from lpgnn import synth
 
-    return synth.c4_spec(scale=50, seed=3)  # 40K x 80K, nnz 800K: the c4 generator at 1/50 size
+    return synth.c4_spec(scale=scale, seed=3)  # 1/50: 40K x 80K, nnz 800K -- the c4 generator reduced
 
 
-def _worker_c4(rank, world, port, out_dir, mode):
+def _worker_c4(rank, world, port, out_dir, mode, scale=50, hids=256):
     """c4's generator and its rank-local planner, HIP kernels on every rank (ranks share the GPU,
     gloo), against mode "oracle": the single-graph oracle evaluation (MKL fp32, the reference's
     arithmetic; dropout 0), or mode "dropout": the single-GPU HIP model in train mode with
@@ -189,13 +220,13 @@ def _worker_c4(rank, world, port, out_dir, mode):
         from oracle import model_ref as O
 
         dev = "cuda:0"
-        spec = _c4_small()
+        spec = _c4_small(scale)
         plan = part.plan_partition_blocks(spec, world, rank)
         assert plan.owned[-1] - plan.owned[0] + 1 == plan.n_own  # block plans: contiguous owners
         batch = part.make_block_batch(spec, plan, device=dev)
         dp = 0.1 if mode == "dropout" else 0.0
         torch.manual_seed(0)
-        model = GCN_FC(8, 8, hids=256, depth=3, dp=dp).to(dev).train()
+        model = GCN_FC(8, 8, hids=hids, depth=3, dp=dp).to(dev).train()
         sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
         torch.manual_seed(7)
         lc, lv = model(batch)
@@ -221,7 +252,7 @@ def _worker_c4(rank, world, port, out_dir, mode):
             b = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(dev), x_t=torch.from_numpy(g.x_t).to(dev),
                                y_s=torch.from_numpy(g.y_s).to(dev), y_t=torch.from_numpy(g.y_t).to(dev),
                                edge_index=adj, s_bs=g.m, t_bs=g.n)
-            ref = GCN_FC(8, 8, hids=256, depth=3, dp=dp).to(dev).train()
+            ref = GCN_FC(8, 8, hids=hids, depth=3, dp=dp).to(dev).train()
             ref.load_state_dict(sd0)
             torch.manual_seed(7)  # the same dropout seeds as the partitioned forward
             rc, rv = ref(b)
@@ -254,6 +285,14 @@ def test_c4_reduced_dropout_two_ranks_equal_one_gpu(tmp_path):
     """Train mode with dropout 0.1: N = 2 equals the one-GPU model within fp32 tolerance -- the
     dropout masks are keyed on global node ids, so both draw the same mask for every node."""
     mp.spawn(_worker_c4, args=(2, _free_port(), str(tmp_path), "dropout"), nprocs=2, join=True)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+
+
+@pytest.mark.timeout(900)
+def test_c4_reduced_two_ranks_hid1024_vs_oracle(tmp_path):
+    """The north-star width: c4 at 1/100 size, GCN_FC(8, 8, hids=1024, depth=3), 2 HIP ranks vs the
+    single-graph oracle (owned and halo logits within 1e-4, loss, every gradient)."""
+    mp.spawn(_worker_c4, args=(2, _free_port(), str(tmp_path), "oracle", 100, 1024), nprocs=2, join=True)
     assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
 
 

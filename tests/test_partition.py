@@ -93,13 +93,13 @@ def _cpu_knowledge(logit, feas, bound=10):
     return l
 
 
-def _c4_small():
+def _c4_small(scale=50):
     from lpgnn import synth
 
-    return synth.c4_spec(scale=50, seed=3)  # 40K x 80K, nnz 800K, the c4 generator at 1/50 size
+    return synth.c4_spec(scale=scale, seed=3)  # 1/50: 40K x 80K, nnz 800K -- the c4 generator reduced
 
 
-def _worker(rank, world, port, out_dir, mode="global"):
+def _worker(rank, world, port, out_dir, mode="global", scale=50, hids=16):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
@@ -114,7 +114,7 @@ def _worker(rank, world, port, out_dir, mode="global"):
         fc.knowledge = _cpu_knowledge
 
         if mode == "c4":  # each rank generates and plans only its own blocks
-            spec = _c4_small()
+            spec = _c4_small(scale)
             plan = part.plan_partition_blocks(spec, world, rank)
             batch = part.make_block_batch(spec, plan, device="cpu")
             g = spec.full()  # the single-graph reference below
@@ -124,7 +124,7 @@ def _worker(rank, world, port, out_dir, mode="global"):
             plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
             batch = part.make_local_batch(plan, g.x_s, g.x_t, g.y_s, g.y_t, device="cpu")
         torch.manual_seed(0)
-        model = GCN_FC(8, 8, hids=16, depth=4, dp=0.0)
+        model = GCN_FC(8, 8, hids=hids, depth=4, dp=0.0)
         sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
         model.train()
         lc, lv = model(batch)
@@ -145,9 +145,12 @@ def _worker(rank, world, port, out_dir, mode="global"):
         rloss = O.balanced(rc, rv, torch.from_numpy(g.y_s), torch.from_numpy(g.y_t))
         rloss.backward()
 
-        np.testing.assert_allclose(lc.detach().numpy(), rc.detach().numpy()[plan.row_lo:plan.row_hi], atol=2e-5)
+        # the owner reduce adds the halo partials in source-rank order (a re-association of each boundary
+        # variable's edge sum): fp32 rounding -- the north star's 1e-4 per logit (|logit| <= 20)
+        np.testing.assert_allclose(lc.detach().numpy(), rc.detach().numpy()[plan.row_lo:plan.row_hi], rtol=2e-5,
+                                   atol=1e-4)
         # owned AND halo rows agree with the full graph (halo = owners' values)
-        np.testing.assert_allclose(lv.detach().numpy(), rv.detach().numpy()[plan.local_vars], atol=2e-5)
+        np.testing.assert_allclose(lv.detach().numpy(), rv.detach().numpy()[plan.local_vars], rtol=2e-5, atol=1e-4)
         assert abs(tot.item() - rloss.item()) < 1e-4, (tot.item(), rloss.item())
         for k, p in model.named_parameters():
             np.testing.assert_allclose(p.grad.numpy(), params[k].grad.numpy(), rtol=1e-3, atol=1e-5, err_msg=k)
@@ -208,6 +211,18 @@ def test_c4_reduced_two_ranks_match_single_graph(tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), "c4"), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"ok{r}").exists()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_c4_reduced_world_4_8_match_single_graph(tmp_path, world):
+    """The N = 4 and N = 8 topologies of the c4 block planner (3 and 7 exchange peers per rank at
+    N = 8) at 1/200 size, hid 32, oracle local compute: rank-local plans == the global planner,
+    owned AND halo logits, the summed loss and every gradient == the single-graph oracle."""
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), "c4", 200, 32), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").exists()
+    # every rank exchanged with at least one other rank (the block LP has boundary variables)
+    assert all(int((tmp_path / f"ok{r}").read_text().split()[2]) > 0 for r in range(world))
 
 
 def _worker_rho(rank, world, port, out_dir):

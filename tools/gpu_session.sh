@@ -13,7 +13,6 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 STAGES="${*:-tests smoke bench prof}"
-TAG="${LPG_TAG:-r01}"
 
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 tmo=$2; shift 2
@@ -48,6 +47,14 @@ for s in $STAGES; do
         python "$ROOT/bench.py" --config c5 --steps 3 --warmup 2 --profile-only
       ;;
     kbench) step kbench 600 python tools/kbench.py ;;
+    rehearse8)  # the N = 8 topology: 8 self-launched ranks sharing the GPU over gloo, 1/10 sizes
+      step rehearse8 900 python bench.py --gpus 8 --share-gpu --steps 2 --warmup 1 --m 10000 --n 20000 \
+        --nnz 200000 --c4-scale 10 --c4-steps 2 --c4-warmup 1 ;;
+    rehearse2)
+      step rehearse2 900 python bench.py --gpus 2 --share-gpu --steps 3 --warmup 1 --c4-scale 10 ;;
+    pmc_rs) step pmc_rs 1200 bash tools/pmc_rank_shares.sh ;;
+    tests_part) step pytest_part 900 python -u -m pytest tests/test_gpu_partition.py -m gpu -x -v -p no:cacheprovider \
+        --timeout 900 --timeout-method thread ;;
     mfma) step mfma_peak 120 tools/experiments/mfma_peak 3 ;;  # sustained bf16 MFMA rate (build: see the source)
     kbfc) step kbench_fc 600 python tools/kbench.py fc ;;
     pmc)
