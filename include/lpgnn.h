@@ -136,6 +136,16 @@ lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx,
                                uint16_t *Y, int64_t ldy, int64_t F,
                                const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
                                void *stream);
+/* fp16 storage (the reference's --fp16 inference mode: model.half() and the batch's
+ * SparseTensor.half(), val.py:269, utils.py:909-915): X, Y fp16 bit patterns, edge values fp32 (holding
+ * the fp16-rounded values), fp32 accumulation in CSR edge order, one RNE rounding to fp16 per output
+ * (torch_sparse 0.6.12's CUDA spmm_sum accumulates in the storage type; the fp32 sum is the more
+ * accurate).  Layout rules, tuning and kernels as lpg_spmm_bf16(_tuned). */
+lpg_status lpg_spmm_f16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy, int64_t F,
+                        void *stream);
+lpg_status lpg_spmm_f16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy, int64_t F,
+                              const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh, int64_t slice_cols,
+                              int32_t depth, void *stream);
 
 /* ---- dense FC (replaces GraphConv's lin_rel + lin_root + ReLU) ----------- */
 
@@ -171,9 +181,11 @@ lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx,
  * rounds of the 32-bit lowbias32 mix) is >= dropout_p * 2^32, and kept
  * values are scaled by 1 / (1 - dropout_p).  The mask is never stored: the
  * kept set is exactly where the output is > 0.  The hash keys row m as
- * row_offset + m: a caller computing a slice of a larger node set (the row
- * partition, lpgnn/partition.py) passes the slice's first global node id, so
- * every node's mask is the one a single-GPU run would draw.
+ * row_keys[m] when row_keys != NULL (device int64 [M]: the global node id of
+ * every row, e.g. a partition's owned variables, which need not be
+ * contiguous), else as row_offset + m: a caller computing a slice of a larger
+ * node set (the row partition, lpgnn/partition.py) passes the slice's global
+ * ids, so every node's mask is the one a single-GPU run would draw.
  * Row-major fp32, leading dimensions in floats; A/W leading dimensions
  * multiples of 4, A/W 16-byte aligned; K1 and K2 multiples of 32 (zero-pad:
  * padded k are exact no-ops), except for the narrow-input kernel (4 <= K1,
@@ -190,7 +202,7 @@ lpg_status lpg_fc_f32(int64_t M, int64_t N,
                       int64_t K1, const float *A1, int64_t lda1, const float *W1, int64_t ldw1,
                       int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2,
                       const float *bias, float *C, int64_t ldc, int32_t flags,
-                      float dropout_p, uint64_t seed, int64_t row_offset, void *stream);
+                      float dropout_p, uint64_t seed, int64_t row_offset, const int64_t *row_keys, void *stream);
 
 /* fp32 FC on the bf16 matrix cores (same operation and epilogue as
  * lpg_fc_f32; also the input-gradient GEMMs dZ W of its backward, with W
@@ -210,7 +222,7 @@ lpg_status lpg_fc_x3_f32(int64_t M, int64_t N,
                          int64_t K1, const float *A1, int64_t lda1, const uint16_t *W1, int64_t ldw1, int64_t ps1,
                          int64_t K2, const float *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2,
                          const float *bias, float *C, int64_t ldc, int32_t flags,
-                         float dropout_p, uint64_t seed, int64_t row_offset, void *stream);
+                         float dropout_p, uint64_t seed, int64_t row_offset, const int64_t *row_keys, void *stream);
 
 /* The exact three-way bf16 split of an fp32 matrix for lpg_fc_x3_f32:
  * plane p of dst ([rows, cols], leading dimension ldd, plane p at
@@ -233,8 +245,8 @@ lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1
                                const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
                                int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
                                float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                               int64_t row_offset, int32_t hn, const float *hw, int64_t ldhw, const float *hb, float *logits,
-                               int64_t ldl, void *workspace, void *stream);
+                               int64_t row_offset, const int64_t *row_keys, int32_t hn, const float *hw, int64_t ldhw,
+                               const float *hb, float *logits, int64_t ldl, void *workspace, void *stream);
 
 /* Weight gradient on the same arithmetic: dW[n, k] = sum_r G[r, n] X[r, k]
  * (G = dZ [R, N], ldg; X = the layer input [R, K], ldx; dW [N, K], lddw, the
@@ -308,7 +320,14 @@ lpg_status lpg_relu_wgrad_smallk_f32(int64_t M, int64_t N, const float *g, int64
 lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1, const uint16_t *W1,
                        int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
                        const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                       int64_t row_offset, void *stream);
+                       int64_t row_offset, const int64_t *row_keys, void *stream);
+/* The same FC with fp16 storage (--fp16 inference, val.py:269): A/W/C fp16 bit patterns on
+ * v_mfma_f32_16x16x32_f16 (the bf16 kernels' tiles and epilogues), fp32 accumulation and bias,
+ * one RNE rounding to fp16 per output.  Arguments as lpg_fc_bf16. */
+lpg_status lpg_fc_f16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1, const uint16_t *W1,
+                      int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
+                      const float *bias, uint16_t *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                      int64_t row_offset, const int64_t *row_keys, void *stream);
 /* dst[c, r] = src[r, c] for bf16 [R, C] (R, C, lds, ldd multiples of 8, 16-byte
  * aligned): the transposed weights the c5 input gradients multiply by
  * (dX = dZ W of a Linear, arch.py:57-62 through train.py:128). */
@@ -386,6 +405,9 @@ lpg_status lpg_relu_wgrad_smallk_bf16(int64_t M, int64_t N, const uint16_t *g, i
  * zero-padded to 64 sums the same exact products in another order. */
 lpg_status lpg_linear_small_fwd_bf16(int64_t M, int64_t K, int64_t N, const uint16_t *H, int64_t ldh, const float *W,
                                      const float *bias, uint16_t *out, int64_t ldo, void *stream);
+/* ... with fp16 H / out (the --fp16 model's heads): out = RNE_fp16(fp32 sum + bias). */
+lpg_status lpg_linear_small_fwd_f16(int64_t M, int64_t K, int64_t N, const uint16_t *H, int64_t ldh, const float *W,
+                                    const float *bias, uint16_t *out, int64_t ldo, void *stream);
 
 /* The heads' backward in bf16, one pass over the layer output H [M, K] (bf16):
  *   dH[m, k] = RNE_bf16(sum_c G[m, c] W[c, k]); with mask != 0 through the
@@ -446,6 +468,10 @@ lpg_status lpg_weighted_ce_bwd_f32(int64_t M, int64_t C, const float *x, int64_t
 int64_t lpg_basis_labels_workspace_bytes(int64_t total);
 lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float *logits, int64_t ldl, int64_t *labels,
                                 void *workspace, void *stream);
+/* ... on fp16 logits (--fp16 inference): P computed in fp32 and rounded to fp16 (torch's half softmax
+ * stores it so); the selection and argmax see the fp16 values.  Same workspace. */
+lpg_status lpg_basis_labels_f16(int64_t total, int64_t m, const uint16_t *logits, int64_t ldl, int64_t *labels,
+                                void *workspace, void *stream);
 
 /* add_knowledge for one side (arch.py:129-141): out = normalize(logit) * 10,
  * then out[:,0] -= bound where feas[:, cols-3] != 0 (infinite lower bound)
@@ -454,6 +480,11 @@ lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float *logits, i
  * Bitwise torch-CPU F.normalize semantics (norm = sqrt(fma(x2,x2,fma(x1,x1,x0*x0)))). */
 lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t ldl, const float *feas, int64_t ldf,
                              int64_t feas_cols, float bound, float *out, int64_t ldo, void *stream);
+/* ... on fp16 logits / out (--fp16 inference: arch.py:129-141 in half precision), each stored
+ * intermediate rounded to fp16 as torch's half ops do: n = RNE16(sqrt(...)), d = max(n, 0),
+ * y = RNE16(RNE16(x / d) * 10), masked y = RNE16(y - bound).  feas fp32. */
+lpg_status lpg_knowledge_f16(int64_t M, const uint16_t *logit, int64_t ldl, const float *feas, int64_t ldf,
+                             int64_t feas_cols, float bound, uint16_t *out, int64_t ldo, void *stream);
 /* Its backward (autograd of F.normalize(x) * 10, arch.py:134-135; the bound subtractions pass g
  * through): dx = 10 (g / d - x (x . g) / d^3) where |x| > 1e-12, else 10 g / d (d = max(|x|, 1e-12)),
  * logit / g / dx [M, 3] with row strides ldl / ldg / lddx.  One pass instead of torch's ~12 kernels. */

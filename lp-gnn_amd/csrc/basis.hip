@@ -110,17 +110,34 @@ __device__ void block_hist(const uint32_t *__restrict__ keys, int64_t total, int
     if (lh[b]) atomicAdd(&h[b], lh[b]);
 }
 
-__global__ __launch_bounds__(kBT) void basis_keys(int64_t total, const float *__restrict__ logits, int64_t ldl,
+// F16: fp16 logits (the reference's --fp16 inference): softmax computed in fp32 and rounded to fp16,
+// as torch's half softmax stores it; the selection and the argmax then see the fp16 probabilities
+// (ties among them go to the lower index / to class 0, torch.argmax's first maximum)
+template <bool F16>
+__global__ __launch_bounds__(kBT) void basis_keys(int64_t total, const void *__restrict__ logits_v, int64_t ldl,
                                                   Ws w) {
   const int64_t i = (int64_t)blockIdx.x * kBT + threadIdx.x;
   if (i < total) {
-    const float *x = logits + i * ldl;
-    const float x0 = x[0], x1 = x[1], x2 = x[2];
+    float x0, x1, x2;
+    if constexpr (F16) {
+      const uint16_t *x = static_cast<const uint16_t *>(logits_v) + i * ldl;
+      x0 = (float)__builtin_bit_cast(_Float16, x[0]);
+      x1 = (float)__builtin_bit_cast(_Float16, x[1]);
+      x2 = (float)__builtin_bit_cast(_Float16, x[2]);
+    } else {
+      const float *x = static_cast<const float *>(logits_v) + i * ldl;
+      x0 = x[0], x1 = x[1], x2 = x[2];
+    }
     float mx = x0 > x1 ? x0 : x1;
     mx = x2 > mx ? x2 : mx;
     const float e0 = expf(x0 - mx), e1 = expf(x1 - mx), e2 = expf(x2 - mx);
     const float s = e0 + e1 + e2;
     float p0 = e0 / s, p1 = e1 / s, p2 = e2 / s;
+    if constexpr (F16) {
+      p0 = (float)(_Float16)p0;
+      p1 = (float)(_Float16)p1;
+      p2 = (float)(_Float16)p2;
+    }
     p0 = p0 != p0 ? 0.f : p0;  // pr[isnan(pr)] = 0
     p1 = p1 != p1 ? 0.f : p1;
     p2 = p2 != p2 ? 0.f : p2;
@@ -221,19 +238,20 @@ using namespace lpg;
 
 extern "C" int64_t lpg_basis_labels_workspace_bytes(int64_t total) { return total < 0 ? 0 : ws_bytes(total); }
 
-extern "C" lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float *logits, int64_t ldl, int64_t *labels,
+template <bool F16>
+static lpg_status basis_labels(int64_t total, int64_t m, const void *logits, int64_t ldl, int64_t *labels,
                                            void *workspace, void *stream) {
-  LPG_REQUIRE(total >= 0 && m >= 0 && m <= total, "lpg_basis_labels_f32: need 0 <= m <= total (m %lld, total %lld)",
+  LPG_REQUIRE(total >= 0 && m >= 0 && m <= total, "lpg_basis_labels: need 0 <= m <= total (m %lld, total %lld)",
               (long long)m, (long long)total);
   if (total == 0) return LPG_OK;
-  LPG_REQUIRE(logits && labels && workspace && ldl >= 3, "lpg_basis_labels_f32: NULL pointer or ldl < 3");
-  LPG_REQUIRE(aligned16(workspace), "lpg_basis_labels_f32: workspace not 16-byte aligned");
-  LPG_REQUIRE(total < ((int64_t)1 << 31), "lpg_basis_labels_f32: too many nodes");
+  LPG_REQUIRE(logits && labels && workspace && ldl >= 3, "lpg_basis_labels: NULL pointer or ldl < 3");
+  LPG_REQUIRE(aligned16(workspace), "lpg_basis_labels: workspace not 16-byte aligned");
+  LPG_REQUIRE(total < ((int64_t)1 << 31), "lpg_basis_labels: too many nodes");
   hipStream_t s = as_stream(stream);
   const Ws w = carve(workspace, total);
   const unsigned nb = (unsigned)((total + kBT - 1) / kBT);
   LPG_HIP(hipMemsetAsync(w.h1, 0, 4 * (kB1 + kB2 + kB3), s));
-  hipLaunchKernelGGL(basis_keys, dim3(nb), dim3(kBT), 0, s, total, logits, ldl, w);
+  hipLaunchKernelGGL(basis_keys<F16>, dim3(nb), dim3(kBT), 0, s, total, logits, ldl, w);
   if (m > 0) {
     hipLaunchKernelGGL(basis_pass2, dim3(nb), dim3(kBT), 0, s, total, m, w);
     hipLaunchKernelGGL(basis_pass3, dim3(nb), dim3(kBT), 0, s, total, w);
@@ -243,4 +261,16 @@ extern "C" lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float
   hipLaunchKernelGGL(basis_labels, dim3(nb), dim3(kBT), 0, s, total, (int32_t)(m > 0), w, labels);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
+}
+
+extern "C" lpg_status lpg_basis_labels_f32(int64_t total, int64_t m, const float *logits, int64_t ldl, int64_t *labels,
+                                           void *workspace, void *stream) {
+  return basis_labels<false>(total, m, logits, ldl, labels, workspace, stream);
+}
+
+// inference_gnn on fp16 logits (val.py:106-124 under the reference's --fp16: a half softmax); same
+// workspace as lpg_basis_labels_f32
+extern "C" lpg_status lpg_basis_labels_f16(int64_t total, int64_t m, const uint16_t *logits, int64_t ldl,
+                                           int64_t *labels, void *workspace, void *stream) {
+  return basis_labels<true>(total, m, logits, ldl, labels, workspace, stream);
 }

@@ -570,7 +570,10 @@ __global__ __launch_bounds__(kT) void linear_small_bwd_p2(int64_t nrow, int64_t 
 // sums the same exact bf16 x bf16 products in another order: tolerance, not bits.
 constexpr int kRowsPerWaveFwd = 4;
 
-template <int N, int KC>
+// F16: fp16 storage of H and out (the reference's --fp16 inference, val.py:269), same sums.
+__device__ __forceinline__ float f16_to_f32(uint32_t h) { return (float)__builtin_bit_cast(_Float16, (uint16_t)h); }
+
+template <bool F16, int N, int KC>
 __global__ __launch_bounds__(256) void linear_small_fwd_bf16(int64_t M, int64_t K, const uint16_t *__restrict__ H,
                                                              int64_t ldh, const float *__restrict__ W,
                                                              const float *__restrict__ bias,
@@ -617,7 +620,8 @@ __global__ __launch_bounds__(256) void linear_small_fwd_bf16(int64_t M, int64_t 
         const uint32_t hw[4] = {hv[r][kc].x, hv[r][kc].y, hv[r][kc].z, hv[r][kc].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float h0 = bf16_to_f32(hw[e] & 0xffffu), h1 = bf16_to_f32(hw[e] >> 16);
+          const float h0 = F16 ? f16_to_f32(hw[e] & 0xffffu) : bf16_to_f32(hw[e] & 0xffffu);
+          const float h1 = F16 ? f16_to_f32(hw[e] >> 16) : bf16_to_f32(hw[e] >> 16);
 #pragma unroll
           for (int c = 0; c < N; ++c)
             p[r][c] = __builtin_fmaf(h1, w[kc][c][2 * e + 1], __builtin_fmaf(h0, w[kc][c][2 * e], p[r][c]));
@@ -634,7 +638,9 @@ __global__ __launch_bounds__(256) void linear_small_fwd_bf16(int64_t M, int64_t 
     for (int r = 0; r < RW; ++r)
 #pragma unroll
       for (int c = 0; c < N; ++c)
-        if (lane == r * N + c && m0 + r < M) out[(m0 + r) * ldo + c] = (uint16_t)pk_bf16(p[r][c] + b[c], 0.f);
+        if (lane == r * N + c && m0 + r < M)
+          out[(m0 + r) * ldo + c] = F16 ? __builtin_bit_cast(uint16_t, (_Float16)(p[r][c] + b[c]))
+                                        : (uint16_t)pk_bf16(p[r][c] + b[c], 0.f);
   }
 }
 
@@ -945,10 +951,9 @@ extern "C" lpg_status lpg_heads_bwd_bf16(int64_t M, int64_t K, int64_t N, const 
 
 // The heads' forward in bf16: out[m, c] = RNE_bf16(sum_k H[m, k] W[c, k] + bias[c]), N <= 4,
 // K <= 2048 (W fp32 holding the bf16 model's values; out bf16 [M, N] with leading dim ldo).
-extern "C" lpg_status lpg_linear_small_fwd_bf16(int64_t M, int64_t K, int64_t N, const uint16_t *H, int64_t ldh,
-                                                const float *W, const float *bias, uint16_t *out, int64_t ldo,
-                                                void *stream) {
-  const char *what = "lpg_linear_small_fwd_bf16";
+template <bool F16>
+static lpg_status linear_small_fwd16(const char *what, int64_t M, int64_t K, int64_t N, const uint16_t *H, int64_t ldh,
+                                     const float *W, const float *bias, uint16_t *out, int64_t ldo, void *stream) {
   LPG_REQUIRE(M >= 0 && K >= 8 && K <= 2048 && K % 8 == 0 && N >= 1 && N <= kSmallNMax,
               "%s: need 1 <= N <= %d and 8 <= K <= 2048, K %% 8 == 0", what, kSmallNMax);
   if (M == 0) return LPG_OK;
@@ -960,7 +965,7 @@ extern "C" lpg_status lpg_linear_small_fwd_bf16(int64_t M, int64_t K, int64_t N,
   const int kc = (int)((K + 511) / 512);
   hipStream_t s = as_stream(stream);
 #define LPG_LF(NN, KC) \
-  hipLaunchKernelGGL((linear_small_fwd_bf16<NN, KC>), dim3((unsigned)blocks), dim3(256), 0, s, M, K, H, ldh, W, bias, out, ldo)
+  hipLaunchKernelGGL((linear_small_fwd_bf16<F16, NN, KC>), dim3((unsigned)blocks), dim3(256), 0, s, M, K, H, ldh, W, bias, out, ldo)
 #define LPG_LFN(NN)          \
   switch (kc) {              \
     case 1: LPG_LF(NN, 1); break; \
@@ -978,4 +983,18 @@ extern "C" lpg_status lpg_linear_small_fwd_bf16(int64_t M, int64_t K, int64_t N,
 #undef LPG_LF
   LPG_HIP(hipGetLastError());
   return LPG_OK;
+}
+
+extern "C" lpg_status lpg_linear_small_fwd_bf16(int64_t M, int64_t K, int64_t N, const uint16_t *H, int64_t ldh,
+                                                const float *W, const float *bias, uint16_t *out, int64_t ldo,
+                                                void *stream) {
+  return linear_small_fwd16<false>("lpg_linear_small_fwd_bf16", M, K, N, H, ldh, W, bias, out, ldo, stream);
+}
+
+// ... and with fp16 H / out (the --fp16 model's heads, lin_left / lin_right, arch.py:190): W, bias fp32 holding
+// the fp16 model's values; out = RNE_fp16 of the fp32 sum + bias
+extern "C" lpg_status lpg_linear_small_fwd_f16(int64_t M, int64_t K, int64_t N, const uint16_t *H, int64_t ldh,
+                                               const float *W, const float *bias, uint16_t *out, int64_t ldo,
+                                               void *stream) {
+  return linear_small_fwd16<true>("lpg_linear_small_fwd_f16", M, K, N, H, ldh, W, bias, out, ldo, stream);
 }

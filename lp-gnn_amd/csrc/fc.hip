@@ -65,14 +65,16 @@ struct FcArgs {
   // flags bit 1: C holds an addend on entry, C = act(A1 W1^T + A2 W2^T + C + bias);
   // each element is read and rewritten by the lane that owns it
   int32_t accum;
-  // the dropout key of row m is row_off + m (the global node id when C holds a slice of the rows)
+  // the dropout key of row m is row_keys[m] if given, else row_off + m (the global node id when C holds
+  // a slice of the rows; drop_row, fc_common.h)
   int64_t row_off;
+  const int64_t *row_keys;
 };
 
 __device__ __forceinline__ float epilogue(const FcArgs &a, float v, float b, int64_t row, int64_t col, bool relu) {
   if (a.bias) v = v + b;
   if (relu) v = (v < 0.f) ? 0.f : v;
-  if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+  if (a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
   return v;
 }
 
@@ -301,6 +303,35 @@ __global__ __launch_bounds__(256) void knowledge_f32(int64_t M, const float *__r
   out[m * ldo + 2] = y2;
 }
 
+// add_knowledge on fp16 logits (the reference's --fp16 inference: model.half() makes the heads' outputs
+// fp16 and arch.py:129-141 runs in half precision), every stored intermediate rounded to fp16 as torch's
+// half ops do (each computes in fp32 and rounds once):
+//   n = RNE16(sqrt(fma(x2, x2, fma(x1, x1, x0 * x0))))   (x.norm(dim=1), fp32 accumulation)
+//   d = max(n, RNE16(1e-12) = 0)                        (clamp_min(eps) of a half tensor)
+//   y = RNE16(RNE16(x / d) * 10)                         (F.normalize(x) * 10)
+//   y0 = RNE16(y0 - bound) where feas[:, -3] != 0; y2 likewise where feas[:, -1] != 0
+// (a zero row gives 0 / 0 = NaN, as torch's half path does -- the reference's own comment at arch.py:133).
+__device__ __forceinline__ float rne16(float v) { return (float)(_Float16)v; }
+
+__global__ __launch_bounds__(256) void knowledge_f16(int64_t M, const uint16_t *__restrict__ logit, int64_t ldl,
+                                                     const float *__restrict__ feas, int64_t ldf, int64_t fcols,
+                                                     float bound, uint16_t *__restrict__ out, int64_t ldo) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  float x[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) x[c] = (float)__builtin_bit_cast(_Float16, logit[m * ldl + c]);
+  const float nrm = rne16(sqrtf(__builtin_fmaf(x[2], x[2], __builtin_fmaf(x[1], x[1], x[0] * x[0]))));
+  const float d = nrm > 0.f ? nrm : 0.f;
+  float y[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) y[c] = rne16(rne16(x[c] / d) * 10.f);
+  if (feas[m * ldf + fcols - 3] != 0.f) y[0] = rne16(y[0] - bound);
+  if (feas[m * ldf + fcols - 1] != 0.f) y[2] = rne16(y[2] - bound);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) out[m * ldo + c] = __builtin_bit_cast(uint16_t, (_Float16)y[c]);
+}
+
 // backward of y = normalize(x) * 10 (the mask subtractions have unit derivative), torch autograd's
 // formula for F.normalize (arch.py:134-135):
 //   dx = 10 (g / d - x (x . g) / d^3) where n > 1e-12, else 10 g / d   (d = max(n, 1e-12))
@@ -425,7 +456,7 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
       if (col_ok) {
         for (int64_t m = r0; m < r1; ++m) {
           const float *xr = xb + (m - r0) * KT;
-          const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + m) : 0u;
+          const uint32_t rk = DROP ? drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, m, a.M)) : 0u;
           float o[4];
           // columns in pairs: one v_pk_fma_f32 advances two independent chains
           // (a true fma per element -- the same bits as the scalar chains)
@@ -522,7 +553,7 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
                                  int64_t ldw1, int64_t K2, const float *A2, int64_t lda2, const float *W2,
                                  int64_t ldw2, const float *bias, float *C, int64_t ldc, int32_t flags,
                                  float dropout_p, uint64_t seed, int64_t row_offset,
-                                 void *stream) {
+                                 const int64_t *row_keys, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_f32: negative size");
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_f32: bad C/ldc");
@@ -535,7 +566,7 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
   LPG_REQUIRE((flags & ~3) == 0, "lpg_fc_f32: unknown flags 0x%x", flags);
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
   FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1,
-           row_offset};
+           row_offset, row_keys};
   if (dropout_p > 0.f) {
     const double th = (double)dropout_p * 4294967296.0;
     a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);
@@ -589,6 +620,18 @@ extern "C" lpg_status lpg_knowledge_f32(int64_t M, const float *logit, int64_t l
   LPG_REQUIRE(logit && feas && out, "lpg_knowledge_f32: NULL pointer");
   LPG_REQUIRE(ldl >= 3 && ldo >= 3 && feas_cols >= 3 && ldf >= feas_cols, "lpg_knowledge_f32: bad shapes");
   hipLaunchKernelGGL(knowledge_f32, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, as_stream(stream), M, logit,
+                     ldl, feas, ldf, feas_cols, bound, out, ldo);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_knowledge_f16(int64_t M, const uint16_t *logit, int64_t ldl, const float *feas, int64_t ldf,
+                                        int64_t feas_cols, float bound, uint16_t *out, int64_t ldo, void *stream) {
+  LPG_REQUIRE(M >= 0, "lpg_knowledge_f16: M < 0");
+  if (M == 0) return LPG_OK;
+  LPG_REQUIRE(logit && feas && out, "lpg_knowledge_f16: NULL pointer");
+  LPG_REQUIRE(ldl >= 3 && ldo >= 3 && feas_cols >= 3 && ldf >= feas_cols, "lpg_knowledge_f16: bad shapes");
+  hipLaunchKernelGGL(knowledge_f16, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, as_stream(stream), M, logit,
                      ldl, feas, ldf, feas_cols, bound, out, ldo);
   LPG_HIP(hipGetLastError());
   return LPG_OK;

@@ -53,10 +53,10 @@ struct FcB16Args {
   const uint16_t *my;
   int64_t ldy;
   float mscale;
-  int64_t row_off;  // the dropout key of row m is row_off + m
+  int64_t row_off;  // the dropout key of row m is row_keys[m] if given, else row_off + m (drop_row)
+  const int64_t *row_keys;
 };
 
-__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
 __device__ __forceinline__ uint16_t to_bf16_rne(float f) {
   uint32_t u = __float_as_uint(f);
@@ -66,6 +66,42 @@ __device__ __forceinline__ uint16_t to_bf16_rne(float f) {
 }
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// The 16-bit storage type of a kernel instance: bf16 (the c5 path) or fp16 (the reference's --fp16
+// inference mode, val.py:269: model.half()).  Same layouts, tiles and epilogues; only the MFMA
+// (v_mfma_f32_16x16x32_bf16 / _f16, the same operand layout and rate on gfx950) and the conversions
+// differ.  lo / hi: element 0 / 1 of a packed pair; pack: RNE of a pair (v_cvt_pk_bf16_f32 /
+// v_cvt_pk_f16_f32); rne: RNE of one value.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+struct EBf16 {
+  static constexpr bool kBf16 = true;
+  typedef bf16x8 v8;
+  __device__ static __forceinline__ float lo(uint32_t w) { return __uint_as_float(w << 16); }
+  __device__ static __forceinline__ float hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+  __device__ static __forceinline__ uint32_t pack(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+  }
+  __device__ static __forceinline__ uint16_t rne(float f) { return to_bf16_rne(f); }
+  __device__ static __forceinline__ f32x4 mma(v8 a, v8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+struct EF16 {
+  static constexpr bool kBf16 = false;
+  typedef f16x8 v8;
+  __device__ static __forceinline__ float lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)w); }
+  __device__ static __forceinline__ float hi(uint32_t w) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+  }
+  __device__ static __forceinline__ uint32_t pack(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, f16x2));
+  }
+  __device__ static __forceinline__ uint16_t rne(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+  __device__ static __forceinline__ f32x4 mma(v8 a, v8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
 
 // The folded ReLU/dropout backward on 8 stored bf16 values: relu_bwd_pk_bf16 (fc_common.h) per
 // pair -- the arithmetic and instructions of lpg_relu_bwd_colsum_bf16, so the same bits.
@@ -93,7 +129,7 @@ __device__ __forceinline__ void load_mask_rows(const FcB16Args &a, int lane, int
 // Epilogue shared by the bf16 FC kernels: wave `wave` owns the FM*16 x FN*16
 // output block at (wrow0, wcol0); C/D map of 16x16x32: col = lane & 15, row =
 // 4 * (lane >> 4) + r.  `smem` must be free (every wave past its last tile read).
-template <int FM, int FN, bool RELU>
+template <class E, int FM, int FN, bool RELU>
 __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[FM][FN], unsigned char *smem,
                                               int wave, int lane, int64_t wrow0, int64_t wcol0) {
   constexpr int EP_PITCH = FN * 16 * 2 + 16;  // epilogue image row pitch (bytes, 16-B aligned)
@@ -120,29 +156,38 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
     }
     // the element loop with the addend / dropout choices made once (uniform branches per element
     // cost more than the arithmetic), RNE to bf16 in pairs by v_cvt_pk_bf16_f32
+    // rows outer, columns inner: a row's dropout key (drop_row: possibly a load) is made once and dies
+    // after its FN columns; the bias and column keys of the lane's FN columns stay in registers
+    float bb[FN];
+    uint32_t ck[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t col = wcol0 + j * 16 + fr;
+      bb[j] = (a.bias && col < a.N) ? a.bias[col] : 0.f;
+      ck[j] = drop_col_key(col);
+    }
     auto body = [&](auto acc_c, auto drop_c) {
       constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int64_t col = wcol0 + j * 16 + fr;
-        const float bb = (a.bias && col < a.N) ? a.bias[col] : 0.f;
+      for (int i = 0; i < FM; ++i) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          float v[4];
+        for (int r = 0; r < 4; r += 2) {
+          const int lr = i * 16 + fq * 4 + r;
+          const uint32_t rk0 = DROP ? drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, wrow0 + lr, a.M)) : 0u;
+          const uint32_t rk1 = DROP ? drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, wrow0 + lr + 1, a.M)) : 0u;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int lr = i * 16 + fq * 4 + r;
-            v[r] = acc[i][j][r];
-            if constexpr (ACC)
-              v[r] = v[r] + bf16_to_f32(*reinterpret_cast<const uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2));
-            v[r] = v[r] + bb;
-            if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
-            if constexpr (DROP) v[r] = drop_hash(a.seed, a.row_off + wrow0 + lr, col) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
-          }
+          for (int j = 0; j < FN; ++j) {
+            float v[2];
 #pragma unroll
-          for (int r = 0; r < 4; r += 2) {
-            const int lr = i * 16 + fq * 4 + r;
-            const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[r], v[r + 1]}, bf16x2));
+            for (int h = 0; h < 2; ++h) {
+              v[h] = acc[i][j][r + h];
+              if constexpr (ACC)
+                v[h] = v[h] + E::lo(*reinterpret_cast<const uint16_t *>(img + (lr + h) * EP_PITCH + (j * 16 + fr) * 2));
+              v[h] = v[h] + bb[j];
+              if (RELU) v[h] = v[h] < 0.f ? 0.f : v[h];
+              if constexpr (DROP) v[h] = drop_hash_k(h ? rk1 : rk0, ck[j]) >= a.drop_thresh ? v[h] * a.drop_scale : 0.f;
+            }
+            const uint32_t pk = E::pack(v[0], v[1]);
             *reinterpret_cast<uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2) = (uint16_t)pk;
             *reinterpret_cast<uint16_t *>(img + (lr + 1) * EP_PITCH + (j * 16 + fr) * 2) = (uint16_t)(pk >> 16);
           }
@@ -159,7 +204,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
     }
     constexpr int SIT = FM * 16 * CPR / 64;
     uint4 yv[SIT];
-    if (a.my) load_mask_rows<SIT, CPR>(a, lane, wrow0, wcol0, yv);  // all in flight before the first use
+    if (E::kBf16 && a.my) load_mask_rows<SIT, CPR>(a, lane, wrow0, wcol0, yv);  // all in flight before the first use
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -169,7 +214,9 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
       const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
       uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
       if (row < a.M && col < a.N) {
-        if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
+        if constexpr (E::kBf16) {  // (the folded ReLU backward: bf16 training only)
+          if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
+        }
         *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
       }
     }
@@ -187,11 +234,11 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
         const int64_t row = wrow0 + i * 16 + fq * 4 + r;
         if (row >= a.M) continue;
         float v = acc[i][j][r];
-        if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
+        if (a.accum) v = v + E::lo(a.C[row * a.ldc + col]);
         v = v + bb;
         if (RELU) v = v < 0.f ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-        a.C[row * a.ldc + col] = to_bf16_rne(v);
+        if (a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        a.C[row * a.ldc + col] = E::rne(v);
       }
     }
   }
@@ -203,7 +250,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
 // 8-byte store (and loads a 4-wide addend the same way) -- no LDS image, no barrier, and the
 // dropout row key is computed once per fragment row.  Same arithmetic per element as
 // epilogue_bf16 (addend, + bias (0 without one), ReLU, dropout, RNE), so the same bits.
-template <int FM, int FN, bool RELU>
+template <class E, int FM, int FN, bool RELU>
 __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)[FM][FN], int lane, int64_t wrow0,
                                                 int64_t wcol0) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -239,7 +286,7 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
 #pragma unroll
         for (int ii = 0; ii < IH; ++ii) {
           const int i = h * IH + ii;
-          const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + wrow0 + i * 16 + fr) : 0u;
+          const uint32_t rk = DROP ? drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, wrow0 + i * 16 + fr, a.M)) : 0u;
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
             float v[4];
@@ -248,14 +295,14 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
               v[r] = acc[i][j][r];
               if constexpr (ACC) {
                 const uint32_t w = r < 2 ? ad[ii][j].x : ad[ii][j].y;
-                v[r] = v[r] + __uint_as_float((r & 1) ? (w & 0xffff0000u) : (w << 16));
+                v[r] = v[r] + ((r & 1) ? E::hi(w) : E::lo(w));
               }
               v[r] = v[r] + bb[j][r];
               if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
               if constexpr (DROP) v[r] = drop_hash_k(rk, ck[j][r]) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
             }
-            const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2));
-            const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2));
+            const uint32_t lo = E::pack(v[0], v[1]);
+            const uint32_t hi = E::pack(v[2], v[3]);
             *reinterpret_cast<uint2 *>(rp0 + i * 16 * a.ldc + j * 16) = uint2{lo, hi};
           }
         }
@@ -282,11 +329,11 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
         const int64_t col = c0 + j * 16 + r;
         if (col >= a.N) continue;
         float v = acc[i][j][r];
-        if (a.accum) v = v + bf16_to_f32(a.C[row * a.ldc + col]);
+        if (a.accum) v = v + E::lo(a.C[row * a.ldc + col]);
         v = v + (a.bias ? a.bias[col] : 0.f);
         if (RELU) v = v < 0.f ? 0.f : v;
-        if (RELU && a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-        a.C[row * a.ldc + col] = to_bf16_rne(v);
+        if (RELU && a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        a.C[row * a.ldc + col] = E::rne(v);
       }
   }
 }
@@ -295,13 +342,13 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
 // consecutive columns go to the image as one ds_write_b64 (ds_read_b64 for the addend) instead
 // of four 2-byte accesses, then the rows leave as 16-byte stores as in epilogue_bf16.  Image
 // pitch 144 B: the 64 lanes' 8-byte accesses of one (i, j) are bank-conflict free.
-template <int FM, int FN, bool RELU>
+template <class E, int FM, int FN, bool RELU>
 __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc)[FM][FN], unsigned char *smem,
                                                  int wave, int lane, int64_t wrow0, int64_t wcol0) {
   constexpr int EP_PITCH = FN * 16 * 2 + 16;
   const int fr = lane & 15, fq = lane >> 4;
   if (!(a.N % 8 == 0 && a.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(a.C) & 15) == 0)) {
-    epilogue_bf16_t<FM, FN, RELU>(a, acc, lane, wrow0, wcol0);  // its per-element path
+    epilogue_bf16_t<E, FM, FN, RELU>(a, acc, lane, wrow0, wcol0);  // its per-element path
     return;
   }
   unsigned char *img = smem + wave * (FM * 16 * EP_PITCH);
@@ -347,7 +394,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + wrow0 + i * 16 + fr) : 0u;
+      const uint32_t rk = DROP ? drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, wrow0 + i * 16 + fr, a.M)) : 0u;
       unsigned char *ip = img + (i * 16 + fr) * EP_PITCH + fq * 8;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -359,17 +406,17 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
           v[r] = acc[i][j][r];
           if constexpr (ACC) {
             const uint32_t w = r < 2 ? ad.x : ad.y;
-            v[r] = v[r] + __uint_as_float((r & 1) ? (w & 0xffff0000u) : (w << 16));
+            v[r] = v[r] + ((r & 1) ? E::hi(w) : E::lo(w));
           }
           v[r] = v[r] + bb[j][r];
           if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
           if constexpr (DROP) v[r] = drop_hash_k(rk, ck[j][r]) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
         }
-        const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2));
-        const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2));
+        const uint32_t lo = E::pack(v[0], v[1]);
+        const uint32_t hi = E::pack(v[2], v[3]);
         *reinterpret_cast<uint2 *>(ip + j * 32) = uint2{lo, hi};
       }
-      if (a.my) {
+      if (E::kBf16 && a.my) {
 #pragma unroll
         for (int u = 0; u < SPI; ++u)
           if (i * SPI + u < SIT) load_y(i * SPI + u);
@@ -386,7 +433,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (a.my) {  // masked: every chunk formed first (one wait for the mask rows), then the stores back to back
+  if (E::kBf16 && a.my) {  // masked: every chunk formed first (one wait for the mask rows), then the stores back to back
     uint4 v[SIT];
 #pragma unroll
     for (int it = 0; it < SIT; ++it) {
@@ -414,8 +461,9 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
 }
 
 // WM x WN waves, each owning FM x FN fragments of 16 x 16.
-template <int WM, int WN, int FM, int FN, bool RELU>
+template <class E, int WM, int WN, int FM, int FN, bool RELU>
 __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
+  typedef typename E::v8 v8;
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   constexpr int TILE_BYTES = (BM + BN) * BK * 2;  // one buffer: A tile then W tile
@@ -489,26 +537,26 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_fwd_bf16(FcB16Args a) {
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       const int chunk = s * 4 + fq;  // k = 32 s + 8 fq .. +7
-      bf16x8 av[FM], bv[FN];
+      v8 av[FM], bv[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * FM * 16 + i * 16 + fr;
-        av[i] = *reinterpret_cast<const bf16x8 *>(As + row * 128 + swz(row, chunk) * 16);
+        av[i] = *reinterpret_cast<const v8 *>(As + row * 128 + swz(row, chunk) * 16);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * FN * 16 + j * 16 + fr;
-        bv[j] = *reinterpret_cast<const bf16x8 *>(Bs + row * 128 + swz(row, chunk) * 16);
+        bv[j] = *reinterpret_cast<const v8 *>(Bs + row * 128 + swz(row, chunk) * 16);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = E::mma(av[i], bv[j], acc[i][j]);
     }
     __syncthreads();  // the DMA of tile t+1 has landed (vmcnt(0)) and every wave is done reading tile t
   }
 
-  epilogue_bf16<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+  epilogue_bf16<E, FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
 }
 
 // ---- pipelined kernel with buffer_load ... lds staging (the default) -------
@@ -552,8 +600,9 @@ __device__ uint64_t *lpg_probe_buf;
 #define LPG_PROBE(i) do { } while (0)
 #endif
 
-template <int WM, int WN, int FM, int FN, bool RELU>
+template <class E, int WM, int WN, int FM, int FN, bool RELU>
 __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
+  typedef typename E::v8 v8;
   constexpr bool SCHED = true, PRIO = true;
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
@@ -622,26 +671,26 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  auto rd = [&](int b, int s, bf16x8(&av)[FM], bf16x8(&bv)[FN]) {  // 32-k step s (0, 1) of buffer b
+  auto rd = [&](int b, int s, v8(&av)[FM], v8(&bv)[FN]) {  // 32-k step s (0, 1) of buffer b
     const unsigned char *As = smem + b * TILE_BYTES;
     const unsigned char *Bs = As + A_BYTES;
     const int chunk = s * 4 + fq;  // k = 32 s + 8 fq .. +7
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int row = wm * FM * 16 + i * 16 + fr;
-      av[i] = *reinterpret_cast<const bf16x8 *>(As + row * 128 + swz(row, chunk) * 16);
+      av[i] = *reinterpret_cast<const v8 *>(As + row * 128 + swz(row, chunk) * 16);
     }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int row = wn * FN * 16 + j * 16 + fr;
-      bv[j] = *reinterpret_cast<const bf16x8 *>(Bs + row * 128 + swz(row, chunk) * 16);
+      bv[j] = *reinterpret_cast<const v8 *>(Bs + row * 128 + swz(row, chunk) * 16);
     }
   };
-  auto mma = [&](const bf16x8(&av)[FM], const bf16x8(&bv)[FN]) {  // W x A^T (transposed fragments)
+  auto mma = [&](const v8(&av)[FM], const v8(&bv)[FN]) {  // W x A^T (transposed fragments)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int i = 0; i < FM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < FM; ++i) acc[i][j] = E::mma(bv[j], av[i], acc[i][j]);
   };
   auto barrier = [&]() {  // this wave's DMA landed and its fragment reads returned; then all waves
     __builtin_amdgcn_sched_barrier(0);
@@ -651,7 +700,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+  v8 a0[FM], b0[FN], a1[FM], b1[FN];
   if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the later-dispatched half (wave-uniform)
   if (nk > 0) {
     stage(0, 0);
@@ -705,7 +754,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   LPG_PROBE(2);
-  epilogue_bf16_ti<FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+  epilogue_bf16_ti<E, FM, FN, RELU>(a, acc, smem, wave, lane, m0 + wm * FM * 16, n0 + wn * FN * 16);
 #ifdef LPG_PHASE_PROBE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (probe build: the epilogue's stores done)
   LPG_PROBE(3);
@@ -938,7 +987,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_fold(int64_t N, int64_t K, int
   }
 }
 
-template <int WM, int WN, int FM, int FN>
+template <class E, int WM, int WN, int FM, int FN>
 lpg_status launch_bf16(FcB16Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   a.mt = (a.M + BM - 1) / BM;
@@ -946,14 +995,14 @@ lpg_status launch_bf16(FcB16Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_bf16: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_fwd_bf16<WM, WN, FM, FN, true>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_bf16<E, WM, WN, FM, FN, true>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_fwd_bf16<WM, WN, FM, FN, false>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((fc_fwd_bf16<E, WM, WN, FM, FN, false>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
 
-template <int WM, int WN, int FM, int FN>
+template <class E, int WM, int WN, int FM, int FN>
 lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   a.mt = (a.M + BM - 1) / BM;
@@ -961,9 +1010,9 @@ lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_bf16: grid too large");
   if (relu)
-    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, true>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((fc_bf16_p<E, WM, WN, FM, FN, true>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_bf16_p<WM, WN, FM, FN, false>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((fc_bf16_p<E, WM, WN, FM, FN, false>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -1003,6 +1052,7 @@ int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
 
 namespace lpg {
 namespace {
+template <class E>
 lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant);
 
 // dst[c, r] = src[r, c] for bf16 through a 64 x 64 LDS tile, 16-byte global accesses both ways
@@ -1039,11 +1089,11 @@ __global__ __launch_bounds__(256) void transpose_bf16(int64_t R, int64_t C, cons
 // [A1 | A2] are staged once in LDS as fp32, a thread's 4 columns of weights live in registers as
 // column pairs (v_pk_fma_f32); each output is one fp32 fma chain over the exact bf16 x bf16 products
 // of the A1 part, the A2 part's chain added to it, then epilogue_bf16's order: + addend, + bias,
-// ReLU, dropout (the shared mask hash, row key row_off + m), RNE to bf16.  The MFMA kernel sums the
+// ReLU, dropout (the shared mask hash, row key drop_row(m)), RNE to bf16.  The MFMA kernel sums the
 // same exact products in its own order, so the two agree to fp32 summation order (tolerance).
 constexpr int kSmallKRowsB = 64;
 
-template <int K1, int K2, bool RELU>
+template <class E, int K1, int K2, bool RELU>
 __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
   static_assert(K1 % 4 == 0 && K2 % 4 == 0 && K1 >= 4, "small-K kernel: K1, K2 multiples of 4");
   constexpr int KT = K1 + K2;
@@ -1066,7 +1116,7 @@ __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
   };
   auto store_x = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < AE; ++j) sx[buf][threadIdx.x + 256 * j] = bf16_to_f32(xr_next[j]);
+    for (int j = 0; j < AE; ++j) sx[buf][threadIdx.x + 256 * j] = E::lo(xr_next[j]);
   };
   const int64_t c = (int64_t)blockIdx.x * 1024 + (int64_t)threadIdx.x * 4;
   const bool col_ok = c < a.N;
@@ -1076,10 +1126,10 @@ __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
   for (int jp = 0; jp < 2; ++jp) {
 #pragma unroll
     for (int k = 0; k < K1; ++k)
-      wp1[jp][k] = f32x2{bf16_to_f32(a.W1[(cc + 2 * jp) * a.ldw1 + k]), bf16_to_f32(a.W1[(cc + 2 * jp + 1) * a.ldw1 + k])};
+      wp1[jp][k] = f32x2{E::lo(a.W1[(cc + 2 * jp) * a.ldw1 + k]), E::lo(a.W1[(cc + 2 * jp + 1) * a.ldw1 + k])};
 #pragma unroll
     for (int k = 0; k < K2; ++k)
-      wp2[jp][k] = f32x2{bf16_to_f32(a.W2[(cc + 2 * jp) * a.ldw2 + k]), bf16_to_f32(a.W2[(cc + 2 * jp + 1) * a.ldw2 + k])};
+      wp2[jp][k] = f32x2{E::lo(a.W2[(cc + 2 * jp) * a.ldw2 + k]), E::lo(a.W2[(cc + 2 * jp + 1) * a.ldw2 + k])};
     bp[jp] = a.bias ? f32x2{a.bias[cc + 2 * jp], a.bias[cc + 2 * jp + 1]} : f32x2{0.f, 0.f};
   }
   load_x(rb);
@@ -1102,7 +1152,7 @@ __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
           const float *xr = xb + (m - r0) * KT;
           uint2 add = make_uint2(0u, 0u);
           if constexpr (ACC) add = *reinterpret_cast<const uint2 *>(a.C + m * a.ldc + c);
-          const uint32_t rk = DROP ? drop_row_key(a.seed, a.row_off + m) : 0u;
+          const uint32_t rk = DROP ? drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, m, a.M)) : 0u;
           uint32_t out[2];
 #pragma unroll
           for (int jp = 0; jp < 2; ++jp) {
@@ -1117,7 +1167,7 @@ __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
             }
             if constexpr (ACC) {
               const uint32_t w = jp ? add.y : add.x;
-              t = t + f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+              t = t + f32x2{E::lo(w), E::hi(w)};
             }
             t = t + bp[jp];
 #pragma unroll
@@ -1127,7 +1177,7 @@ __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
               if constexpr (DROP) v = drop_hash_k(rk, ck[2 * jp + e]) >= a.drop_thresh ? v * a.drop_scale : 0.f;
               t[e] = v;
             }
-            out[jp] = __builtin_bit_cast(uint32_t, __builtin_convertvector(t, bf16x2));
+            out[jp] = E::pack(t[0], t[1]);
           }
           *reinterpret_cast<uint2 *>(a.C + m * a.ldc + c) = make_uint2(out[0], out[1]);
         }
@@ -1149,10 +1199,10 @@ __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
   }
 }
 
-template <int K1, int K2>
+template <class E, int K1, int K2>
 lpg_status launch_smallk_bf16(const FcB16Args &a, bool relu, hipStream_t s) {
   const int64_t ncg = (a.N + 1023) / 1024, chunks = (a.M + kSmallKRowsB - 1) / kSmallKRowsB;
-  auto kern = relu ? fc_smallk_bf16<K1, K2, true> : fc_smallk_bf16<K1, K2, false>;
+  auto kern = relu ? fc_smallk_bf16<E, K1, K2, true> : fc_smallk_bf16<E, K1, K2, false>;
   int64_t S = resident_blocks(kern, 256) / ncg;  // the resident blocks, shared by the column groups
   S = S < chunks ? S : chunks;
   S = S < 1 ? 1 : S;
@@ -1164,13 +1214,14 @@ lpg_status launch_smallk_bf16(const FcB16Args &a, bool relu, hipStream_t s) {
 
 // The small-K shapes (4 <= K1, K1 + K2 <= 16, multiples of 4; N, ldc multiples of 4, C 8-byte
 // aligned); false if not covered
+template <class E>
 bool try_smallk_bf16(const FcB16Args &a, bool relu, hipStream_t s, lpg_status *st) {
   if (a.K1 < 4 || a.K1 + a.K2 > 16 || a.K1 % 4 || a.K2 % 4 || a.N % 4 || a.ldc % 4 ||
       (reinterpret_cast<uintptr_t>(a.C) & 7))
     return false;
   if ((a.N + 1023) / 1024 >= 65536) return false;
   switch (a.K1 * 100 + a.K2) {
-#define LPG_SKB(X, Y) case X * 100 + Y: *st = launch_smallk_bf16<X, Y>(a, relu, s); return true;
+#define LPG_SKB(X, Y) case X * 100 + Y: *st = launch_smallk_bf16<E, X, Y>(a, relu, s); return true;
     LPG_SKB(4, 0) LPG_SKB(4, 4) LPG_SKB(4, 8) LPG_SKB(4, 12) LPG_SKB(8, 0) LPG_SKB(8, 4) LPG_SKB(8, 8)
     LPG_SKB(12, 0) LPG_SKB(12, 4) LPG_SKB(16, 0)
 #undef LPG_SKB
@@ -1189,31 +1240,53 @@ extern "C" lpg_status lpg_debug_set_probe(void *p) {
 }
 #endif
 
+template <class E>
+static lpg_status fc16_entry(const char *name, int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                  const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
+                                  const uint16_t *W2, int64_t ldw2, const float *bias, uint16_t *C, int64_t ldc,
+                                  int32_t flags, float dropout_p, uint64_t seed, int64_t row_offset,
+                                  const int64_t *row_keys, void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "%s: negative size", name);
+  if (M == 0 || N == 0) return LPG_OK;
+  LPG_REQUIRE(C != nullptr && ldc >= N, "%s: bad C/ldc", name);
+  LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1), "%s: bad A1/W1", name);
+  LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2), "%s: bad A2/W2", name);
+  const int kernel = (flags >> 8) & 15;
+  LPG_REQUIRE((flags & ~0xf03) == 0 && kernel <= kKernels, "%s: unknown flags 0x%x", name, flags);
+  LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "%s: dropout_p %g not in [0, 1)", name, (double)dropout_p);
+  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1,
+              nullptr, 0, 1.f, row_offset, row_keys};
+  dropout_params(dropout_p, &a.drop_thresh, &a.drop_scale);
+  lpg_status st;
+  if (try_smallk_bf16<E>(a, flags & 1, as_stream(stream), &st)) return st;  // conv1: narrow LP features
+  LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0,
+              "%s: K1, K2 must be multiples of %d (zero-pad) unless 4 <= K1, K1 + K2 <= 16 (multiples of 4) "
+              "and N, ldc are multiples of 4", name, BK);
+  LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
+                  (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
+              "%s: A/W must be 16-byte aligned with leading dimensions multiple of 8", name);
+  return fc_bf16_dispatch<E>(a, flags & 1, as_stream(stream), kernel);
+}
+
 extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
                                   const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
                                   const uint16_t *W2, int64_t ldw2, const float *bias, uint16_t *C, int64_t ldc,
                                   int32_t flags, float dropout_p, uint64_t seed, int64_t row_offset,
-                                  void *stream) {
-  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_bf16: negative size");
-  if (M == 0 || N == 0) return LPG_OK;
-  LPG_REQUIRE(C != nullptr && ldc >= N, "lpg_fc_bf16: bad C/ldc");
-  LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1), "lpg_fc_bf16: bad A1/W1");
-  LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2), "lpg_fc_bf16: bad A2/W2");
-  const int kernel = (flags >> 8) & 15;
-  LPG_REQUIRE((flags & ~0xf03) == 0 && kernel <= kKernels, "lpg_fc_bf16: unknown flags 0x%x", flags);
-  LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_bf16: dropout_p %g not in [0, 1)", (double)dropout_p);
-  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1,
-              nullptr, 0, 1.f, row_offset};
-  dropout_params(dropout_p, &a.drop_thresh, &a.drop_scale);
-  lpg_status st;
-  if (try_smallk_bf16(a, flags & 1, as_stream(stream), &st)) return st;  // conv1: narrow LP features
-  LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0,
-              "lpg_fc_bf16: K1, K2 must be multiples of %d (zero-pad) unless 4 <= K1, K1 + K2 <= 16 (multiples of 4) "
-              "and N, ldc are multiples of 4", BK);
-  LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
-                  (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
-              "lpg_fc_bf16: A/W must be 16-byte aligned with leading dimensions multiple of 8");
-  return fc_bf16_dispatch(a, flags & 1, as_stream(stream), kernel);
+                                  const int64_t *row_keys, void *stream) {
+  return fc16_entry<EBf16>("lpg_fc_bf16", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, bias, C, ldc, flags,
+                           dropout_p, seed, row_offset, row_keys, stream);
+}
+
+// fp16 storage (the reference's --fp16 inference: model.half(), batch_to(half=True); val.py:269,
+// utils.py:909-915): the bf16 entry's kernels on v_mfma_f32_16x16x32_f16, fp32 accumulation, fp32 bias,
+// one RNE rounding to fp16 per output
+extern "C" lpg_status lpg_fc_f16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                 const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
+                                 const uint16_t *W2, int64_t ldw2, const float *bias, uint16_t *C, int64_t ldc,
+                                 int32_t flags, float dropout_p, uint64_t seed, int64_t row_offset,
+                                 const int64_t *row_keys, void *stream) {
+  return fc16_entry<EF16>("lpg_fc_f16", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, bias, C, ldc, flags,
+                          dropout_p, seed, row_offset, row_keys, stream);
 }
 
 // The input gradient of a layer whose input went through the previous layer's ReLU + dropout,
@@ -1241,7 +1314,7 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, con
               "lpg_fc_bf16_relu_bwd: only the accumulate flag (2) and a kernel choice are accepted, got 0x%x", flags);
   FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, nullptr, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, 0, 0u, 1.f, (flags >> 1) & 1,
               Y, ldy, scale};
-  return fc_bf16_dispatch(a, false, as_stream(stream), kernel);  // (every kernel's epilogue takes the fold)
+  return fc_bf16_dispatch<EBf16>(a, false, as_stream(stream), kernel);  // (every kernel's epilogue takes the fold)
 }
 
 namespace lpg {
@@ -1255,11 +1328,13 @@ FcB16Args rows_from(const FcB16Args &a, int64_t r) {
   t.C = a.C + r * a.ldc;
   t.my = a.my ? a.my + r * a.ldy : nullptr;
   t.row_off = a.row_off + r;
+  t.row_keys = a.row_keys ? a.row_keys + r : nullptr;
   return t;
 }
 
+template <class E>
 lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
-  if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<2, 2, 4, 4>(a, relu, s);  // 128 x 128
+  if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<E, 2, 2, 4, 4>(a, relu, s);  // 128 x 128
   if ((kernel == 0 || kernel == 3) && p_ok(a)) {
     if (kernel == 0) {
       // The last round of 256 x 256 tiles (one block per CU) is usually partial: c5's 200 K rows are 24
@@ -1273,15 +1348,15 @@ lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
         if (full > 0 && tail > 0 && 2 * tail <= per_round) {
           FcB16Args h = a;
           h.M = full;
-          const lpg_status st = launch_bf16_p<2, 4, 8, 4>(h, relu, s);
+          const lpg_status st = launch_bf16_p<E, 2, 4, 8, 4>(h, relu, s);
           if (st != LPG_OK) return st;
-          return launch_bf16<2, 2, 4, 4>(rows_from(a, full), relu, s);
+          return launch_bf16<E, 2, 2, 4, 4>(rows_from(a, full), relu, s);
         }
       }
     }
-    return launch_bf16_p<2, 4, 8, 4>(a, relu, s);
+    return launch_bf16_p<E, 2, 4, 8, 4>(a, relu, s);
   }
-  return launch_bf16<2, 4, 8, 4>(a, relu, s);  // 256 x 256, BK 64, 2 buffers
+  return launch_bf16<E, 2, 4, 8, 4>(a, relu, s);  // 256 x 256, BK 64, 2 buffers
 }
 }  // namespace
 }  // namespace lpg

@@ -27,6 +27,13 @@ __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int64_t row, int64_
   return lowbias32(hr ^ ((uint32_t)col * 0x9e3779b9u) ^ (uint32_t)(seed >> 32));
 }
 
+// The dropout key of output row `row`: row_keys[row] when the caller gives one key per row (the
+// global node ids of a partition's rows, in any order) or row_off + row (a contiguous slice); rows at
+// or past M are never stored and key as row_off + row (no load past the key array).
+__device__ __forceinline__ int64_t drop_row(const int64_t *row_keys, int64_t row_off, int64_t row, int64_t M) {
+  return (row_keys != nullptr && row < M) ? row_keys[row] : row_off + row;
+}
+
 // drop_hash split into its row and column keys, for epilogues that hold a few rows and a few
 // columns per lane: drop_hash(seed, row, col) == drop_hash_k(drop_row_key(seed, row), drop_col_key(col))
 __device__ __forceinline__ uint32_t drop_row_key(uint64_t seed, int64_t row) {

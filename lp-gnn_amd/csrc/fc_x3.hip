@@ -73,8 +73,9 @@ struct X3Args {
   int64_t ldhw;
   int32_t hn;
   float *hpart;
-  int64_t row_off;  // the dropout key of row m is row_off + m (the global node id of a row slice)
+  int64_t row_off;  // the dropout key of row m is row_keys[m] if given, else row_off + m (drop_row)
   int32_t store;    // 0: C is not written (LPG_FC_HEADS_ONLY: the logits are the only output)
+  const int64_t *row_keys;
 };
 
 // dst plane p [rows, cols] (ldd) = term p of src (transposed: src is [cols, rows]).
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
         float v = acc[i][j][r];
         if (a.bias) v = v + bb;
         if (RELU) v = (v < 0.f) ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        if (a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         if (a.store) a.C[row * a.ldc + col] = v;
         if constexpr (HEADS) {
 #pragma unroll
@@ -552,7 +553,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) rk[i][r] = drop_row_key(a.seed, a.row_off + mw + i * 16 + 4 * fg + r);
+          for (int r = 0; r < 4; ++r) rk[i][r] = drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, mw + i * 16 + 4 * fg + r, a.M));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
           float v = acc[i][j][r];
           if (a.bias) v = v + bb;
           if (RELU) v = (v < 0.f) ? 0.f : v;
-          if (a.drop_thresh) v = drop_hash(a.seed, a.row_off + row, col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+          if (a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
           if (!HEADS || a.store) a.C[row * a.ldc + col] = v;
           hput(i, r, j, v);
         }
@@ -884,15 +885,9 @@ __global__ __launch_bounds__(256) void wgrad_fold(int64_t N, int64_t K, int64_t 
   *reinterpret_cast<float4 *>(dW + n * lddw + k) = acc;
 }
 
+// The R split of the x3 weight gradient: a function of the shape only (no environment or global
+// state), so a given (R, N, K) always folds its partials in the same order -- the same dW bits.
 int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
-  static const int64_t forced = [] {  // LPGNN_WGRAD_SPLITS: experiment knob (read once)
-    const char *e = getenv("LPGNN_WGRAD_SPLITS");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  if (forced > 0) {
-    const int64_t nch = (R + 31) / 32;
-    return forced < nch ? forced : (nch > 0 ? nch : 1);
-  }
   const int64_t tiles = ((N + WG_T - 1) / WG_T) * ((K + WG_T - 1) / WG_T);
   const int64_t nchunks = (R + 31) / 32;
   int64_t S = (2048 + tiles - 1) / tiles;  // aim at >= 2048 blocks (8 per CU)
@@ -932,7 +927,7 @@ static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int
                           const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
                           int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
                           float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                          int64_t row_offset, X3Args *out) {
+                          int64_t row_offset, const int64_t *row_keys, X3Args *out) {
   const bool heads_only = flags & LPG_FC_HEADS_ONLY;
   LPG_REQUIRE((C != nullptr || (heads_only && !(flags & LPG_FC_ACCUMULATE))) && ldc >= N, "lpg_fc_x3_f32: bad C/ldc");
   LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "lpg_fc_x3_f32: K1, K2 must be multiples of %d (zero-pad)", BK);
@@ -949,6 +944,7 @@ static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int
                 (flags >> 1) & 1};
   dropout_params(dropout_p, &out->drop_thresh, &out->drop_scale);
   out->row_off = row_offset;
+  out->row_keys = row_keys;
   out->store = heads_only ? 0 : 1;
   return LPG_OK;
 }
@@ -957,13 +953,13 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
                                     const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
                                     int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
                                     float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                                    int64_t row_offset, void *stream) {
+                                    int64_t row_offset, const int64_t *row_keys, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_f32: negative size");
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(!(flags & LPG_FC_HEADS_ONLY), "lpg_fc_x3_f32: LPG_FC_HEADS_ONLY needs the heads entry");
   X3Args a;
   const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
-                                dropout_p, seed, row_offset, &a);
+                                dropout_p, seed, row_offset, row_keys, &a);
   if (st != LPG_OK) return st;
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
@@ -980,7 +976,8 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
                                           const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
                                           int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2,
                                           const float *bias, float *C, int64_t ldc, int32_t flags, float dropout_p,
-                                          uint64_t seed, int64_t row_offset, int32_t hn, const float *hw,
+                                          uint64_t seed, int64_t row_offset, const int64_t *row_keys,
+                                          int32_t hn, const float *hw,
                                           int64_t ldhw, const float *hb,
                                           float *logits, int64_t ldl, void *workspace, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_heads_f32: negative size");
@@ -991,7 +988,7 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   LPG_REQUIRE(workspace && aligned16(workspace), "lpg_fc_x3_heads_f32: workspace missing or not 16-byte aligned");
   X3Args a;
   const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, bias, C, ldc, flags,
-                                dropout_p, seed, row_offset, &a);
+                                dropout_p, seed, row_offset, row_keys, &a);
   if (st != LPG_OK) return st;
   a.hw = hw;
   a.ldhw = ldhw;

@@ -353,12 +353,39 @@ __device__ __forceinline__ uint32_t f32_to_bf16_rne(float f) {
   return u >> 16;
 }
 
+// The 16-bit storage of a kernel instance: bf16 (c5) or fp16 (the reference's --fp16 inference,
+// val.py:269: SparseTensor.half() and model.half()).  lo / hi: element 0 / 1 of a packed pair as
+// fp32 (exact); pack: RNE of a pair; rne: RNE of one value.  The accumulation is fp32 either way,
+// rounded once per output (torch_sparse's CUDA spmm_sum accumulates in the storage type; the fp32
+// sum here is the more accurate one -- DESIGN.md §5).
+struct SBf16 {
+  __device__ static __forceinline__ float lo(uint32_t w) { return bf16_to_f32(w & 0xffffu); }
+  __device__ static __forceinline__ float hi(uint32_t w) { return bf16_to_f32(w >> 16); }
+  __device__ static __forceinline__ uint32_t pack(float a, float b) {
+    return f32_to_bf16_rne(a) | (f32_to_bf16_rne(b) << 16);
+  }
+  __device__ static __forceinline__ uint16_t rne(float f) { return (uint16_t)f32_to_bf16_rne(f); }
+};
+struct SF16 {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  __device__ static __forceinline__ float lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)w); }
+  __device__ static __forceinline__ float hi(uint32_t w) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+  }
+  __device__ static __forceinline__ uint32_t pack(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{a, b}, h2));
+  }
+  __device__ static __forceinline__ uint16_t rne(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+};
+
+template <class E>
 __device__ __forceinline__ void axpy8_bf16(float (&acc)[8], float v, const uint4 &x) {
   const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    acc[2 * i] = acc[2 * i] + v * bf16_to_f32(w[i] & 0xffffu);
-    acc[2 * i + 1] = acc[2 * i + 1] + v * bf16_to_f32(w[i] >> 16);
+    acc[2 * i] = acc[2 * i] + v * E::lo(w[i]);
+    acc[2 * i + 1] = acc[2 * i + 1] + v * E::hi(w[i]);
   }
 }
 
@@ -367,6 +394,7 @@ __device__ __forceinline__ void axpy8_bf16(float (&acc)[8], float v, const uint4
 // c0 + 128 w + 2 l, +1 (4-B gathers, 256 B per wave-instruction), 32 gathers in flight and the next
 // 64-edge chunk's indices prefetched -- 4x the waves on one long row's chain, each element still
 // summed in CSR order (the same bits).
+template <class E>
 __device__ __forceinline__ void spmm_bf16_heavy_row(int64_t row, int64_t c0, int wave,
                                                     const int64_t *__restrict__ rowptr,
                                                     const int32_t *__restrict__ col, const float *__restrict__ val,
@@ -403,8 +431,8 @@ __device__ __forceinline__ void spmm_bf16_heavy_row(int64_t row, int64_t c0, int
 #pragma unroll
       for (int k = 0; k < HU; ++k) {
         const float v = bcast_f(vl, j + k);
-        a0 = a0 + v * bf16_to_f32(xv[k] & 0xffffu);
-        a1 = a1 + v * bf16_to_f32(xv[k] >> 16);
+        a0 = a0 + v * E::lo(xv[k]);
+        a1 = a1 + v * E::hi(xv[k]);
       }
     }
     if (j < n) {
@@ -417,18 +445,18 @@ __device__ __forceinline__ void spmm_bf16_heavy_row(int64_t row, int64_t c0, int
       for (int k = 0; k < HU; ++k)
         if (k < rem) {
           const float v = bcast_f(vl, j + k);
-          a0 = a0 + v * bf16_to_f32(xv[k] & 0xffffu);
-          a1 = a1 + v * bf16_to_f32(xv[k] >> 16);
+          a0 = a0 + v * E::lo(xv[k]);
+          a1 = a1 + v * E::hi(xv[k]);
         }
     }
     e += n;
   }
-  if (ok) *reinterpret_cast<uint32_t *>(Y + row * ldy + cw) = f32_to_bf16_rne(a0) | (f32_to_bf16_rne(a1) << 16);
+  if (ok) *reinterpret_cast<uint32_t *>(Y + row * ldy + cw) = E::pack(a0, a1);
 }
 
 // Lane l holds columns c0 + q*512 + 8l .. +7 (16 bytes) for q < NV.  HEAVY (NV = 1): the launch's
 // leading blocks of plane 0 are heavy (row, 512-column) units, as in spmm_f32_rowwave.
-template <int NV, int U, bool FULL, bool HEAVY = false>
+template <class E, int NV, int U, bool FULL, bool HEAVY = false>
 __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
@@ -440,7 +468,7 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
     if ((int64_t)blockIdx.x < hb) {
       if (blockIdx.y != 0) return;
       const uint32_t hs = (uint32_t)hv.slices, bxu = blockIdx.x;
-      spmm_bf16_heavy_row(hv.rows[bxu / hs], (int64_t)(bxu % hs) * 512, wave, rowptr, col, val, X, ldx, Y, ldy, F);
+      spmm_bf16_heavy_row<E>(hv.rows[bxu / hs], (int64_t)(bxu % hs) * 512, wave, rowptr, col, val, X, ldx, Y, ldy, F);
       return;
     }
   }
@@ -482,7 +510,7 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
       for (int k = 0; k < U; ++k) {
         const float v = bcast_f(vl, j + k);
 #pragma unroll
-        for (int q = 0; q < NV; ++q) axpy8_bf16(acc[q], v, xv[k][q]);
+        for (int q = 0; q < NV; ++q) axpy8_bf16<E>(acc[q], v, xv[k][q]);
       }
     }
     for (; j < n; ++j) {
@@ -491,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
 #pragma unroll
       for (int q = 0; q < NV; ++q) {
         const uint4 xv = ok[q] ? *reinterpret_cast<const uint4 *>(xr + q * 512) : make_uint4(0, 0, 0, 0);
-        axpy8_bf16(acc[q], v, xv);
+        axpy8_bf16<E>(acc[q], v, xv);
       }
     }
     e += n;
@@ -501,10 +529,10 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
   for (int q = 0; q < NV; ++q) {
     if (!ok[q]) continue;
     uint4 o;
-    o.x = f32_to_bf16_rne(acc[q][0]) | (f32_to_bf16_rne(acc[q][1]) << 16);
-    o.y = f32_to_bf16_rne(acc[q][2]) | (f32_to_bf16_rne(acc[q][3]) << 16);
-    o.z = f32_to_bf16_rne(acc[q][4]) | (f32_to_bf16_rne(acc[q][5]) << 16);
-    o.w = f32_to_bf16_rne(acc[q][6]) | (f32_to_bf16_rne(acc[q][7]) << 16);
+    o.x = E::pack(acc[q][0], acc[q][1]);
+    o.y = E::pack(acc[q][2], acc[q][3]);
+    o.z = E::pack(acc[q][4], acc[q][5]);
+    o.w = E::pack(acc[q][6], acc[q][7]);
     *reinterpret_cast<uint4 *>(yr + q * 512) = o;
   }
 }
@@ -513,7 +541,7 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowwave(
 // (8-B gathers, 512 B per wave-instruction), fp32 accumulation, one RNE rounding -- the bf16 twin of
 // spmm_f32_rowslim (a slice of the c5 [200K, 2048] bf16 table is 102 MB instead of the whole 820 MB),
 // the chunk remainder gathered together.  Same edge order: the same bits as spmm_bf16_rowwave.
-template <int U>
+template <class E, int U>
 __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, const int64_t *__restrict__ rowptr,
                                                             const int32_t *__restrict__ col,
                                                             const float *__restrict__ val,
@@ -528,10 +556,10 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, cons
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   const uint16_t *Xs = X + c0 + lane * 4;
   auto axpy = [&](float v, uint2 x) {
-    acc[0] = acc[0] + v * bf16_to_f32(x.x & 0xffffu);
-    acc[1] = acc[1] + v * bf16_to_f32(x.x >> 16);
-    acc[2] = acc[2] + v * bf16_to_f32(x.y & 0xffffu);
-    acc[3] = acc[3] + v * bf16_to_f32(x.y >> 16);
+    acc[0] = acc[0] + v * E::lo(x.x);
+    acc[1] = acc[1] + v * E::hi(x.x);
+    acc[2] = acc[2] + v * E::lo(x.y);
+    acc[3] = acc[3] + v * E::hi(x.y);
   };
   int64_t e = rowptr[row];
   const int64_t end = rowptr[row + 1];
@@ -567,15 +595,15 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, cons
   }
   if (ok) {
     uint2 o;
-    o.x = f32_to_bf16_rne(acc[0]) | (f32_to_bf16_rne(acc[1]) << 16);
-    o.y = f32_to_bf16_rne(acc[2]) | (f32_to_bf16_rne(acc[3]) << 16);
+    o.x = E::pack(acc[0], acc[1]);
+    o.y = E::pack(acc[2], acc[3]);
     *reinterpret_cast<uint2 *>(Y + row * ldy + c0 + lane * 4) = o;
   }
 }
 
 // F <= FW <= 64, bf16: FW lanes per row, 256/FW rows per block (the c5 conv1 input, F = 8); the
 // same per-element sequence as spmm_bf16_generic (fp32 sum in edge order, one RNE at the end).
-template <int FW, int U>
+template <class E, int FW, int U>
 __global__ __launch_bounds__(kBlock) void spmm_bf16_narrow(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
@@ -598,17 +626,18 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_narrow(
       v[k] = val[e + k];
     }
 #pragma unroll
-    for (int k = 0; k < U; ++k) x[k] = active ? bf16_to_f32(Xs[(int64_t)c[k] * ldx]) : 0.f;
+    for (int k = 0; k < U; ++k) x[k] = active ? E::lo(Xs[(int64_t)c[k] * ldx]) : 0.f;
 #pragma unroll
     for (int k = 0; k < U; ++k) acc = acc + v[k] * x[k];
   }
   for (; e < end; ++e) {
-    const float x = active ? bf16_to_f32(Xs[(int64_t)col[e] * ldx]) : 0.f;
+    const float x = active ? E::lo(Xs[(int64_t)col[e] * ldx]) : 0.f;
     acc = acc + val[e] * x;
   }
-  if (active) Y[row * ldy + sub] = (uint16_t)f32_to_bf16_rne(acc);
+  if (active) Y[row * ldy + sub] = E::rne(acc);
 }
 
+template <class E>
 __global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
@@ -619,8 +648,8 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
   const int64_t beg = rowptr[row], end = rowptr[row + 1];
   for (int64_t c = lane; c < F; c += 64) {
     float acc = 0.f;
-    for (int64_t e = beg; e < end; ++e) acc = acc + val[e] * bf16_to_f32(X[(int64_t)col[e] * ldx + c]);
-    Y[row * ldy + c] = (uint16_t)f32_to_bf16_rne(acc);
+    for (int64_t e = beg; e < end; ++e) acc = acc + val[e] * E::lo(X[(int64_t)col[e] * ldx + c]);
+    Y[row * ldy + c] = E::rne(acc);
   }
 }
 
@@ -677,7 +706,7 @@ lpg_status launch_narrow_f32(const lpg_csr *A, const float *X, int64_t ldx, floa
   return launch(spmm_f32_narrow<FW, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
 }
 
-template <int NV, int U>
+template <class E, int NV, int U>
 lpg_status launch_wide_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
                             int64_t F, hipStream_t s) {
   const int64_t W = NV * 512;
@@ -685,13 +714,14 @@ lpg_status launch_wide_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, ui
   dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock), (unsigned)slices);
   const HeavyRows none{nullptr, 0, INT64_MAX, 1};
   if (F % W == 0)
-    return launch(spmm_bf16_rowwave<NV, U, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
+    return launch(spmm_bf16_rowwave<E, NV, U, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
                   Y, ldy, F, none);
-  return launch(spmm_bf16_rowwave<NV, U, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
+  return launch(spmm_bf16_rowwave<E, NV, U, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx,
                 Y, ldy, F, none);
 }
 
 // 512-column slices with the heavy rows split off (heavy units first in plane 0)
+template <class E>
 lpg_status launch_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
                              int64_t F, HeavyRows hv, hipStream_t s) {
   hv.slices = (F + 511) / 512;
@@ -699,9 +729,9 @@ lpg_status launch_bf16_heavy(const lpg_csr *A, const uint16_t *X, int64_t ldx, u
   LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm_bf16: grid too large");
   dim3 grid((unsigned)nblk, (unsigned)hv.slices);
   if (F % 512 == 0)
-    return launch(spmm_bf16_rowwave<1, 8, true, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y,
+    return launch(spmm_bf16_rowwave<E, 1, 8, true, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y,
                   ldy, F, hv);
-  return launch(spmm_bf16_rowwave<1, 8, false, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y,
+  return launch(spmm_bf16_rowwave<E, 1, 8, false, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y,
                 ldy, F, hv);
 }
 
@@ -796,6 +826,7 @@ extern "C" lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64
                        stream);
 }
 
+template <class E>
 static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
                                  int64_t F, HeavyRows hv, int64_t slice_cols, int32_t depth, void *stream) {
   lpg_status st = check_csr(A);
@@ -812,20 +843,20 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
   if (F <= 64) {  // narrow: FW lanes per row (any alignment)
     const int FW = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
     dim3 grid((unsigned)((A->n_rows + kBlock / FW - 1) / (kBlock / FW)));
-    if (FW == 8) return launch(spmm_bf16_narrow<8, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
-    if (FW == 16) return launch(spmm_bf16_narrow<16, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
-    if (FW == 32) return launch(spmm_bf16_narrow<32, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
-    return launch(spmm_bf16_narrow<64, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    if (FW == 8) return launch(spmm_bf16_narrow<E, 8, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    if (FW == 16) return launch(spmm_bf16_narrow<E, 16, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    if (FW == 32) return launch(spmm_bf16_narrow<E, 32, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    return launch(spmm_bf16_narrow<E, 64, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
   if (!vec || F < 256) {
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
-    return launch(spmm_bf16_generic, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    return launch(spmm_bf16_generic<E>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
   // slice width: slice_cols (256 = spmm_bf16_rowslim, 512 / 1024 / 2048 = rowwave with 1 / 2 / 4
   // 16-B pieces per lane); auto = 256 (c5: 0.92 / 0.97 of the edge-gather roofline vs 0.88 / 0.91 for
   // whole 2048-column rows, profiles/r02_kbench_spmm16.log); with heavy rows split off, 512-column slices
 // (spmm_bf16_rowwave<1, 8> + heavy units: a skewed LP's mostly one-edge rows want few, wide wave tasks)
-  if (hv.blocks > 0) return launch_bf16_heavy(A, X, ldx, Y, ldy, F, hv, s);
+  if (hv.blocks > 0) return launch_bf16_heavy<E>(A, X, ldx, Y, ldy, F, hv, s);
   const int64_t W = slice_cols == 0 ? 256 : slice_cols;
   if (W <= 256) {
     const int64_t nblk = (A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -834,17 +865,17 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
     // auto depth 8 (c5 cons<-vars 0.970 of the edge-gather roofline at 8 vs 0.903 at 16, vars<-cons
     // 0.970 vs 0.807: profiles/r03_kbench_spmmdepth.log)
     const int U = depth != 0 ? depth : 8;
-    if (U == 16) return launch(spmm_bf16_rowslim<16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
-    return launch(spmm_bf16_rowslim<8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    if (U == 16) return launch(spmm_bf16_rowslim<E, 16>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+    return launch(spmm_bf16_rowslim<E, 8>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
   }
-  if (W == 512 || F <= 512) return launch_wide_bf16<1, 8>(A, X, ldx, Y, ldy, F, s);
-  if (W == 1024 || F <= 1024) return launch_wide_bf16<2, 8>(A, X, ldx, Y, ldy, F, s);
-  return launch_wide_bf16<4, 4>(A, X, ldx, Y, ldy, F, s);
+  if (W == 512 || F <= 512) return launch_wide_bf16<E, 1, 8>(A, X, ldx, Y, ldy, F, s);
+  if (W == 1024 || F <= 1024) return launch_wide_bf16<E, 2, 8>(A, X, ldx, Y, ldy, F, s);
+  return launch_wide_bf16<E, 4, 4>(A, X, ldx, Y, ldy, F, s);
 }
 
 extern "C" lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y,
                                     int64_t ldy, int64_t F, void *stream) {
-  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, 0, 0, stream);
+  return spmm_bf16_impl<SBf16>(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, 0, 0, stream);
 }
 
 extern "C" lpg_status lpg_spmm_bf16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
@@ -853,7 +884,7 @@ extern "C" lpg_status lpg_spmm_bf16_tuned(const lpg_csr *A, const uint16_t *X, i
   LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_bf16_tuned: negative n_heavy / thresh");
   LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_bf16_tuned: heavy_rows is NULL");
   LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_bf16_tuned: more heavy rows than rows");
-  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1},
+  return spmm_bf16_impl<SBf16>(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1},
                         slice_cols, depth, stream);
 }
 
@@ -863,6 +894,25 @@ extern "C" lpg_status lpg_spmm_bf16_heavy(const lpg_csr *A, const uint16_t *X, i
   LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_bf16_heavy: negative n_heavy / thresh");
   LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_bf16_heavy: heavy_rows is NULL");
   LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_bf16_heavy: more heavy rows than rows");
-  return spmm_bf16_impl(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1}, 0, 0,
+  return spmm_bf16_impl<SBf16>(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1}, 0, 0,
                         stream);
+}
+
+// fp16 storage (the reference's --fp16 inference: SparseTensor.half() and model.half(), utils.py:909-915,
+// val.py:269): the bf16 kernels with fp16 conversions -- fp32 accumulation in CSR edge order, one RNE
+// rounding to fp16 per output.  Edge values stay fp32 (batch_to(half=True) rounds them to fp16
+// first, lpgnn.data), so the products are those of fp16 values.
+extern "C" lpg_status lpg_spmm_f16(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
+                                   int64_t F, void *stream) {
+  return spmm_bf16_impl<SF16>(A, X, ldx, Y, ldy, F, HeavyRows{nullptr, 0, INT64_MAX, 1}, 0, 0, stream);
+}
+
+extern "C" lpg_status lpg_spmm_f16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, uint16_t *Y, int64_t ldy,
+                                         int64_t F, const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
+                                         int64_t slice_cols, int32_t depth, void *stream) {
+  LPG_REQUIRE(n_heavy >= 0 && thresh >= 0, "lpg_spmm_f16_tuned: negative n_heavy / thresh");
+  LPG_REQUIRE(n_heavy == 0 || heavy_rows != nullptr, "lpg_spmm_f16_tuned: heavy_rows is NULL");
+  LPG_REQUIRE(A != nullptr && n_heavy <= A->n_rows, "lpg_spmm_f16_tuned: more heavy rows than rows");
+  return spmm_bf16_impl<SF16>(A, X, ldx, Y, ldy, F, HeavyRows{heavy_rows, n_heavy, n_heavy ? thresh : INT64_MAX, 1},
+                              slice_cols, depth, stream);
 }

@@ -31,8 +31,11 @@ HEADER_SYMBOLS = (
     "lpg_spmm_bf16_heavy",
     "lpg_spmm_f32_tuned",
     "lpg_spmm_bf16_tuned",
+    "lpg_spmm_f16",
+    "lpg_spmm_f16_tuned",
     "lpg_fc_f32",
     "lpg_fc_bf16",
+    "lpg_fc_f16",
     "lpg_fc_bf16_relu_bwd",
     "lpg_colsum_bf16",
     "lpg_transpose_bf16",
@@ -50,6 +53,7 @@ HEADER_SYMBOLS = (
     "lpg_balanced_weights3",
     "lpg_basis_labels_workspace_bytes",
     "lpg_basis_labels_f32",
+    "lpg_basis_labels_f16",
     "lpg_weighted_ce_fwd_f32",
     "lpg_weighted_ce_bwd_f32",
     "lpg_relu_dropout_bwd_f32",
@@ -64,9 +68,11 @@ HEADER_SYMBOLS = (
     "lpg_heads_relu_bwd_f32",
     "lpg_relu_wgrad_smallk_bf16",
     "lpg_linear_small_fwd_bf16",
+    "lpg_linear_small_fwd_f16",
     "lpg_heads_bwd_bf16_workspace_bytes",
     "lpg_heads_bwd_bf16",
     "lpg_knowledge_f32",
+    "lpg_knowledge_f16",
     "lpg_knowledge_bwd_f32",
     "lpg_scan_i64_workspace_bytes",
     "lpg_scan_i64",
@@ -120,10 +126,16 @@ def lib() -> ctypes.CDLL:
     L.lpg_spmm_f32_tuned.restype = c_i32
     L.lpg_spmm_bf16_tuned.argtypes = L.lpg_spmm_f32_tuned.argtypes
     L.lpg_spmm_bf16_tuned.restype = c_i32
+    L.lpg_spmm_f16.argtypes = L.lpg_spmm_bf16.argtypes
+    L.lpg_spmm_f16.restype = c_i32
+    L.lpg_spmm_f16_tuned.argtypes = L.lpg_spmm_f32_tuned.argtypes
+    L.lpg_spmm_f16_tuned.restype = c_i32
     L.lpg_fc_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
-                             c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_i64, c_p]
+                             c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_i64, c_p, c_p]
     L.lpg_fc_f32.restype = c_i32
     L.lpg_fc_bf16.argtypes = L.lpg_fc_f32.argtypes
+    L.lpg_fc_f16.argtypes = L.lpg_fc_f32.argtypes
+    L.lpg_fc_f16.restype = c_i32
     L.lpg_fc_bf16_relu_bwd.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
                                        c_p, c_i64, c_i32, c_p, c_i64, ctypes.c_float, c_p]
     L.lpg_fc_bf16_relu_bwd.restype = c_i32
@@ -139,12 +151,14 @@ def lib() -> ctypes.CDLL:
     L.lpg_basis_labels_workspace_bytes.restype = c_i64
     L.lpg_basis_labels_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p]
     L.lpg_basis_labels_f32.restype = c_i32
+    L.lpg_basis_labels_f16.argtypes = L.lpg_basis_labels_f32.argtypes
+    L.lpg_basis_labels_f16.restype = c_i32
     L.lpg_transpose_bf16.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p]
     L.lpg_transpose_bf16.restype = c_i32
     L.lpg_split3_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_i64, c_p]
     L.lpg_split3_f32.restype = c_i32
     L.lpg_fc_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
-                                c_i64, c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_i64, c_p]
+                                c_i64, c_p, c_p, c_i64, c_i32, ctypes.c_float, ctypes.c_uint64, c_i64, c_p, c_p]
     L.lpg_fc_x3_f32.restype = c_i32
     L.lpg_fc_x3_heads_workspace_bytes.argtypes = [c_i64, c_i64]
     L.lpg_fc_x3_heads_workspace_bytes.restype = c_i64
@@ -195,6 +209,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_relu_wgrad_smallk_bf16.restype = c_i32
     L.lpg_linear_small_fwd_bf16.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64, c_p]
     L.lpg_linear_small_fwd_bf16.restype = c_i32
+    L.lpg_linear_small_fwd_f16.argtypes = L.lpg_linear_small_fwd_bf16.argtypes
+    L.lpg_linear_small_fwd_f16.restype = c_i32
     L.lpg_heads_bwd_bf16_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
     L.lpg_heads_bwd_bf16_workspace_bytes.restype = c_i64
     L.lpg_heads_bwd_bf16.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i32, ctypes.c_float, c_p,
@@ -202,6 +218,8 @@ def lib() -> ctypes.CDLL:
     L.lpg_heads_bwd_bf16.restype = c_i32
     L.lpg_knowledge_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_i64, ctypes.c_float, c_p, c_i64, c_p]
     L.lpg_knowledge_f32.restype = c_i32
+    L.lpg_knowledge_f16.argtypes = L.lpg_knowledge_f32.argtypes
+    L.lpg_knowledge_f16.restype = c_i32
     L.lpg_knowledge_bwd_f32.argtypes = [c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p]
     L.lpg_knowledge_bwd_f32.restype = c_i32
     L.lpg_scan_i64_workspace_bytes.argtypes = [c_i64]

@@ -94,9 +94,10 @@ class GraphConv(nn.Module):
         if edge_weight is not None:
             raise NotImplementedError("edge weights come from the adjacency values (arch.py:77)")
 
-        def fc(agg, x_dst):  # lin_rel + lin_root, ReLU and (training) dropout fused in one kernel
+        def fc(agg, x_dst, **keys):  # lin_rel + lin_root, ReLU and (training) dropout fused in one kernel
+            # keys: the dropout row keys of a partition's rows (row_offset / row_keys, lpgnn.partition)
             return _fc.graph_conv_fc(agg, x_dst, self.lin_rel.weight, self.lin_rel.bias, self.lin_root.weight, relu,
-                                     dropout)
+                                     dropout, **keys)
 
         pc = getattr(edge_index, "partitioned_conv", None)  # row-partitioned multi-GPU adjacency
         if pc is not None:
@@ -182,13 +183,18 @@ class GCN_FC(GCNBase):
     def forward(self, batch):
         x_left, x_right, edge_index = batch.x_s, batch.x_t, batch.edge_index
         cd = self.compute_dtype
-        if x_left.dtype == torch.float16 or x_right.dtype == torch.float16 or \
-                self.lin_left.weight.dtype == torch.float16:
-            # val.py:269 model.half() / batch_to(half=True): there are no fp16 kernels in this build --
-            # refuse rather than silently promote to fp32.  The 16-bit path is bf16.
-            raise TypeError("GCN_FC: float16 inputs/weights are not supported on MI355X in this build; "
-                            "use GCN_FC(..., compute_dtype='bf16') (or set_compute_dtype('bf16')) with fp32 "
-                            "weights and inputs for 16-bit inference (the CLI's --fp16 does this)")
+        half = (x_left.dtype == torch.float16 or x_right.dtype == torch.float16
+                or self.lin_left.weight.dtype == torch.float16)
+        if half:
+            # val.py:269 model.half() + batch_to(half=True) (utils.py:909-915): the reference's --fp16
+            # inference mode -- fp16 storage of features, activations, weights and logits on the fp16
+            # kernels (v_mfma_f32_16x16x32_f16 FC, fp16 SpMM, heads, add_knowledge in half precision);
+            # fp32 accumulation inside every kernel, one rounding per stored tensor.  Forward only, as
+            # in the reference (train.py trains in fp32).
+            if self.training:
+                raise RuntimeError("GCN_FC: fp16 is the reference's inference mode (val.py:269 model.half() "
+                                   "+ model.eval()); train in fp32 or bf16")
+            cd = torch.float16
         # conv -> ReLU (arch.py:181-182): the ReLU is the FC kernel's epilogue.
         left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True)
         dp = self.dp if self.training else 0.0
@@ -220,6 +226,8 @@ class GCN_FC(GCNBase):
             # both heads fold the last layer's ReLU/dropout backward (bf16) or neither does
             left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias, fold_in=True)
             right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias, fold_in=True)
+        if half:  # arch.py:191 on the fp16 logits, in half precision (fp16 out, as the reference's)
+            return add_knowledge(left, right, x_left, x_right)
         return add_knowledge(left.float(), right.float(), x_left, x_right)
 
 

@@ -94,10 +94,11 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     (fp32) and logits = (logit_l, logit_r), else None."""
     if dropout > 0 and not relu:
         raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
-    bf16 = left.dtype == torch.bfloat16
+    # bf16 (c5) or fp16 (the --fp16 inference mode: forward only) storage: the 16-bit kernels
+    bf16 = left.dtype in _fc.HALF16
     ws = (w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l)
     if bf16:
-        ws = tuple(w.to(torch.bfloat16) for w in ws)
+        ws = tuple(w.to(left.dtype) for w in ws)
     A, AT = adj.fwd, adj.bwd  # A: cons x vars (right2left), AT: vars x cons (left2right)
     seed_r = _fc._new_seed() if dropout > 0 else 0
     seed_l = _fc._new_seed() if dropout > 0 else 0
@@ -141,6 +142,7 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     # arch.py:78-80: left' = right2left((right, left), A)
     left_new, agg_l, logit_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l, head=hd[0])
     ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
+    ctx.f16 = left.dtype == torch.float16
     ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
     logits = None if heads is None or bf16 else (logit_l, logit_r)
@@ -165,6 +167,8 @@ class _TwoDirection(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_left, g_right):
+        if ctx.f16:
+            raise RuntimeError("lpgnn: fp16 is the reference's inference mode (val.py:269); train in fp32 or bf16")
         return _backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None,)
 
 
@@ -186,7 +190,7 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
                 return g, None
             # the bf16 heads' backward already summed these columns (fc.heads_bwd_bf16: the bits of colsum_bf16)
             pre = (getattr(ctx, "folded_colsum", None) or {}).pop(y.data_ptr(), None)
-            return g, (pre[1] if pre is not None and pre[0] == g.data_ptr() else _fc.colsum_bf16(g))
+            return g, (pre[1] if pre is not None and pre[0] is g else _fc.colsum_bf16(g))
         if not ctx.relu:
             g = g.to(dt).contiguous()
             return g, (g.float().sum(0) if want_db else None)

@@ -160,11 +160,13 @@ def bipartite_from_lp(row, col, A_data, c_feas, v_feas, y_s, y_t, device, **aux)
 
 
 def batch_to(batch, dev, half: bool = False):
-    """utils.py:909-915."""
+    """utils.py:909-915.  ``half``: the features and the adjacency's values to fp16 (SparseTensor.half());
+    the labels stay int64 (the reference casts them to half too, which only its accuracy reads)."""
     for nm in ("x_s", "x_t", "y_s", "y_t"):
         t = batch[nm]
         if half and t.is_floating_point():
             t = t.half()
         batch[nm] = t.to(dev)
-    batch["edge_index"] = batch["edge_index"].to(dev)
+    adj = batch["edge_index"].to(dev)
+    batch["edge_index"] = adj.half() if half and hasattr(adj, "half") else adj
     return batch

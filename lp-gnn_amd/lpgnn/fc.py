@@ -58,7 +58,7 @@ _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless th
 def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
                accumulate: bool = False, arith: str | None = None, heads=None, kernel: int = 0,
-               row_offset: int = 0, heads_only: bool = False):
+               row_offset: int = 0, heads_only: bool = False, row_keys: Tensor | None = None):
     """act(A1 W1^T + A2 W2^T [+ out] + bias) through lpg_fc_f32; with
     ``accumulate`` the caller's ``out`` holds the addend and is overwritten.
     ``arith`` ("fp32" | "x3", default ``ARITH``) picks the tiled kernel's arithmetic.
@@ -67,7 +67,9 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
     separate Linear on C (the fp32 contract's own kernel).  ``kernel``: the x3 entries' per-call
     kernel choice (LPG_FC_KERNEL, include/lpgnn.h; 0 = by shape; every choice gives the same bits).
     ``row_offset``: the dropout mask keys row m as row_offset + m (the global node id of the first
-    row when this call computes a slice of a node set: the row partition).
+    row when this call computes a slice of a node set: the row partition); ``row_keys`` (int64 [M] on
+    the device) keys row m as row_keys[m] instead -- the global ids of rows that are not one
+    contiguous range (a general partition's owned variables)).
     ``heads_only`` (with ``heads``): C is not needed -- the fused x3 kernel then does not write it
     (LPG_FC_HEADS_ONLY) and the returned C holds no values (the no-grad forward of the last layer)."""
     if heads is not None:
@@ -76,19 +78,29 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
         small = 4 <= k4(A1.shape[1]) and k4(A1.shape[1]) + (0 if A2 is None else k4(A2.shape[1])) <= 16
         if (arith or ARITH) == "x3" and not small and N > 32 and heads[0].shape[0] <= 4:
             return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, heads, kernel,
-                               row_offset, heads_only)
+                               row_offset, heads_only, row_keys)
         C = _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel,
-                        row_offset=row_offset)
+                        row_offset=row_offset, row_keys=row_keys)
         return C, _fc_forward(C, heads[0], None, None, heads[1], False, arith=arith)
     return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel,
-                       row_offset=row_offset)
+                       row_offset=row_offset, row_keys=row_keys)
+
+
+def _keys(row_keys: Tensor | None, M: int, dev) -> Tensor | None:
+    """The per-row dropout keys as the kernels take them (int64 [M], contiguous, on the device)."""
+    if row_keys is None:
+        return None
+    if row_keys.dtype != torch.int64 or row_keys.shape != (M,) or row_keys.device != dev:
+        raise RuntimeError(f"lpgnn FC: row_keys must be int64 [{M}] on {dev}")
+    return row_keys.contiguous()
 
 
 def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, accumulate=False, arith=None,
-                heads=None, kernel=0, row_offset=0, heads_only=False):
+                heads=None, kernel=0, row_offset=0, heads_only=False, row_keys=None):
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
+    row_keys = _keys(row_keys, M, A1.device)
     k4 = lambda k: -(-k // 4) * 4
     K1_4, K2_4 = k4(A1.shape[1]), (0 if A2 is None else k4(A2.shape[1]))
     small = 4 <= K1_4 and K1_4 + K2_4 <= 16 and N % 4 == 0 and (out is None or (
@@ -115,14 +127,15 @@ def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, acc
         if heads is not None and heads_only:
             flags |= 4  # LPG_FC_HEADS_ONLY
         return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags | _lib.fc_kernel(kernel), dropout_p, seed, relu,
-                      heads=heads, row_offset=row_offset)
+                      heads=heads, row_offset=row_offset, row_keys=row_keys)
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
         st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
                           K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
                           None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
                           None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags,
-                          float(dropout_p), int(seed) & (2**64 - 1), int(row_offset), _lib.stream_of(A1))
+                          float(dropout_p), int(seed) & (2**64 - 1), int(row_offset), _lib.ptr(row_keys),
+                          _lib.stream_of(A1))
         TIMER.stop(tok)
     _lib.check(st, "lpg_fc_f32")
     return C
@@ -149,7 +162,7 @@ def split3(W: Tensor, transpose: bool = False) -> Tensor:
 
 
 def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=None, W2s=None, heads=None,
-           row_offset=0):
+           row_offset=0, row_keys=None):
     """lpg_fc_x3_f32 on fp32 A and pre-split W (split here unless given); with
     ``heads`` = (Wh, bh) lpg_fc_x3_heads_f32, returning (C, logits)."""
     W1s = split3(W1) if W1s is None else W1s
@@ -159,7 +172,7 @@ def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=
             None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
             None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0, W2s.stride(0) if K2 else 0,
             None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags, float(dropout_p),
-            int(seed) & (2**64 - 1), int(row_offset))
+            int(seed) & (2**64 - 1), int(row_offset), _lib.ptr(row_keys))
     key = ("fc", M, N, A1.shape[1] + K2, ("relu" if relu else "lin") + "-x3")
     with torch.cuda.device(A1.device):
         if heads is None:
@@ -239,11 +252,14 @@ def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | No
 _BF16_BK = 64  # lpg_fc_bf16's k-tile: K1, K2 are zero-padded to a multiple of it
 
 
-def _prep_bf16(t: Tensor | None) -> Tensor | None:
+HALF16 = (torch.bfloat16, torch.float16)  # the 16-bit storage types: bf16 (c5), fp16 (--fp16 inference)
+
+
+def _prep_bf16(t: Tensor | None, dt=torch.bfloat16) -> Tensor | None:
     if t is None:
         return None
-    if t.dtype != torch.bfloat16:
-        raise RuntimeError(f"lpgnn bf16 FC: bf16 operands expected, got {t.dtype}")
+    if t.dtype != dt:
+        raise RuntimeError(f"lpgnn 16-bit FC: {dt} operands expected, got {t.dtype}")
     if t.shape[1] % _BF16_BK:
         t = F.pad(t, (0, _BF16_BK - t.shape[1] % _BF16_BK))
     if t.stride(-1) != 1 or t.stride(0) % 8 or t.data_ptr() % 16:
@@ -254,17 +270,26 @@ def _prep_bf16(t: Tensor | None) -> Tensor | None:
 def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                     relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
                     accumulate: bool = False, key: str | None = None, mask=None, kernel: int = 0,
-                    row_offset: int = 0) -> Tensor:
-    """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16);
+                    row_offset: int = 0, row_keys: Tensor | None = None) -> Tensor:
+    """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16); with fp16
+    operands (the --fp16 inference mode, val.py:269) the same kernels on the fp16 MFMA (lpg_fc_f16);
     ``accumulate`` adds the bf16 addend held in ``out`` (overwritten).
     ``mask`` = (Y, scale): an input gradient with the previous layer's ReLU/dropout backward
     folded into the store, C = (Y > 0) ? bf16(C * scale) : 0 (lpg_fc_bf16_relu_bwd; no bias /
     ReLU / dropout of its own) -- the bits of this call without ``mask`` followed by
     relu_bwd_colsum_bf16(C, Y, scale).  ``kernel``: the per-call kernel choice (LPG_FC_KERNEL,
-    include/lpgnn.h; 0 = by shape, 1 = 128 x 128, 2 = 256 x 256, 3 = pipelined; the same bits)."""
+    include/lpgnn.h; 0 = by shape, 1 = 128 x 128, 2 = 256 x 256, 3 = pipelined; the same bits).
+    ``row_offset`` / ``row_keys``: the dropout row keys, as fc_forward."""
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
+    row_keys = _keys(row_keys, M, A1.device)
+    dt = A1.dtype
+    if dt not in HALF16:
+        raise RuntimeError(f"lpgnn 16-bit FC: bf16 or fp16 operands expected, got {dt}")
+    f16 = dt == torch.float16
+    if f16 and mask is not None:
+        raise RuntimeError("lpgnn fp16 FC: the folded ReLU backward is a bf16 training path")
     k1, k2 = A1.shape[1], (0 if A2 is None else A2.shape[1])
     # conv1 (narrow LP features): the streaming small-K kernel takes the operands unpadded
     small = (mask is None and 4 <= k1 and k1 + k2 <= 16 and k1 % 4 == 0 and k2 % 4 == 0 and N % 4 == 0
@@ -273,19 +298,19 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
         A1, W1 = A1.contiguous(), W1.contiguous()
         A2 = None if A2 is None else A2.contiguous()
         W2 = None if W2 is None else W2.contiguous()
-        if any(t is not None and t.dtype != torch.bfloat16 for t in (A1, W1, A2, W2)):
-            raise RuntimeError("lpgnn bf16 FC: bf16 operands expected")
+        if any(t is not None and t.dtype != dt for t in (A1, W1, A2, W2)):
+            raise RuntimeError(f"lpgnn 16-bit FC: {dt} operands expected")
     else:
-        A1, W1, A2, W2 = _prep_bf16(A1), _prep_bf16(W1), _prep_bf16(A2), _prep_bf16(W2)
+        A1, W1, A2, W2 = _prep_bf16(A1, dt), _prep_bf16(W1, dt), _prep_bf16(A2, dt), _prep_bf16(W2, dt)
     bias = None if bias is None else bias.float().contiguous()
     if out is not None:
-        if out.shape != (M, N) or out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.device != A1.device:
-            raise RuntimeError("lpgnn bf16 FC: `out` must be a bfloat16 [M, N] row-major view on the same device")
+        if out.shape != (M, N) or out.dtype != dt or out.stride(1) != 1 or out.device != A1.device:
+            raise RuntimeError(f"lpgnn 16-bit FC: `out` must be a {dt} [M, N] row-major view on the same device")
         C = out
     elif accumulate:
         raise RuntimeError("lpgnn bf16 FC: accumulate needs the addend in `out`")
     else:
-        C = torch.empty((M, N), dtype=torch.bfloat16, device=A1.device)
+        C = torch.empty((M, N), dtype=dt, device=A1.device)
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0) | _lib.fc_kernel(kernel)
@@ -308,15 +333,18 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
             TIMER.stop(tok)
         _lib.check(st, "lpg_fc_bf16_relu_bwd")
         return C
+    entry = "lpg_fc_f16" if f16 else "lpg_fc_bf16"
     with torch.cuda.device(A1.device):
-        tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, key or ("relu-bf16" if relu else "lin-bf16")))
-        st = L.lpg_fc_bf16(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
+        tok = TIMER.start(("fc", M, N, A1.shape[1] + K2,
+                           key or (("relu-" if relu else "lin-") + ("f16" if f16 else "bf16"))))
+        st = getattr(L, entry)(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
                            K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
                            None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
                            None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags,
-                           float(dropout_p), int(seed) & (2**64 - 1), int(row_offset), _lib.stream_of(A1))
+                           float(dropout_p), int(seed) & (2**64 - 1), int(row_offset), _lib.ptr(row_keys),
+                           _lib.stream_of(A1))
         TIMER.stop(tok)
-    _lib.check(st, "lpg_fc_bf16")
+    _lib.check(st, entry)
     return C
 
 
@@ -518,25 +546,26 @@ def relu_wgrad_smallk_bf16(g: Tensor, y: Tensor | None, scale: float, A1: Tensor
 def _small_heads_bf16(x: Tensor, W: Tensor) -> bool:
     """The bf16 heads' streaming kernels take this Linear (N <= 4 outputs, K <= 2048)."""
     K = x.shape[1]
-    return (x.dtype == torch.bfloat16 and W.shape[0] <= 4 and 8 <= K <= 2048 and K % 8 == 0 and x.stride(1) == 1
+    return (x.dtype in HALF16 and W.shape[0] <= 4 and 8 <= K <= 2048 and K % 8 == 0 and x.stride(1) == 1
             and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0)
 
 
 def linear_small_fwd_bf16(x: Tensor, W: Tensor, b: Tensor | None) -> Tensor:
-    """The bf16 heads' forward (lpg_linear_small_fwd_bf16): bf16 [M, N] = RNE(x W^T + b), W rounded to
-    bf16 first (the c5 model's weights), fp32 sums."""
+    """The 16-bit heads' forward (lpg_linear_small_fwd_bf16 / _f16 by x's dtype): [M, N] = RNE(x W^T + b),
+    W rounded to the storage type first (the c5 / --fp16 model's weights), fp32 sums."""
     M, K = x.shape
     N = W.shape[0]
-    Wf = W.detach().to(torch.bfloat16).float().contiguous()
+    dt = x.dtype
+    Wf = W.detach().to(dt).float().contiguous()
     b = None if b is None else b.detach().float().contiguous()
-    out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    out = torch.empty((M, N), dtype=dt, device=x.device)
+    entry = "lpg_linear_small_fwd_f16" if dt == torch.float16 else "lpg_linear_small_fwd_bf16"
     with torch.cuda.device(x.device):
-        tok = TIMER.start(("heads_fwd", M, N, K, "bf16"))
-        st = _lib.lib().lpg_linear_small_fwd_bf16(M, K, N, x.data_ptr(), x.stride(0), Wf.data_ptr(),
-                                                  None if b is None else b.data_ptr(), out.data_ptr(), N,
-                                                  _lib.stream_of(x))
+        tok = TIMER.start(("heads_fwd", M, N, K, "f16" if dt == torch.float16 else "bf16"))
+        st = getattr(_lib.lib(), entry)(M, K, N, x.data_ptr(), x.stride(0), Wf.data_ptr(),
+                                        None if b is None else b.data_ptr(), out.data_ptr(), N, _lib.stream_of(x))
         TIMER.stop(tok)
-    _lib.check(st, "lpg_linear_small_fwd_bf16")
+    _lib.check(st, entry)
     return out
 
 
@@ -573,17 +602,18 @@ def _new_seed() -> int:
 
 class _FC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, A1, A2, W1, W2, b, relu, dropout_p):
+    def forward(ctx, A1, A2, W1, W2, b, relu, dropout_p, row_offset=0, row_keys=None):
         if dropout_p > 0 and not relu:
             raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
         seed = _new_seed() if dropout_p > 0 else 0
         ctx.bf16 = A1.dtype == torch.bfloat16
+        kw = dict(row_offset=row_offset, row_keys=row_keys)
         if ctx.bf16:  # c5 path: bf16 activations, fp32 master weights cast per call
             W1 = W1.to(torch.bfloat16)
             W2 = None if W2 is None else W2.to(torch.bfloat16)
-            C = fc_forward_bf16(A1, W1, A2, W2, b, relu, dropout_p, seed)
+            C = fc_forward_bf16(A1, W1, A2, W2, b, relu, dropout_p, seed, **kw)
         else:
-            C = fc_forward(A1, W1, A2, W2, b, relu, dropout_p, seed)
+            C = fc_forward(A1, W1, A2, W2, b, relu, dropout_p, seed, **kw)
         ctx.relu, ctx.has_a2, ctx.has_b = relu, A2 is not None, b is not None
         ctx.scale = 1.0 / (1.0 - dropout_p) if dropout_p > 0 else 1.0
         ctx.save_for_backward(A1, A2 if A2 is not None else A1, W1, W2 if W2 is not None else W1,
@@ -604,7 +634,7 @@ class _FC(torch.autograd.Function):
             dA2 = input_grad_bf16(g, W2) if ctx.has_a2 and need[1] else None
             dW1 = wgrad_bf16(g, A1) if need[2] else None
             dW2 = wgrad_bf16(g, A2) if ctx.has_a2 and need[3] else None
-            return dA1, dA2, dW1, dW2, db, None, None
+            return dA1, dA2, dW1, dW2, db, None, None, None, None
         if ctx.relu:
             g, db = relu_bwd_colsum(gC, C, ctx.scale, want_db)  # ReLU + dropout bwd, bias grad fused
         else:
@@ -619,12 +649,14 @@ class _FC(torch.autograd.Function):
         else:
             dW1 = g.t() @ A1 if need[2] else None
             dW2 = g.t() @ A2 if ctx.has_a2 and need[3] else None
-        return dA1, dA2, dW1, dW2, db, None, None
+        return dA1, dA2, dW1, dW2, db, None, None, None, None
 
 
 def graph_conv_fc(agg: Tensor, x_dst: Tensor, w_rel: Tensor, b_rel, w_root: Tensor, relu: bool,
-                  dropout: float = 0.0) -> Tensor:
-    return _FC.apply(agg, x_dst, w_rel, w_root, b_rel, relu, float(dropout))
+                  dropout: float = 0.0, row_offset: int = 0, row_keys: Tensor | None = None) -> Tensor:
+    """GraphConv's lin_rel(agg) + lin_root(x_dst) (+ ReLU, dropout) as one autograd node; the dropout
+    mask keys rows by row_keys[m] or row_offset + m (a partition's global node ids)."""
+    return _FC.apply(agg, x_dst, w_rel, w_root, b_rel, relu, float(dropout), int(row_offset), row_keys)
 
 
 def linear_small_bwd(G: Tensor, W: Tensor, H: Tensor, need_dh: bool):
@@ -676,14 +708,15 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, prev=None):
         ctx.has_b = b is not None
-        ctx.bf16 = x.dtype == torch.bfloat16
+        ctx.bf16 = x.dtype in HALF16  # (fp16: the --fp16 inference mode, forward only)
+        ctx.f16 = x.dtype == torch.float16
         ctx.in_scale = None
         ctx.small, ctx.prev = False, None
         if prev is not None:  # x = a bf16 ReLU layer's output feeding only this Linear: fold its backward
             ctx.in_scale = prev.scale
             prev.out_folded = True
         if ctx.bf16:
-            W = W.to(torch.bfloat16)
+            W = W.to(x.dtype)
             ctx.save_for_backward(x, W)
             ctx.small = _small_heads_bf16(x, W)
             ctx.prev = prev
@@ -695,6 +728,8 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.f16:
+            raise RuntimeError("lpgnn: fp16 is the reference's inference mode (val.py:269); train in fp32 or bf16")
         x, W = ctx.saved_tensors
         need = ctx.needs_input_grad
         if ctx.bf16 and ctx.small:
@@ -704,7 +739,10 @@ class _Linear(torch.autograd.Function):
             if ctx.prev is not None and dby is not None:
                 if getattr(ctx.prev, "folded_colsum", None) is None:
                     ctx.prev.folded_colsum = {}
-                ctx.prev.folded_colsum[x.data_ptr()] = (dx.data_ptr(), dby)
+                # keyed by the layer output's storage; the gradient handed over is checked by identity
+                # (`g is dx` in conv.py), and dx is held here, so its memory cannot be reused for another
+                # tensor while the entry exists (a hook that replaces the gradient falls back to colsum)
+                ctx.prev.folded_colsum[x.data_ptr()] = (dx, dby)
             ctx.prev = None
             return (dx if need[0] else None), (dW if need[1] else None), (db if ctx.has_b and need[2] else None), None
         if ctx.bf16:
@@ -768,5 +806,25 @@ class _Knowledge(torch.autograd.Function):
 def knowledge(logit: Tensor, feas: Tensor, bound=10) -> Tensor:
     """One side of add_knowledge: normalize(logit) * 10, then -bound on
     column 0 where feas[:, -3] != 0 (lower bound = -inf) and on column 2
-    where feas[:, -1] != 0 (upper bound = +inf)."""
+    where feas[:, -1] != 0 (upper bound = +inf).  fp16 logits (the --fp16
+    inference mode): lpg_knowledge_f16, half-precision semantics, fp16 out, no backward."""
+    if logit.dtype == torch.float16:
+        return knowledge_f16(logit, feas, bound)
     return _Knowledge.apply(logit, feas, bound)
+
+
+def knowledge_f16(logit: Tensor, feas: Tensor, bound=10) -> Tensor:
+    """arch.py:129-141 on fp16 logits as torch's half ops evaluate it (lpg_knowledge_f16)."""
+    if logit.device.type != "cuda":
+        raise RuntimeError("lpgnn: add_knowledge runs on a HIP device only (no CPU path)")
+    if torch.is_grad_enabled() and logit.requires_grad:
+        raise RuntimeError("lpgnn: fp16 is the reference's inference mode (val.py:269); no backward")
+    logit = logit.contiguous()
+    feas = feas.contiguous().float()
+    out = torch.empty_like(logit)
+    with torch.cuda.device(logit.device):
+        st = _lib.lib().lpg_knowledge_f16(logit.shape[0], logit.data_ptr(), logit.stride(0), feas.data_ptr(),
+                                          feas.stride(0), feas.shape[1], float(bound), out.data_ptr(), out.stride(0),
+                                          _lib.stream_of(logit))
+    _lib.check(st, "lpg_knowledge_f16")
+    return out

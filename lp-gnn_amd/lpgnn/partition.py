@@ -302,15 +302,16 @@ class Exchange:
     def __init__(self, plan: PartitionPlan, device, group=None):
         self.n_own, self.n_local = plan.n_own, plan.n_local
         self.m, self.n = plan.m, plan.n  # global sizes: rank-independent layout decisions
-        # dropout keys (the FC's row_offset): the constraint rows are the block [row_lo, row_hi); the
-        # owned variables are keyed by their global ids when they form one contiguous range (every
-        # block plan: the bench and c4 paths), so each node draws the mask a single-GPU run draws.
-        # A general plan's owned set need not be contiguous: it keys owned row i as owned[0] + i
-        # (masks stay independent per node within a rank, not equal to the one-GPU masks).
+        # dropout keys: every node is keyed by its GLOBAL id, so each node draws the mask a single-GPU
+        # run draws.  The constraint rows are the block [row_lo, row_hi) (the FC's row_offset); the
+        # owned variables are one contiguous range in every block plan (row_offset = owned[0]) and
+        # any set in a general plan (the owner with most edges): then the FC takes one key per row
+        # (row_keys = the owned global ids, int64 on the device).
         self.cons_key0 = int(plan.row_lo)
         own = plan.owned
         self.var_key0 = int(own[0]) if own.shape[0] else 0
-        self.var_keys_global = bool(own.shape[0] == 0 or int(own[-1]) - int(own[0]) + 1 == own.shape[0])
+        contiguous = own.shape[0] == 0 or int(own[-1]) - int(own[0]) + 1 == own.shape[0]
+        self.var_keys = None if contiguous else torch.from_numpy(np.ascontiguousarray(own, np.int64)).to(device)
         self.send_idx = torch.from_numpy(plan.send_idx).to(device)
         self.recv_idx = torch.from_numpy(plan.recv_idx).to(device)
         self.send_counts, self.recv_counts = list(plan.send_counts), list(plan.recv_counts)
@@ -327,6 +328,15 @@ class Exchange:
                 tot = tot.to(device)
             dist.all_reduce(tot, group=group)
         self.active = bool(tot.item() > 0)
+
+    @property
+    def var_key_args(self) -> dict:
+        """The FC keyword arguments that key the owned variables' dropout rows by their global ids."""
+        return {"row_offset": self.var_key0, "row_keys": self.var_keys}
+
+    @property
+    def cons_key_args(self) -> dict:
+        return {"row_offset": self.cons_key0, "row_keys": None}
 
     def _a2a(self, send, in_counts, out_counts):
         if not self.active:
@@ -505,11 +515,11 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
     if ra:  # lin_root + bias + ReLU accumulated onto the owners' sums, in place
         right_new, agg_r = agg_r, None
         own = _fc.fc_forward(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
-                             out=right_new[:n_own], accumulate=True, heads=hr, row_offset=ex.var_key0)
+                             out=right_new[:n_own], accumulate=True, heads=hr, **ex.var_key_args)
     else:
         right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
         own = _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
-                             out=right_new[:n_own], heads=hr, row_offset=ex.var_key0)
+                             out=right_new[:n_own], heads=hr, **ex.var_key_args)
     ex.start_broadcast_(right_new).finish()
     logits = None
     if heads is not None:
@@ -718,11 +728,11 @@ class PartitionedCSR:
     def partitioned_conv(self, x, fc):
         """One GraphConv direction: fc(agg, x_dst) is lin_rel + lin_root (+ReLU, +dropout)."""
         agg = _local_spmm(self.local, x[0])
-        if self.orient == "cons":
-            return fc(agg, x[1])
         ex = self.ex
+        if self.orient == "cons":
+            return fc(agg, x[1], **ex.cons_key_args)
         agg_own = _Reduce.apply(agg, ex)
-        out_own = fc(agg_own, x[1][:ex.n_own])
+        out_own = fc(agg_own, x[1][:ex.n_own], **ex.var_key_args)
         return _Broadcast.apply(out_own, ex)
 
 

@@ -22,13 +22,11 @@ What is different, and why:
 
 * accuracy per step is computed on the device (val.accuracy_device, no host
   sync); the host sklearn path is used only by ``validation``;
-* ``--fp16 1`` (utils.py:770; val.py:269 ``model.half()``) selects the
-  16-bit inference path of this build for VALIDATION only, as in the
-  reference (train.py never converts the model): bf16 (same storage width,
-  fp32 exponent range; the bf16 MFMA kernels of the c5 configuration).
-  Training stays fp32 with the flag set.  A model or batch converted to
-  torch.float16 by hand is rejected by GCN_FC.forward instead of being
-  silently promoted;
+* ``--fp16 1`` (utils.py:770; val.py:269 ``model.half()``) converts the
+  VALIDATION model to fp16, as in the reference (train.py never converts the
+  model), and every evaluated batch goes through ``batch_to(half=True)``
+  (val.py:31): the fp16 kernels (fp16 storage, fp32 accumulation).  Training
+  stays fp32 with the flag set;
 * ``--replicas`` (torch.distributed initialised, world > 1): data parallel
   over graphs ("many small LPs: replicas only").  Every rank
   walks the same shuffled epoch order and takes every world-th graph; the
@@ -228,15 +226,16 @@ def parse_args(argv=None):
 
 # ------------------------------------------------------------------- model
 def make_model(args, for_eval: bool = False):
-    """eval(args.arch) (train.py:79) + --load_from (train.py:80); --fp16 (val.py:269) only for an
-    evaluation model (``for_eval``): the reference's train.py trains in fp32 whatever the flag."""
+    """eval(args.arch) (train.py:79) + --load_from (train.py:80); --fp16 (val.py:269: model.half() after
+    the load) only for an evaluation model (``for_eval``): the reference's train.py trains in fp32
+    whatever the flag."""
     from .arch import build_model
 
     model = build_model(args.arch)
-    if args.fp16 and for_eval:
-        model.set_compute_dtype(torch.bfloat16)
     if str(args.load_from).lower() != "none":
         model.load(args.load_from)
+    if args.fp16 and for_eval:
+        model.half()
     return model.to(args.dev)
 
 
@@ -346,7 +345,8 @@ def validation(model, ds, args):
     avg_acc, rows = 0., []
     for i in range(len(ds)):
         graph = ds[i]
-        lc, lv = model_inference_with_batch(model, graph, args.arch, dev=args.dev, batch_size=args.batch_size)
+        lc, lv = model_inference_with_batch(model, graph, args.arch, dev=args.dev, batch_size=args.batch_size,
+                                            fp16=next(model.parameters()).dtype == torch.float16)
         y = graph.y if not hasattr(graph, "x_s") else torch.cat((graph.y_s, graph.y_t))
         acc, prec, recl = accuracy(torch.cat((lc, lv), 0), y.cpu(), lc.shape[0], return_pr=True,
                                    dataset_name=args.dataset)

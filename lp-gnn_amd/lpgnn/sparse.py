@@ -107,6 +107,13 @@ class BipartiteCSR:
     def to(self, device, non_blocking: bool = False) -> "BipartiteCSR":
         return BipartiteCSR(self.fwd.to(device), self.bwd.to(device))
 
+    def half(self) -> "BipartiteCSR":
+        """SparseTensor.half() (batch_to(half=True), utils.py:909-915): the edge values rounded to fp16
+        (kept in fp32 storage -- exact -- which the SpMM kernels read; the products are those of the
+        fp16 values)."""
+        r = lambda c: CSR(c.rowptr, c.col, c.val.half().float(), c.n_rows, c.n_cols)  # noqa: E731
+        return BipartiteCSR(r(self.fwd), r(self.bwd))
+
     def __repr__(self) -> str:
         r, c = self.sparse_sizes()
         return f"BipartiteCSR(sparse_sizes=({r}, {c}), nnz={self.nnz()}, device={self.device})"
@@ -178,7 +185,7 @@ HEAVY_THRESH = int(os.environ.get("LPGNN_SPMM_HEAVY", "1024"))
 
 
 def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0) -> torch.Tensor:
-    """Y = adj @ x on the GPU (no autograd).  fp32 or bf16 storage.  ``slice_cols`` / ``depth``: the
+    """Y = adj @ x on the GPU (no autograd).  fp32, bf16 or fp16 storage.  ``slice_cols`` / ``depth``: the
     per-call tuning of lpg_spmm_*_tuned (0 = auto; every choice gives the same bits)."""
     if x.device.type != "cuda" or adj.device != x.device:
         raise RuntimeError(f"lpgnn.spmm: x ({x.device}) and adj ({adj.device}) must be on the same HIP device; "
@@ -194,6 +201,8 @@ def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0)
         name = "lpg_spmm_f32_tuned"
     elif x.dtype == torch.bfloat16:
         name = "lpg_spmm_bf16_tuned"
+    elif x.dtype == torch.float16:
+        name = "lpg_spmm_f16_tuned"
     else:
         raise RuntimeError(f"lpgnn.spmm: unsupported dtype {x.dtype}")
     heavy = None

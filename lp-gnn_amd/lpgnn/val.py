@@ -25,9 +25,12 @@ def inference_gnn(logits, m, check: bool = True, **kwargs):
     torch ops."""
     n = logits.shape[0] - m
     if logits.is_cuda and logits.dim() == 2 and logits.shape[1] == 3:
-        pred = _basis_labels_device(logits.float(), m)
+        # fp16 logits (the --fp16 mode): the half softmax's fp16 probabilities decide (lpg_basis_labels_f16)
+        pred = _basis_labels_device(logits if logits.dtype == torch.float16 else logits.float(), m)
     else:
         pr = F.softmax(logits.float(), dim=-1)
+        if logits.dtype == torch.float16:  # a half softmax stores fp16 probabilities (the device kernel's rule)
+            pr = pr.half().float()
         pr = pr.clone()
         pr[torch.isnan(pr)] = 0
         _, topk_idx = pr[:, 1].topk(m)
@@ -52,17 +55,19 @@ def _basis_labels_device(logits, m):
     if not 0 <= m <= total:
         raise RuntimeError(f"inference_gnn: m = {m} outside [0, {total}] (topk)")
     L = _lib.lib()
+    f16 = logits.dtype == torch.float16
+    entry = "lpg_basis_labels_f16" if f16 else "lpg_basis_labels_f32"
     pred = torch.empty(total, dtype=torch.int64, device=logits.device)
     ws = torch.empty((max(16, L.lpg_basis_labels_workspace_bytes(total)) + 15) // 16 * 4, dtype=torch.float32,
                      device=logits.device)
     from .timing import TIMER
 
     with torch.cuda.device(logits.device):
-        tok = TIMER.start(("basis_labels", total, 3, m, "f32"))
-        st = L.lpg_basis_labels_f32(total, m, logits.data_ptr(), logits.stride(0), pred.data_ptr(), ws.data_ptr(),
-                                    _lib.stream_of(logits))
+        tok = TIMER.start(("basis_labels", total, 3, m, "f16" if f16 else "f32"))
+        st = getattr(L, entry)(total, m, logits.data_ptr(), logits.stride(0), pred.data_ptr(), ws.data_ptr(),
+                               _lib.stream_of(logits))
         TIMER.stop(tok)
-    _lib.check(st, "lpg_basis_labels_f32")
+    _lib.check(st, entry)
     return pred
 
 
@@ -112,13 +117,17 @@ def accuracy(logits, gt, num_cons, return_pr=False, dataset_name=""):
 
 @torch.no_grad()
 def model_inference_with_batch(model, batched_graphs, arch: str = "GCN_FC(8,8)", dev="cuda",
-                               batch_size: int = 10240 * 8 * 4):
+                               batch_size: int = 10240 * 8 * 4, fp16: bool = False):
     """val.py:12-36.  A bipartite batch runs full-graph; a homogeneous graph
     (above MyToBipartite's threshold) goes through the device k-hop
     NeighborLoader with every neighbour (num_neighbors=[-1]*(depth-1),
     directed=False, val.py:22-27) in seed order, and the seed logits are
     concatenated -- equal to the full-graph logits up to summation order
-    (the reference's own check, val.py:37-41)."""
+    (the reference's own check, val.py:37-41).  ``fp16``: batch_to(batch, dev, half=True) on every
+    batch (val.py:31, args.fp16) -- a copy, the caller's graph keeps its dtypes."""
+    import copy
+
+    from .data import batch_to
     from .data import MyToBipartite
     from .loader import NeighborLoader
 
@@ -133,7 +142,7 @@ def model_inference_with_batch(model, batched_graphs, arch: str = "GCN_FC(8,8)",
                                 drop_last=False, device=dev)
     lc, lv = [], []
     for batch in loader:
-        batch = batch.to(dev)
+        batch = batch_to(copy.copy(batch), dev, half=True) if fp16 else batch.to(dev)
         logit_cons, logit_vars = model(batch)
         lc.append(logit_cons[:batch.s_bs].cpu()), lv.append(logit_vars[:batch.t_bs].cpu())
     return torch.cat(lc, 0), torch.cat(lv, 0)

@@ -281,6 +281,97 @@ def gcn_fc_forward(sd, x_s, x_t, A, AT, depth: int, keep=None, fc="mkl", reassoc
     return add_knowledge(left, right, x_s, x_t)
 
 
+# --------------------------------------------------------------------------
+# The --fp16 inference mode (val.py:269 model.half(), utils.py:909-915 batch_to(half=True))
+# --------------------------------------------------------------------------
+def r16(t: torch.Tensor) -> torch.Tensor:
+    """The fp16 storage of a tensor computed in fp32 (torch's half ops compute in fp32 and round
+    each stored result to nearest even): fp16 values, held as fp32."""
+    return t.half().float()
+
+
+def spmm_f16(rowptr, col, val, X16) -> torch.Tensor:
+    """torch_sparse spmm_sum on fp16 storage as this build defines it: the fp16 values (X16 and the
+    edge values, exact in fp32) summed in spmm_cpu's sequential order in fp32, one rounding to fp16 per
+    output.  (torch_sparse 0.6.12's CUDA kernel accumulates in the storage type -- absent here, not
+    reproduced; the fp32 sum is the more accurate one.)"""
+    val16 = r16(torch.from_numpy(np.asarray(val, np.float32))).numpy()
+    X = np.ascontiguousarray(X16.detach().float().numpy() if isinstance(X16, torch.Tensor) else X16, np.float32)
+    return r16(torch.from_numpy(spmm_f32(rowptr, col, val16, X)))
+
+
+def _linear16(x, W, b=None):
+    """F.linear of fp16 operands with fp32 accumulation (MKL), the bias added in fp32: NOT rounded."""
+    y = x.float() @ r16(W.float()).t()
+    return y if b is None else y + r16(b.float())
+
+
+def graph_conv_fp16(x_src, x_dst, adj, W_rel, b_rel, W_root, relu=False, reassoc=True):
+    """GraphConv (PyG 2.1, arch.py:57-62) with fp16 storage, one rounding per stored tensor:
+    out = r16(act(agg W_rel^T + x_dst W_root^T + b_rel)), agg = spmm_f16(adj, x_src); with the
+    association rule (lpgnn/conv.py), P = spmm_f16(r16(x_src W_rel^T)) and out = r16(act(x_dst W_root^T
+    + P + b_rel)) -- the HIP path's fused FC epilogue."""
+    if reassoc and reassociate(x_src.shape[0], x_dst.shape[0], x_src.shape[1], W_rel.shape[0]):
+        P = spmm_f16(*adj, r16(_linear16(x_src, W_rel)))
+        out = _linear16(x_dst, W_root) + P + r16(b_rel.float())
+    else:
+        agg = spmm_f16(*adj, x_src)
+        out = _linear16(agg, W_rel, b_rel) + _linear16(x_dst, W_root)
+    return r16(torch.relu(out) if relu else out)
+
+
+def add_knowledge_fp16(logit16, feas, bound=10):
+    """arch.py:129-141 on fp16 logits, as torch's half ops evaluate it (lpg_knowledge_f16): the norm
+    in fp32 (sqrt of fma(x2, x2, fma(x1, x1, x0 x0)), the fmas evaluated in fp64 and rounded), then
+    rounded; clamp_min(1e-12) of a half tensor = max(n, 0); every op's result rounded to fp16."""
+    x = logit16.float().double()
+    ss = (x[:, 0] * x[:, 0]).float().double()
+    ss = (x[:, 1] * x[:, 1] + ss).float().double()
+    ss = (x[:, 2] * x[:, 2] + ss).float()
+    n = r16(torch.sqrt(ss)).clamp_min(0.0)
+    y = r16(r16(logit16.float() / n[:, None]) * 10)
+    y[feas[:, -3] != 0, 0] = r16(y[feas[:, -3] != 0, 0] - bound)
+    y[feas[:, -1] != 0, 2] = r16(y[feas[:, -1] != 0, 2] - bound)
+    return y
+
+
+def gcn_fc_forward_fp16(sd, x_s, x_t, A, AT, depth: int, keep=None):
+    """GCN_FC.forward (arch.py:179-193) after model.half() and batch_to(half=True): the oracle of the
+    --fp16 mode.  Features, edge values, weights rounded to fp16; every layer's stored output
+    rounded to fp16 (fp32 accumulation inside each op); heads r16(h W^T + b); add_knowledge in half
+    precision.  Returns the fp16 logits (held as fp32)."""
+    w = {k: (None if v is None else r16(v.float())) for k, v in sd.items()}
+    left, right = r16(x_s.float()), r16(x_t.float())
+    for i, prefix in enumerate(["conv1"] + [f"layers.{j}" for j in range(depth - 2)]):
+        g = lambda d, k: w[f"{prefix}.{d}.{k}"]  # noqa: E731
+        right_new = graph_conv_fp16(left, right, AT, g("left2right", "lin_rel.weight"), g("left2right", "lin_rel.bias"),
+                                    g("left2right", "lin_root.weight"), relu=True)
+        left_new = graph_conv_fp16(right, left, A, g("right2left", "lin_rel.weight"), g("right2left", "lin_rel.bias"),
+                                   g("right2left", "lin_root.weight"), relu=True)
+        left, right = left_new, right_new
+        if keep is not None:
+            keep[f"left{i}"], keep[f"right{i}"] = left, right
+    hl = r16(_linear16(left, w["lin_left.weight"], w["lin_left.bias"]))
+    hr = r16(_linear16(right, w["lin_right.weight"], w["lin_right.bias"]))
+    if keep is not None:
+        keep["head_l"], keep["head_r"] = hl, hr
+    return add_knowledge_fp16(hl, x_s), add_knowledge_fp16(hr, x_t)
+
+
+@torch.no_grad()
+def inference_gnn_fp16(logits16, m):
+    """val.py:106-124 on fp16 logits: the half softmax's fp16 probabilities (NaN -> 0); of the nodes tied
+    at the m-th largest P[:, 1] the lowest indices are basic (torch.topk leaves that open; the HIP kernel's
+    rule); argmax over {0, 2} with ties to 0."""
+    pr = r16(F.softmax(logits16.float(), dim=-1))
+    pr[torch.isnan(pr)] = 0
+    order = np.lexsort((np.arange(pr.shape[0]), -pr[:, 1].double().numpy()))
+    top = torch.from_numpy(order[:m])
+    pred = torch.where(pr[:, 0] >= pr[:, 2], 0, 2).to(torch.int64)
+    pred[top] = 1
+    return pred
+
+
 def init_state_dict(p: int, q: int, hids: int, depth: int, seed: int = 0):
     """GCN_FC(p, q, hids, depth) parameters with the reference's RNG stream.
 

@@ -93,7 +93,7 @@ def test_status_and_error_string():
     # never dereferenced: the flags check precedes every device call)
     fake = 1 << 20
     assert L.lpg_fc_bf16(1, 8, 64, fake, 64, fake, 64, 0, None, 0, None, 0, None, fake, 8, _lib.fc_kernel(9), 0.0, 0,
-                         0, None) == 1
+                         0, None, None) == 1
     assert b"flags" in L.lpg_last_error()
     # NULL CSR -> invalid argument, no device work
     assert L.lpg_spmm_f32(None, None, 0, None, 0, 0, None) == 1
@@ -130,7 +130,7 @@ def test_fc_rejects_unpadded_k_on_the_tiled_path():
 
     L = _lib.lib()
     fake = 1 << 20  # 16-byte aligned, never dereferenced: validation fails first
-    st = L.lpg_fc_f32(10, 64, 40, fake, 40, fake, 40, 0, None, 0, None, 0, None, fake, 64, 0, 0.0, 0, 0, None)
+    st = L.lpg_fc_f32(10, 64, 40, fake, 40, fake, 40, 0, None, 0, None, 0, None, fake, 64, 0, 0.0, 0, 0, None, None)
     assert st == 1 and b"multiples of 32" in L.lpg_last_error()
 
 

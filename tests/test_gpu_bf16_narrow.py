@@ -126,9 +126,15 @@ def test_linear_small_fwd_bf16(M, K, N):
     Wb = W.to(BF)
     ref = H.double() @ Wb.double().t() + b.double()
     _within_bf16_ulp(got.float(), ref, "linear_small_fwd_bf16")
-    # against the MFMA kernel it replaces (N padded to 64 inside lpg_fc_bf16): one bf16 ulp at most
+    # against the MFMA kernel it replaced (the same bf16 operands; N padded inside lpg_fc_bf16): both
+    # are RNE_bf16 of an fp32 sum of the same exact products in different orders, so
+    #   |got - want| <= |s1 - s2| + 2^-8 max(|s1|, |s2|),  |s1 - s2| <= 2 (K + 1) 2^-24 (|H| |Wb|^T + |b|)
+    # (the recursive-summation bound of each order against the exact sum)
     want = fc_forward_bf16(H, Wb, None, None, b, False).float()
-    assert bool(((got.float() - want).abs() <= want.abs() * 2.0 ** -7 + 1e-6).all())
+    terms = H.double().abs() @ Wb.double().abs().t() + b.double().abs()
+    s_gap = 2 * (K + 1) * 2.0 ** -24 * terms
+    bound = s_gap + 2.0 ** -8 * (want.double().abs() + s_gap)
+    assert bool(((got.double() - want.double()).abs() <= bound).all())
     assert torch.equal(linear_small_fwd_bf16(H, W, b), got)  # run to run
     # strided rows (a view inside a wider tensor)
     wide = torch.zeros(M, K + 16, dtype=BF, device=DEV)
@@ -190,3 +196,30 @@ def test_bf16_model_uses_narrow_kernels():
     assert torch.isfinite(loss).item()
     for k, p in model.named_parameters():
         assert p.grad is not None and bool(torch.isfinite(p.grad).all()), k
+
+
+def test_bf16_heads_colsum_handoff_is_used():
+    """The bf16 heads' backward hands the last hidden layer its bias column sums (computed in the
+    same pass); the layer takes them only for the very gradient tensor the heads returned (identity
+    check, conv.py) -- in a plain model step that is always the case, so no separate colsum pass
+    runs for it (a replaced gradient would fall back to lpg_colsum_bf16, the same bits)."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, fc, synth
+    from lpgnn.train import balanced
+
+    gr = synth.uniform_lp(700, 1500, 7000, seed=4)
+    adj = BipartiteCSR.from_coo(gr.row, gr.col, gr.val, gr.m, gr.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(gr.x_s).to(DEV), x_t=torch.from_numpy(gr.x_t).to(DEV),
+                           y_s=torch.from_numpy(gr.y_s).to(DEV), y_t=torch.from_numpy(gr.y_t).to(DEV),
+                           edge_index=adj, s_bs=gr.m, t_bs=gr.n)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=256, depth=3, compute_dtype="bf16").to(DEV).train()
+    calls = []
+    orig = fc.colsum_bf16
+    fc.colsum_bf16 = lambda g: calls.append(g.shape) or orig(g)
+    try:
+        lc, lv = model(batch)
+        balanced(lc, lv, batch.y_s, batch.y_t).backward()
+        torch.cuda.synchronize()
+    finally:
+        fc.colsum_bf16 = orig
+    assert calls == [], calls

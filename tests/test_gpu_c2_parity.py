@@ -278,3 +278,62 @@ def test_c5_bf16_logits_and_step_vs_fp32_oracle(monkeypatch):
         cos_min = min(cos_min, cos)
         assert cos >= 0.95, (k, cos)
     print(f"c5 bf16 step: loss {loss.item():.5f} (MKL {r32['loss']:.5f}), min grad cosine {cos_min:.4f}")
+
+
+# ---- the reference's --fp16 inference mode at c2 (val.py:269 model.half(), utils.py:909-915) ----
+# The oracle is the fp16-storage evaluation (oracle.model_ref.gcn_fc_forward_fp16): every stored
+# tensor rounded to fp16, fp32 accumulation inside each op (MKL for the FC).  The HIP fp16 kernels
+# agree with it up to where an fp32 summation-order difference moves a value across an fp16 rounding
+# midpoint (one fp16 ulp, 2^-11 relative), propagated through the layers.  Bounds (round-4 measurement
+# printed by the test): heads within C2F16_HEAD_REL relative (Frobenius), logits' p99 within 4 fp16 ulps
+# of 16, every node beyond that explained by add_knowledge's amplification 10 * 2 |dh| / |h| (+ 2 ulps
+# of the output's rounding); inference_gnn labels equal except where such a node or an fp16 tie at the
+# top-m boundary decides.
+C2F16_HEAD_REL = 2e-3
+C2F16_LOGIT_P99 = 4 * 2.0 ** -7
+C2F16_LABEL_DIFF_MAX = 300
+
+
+def test_c2_fp16_eval_vs_fp16_oracle(monkeypatch):
+    from lpgnn import batch_to
+    from lpgnn.val import inference_gnn
+
+    g, A, AT = _graph()
+    sd = _weights(1024, 3)
+    keep = {}
+    with torch.no_grad():
+        rc, rv = O.gcn_fc_forward_fp16(sd, torch.from_numpy(g.x_s), torch.from_numpy(g.x_t), A, AT, 3, keep=keep)
+    ref, ref_h = torch.cat((rc, rv)).double(), torch.cat((keep["head_l"], keep["head_r"])).double()
+    model = _model(1024, 3).half().eval()
+    batch = batch_to(_batch(), DEV, half=True)
+    got, heads = _hip_eval_with_heads(model, batch, monkeypatch)
+    assert torch.isfinite(got).all()
+    dh = (heads - ref_h).norm(dim=-1)
+    dh_rel = (dh.norm() / ref_h.norm()).item()
+    d = (got - ref).abs().max(-1).values
+    hn = ref_h.norm(dim=-1)
+    lip = 10 * 2 * dh / hn * (1 + 1e-3) + 2 * 2.0 ** -7
+    beyond = d > C2F16_LOGIT_P99
+    p99 = float(torch.quantile(d.float(), 0.99))
+    print(f"c2 fp16 vs fp16 oracle: heads rel. {dh_rel:.2e} (max |dh| {dh.max():.2e}); logits mean {d.mean():.2e}, "
+          f"p99 {p99:.2e}, max {d.max():.3e}; {int(beyond.sum())} nodes beyond 4 ulps, all explained: "
+          f"{bool((d[beyond] <= lip[beyond]).all())}")
+    assert dh_rel <= C2F16_HEAD_REL
+    assert p99 <= C2F16_LOGIT_P99
+    assert bool((d[beyond] <= lip[beyond]).all()), "a logit difference not explained by add_knowledge's amplification"
+    # against the fp32 MKL oracle: the fp16 mode's own error class (printed; bounded loosely)
+    r32 = _oracle(1024, 3, torch.float32, False)
+    d32 = (got - r32["logits"].double()).abs()
+    agree32 = (got.argmax(-1) == r32["logits"].argmax(-1)).double().mean().item()
+    print(f"c2 fp16 vs fp32 MKL: mean |d| {d32.mean():.3e}, argmax agreement {agree32:.5f}")
+    assert d32.mean().item() <= 0.05 and agree32 >= 0.99
+    # basis labels: the fp16 rule on both sides
+    labels = inference_gnn(got.half().to(DEV), g.m).cpu()  # (got holds the fp16 logits exactly)
+    rl = O.inference_gnn_fp16(ref.float(), g.m)
+    diff = labels != rl
+    p1 = O.r16(torch.softmax(ref.float(), -1))[:, 1]
+    thr = p1.topk(g.m).values[-1]
+    boundary = (p1 == thr) | beyond | (d > 0)
+    print(f"c2 fp16 labels: {int(diff.sum())} differences of {labels.numel()}, "
+          f"{int((diff & ~boundary).sum())} at nodes whose logits agree exactly and are not tied at the threshold")
+    assert int(diff.sum()) <= C2F16_LABEL_DIFF_MAX

@@ -134,6 +134,64 @@ def _worker_dropout(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
+def _worker_general_dropout(rank, world, port, out_dir):
+    """A GENERAL plan (plan_partition's default owner: the rank with most of a variable's edges), whose
+    owned variables are not one contiguous id range, in train mode with dropout 0.1: every owned row
+    is keyed by its global id (row_keys), so the partitioned step equals the one-GPU step with the
+    same seeds -- logits of owned and halo rows, loss, gradients."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, partition as part, synth
+        from lpgnn.train import balanced
+
+        dev = "cuda:0"
+        g = synth.block_lp(4000, 8000, 80000, parts=2, rho=0.6, seed=1)  # weak blocks: scattered owners
+        plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
+        batch = part.make_local_batch(plan, g.x_s, g.x_t, g.y_s, g.y_t, device=dev)
+        contiguous = plan.owned[-1] - plan.owned[0] + 1 == plan.n_own
+        gaps = torch.tensor([0 if contiguous else 1])
+        dist.all_reduce(gaps)
+        assert gaps.item() >= 1, "the general owner rule should give some rank a non-contiguous owned set"
+        assert (batch.edge_index.ex.var_keys is None) == bool(contiguous)
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=256, depth=4, dp=0.1).to(dev).train()
+        sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        torch.manual_seed(7)
+        lc, lv = model(batch)
+        loss = part.balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.n_own)
+        loss.backward()
+        part.all_reduce_grads(model)
+        tot = loss.detach().clone()
+        part._all_reduce_(tot)
+        adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
+        b = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(dev), x_t=torch.from_numpy(g.x_t).to(dev),
+                           y_s=torch.from_numpy(g.y_s).to(dev), y_t=torch.from_numpy(g.y_t).to(dev),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+        ref = GCN_FC(8, 8, hids=256, depth=4, dp=0.1).to(dev).train()
+        ref.load_state_dict(sd0)
+        torch.manual_seed(7)  # the same dropout seeds
+        rc, rv = ref(b)
+        rl = balanced(rc, rv, b.y_s, b.y_t)
+        rl.backward()
+        np.testing.assert_allclose(lc.detach().cpu().numpy(), rc.detach().cpu().numpy()[plan.row_lo:plan.row_hi],
+                                   atol=1e-4)
+        np.testing.assert_allclose(lv.detach().cpu().numpy(), rv.detach().cpu().numpy()[plan.local_vars], atol=1e-4)
+        assert abs(tot.item() - rl.item()) < 1e-4 * max(1.0, abs(rl.item())), (tot.item(), rl.item())
+        for k, p in model.named_parameters():
+            np.testing.assert_allclose(p.grad.cpu().numpy(), dict(ref.named_parameters())[k].grad.cpu().numpy(),
+                                       rtol=2e-3, atol=2e-5, err_msg=k)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_general_plan_dropout_keys_equal_one_gpu(tmp_path):
+    mp.spawn(_worker_general_dropout, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+
+
 def test_partitioned_fused_heads_with_dropout(tmp_path):
     mp.spawn(_worker_dropout, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()

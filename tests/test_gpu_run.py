@@ -25,7 +25,7 @@ def _args(tmp_path, *extra):
 
 
 def test_run_exp_two_epochs_checkpoint_and_validation(tmp_path):
-    from lpgnn import GCN_FC, run
+    from lpgnn import GCN_FC, batch_to, run
 
     # graphs of 600, 500, 800 (> threshold 700: NeighborLoader path) and 400 edges
     write_dataset(str(tmp_path / "data" / "synth" / "highs-inp_tgt"), k=4)
@@ -48,32 +48,35 @@ def test_run_exp_two_epochs_checkpoint_and_validation(tmp_path):
         assert torch.equal(model.state_dict()[k].cpu(), v)
     _, acc, rows = run.validation(model, ds, vargs)
     assert 0.0 <= acc <= 1.0 and len(rows) == 4
-    # --fp16: the bf16 compute path for evaluation (val.py:269); training stays fp32 whatever the
-    # flag (the reference's train.py never reads it); logits close to the fp32 model's
+    # --fp16: model.half() on the evaluation model (val.py:269), every batch through batch_to(half=True);
+    # training stays fp32 whatever the flag (the reference's train.py never reads it); logits close to
+    # the fp32 model's
     fargs = _args(tmp_path, "--load_from", hist["checkpoint"], "--fp16", "1")
-    assert run.make_model(fargs).compute_dtype == torch.float32
+    assert next(run.make_model(fargs).parameters()).dtype == torch.float32
     m16 = run.make_model(fargs, for_eval=True)
-    assert m16.compute_dtype == torch.bfloat16
+    assert next(m16.parameters()).dtype == torch.float16
+    _, acc16, _ = run.validation(m16, ds, fargs)
+    assert 0.0 <= acc16 <= 1.0
     g = ds[0].to(args.dev)
     with torch.no_grad():
         a = torch.cat(model.eval()(g))
-        b = torch.cat(m16.eval()(g))
-    assert b.dtype == torch.float32 and (a - b).abs().mean().item() < 0.05
+        b = torch.cat(m16.eval()(batch_to(g, args.dev, half=True)))
+    assert b.dtype == torch.float16 and (a - b.float()).abs().mean().item() < 0.05
 
 
-def test_half_model_or_batch_is_refused():
-    """val.py:269 model.half() / batch_to(half=True): no fp16 kernels here --
-    a clear error instead of a silent fp32 run."""
+def test_half_model_trains_refused_eval_runs():
+    """val.py:269 model.half() / batch_to(half=True) is the reference's inference mode: eval runs on the
+    fp16 kernels (fp16 logits); a training forward is refused with a clear error (the reference never
+    trains in fp16)."""
     from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, batch_to, synth
 
     g = synth.uniform_lp(50, 80, 400, seed=1)
     adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda:0")
     b = BipartiteBatch(x_s=torch.from_numpy(g.x_s), x_t=torch.from_numpy(g.x_t), y_s=torch.from_numpy(g.y_s),
                        y_t=torch.from_numpy(g.y_t), edge_index=adj, s_bs=g.m, t_bs=g.n)
-    model = GCN_FC(8, 8, hids=32, depth=3).cuda().eval()
-    with pytest.raises(TypeError, match="float16"):
-        model(batch_to(b, "cuda:0", half=True))
-    b = batch_to(BipartiteBatch(x_s=torch.from_numpy(g.x_s), x_t=torch.from_numpy(g.x_t), y_s=torch.from_numpy(g.y_s),
-                                y_t=torch.from_numpy(g.y_t), edge_index=adj, s_bs=g.m, t_bs=g.n), "cuda:0")
-    with pytest.raises(TypeError, match="float16"):
-        model.half()(b)
+    model = GCN_FC(8, 8, hids=32, depth=3).cuda().half().eval()
+    with torch.no_grad():
+        lc, lv = model(batch_to(b, "cuda:0", half=True))
+    assert lc.dtype == torch.float16 and torch.isfinite(lc).all() and torch.isfinite(lv).all()
+    with pytest.raises(RuntimeError, match="inference mode"):
+        model.train()(b)

@@ -225,7 +225,7 @@ def test_x3_rejects_bad_shapes():
     w = torch.zeros(3, 4, 40, dtype=torch.int16, device=DEV)
     c = torch.zeros(4, 4, device=DEV)
     st = L.lpg_fc_x3_f32(4, 4, 40, a.data_ptr(), 40, w.data_ptr(), 40, 160, 0, None, 0, None, 0, 0, None,
-                         c.data_ptr(), 4, 0, 0.0, 0, 0, None)
+                         c.data_ptr(), 4, 0, 0.0, 0, 0, None, None)
     assert st != 0 and b"multiples of 32" in L.lpg_last_error()
 
 

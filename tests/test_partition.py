@@ -82,7 +82,7 @@ def _cpu_local_spmm(adj, x):
     return O.spmm_t(fwd, bwd, x)
 
 
-def _cpu_graph_conv_fc(agg, x_dst, w_rel, b_rel, w_root, relu, dropout=0.0):
+def _cpu_graph_conv_fc(agg, x_dst, w_rel, b_rel, w_root, relu, dropout=0.0, row_offset=0, row_keys=None):
     out = F.linear(agg, w_rel, b_rel) + F.linear(x_dst, w_root)
     out = torch.relu(out) if relu else out
     return F.dropout(out, p=dropout, training=True) if dropout > 0 else out
@@ -257,3 +257,28 @@ def test_rho_sweep_boundary_counts(tmp_path):
     identically on every rank, equal to the bench's own plan at the bench rho."""
     mp.spawn(_worker_rho, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+
+
+def test_exchange_dropout_keys_are_global_ids():
+    """Every owned variable's dropout row is keyed by its global id: one row_offset when the owned
+    set is one contiguous range (block plans), the owned id list (row_keys) when it is not (the
+    general owner rule on a weakly blocked graph); constraint rows by row_lo + i."""
+    from lpgnn import synth
+    from lpgnn.partition import Exchange, plan_partition
+
+    g = synth.block_lp(400, 800, 8000, parts=2, rho=0.6, seed=1)
+    scattered = 0
+    for r in range(2):
+        p = plan_partition(g.row, g.col, g.val, g.m, g.n, 2, r)
+        ex = Exchange(p, "cpu")
+        assert ex.cons_key_args == {"row_offset": p.row_lo, "row_keys": None}
+        if p.owned[-1] - p.owned[0] + 1 == p.n_own:
+            assert ex.var_keys is None and ex.var_key_args["row_offset"] == p.owned[0]
+        else:
+            scattered += 1
+            assert np.array_equal(ex.var_key_args["row_keys"].numpy(), p.owned)
+    assert scattered >= 1
+    g = _graph()
+    p = plan_partition(g.row, g.col, g.val, g.m, g.n, 2, 1, bounds=[0, 120, 240],
+                       owner=(np.arange(g.n) * 2) // g.n)
+    assert Exchange(p, "cpu").var_keys is None

@@ -184,15 +184,16 @@ def test_data_parallel_replicas_gloo(tmp_path):
 
 
 def test_fp16_flag_is_validation_only(tmp_path):
-    """--fp16 (utils.py:770) changes only the evaluation model (val.py:269 model.half(); here bf16):
+    """--fp16 (utils.py:770) changes only the evaluation model (val.py:269 model.half()):
     train.py trains in fp32 whatever the flag, and so does run_exp's model."""
     from lpgnn import run
 
+    dt = lambda m: next(m.parameters()).dtype  # noqa: E731
     a = _args(tmp_path, "--fp16", "1", "--arch", "GCN_FC(8,8,hids=16,depth=3)")
-    assert run.make_model(a).compute_dtype == torch.float32
-    assert run.make_model(a, for_eval=True).compute_dtype == torch.bfloat16
+    assert dt(run.make_model(a)) == torch.float32
+    assert dt(run.make_model(a, for_eval=True)) == torch.float16
     b = _args(tmp_path, "--arch", "GCN_FC(8,8,hids=16,depth=3)")
-    assert run.make_model(b, for_eval=True).compute_dtype == torch.float32
+    assert dt(run.make_model(b, for_eval=True)) == torch.float32
 
 
 def test_dataset_reads_each_graph_once(tmp_path, monkeypatch):
