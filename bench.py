@@ -18,7 +18,8 @@ One workload family at every N (the line the driver turns into a scaling curve):
   graph on one GPU at N=1, row-partitioned over the N ranks at N>1 (STRONG scaling), with the
   locality (rho) sweep of the partition at N>1.
 * sub-record ``inference`` (N=1) -- the reference's own timed path (scripts/pred_basis.py:157-176):
-  eval-mode model(batch) + inference_gnn on c2, ms/graph, with the oracle's CPU inference beside it.
+  eval-mode model(batch) + inference_gnn on c2, ms/graph, with the oracle's CPU inference beside it;
+  ``inference_fp16`` the same after model.half() + batch_to(half=True) (its --fp16 mode, val.py:269).
 
 With --gpus N > 1 and no RANK / WORLD_SIZE in the environment, bench.py launches the N ranks
 itself (one child process per GPU, started before this process touches the GPU; rank 0 prints
@@ -80,9 +81,10 @@ def parse(argv=None):
                     help="time eval-mode forward + inference_gnn (the reference's timed path) instead of training")
     ap.add_argument("--fp16", action="store_true",
                     help="with --inference: the reference's --fp16 mode (model.half(), batch_to(half=True))")
-    ap.add_argument("--sub", default="c4,inference",
+    ap.add_argument("--sub", default="c4,inference,inference_fp16",
                     help="sub-records after the headline ('' = none): c4 (configs[3] at the same N), "
-                         "inference (N=1: the reference's timed eval path on c2)")
+                         "inference (N=1: the reference's timed eval path on c2), inference_fp16 (the same in "
+                         "the reference's --fp16 mode)")
     ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--c4-warmup", type=int, default=2)
     ap.add_argument("--c4-scale", type=int, default=1, help="c4 sub-record at 1/scale size (rehearsals)")
@@ -656,6 +658,11 @@ def main():
         a_inf.inference = True
         rec, _ = run_inference(ctx, a_inf, args.inf_steps, 3, False, with_cpu=rank == 0)
         out["inference"] = rec
+    if "inference_fp16" in subs and not args.inference and world == 1 and not args.partitioned and args.config == "c2":
+        a_inf = copy.copy(args)
+        a_inf.inference, a_inf.fp16 = True, True
+        rec, _ = run_inference(ctx, a_inf, args.inf_steps, 3, True, with_cpu=rank == 0)
+        out["inference_fp16"] = rec
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

@@ -248,6 +248,26 @@ lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1
                                int64_t row_offset, const int64_t *row_keys, int32_t hn, const float *hw, int64_t ldhw,
                                const float *hb, float *logits, int64_t ldl, void *workspace, void *stream);
 
+/* An input-gradient GEMM of lpg_fc_x3_f32 (same A / W / K / lda / ldw / plane arguments; flags: only
+ * LPG_FC_ACCUMULATE, C then holding the addend, read and never written) whose result g [M, N] is the
+ * gradient of a ReLU layer's output Y [M, N] (ldy) computed from ks1 + ks2 <= 16 input features
+ * X1 [M, ks1], X2 [M, ks2] -- conv1 of GCN_FC (arch.py:170, 181-182), no dropout: instead of storing g,
+ * the epilogue forms dZ = (Y > 0) ? g : 0 and each 128-row tile writes its partial sums of
+ * dZ^T [X1 | X2 | 1] to the workspace, folded in tile order into that layer's weight gradients
+ *   dW1 [N, ks1] = dZ^T X1,  dW2 [N, ks2] = dZ^T X2,  db [N] = sum_m dZ   (any of them may be NULL)
+ * -- the gradient never makes the round trip through HBM that lpg_relu_wgrad_smallk_f32 reads back.
+ * Tolerance-level like every weight gradient here (fp32 fma chains per tile, tiles folded in order;
+ * deterministic).  Needs the wide x3 kernel's operand rules (lda1 == lda2, ldw1 == ldw2, ps1 == ps2)
+ * -- otherwise LPG_ERR_INVALID and the caller takes the two-pass route.  Workspace:
+ * lpg_fc_x3_relu_wgrad_workspace_bytes(M, N, ks1 + ks2), 16-byte aligned. */
+int64_t lpg_fc_x3_relu_wgrad_workspace_bytes(int64_t M, int64_t N, int64_t K);
+lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                    const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                    int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *C,
+                                    int64_t ldc, int32_t flags, const float *Y, int64_t ldy, int64_t ks1,
+                                    const float *X1, int64_t ldx1, int64_t ks2, const float *X2, int64_t ldx2,
+                                    float *dW1, float *dW2, float *db, void *workspace, void *stream);
+
 /* Weight gradient on the same arithmetic: dW[n, k] = sum_r G[r, n] X[r, k]
  * (G = dZ [R, N], ldg; X = the layer input [R, K], ldx; dW [N, K], lddw, the
  * torch Linear weight layout) -- the lin_rel / lin_root weight gradients of

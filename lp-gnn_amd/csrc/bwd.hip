@@ -807,6 +807,26 @@ lpg_status wgrad_smallk(int64_t M, int64_t N, const void *dz, int64_t ldz, const
   return LPG_OK;
 }
 
+}  // namespace
+
+// The fold of a small-K weight-gradient partial image [nblk][K + 1][N] (rows = blocks of rows) into
+// dW1 [N, K1], dW2 [N, K - K1], db [N] in block order -- wgrad_smallk's tail, shared with the x3 FC's
+// fused conv1 weight gradient (fc_x3.hip, lpg_fc_x3_relu_wgrad_f32).  seg: smallk_fold_floats floats
+// after part (the segment sums).
+int64_t smallk_fold_floats(int64_t nblk, int64_t KR, int64_t N) { return fold_floats(nblk, KR * N); }
+
+lpg_status smallk_fold(int64_t nblk, int64_t N, int K1, int K, const float *part, float *seg, float *dW1, float *dW2,
+                       float *db, hipStream_t s) {
+  const int64_t KR = K + 1;
+  const float *img;
+  const int64_t nrow = fold(nblk, KR * N, part, seg, &img, s);
+  hipLaunchKernelGGL(wgrad_smallk_p2, dim3((unsigned)((KR * N + kT - 1) / kT)), dim3(kT), 0, s, nrow, N, K, (int)KR,
+                     K1, img, dW1, dW2, db);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+namespace {
 int64_t heads_bwd_floats(int64_t M, int64_t K, int64_t N) {
   const int64_t nblk = (M + kRowsLinear - 1) / kRowsLinear, nchunk = (M + kRowsColsum - 1) / kRowsColsum;
   return fold_floats(nblk, N * K + N) + fold_floats(nchunk, K);

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "lpgnn.h"
+
 namespace lpg {
 
 // Counter-based dropout RNG over (seed, row, col): two rounds of the 32-bit
@@ -74,6 +76,12 @@ __device__ __forceinline__ uint32_t relu_bwd_pk_bf16(uint32_t g, uint32_t y, flo
 // global load and store the wave has in flight -- a streaming kernel that stages rows in LDS
 // drained its prefetched loads (and its stores) at each such barrier.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// bwd.hip: the fold of a small-K weight-gradient partial image [nblk][K + 1][N] into dW1 [N, K1],
+// dW2 [N, K - K1], db [N] (block order); the part + segment floats it needs
+int64_t smallk_fold_floats(int64_t nblk, int64_t KR, int64_t N);
+lpg_status smallk_fold(int64_t nblk, int64_t N, int K1, int K, const float *part, float *seg, float *dW1, float *dW2,
+                       float *db, hipStream_t s);
 
 // Host-side dropout threshold / scale shared by the FC entry points.
 inline void dropout_params(float p, uint32_t *thresh, float *scale) {

@@ -76,6 +76,14 @@ struct X3Args {
   int64_t row_off;  // the dropout key of row m is row_keys[m] if given, else row_off + m (drop_row)
   int32_t store;    // 0: C is not written (LPG_FC_HEADS_ONLY: the logits are the only output)
   const int64_t *row_keys;
+  // fused small-K weight gradient (fc_x3_wide WGK, lpg_fc_x3_relu_wgrad_f32): this GEMM's output g is the
+  // gradient of a ReLU layer's output wy [M, N] whose inputs were [wx1 | wx2] (wk1 + wk2 <= 16 features,
+  // conv1); each block writes the partial sums over its rows of dZ^T [wx1 | wx2 | 1], dZ = (wy > 0) ? g : 0,
+  // to wpart[m-tile][k][n] (k < wk1 + wk2 + 1); g itself is not stored
+  const float *wy, *wx1, *wx2;
+  int64_t ldwy, ldwx1, ldwx2;
+  int32_t wk1, wk2;
+  float *wpart;
 };
 
 // dst plane p [rows, cols] (ldd) = term p of src (transposed: src is [cols, rows]).
@@ -379,7 +387,7 @@ lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
 // k order and product sequence per output as fc_fwd_x3_16: the same C, bit for bit.
 // Requires lda1 == lda2, ldw1 == ldw2, ps1 == ps2 (one offset set for both k phases; the host
 // falls back to fc_fwd_x3_16 otherwise).
-template <int WM, int TM, int TN, int MINW, bool RELU, bool HEADS>
+template <int WM, int TM, int TN, int MINW, bool RELU, bool HEADS, bool WGK = false>
 __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   constexpr int NW = WM;
   constexpr int BM = WM * TM * 16, BN = TN * 16;
@@ -397,8 +405,16 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   const int64_t bid = blockIdx.x;
   const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
   const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
+#if defined(LPG_X3_TRAFFIC_PROBE)
+  // probe builds only (tools/experiments/x3_traffic_probe.py; wrong results by design): every block
+  // reads one W column slice (1: the A panels' traffic alone) or one A row panel (2: the W slices'
+  // traffic alone), with the default schedule of the other operand
+  const int64_t m0 = LPG_X3_TRAFFIC_PROBE == 2 ? 0 : (wgid / a.nt) * BM;
+  const int64_t n0 = LPG_X3_TRAFFIC_PROBE == 1 ? 0 : (wgid % a.nt) * BN;
+#else
   const int64_t m0 = (wgid / a.nt) * BM;
   const int64_t n0 = (wgid % a.nt) * BN;
+#endif
   const int64_t mrows = a.M - m0 < BM ? a.M - m0 : BM;  // rows of this block (>= 1)
   const int64_t ncols = a.N - n0 < BN ? a.N - n0 : BN;
 
@@ -527,6 +543,66 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   // loop, without 24 partial sums live beside the 64 outputs (that form spilled)
   constexpr int HC = HEADS ? 3 : 1;
   constexpr int HP = BN + 4;  // image row pitch (floats): rows 4 fg apart land 16 banks apart
+  if constexpr (WGK) {
+    // conv1's weight gradient folded into this input-gradient GEMM (the hidden layer's dZ W for the
+    // conv1 output): dZ = (Y > 0) ? g : 0 (conv1: ReLU, no dropout) into per-wave LDS images, the
+    // block's [BM][wk1 + wk2] input rows beside them, then each thread sums one column's dZ * x over
+    // the block's rows in row order (half the k per thread) -- one partial per (m-tile, k, n); g, the
+    // [M, N] gradient the separate pass re-read with Y, is never stored
+    constexpr int KMAX = 16, KH = (KMAX + 2) / 2;  // k + the bias row, split over two threads
+    static_assert(NW * 64 == 2 * BN, "two threads per output column");
+    static_assert((NW * TM * 16 * HP + BM * KMAX) * 4 <= 2 * TILE_BYTES, "images fit the tile buffers");
+    float *const wimg = reinterpret_cast<float *>(smem);
+    float *const xs = wimg + NW * TM * 16 * HP;
+    const int ks = a.wk1 + a.wk2;
+    const bool inner = mw + TM * 16 <= a.M && nw + BN <= a.N;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = nw + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = mw + i * 16 + 4 * fg + r;
+          const bool ok = inner || (row < a.M && col < a.N);
+          const int64_t rr = ok ? row : 0, cc = ok ? col : 0;
+          float g = acc[i][j][r];
+          if (a.accum) g = g + a.C[rr * a.ldc + cc];
+          const float y = a.wy[rr * a.ldwy + cc];
+          wimg[wave * (TM * 16 * HP) + (i * 16 + 4 * fg + r) * HP + j * 16 + fr] = (ok && y > 0.f) ? g : 0.f;
+        }
+    }
+    for (int q = tid; q < BM * KMAX; q += NW * 64) {
+      const int r = q / KMAX, k = q % KMAX;
+      const int64_t row = m0 + r;
+      float x = 0.f;
+      if (row < a.M && k < ks) x = k < a.wk1 ? a.wx1[row * a.ldwx1 + k] : a.wx2[row * a.ldwx2 + (k - a.wk1)];
+      xs[q] = x;
+    }
+    __syncthreads();
+    const int c = tid % BN, kb = (tid / BN) * KH;
+    float sk[KH];
+#pragma unroll
+    for (int u = 0; u < KH; ++u) sk[u] = 0.f;
+    for (int r = 0; r < BM; ++r) {
+      const float d = wimg[(r / (TM * 16)) * (TM * 16 * HP) + (r % (TM * 16)) * HP + c];
+      const float *xr = xs + r * KMAX;
+#pragma unroll
+      for (int u = 0; u < KH; ++u) {
+        const int k = kb + u;  // (k == ks: the bias row, x = 1)
+        const float x = k < ks ? xr[k < KMAX ? k : 0] : 1.f;
+        sk[u] = __builtin_fmaf(d, x, sk[u]);
+      }
+    }
+    const int64_t col = nw + c;
+    if (col < a.N) {
+      float *const pp = a.wpart + (m0 / BM) * (int64_t)(ks + 1) * a.N + col;
+#pragma unroll
+      for (int u = 0; u < KH; ++u)
+        if (kb + u <= ks) pp[(int64_t)(kb + u) * a.N] = sk[u];
+    }
+    return;
+  }
   static_assert(!HEADS || NW * TM * 16 * HP * 4 <= 2 * TILE_BYTES, "heads image fits the tile buffers");
   float *const himg = reinterpret_cast<float *>(smem) + wave * (TM * 16 * HP) + 4 * fg * HP + fr;
   auto hput = [&](int i, int r, int j, float v) {
@@ -675,13 +751,18 @@ bool wide_ok(const X3Args &a, int64_t BM, int64_t BN) {
   return (BM * a.lda1 + K) * 4 < ((int64_t)1 << 31) && (2 * a.ps1 + BN * a.ldw1 + K) * 2 < ((int64_t)1 << 31);
 }
 
-template <int WM, int TM, int TN, int MINW, bool HEADS = false>
+template <int WM, int TM, int TN, int MINW, bool HEADS = false, bool WGK = false>
 lpg_status launch_x3_wide(X3Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * TM * 16, BN = TN * 16, NT = 64 * WM;
   a.mt = (a.M + BM - 1) / BM;
   a.nt = (a.N + BN - 1) / BN;
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
+  if constexpr (WGK) {
+    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, false, false, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    LPG_HIP(hipGetLastError());
+    return LPG_OK;
+  }
   if (relu)
     hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, true, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   else
@@ -1049,4 +1130,57 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   hipLaunchKernelGGL(wgrad_fold, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, N, K, S_used, part, dW, lddw);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
+}
+
+// ---- the conv1 weight gradient folded into the input-gradient GEMM ----------
+extern "C" int64_t lpg_fc_x3_relu_wgrad_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K < 1 || K > 16) return 0;
+  return smallk_fold_floats((M + 127) / 128, K + 1, N) * (int64_t)sizeof(float);
+}
+
+extern "C" lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                               const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2,
+                                               const float *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
+                                               int64_t ps2, const float *C, int64_t ldc, int32_t flags, const float *Y,
+                                               int64_t ldy, int64_t ks1, const float *X1, int64_t ldx1, int64_t ks2,
+                                               const float *X2, int64_t ldx2, float *dW1, float *dW2, float *db,
+                                               void *workspace, void *stream) {
+  const char *name = "lpg_fc_x3_relu_wgrad_f32";
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "%s: negative size", name);
+  LPG_REQUIRE((flags & ~LPG_FC_ACCUMULATE) == 0, "%s: only the accumulate flag is accepted, got 0x%x", name, flags);
+  LPG_REQUIRE(ks1 >= 0 && ks2 >= 0 && ks1 + ks2 >= 1 && ks1 + ks2 <= 16, "%s: need 1 <= ks1 + ks2 <= 16", name);
+  LPG_REQUIRE(Y && ldy >= N && (ks1 == 0 || (X1 && ldx1 >= ks1)) && (ks2 == 0 || (X2 && ldx2 >= ks2)),
+              "%s: bad Y / X1 / X2", name);
+  LPG_REQUIRE(!(flags & LPG_FC_ACCUMULATE) || (C && ldc >= N), "%s: the accumulate flag needs C", name);
+  const int64_t ks = ks1 + ks2;
+  hipStream_t s = as_stream(stream);
+  if (M == 0 || N == 0) {
+    if (dW1 && N * ks1) LPG_HIP(hipMemsetAsync(dW1, 0, sizeof(float) * N * ks1, s));
+    if (dW2 && N * ks2) LPG_HIP(hipMemsetAsync(dW2, 0, sizeof(float) * N * ks2, s));
+    if (db && N) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, s));
+    return LPG_OK;
+  }
+  LPG_REQUIRE(workspace && aligned16(workspace), "%s: workspace missing or not 16-byte aligned", name);
+  X3Args a;
+  // (C is only read -- the addend -- and never written here; without the flag Y stands in for it)
+  const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, nullptr,
+                                const_cast<float *>(C ? C : Y), C ? ldc : ldy, flags, 0.f, 0, 0, nullptr, &a);
+  if (st != LPG_OK) return st;
+  a.store = 0;
+  LPG_REQUIRE(wide_ok(a, 128, 128), "%s: operands the wide kernel does not take (lda1 == lda2, ldw1 == ldw2, "
+              "ps1 == ps2, 32-bit offsets)", name);
+  a.wy = Y;
+  a.ldwy = ldy;
+  a.wx1 = X1;
+  a.ldwx1 = ldx1;
+  a.wx2 = X2;
+  a.ldwx2 = ldx2;
+  a.wk1 = (int32_t)ks1;
+  a.wk2 = (int32_t)ks2;
+  float *part = static_cast<float *>(workspace);
+  a.wpart = part;
+  lpg_status r = launch_x3_wide<4, 2, 8, 2, false, true>(a, false, s);
+  if (r != LPG_OK) return r;
+  const int64_t mt = (M + 127) / 128;
+  return smallk_fold(mt, N, (int)ks1, (int)ks, part, part + mt * (ks + 1) * N, dW1, dW2, db, s);
 }

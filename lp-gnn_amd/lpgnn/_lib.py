@@ -45,6 +45,8 @@ HEADER_SYMBOLS = (
     "lpg_fc_x3_f32",
     "lpg_fc_x3_heads_workspace_bytes",
     "lpg_fc_x3_heads_f32",
+    "lpg_fc_x3_relu_wgrad_workspace_bytes",
+    "lpg_fc_x3_relu_wgrad_f32",
     "lpg_wgrad_x3_workspace_bytes",
     "lpg_wgrad_x3_f32",
     "lpg_weighted_ce_workspace_bytes",
@@ -164,6 +166,12 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_x3_heads_workspace_bytes.restype = c_i64
     L.lpg_fc_x3_heads_f32.argtypes = L.lpg_fc_x3_f32.argtypes[:-1] + [c_i32, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p]
     L.lpg_fc_x3_heads_f32.restype = c_i32
+    L.lpg_fc_x3_relu_wgrad_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
+    L.lpg_fc_x3_relu_wgrad_workspace_bytes.restype = c_i64
+    L.lpg_fc_x3_relu_wgrad_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
+                                           c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p,
+                                           c_i64, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_fc_x3_relu_wgrad_f32.restype = c_i32
     L.lpg_wgrad_x3_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
     L.lpg_wgrad_x3_workspace_bytes.restype = c_i64
     L.lpg_wgrad_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p]

@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import ast
 import math
-import os
 import re
 from typing import Optional, Tuple
 
@@ -30,9 +29,7 @@ from torch import Tensor, nn
 from .sparse import BipartiteCSR, spmm
 from . import conv as _conv
 from . import fc as _fc
-
-# LPGNN_FUSE_HEADS=0: heads as their own autograd node (the last layer's ReLU backward then runs separately)
-FUSE_HEADS = os.environ.get("LPGNN_FUSE_HEADS", "1") == "1"
+from .options import DEFAULT as _DEFAULT_OPTIONS, PathOptions
 
 
 class Linear(nn.Module):
@@ -88,16 +85,17 @@ class GraphConv(nn.Module):
         self.lin_root.reset_parameters()
 
     def forward(self, x, edge_index: BipartiteCSR, edge_weight=None, size=None, relu: bool = False,
-                dropout: float = 0.0) -> Tensor:
+                dropout: float = 0.0, opts: PathOptions | None = None) -> Tensor:
         if isinstance(x, Tensor):
             x = (x, x)
         if edge_weight is not None:
             raise NotImplementedError("edge weights come from the adjacency values (arch.py:77)")
+        arith = (opts or _DEFAULT_OPTIONS).arith
 
         def fc(agg, x_dst, **keys):  # lin_rel + lin_root, ReLU and (training) dropout fused in one kernel
             # keys: the dropout row keys of a partition's rows (row_offset / row_keys, lpgnn.partition)
             return _fc.graph_conv_fc(agg, x_dst, self.lin_rel.weight, self.lin_rel.bias, self.lin_root.weight, relu,
-                                     dropout, **keys)
+                                     dropout, arith=arith, **keys)
 
         pc = getattr(edge_index, "partitioned_conv", None)  # row-partitioned multi-GPU adjacency
         if pc is not None:
@@ -114,22 +112,25 @@ class GraphConvTwoDirection(nn.Module):
         self.right2left = GraphConv((right_dim, left_dim), out_dim)
 
     def forward(self, left_feas, right_feas, edge_index: BipartiteCSR, edge_weight=None, relu: bool = False,
-                dropout: float = 0.0, fold_in: bool = False):
+                dropout: float = 0.0, fold_in: bool = False, opts: PathOptions | None = None):
         # edge_index is A (m x n, rows = cons).  arch.py:71-74: l2r = A^T, r2l = A.
+        opts = opts or _DEFAULT_OPTIONS
         if edge_weight is None and isinstance(edge_index, BipartiteCSR) and \
                 getattr(edge_index, "partitioned_conv", None) is None:
             # one autograd node for both directions (lpgnn.conv): same forward,
             # fused gradient sums and the cheaper association in backward
             return _conv.two_direction(left_feas, right_feas, edge_index, self.left2right, self.right2left,
-                                       relu, dropout, fold_in)
+                                       relu, dropout, fold_in, opts)
         tdc = getattr(edge_index, "two_direction_conv", None)  # row-partitioned multi-GPU adjacency
         if tdc is not None and edge_weight is None:
-            out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout)
+            out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout, opts)
             if out is not None:
                 return out
         l2r, r2l = edge_index.t(), edge_index
-        right_updated = self.left2right((left_feas, right_feas), l2r, edge_weight, relu=relu, dropout=dropout)
-        left_updated = self.right2left((right_feas, left_feas), r2l, edge_weight, relu=relu, dropout=dropout)
+        right_updated = self.left2right((left_feas, right_feas), l2r, edge_weight, relu=relu, dropout=dropout,
+                                        opts=opts)
+        left_updated = self.right2left((right_feas, left_feas), r2l, edge_weight, relu=relu, dropout=dropout,
+                                       opts=opts)
         return left_updated, right_updated
 
 
@@ -152,8 +153,11 @@ class GCNBase(nn.Module):
 class GCN_FC(GCNBase):
     """arch.py:167-193."""
 
-    def __init__(self, p, q, hids=128, depth=3, dp=.1, *args, compute_dtype=torch.float32, **kwargs):
+    def __init__(self, p, q, hids=128, depth=3, dp=.1, *args, compute_dtype=torch.float32,
+                 options: PathOptions | None = None, **kwargs):
         super().__init__()
+        # the kernel / fusion choices of this model's hot path (lpgnn.options; defaults from the environment)
+        self.options = options or _DEFAULT_OPTIONS
         # bf16 = the c5 configuration (BASELINE.json configs[4]): activations,
         # SpMM storage and FC operands in bf16 (fp32 accumulation, fp32 master
         # weights); logits return to fp32 before add_knowledge.
@@ -196,12 +200,13 @@ class GCN_FC(GCNBase):
                                    "+ model.eval()); train in fp32 or bf16")
             cd = torch.float16
         # conv -> ReLU (arch.py:181-182): the ReLU is the FC kernel's epilogue.
-        left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True)
+        opts = self.options
+        left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True, opts=opts)
         dp = self.dp if self.training else 0.0
         layers = list(self.layers)
         single = isinstance(edge_index, BipartiteCSR) and getattr(edge_index, "partitioned_conv", None) is None
         part_heads = getattr(edge_index, "two_direction_heads", None)  # row-partitioned multi-GPU adjacency
-        fuse_heads = FUSE_HEADS and len(layers) > 0 and cd == torch.float32 and (single or part_heads is not None)
+        fuse_heads = opts.fuse_heads and len(layers) > 0 and cd == torch.float32 and (single or part_heads is not None)
         for conv in (layers[:-1] if fuse_heads else layers):
             # conv -> dropout -> ReLU (arch.py:185-188).  ReLU commutes with
             # dropout (x * mask / (1-p), a non-negative scale), so the ReLU is
@@ -209,23 +214,24 @@ class GCN_FC(GCNBase):
             # partitioned run drops each variable once, at its owner).
             # fold_in: the previous layer's outputs feed only this layer (bf16: its ReLU/dropout
             # backward runs in this layer's input-gradient stores)
-            left, right = conv(left, right, edge_index, relu=True, dropout=dp, fold_in=True)
+            left, right = conv(left, right, edge_index, relu=True, dropout=dp, fold_in=True, opts=opts)
         out = None
         if fuse_heads:  # last layer + heads (arch.py:184-190) as one node: one backward pass over its output
             last = layers[-1]
             if single:
                 out = _conv.two_direction_heads(left, right, edge_index, last.left2right, last.right2left,
-                                                self.lin_left, self.lin_right, dp)
+                                                self.lin_left, self.lin_right, dp, fold_in=True, opts=opts)
             else:
-                out = part_heads(left, right, last.left2right, last.right2left, self.lin_left, self.lin_right, dp)
+                out = part_heads(left, right, last.left2right, last.right2left, self.lin_left, self.lin_right, dp,
+                                 opts)
                 if out is None:  # not applicable on this adjacency: the separate path
-                    left, right = last(left, right, edge_index, relu=True, dropout=dp)
+                    left, right = last(left, right, edge_index, relu=True, dropout=dp, opts=opts)
         if out is not None:
             left, right = out
         else:
             # both heads fold the last layer's ReLU/dropout backward (bf16) or neither does
-            left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias, fold_in=True)
-            right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias, fold_in=True)
+            left = _fc.linear(left, self.lin_left.weight, self.lin_left.bias, fold_in=True, opts=opts)
+            right = _fc.linear(right, self.lin_right.weight, self.lin_right.bias, fold_in=True, opts=opts)
         if half:  # arch.py:191 on the fp16 logits, in half precision (fp16 out, as the reference's)
             return add_knowledge(left, right, x_left, x_right)
         return add_knowledge(left.float(), right.float(), x_left, x_right)

@@ -35,28 +35,22 @@ tolerance-level (the reference's own backward is autograd through MKL).
 """
 from __future__ import annotations
 
-import os
+import functools
 
 import torch
 from torch import Tensor
 
 from . import fc as _fc
+from .options import DEFAULT, PathOptions
 from .sparse import BipartiteCSR, CSR, spmm_forward
 
 _GEMM_FLOPS = 160e12  # in-step rates used only to pick the cheaper association
 _SPMM_BYTES = 7e12
-# LPGNN_OVERLAP=1: run the HBM-bound SpMMs that are independent of the current FC / GEMM on a
-# second stream beside it.  Measured on c2: ~1 ms (2.6 %) more whole-step throughput in round 1; at
-# the round-3 kernels 20.88-21.09 against 21.05-21.08 ms (noise), while the overlapped SpMM launches
-# share CUs and HBM with the FC and read 0.85 of the roofline instead of 0.98 -- off by default
-# (DESIGN.md §6, §9).
-_OVERLAP = os.environ.get("LPGNN_OVERLAP", "0") == "1"
-REASSOCIATE = os.environ.get("LPGNN_REASSOC", "1") == "1"
-# LPGNN_FUSE_HEAD_FWD=0: the heads' forward as its own Linear kernels instead of in the last layer's FC epilogue
-FUSE_HEAD_FWD = os.environ.get("LPGNN_FUSE_HEAD_FWD", "1") == "1"
-# LPGNN_FOLD_RELU_BWD=0: in the bf16 (c5) model, keep the previous layer's ReLU/dropout backward as
-# its own pass (relu_bwd_colsum_bf16) instead of folding it into this layer's input-gradient store
-FOLD_RELU_BWD = os.environ.get("LPGNN_FOLD_RELU_BWD", "1") == "1"
+# options.overlap (LPGNN_OVERLAP=1): run the HBM-bound SpMMs that are independent of the current FC /
+# GEMM on a second stream beside it.  Measured on c2: ~1 ms (2.6 %) more whole-step throughput in
+# round 1; at the round-3 kernels 20.88-21.09 against 21.05-21.08 ms (noise), while the overlapped
+# SpMM launches share CUs and HBM with the FC and read 0.85 of the roofline instead of 0.98 -- off by
+# default.
 _SIDE = {}
 
 
@@ -66,17 +60,11 @@ def _side_stream(device):
     return _SIDE[device]
 
 
-def _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, p, seed, bf16):
-    if bf16:
-        return _fc.fc_forward_bf16(agg, w_rel, x_dst, w_root, b, relu, p, seed)
-    return _fc.fc_forward(agg, w_rel, x_dst, w_root, b, relu, p, seed)
-
-
-def reassociate(n_src: int, n_dst: int, f_src: int, f_out: int) -> bool:
+def reassociate(n_src: int, n_dst: int, f_src: int, f_out: int, enabled: bool = True) -> bool:
     """The association rule: lin_rel(S x) evaluated as S (x W_rel^T) iff the
     source side is the smaller node set and the SpMM does not get wider
-    (never worse on either the GEMM or the SpMM)."""
-    return REASSOCIATE and n_src < n_dst and f_out <= f_src
+    (never worse on either the GEMM or the SpMM); ``enabled`` = options.reassociate."""
+    return enabled and n_src < n_dst and f_out <= f_src
 
 
 def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
@@ -87,7 +75,7 @@ def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
 
 
 def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                  heads=None, heads_only=False):
+                  heads=None, heads_only=False, opts: PathOptions = DEFAULT):
     """The layer's forward (both directions); records on ctx what the backward
     needs and returns (left_new, right_new, tensors to save, logits).  With
     heads = ((Wh_l, bh_l), (Wh_r, bh_r)) the heads run in the FC epilogues
@@ -103,8 +91,9 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     seed_r = _fc._new_seed() if dropout > 0 else 0
     seed_l = _fc._new_seed() if dropout > 0 else 0
     f_out = ws[0].shape[0]
-    ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out)
-    ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out)
+    ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out, opts.reassociate)
+    ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out, opts.reassociate)
+    fwd32 = functools.partial(_fc.fc_forward, arith=opts.arith)
 
     hd = heads if heads is not None and not bf16 else (None, None)
     # no-grad (eval) forward of the heads layer: its output feeds only the heads, so the fused kernels
@@ -114,21 +103,21 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
 
     def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None, head=None):
         """(output, aggregate kept for the backward, logits of `head` or None)."""
+        fc = _fc.fc_forward_bf16 if bf16 else fwd32
         if ra:  # S (x_src W_rel^T), then lin_root + bias + ReLU accumulated onto it in place
-            fc = _fc.fc_forward_bf16 if bf16 else _fc.fc_forward
             y = spmm_forward(S, fc(x_src, w_rel, None, None, None, False))
             if head is not None:
-                y, lg = _fc.fc_forward(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True,
-                                       heads=head, heads_only=ho)
+                y, lg = fwd32(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True, heads=head,
+                              heads_only=ho)
                 return y, None, lg
             return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None, None
         agg = spmm_forward(S, x_src) if agg is None else agg
         if head is not None:
-            y, lg = _fc.fc_forward(agg, w_rel, x_dst, w_root, b, relu, dropout, seed, heads=head, heads_only=ho)
+            y, lg = fwd32(agg, w_rel, x_dst, w_root, b, relu, dropout, seed, heads=head, heads_only=ho)
             return y, agg, lg
-        return _fc_fwd(agg, x_dst, w_rel, b, w_root, relu, dropout, seed, bf16), agg, None
+        return fc(agg, w_rel, x_dst, w_root, b, relu, dropout, seed), agg, None
 
-    side = _side_stream(left.device) if _OVERLAP and not ra_l else None
+    side = _side_stream(left.device) if opts.overlap and not ra_l else None
     agg_l = None
     if side is not None:  # right2left's HBM-bound SpMM beside left2right's MFMA-bound FC
         side.wait_stream(torch.cuda.current_stream(left.device))
@@ -141,10 +130,14 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
         agg_l.record_stream(torch.cuda.current_stream(left.device))
     # arch.py:78-80: left' = right2left((right, left), A)
     left_new, agg_l, logit_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l, head=hd[0])
-    ctx.adj, ctx.relu, ctx.bf16 = adj, relu, bf16
+    ctx.adj, ctx.relu, ctx.bf16, ctx.opts = adj, relu, bf16, opts
     ctx.f16 = left.dtype == torch.float16
     ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
+    # conv1's shape (narrow LP-feature inputs, kept aggregates, ReLU without dropout, fp32): its weight
+    # gradients can be folded into the next layer's input-gradient GEMM (lpg_fc_x3_relu_wgrad_f32)
+    ctx.small_relu = (not bf16 and relu and dropout == 0 and agg_l is not None and agg_r is not None
+                      and agg_l.shape[1] + left.shape[1] <= 16 and agg_r.shape[1] + right.shape[1] <= 16)
     logits = None if heads is None or bf16 else (logit_l, logit_r)
     return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, *ws), logits
 
@@ -152,16 +145,15 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
 class _TwoDirection(torch.autograd.Function):
     @staticmethod
     def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                prev=None):
-        """``prev``: the backward node of the layer that produced (left, right) with ReLU (bf16), whose
-        outputs feed only this layer -- its ReLU/dropout backward is then folded into this layer's
-        input-gradient stores (lpg_fc_bf16_relu_bwd) and it takes dZ as given (column sums only)."""
+                prev=None, opts=DEFAULT):
+        """``prev``: the backward node of the layer that produced (left, right) and feeds only this
+        layer (foldable_producer): bf16 -- its ReLU/dropout backward is folded into this layer's
+        input-gradient stores (lpg_fc_bf16_relu_bwd) and it takes dZ as given (column sums only);
+        fp32 conv1 -- its weight gradients are folded into this layer's input-gradient GEMMs
+        (lpg_fc_x3_relu_wgrad_f32) and handed to it (``folded_wgk``)."""
         left_new, right_new, saved, _ = _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r,
-                                                      w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
-        ctx.in_scale = None
-        if prev is not None:
-            ctx.in_scale = prev.scale
-            prev.out_folded = True
+                                                      w_rel_r2l, b_r2l, w_root_r2l, relu, dropout, opts=opts)
+        _link_prev(ctx, prev)
         ctx.save_for_backward(*saved)
         return left_new, right_new
 
@@ -169,7 +161,19 @@ class _TwoDirection(torch.autograd.Function):
     def backward(ctx, g_left, g_right):
         if ctx.f16:
             raise RuntimeError("lpgnn: fp16 is the reference's inference mode (val.py:269); train in fp32 or bf16")
-        return _backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None,)
+        return _backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None, None)
+
+
+def _link_prev(ctx, prev):
+    ctx.in_scale, ctx.wgk_prev = None, None
+    if prev is None:
+        return
+    if prev.bf16:
+        ctx.in_scale = prev.scale
+        prev.out_folded = True
+    else:
+        ctx.wgk_prev = prev
+        prev.wgk_folded = True
 
 
 def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
@@ -180,6 +184,15 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
     A, AT = ctx.adj.fwd, ctx.adj.bwd
     bf16 = ctx.bf16
     dt = torch.bfloat16 if bf16 else torch.float32
+    opts = ctx.opts
+    pre = getattr(ctx, "folded_wgk", None)
+    if getattr(ctx, "wgk_folded", False) and pre is not None:
+        # conv1 whose weight gradients the next layer computed in its input-gradient GEMMs
+        ctx.folded_wgk = None
+        (dw_rel_l2r, dw_root_l2r, db_l2r), (dw_rel_r2l, dw_root_r2l, db_r2l) = pre
+        keep = lambda t, i, has=True: t if (need[i] and has) else None  # noqa: E731
+        return (None, None, None, keep(dw_rel_l2r, 3), keep(db_l2r, 4, ctx.has_b[0]), keep(dw_root_l2r, 5),
+                keep(dw_rel_r2l, 6), keep(db_r2l, 7, ctx.has_b[1]), keep(dw_root_r2l, 8), None, None)
 
     def mask(g, y, want_db):
         if g is None:
@@ -223,7 +236,7 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
     else:
         dz_l, db_r2l, dz_r, db_l2r = dz
     main = torch.cuda.current_stream(dz_r.device)
-    side = _side_stream(dz_r.device) if _OVERLAP else None
+    side = _side_stream(dz_r.device) if opts.overlap else None
     esz = 2 if bf16 else 4
 
     # Per direction (S = dst x src): T = S^T dZ serves the source-side gradient T W_rel when
@@ -248,8 +261,8 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
 
     # fp32: the x3 kernels (weight gradient G^T X, input gradient G W) unless LPGNN_FC_ARITH=fp32;
     # bf16: lpg_wgrad_bf16 (fp32 weight gradients) and lpg_fc_bf16 on the transposed weights
-    wg = _fc.wgrad_bf16 if bf16 else _fc.wgrad
-    ig = _fc.input_grad_bf16 if bf16 else _fc.input_grad
+    wg = _fc.wgrad_bf16 if bf16 else functools.partial(_fc.wgrad, arith=opts.arith)
+    ig = _fc.input_grad_bf16 if bf16 else functools.partial(_fc.input_grad, arith=opts.arith)
 
     def wgrads(dz, agg, x_dst, need_rel, need_root):
         if not (need_rel or need_root):
@@ -275,20 +288,51 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
         dw_rel_r2l = wg(t_l, right)
 
     in_scale = getattr(ctx, "in_scale", None) if bf16 else None
+    # fp32: conv1 produced (left, right) and feeds only this layer -- its weight gradients come out of
+    # this layer's input-gradient GEMMs (prev = conv1's node; its saved inputs, aggregates and outputs)
+    prev = getattr(ctx, "wgk_prev", None)
+    ctx.wgk_prev = None
+    p_saved = prev.saved_tensors if prev is not None and (need[0] or need[1]) else None
 
-    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in):
+    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in, conv1=None):
         """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients);
-        with a folded previous layer, through its ReLU/dropout backward (x_in = its output)."""
+        with a folded previous layer, through its ReLU/dropout backward (x_in = its output).  conv1 =
+        (Y, X1, X2) of the conv1 direction whose output x_in is: returns that direction's weight
+        gradients (dW_rel, dW_root, db) instead, the gradient itself never stored."""
+        if conv1 is not None:
+            y, x1, x2 = conv1
+            if t_src:
+                r = _fc.input_grad_relu_wgrad(T, w_rel, dz_root, w_root, None, y, x1, x2)
+            else:
+                r = _fc.input_grad_relu_wgrad(dz_root, w_root, None, None, spmm_forward(St, ig(dz, w_rel)), y, x1,
+                                              x2)
+            if r is not None:
+                return r
+            g = src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in)  # the two-pass route
+            return _fc.relu_wgrad_smallk(g, y, 1.0, x1, x2, True)
         kw = {} if in_scale is None else {"mask": (x_in, in_scale)}
         if t_src:  # both terms over the same rows: one two-part GEMM
             return ig(T, w_rel, dz_root, w_root, **kw)
         return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True, **kw)
 
     g_l = g_r = None
-    if need[1]:  # right = src of right2left (S = A), dst of left2right
-        g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r, right)
-    if need[0]:  # left = src of left2right (S = A^T), dst of right2left
-        g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l, left)
+    if p_saved is not None:
+        p_left, p_right, p_agg_l, p_agg_r, p_left_new, p_right_new = p_saved[:6]
+        # right = conv1's left2right output (Y, from A^T x_s and x_t); left = its right2left output
+        wk_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r, right,
+                             conv1=(p_right_new, p_agg_r, p_right))
+        wk_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l, left,
+                             conv1=(p_left_new, p_agg_l, p_left))
+        prev.folded_wgk = (wk_r, wk_l)
+        # conv1's node still runs (it returns the gradients handed to it): its incoming gradients carry
+        # no values -- zero-stride views, no memory
+        g_r = torch.zeros((), dtype=right.dtype, device=right.device).expand(right.shape)
+        g_l = torch.zeros((), dtype=left.dtype, device=left.device).expand(left.shape)
+    else:
+        if need[1]:  # right = src of right2left (S = A), dst of left2right
+            g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r, right)
+        if need[0]:  # left = src of left2right (S = A^T), dst of right2left
+            g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l, left)
     return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 
@@ -301,16 +345,17 @@ class _TwoDirectionHeads(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                wh_l, bh_l, wh_r, bh_r, heads_only=False):
+                wh_l, bh_l, wh_r, bh_r, heads_only=False, prev=None, opts=DEFAULT):
         # the heads fused into the layer's FC epilogues (x3 arithmetic), else their own Linear kernels
         left_new, right_new, saved, logits = _forward_core(
             ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-            heads=((wh_l, bh_l), (wh_r, bh_r)) if FUSE_HEAD_FWD else None, heads_only=heads_only)
+            heads=((wh_l, bh_l), (wh_r, bh_r)) if opts.fuse_head_fwd else None, heads_only=heads_only, opts=opts)
         if logits is None:
-            logits = (_fc.fc_forward(left_new, wh_l, None, None, bh_l, False),
-                      _fc.fc_forward(right_new, wh_r, None, None, bh_r, False))
+            logits = (_fc.fc_forward(left_new, wh_l, None, None, bh_l, False, arith=opts.arith),
+                      _fc.fc_forward(right_new, wh_r, None, None, bh_r, False, arith=opts.arith))
         logit_l, logit_r = logits
         ctx.heads_b = (bh_l is not None, bh_r is not None)
+        _link_prev(ctx, prev)
         ctx.save_for_backward(*saved, wh_l, wh_r)
         return logit_l, logit_r
 
@@ -326,44 +371,57 @@ class _TwoDirectionHeads(torch.autograd.Function):
         core = _backward_core(ctx, saved, need, None, None, dz=(dz_l, db_r2l, dz_r, db_l2r))
         keep = lambda t, i, has=True: t if (need[i] and has) else None
         return (*core, keep(dwh_l, 11), keep(dbh_l, 12, ctx.heads_b[0]), keep(dwh_r, 13),
-                keep(dbh_r, 14, ctx.heads_b[1]), None)
+                keep(dbh_r, 14, ctx.heads_b[1]), None, None, None)
 
 
 def two_direction_heads(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, lin_left, lin_right,
-                        dropout: float = 0.0):
+                        dropout: float = 0.0, fold_in: bool = False, opts: PathOptions = DEFAULT):
     """GraphConvTwoDirection (ReLU, dropout) followed by the heads lin_left /
-    lin_right (arch.py:184-190) through one autograd node: (logit_l, logit_r)."""
+    lin_right (arch.py:184-190) through one autograd node: (logit_l, logit_r).  ``fold_in`` as
+    two_direction's."""
     ts = (left, right, left2right.lin_rel.weight, left2right.lin_rel.bias, left2right.lin_root.weight,
           right2left.lin_rel.weight, right2left.lin_rel.bias, right2left.lin_root.weight, lin_left.weight,
           lin_left.bias, lin_right.weight, lin_right.bias)
     # nothing will differentiate through this call: the layer output (which feeds only the heads) is not needed
     heads_only = not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts))
+    prev = _fold_prev(left, right, fold_in, opts)
     return _TwoDirectionHeads.apply(left, right, adj, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                     left2right.lin_root.weight, right2left.lin_rel.weight, right2left.lin_rel.bias,
                                     right2left.lin_root.weight, True, float(dropout), lin_left.weight,
-                                    lin_left.bias, lin_right.weight, lin_right.bias, heads_only)
+                                    lin_left.bias, lin_right.weight, lin_right.bias, heads_only, prev, opts)
 
 
-def foldable_producer(x: Tensor):
-    """The backward node of the bf16 ReLU layer (_TwoDirection) that produced x, whose ReLU/dropout
-    backward a consumer may fold into its input-gradient stores, or None."""
+def foldable_producer(x: Tensor, opts: PathOptions = DEFAULT):
+    """The backward node of the layer (_TwoDirection) that produced x, if a consumer may fold part of
+    its backward into its own: a bf16 ReLU layer (its ReLU/dropout backward into the consumer's
+    input-gradient stores, options.fold_relu_bwd) or fp32 conv1 (its weight gradients into the
+    consumer's x3 input-gradient GEMMs, options.fold_conv1_wgrad); else None."""
     g = x.grad_fn
-    if FOLD_RELU_BWD and g is not None and isinstance(g, _TwoDirection._backward_cls) and \
-            getattr(g, "relu", False) and getattr(g, "bf16", False):
+    if g is None or not isinstance(g, _TwoDirection._backward_cls) or not getattr(g, "relu", False):
+        return None
+    if getattr(g, "bf16", False):
+        return g if opts.fold_relu_bwd and x.dtype == torch.bfloat16 else None
+    if opts.fold_conv1_wgrad and opts.arith == "x3" and getattr(g, "small_relu", False) and \
+            x.dtype == torch.float32 and g.opts.arith == "x3":
         return g
     return None
 
 
+def _fold_prev(left: Tensor, right: Tensor, fold_in: bool, opts: PathOptions):
+    if not (fold_in and torch.is_grad_enabled()):
+        return None
+    prev = foldable_producer(left, opts)
+    return prev if prev is not None and prev is right.grad_fn else None
+
+
 def two_direction(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, relu: bool = False,
-                  dropout: float = 0.0, fold_in: bool = False):
+                  dropout: float = 0.0, fold_in: bool = False, opts: PathOptions = DEFAULT):
     """GraphConvTwoDirection.forward (arch.py:65-81) through one autograd node.  ``fold_in``: the
     caller guarantees (left, right) feed nothing but this layer (GCN_FC's layer chain) -- if they
     are a bf16 ReLU layer's outputs, that layer's ReLU/dropout backward is folded into this one's
-    input-gradient stores."""
-    prev = None
-    if fold_in and left.dtype == torch.bfloat16 and torch.is_grad_enabled():
-        prev = foldable_producer(left)
-        prev = prev if prev is not None and prev is right.grad_fn else None
+    input-gradient stores; if they are fp32 conv1's, conv1's weight gradients come out of this
+    layer's input-gradient GEMMs."""
+    prev = _fold_prev(left, right, fold_in, opts)
     return _TwoDirection.apply(left, right, adj, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                left2right.lin_root.weight, right2left.lin_rel.weight, right2left.lin_rel.bias,
-                               right2left.lin_root.weight, bool(relu), float(dropout), prev)
+                               right2left.lin_root.weight, bool(relu), float(dropout), prev, opts)

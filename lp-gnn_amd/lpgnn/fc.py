@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from . import _lib
+from .options import DEFAULT as _DEFAULT_OPTIONS
 from .timing import TIMER
 
 
@@ -50,7 +51,8 @@ def _pad_k(t: Tensor, mult: int = 4) -> Tensor:
 
 # fp32 FC arithmetic: "fp32" = the exact fp32 MFMA kernel (bitwise contract of oracle/fc_ref.c),
 # "x3" = fp32 on the bf16 matrix cores through the exact three-way bf16 split (lpg_fc_x3_f32, lpg_wgrad_x3_f32).
-ARITH = os.environ.get("LPGNN_FC_ARITH", "x3")
+# The default of calls that pass no ``arith``; a model passes its own (GCN_FC(options=...), lpgnn.options).
+ARITH = _DEFAULT_OPTIONS.arith
 
 _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless the narrow-input kernel applies
 
@@ -247,6 +249,53 @@ def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | No
     K2 = 0 if G2 is None else G2.shape[1]
     return _fc_x3(M, N, G1, None, G2, None, K2, None, out, 2 if accumulate else 0, 0.0, 0, False,
                   W1s=split3(W1, transpose=True), W2s=split3(W2, transpose=True) if K2 else None)
+
+
+def input_grad_relu_wgrad(G1: Tensor, W1: Tensor, G2: Tensor | None, W2: Tensor | None, addend: Tensor | None,
+                          Y: Tensor, X1: Tensor, X2: Tensor | None):
+    """conv1's weight gradients folded into the input-gradient GEMM of the layer it feeds
+    (lpg_fc_x3_relu_wgrad_f32): g = G1 W1 [+ G2 W2] [+ addend] is the gradient of conv1's ReLU output
+    Y, and instead of g the call returns (dW1 [N, k1] = dZ^T X1, dW2 [N, k2] = dZ^T X2 or None,
+    db [N] = sum dZ), dZ = (Y > 0) ? g : 0 (conv1 has no dropout; arch.py:181-182) -- what
+    relu_wgrad_smallk computes from the stored g, without storing it.  None when the operands do not
+    fit the fused kernel (the caller then takes input_grad + relu_wgrad_smallk)."""
+    k1, k2 = X1.shape[1], (0 if X2 is None else X2.shape[1])
+    if (G1.dtype != torch.float32 or G1.shape[1] % 32 or (G2 is not None and G2.shape[1] % 32)
+            or W1.shape[1] <= 32 or not 1 <= k1 + k2 <= 16 or Y.dtype != torch.float32):
+        return None
+    G1, G2 = _prep(G1), _prep(G2)
+    if G2 is not None and G2.stride(0) != G1.stride(0):
+        return None
+    M, N = G1.shape[0], W1.shape[1]
+    W1s = split3(W1, transpose=True)
+    W2s = split3(W2, transpose=True) if G2 is not None else None
+    if W2s is not None and W2s.shape != W1s.shape:
+        return None
+    Y = Y if (Y.stride(1) == 1) else Y.contiguous()
+    X1 = X1.contiguous()
+    X2 = None if X2 is None else X2.contiguous()
+    if addend is not None and (addend.shape != (M, N) or addend.stride(1) != 1 or addend.dtype != torch.float32):
+        return None
+    L = _lib.lib()
+    dW1 = torch.empty((N, k1), dtype=torch.float32, device=G1.device)
+    dW2 = torch.empty((N, k2), dtype=torch.float32, device=G1.device) if k2 else None
+    db = torch.empty(N, dtype=torch.float32, device=G1.device)
+    ws = torch.empty(max(16, L.lpg_fc_x3_relu_wgrad_workspace_bytes(M, N, k1 + k2)) // 4 + 4, dtype=torch.float32,
+                     device=G1.device)
+    K2 = 0 if G2 is None else G2.shape[1]
+    with torch.cuda.device(G1.device):
+        tok = TIMER.start(("fc", M, N, G1.shape[1] + K2, "wgk-x3"))
+        st = L.lpg_fc_x3_relu_wgrad_f32(
+            M, N, G1.shape[1], G1.data_ptr(), G1.stride(0), W1s.data_ptr(), W1s.stride(1), W1s.stride(0), K2,
+            None if G2 is None else G2.data_ptr(), G2.stride(0) if K2 else 0,
+            None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0, W2s.stride(0) if K2 else 0,
+            None if addend is None else addend.data_ptr(), N if addend is None else addend.stride(0),
+            2 if addend is not None else 0, Y.data_ptr(), Y.stride(0), k1, X1.data_ptr(), X1.stride(0), k2,
+            None if X2 is None else X2.data_ptr(), X2.stride(0) if k2 else 0, dW1.data_ptr(),
+            None if dW2 is None else dW2.data_ptr(), db.data_ptr(), ws.data_ptr(), _lib.stream_of(G1))
+        TIMER.stop(tok)
+    _lib.check(st, "lpg_fc_x3_relu_wgrad_f32")
+    return dW1, dW2, db
 
 
 _BF16_BK = 64  # lpg_fc_bf16's k-tile: K1, K2 are zero-padded to a multiple of it
@@ -602,7 +651,7 @@ def _new_seed() -> int:
 
 class _FC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, A1, A2, W1, W2, b, relu, dropout_p, row_offset=0, row_keys=None):
+    def forward(ctx, A1, A2, W1, W2, b, relu, dropout_p, row_offset=0, row_keys=None, arith=None):
         if dropout_p > 0 and not relu:
             raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
         seed = _new_seed() if dropout_p > 0 else 0
@@ -613,7 +662,7 @@ class _FC(torch.autograd.Function):
             W2 = None if W2 is None else W2.to(torch.bfloat16)
             C = fc_forward_bf16(A1, W1, A2, W2, b, relu, dropout_p, seed, **kw)
         else:
-            C = fc_forward(A1, W1, A2, W2, b, relu, dropout_p, seed, **kw)
+            C = fc_forward(A1, W1, A2, W2, b, relu, dropout_p, seed, arith=arith, **kw)
         ctx.relu, ctx.has_a2, ctx.has_b = relu, A2 is not None, b is not None
         ctx.scale = 1.0 / (1.0 - dropout_p) if dropout_p > 0 else 1.0
         ctx.save_for_backward(A1, A2 if A2 is not None else A1, W1, W2 if W2 is not None else W1,
@@ -634,7 +683,7 @@ class _FC(torch.autograd.Function):
             dA2 = input_grad_bf16(g, W2) if ctx.has_a2 and need[1] else None
             dW1 = wgrad_bf16(g, A1) if need[2] else None
             dW2 = wgrad_bf16(g, A2) if ctx.has_a2 and need[3] else None
-            return dA1, dA2, dW1, dW2, db, None, None, None, None
+            return dA1, dA2, dW1, dW2, db, None, None, None, None, None
         if ctx.relu:
             g, db = relu_bwd_colsum(gC, C, ctx.scale, want_db)  # ReLU + dropout bwd, bias grad fused
         else:
@@ -649,14 +698,15 @@ class _FC(torch.autograd.Function):
         else:
             dW1 = g.t() @ A1 if need[2] else None
             dW2 = g.t() @ A2 if ctx.has_a2 and need[3] else None
-        return dA1, dA2, dW1, dW2, db, None, None, None, None
+        return dA1, dA2, dW1, dW2, db, None, None, None, None, None
 
 
 def graph_conv_fc(agg: Tensor, x_dst: Tensor, w_rel: Tensor, b_rel, w_root: Tensor, relu: bool,
-                  dropout: float = 0.0, row_offset: int = 0, row_keys: Tensor | None = None) -> Tensor:
+                  dropout: float = 0.0, row_offset: int = 0, row_keys: Tensor | None = None,
+                  arith: str | None = None) -> Tensor:
     """GraphConv's lin_rel(agg) + lin_root(x_dst) (+ ReLU, dropout) as one autograd node; the dropout
     mask keys rows by row_keys[m] or row_offset + m (a partition's global node ids)."""
-    return _FC.apply(agg, x_dst, w_rel, w_root, b_rel, relu, float(dropout), int(row_offset), row_keys)
+    return _FC.apply(agg, x_dst, w_rel, w_root, b_rel, relu, float(dropout), int(row_offset), row_keys, arith)
 
 
 def linear_small_bwd(G: Tensor, W: Tensor, H: Tensor, need_dh: bool):
@@ -706,7 +756,7 @@ class _Linear(torch.autograd.Function):
     """torch.nn.Linear on lpg_fc_f32; few-output backward on the HIP kernel."""
 
     @staticmethod
-    def forward(ctx, x, W, b, prev=None):
+    def forward(ctx, x, W, b, prev=None, arith=None):
         ctx.has_b = b is not None
         ctx.bf16 = x.dtype in HALF16  # (fp16: the --fp16 inference mode, forward only)
         ctx.f16 = x.dtype == torch.float16
@@ -724,7 +774,7 @@ class _Linear(torch.autograd.Function):
                 return linear_small_fwd_bf16(x, W, b)
             return fc_forward_bf16(x, W, None, None, b, False)
         ctx.save_for_backward(x, W)
-        return fc_forward(x, W, None, None, b, False)
+        return fc_forward(x, W, None, None, b, False, arith=arith)
 
     @staticmethod
     def backward(ctx, g):
@@ -744,33 +794,35 @@ class _Linear(torch.autograd.Function):
                 # tensor while the entry exists (a hook that replaces the gradient falls back to colsum)
                 ctx.prev.folded_colsum[x.data_ptr()] = (dx, dby)
             ctx.prev = None
-            return (dx if need[0] else None), (dW if need[1] else None), (db if ctx.has_b and need[2] else None), None
+            return (dx if need[0] else None), (dW if need[1] else None), (db if ctx.has_b and need[2] else None), \
+                None, None
         if ctx.bf16:
             g = g.to(torch.bfloat16)
             mask = None if ctx.in_scale is None else (x, ctx.in_scale)
             dx = input_grad_bf16(g, W, mask=mask) if need[0] else None
             dW = wgrad_bf16(g, x) if need[1] else None
             db = g.float().sum(0) if ctx.has_b and need[2] else None
-            return dx, dW, db, None
+            return dx, dW, db, None, None
         if W.shape[0] <= 4 and x.shape[1] % 4 == 0:
             dx, dW, db = linear_small_bwd(g, W, x, need[0])
-            return dx, dW if need[1] else None, db if (ctx.has_b and need[2]) else None, None
+            return dx, dW if need[1] else None, db if (ctx.has_b and need[2]) else None, None, None
         dx = g @ W if need[0] else None
         dW = g.t() @ x if need[1] else None
         db = g.sum(0) if ctx.has_b and need[2] else None
-        return dx, dW, db, None
+        return dx, dW, db, None, None
 
 
-def linear(x: Tensor, weight: Tensor, bias, fold_in: bool = False) -> Tensor:
+def linear(x: Tensor, weight: Tensor, bias, fold_in: bool = False, opts=None) -> Tensor:
     """torch.nn.Linear.forward on lpg_fc_f32 (heads, arch.py:190).  ``fold_in`` (GCN_FC's heads,
     bf16): the caller guarantees both outputs of the producing layer feed only its heads, so that
     layer's ReLU/dropout backward is folded into the heads' input-gradient stores."""
+    opts = opts or _DEFAULT_OPTIONS
     prev = None
     if fold_in and x.dtype == torch.bfloat16 and torch.is_grad_enabled():
         from . import conv as _conv
 
-        prev = _conv.foldable_producer(x)
-    return _Linear.apply(x, weight, bias, prev)
+        prev = _conv.foldable_producer(x, opts)
+    return _Linear.apply(x, weight, bias, prev, opts.arith)
 
 
 class _Knowledge(torch.autograd.Function):

@@ -1,0 +1,56 @@
+"""Per-model choices of the hot path's kernels and fusions (no module state that callers mutate).
+
+Every choice here computes the same function (the tests compare them); they exist for A/B
+measurements and for the bitwise contract of the exact-fp32 FC.  A model carries its own
+``PathOptions`` (``GCN_FC(..., options=...)``); the defaults come from the environment once, at
+import, so a whole run can be switched from the shell:
+
+  LPGNN_FC_ARITH=fp32        the exact-fp32 MFMA FC (bitwise oracle/fc_ref.c) + hipBLASLt backward
+                             instead of the x3 kernels (fp32 on the bf16 matrix cores, exact split)
+  LPGNN_REASSOC=0            lin_rel(S x) never re-associated as S (x W_rel^T)
+  LPGNN_FUSE_HEADS=0         the heads as their own autograd node
+  LPGNN_FUSE_HEAD_FWD=0      the heads' forward as their own kernels (not in the last FC's epilogue)
+  LPGNN_FOLD_RELU_BWD=0      bf16: a layer's ReLU/dropout backward as its own pass
+  LPGNN_FOLD_CONV1_WGRAD=0   fp32: conv1's weight gradient as its own pass (not in the next layer's
+                             input-gradient GEMM)
+  LPGNN_OVERLAP=1            independent SpMMs on a second stream beside the FC
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+
+
+def _env(name: str, default: str) -> str:
+    return os.environ.get(name, default)
+
+
+@dataclasses.dataclass(frozen=True)
+class PathOptions:
+    arith: str = "x3"
+    reassociate: bool = True
+    fuse_heads: bool = True
+    fuse_head_fwd: bool = True
+    fold_relu_bwd: bool = True
+    fold_conv1_wgrad: bool = True
+    overlap: bool = False
+
+    def __post_init__(self):
+        if self.arith not in ("x3", "fp32"):
+            raise ValueError(f"PathOptions.arith must be 'x3' or 'fp32', got {self.arith!r}")
+
+    @classmethod
+    def from_env(cls) -> "PathOptions":
+        return cls(arith=_env("LPGNN_FC_ARITH", "x3"),
+                   reassociate=_env("LPGNN_REASSOC", "1") == "1",
+                   fuse_heads=_env("LPGNN_FUSE_HEADS", "1") == "1",
+                   fuse_head_fwd=_env("LPGNN_FUSE_HEAD_FWD", "1") == "1",
+                   fold_relu_bwd=_env("LPGNN_FOLD_RELU_BWD", "1") == "1",
+                   fold_conv1_wgrad=_env("LPGNN_FOLD_CONV1_WGRAD", "1") == "1",
+                   overlap=_env("LPGNN_OVERLAP", "0") == "1")
+
+    def replace(self, **kw) -> "PathOptions":
+        return dataclasses.replace(self, **kw)
+
+
+DEFAULT = PathOptions.from_env()

@@ -468,25 +468,32 @@ class _PartTwoDirection(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout):
+    def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
+                opts=None):
         left_new, right_new, saved, _ = _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r,
-                                                           w_rel_r2l, b_r2l, w_root_r2l, relu, dropout)
+                                                           w_rel_r2l, b_r2l, w_root_r2l, relu, dropout, opts=opts)
         ctx.save_for_backward(*saved)
         return left_new, right_new
 
     @staticmethod
     def backward(ctx, g_left, g_right):
-        return _part_backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right)
+        return _part_backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None,)
 
 
 def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu,
-                       dropout, heads=None):
+                       dropout, heads=None, opts=None):
     """_PartTwoDirection's forward; returns (left_new, right_new, tensors to save, logits).
     heads = ((Wh_l, bh_l), (Wh_r, bh_r)): the heads in the FC epilogues (conv._forward_core's
     rule) for the rows the FCs compute, a separate Linear for the halo rows; logits None without."""
+    import functools
+
     from . import fc as _fc
     from .conv import reassociate
+    from .options import DEFAULT
     from .sparse import spmm_forward
+
+    opts = DEFAULT if opts is None else opts
+    fcf = functools.partial(_fc.fc_forward, arith=opts.arith)
 
     if dropout > 0 and not relu:
         raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
@@ -499,26 +506,26 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
     seed_l = _fc._new_seed() if dropout > 0 else 0
     # conv.py's association rule on the GLOBAL node counts (every rank decides alike, so the
     # reduced rows have the same width everywhere)
-    ra = reassociate(ex.m, ex.n, left.shape[1], w_rel_l2r.shape[0])
+    ra = reassociate(ex.m, ex.n, left.shape[1], w_rel_l2r.shape[0], opts.reassociate)
     if ra:  # partials of A^T (left W_rel^T) for [owned | halo]
-        agg_r = spmm_forward(AT, _fc.fc_forward(left, w_rel_l2r, None, None, None, False))
+        agg_r = spmm_forward(AT, fcf(left, w_rel_l2r, None, None, None, False))
     else:
         agg_r = spmm_forward(AT, left)          # partials for [owned | halo]
     red = ex.start_reduce(agg_r, inplace=True)  # halo partials -> owners, in flight ...
     agg_l = spmm_forward(A, right)              # ... under the purely local constraint side
     hl, hr = heads if heads is not None else (None, None)
-    left_new = _fc.fc_forward(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l, heads=hl,
+    left_new = fcf(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l, heads=hl,
                               row_offset=ex.cons_key0)
     if hl is not None:
         left_new, logit_l = left_new
     red.finish()                                # owners' rows of agg_r now hold the full sums
     if ra:  # lin_root + bias + ReLU accumulated onto the owners' sums, in place
         right_new, agg_r = agg_r, None
-        own = _fc.fc_forward(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
+        own = fcf(right[:n_own], w_root_l2r, None, None, b_l2r, relu, dropout, seed_r,
                              out=right_new[:n_own], accumulate=True, heads=hr, **ex.var_key_args)
     else:
         right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
-        own = _fc.fc_forward(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
+        own = fcf(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
                              out=right_new[:n_own], heads=hr, **ex.var_key_args)
     ex.start_broadcast_(right_new).finish()
     logits = None
@@ -529,7 +536,7 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
         logit_r[:n_own] = own[1]
         ex.start_broadcast_(logit_r).finish()
         logits = (logit_l, logit_r)
-    ctx.padj, ctx.relu = padj, relu
+    ctx.padj, ctx.relu, ctx.opts = padj, relu, opts
     ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
     return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r,
@@ -540,9 +547,14 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     """_PartTwoDirection's backward from the output gradients, or -- dz =
     (dz_l, db_r2l, dz_r_own, db_l2r) -- from gradients that already went
     through the layer's ReLU/dropout, owners' rows reduced (fused heads)."""
+    import functools
+
     from . import fc as _fc
     from .conv import _src_first
     from .sparse import spmm_forward
+
+    igf = functools.partial(_fc.input_grad, arith=ctx.opts.arith)
+    wgf = functools.partial(_fc.wgrad, arith=ctx.opts.arith)
 
     left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
     ex = ctx.padj.ex
@@ -567,8 +579,8 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
         if agg is not None and agg.shape[1] + x_dst.shape[1] <= 16 and dz.shape[1] % 4 == 0:
             d_rel, d_root = _fc.wgrad_smallk(dz, agg.contiguous(), x_dst.contiguous())
         else:
-            d_rel = _fc.wgrad(dz, agg) if need_rel else None
-            d_root = _fc.wgrad(dz, x_dst) if need_root else None
+            d_rel = wgf(dz, agg) if need_rel else None
+            d_root = wgf(dz, x_dst) if need_root else None
         return (d_rel if need_rel else None), (d_root if need_root else None)
 
     def narrow(agg, x_dst):  # conv1: the inputs are features -- weight gradients straight from (g, y)
@@ -589,9 +601,9 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     g_r = None
     if need[1]:  # right [owned | halo] as the source of right2left: every local row
         if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
-            g_r = _fc.input_grad(spmm_forward(AT, dz_l), w_rel_r2l)
+            g_r = igf(spmm_forward(AT, dz_l), w_rel_r2l)
         else:
-            g_r = spmm_forward(AT, _fc.input_grad(dz_l, w_rel_r2l))
+            g_r = spmm_forward(AT, igf(dz_l, w_rel_r2l))
     g_right_own = red.finish() if dz is None else None
     if narrow(agg_r, right):
         dw_rel_l2r, dw_root_l2r, db_l2r = _fc.relu_wgrad_smallk(g_right_own, right_new[:n_own], ctx.scale,
@@ -612,7 +624,7 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     dw_rel_l2r, dw_root_l2r = wgrads(dz_r, None if agg_r is None else agg_r[:n_own], right[:n_own],
                                      need[3] and not rel_from_t, need[5])
     if need[1]:  # ... and as the destination of left2right (owned rows)
-        _fc.input_grad(dz_r, w_root_l2r, out=g_r[:n_own], accumulate=True)
+        igf(dz_r, w_root_l2r, out=g_r[:n_own], accumulate=True)
 
     g_l = None
     if need[0] or use_t:  # left: source of left2right through reduce(AT @ left)[:n_own]
@@ -621,16 +633,16 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
         if use_t:
             full[:n_own] = dz_r
         else:
-            _fc.input_grad(dz_r, w_rel_l2r, out=full[:n_own])
+            igf(dz_r, w_rel_l2r, out=full[:n_own])
         bc = ex.start_broadcast_(full)           # owners' aggregate gradient -> halo rows, in flight ...
-        root = _fc.input_grad(dz_l, w_root_r2l) if need[0] else None  # ... under the root-path gradient
+        root = igf(dz_l, w_root_r2l) if need[0] else None  # ... under the root-path gradient
         bc.finish()
         if use_t:
             t = spmm_forward(A, full)
             if rel_from_t:
-                dw_rel_l2r = _fc.wgrad(t, left)
+                dw_rel_l2r = wgf(t, left)
             if need[0]:
-                g_l = _fc.input_grad(t, w_rel_l2r, out=root, accumulate=True)
+                g_l = igf(t, w_rel_l2r, out=root, accumulate=True)
         else:
             g_l = spmm_forward(A, full).add_(root)
     return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
@@ -646,17 +658,20 @@ class _PartTwoDirectionHeads(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                wh_l, bh_l, wh_r, bh_r):
+                wh_l, bh_l, wh_r, bh_r, opts=None):
+        import functools
+
         from . import fc as _fc
+        from .options import DEFAULT
 
-        from .conv import FUSE_HEAD_FWD
-
+        opts = DEFAULT if opts is None else opts
+        fcf = functools.partial(_fc.fc_forward, arith=opts.arith)
         left_new, right_new, saved, logits = _part_forward_core(
             ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-            heads=((wh_l, bh_l), (wh_r, bh_r)) if FUSE_HEAD_FWD else None)
+            heads=((wh_l, bh_l), (wh_r, bh_r)) if opts.fuse_head_fwd else None, opts=opts)
         if logits is None:
-            logits = (_fc.fc_forward(left_new, wh_l, None, None, bh_l, False),
-                      _fc.fc_forward(right_new, wh_r, None, None, bh_r, False))
+            logits = (fcf(left_new, wh_l, None, None, bh_l, False),
+                      fcf(right_new, wh_r, None, None, bh_r, False))
         logit_l, logit_r = logits
         ctx.heads_b = (bh_l is not None, bh_r is not None)
         ctx.save_for_backward(*saved, wh_l, wh_r)
@@ -680,7 +695,7 @@ class _PartTwoDirectionHeads(torch.autograd.Function):
         core = _part_backward_core(ctx, saved, need, None, None, dz=(dz_l, db_r2l, dz_r, db_l2r))
         keep = lambda t, i, has=True: t if (need[i] and has) else None
         return (*core, keep(dwh_l, 11), keep(dbh_l, 12, ctx.heads_b[0]), keep(dwh_r, 13),
-                keep(dbh_r, 14, ctx.heads_b[1]))
+                keep(dbh_r, 14, ctx.heads_b[1]), None)
 
 
 class PartitionedCSR:
@@ -706,16 +721,16 @@ class PartitionedCSR:
     def device(self):
         return self.local.device
 
-    def two_direction_conv(self, left, right, left2right, right2left, relu=False, dropout=0.0):
+    def two_direction_conv(self, left, right, left2right, right2left, relu=False, dropout=0.0, opts=None):
         """GraphConvTwoDirection.forward on this partition (one autograd node)."""
         if self.orient != "cons" or left.dtype != torch.float32 or _local_spmm is not _product_spmm:
             return None  # generic per-direction path (oracle tests, bf16)
         return _PartTwoDirection.apply(left, right, self, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                        left2right.lin_root.weight, right2left.lin_rel.weight,
                                        right2left.lin_rel.bias, right2left.lin_root.weight, bool(relu),
-                                       float(dropout))
+                                       float(dropout), opts)
 
-    def two_direction_heads(self, left, right, left2right, right2left, lin_left, lin_right, dropout=0.0):
+    def two_direction_heads(self, left, right, left2right, right2left, lin_left, lin_right, dropout=0.0, opts=None):
         """The last layer + heads (arch.py:184-190) on this partition, one autograd node (None: not applicable)."""
         if self.orient != "cons" or left.dtype != torch.float32 or _local_spmm is not _product_spmm:
             return None
@@ -723,7 +738,7 @@ class PartitionedCSR:
                                             left2right.lin_root.weight, right2left.lin_rel.weight,
                                             right2left.lin_rel.bias, right2left.lin_root.weight, True,
                                             float(dropout), lin_left.weight, lin_left.bias, lin_right.weight,
-                                            lin_right.bias)
+                                            lin_right.bias, opts)
 
     def partitioned_conv(self, x, fc):
         """One GraphConv direction: fc(agg, x_dst) is lin_rel + lin_root (+ReLU, +dropout)."""

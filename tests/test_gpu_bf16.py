@@ -389,7 +389,7 @@ def test_gcn_fc_bf16_folded_relu_bwd_identical(monkeypatch):
     """The c5 model's backward with each layer's ReLU/dropout backward folded into the next layer's
     input-gradient stores gives the same loss and the same gradient bits as the separate passes
     (training dropout, same dropout seeds)."""
-    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, conv, synth
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
     from lpgnn.train import balanced
 
     g = synth.uniform_lp(1500, 5200, 30000, seed=5)
@@ -400,8 +400,9 @@ def test_gcn_fc_bf16_folded_relu_bwd_identical(monkeypatch):
     torch.manual_seed(0)
     model = GCN_FC(8, 8, hids=256, depth=5, dp=0.1, compute_dtype="bf16").to(DEV).train()
     out = {}
+    base = model.options
     for fold in (True, False):
-        monkeypatch.setattr(conv, "FOLD_RELU_BWD", fold)
+        model.options = base.replace(fold_relu_bwd=fold)
         model.zero_grad()
         torch.manual_seed(321)  # same dropout seeds
         lc, lv = model(batch)

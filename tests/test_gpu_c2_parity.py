@@ -98,10 +98,11 @@ def _batch(with_labels=True):
                           edge_index=adj, s_bs=g.m, t_bs=g.n, **kw)
 
 
-def _model(hids, depth, dtype=torch.float32, dp=0.1):
+def _model(hids, depth, dtype=torch.float32, dp=0.1, arith="x3"):
     from lpgnn import GCN_FC
+    from lpgnn.options import DEFAULT
 
-    model = GCN_FC(8, 8, hids=hids, depth=depth, dp=dp, compute_dtype=dtype)
+    model = GCN_FC(8, 8, hids=hids, depth=depth, dp=dp, compute_dtype=dtype, options=DEFAULT.replace(arith=arith))
     model.load_state_dict(_weights(hids, depth))
     return model.to(DEV)
 
@@ -136,13 +137,11 @@ def _near_tie_labels(logits, m, eps):
 
 @pytest.mark.parametrize("arith", ["x3", "fp32"])
 def test_c2_eval_logits_labels_vs_reference_arithmetic(arith, monkeypatch):
-    from lpgnn import fc
     from lpgnn.val import inference_gnn
 
-    monkeypatch.setattr(fc, "ARITH", arith)
     g, _, _ = _graph()
     r32, r64 = _oracle(1024, 3, torch.float32, False), _oracle(1024, 3, torch.float64, False)
-    got, heads = _hip_eval_with_heads(_model(1024, 3), _batch(False), monkeypatch)
+    got, heads = _hip_eval_with_heads(_model(1024, 3, arith=arith), _batch(False), monkeypatch)
     ref, ref_h = r32["logits"].double(), r32["heads"].double()
 
     # (1) the heads meet the north-star 1e-4 against the reference arithmetic, everywhere
@@ -185,12 +184,10 @@ def test_c2_training_step_grads_vs_oracle_autograd(arith, monkeypatch):
     parameter gradient vs the oracle's MKL autograd; each gradient's distance
     to fp64 is at most 2x MKL's own (+ a floor at fp32 resolution of the
     tensor), and within rtol 1e-3 of MKL in the relative Frobenius norm."""
-    from lpgnn import fc
     from lpgnn.train import balanced
 
-    monkeypatch.setattr(fc, "ARITH", arith)
     r32, r64 = _oracle(1024, 3, torch.float32, True), _oracle(1024, 3, torch.float64, True)
-    model = _model(1024, 3, dp=0.0).train()
+    model = _model(1024, 3, dp=0.0, arith=arith).train()
     batch = _batch()
     lc, lv = model(batch)
     loss = balanced(lc, lv, batch.y_s, batch.y_t)

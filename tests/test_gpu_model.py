@@ -86,15 +86,15 @@ def test_forward_bitwise_vs_kchain_oracle(depth, hids, reassoc, monkeypatch):
     with the re-associated left2right (conv.py's association rule) and with
     the reference's association everywhere."""
     from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
-    from lpgnn import conv, fc
+    from lpgnn.options import PathOptions
     from lpgnn.val import inference_gnn
 
-    monkeypatch.setattr(conv, "REASSOCIATE", reassoc)
-    monkeypatch.setattr(fc, "ARITH", "fp32")  # the exact-fp32 FC kernel (the bitwise contract)
+    # the exact-fp32 FC kernel (the bitwise contract)
+    opts = PathOptions(arith="fp32", reassociate=reassoc)
 
     g = synth.uniform_lp(1500, 3000, 30000, seed=4)
     torch.manual_seed(0)
-    model = GCN_FC(8, 8, hids=hids, depth=depth).to(DEV).eval()
+    model = GCN_FC(8, 8, hids=hids, depth=depth, options=opts).to(DEV).eval()
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
     batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
@@ -117,13 +117,12 @@ def test_forward_bitwise_vs_kchain_oracle(depth, hids, reassoc, monkeypatch):
 def test_random_graph_vs_oracle(depth, hids, arith, monkeypatch):
     """Mid-size synthetic LP, eval-mode logits vs the oracle fp32 CPU path
     (MKL F.linear, the reference's own evaluation), for both FC arithmetics."""
-    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, fc, synth
-
-    monkeypatch.setattr(fc, "ARITH", arith)
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.options import DEFAULT
 
     g = synth.uniform_lp(2000, 4000, 40000, seed=3)
     torch.manual_seed(0)
-    model = GCN_FC(8, 8, hids=hids, depth=depth).to(DEV).eval()
+    model = GCN_FC(8, 8, hids=hids, depth=depth, options=DEFAULT.replace(arith=arith)).to(DEV).eval()
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
     batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
@@ -148,14 +147,13 @@ def test_random_graph_vs_oracle(depth, hids, arith, monkeypatch):
 
 @pytest.mark.parametrize("arith,hids", [("x3", 128), ("fp32", 128), ("x3", 1024)])
 def test_training_step_runs_and_matches_oracle_grads(arith, hids, monkeypatch):
-    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, fc, synth
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.options import DEFAULT
     from lpgnn.train import balanced, make_optimizer, train_step
-
-    monkeypatch.setattr(fc, "ARITH", arith)
 
     g = synth.uniform_lp(1000, 2000, 20000, seed=5)
     torch.manual_seed(0)
-    model = GCN_FC(8, 8, hids=hids, depth=3, dp=0.0).to(DEV)
+    model = GCN_FC(8, 8, hids=hids, depth=3, dp=0.0, options=DEFAULT.replace(arith=arith)).to(DEV)
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
     batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
@@ -213,7 +211,7 @@ def test_fused_heads_node_equals_separate_heads(monkeypatch):
     """The last layer + heads as one autograd node (one backward pass over the
     layer output) gives the same loss and gradients as heads as their own
     node, with training dropout (same dropout seeds)."""
-    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, arch, synth
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
     from lpgnn.train import balanced
 
     g = synth.uniform_lp(900, 1700, 18000, seed=8)
@@ -224,8 +222,9 @@ def test_fused_heads_node_equals_separate_heads(monkeypatch):
     torch.manual_seed(0)
     model = GCN_FC(8, 8, hids=256, depth=4, dp=0.1).to(DEV).train()
     out = {}
+    base = model.options
     for fuse in (True, False):
-        monkeypatch.setattr(arch, "FUSE_HEADS", fuse)
+        model.options = base.replace(fuse_heads=fuse)
         model.zero_grad()
         torch.manual_seed(123)  # same dropout seeds
         lc, lv = model(batch)

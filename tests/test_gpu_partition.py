@@ -103,7 +103,7 @@ def _worker_dropout(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from lpgnn import GCN_FC, conv, partition as part
+        from lpgnn import GCN_FC, partition as part
 
         g = _graph()
         plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
@@ -111,8 +111,9 @@ def _worker_dropout(rank, world, port, out_dir):
         torch.manual_seed(0)
         model = GCN_FC(8, 8, hids=256, depth=4, dp=0.1).to("cuda:0").train()
         out = {}
+        base = model.options
         for fuse in (True, False):
-            conv.FUSE_HEAD_FWD = fuse
+            model.options = base.replace(fuse_head_fwd=fuse)
             model.zero_grad()
             torch.manual_seed(123)  # same dropout seeds
             lc, lv = model(batch)
@@ -121,7 +122,6 @@ def _worker_dropout(rank, world, port, out_dir):
             part.all_reduce_grads(model)
             out[fuse] = (loss.item(), lv.detach()[:plan.n_own].clone(),
                          {k: p.grad.clone() for k, p in model.named_parameters()})
-        conv.FUSE_HEAD_FWD = True
         assert abs(out[True][0] - out[False][0]) < 1e-5
         # the logits after add_knowledge: the fused heads sum each row in a different order than the
         # separate Linear (equal to fp32 rounding, test_x3_fused_heads_match_separate_linear), and

@@ -289,3 +289,82 @@ def test_input_grad_x3(two, accumulate):
                      out=out, accumulate=accumulate, arith="x3").cpu().double()
     bound = 16 * U * s + U * ref.abs() + 1e-30
     assert ((got - ref).abs() <= bound).all()
+
+
+@pytest.mark.parametrize("M,N,K,k1,k2,two,addend", [
+    (3000, 1024, 1024, 8, 8, True, False),   # c2 layer 2: T W_rel + dZ_root W_root, conv1 p = q = 8
+    (2999, 1024, 1024, 8, 8, False, True),   # the other association: dZ_root W_root + S^T(dZ W_rel)
+    (517, 256, 256, 8, 8, True, True),       # ragged rows, narrower layer
+    (1000, 128, 64, 12, 0, False, False),    # no root input, k = 12
+])
+def test_input_grad_relu_wgrad_vs_fp64(M, N, K, k1, k2, two, addend):
+    """lpg_fc_x3_relu_wgrad_f32: conv1's (dW_rel, dW_root, db) from the next layer's input-gradient
+    GEMM without storing g = G1 W1 [+ G2 W2] [+ addend] -- against fp64 of the same formula and at
+    most as far from it as the two-pass route (input_grad + relu_wgrad_smallk) plus a floor at fp32
+    resolution of the tensor (the fold sums the R = M rows in a different order)."""
+    from lpgnn.fc import input_grad, input_grad_relu_wgrad, relu_wgrad_smallk
+
+    gen = torch.Generator(device=DEV).manual_seed(M + N)
+    r = lambda *s: torch.randn(*s, device=DEV, generator=gen)
+    G1, W1 = r(M, K) * 1e-3, r(K, N) / K ** 0.5
+    G2, W2 = (r(M, K) * 1e-3, r(K, N) / K ** 0.5) if two else (None, None)
+    add = r(M, N) * 1e-3 if addend else None
+    Y = torch.relu(r(M, N))  # conv1's ReLU output: about half the entries are zero
+    X1 = r(M, k1)
+    X2 = r(M, k2) if k2 else None
+    got = input_grad_relu_wgrad(G1, W1, G2, W2, add, Y, X1, X2)
+    assert got is not None
+    g64 = G1.double() @ W1.double()
+    if two:
+        g64 += G2.double() @ W2.double()
+    if addend:
+        g64 += add.double()
+    dz = torch.where(Y > 0, g64, torch.zeros_like(g64))
+    want = (dz.t() @ X1.double(), None if X2 is None else dz.t() @ X2.double(), dz.sum(0))
+    g = input_grad(G1, W1, G2, W2) if two else input_grad(G1, W1)
+    if addend:
+        g = g + add
+    two_pass = relu_wgrad_smallk(g, Y, 1.0, X1, X2, True)
+    for name, a, b, w in zip(("dW_rel", "dW_root", "db"), got, two_pass, want):
+        if w is None:
+            assert a is None
+            continue
+        e_fold, e_two = (a.double() - w).abs().max().item(), (b.double() - w).abs().max().item()
+        floor = 64 * U * w.abs().max().item()
+        print(f"{name}: max|fold - fp64| = {e_fold:.3e}, max|two-pass - fp64| = {e_two:.3e}")
+        assert e_fold <= 2 * e_two + floor, name
+
+
+@pytest.mark.parametrize("hids,depth", [(1024, 3), (256, 4)])
+def test_conv1_wgrad_fold_equals_separate_pass(hids, depth):
+    """options.fold_conv1_wgrad: conv1's weight gradients out of layer 2's input-gradient GEMMs give
+    the same loss and, within fp32 summation-order differences, the same gradients as the separate
+    input-gradient + relu_wgrad_smallk passes (training dropout, same dropout seeds); the other
+    parameters' gradients are bitwise unchanged."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.train import balanced
+
+    g = synth.uniform_lp(1300, 2600, 26000, seed=11)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                           y_s=torch.from_numpy(g.y_s).to(DEV), y_t=torch.from_numpy(g.y_t).to(DEV),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=hids, depth=depth, dp=0.1).to(DEV).train()
+    base = model.options.replace(arith="x3")
+    out = {}
+    for fold in (True, False):
+        model.options = base.replace(fold_conv1_wgrad=fold)
+        model.zero_grad()
+        torch.manual_seed(77)
+        lc, lv = model(batch)
+        loss = balanced(lc, lv, batch.y_s, batch.y_t)
+        loss.backward()
+        out[fold] = (loss.item(), {k: p.grad.clone() for k, p in model.named_parameters()})
+    assert out[True][0] == out[False][0]
+    for k, v in out[True][1].items():
+        w = out[False][1][k]
+        if k.startswith("conv1."):
+            torch.testing.assert_close(v, w, rtol=1e-4, atol=1e-4 * w.abs().max().item(), msg=k)
+        else:
+            assert torch.equal(v, w), k

@@ -82,7 +82,8 @@ def _cpu_local_spmm(adj, x):
     return O.spmm_t(fwd, bwd, x)
 
 
-def _cpu_graph_conv_fc(agg, x_dst, w_rel, b_rel, w_root, relu, dropout=0.0, row_offset=0, row_keys=None):
+def _cpu_graph_conv_fc(agg, x_dst, w_rel, b_rel, w_root, relu, dropout=0.0, row_offset=0, row_keys=None,
+                       arith=None):
     out = F.linear(agg, w_rel, b_rel) + F.linear(x_dst, w_root)
     out = torch.relu(out) if relu else out
     return F.dropout(out, p=dropout, training=True) if dropout > 0 else out
@@ -110,7 +111,7 @@ def _worker(rank, world, port, out_dir, mode="global", scale=50, hids=16):
 
         part._local_spmm = _cpu_local_spmm
         fc.graph_conv_fc = _cpu_graph_conv_fc
-        fc.linear = lambda x, w, b, fold_in=False: F.linear(x, w, b)
+        fc.linear = lambda x, w, b, fold_in=False, opts=None: F.linear(x, w, b)
         fc.knowledge = _cpu_knowledge
 
         if mode == "c4":  # each rank generates and plans only its own blocks
