@@ -177,9 +177,10 @@ lpg_status lpg_spmm_f16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, 
  * with S (x_src W_rel^T) computed by lpg_fc_f32 + lpg_spmm_f32 into C first).
  * bias may be NULL.
  * dropout_p > 0 fuses F.dropout after the ReLU (arch.py:186-188, training):
- * element (m, n) is kept iff a counter-based hash of (seed, m, n) (two
- * rounds of the 32-bit lowbias32 mix) is >= dropout_p * 2^32, and kept
- * values are scaled by 1 / (1 - dropout_p).  The mask is never stored: the
+ * element (m, n) is kept iff its 16 mask bits -- half of the 32-bit
+ * lowbias32 hash of (seed, key(m), n / 2): the low half for even n, the high
+ * half for odd n -- are >= round(dropout_p * 2^16), and kept values are
+ * scaled by 1 / (1 - dropout_p) (oracle/dropout_ref.py restates the mask).  The mask is never stored: the
  * kept set is exactly where the output is > 0.  The hash keys row m as
  * row_keys[m] when row_keys != NULL (device int64 [M]: the global node id of
  * every row, e.g. a partition's owned variables, which need not be

@@ -57,8 +57,8 @@ struct FcArgs {
   float *C;
   int64_t ldc;
   int64_t mt, nt;  // tiles
-  // fused dropout (after the ReLU): keep element (row, col) iff
-  // hash(seed, row * N + col) >= drop_thresh; kept values are scaled.
+  // fused dropout (after the ReLU): keep element (row, col) iff its 16 mask bits
+  // drop_bits(seed, key(row), col) >= drop_thresh (fc_common.h); kept values are scaled.
   uint64_t seed;
   uint32_t drop_thresh;  // 0 = no dropout
   float drop_scale;
@@ -74,7 +74,7 @@ struct FcArgs {
 __device__ __forceinline__ float epilogue(const FcArgs &a, float v, float b, int64_t row, int64_t col, bool relu) {
   if (a.bias) v = v + b;
   if (relu) v = (v < 0.f) ? 0.f : v;
-  if (a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+  if (a.drop_thresh) v = drop_bits(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
   return v;
 }
 
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
   if (nch > 1) load_x(rb + kSmallKRows);
   // the row loop with the addend / bias / dropout choices made once per launch (uniform branches
   // per element cost more than the arithmetic of this write-bound kernel); the dropout column keys
-  // once per thread, the row key once per row -- the same mask bits as drop_hash(seed, row, col)
+  // once per thread, the row key once per row, one hash per column pair -- the mask bits of drop_bits
   auto rows = [&](auto acc_c, auto bias_c, auto drop_c) {
     constexpr bool ACC = decltype(acc_c)::value, BIAS = decltype(bias_c)::value, DROP = decltype(drop_c)::value;
     uint32_t ck[4];
@@ -480,12 +480,13 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
               t = t + p2;
             }
             if constexpr (ACC) t = t + f32x2{a.C[m * a.ldc + c + j], a.C[m * a.ldc + c + j + 1]};
+            const uint32_t hp = DROP ? drop_hash_k(rk, ck[j]) : 0u;  // columns c + j, c + j + 1: one pair
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
               float v = t[e];
               if constexpr (BIAS) v = v + b[j + e];
               if (RELU) v = (v < 0.f) ? 0.f : v;
-              if constexpr (DROP) v = drop_hash_k(rk, ck[j + e]) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+              if constexpr (DROP) v = drop_half(hp, e) >= a.drop_thresh ? v * a.drop_scale : 0.f;
               o[j + e] = v;
             }
           }
@@ -567,11 +568,7 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
   LPG_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "lpg_fc_f32: dropout_p %g not in [0, 1)", (double)dropout_p);
   FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1,
            row_offset, row_keys};
-  if (dropout_p > 0.f) {
-    const double th = (double)dropout_p * 4294967296.0;
-    a.drop_thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);
-    a.drop_scale = 1.f / (1.f - dropout_p);
-  }
+  dropout_params(dropout_p, &a.drop_thresh, &a.drop_scale);
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
   lpg_status st;

@@ -185,7 +185,8 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
                 v[h] = v[h] + E::lo(*reinterpret_cast<const uint16_t *>(img + (lr + h) * EP_PITCH + (j * 16 + fr) * 2));
               v[h] = v[h] + bb[j];
               if (RELU) v[h] = v[h] < 0.f ? 0.f : v[h];
-              if constexpr (DROP) v[h] = drop_hash_k(h ? rk1 : rk0, ck[j]) >= a.drop_thresh ? v[h] * a.drop_scale : 0.f;
+              if constexpr (DROP)
+                v[h] = drop_half(drop_hash_k(h ? rk1 : rk0, ck[j]), fr) >= a.drop_thresh ? v[h] * a.drop_scale : 0.f;
             }
             const uint32_t pk = E::pack(v[0], v[1]);
             *reinterpret_cast<uint16_t *>(img + lr * EP_PITCH + (j * 16 + fr) * 2) = (uint16_t)pk;
@@ -237,7 +238,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
         if (a.accum) v = v + E::lo(a.C[row * a.ldc + col]);
         v = v + bb;
         if (RELU) v = v < 0.f ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        if (a.drop_thresh) v = drop_bits(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         a.C[row * a.ldc + col] = E::rne(v);
       }
     }
@@ -266,12 +267,12 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
     auto body = [&](auto acc_c, auto drop_c) {
       constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
       constexpr int IH = FM / 2;  // addend loads in two halves of IH fragment rows (register budget)
-      uint32_t ck[FN][4];
+      uint32_t ck[FN][2];  // column-pair keys of the lane's columns c0 + 16 j + {0,1} and {2,3}
       if constexpr (DROP) {
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) ck[j][r] = drop_col_key(c0 + j * 16 + r);
+          for (int q = 0; q < 2; ++q) ck[j][q] = drop_col_key(c0 + j * 16 + 2 * q);
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -290,6 +291,8 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
             float v[4];
+            uint32_t hp[2] = {0u, 0u};
+            if constexpr (DROP) hp[0] = drop_hash_k(rk, ck[j][0]), hp[1] = drop_hash_k(rk, ck[j][1]);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               v[r] = acc[i][j][r];
@@ -299,7 +302,7 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
               }
               v[r] = v[r] + bb[j][r];
               if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
-              if constexpr (DROP) v[r] = drop_hash_k(rk, ck[j][r]) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
+              if constexpr (DROP) v[r] = drop_half(hp[r >> 1], r) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
             }
             const uint32_t lo = E::pack(v[0], v[1]);
             const uint32_t hi = E::pack(v[2], v[3]);
@@ -332,7 +335,7 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
         if (a.accum) v = v + E::lo(a.C[row * a.ldc + col]);
         v = v + (a.bias ? a.bias[col] : 0.f);
         if (RELU) v = v < 0.f ? 0.f : v;
-        if (RELU && a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        if (RELU && a.drop_thresh) v = drop_bits(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         a.C[row * a.ldc + col] = E::rne(v);
       }
   }
@@ -385,12 +388,12 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
   };
   auto body = [&](auto acc_c, auto drop_c) {
     constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
-    uint32_t ck[FN][4];
+    uint32_t ck[FN][2];
     if constexpr (DROP) {
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ck[j][r] = drop_col_key(c0 + j * 16 + r);
+        for (int q = 0; q < 2; ++q) ck[j][q] = drop_col_key(c0 + j * 16 + 2 * q);
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -401,6 +404,8 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
         uint2 ad = {0u, 0u};
         if constexpr (ACC) ad = *reinterpret_cast<const uint2 *>(ip + j * 32);
         float v[4];
+        uint32_t hp[2] = {0u, 0u};
+        if constexpr (DROP) hp[0] = drop_hash_k(rk, ck[j][0]), hp[1] = drop_hash_k(rk, ck[j][1]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           v[r] = acc[i][j][r];
@@ -410,7 +415,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
           }
           v[r] = v[r] + bb[j][r];
           if (RELU) v[r] = v[r] < 0.f ? 0.f : v[r];
-          if constexpr (DROP) v[r] = drop_hash_k(rk, ck[j][r]) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
+          if constexpr (DROP) v[r] = drop_half(hp[r >> 1], r) >= a.drop_thresh ? v[r] * a.drop_scale : 0.f;
         }
         const uint32_t lo = E::pack(v[0], v[1]);
         const uint32_t hi = E::pack(v[2], v[3]);
@@ -1170,11 +1175,12 @@ __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
               t = t + f32x2{E::lo(w), E::hi(w)};
             }
             t = t + bp[jp];
+            const uint32_t hp = DROP ? drop_hash_k(rk, ck[2 * jp]) : 0u;  // columns c + 2 jp, c + 2 jp + 1
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
               float v = t[e];
               if (RELU) v = v < 0.f ? 0.f : v;
-              if constexpr (DROP) v = drop_hash_k(rk, ck[2 * jp + e]) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+              if constexpr (DROP) v = drop_half(hp, e) >= a.drop_thresh ? v * a.drop_scale : 0.f;
               t[e] = v;
             }
             out[jp] = E::pack(t[0], t[1]);

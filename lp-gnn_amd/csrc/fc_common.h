@@ -9,12 +9,15 @@
 
 namespace lpg {
 
-// Counter-based dropout RNG over (seed, row, col): two rounds of the 32-bit
-// "lowbias32" integer hash, the inner one keyed by the row only (so a lane
-// reuses it across its columns).  Stateless, so the backward pass never needs
-// the mask (the kept set is exactly where the stored output is > 0).  32-bit
-// on purpose: 64-bit multiplies are multi-instruction on CDNA and made the
-// epilogue ~10% of a hidden-layer FC.
+// Counter-based dropout mask over (seed, row, column pair): one round of the 32-bit "lowbias32"
+// integer hash per row and one per (row, column pair); the pair's hash carries 16 bits for each of
+// its two columns (low half: the even column, high half: the odd one), kept iff those bits >=
+// the 16-bit threshold round(p * 2^16) (dropout_params; the drop rate is within 2^-17 of p).
+// Stateless, so the backward pass never needs the mask (the kept set is exactly where the stored
+// output is > 0).  One hash per two outputs: the hash's two quarter-rate v_mul_lo_u32 were most of
+// a dropout epilogue's VALU (round 3: 1.56 VALU per MFMA in the bf16 FC with dropout, 0.37
+// without).  32-bit on purpose: 64-bit multiplies are multi-instruction on CDNA.
+// oracle/dropout_ref.py restates this function; every FC kernel draws the same mask through it.
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -24,11 +27,6 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   return x;
 }
 
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int64_t row, int64_t col) {
-  const uint32_t hr = lowbias32((uint32_t)row ^ (uint32_t)seed);
-  return lowbias32(hr ^ ((uint32_t)col * 0x9e3779b9u) ^ (uint32_t)(seed >> 32));
-}
-
 // The dropout key of output row `row`: row_keys[row] when the caller gives one key per row (the
 // global node ids of a partition's rows, in any order) or row_off + row (a contiguous slice); rows at
 // or past M are never stored and key as row_off + row (no load past the key array).
@@ -36,13 +34,19 @@ __device__ __forceinline__ int64_t drop_row(const int64_t *row_keys, int64_t row
   return (row_keys != nullptr && row < M) ? row_keys[row] : row_off + row;
 }
 
-// drop_hash split into its row and column keys, for epilogues that hold a few rows and a few
-// columns per lane: drop_hash(seed, row, col) == drop_hash_k(drop_row_key(seed, row), drop_col_key(col))
-__device__ __forceinline__ uint32_t drop_row_key(uint64_t seed, int64_t row) {
-  return lowbias32((uint32_t)row ^ (uint32_t)seed) ^ (uint32_t)(seed >> 32);
+// The mask split into its row and column-pair keys, for epilogues that hold a few rows and a few
+// columns per lane: the pair hash of (key, col) is drop_hash_k(drop_row_key(seed, key), drop_col_key(col)),
+// the same for col = 2c and 2c + 1; drop_half picks a column's 16 bits out of it.
+__device__ __forceinline__ uint32_t drop_row_key(uint64_t seed, int64_t key) {
+  return lowbias32((uint32_t)key ^ (uint32_t)seed) ^ (uint32_t)(seed >> 32);
 }
-__device__ __forceinline__ uint32_t drop_col_key(int64_t col) { return (uint32_t)col * 0x9e3779b9u; }
+__device__ __forceinline__ uint32_t drop_col_key(int64_t col) { return (uint32_t)(col >> 1) * 0x9e3779b9u; }
 __device__ __forceinline__ uint32_t drop_hash_k(uint32_t rk, uint32_t ck) { return lowbias32(rk ^ ck); }
+__device__ __forceinline__ uint32_t drop_half(uint32_t h, int64_t col) { return (col & 1) ? (h >> 16) : (h & 0xffffu); }
+// element form (fallback epilogues): the 16 mask bits of (key, col)
+__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, int64_t key, int64_t col) {
+  return drop_half(drop_hash_k(drop_row_key(seed, key), drop_col_key(col)), col);
+}
 
 // 16 B per lane, buffer_load_dwordx4 ... lds into M0 = lds (lane-linear): the descriptor over
 // [p, p + n) is built from readfirstlane'd values, so it stays in SGPRs (a select between two
@@ -88,8 +92,8 @@ inline void dropout_params(float p, uint32_t *thresh, float *scale) {
   *thresh = 0u;
   *scale = 1.f;
   if (p > 0.f) {
-    const double th = (double)p * 4294967296.0;
-    *thresh = th >= 4294967295.0 ? 4294967295u : (uint32_t)(th < 1.0 ? 1.0 : th);
+    const double th = (double)p * 65536.0 + 0.5;  // round(p * 2^16), in [1, 65535]
+    *thresh = th >= 65535.0 ? 65535u : (uint32_t)(th < 1.0 ? 1.0 : th);
     *scale = 1.f / (1.f - p);
   }
 }

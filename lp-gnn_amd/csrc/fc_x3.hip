@@ -312,7 +312,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void fc_fwd_x3_16(X3Args a) {
         float v = acc[i][j][r];
         if (a.bias) v = v + bb;
         if (RELU) v = (v < 0.f) ? 0.f : v;
-        if (a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+        if (a.drop_thresh) v = drop_bits(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
         if (a.store) a.C[row * a.ldc + col] = v;
         if constexpr (HEADS) {
 #pragma unroll
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
             float v = acc[i][j][r];
             if constexpr (BIAS) v = v + bb;
             if (RELU) v = (v < 0.f) ? 0.f : v;
-            if constexpr (DROP) v = drop_hash_k(rk[i][r], ck) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+            if constexpr (DROP) v = drop_half(drop_hash_k(rk[i][r], ck), fr) >= a.drop_thresh ? v * a.drop_scale : 0.f;
             if (!HEADS || a.store) rp(i, r)[j * 16] = v;
             hput(i, r, j, v);
           }
@@ -686,7 +686,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
           float v = acc[i][j][r];
           if (a.bias) v = v + bb;
           if (RELU) v = (v < 0.f) ? 0.f : v;
-          if (a.drop_thresh) v = drop_hash(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+          if (a.drop_thresh) v = drop_bits(a.seed, drop_row(a.row_keys, a.row_off, row, a.M), col) >= a.drop_thresh ? v * a.drop_scale : 0.f;
           if (!HEADS || a.store) a.C[row * a.ldc + col] = v;
           hput(i, r, j, v);
         }
