@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests -> smoke -> bench -> rocprofv3 kernel stats.
 # Usage (from the repo root, via gpurun):  bash tools/gpu_session.sh [stages...]
-# stages: tests smoke bench prof pmc bench_c5 prof_c5 kbench kbfc mfma   (default: tests smoke bench prof)
+# stages: tests tests_files smoke bench prof pmc bench_c5 prof_c5 kbench kbfc mfma x3traffic rehearse2/8 pmc_rs   (default: tests smoke bench prof)
 # Every GPU step has its own time limit; the script stops at the first step
 # that crashes, aborts or times out (exit >= 2 or signal), and continues past
 # a plain test failure (exit 1) so the bench still runs.
@@ -33,6 +33,10 @@ rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > "$OUT/device.txt" || tru
 for s in $STAGES; do
   case $s in
     tests) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    tests_files)  # PYTEST_FILES (space-separated), every failure reported (maxfail PYTEST_MAXFAIL, default 30)
+      step pytest_files 700 python -u -m pytest ${PYTEST_FILES} -m gpu --maxfail ${PYTEST_MAXFAIL:-30} -v \
+        -p no:cacheprovider -rf --timeout 120 --timeout-method thread ;;
+    x3traffic) step x3traffic 420 bash tools/experiments/x3_traffic_probe.sh ;;
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py ;;
     prof)
