@@ -549,9 +549,11 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
     // block's [BM][wk1 + wk2] input rows beside them, then each thread sums one column's dZ * x over
     // the block's rows in row order (half the k per thread) -- one partial per (m-tile, k, n); g, the
     // [M, N] gradient the separate pass re-read with Y, is never stored
-    constexpr int KMAX = 16, KH = (KMAX + 2) / 2;  // k + the bias row, split over two threads
+    // x rows in LDS with KP floats: x1 | x2 | 1 (the bias row, k = ks) | zeros; a thread takes KH = 10
+    // consecutive k of one column and advances two of them per v_pk_fma_f32 (the same fma per element)
+    constexpr int KP = 20, KH = KP / 2;
     static_assert(NW * 64 == 2 * BN, "two threads per output column");
-    static_assert((NW * TM * 16 * HP + BM * KMAX) * 4 <= 2 * TILE_BYTES, "images fit the tile buffers");
+    static_assert((NW * TM * 16 * HP + BM * KP) * 4 <= 2 * TILE_BYTES, "images fit the tile buffers");
     float *const wimg = reinterpret_cast<float *>(smem);
     float *const xs = wimg + NW * TM * 16 * HP;
     const int ks = a.wk1 + a.wk2;
@@ -572,34 +574,32 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
           wimg[wave * (TM * 16 * HP) + (i * 16 + 4 * fg + r) * HP + j * 16 + fr] = (ok && y > 0.f) ? g : 0.f;
         }
     }
-    for (int q = tid; q < BM * KMAX; q += NW * 64) {
-      const int r = q / KMAX, k = q % KMAX;
+    for (int q = tid; q < BM * KP; q += NW * 64) {
+      const int r = q / KP, k = q % KP;
       const int64_t row = m0 + r;
-      float x = 0.f;
+      float x = k == ks ? 1.f : 0.f;
       if (row < a.M && k < ks) x = k < a.wk1 ? a.wx1[row * a.ldwx1 + k] : a.wx2[row * a.ldwx2 + (k - a.wk1)];
       xs[q] = x;
     }
     __syncthreads();
     const int c = tid % BN, kb = (tid / BN) * KH;
-    float sk[KH];
+    f32x2 sk[KH / 2];
 #pragma unroll
-    for (int u = 0; u < KH; ++u) sk[u] = 0.f;
+    for (int u = 0; u < KH / 2; ++u) sk[u] = f32x2{0.f, 0.f};
     for (int r = 0; r < BM; ++r) {
       const float d = wimg[(r / (TM * 16)) * (TM * 16 * HP) + (r % (TM * 16)) * HP + c];
-      const float *xr = xs + r * KMAX;
+      const f32x2 *xr = reinterpret_cast<const f32x2 *>(xs + r * KP + kb);
 #pragma unroll
-      for (int u = 0; u < KH; ++u) {
-        const int k = kb + u;  // (k == ks: the bias row, x = 1)
-        const float x = k < ks ? xr[k < KMAX ? k : 0] : 1.f;
-        sk[u] = __builtin_fmaf(d, x, sk[u]);
-      }
+      for (int u = 0; u < KH / 2; ++u) sk[u] = __builtin_elementwise_fma(f32x2{d, d}, xr[u], sk[u]);
     }
     const int64_t col = nw + c;
     if (col < a.N) {
       float *const pp = a.wpart + (m0 / BM) * (int64_t)(ks + 1) * a.N + col;
 #pragma unroll
-      for (int u = 0; u < KH; ++u)
-        if (kb + u <= ks) pp[(int64_t)(kb + u) * a.N] = sk[u];
+      for (int u = 0; u < KH / 2; ++u)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          if (kb + 2 * u + e <= ks) pp[(int64_t)(kb + 2 * u + e) * a.N] = sk[u][e];
     }
     return;
   }
