@@ -624,12 +624,17 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
     }
     auto body = [&](auto bias_c, auto drop_c) {
       constexpr bool BIAS = decltype(bias_c)::value, DROP = decltype(drop_c)::value;
-      uint32_t rk[TM][4];
+      // dropout: lanes fr = 2c and 2c + 1 hold the column pair c of the same four rows; the even lane
+      // hashes rows 0-1 of the pair, the odd lane rows 2-3, and one DPP swap of adjacent lanes hands
+      // each its partner's two -- two row keys and two pair hashes per lane and fragment, not four
+      const int odd = fr & 1;
+      uint32_t rk[TM][2];
       if constexpr (DROP) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) rk[i][r] = drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, mw + i * 16 + 4 * fg + r, a.M));
+          for (int h = 0; h < 2; ++h)
+            rk[i][h] = drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, mw + i * 16 + 4 * fg + 2 * odd + h, a.M));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -637,16 +642,27 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
         const float bb = BIAS ? a.bias[col] : 0.f;
         const uint32_t ck = drop_col_key(col);
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) {
+          uint32_t hr[4] = {0u, 0u, 0u, 0u};  // the pair hash of row 4 fg + r
+          if constexpr (DROP) {
+            const uint32_t h0 = drop_hash_k(rk[i][0], ck), h1 = drop_hash_k(rk[i][1], ck);
+            const uint32_t p0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)h0, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+            const uint32_t p1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)h1, 0xB1, 0xF, 0xF, false);
+            hr[0] = odd ? p0 : h0;
+            hr[1] = odd ? p1 : h1;
+            hr[2] = odd ? h0 : p0;
+            hr[3] = odd ? h1 : p1;
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[i][j][r];
             if constexpr (BIAS) v = v + bb;
             if (RELU) v = (v < 0.f) ? 0.f : v;
-            if constexpr (DROP) v = drop_half(drop_hash_k(rk[i][r], ck), fr) >= a.drop_thresh ? v * a.drop_scale : 0.f;
+            if constexpr (DROP) v = drop_half(hr[r], fr) >= a.drop_thresh ? v * a.drop_scale : 0.f;
             if (!HEADS || a.store) rp(i, r)[j * 16] = v;
             hput(i, r, j, v);
           }
+        }
       }
     };
     using T_ = std::true_type;
