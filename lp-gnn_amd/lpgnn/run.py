@@ -372,10 +372,10 @@ def main(argv=None):
 
         if world_env > 1 and not dist.is_initialized():
             backend = "nccl" if torch.cuda.is_available() else "gloo"
-            dist.init_process_group(backend)
-            if torch.cuda.is_available():
+            if torch.cuda.is_available():  # the rank's GPU first: RCCL binds its communicator to the current device
                 args.dev = f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}"
                 torch.cuda.set_device(args.dev)
+            dist.init_process_group(backend, device_id=torch.device(args.dev) if backend == "nccl" else None)
     if args.phase == "train":
         hist = run_exp(args)
         print(json.dumps({"epoch_loss": hist["epoch_loss"], "checkpoint": hist["checkpoint"]}))
