@@ -355,8 +355,13 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
     fc_flops = sum(kern[k][0] * 2.0 * k[1] * k[2] * k[3] for k in fc_keys)
     fc_ms = sum(kern[k][1] for k in fc_keys)
     fc_launches = sum(kern[k][0] for k in fc_keys)
+    # RCCL exchanges (lpgnn.partition._Pending): issue -> consumption span and the compute stream's
+    # exposed wait, both HIP-event spans on the compute stream
+    ex_span = sum(v[1] for k, v in kern.items() if k[0] == "exchange" and k[4] == "span")
+    ex_exposed = sum(v[1] for k, v in kern.items() if k[0] == "exchange" and k[4] == "exposed")
+    ex_n = sum(v[0] for k, v in kern.items() if k[0] == "exchange" and k[4] == "span")
     mine = dict(dt=dt, edges=launches * local_nnz, bytes=bytes_total, spmm_ms=spmm_ms, launches=launches,
-                fc_flops=fc_flops, fc_ms=fc_ms)
+                fc_flops=fc_flops, fc_ms=fc_ms, ex_span=ex_span, ex_exposed=ex_exposed, ex_n=ex_n)
     every = ctx.gather(mine)
     dt_max = max(r["dt"] for r in every)
     world = len(every)
@@ -403,12 +408,25 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
         med = float(np.median(v))
         dirs[name] = {"median_ms": med, "launches": len(v), "edges_per_s": local_nnz / (med / 1e3),
                       "roofline_frac": spmm_bytes(k[1], local_nnz, k[3], esz) / (med / 1e3) / 1e9 / HBM_PEAK_GBS}
-    return {"value": value, "ms_per_step": dt_max / max(1, steps) * 1e3, "roofline": roof, "fc_roofline": fc,
-            "spmm_directions": dirs,
+    out = {"value": value, "ms_per_step": dt_max / max(1, steps) * 1e3, "roofline": roof, "fc_roofline": fc}
+    if any(r["ex_n"] for r in every):
+        st = max(1, steps)
+        out["exchange_overlap"] = {
+            "what": "RCCL all_to_all boundary exchanges of the timed steps: span = issue -> rows consumed, "
+                    "exposed = the compute stream's wait for the collective (HIP events on the compute stream); "
+                    "hidden = 1 - exposed / span",
+            "per_rank": [{"exchanges_per_step": r["ex_n"] / st, "span_ms_per_step": r["ex_span"] / st,
+                          "exposed_ms_per_step": r["ex_exposed"] / st,
+                          "hidden_frac": (1.0 - r["ex_exposed"] / r["ex_span"]) if r["ex_span"] > 0 else None}
+                         for r in every],
+            "max_exposed_ms_per_step": max(r["ex_exposed"] for r in every) / st}
+    out.update({"spmm_directions": dirs,
             "spmm_edges_per_s_kernel": launches * local_nnz / (spmm_ms / 1e3) if spmm_ms > 0 else None,
             "spmm_ms_per_step": spmm_ms / max(1, steps),
             "kernels": {f"{k[0]}[{k[1]}x{k[2]},F={k[3]},{k[4]}]": {"launches": v[0], "ms": v[1]}
-                        for k, v in sorted(kern.items())}}
+                        for k, v in sorted(kern.items(), key=lambda kv: tuple(map(str, kv[0])))
+                        if k[0] != "exchange"}})
+    return out
 
 
 # ------------------------------------------------------------------------ jobs

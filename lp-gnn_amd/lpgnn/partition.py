@@ -43,6 +43,7 @@ import torch.nn.functional as F
 
 from . import sparse as _sparse
 from .sparse import CSR, BipartiteCSR
+from .timing import TIMER
 
 
 # ----------------------------------------------------------------------- plan
@@ -273,14 +274,23 @@ def _a2a(send: torch.Tensor, in_counts: list, out_counts: list, group) -> torch.
 class _Pending:
     """An all_to_all in flight (RCCL runs it on its own stream; `finish`
     makes the current stream wait, then applies `then` to the received rows).
-    gloo with HIP tensors stages through the host synchronously."""
+    gloo with HIP tensors stages through the host synchronously.
 
-    def __init__(self, recv, work=None, host=None, then=None):
-        self.recv, self.work, self.host, self.then = recv, work, host, then
+    With bench.py's timer on (lpgnn.timing), an RCCL exchange records two HIP-event spans on the
+    compute stream: "span" from the issue to the point where the rows are consumed, and "exposed"
+    across the wait itself -- the time the compute stream sat idle for the collective, i.e. the part
+    of the exchange NOT hidden under independent compute."""
+
+    def __init__(self, recv, work=None, host=None, then=None, tok=None):
+        self.recv, self.work, self.host, self.then, self.tok = recv, work, host, then, tok
 
     def finish(self):
         if self.work is not None:
+            key = None if self.tok is None else self.tok[0]
+            tok = TIMER.start(key[:4] + ("exposed",)) if key is not None else None
             self.work.wait()
+            TIMER.stop(tok)
+            TIMER.stop(self.tok)
         if self.host is not None:
             self.recv.copy_(self.host)
         return self.then(self.recv) if self.then is not None else self.recv
@@ -292,8 +302,9 @@ def _a2a_start(send: torch.Tensor, in_counts: list, out_counts: list, group) -> 
         h = torch.empty(recv.shape, dtype=recv.dtype)
         dist.all_to_all_single(h, send.cpu(), out_counts, in_counts, group=group)
         return _Pending(recv, host=h)
+    tok = TIMER.start(("exchange", sum(in_counts), sum(out_counts), int(np.prod(send.shape[1:])), "span"))
     work = dist.all_to_all_single(recv, send.contiguous(), out_counts, in_counts, group=group, async_op=True)
-    return _Pending(recv, work=work)
+    return _Pending(recv, work=work, tok=tok)
 
 
 class Exchange:
