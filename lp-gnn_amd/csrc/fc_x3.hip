@@ -84,6 +84,10 @@ struct X3Args {
   int64_t ldwy, ldwx1, ldwx2;
   int32_t wk1, wk2;
   float *wpart;
+  // tile order of fc_x3_wide (the per-call kernel choice 2): 0 = each XCD walks contiguous m-tiles with
+  // all their n-tiles; 1 = n-split: the first half of the block ids (XCDs 0-3) take n-tiles [0, nt/2) of
+  // every m-tile, the second half the rest -- each XCD's rounds read half of W and twice the A panels
+  int32_t order;
 };
 
 // dst plane p [rows, cols] (ldd) = term p of src (transposed: src is [cols, rows]).
@@ -412,8 +416,19 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   const int64_t m0 = LPG_X3_TRAFFIC_PROBE == 2 ? 0 : (wgid / a.nt) * BM;
   const int64_t n0 = LPG_X3_TRAFFIC_PROBE == 1 ? 0 : (wgid % a.nt) * BN;
 #else
-  const int64_t m0 = (wgid / a.nt) * BM;
-  const int64_t n0 = (wgid % a.nt) * BN;
+  int64_t mi = wgid / a.nt, ni = wgid % a.nt;
+  if (a.order == 1 && a.nt >= 2) {
+    const int64_t nh = a.nt / 2, t0 = a.mt * nh;
+    if (wgid < t0) {
+      mi = wgid / nh;
+      ni = wgid % nh;
+    } else {
+      mi = (wgid - t0) / (a.nt - nh);
+      ni = nh + (wgid - t0) % (a.nt - nh);
+    }
+  }
+  const int64_t m0 = mi * BM;
+  const int64_t n0 = ni * BN;
 #endif
   const int64_t mrows = a.M - m0 < BM ? a.M - m0 : BM;  // rows of this block (>= 1)
   const int64_t ncols = a.N - n0 < BN ? a.N - n0 : BN;
@@ -995,10 +1010,11 @@ int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
 }
 
 // FC kernel choice, per call in flags bits 8-11 (LPG_FC_KERNEL(k), include/lpgnn.h): 0 = fc_x3_wide
-// <4,2,8,2> when wide_ok (else 1), 1 = fc_fwd_x3_16 <4,1,2,8>.  Same MFMA shape, k order and product
+// <4,2,8,2> when wide_ok (else 1), 1 = fc_fwd_x3_16 <4,1,2,8>, 2 = fc_x3_wide in the n-split tile
+// order (X3Args::order).  Same MFMA shape, k order and product
 // sequence per output: the same C, bit for bit.  (tools/experiments/exp_wide.py at the c2 shapes:
 // 207-221 TF/s for the wide form, +3-6 % over fc_fwd_x3_16.)
-constexpr int kX3Kernels = 1;
+constexpr int kX3Kernels = 2;
 
 }  // namespace
 }  // namespace lpg
@@ -1060,7 +1076,9 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
   if (st != LPG_OK) return st;
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
-  if (((flags >> 8) & 15) == 0 && wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);
+  const int kern = (flags >> 8) & 15;
+  a.order = kern == 2 ? 1 : 0;
+  if (kern != 1 && wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);
   return launch_x3_16<4, 1, 2, 8>(a, relu, s);
 }
 
@@ -1095,7 +1113,8 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   // one partial per (128-column tile, row); fc_x3_wide carries three head slots, so hn = 4 (and the
   // per-call alternative) takes fc_fwd_x3_16 -- the same C, bit for bit
   lpg_status r;
-  if (hn <= 3 && ((flags >> 8) & 15) == 0 && wide_ok(a, 128, 128))
+  a.order = ((flags >> 8) & 15) == 2 ? 1 : 0;
+  if (hn <= 3 && ((flags >> 8) & 15) != 1 && wide_ok(a, 128, 128))
     r = launch_x3_wide<4, 2, 8, 2, true>(a, flags & 1, s);
   else
     r = launch_x3_16<4, 1, 2, 8, true>(a, flags & 1, s);

@@ -1,5 +1,6 @@
 """x3 FC at the verdict's K = 2048 shape (M = 200 K, K = 1024 + 1024, N = 1024, ReLU), a few
-launches, for rocprofv3 --pmc passes (past-L2 bytes, MFMA busy, clock)."""
+launches, for rocprofv3 --pmc passes (past-L2 bytes, MFMA busy, clock).  X3_KERNEL = the per-call
+kernel choice (LPG_FC_KERNEL: 0 default, 2 = the n-split tile order)."""
 import os
 import sys
 
@@ -15,7 +16,8 @@ A2 = torch.randn(200_000, 1024, device="cuda")
 W1 = torch.randn(1024, 1024, device="cuda") * 0.03
 W2 = torch.randn(1024, 1024, device="cuda") * 0.03
 b = torch.randn(1024, device="cuda")
+kern = int(os.environ.get("X3_KERNEL", "0"))
 for _ in range(4):
-    fc_forward(A1, W1, A2, W2, b, True, arith="x3")
+    fc_forward(A1, W1, A2, W2, b, True, arith="x3", kernel=kern)
 torch.cuda.synchronize()
 print("done")
