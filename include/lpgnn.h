@@ -155,7 +155,8 @@ lpg_status lpg_spmm_f16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, 
  * computes the same bits (the tests compare them); the choice exists so that
  * benchmarks and tests can pick a kernel per call, without global state.
  *   lpg_fc_x3_f32 / _heads: 1 = fc_fwd_x3_16 (global_load_lds staging), 2 = the default kernel
- *     in the n-split tile order (half the XCDs take the first half of the n-tiles);
+ *     in round 3's tile order (each XCD walks contiguous m-tiles with all their n-tiles; the default
+ *     is the n-split order: half the XCDs take the first half of the n-tiles);
  *   lpg_fc_bf16 / _relu_bwd: 1 = 128 x 128 tiles, 2 = 256 x 256 tiles,
  *     3 = the pipelined 256 x 256 kernel (the default from 4096 rows). */
 #define LPG_FC_RELU 1

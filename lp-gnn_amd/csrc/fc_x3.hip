@@ -84,9 +84,12 @@ struct X3Args {
   int64_t ldwy, ldwx1, ldwx2;
   int32_t wk1, wk2;
   float *wpart;
-  // tile order of fc_x3_wide (the per-call kernel choice 2): 0 = each XCD walks contiguous m-tiles with
-  // all their n-tiles; 1 = n-split: the first half of the block ids (XCDs 0-3) take n-tiles [0, nt/2) of
-  // every m-tile, the second half the rest -- each XCD's rounds read half of W and twice the A panels
+  // tile order of fc_x3_wide: 1 (the default) = n-split: the first half of the block ids (XCDs 0-3)
+  // take n-tiles [0, nt/2) of every m-tile, the second half the rest -- an XCD's round of 64 blocks is
+  // 16 m-tiles x 4 n-tiles, half of W and twice the A panels of the 8 x 8 order; 0 (the per-call kernel
+  // choice 2, round 3's order) = each XCD walks contiguous m-tiles with all their n-tiles.  Past-L2
+  // reads at 200 K x (1024 + 1024) -> 1024: 10.1 GB -> 6.7 GB per launch, 1-2 % faster
+  // (profiles/r04_pmc_fc_x3_k2048_probe.json, r04_x3_order_ab.log)
   int32_t order;
 };
 
@@ -560,35 +563,28 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   constexpr int HP = BN + 4;  // image row pitch (floats): rows 4 fg apart land 16 banks apart
   if constexpr (WGK) {
     // conv1's weight gradient folded into this input-gradient GEMM (the hidden layer's dZ W for the
-    // conv1 output): dZ = (Y > 0) ? g : 0 (conv1: ReLU, no dropout) into per-wave LDS images, the
-    // block's [BM][wk1 + wk2] input rows beside them, then each thread sums one column's dZ * x over
-    // the block's rows in row order (half the k per thread) -- one partial per (m-tile, k, n); g, the
-    // [M, N] gradient the separate pass re-read with Y, is never stored
-    // x rows in LDS with KP floats: x1 | x2 | 1 (the bias row, k = ks) | zeros; a thread takes KH = 10
-    // consecutive k of one column and advances two of them per v_pk_fma_f32 (the same fma per element)
-    constexpr int KP = 20, KH = KP / 2;
+    // conv1 output): the accumulators go to per-wave LDS images and the block's [BM][wk1 + wk2] input
+    // rows beside them (x1 | x2 | 1 for the bias | zeros, KP floats a row); then two threads per column
+    // each stream half the block's rows -- the addend C and conv1's output Y read row by row, 256
+    // contiguous bytes per wave and row, U rows in flight -- form dZ = (Y > 0) ? acc (+ C) : 0 and
+    // advance the column's KP sums two at a time (v_pk_fma_f32); the two halves are added in a fixed
+    // order.  One partial per (m-tile, k, n); g, the [M, N] gradient the separate pass re-read with Y,
+    // is never stored.  (The first form loaded Y and C per accumulator register before the images,
+    // one dependent 4-byte load after another: 2.94 ms against 1.76 for the plain launch at 200 K rows.)
+    constexpr int KP = 20, RH = BM / 2, U = 8;
     static_assert(NW * 64 == 2 * BN, "two threads per output column");
     static_assert((NW * TM * 16 * HP + BM * KP) * 4 <= 2 * TILE_BYTES, "images fit the tile buffers");
+    static_assert(RH % U == 0, "whole row groups");
     float *const wimg = reinterpret_cast<float *>(smem);
     float *const xs = wimg + NW * TM * 16 * HP;
     const int ks = a.wk1 + a.wk2;
-    const bool inner = mw + TM * 16 <= a.M && nw + BN <= a.N;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t col = nw + j * 16 + fr;
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = mw + i * 16 + 4 * fg + r;
-          const bool ok = inner || (row < a.M && col < a.N);
-          const int64_t rr = ok ? row : 0, cc = ok ? col : 0;
-          float g = acc[i][j][r];
-          if (a.accum) g = g + a.C[rr * a.ldc + cc];
-          const float y = a.wy[rr * a.ldwy + cc];
-          wimg[wave * (TM * 16 * HP) + (i * 16 + 4 * fg + r) * HP + j * 16 + fr] = (ok && y > 0.f) ? g : 0.f;
-        }
-    }
+        for (int r = 0; r < 4; ++r)
+          wimg[wave * (TM * 16 * HP) + (i * 16 + 4 * fg + r) * HP + j * 16 + fr] = acc[i][j][r];
     for (int q = tid; q < BM * KP; q += NW * 64) {
       const int r = q / KP, k = q % KP;
       const int64_t row = m0 + r;
@@ -597,24 +593,47 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
       xs[q] = x;
     }
     __syncthreads();
-    const int c = tid % BN, kb = (tid / BN) * KH;
-    f32x2 sk[KH / 2];
-#pragma unroll
-    for (int u = 0; u < KH / 2; ++u) sk[u] = f32x2{0.f, 0.f};
-    for (int r = 0; r < BM; ++r) {
-      const float d = wimg[(r / (TM * 16)) * (TM * 16 * HP) + (r % (TM * 16)) * HP + c];
-      const f32x2 *xr = reinterpret_cast<const f32x2 *>(xs + r * KP + kb);
-#pragma unroll
-      for (int u = 0; u < KH / 2; ++u) sk[u] = __builtin_elementwise_fma(f32x2{d, d}, xr[u], sk[u]);
-    }
+    const int c = tid % BN, h = tid / BN;
     const int64_t col = nw + c;
-    if (col < a.N) {
+    const bool cok = col < a.N;
+    const bool acc_c = a.accum != 0;
+    f32x2 sk[KP / 2];
+#pragma unroll
+    for (int u = 0; u < KP / 2; ++u) sk[u] = f32x2{0.f, 0.f};
+    for (int r0 = h * RH; r0 < h * RH + RH; r0 += U) {
+      float yv[U], cv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = m0 + r0 + u;
+        const bool ok = cok && row < a.M;
+        yv[u] = ok ? a.wy[row * a.ldwy + col] : 0.f;
+        cv[u] = (ok && acc_c) ? a.C[row * a.ldc + col] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int lr = r0 + u;
+        float d = wimg[(lr / (TM * 16)) * (TM * 16 * HP) + (lr % (TM * 16)) * HP + c];
+        if (acc_c) d = d + cv[u];
+        d = yv[u] > 0.f ? d : 0.f;
+        const f32x2 *xr = reinterpret_cast<const f32x2 *>(xs + lr * KP);
+#pragma unroll
+        for (int p = 0; p < KP / 2; ++p) sk[p] = __builtin_elementwise_fma(f32x2{d, d}, xr[p], sk[p]);
+      }
+    }
+    __syncthreads();  // the images are read: the upper half's sums go through LDS
+    float *const hs = wimg;
+    if (h == 1) {
+#pragma unroll
+      for (int p = 0; p < KP / 2; ++p) *reinterpret_cast<f32x2 *>(hs + c * KP + 2 * p) = sk[p];
+    }
+    __syncthreads();
+    if (h == 0 && cok) {
       float *const pp = a.wpart + (m0 / BM) * (int64_t)(ks + 1) * a.N + col;
 #pragma unroll
-      for (int u = 0; u < KH / 2; ++u)
+      for (int p = 0; p < KP / 2; ++p)
 #pragma unroll
         for (int e = 0; e < 2; ++e)
-          if (kb + 2 * u + e <= ks) pp[(int64_t)(kb + 2 * u + e) * a.N] = sk[u][e];
+          if (2 * p + e <= ks) pp[(int64_t)(2 * p + e) * a.N] = sk[p][e] + hs[c * KP + 2 * p + e];
     }
     return;
   }
@@ -1010,8 +1029,8 @@ int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
 }
 
 // FC kernel choice, per call in flags bits 8-11 (LPG_FC_KERNEL(k), include/lpgnn.h): 0 = fc_x3_wide
-// <4,2,8,2> when wide_ok (else 1), 1 = fc_fwd_x3_16 <4,1,2,8>, 2 = fc_x3_wide in the n-split tile
-// order (X3Args::order).  Same MFMA shape, k order and product
+// <4,2,8,2> in the n-split tile order when wide_ok (else 1), 1 = fc_fwd_x3_16 <4,1,2,8>, 2 = fc_x3_wide
+// in round 3's contiguous-m tile order (X3Args::order).  Same MFMA shape, k order and product
 // sequence per output: the same C, bit for bit.  (tools/experiments/exp_wide.py at the c2 shapes:
 // 207-221 TF/s for the wide form, +3-6 % over fc_fwd_x3_16.)
 constexpr int kX3Kernels = 2;
@@ -1077,7 +1096,7 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
   const int kern = (flags >> 8) & 15;
-  a.order = kern == 2 ? 1 : 0;
+  a.order = kern == 2 ? 0 : 1;
   if (kern != 1 && wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);
   return launch_x3_16<4, 1, 2, 8>(a, relu, s);
 }
@@ -1113,7 +1132,7 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   // one partial per (128-column tile, row); fc_x3_wide carries three head slots, so hn = 4 (and the
   // per-call alternative) takes fc_fwd_x3_16 -- the same C, bit for bit
   lpg_status r;
-  a.order = ((flags >> 8) & 15) == 2 ? 1 : 0;
+  a.order = ((flags >> 8) & 15) == 2 ? 0 : 1;
   if (hn <= 3 && ((flags >> 8) & 15) != 1 && wide_ok(a, 128, 128))
     r = launch_x3_wide<4, 2, 8, 2, true>(a, flags & 1, s);
   else
@@ -1214,6 +1233,7 @@ extern "C" lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1,
   a.wk2 = (int32_t)ks2;
   float *part = static_cast<float *>(workspace);
   a.wpart = part;
+  a.order = 1;
   lpg_status r = launch_x3_wide<4, 2, 8, 2, false, true>(a, false, s);
   if (r != LPG_OK) return r;
   const int64_t mt = (M + 127) / 128;

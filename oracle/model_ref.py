@@ -320,19 +320,44 @@ def graph_conv_fp16(x_src, x_dst, adj, W_rel, b_rel, W_root, relu=False, reassoc
     return r16(torch.relu(out) if relu else out)
 
 
+def _fma_f32_exact(a64: np.ndarray, b64: np.ndarray, c32: np.ndarray) -> np.ndarray:
+    """fma(a, b, c) correctly rounded to fp32 for a * b exact in fp64 (fp16 operands) and fp32 c:
+    TwoSum of the product and c, then a round-to-nearest-even of hi + lo that resolves fp64 ties."""
+    p = a64 * b64
+    c = c32.astype(np.float64)
+    hi = p + c
+    bb = hi - p
+    lo = (p - (hi - bb)) + (c - bb)
+    r = hi.astype(np.float32)
+    r64 = r.astype(np.float64)
+    diff = hi - r64
+    other = np.nextafter(r, np.where(diff > 0, np.float32(np.inf), np.float32(-np.inf)).astype(np.float32))
+    tie = (diff != 0) & (np.abs(diff) * 2 == np.abs(other.astype(np.float64) - r64))
+    return np.where(tie & (np.sign(lo) == np.sign(diff)), other, r)
+
+
 def add_knowledge_fp16(logit16, feas, bound=10):
-    """arch.py:129-141 on fp16 logits, as torch's half ops evaluate it (lpg_knowledge_f16): the norm
-    in fp32 (sqrt of fma(x2, x2, fma(x1, x1, x0 x0)), the fmas evaluated in fp64 and rounded), then
-    rounded; clamp_min(1e-12) of a half tensor = max(n, 0); every op's result rounded to fp16."""
-    x = logit16.float().double()
-    ss = (x[:, 0] * x[:, 0]).float().double()
-    ss = (x[:, 1] * x[:, 1] + ss).float().double()
-    ss = (x[:, 2] * x[:, 2] + ss).float()
-    n = r16(torch.sqrt(ss)).clamp_min(0.0)
-    y = r16(r16(logit16.float() / n[:, None]) * 10)
-    y[feas[:, -3] != 0, 0] = r16(y[feas[:, -3] != 0, 0] - bound)
-    y[feas[:, -1] != 0, 2] = r16(y[feas[:, -1] != 0, 2] - bound)
-    return y
+    """arch.py:129-141 on fp16 logits as torch's half ops define it on the device the reference's
+    --fp16 mode runs on (lpg_knowledge_f16): each op computes in fp32 with IEEE-correct rounding and
+    stores fp16 -- n = fp16(sqrt(fma(x2, x2, fma(x1, x1, x0 x0)))), clamp_min(1e-12) of a half tensor
+    = max(n, 0), y = fp16(fp16(x / n) * 10), y0 / y2 = fp16(y - bound) where the masks say so.  Restated
+    with numpy's IEEE float32 sqrt / divide and an exact fma (torch's vectorised CPU sqrt is not
+    correctly rounded on every host: one box's oracle differed in 3 of 720 000 values)."""
+    x16 = logit16.numpy().astype(np.float16)
+    x = x16.astype(np.float64)
+    ss = (x[:, 0] * x[:, 0]).astype(np.float32)  # exact: 22-bit product
+    ss = _fma_f32_exact(x[:, 1], x[:, 1], ss)
+    ss = _fma_f32_exact(x[:, 2], x[:, 2], ss)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        n = np.sqrt(ss).astype(np.float16).astype(np.float32)
+        d = np.maximum(n, np.float32(0.0))
+        q = (x16.astype(np.float32) / d[:, None]).astype(np.float16).astype(np.float32)
+        y = (q * np.float32(10.0)).astype(np.float16).astype(np.float32)
+    m0 = feas[:, -3].numpy() != 0
+    m2 = feas[:, -1].numpy() != 0
+    y[m0, 0] = (y[m0, 0] - np.float32(bound)).astype(np.float16).astype(np.float32)
+    y[m2, 2] = (y[m2, 2] - np.float32(bound)).astype(np.float16).astype(np.float32)
+    return torch.from_numpy(y)
 
 
 def gcn_fc_forward_fp16(sd, x_s, x_t, A, AT, depth: int, keep=None):

@@ -107,7 +107,7 @@ def test_x3_kernels_identical_when_strides_differ():
 def test_x3_wide_variants_bitwise(M, N, K1, K2, accum, drop):
     """fc_x3_wide (the default): buffer_load ... lds staging and wide wave strips, the same MFMA
     shape, k order and product sequence per output as fc_fwd_x3_16 (LPG_FC_KERNEL(1)) and as itself in
-    the n-split tile order (LPG_FC_KERNEL(2)) -- bitwise the same C, incl. ragged edges (clamped rows/columns), dropout and the accumulate flag's addend."""
+    round 3's tile order (LPG_FC_KERNEL(2)) -- bitwise the same C, incl. ragged edges (clamped rows/columns), dropout and the accumulate flag's addend."""
     from lpgnn.fc import fc_forward
 
     g = torch.Generator().manual_seed(M + N + K1)
@@ -120,7 +120,7 @@ def test_x3_wide_variants_bitwise(M, N, K1, K2, accum, drop):
     outs = [fc_forward(A1, W1, A2, W2, b, True, drop, 5, out=None if P is None else P.clone(), accumulate=accum,
                        arith="x3", kernel=k) for k in (1, 0, 2)]
     assert torch.equal(outs[0], outs[1])
-    assert torch.equal(outs[0], outs[2])  # choice 2: the same kernel in the n-split tile order
+    assert torch.equal(outs[0], outs[2])  # choice 2: the default kernel in round 3's tile order
 
 
 @pytest.mark.parametrize("M,N,K,hn,accum,drop", [

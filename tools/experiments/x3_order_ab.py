@@ -1,6 +1,8 @@
-"""A/B of the x3 FC's tile orders at the c2 shapes: LPG_FC_KERNEL(0) (each XCD walks contiguous
-m-tiles with all their n-tiles) against LPG_FC_KERNEL(2) (n-split: half the XCDs take the first half of
-the n-tiles), alternating in one process; checks the outputs are bitwise equal.
+"""A/B of the x3 FC's tile orders at the c2 shapes, alternating in one process, outputs checked
+bitwise equal.  Round 4 ran it with LPG_FC_KERNEL(0) = the m-major order (each XCD walks contiguous
+m-tiles with all their n-tiles) and (2) = the n-split order (half the XCDs take the first half of the
+n-tiles), profiles/r04_x3_order_ab.log; the n-split order has been kernel 0 (the default) since, and
+kernel 2 the m-major order.
 
   python tools/experiments/x3_order_ab.py
 """

@@ -6,17 +6,18 @@
 # built on the CPU side with
 #   make -C lp-gnn_amd OUT=../tools/experiments/var_x3p1/liblpgnn_hip.so OBJDIR=build_x3p1 EXTRA=-DLPG_X3_TRAFFIC_PROBE=1
 #   make -C lp-gnn_amd OUT=../tools/experiments/var_x3p2/liblpgnn_hip.so OBJDIR=build_x3p2 EXTRA=-DLPG_X3_TRAFFIC_PROBE=2
-#   nsplit: the default library with LPG_FC_KERNEL(2), the n-split tile order
+#   order0: the library with LPG_FC_KERNEL(2), round 3's m-major tile order (the default is the n-split
+#           order since round 4; the probe builds keep the m-major order)
 # plus an SQ/GRBM pass (MFMA busy, clock) of the default.  Summary: gpurun_out/x3traffic/summary.json.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT=gpurun_out/x3traffic; mkdir -p "$OUT"; export TMPDIR=/tmp
-VARIANTS=${VARIANTS:-"default x3p1 x3p2 nsplit"}
+VARIANTS=${VARIANTS:-"default x3p1 x3p2 order0"}
 DRIVER=${DRIVER:-tools/experiments/x3_k2048_pmc.py}
 for v in $VARIANTS; do
   unset X3_KERNEL
   if [ "$v" = default ]; then unset LPGNN_LIB
-  elif [ "$v" = nsplit ]; then unset LPGNN_LIB; export X3_KERNEL=2   # the library's n-split tile order
+  elif [ "$v" = order0 ]; then unset LPGNN_LIB; export X3_KERNEL=2   # round 3's m-major tile order
   else export LPGNN_LIB="$PWD/tools/experiments/var_$v/liblpgnn_hip.so"; fi
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/${v}_$c" -o run -- python3 $DRIVER > "$OUT/${v}_$c.log" 2>&1
