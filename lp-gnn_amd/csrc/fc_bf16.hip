@@ -55,6 +55,10 @@ struct FcB16Args {
   float mscale;
   int64_t row_off;  // the dropout key of row m is row_keys[m] if given, else row_off + m (drop_row)
   const int64_t *row_keys;
+  // fc_bf16_p's tile order: 0 = each XCD walks contiguous m-tiles with all their n-tiles; 1 = n-split
+  // (the first half of the block ids -- XCDs 0-3 -- take n-tiles [0, nt/2) of every m-tile, the second
+  // half the rest: an XCD's round reads half of W and twice the A panels)
+  int32_t order;
 };
 
 
@@ -622,8 +626,19 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
   const int64_t bid = blockIdx.x;
   const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
   const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
-  const int64_t m0 = (wgid / a.nt) * BM;
-  const int64_t n0 = (wgid % a.nt) * BN;
+  int64_t mi = wgid / a.nt, ni = wgid % a.nt;
+  if (a.order == 1 && a.nt >= 2) {
+    const int64_t nh = a.nt / 2, t0 = a.mt * nh;
+    if (wgid < t0) {
+      mi = wgid / nh;
+      ni = wgid % nh;
+    } else {
+      mi = (wgid - t0) / (a.nt - nh);
+      ni = nh + (wgid - t0) % (a.nt - nh);
+    }
+  }
+  const int64_t m0 = mi * BM;
+  const int64_t n0 = ni * BN;
   const int64_t mrows = a.M - m0 < BM ? a.M - m0 : BM;
   const int64_t ncols = a.N - n0 < BN ? a.N - n0 : BN;
 
@@ -1033,10 +1048,11 @@ bool p_ok(const FcB16Args &a) {
 // Kernel choice, per call in flags bits 8-11 (LPG_FC_KERNEL(k), include/lpgnn.h): 0 = by shape
 // (128 x 128 below 4096 rows, else the pipelined kernel when p_ok, else 256 x 256), 1 = fc_fwd_bf16
 // 128 x 128 (4 waves), 2 = fc_fwd_bf16 256 x 256 (8 waves), 3 = fc_bf16_p (falls back to 2 when
-// !p_ok).  Every choice computes the same bits.  Measured at the c5 shapes
+// !p_ok), 4 = choice 0 with fc_bf16_p in the n-split tile order (FcB16Args::order).  Every choice
+// computes the same bits.  Measured at the c5 shapes
 // (profiles/r02_kbench_bf16.log, r02_kbench_fck10.log): fc_bf16_p 1212-1300 TF/s vs hipBLASLt
 // 1248-1268, fc_fwd_bf16 256^2 1033; wgrad_bf16 1172-1222 vs hipBLASLt's bf16-output GEMM 924-1004.
-constexpr int kKernels = 3;
+constexpr int kKernels = 4;
 
 int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
   const int64_t tiles = ((N + 255) / 256) * ((K + 255) / 256);
@@ -1341,8 +1357,9 @@ FcB16Args rows_from(const FcB16Args &a, int64_t r) {
 template <class E>
 lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
   if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<E, 2, 2, 4, 4>(a, relu, s);  // 128 x 128
-  if ((kernel == 0 || kernel == 3) && p_ok(a)) {
-    if (kernel == 0) {
+  if ((kernel == 0 || kernel == 3 || kernel == 4) && p_ok(a)) {
+    a.order = kernel == 4 ? 1 : 0;
+    if (kernel == 0 || kernel == 4) {
       // The last round of 256 x 256 tiles (one block per CU) is usually partial: c5's 200 K rows are 24
       // rounds + 41 % of one, 100 K rows 12 + 21 %, and the CUs without a tile idle for a whole block
       // time.  Those rows run as a second launch on 128 x 128 tiles (4 x the blocks, 2 per CU) -- the

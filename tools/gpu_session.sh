@@ -38,6 +38,7 @@ for s in $STAGES; do
         -p no:cacheprovider -rf --timeout 120 --timeout-method thread ;;
     x3traffic) step x3traffic 420 bash tools/experiments/x3_traffic_probe.sh ;;
     x3ab) step x3ab 300 python tools/experiments/x3_order_ab.py ;;
+    bf16ab) step bf16ab 300 python tools/experiments/bf16_order_ab.py ;;
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py ;;
     prof)
