@@ -571,7 +571,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
     // order.  One partial per (m-tile, k, n); g, the [M, N] gradient the separate pass re-read with Y,
     // is never stored.  (The first form loaded Y and C per accumulator register before the images,
     // one dependent 4-byte load after another: 2.94 ms against 1.76 for the plain launch at 200 K rows.)
-    constexpr int KP = 20, RH = BM / 2, U = 8;
+    constexpr int KP = 20, RH = BM / 2, U = 4;
     static_assert(NW * 64 == 2 * BN, "two threads per output column");
     static_assert((NW * TM * 16 * HP + BM * KP) * 4 <= 2 * TILE_BYTES, "images fit the tile buffers");
     static_assert(RH % U == 0, "whole row groups");
@@ -593,22 +593,28 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
       xs[q] = x;
     }
     __syncthreads();
-    const int c = tid % BN, h = tid / BN;
+    const int c = tid % BN, h = __builtin_amdgcn_readfirstlane(tid / BN);  // wave-uniform half
     const int64_t col = nw + c;
     const bool cok = col < a.N;
     const bool acc_c = a.accum != 0;
     f32x2 sk[KP / 2];
 #pragma unroll
     for (int u = 0; u < KP / 2; ++u) sk[u] = f32x2{0.f, 0.f};
-    for (int r0 = h * RH; r0 < h * RH + RH; r0 += U) {
-      float yv[U], cv[U];
+    // rows in groups of U, the next group's Y / C loads issued before the current group's arithmetic
+    // (two register sets, alternating at compile time: a copy between them made hipcc wait first)
+    auto load = [&](int r0, float (&yv)[U], float (&cv)[U]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) {  // unconditional loads at clamped addresses (a conditional load
+        // became a branch with a vmcnt(0) at its join), values selected after
         const int64_t row = m0 + r0 + u;
         const bool ok = cok && row < a.M;
-        yv[u] = ok ? a.wy[row * a.ldwy + col] : 0.f;
-        cv[u] = (ok && acc_c) ? a.C[row * a.ldc + col] : 0.f;
+        const int64_t rr = row < a.M ? row : a.M - 1, cc = cok ? col : a.N - 1;
+        const float y = a.wy[rr * a.ldwy + cc], cval = a.C[rr * a.ldc + cc];
+        yv[u] = ok ? y : 0.f;
+        cv[u] = (ok && acc_c) ? cval : 0.f;
       }
+    };
+    auto rows = [&](int r0, const float (&yv)[U], const float (&cv)[U]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int lr = r0 + u;
@@ -619,6 +625,15 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
 #pragma unroll
         for (int p = 0; p < KP / 2; ++p) sk[p] = __builtin_elementwise_fma(f32x2{d, d}, xr[p], sk[p]);
       }
+    };
+    static_assert(RH % (2 * U) == 0, "pairs of row groups");
+    float ya[U], ca[U], yb[U], cb[U];
+    load(h * RH, ya, ca);
+    for (int r0 = h * RH; r0 < h * RH + RH; r0 += 2 * U) {
+      load(r0 + U, yb, cb);
+      rows(r0, ya, ca);
+      load(r0 + 2 * U, ya, ca);  // past the last group: rows of the other half, never used (no branch)
+      rows(r0 + U, yb, cb);
     }
     __syncthreads();  // the images are read: the upper half's sums go through LDS
     float *const hs = wimg;
