@@ -564,17 +564,14 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   if constexpr (WGK) {
     // conv1's weight gradient folded into this input-gradient GEMM (the hidden layer's dZ W for the
     // conv1 output): the accumulators go to per-wave LDS images and the block's [BM][wk1 + wk2] input
-    // rows beside them (x1 | x2 | 1 for the bias | zeros, KP floats a row); then two threads per column
-    // each stream half the block's rows -- the addend C and conv1's output Y read row by row, 256
-    // contiguous bytes per wave and row, U rows in flight -- form dZ = (Y > 0) ? acc (+ C) : 0 and
-    // advance the column's KP sums two at a time (v_pk_fma_f32); the two halves are added in a fixed
-    // order.  One partial per (m-tile, k, n); g, the [M, N] gradient the separate pass re-read with Y,
+    // rows beside them (x1 | x2 | 1 for the bias | zeros, KP floats a row); then each wave streams a
+    // quarter of the block's rows -- the addend C and conv1's output Y read row by row, 512 contiguous
+    // bytes per wave and row, U rows in flight -- forms dZ = (Y > 0) ? acc (+ C) : 0 for its lane's two
+    // columns and advances their KP sums (v_pk_fma_f32); the four quarters are added in a fixed order.  One partial per (m-tile, k, n); g, the [M, N] gradient the separate pass re-read with Y,
     // is never stored.  (The first form loaded Y and C per accumulator register before the images,
     // one dependent 4-byte load after another: 2.94 ms against 1.76 for the plain launch at 200 K rows.)
-    constexpr int KP = 20, RH = BM / 2, U = 4;
-    static_assert(NW * 64 == 2 * BN, "two threads per output column");
+    constexpr int KP = 20, U = 4;
     static_assert((NW * TM * 16 * HP + BM * KP) * 4 <= 2 * TILE_BYTES, "images fit the tile buffers");
-    static_assert(RH % U == 0, "whole row groups");
     float *const wimg = reinterpret_cast<float *>(smem);
     float *const xs = wimg + NW * TM * 16 * HP;
     const int ks = a.wk1 + a.wk2;
@@ -593,62 +590,74 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
       xs[q] = x;
     }
     __syncthreads();
-    const int c = tid % BN, h = __builtin_amdgcn_readfirstlane(tid / BN);  // wave-uniform half
-    const int64_t col = nw + c;
-    const bool cok = col < a.N;
+    // wave q streams rows 32 q .. 32 q + 31 (wave-uniform, so the x rows are broadcast reads), lane l
+    // columns 2 l and 2 l + 1: one x read serves four fmas, one 8-byte Y / C / d load two columns
+    constexpr int RQ = BM / NW;
+    static_assert(BN == 128 && RQ % (2 * U) == 0, "a wave row covers the 128 columns in pairs");
+    const int64_t col0 = nw + 2 * lane;
+    const bool cok0 = col0 < a.N;  // (N even: the pair is in or out together)
+    const int64_t cc = cok0 ? col0 : a.N - 2;
     const bool acc_c = a.accum != 0;
-    f32x2 sk[KP / 2];
+    f32x2 s0[KP / 2], s1[KP / 2];
 #pragma unroll
-    for (int u = 0; u < KP / 2; ++u) sk[u] = f32x2{0.f, 0.f};
+    for (int u = 0; u < KP / 2; ++u) s0[u] = s1[u] = f32x2{0.f, 0.f};
     // rows in groups of U, the next group's Y / C loads issued before the current group's arithmetic
-    // (two register sets, alternating at compile time: a copy between them made hipcc wait first)
-    auto load = [&](int r0, float (&yv)[U], float (&cv)[U]) {
+    // (two register sets, alternating at compile time: a copy between them made hipcc wait first);
+    // unconditional loads at clamped addresses (a conditional load became a branch with a vmcnt(0) at
+    // its join), values selected after
+    auto load = [&](int r0, f32x2 (&yv)[U], f32x2 (&cv)[U]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {  // unconditional loads at clamped addresses (a conditional load
-        // became a branch with a vmcnt(0) at its join), values selected after
+      for (int u = 0; u < U; ++u) {
         const int64_t row = m0 + r0 + u;
-        const bool ok = cok && row < a.M;
-        const int64_t rr = row < a.M ? row : a.M - 1, cc = cok ? col : a.N - 1;
-        const float y = a.wy[rr * a.ldwy + cc], cval = a.C[rr * a.ldc + cc];
-        yv[u] = ok ? y : 0.f;
-        cv[u] = (ok && acc_c) ? cval : 0.f;
+        const bool ok = cok0 && row < a.M;
+        const int64_t rr = row < a.M ? row : a.M - 1;
+        const f32x2 y = *reinterpret_cast<const f32x2 *>(a.wy + rr * a.ldwy + cc);
+        const f32x2 cval = *reinterpret_cast<const f32x2 *>(a.C + rr * a.ldc + cc);
+        yv[u] = ok ? y : f32x2{0.f, 0.f};
+        cv[u] = (ok && acc_c) ? cval : f32x2{0.f, 0.f};
       }
     };
-    auto rows = [&](int r0, const float (&yv)[U], const float (&cv)[U]) {
+    auto rows = [&](int r0, const f32x2 (&yv)[U], const f32x2 (&cv)[U]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int lr = r0 + u;
-        float d = wimg[(lr / (TM * 16)) * (TM * 16 * HP) + (lr % (TM * 16)) * HP + c];
+        f32x2 d = *reinterpret_cast<const f32x2 *>(wimg + (lr / (TM * 16)) * (TM * 16 * HP) + (lr % (TM * 16)) * HP +
+                                                   2 * lane);
         if (acc_c) d = d + cv[u];
-        d = yv[u] > 0.f ? d : 0.f;
+        const float d0 = yv[u][0] > 0.f ? d[0] : 0.f, d1 = yv[u][1] > 0.f ? d[1] : 0.f;
         const f32x2 *xr = reinterpret_cast<const f32x2 *>(xs + lr * KP);
 #pragma unroll
-        for (int p = 0; p < KP / 2; ++p) sk[p] = __builtin_elementwise_fma(f32x2{d, d}, xr[p], sk[p]);
+        for (int p = 0; p < KP / 2; ++p) {
+          const f32x2 x = xr[p];
+          s0[p] = __builtin_elementwise_fma(f32x2{d0, d0}, x, s0[p]);
+          s1[p] = __builtin_elementwise_fma(f32x2{d1, d1}, x, s1[p]);
+        }
       }
     };
-    static_assert(RH % (2 * U) == 0, "pairs of row groups");
-    float ya[U], ca[U], yb[U], cb[U];
-    load(h * RH, ya, ca);
-    for (int r0 = h * RH; r0 < h * RH + RH; r0 += 2 * U) {
+    f32x2 ya[U], ca[U], yb[U], cb[U];
+    load(wave * RQ, ya, ca);
+    for (int r0 = wave * RQ; r0 < wave * RQ + RQ; r0 += 2 * U) {
       load(r0 + U, yb, cb);
       rows(r0, ya, ca);
-      load(r0 + 2 * U, ya, ca);  // past the last group: rows of the other half, never used (no branch)
+      load(r0 + 2 * U, ya, ca);  // past the last group: rows of the next wave, never used (no branch)
       rows(r0 + U, yb, cb);
     }
-    __syncthreads();  // the images are read: the upper half's sums go through LDS
-    float *const hs = wimg;
-    if (h == 1) {
+    __syncthreads();  // the images are read: each wave's sums to LDS, added over the waves in order
+    float *const hs = wimg;  // [wave][k][128 columns]
+    static_assert(NW * KP * BN <= NW * TM * 16 * HP, "partial image fits the accumulator images");
 #pragma unroll
-      for (int p = 0; p < KP / 2; ++p) *reinterpret_cast<f32x2 *>(hs + c * KP + 2 * p) = sk[p];
-    }
+    for (int p = 0; p < KP / 2; ++p)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        *reinterpret_cast<f32x2 *>(hs + (wave * KP + 2 * p + e) * BN + 2 * lane) = f32x2{s0[p][e], s1[p][e]};
     __syncthreads();
-    if (h == 0 && cok) {
-      float *const pp = a.wpart + (m0 / BM) * (int64_t)(ks + 1) * a.N + col;
+    float *const pp = a.wpart + (m0 / BM) * (int64_t)(ks + 1) * a.N;
+    for (int o = tid; o < (ks + 1) * BN; o += NW * 64) {
+      const int k = o / BN, c = o % BN;
+      float v = hs[k * BN + c];
 #pragma unroll
-      for (int p = 0; p < KP / 2; ++p)
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-          if (2 * p + e <= ks) pp[(int64_t)(2 * p + e) * a.N] = sk[p][e] + hs[c * KP + 2 * p + e];
+      for (int q = 1; q < NW; ++q) v = v + hs[(q * KP + k) * BN + c];
+      if (nw + c < a.N) pp[(int64_t)k * a.N + nw + c] = v;
     }
     return;
   }
@@ -1221,6 +1230,9 @@ extern "C" lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1,
   LPG_REQUIRE(Y && ldy >= N && (ks1 == 0 || (X1 && ldx1 >= ks1)) && (ks2 == 0 || (X2 && ldx2 >= ks2)),
               "%s: bad Y / X1 / X2", name);
   LPG_REQUIRE(!(flags & LPG_FC_ACCUMULATE) || (C && ldc >= N), "%s: the accumulate flag needs C", name);
+  LPG_REQUIRE(N % 2 == 0 && ldy % 2 == 0 && (reinterpret_cast<uintptr_t>(Y) & 7) == 0 &&
+                  (!(flags & LPG_FC_ACCUMULATE) || (ldc % 2 == 0 && (reinterpret_cast<uintptr_t>(C) & 7) == 0)),
+              "%s: N and the leading dimensions of Y and C even, Y and C 8-byte aligned (column pairs)", name);
   const int64_t ks = ks1 + ks2;
   hipStream_t s = as_stream(stream);
   if (M == 0 || N == 0) {

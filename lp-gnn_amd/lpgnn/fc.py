@@ -261,7 +261,7 @@ def input_grad_relu_wgrad(G1: Tensor, W1: Tensor, G2: Tensor | None, W2: Tensor 
     fit the fused kernel (the caller then takes input_grad + relu_wgrad_smallk)."""
     k1, k2 = X1.shape[1], (0 if X2 is None else X2.shape[1])
     if (G1.dtype != torch.float32 or G1.shape[1] % 32 or (G2 is not None and G2.shape[1] % 32)
-            or W1.shape[1] <= 32 or not 1 <= k1 + k2 <= 16 or Y.dtype != torch.float32):
+            or W1.shape[1] <= 32 or W1.shape[1] % 2 or not 1 <= k1 + k2 <= 16 or Y.dtype != torch.float32):
         return None
     G1, G2 = _prep(G1), _prep(G2)
     if G2 is not None and G2.stride(0) != G1.stride(0):
@@ -271,10 +271,11 @@ def input_grad_relu_wgrad(G1: Tensor, W1: Tensor, G2: Tensor | None, W2: Tensor 
     W2s = split3(W2, transpose=True) if G2 is not None else None
     if W2s is not None and W2s.shape != W1s.shape:
         return None
-    Y = Y if (Y.stride(1) == 1) else Y.contiguous()
+    Y = Y if (Y.stride(1) == 1 and Y.stride(0) % 2 == 0 and Y.data_ptr() % 8 == 0) else Y.contiguous()
     X1 = X1.contiguous()
     X2 = None if X2 is None else X2.contiguous()
-    if addend is not None and (addend.shape != (M, N) or addend.stride(1) != 1 or addend.dtype != torch.float32):
+    if addend is not None and (addend.shape != (M, N) or addend.stride(1) != 1 or addend.dtype != torch.float32
+                               or addend.stride(0) % 2 or addend.data_ptr() % 8):
         return None
     L = _lib.lib()
     dW1 = torch.empty((N, k1), dtype=torch.float32, device=G1.device)
