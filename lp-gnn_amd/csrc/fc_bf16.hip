@@ -55,9 +55,10 @@ struct FcB16Args {
   float mscale;
   int64_t row_off;  // the dropout key of row m is row_keys[m] if given, else row_off + m (drop_row)
   const int64_t *row_keys;
-  // fc_bf16_p's tile order: 0 = each XCD walks contiguous m-tiles with all their n-tiles; 1 = n-split
-  // (the first half of the block ids -- XCDs 0-3 -- take n-tiles [0, nt/2) of every m-tile, the second
-  // half the rest: an XCD's round reads half of W and twice the A panels)
+  // fc_bf16_p's tile order: 1 (the default choice) = n-split (the first half of the block ids -- XCDs
+  // 0-3 -- take n-tiles [0, nt/2) of every m-tile, the second half the rest: an XCD's round reads half
+  // of W and twice the A panels); 0 (choices 3 and 4) = each XCD walks contiguous m-tiles with all
+  // their n-tiles
   int32_t order;
 };
 
@@ -1048,8 +1049,9 @@ bool p_ok(const FcB16Args &a) {
 // Kernel choice, per call in flags bits 8-11 (LPG_FC_KERNEL(k), include/lpgnn.h): 0 = by shape
 // (128 x 128 below 4096 rows, else the pipelined kernel when p_ok, else 256 x 256), 1 = fc_fwd_bf16
 // 128 x 128 (4 waves), 2 = fc_fwd_bf16 256 x 256 (8 waves), 3 = fc_bf16_p (falls back to 2 when
-// !p_ok), 4 = choice 0 with fc_bf16_p in the n-split tile order (FcB16Args::order).  Every choice
-// computes the same bits.  Measured at the c5 shapes
+// !p_ok), 4 = choice 0 with fc_bf16_p in the m-major tile order (FcB16Args::order; the default
+// runs the n-split order: 1020-1225 vs 1020-1202 TF/s at the c5 shapes, profiles/r04_bf16_order_ab.log).
+// Every choice computes the same bits.  Measured at the c5 shapes
 // (profiles/r02_kbench_bf16.log, r02_kbench_fck10.log): fc_bf16_p 1212-1300 TF/s vs hipBLASLt
 // 1248-1268, fc_fwd_bf16 256^2 1033; wgrad_bf16 1172-1222 vs hipBLASLt's bf16-output GEMM 924-1004.
 constexpr int kKernels = 4;
@@ -1358,7 +1360,7 @@ template <class E>
 lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
   if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<E, 2, 2, 4, 4>(a, relu, s);  // 128 x 128
   if ((kernel == 0 || kernel == 3 || kernel == 4) && p_ok(a)) {
-    a.order = kernel == 4 ? 1 : 0;
+    a.order = kernel == 0 ? 1 : 0;  // the default in the n-split order (1-2 % at the c5 shapes)
     if (kernel == 0 || kernel == 4) {
       // The last round of 256 x 256 tiles (one block per CU) is usually partial: c5's 200 K rows are 24
       // rounds + 41 % of one, 100 K rows 12 + 21 %, and the CUs without a tile idle for a whole block

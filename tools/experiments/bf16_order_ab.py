@@ -1,7 +1,8 @@
-"""A/B of the bf16 FC's tile orders at the c5 shapes: LPG_FC_KERNEL(0) (the default: the pipelined
-256 x 256 kernel, each XCD walking contiguous m-tiles with all their n-tiles, + the tail launch) against
-LPG_FC_KERNEL(4) (the same in the n-split order: half the XCDs take the first half of the n-tiles),
-alternating in one process; checks the outputs are bitwise equal.
+"""A/B of the bf16 FC's tile orders at the c5 shapes, alternating in one process, outputs checked bitwise
+equal.  Round 4 ran it with LPG_FC_KERNEL(0) = the pipelined 256 x 256 kernel in the m-major order (each
+XCD walking contiguous m-tiles with all their n-tiles) + the tail launch, and (4) = the same in the
+n-split order (profiles/r04_bf16_order_ab.log); the n-split order has been choice 0 since, choice 4 the
+m-major one.
 
   python tools/experiments/bf16_order_ab.py
 """
