@@ -36,6 +36,9 @@ for s in $STAGES; do
     tests_files)  # PYTEST_FILES (space-separated), every failure reported (maxfail PYTEST_MAXFAIL, default 30)
       step pytest_files 700 python -u -m pytest ${PYTEST_FILES} -m gpu --maxfail ${PYTEST_MAXFAIL:-30} -v \
         -p no:cacheprovider -rf --timeout 120 --timeout-method thread ;;
+    tests_all)  # the whole -m gpu suite, every failure reported
+      step pytest_all 800 python -u -m pytest tests -m gpu --maxfail ${PYTEST_MAXFAIL:-30} -v -p no:cacheprovider -rf \
+        --timeout 300 --timeout-method thread ;;
     x3traffic) step x3traffic 420 bash tools/experiments/x3_traffic_probe.sh ;;
     x3ab) step x3ab 300 python tools/experiments/x3_order_ab.py ;;
     bf16ab) step bf16ab 300 python tools/experiments/bf16_order_ab.py ;;
