@@ -20,7 +20,6 @@ from __future__ import annotations
 import ast
 import math
 import re
-from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F

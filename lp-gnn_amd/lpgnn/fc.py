@@ -21,7 +21,6 @@ runs in lpg_linear_small_bwd_f32.  Tolerance-level parity for gradients.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
