@@ -40,6 +40,7 @@ for s in $STAGES; do
       step pytest_all 800 python -u -m pytest tests -m gpu --maxfail ${PYTEST_MAXFAIL:-30} -v -p no:cacheprovider -rf \
         --timeout 300 --timeout-method thread ;;
     x3traffic) step x3traffic 420 bash tools/experiments/x3_traffic_probe.sh ;;
+    x3calib) step x3calib 180 bash tools/experiments/x3_fetch_calib.sh ;;
     x3ab) step x3ab 300 python tools/experiments/x3_order_ab.py ;;
     bf16ab) step bf16ab 300 python tools/experiments/bf16_order_ab.py ;;
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
