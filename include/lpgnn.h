@@ -156,10 +156,12 @@ lpg_status lpg_spmm_f16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, 
  * benchmarks and tests can pick a kernel per call, without global state.
  *   lpg_fc_x3_f32 / _heads: 1 = fc_fwd_x3_16 (global_load_lds staging), 2 = the default kernel
  *     in round 3's tile order (each XCD walks contiguous m-tiles with all their n-tiles; the default
- *     is the n-split order: half the XCDs take the first half of the n-tiles);
+ *     is the n-split order: half the XCDs take the first half of the n-tiles), 3 = the default kernel
+ *     in the n-quarter order (XCD pairs take a quarter of the n-tiles each);
  *   lpg_fc_bf16 / _relu_bwd: 1 = 128 x 128 tiles, 2 = 256 x 256 tiles,
  *     3 = the pipelined 256 x 256 kernel (the default from 4096 rows, there in the n-split tile
- *     order), 4 = the default choice with the pipelined kernel in the m-major tile order. */
+ *     order), 4 / 5 = the default choice with the pipelined kernel in the m-major / n-quarter
+ *     tile order. */
 #define LPG_FC_RELU 1
 #define LPG_FC_ACCUMULATE 2
 #define LPG_FC_HEADS_ONLY 4 /* lpg_fc_x3_heads_f32 only: C is not written (the logits are the only output;

@@ -637,6 +637,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
       mi = (wgid - t0) / (a.nt - nh);
       ni = nh + (wgid - t0) % (a.nt - nh);
     }
+  } else if (a.order == 2 && a.nt % 4 == 0) {  // n-quarters: XCD pairs take a quarter of the n-tiles each
+    const int64_t nq = a.nt / 4, tq = a.mt * nq, g = wgid / tq, w = wgid % tq;
+    mi = w / nq;
+    ni = g * nq + w % nq;
   }
   const int64_t m0 = mi * BM;
   const int64_t n0 = ni * BN;
@@ -1049,12 +1053,12 @@ bool p_ok(const FcB16Args &a) {
 // Kernel choice, per call in flags bits 8-11 (LPG_FC_KERNEL(k), include/lpgnn.h): 0 = by shape
 // (128 x 128 below 4096 rows, else the pipelined kernel when p_ok, else 256 x 256), 1 = fc_fwd_bf16
 // 128 x 128 (4 waves), 2 = fc_fwd_bf16 256 x 256 (8 waves), 3 = fc_bf16_p (falls back to 2 when
-// !p_ok), 4 = choice 0 with fc_bf16_p in the m-major tile order (FcB16Args::order; the default
+// !p_ok), 4 / 5 = choice 0 with fc_bf16_p in the m-major / n-quarter tile order (FcB16Args::order; the default
 // runs the n-split order: 1020-1225 vs 1020-1202 TF/s at the c5 shapes, profiles/r04_bf16_order_ab.log).
 // Every choice computes the same bits.  Measured at the c5 shapes
 // (profiles/r02_kbench_bf16.log, r02_kbench_fck10.log): fc_bf16_p 1212-1300 TF/s vs hipBLASLt
 // 1248-1268, fc_fwd_bf16 256^2 1033; wgrad_bf16 1172-1222 vs hipBLASLt's bf16-output GEMM 924-1004.
-constexpr int kKernels = 4;
+constexpr int kKernels = 5;
 
 int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
   const int64_t tiles = ((N + 255) / 256) * ((K + 255) / 256);
@@ -1359,9 +1363,9 @@ FcB16Args rows_from(const FcB16Args &a, int64_t r) {
 template <class E>
 lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
   if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<E, 2, 2, 4, 4>(a, relu, s);  // 128 x 128
-  if ((kernel == 0 || kernel == 3 || kernel == 4) && p_ok(a)) {
-    a.order = kernel == 0 ? 1 : 0;  // the default in the n-split order (1-2 % at the c5 shapes)
-    if (kernel == 0 || kernel == 4) {
+  if ((kernel == 0 || kernel >= 3) && p_ok(a)) {
+    a.order = kernel == 0 ? 1 : kernel == 5 ? 2 : 0;  // the default in the n-split order (1-2 % at the c5 shapes)
+    if (kernel == 0 || kernel == 4 || kernel == 5) {
       // The last round of 256 x 256 tiles (one block per CU) is usually partial: c5's 200 K rows are 24
       // rounds + 41 % of one, 100 K rows 12 + 21 %, and the CUs without a tile idle for a whole block
       // time.  Those rows run as a second launch on 128 x 128 tiles (4 x the blocks, 2 per CU) -- the

@@ -429,6 +429,10 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
       mi = (wgid - t0) / (a.nt - nh);
       ni = nh + (wgid - t0) % (a.nt - nh);
     }
+  } else if (a.order == 2 && a.nt % 4 == 0) {  // n-quarters: XCD pairs take a quarter of the n-tiles each
+    const int64_t nq = a.nt / 4, tq = a.mt * nq, g = wgid / tq, w = wgid % tq;
+    mi = w / nq;
+    ni = g * nq + w % nq;
   }
   const int64_t m0 = mi * BM;
   const int64_t n0 = ni * BN;
@@ -1054,10 +1058,11 @@ int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
 
 // FC kernel choice, per call in flags bits 8-11 (LPG_FC_KERNEL(k), include/lpgnn.h): 0 = fc_x3_wide
 // <4,2,8,2> in the n-split tile order when wide_ok (else 1), 1 = fc_fwd_x3_16 <4,1,2,8>, 2 = fc_x3_wide
-// in round 3's contiguous-m tile order (X3Args::order).  Same MFMA shape, k order and product
+// in round 3's contiguous-m tile order, 3 = fc_x3_wide in the n-quarter order (XCD pairs take a quarter
+// of the n-tiles each; X3Args::order).  Same MFMA shape, k order and product
 // sequence per output: the same C, bit for bit.  (tools/experiments/exp_wide.py at the c2 shapes:
 // 207-221 TF/s for the wide form, +3-6 % over fc_fwd_x3_16.)
-constexpr int kX3Kernels = 2;
+constexpr int kX3Kernels = 3;
 
 }  // namespace
 }  // namespace lpg
@@ -1120,7 +1125,7 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
   hipStream_t s = as_stream(stream);
   const bool relu = flags & 1;
   const int kern = (flags >> 8) & 15;
-  a.order = kern == 2 ? 0 : 1;
+  a.order = kern == 2 ? 0 : kern == 3 ? 2 : 1;
   if (kern != 1 && wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);
   return launch_x3_16<4, 1, 2, 8>(a, relu, s);
 }
@@ -1156,7 +1161,7 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   // one partial per (128-column tile, row); fc_x3_wide carries three head slots, so hn = 4 (and the
   // per-call alternative) takes fc_fwd_x3_16 -- the same C, bit for bit
   lpg_status r;
-  a.order = ((flags >> 8) & 15) == 2 ? 0 : 1;
+  a.order = ((flags >> 8) & 15) == 2 ? 0 : ((flags >> 8) & 15) == 3 ? 2 : 1;
   if (hn <= 3 && ((flags >> 8) & 15) != 1 && wide_ok(a, 128, 128))
     r = launch_x3_wide<4, 2, 8, 2, true>(a, flags & 1, s);
   else

@@ -61,7 +61,7 @@ def test_x3_fused_heads_row_keys():
     assert torch.equal(sub, full[idx]) and torch.equal(lgs, lg[idx])
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("M,N,K1,K2", [(5000, 512, 128, 128), (700, 256, 64, 0), (3000, 256, 8, 8)])
 def test_bf16_fc_row_keys(kernel, M, N, K1, K2):
     from lpgnn.fc import fc_forward_bf16

@@ -66,7 +66,7 @@ def test_x3_fused_heads_mask_equals_oracle():
     _check(y, base, seed, np.arange(M), 0.1)
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("M,N,K1,K2", [(5000, 512, 128, 128), (700, 256, 64, 0), (3000, 256, 8, 8)])
 def test_bf16_kernels_mask_equals_oracle(kernel, M, N, K1, K2):
     from lpgnn.fc import fc_forward_bf16

@@ -118,9 +118,10 @@ def test_x3_wide_variants_bitwise(M, N, K1, K2, accum, drop):
     b = torch.randn(N, generator=g).to(DEV)
     P = torch.randn(M, N, generator=g).to(DEV) if accum else None
     outs = [fc_forward(A1, W1, A2, W2, b, True, drop, 5, out=None if P is None else P.clone(), accumulate=accum,
-                       arith="x3", kernel=k) for k in (1, 0, 2)]
+                       arith="x3", kernel=k) for k in (1, 0, 2, 3)]
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(outs[0], outs[2])  # choice 2: the default kernel in round 3's tile order
+    assert torch.equal(outs[0], outs[3])  # choice 3: the n-quarter order
 
 
 @pytest.mark.parametrize("M,N,K,hn,accum,drop", [

@@ -45,21 +45,21 @@ def main():
         b = torch.randn(N, device="cuda")
         P = torch.zeros(M, N, device="cuda").to(BF) if acc else None
         flops = 2.0 * M * N * (K1 + K2)
-        t = {0: [], 4: []}
+        t = {0: [], 4: [], 5: []}
         run(0, A1, A2, W1, W2, b, P, acc, 3)
         for rnd in range(4):
-            for k in (0, 4) if rnd % 2 == 0 else (4, 0):
+            for k in (0, 4, 5) if rnd % 2 == 0 else (5, 4, 0):
                 t[k].append(run(k, A1, A2, W1, W2, b, P, acc, 10)[0])
         outs = {}
-        for k in (0, 4):
+        for k in (0, 4, 5):
             if acc:
                 P.zero_()
             outs[k] = run(k, A1, A2, W1, W2, b, P, acc, 1)[1].clone()
         line = f"M={M} K={K1}+{K2} N={N} acc+drop={acc}: "
-        for k in (0, 4):
+        for k in (0, 4, 5):
             ms = sorted(t[k])[len(t[k]) // 2]
             line += f"kernel {k}: {ms:.3f} ms ({flops / ms / 1e9:.0f} TF/s)  "
-        print(line + f"bitwise equal: {torch.equal(outs[0], outs[4])}", flush=True)
+        print(line + f"bitwise equal: {torch.equal(outs[0], outs[4]) and torch.equal(outs[0], outs[5])}", flush=True)
         del A1, A2, P
 
 

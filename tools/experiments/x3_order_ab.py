@@ -44,20 +44,20 @@ def main():
         b = torch.randn(N, device="cuda")
         P = torch.zeros(M, N, device="cuda") if acc else None
         flops = 2.0 * M * N * (K1 + K2)
-        t = {0: [], 2: []}
+        t = {0: [], 2: [], 3: []}
         for _ in range(2):
             run(M, K1, K2, N, acc, 0, A1, A2, W1, W2, b, P, 3)
         for rnd in range(4):
-            for k in (0, 2) if rnd % 2 == 0 else (2, 0):
+            for k in (0, 2, 3) if rnd % 2 == 0 else (3, 2, 0):
                 t[k].append(run(M, K1, K2, N, acc, k, A1, A2, W1, W2, b, P, 10)[0])
         outs = {}
-        for k in (0, 2):
+        for k in (0, 2, 3):
             if acc:
                 P.zero_()
             outs[k] = run(M, K1, K2, N, acc, k, A1, A2, W1, W2, b, P, 1)[1].clone()
-        same = torch.equal(outs[0], outs[2])
+        same = torch.equal(outs[0], outs[2]) and torch.equal(outs[0], outs[3])
         line = f"M={M} K={K1}+{K2} N={N} acc+drop={acc}: "
-        for k in (0, 2):
+        for k in (0, 2, 3):
             ms = sorted(t[k])[len(t[k]) // 2]
             line += f"kernel {k}: {ms:.3f} ms ({flops / ms / 1e9:.0f} TF/s)  "
         print(line + f"bitwise equal: {same}", flush=True)
