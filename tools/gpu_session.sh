@@ -76,6 +76,14 @@ for s in $STAGES; do
       python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_spmm.json" \
         "$(python bench.py --print-workload)" || true
       ;;
+    pmc_inf16)  # the fp16 inference sub-record's SpMM traffic
+      step pmc_fetch_inf16 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_inf16" -o run -- \
+        python "$ROOT/bench.py" --inference --fp16 --steps 3 --warmup 1 --profile-only
+      step pmc_write_inf16 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_inf16" -o run -- \
+        python "$ROOT/bench.py" --inference --fp16 --steps 3 --warmup 1 --profile-only
+      python tools/pmc_summary.py "$OUT/pmc_fetch_inf16" "$OUT/pmc_write_inf16" "$OUT/r04_pmc_spmm_inference_fp16.json" \
+        "$(python bench.py --inference --fp16 --print-workload)" || true
+      ;;
     pmc_c5)
       step pmc_fetch_c5 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c5" -o run -- \
         python "$ROOT/bench.py" --config c5 --steps 2 --warmup 1 --profile-only
