@@ -60,6 +60,13 @@ struct FcB16Args {
   // of W and twice the A panels); 0 (choices 3 and 4) = each XCD walks contiguous m-tiles with all
   // their n-tiles
   int32_t order;
+  // 1-bit ReLU masks of a bf16 layer output Y, one byte per 8 columns (bit e of byte t of row m:
+  // Y[m, 8 t + e] > 0): `mo` is written by a forward ReLU FC's store loop beside C, `mi` replaces the
+  // Y rows `my` of the folded ReLU backward (lpg_fc_bf16_relu_bwd_bits): 1/16 of the bytes of Y
+  uint8_t *mo;
+  int64_t ldmo;
+  const uint8_t *mi;
+  int64_t ldmi;
 };
 
 
@@ -115,6 +122,31 @@ __device__ __forceinline__ uint4 relu_bwd8(uint4 g, uint4 y, float scale) {
                     relu_bwd_pk_bf16(g.z, y.z, scale), relu_bwd_pk_bf16(g.w, y.w, scale));
 }
 
+// bit e set iff 16-bit bf16 value e of the 8 in v is > 0 (sign clear, nonzero, not NaN): the y > 0.f
+// test of relu_bwd_pk_bf16 on the stored value
+__device__ __forceinline__ uint32_t pos_bits8(uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t b = 0u;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    b |= ((((w[p] & 0xffffu) - 1u) & 0xffffu) < 0x7f80u ? 1u : 0u) << (2 * p);
+    b |= ((((w[p] >> 16) - 1u) & 0xffffu) < 0x7f80u ? 1u : 0u) << (2 * p + 1);
+  }
+  return b;
+}
+
+// relu_bwd8 with the mask as bits (pos_bits8 of the stored Y): the same product and rounding per pair,
+// so the same bits as relu_bwd8 on Y
+__device__ __forceinline__ uint32_t relu_bwd_pk_bits(uint32_t g, uint32_t b2, float scale) {
+  const lpg_f32x2 gf = {__uint_as_float(g << 16), __uint_as_float(g & 0xffff0000u)};
+  const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(gf * lpg_f32x2{scale, scale}, lpg_bf16x2));
+  return ((b2 & 1u) ? (pk & 0xffffu) : 0u) | ((b2 & 2u) ? (pk & 0xffff0000u) : 0u);
+}
+__device__ __forceinline__ uint4 relu_bwd8_bits(uint4 g, uint32_t b, float scale) {
+  return make_uint4(relu_bwd_pk_bits(g.x, b, scale), relu_bwd_pk_bits(g.y, b >> 2, scale),
+                    relu_bwd_pk_bits(g.z, b >> 4, scale), relu_bwd_pk_bits(g.w, b >> 6, scale));
+}
+
 // The mask rows (Y) of a wave's store loop, issued together after the accumulators are in the
 // image: one memory latency per epilogue instead of one per 16-B chunk (a dependent load inside
 // the store loop cost ~0.3 ms per c5 launch).  Out-of-range chunks read as zeros (never stored).
@@ -126,8 +158,11 @@ __device__ __forceinline__ void load_mask_rows(const FcB16Args &a, int lane, int
     const int q = it * 64 + lane;
     const int lr = q / CPR, ch = q % CPR;
     const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
-    yv[it] = (row < a.M && col < a.N) ? *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col)
-                                      : make_uint4(0u, 0u, 0u, 0u);
+    const bool ok = row < a.M && col < a.N;
+    if (a.mi)  // the mask byte of the chunk's 8 columns in .x
+      yv[it] = make_uint4(ok ? (uint32_t)a.mi[row * a.ldmi + col / 8] : 0u, 0u, 0u, 0u);
+    else
+      yv[it] = ok ? *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col) : make_uint4(0u, 0u, 0u, 0u);
   }
 }
 
@@ -210,7 +245,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
     }
     constexpr int SIT = FM * 16 * CPR / 64;
     uint4 yv[SIT];
-    if (E::kBf16 && a.my) load_mask_rows<SIT, CPR>(a, lane, wrow0, wcol0, yv);  // all in flight before the first use
+    if (E::kBf16 && (a.my || a.mi)) load_mask_rows<SIT, CPR>(a, lane, wrow0, wcol0, yv);  // all in flight before the first use
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -221,7 +256,9 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
       uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
       if (row < a.M && col < a.N) {
         if constexpr (E::kBf16) {  // (the folded ReLU backward: bf16 training only)
-          if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
+          if (a.mi) v = relu_bwd8_bits(v, yv[it].x, a.mscale);
+          else if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
+          if (a.mo) a.mo[row * a.ldmo + col / 8] = (uint8_t)pos_bits8(v);
         }
         *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
       }
@@ -388,8 +425,11 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
     const int q = it * 64 + lane;
     const int lr = q / CPR, ch = q % CPR;
     const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
-    yv[it] = (row < a.M && col < a.N) ? *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col)
-                                      : make_uint4(0u, 0u, 0u, 0u);
+    const bool ok = row < a.M && col < a.N;
+    if (a.mi)  // the mask byte of the chunk's 8 columns in .x
+      yv[it] = make_uint4(ok ? (uint32_t)a.mi[row * a.ldmi + col / 8] : 0u, 0u, 0u, 0u);
+    else
+      yv[it] = ok ? *reinterpret_cast<const uint4 *>(a.my + row * a.ldy + col) : make_uint4(0u, 0u, 0u, 0u);
   };
   auto body = [&](auto acc_c, auto drop_c) {
     constexpr bool ACC = decltype(acc_c)::value, DROP = decltype(drop_c)::value;
@@ -426,7 +466,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
         const uint32_t hi = E::pack(v[2], v[3]);
         *reinterpret_cast<uint2 *>(ip + j * 32) = uint2{lo, hi};
       }
-      if (E::kBf16 && a.my) {
+      if (E::kBf16 && (a.my || a.mi)) {
 #pragma unroll
         for (int u = 0; u < SPI; ++u)
           if (i * SPI + u < SIT) load_y(i * SPI + u);
@@ -443,13 +483,14 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (E::kBf16 && a.my) {  // masked: every chunk formed first (one wait for the mask rows), then the stores back to back
+  if (E::kBf16 && (a.my || a.mi)) {  // masked: every chunk formed first (one wait for the mask rows), then the stores back to back
     uint4 v[SIT];
 #pragma unroll
     for (int it = 0; it < SIT; ++it) {
       const int q = it * 64 + lane;
       const int lr = q / CPR, ch = q % CPR;
-      v[it] = relu_bwd8(*reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16), yv[it], a.mscale);
+      const uint4 g = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
+      v[it] = a.mi ? relu_bwd8_bits(g, yv[it].x, a.mscale) : relu_bwd8(g, yv[it], a.mscale);
     }
 #pragma unroll
     for (int it = 0; it < SIT; ++it) {
@@ -466,7 +507,10 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
     const int lr = q / CPR, ch = q % CPR;
     const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
     const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
-    if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+    if (row < a.M && col < a.N) {
+      *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+      if (E::kBf16 && a.mo) a.mo[row * a.ldmo + col / 8] = (uint8_t)pos_bits8(v);  // the layer's ReLU mask
+    }
   }
 }
 
@@ -1208,6 +1252,11 @@ __global__ __launch_bounds__(256) void fc_smallk_bf16(FcB16Args a, int64_t S) {
             out[jp] = E::pack(t[0], t[1]);
           }
           *reinterpret_cast<uint2 *>(a.C + m * a.ldc + c) = make_uint2(out[0], out[1]);
+          if (E::kBf16 && a.mo) {  // the layer's ReLU mask: this lane's 4 columns and its pair lane's 4 (N % 8 == 0)
+            const uint32_t nib = pos_bits8(make_uint4(out[0], out[1], 0u, 0u)) & 0xfu;
+            const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nib, 0xB1, 0xF, 0xF, false);
+            if ((threadIdx.x & 1) == 0) a.mo[m * a.ldmo + c / 8] = (uint8_t)(nib | (other << 4));
+          }
         }
       }
       if (ch + 1 < nch) {  // the next chunk's rows (loaded a chunk ago) into the other buffer
@@ -1273,7 +1322,8 @@ static lpg_status fc16_entry(const char *name, int64_t M, int64_t N, int64_t K1,
                                   const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
                                   const uint16_t *W2, int64_t ldw2, const float *bias, uint16_t *C, int64_t ldc,
                                   int32_t flags, float dropout_p, uint64_t seed, int64_t row_offset,
-                                  const int64_t *row_keys, void *stream) {
+                                  const int64_t *row_keys, void *stream, uint8_t *mask = nullptr,
+                                  int64_t ldm = 0) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "%s: negative size", name);
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(C != nullptr && ldc >= N, "%s: bad C/ldc", name);
@@ -1285,6 +1335,13 @@ static lpg_status fc16_entry(const char *name, int64_t M, int64_t N, int64_t K1,
   FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, seed, 0u, 1.f, (flags >> 1) & 1,
               nullptr, 0, 1.f, row_offset, row_keys};
   dropout_params(dropout_p, &a.drop_thresh, &a.drop_scale);
+  if (mask) {  // the ReLU mask beside C: only the 16-byte-chunk store loops write it
+    LPG_REQUIRE((flags & LPG_FC_RELU) && N % 8 == 0 && ldc % 8 == 0 && aligned16(C) && ldm >= N / 8,
+                "%s: the mask output needs the ReLU flag, N and ldc multiples of 8, C 16-byte aligned, ldm >= N / 8",
+                name);
+    a.mo = mask;
+    a.ldmo = ldm;
+  }
   lpg_status st;
   if (try_smallk_bf16<E>(a, flags & 1, as_stream(stream), &st)) return st;  // conv1: narrow LP features
   LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0,
@@ -1305,6 +1362,18 @@ extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16
                            dropout_p, seed, row_offset, row_keys, stream);
 }
 
+// lpg_fc_bf16 with the ReLU layer's 1-bit output mask beside C (mask[m][t] bit e: C[m, 8 t + e] > 0),
+// the input of lpg_fc_bf16_relu_bwd_bits in the backward of the layer this output feeds
+extern "C" lpg_status lpg_fc_bf16_mask(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                       const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
+                                       int64_t lda2, const uint16_t *W2, int64_t ldw2, const float *bias, uint16_t *C,
+                                       int64_t ldc, int32_t flags, float dropout_p, uint64_t seed, int64_t row_offset,
+                                       const int64_t *row_keys, uint8_t *mask, int64_t ldm, void *stream) {
+  LPG_REQUIRE(mask != nullptr, "lpg_fc_bf16_mask: NULL mask");
+  return fc16_entry<EBf16>("lpg_fc_bf16_mask", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, bias, C, ldc,
+                           flags, dropout_p, seed, row_offset, row_keys, stream, mask, ldm);
+}
+
 // fp16 storage (the reference's --fp16 inference: model.half(), batch_to(half=True); val.py:269,
 // utils.py:909-915): the bf16 entry's kernels on v_mfma_f32_16x16x32_f16, fp32 accumulation, fp32 bias,
 // one RNE rounding to fp16 per output
@@ -1322,27 +1391,54 @@ extern "C" lpg_status lpg_fc_f16(int64_t M, int64_t N, int64_t K1, const uint16_
 // -- bit for bit lpg_fc_bf16 followed by lpg_relu_bwd_colsum_bf16(C, Y, scale) (whose bias column
 // sums the caller takes from lpg_colsum_bf16 on C).  Saves the separate pass's read of C and
 // write of dZ (c5: 2 x [rows, 2048] bf16 per layer input).
+static lpg_status relu_bwd_entry(const char *name, int64_t M, int64_t N, int64_t K1, const uint16_t *A1,
+                                 int64_t lda1, const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
+                                 int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
+                                 int32_t flags, const uint16_t *Y, int64_t ldy, const uint8_t *mask, int64_t ldm,
+                                 float scale, void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "%s: negative size", name);
+  if (M == 0 || N == 0) return LPG_OK;
+  LPG_REQUIRE(C != nullptr && ldc >= N && (Y ? ldy >= N : (mask != nullptr && ldm >= N / 8)),
+              "%s: bad C/ldc or Y/ldy (mask/ldm)", name);
+  LPG_REQUIRE(N % 8 == 0 && ldc % 8 == 0 && aligned16(C) && (!Y || (ldy % 8 == 0 && aligned16(Y))),
+              "%s: N, ldc, ldy must be multiples of 8, C and Y 16-byte aligned", name);
+  LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "%s: K1, K2 must be multiples of %d", name, BK);
+  LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1), "%s: bad A1/W1", name);
+  LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2), "%s: bad A2/W2", name);
+  LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
+                  (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
+              "%s: A/W must be 16-byte aligned with leading dimensions multiple of 8", name);
+  const int kernel = (flags >> 8) & 15;
+  LPG_REQUIRE((flags & ~0xf02) == 0 && kernel <= kKernels,
+              "%s: only the accumulate flag (2) and a kernel choice are accepted, got 0x%x", name, flags);
+  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, nullptr, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, 0, 0u, 1.f, (flags >> 1) & 1,
+              Y, ldy, scale};
+  if (!Y) {
+    a.mi = mask;
+    a.ldmi = ldm;
+  }
+  return fc_bf16_dispatch<EBf16>(a, false, as_stream(stream), kernel);  // (every kernel's epilogue takes the fold)
+}
+
 extern "C" lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
                                            const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
                                            int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
                                            int32_t flags, const uint16_t *Y, int64_t ldy, float scale, void *stream) {
-  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_bf16_relu_bwd: negative size");
-  if (M == 0 || N == 0) return LPG_OK;
-  LPG_REQUIRE(C != nullptr && ldc >= N && Y != nullptr && ldy >= N, "lpg_fc_bf16_relu_bwd: bad C/ldc or Y/ldy");
-  LPG_REQUIRE(N % 8 == 0 && ldc % 8 == 0 && ldy % 8 == 0 && aligned16(C) && aligned16(Y),
-              "lpg_fc_bf16_relu_bwd: N, ldc, ldy must be multiples of 8, C and Y 16-byte aligned");
-  LPG_REQUIRE(K1 % BK == 0 && K2 % BK == 0, "lpg_fc_bf16_relu_bwd: K1, K2 must be multiples of %d", BK);
-  LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1), "lpg_fc_bf16_relu_bwd: bad A1/W1");
-  LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2), "lpg_fc_bf16_relu_bwd: bad A2/W2");
-  LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
-                  (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
-              "lpg_fc_bf16_relu_bwd: A/W must be 16-byte aligned with leading dimensions multiple of 8");
-  const int kernel = (flags >> 8) & 15;
-  LPG_REQUIRE((flags & ~0xf02) == 0 && kernel <= kKernels,
-              "lpg_fc_bf16_relu_bwd: only the accumulate flag (2) and a kernel choice are accepted, got 0x%x", flags);
-  FcB16Args a{M, N, K1, K2, A1, A2, W1, W2, nullptr, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, 0, 0u, 1.f, (flags >> 1) & 1,
-              Y, ldy, scale};
-  return fc_bf16_dispatch<EBf16>(a, false, as_stream(stream), kernel);  // (every kernel's epilogue takes the fold)
+  LPG_REQUIRE(Y != nullptr, "lpg_fc_bf16_relu_bwd: NULL Y");
+  return relu_bwd_entry("lpg_fc_bf16_relu_bwd", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, C, ldc, flags,
+                        Y, ldy, nullptr, 0, scale, stream);
+}
+
+// lpg_fc_bf16_relu_bwd with the previous layer's ReLU as its 1-bit mask (lpg_fc_bf16_mask's output)
+// instead of its output Y: the same bits, 1/16 of the mask bytes
+extern "C" lpg_status lpg_fc_bf16_relu_bwd_bits(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                                const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
+                                                int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C,
+                                                int64_t ldc, int32_t flags, const uint8_t *mask, int64_t ldm,
+                                                float scale, void *stream) {
+  LPG_REQUIRE(mask != nullptr, "lpg_fc_bf16_relu_bwd_bits: NULL mask");
+  return relu_bwd_entry("lpg_fc_bf16_relu_bwd_bits", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, C, ldc,
+                        flags, nullptr, 0, mask, ldm, scale, stream);
 }
 
 namespace lpg {
@@ -1355,6 +1451,8 @@ FcB16Args rows_from(const FcB16Args &a, int64_t r) {
   t.A2 = a.A2 ? a.A2 + r * a.lda2 : nullptr;
   t.C = a.C + r * a.ldc;
   t.my = a.my ? a.my + r * a.ldy : nullptr;
+  t.mo = a.mo ? a.mo + r * a.ldmo : nullptr;
+  t.mi = a.mi ? a.mi + r * a.ldmi : nullptr;
   t.row_off = a.row_off + r;
   t.row_keys = a.row_keys ? a.row_keys + r : nullptr;
   return t;

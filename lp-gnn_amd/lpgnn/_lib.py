@@ -37,6 +37,8 @@ HEADER_SYMBOLS = (
     "lpg_fc_bf16",
     "lpg_fc_f16",
     "lpg_fc_bf16_relu_bwd",
+    "lpg_fc_bf16_mask",
+    "lpg_fc_bf16_relu_bwd_bits",
     "lpg_colsum_bf16",
     "lpg_transpose_bf16",
     "lpg_wgrad_bf16_workspace_bytes",
@@ -141,6 +143,10 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_bf16_relu_bwd.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
                                        c_p, c_i64, c_i32, c_p, c_i64, ctypes.c_float, c_p]
     L.lpg_fc_bf16_relu_bwd.restype = c_i32
+    L.lpg_fc_bf16_mask.argtypes = L.lpg_fc_f32.argtypes[:-1] + [c_p, c_i64, c_p]
+    L.lpg_fc_bf16_mask.restype = c_i32
+    L.lpg_fc_bf16_relu_bwd_bits.argtypes = L.lpg_fc_bf16_relu_bwd.argtypes
+    L.lpg_fc_bf16_relu_bwd_bits.restype = c_i32
     L.lpg_colsum_bf16.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p]
     L.lpg_colsum_bf16.restype = c_i32
     L.lpg_class_counts_workspace_bytes.argtypes = [c_i64]

@@ -101,21 +101,28 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     # the caller: inside an autograd.Function's forward grad mode is always off.)
     ho = heads is not None and heads_only
 
+    # bf16 ReLU layers also write their output's 1-bit ReLU mask (options.relu_bits): the next layer's
+    # folded ReLU backward reads it instead of the output (lpg_fc_bf16_relu_bwd_bits, 1/16 of the bytes)
+    want_bits = bf16 and relu and opts.relu_bits and f_out % 8 == 0 and left.dtype == torch.bfloat16
+
     def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None, head=None):
-        """(output, aggregate kept for the backward, logits of `head` or None)."""
+        """(output, aggregate kept for the backward, logits of `head` or None, ReLU mask bits or None)."""
         fc = _fc.fc_forward_bf16 if bf16 else fwd32
+        bits = (torch.empty((x_dst.shape[0], f_out // 8), dtype=torch.uint8, device=x_dst.device) if want_bits
+                else None)
+        mo = {} if bits is None else {"mask_out": bits}
         if ra:  # S (x_src W_rel^T), then lin_root + bias + ReLU accumulated onto it in place
             y = spmm_forward(S, fc(x_src, w_rel, None, None, None, False))
             if head is not None:
                 y, lg = fwd32(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True, heads=head,
                               heads_only=ho)
-                return y, None, lg
-            return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True), None, None
+                return y, None, lg, None
+            return fc(x_dst, w_root, None, None, b, relu, dropout, seed, out=y, accumulate=True, **mo), None, None, bits
         agg = spmm_forward(S, x_src) if agg is None else agg
         if head is not None:
             y, lg = fwd32(agg, w_rel, x_dst, w_root, b, relu, dropout, seed, heads=head, heads_only=ho)
-            return y, agg, lg
-        return fc(agg, w_rel, x_dst, w_root, b, relu, dropout, seed), agg, None
+            return y, agg, lg, None
+        return fc(agg, w_rel, x_dst, w_root, b, relu, dropout, seed, **mo), agg, None, bits
 
     side = _side_stream(left.device) if opts.overlap and not ra_l else None
     agg_l = None
@@ -124,13 +131,15 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
         with torch.cuda.stream(side):
             agg_l = spmm_forward(A, right)
     # arch.py:75-77: right' = left2right((left, right), A^T)
-    right_new, agg_r, logit_r = direction(AT, left, right, ws[0], b_l2r, ws[1], seed_r, ra_r, head=hd[1])
+    right_new, agg_r, logit_r, bits_r = direction(AT, left, right, ws[0], b_l2r, ws[1], seed_r, ra_r, head=hd[1])
     if side is not None:
         torch.cuda.current_stream(left.device).wait_stream(side)
         agg_l.record_stream(torch.cuda.current_stream(left.device))
     # arch.py:78-80: left' = right2left((right, left), A)
-    left_new, agg_l, logit_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l, head=hd[0])
+    left_new, agg_l, logit_l, bits_l = direction(A, right, left, ws[2], b_r2l, ws[3], seed_l, ra_l, agg_l,
+                                                 head=hd[0])
     ctx.adj, ctx.relu, ctx.bf16, ctx.opts = adj, relu, bf16, opts
+    ctx.out_bits = (bits_l, bits_r) if want_bits else None
     ctx.f16 = left.dtype == torch.float16
     ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
@@ -165,11 +174,12 @@ class _TwoDirection(torch.autograd.Function):
 
 
 def _link_prev(ctx, prev):
-    ctx.in_scale, ctx.wgk_prev = None, None
+    ctx.in_scale, ctx.wgk_prev, ctx.in_bits = None, None, None
     if prev is None:
         return
     if prev.bf16:
         ctx.in_scale = prev.scale
+        ctx.in_bits = getattr(prev, "out_bits", None)  # (bits of left, bits of right) or None
         prev.out_folded = True
     else:
         ctx.wgk_prev = prev
@@ -288,13 +298,15 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
         dw_rel_r2l = wg(t_l, right)
 
     in_scale = getattr(ctx, "in_scale", None) if bf16 else None
+    in_bits = getattr(ctx, "in_bits", None) if bf16 else None
+    ctx.in_bits = None
     # fp32: conv1 produced (left, right) and feeds only this layer -- its weight gradients come out of
     # this layer's input-gradient GEMMs (prev = conv1's node; its saved inputs, aggregates and outputs)
     prev = getattr(ctx, "wgk_prev", None)
     ctx.wgk_prev = None
     p_saved = prev.saved_tensors if prev is not None and (need[0] or need[1]) else None
 
-    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in, conv1=None):
+    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in, conv1=None, bits=None):
         """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients);
         with a folded previous layer, through its ReLU/dropout backward (x_in = its output).  conv1 =
         (Y, X1, X2) of the conv1 direction whose output x_in is: returns that direction's weight
@@ -310,7 +322,7 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
                 return r
             g = src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in)  # the two-pass route
             return _fc.relu_wgrad_smallk(g, y, 1.0, x1, x2, True)
-        kw = {} if in_scale is None else {"mask": (x_in, in_scale)}
+        kw = {} if in_scale is None else {"mask": (x_in if bits is None else bits, in_scale)}
         if t_src:  # both terms over the same rows: one two-part GEMM
             return ig(T, w_rel, dz_root, w_root, **kw)
         return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True, **kw)
@@ -330,9 +342,11 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
         g_l = torch.zeros((), dtype=left.dtype, device=left.device).expand(left.shape)
     else:
         if need[1]:  # right = src of right2left (S = A), dst of left2right
-            g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r, right)
+            g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r, right,
+                                bits=None if in_bits is None else in_bits[1])
         if need[0]:  # left = src of left2right (S = A^T), dst of right2left
-            g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l, left)
+            g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l, left,
+                                bits=None if in_bits is None else in_bits[0])
     return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 

@@ -319,7 +319,7 @@ def _prep_bf16(t: Tensor | None, dt=torch.bfloat16) -> Tensor | None:
 def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                     relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
                     accumulate: bool = False, key: str | None = None, mask=None, kernel: int = 0,
-                    row_offset: int = 0, row_keys: Tensor | None = None) -> Tensor:
+                    row_offset: int = 0, row_keys: Tensor | None = None, mask_out: Tensor | None = None) -> Tensor:
     """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16); with fp16
     operands (the --fp16 inference mode, val.py:269) the same kernels on the fp16 MFMA (lpg_fc_f16);
     ``accumulate`` adds the bf16 addend held in ``out`` (overwritten).
@@ -328,7 +328,9 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
     ReLU / dropout of its own) -- the bits of this call without ``mask`` followed by
     relu_bwd_colsum_bf16(C, Y, scale).  ``kernel``: the per-call kernel choice (LPG_FC_KERNEL,
     include/lpgnn.h; 0 = by shape, 1 = 128 x 128, 2 = 256 x 256, 3 = pipelined; the same bits).
-    ``row_offset`` / ``row_keys``: the dropout row keys, as fc_forward."""
+    ``row_offset`` / ``row_keys``: the dropout row keys, as fc_forward.  ``mask_out`` (uint8 [M, N / 8],
+    bf16 ReLU calls): filled with the output's 1-bit ReLU mask (bit e of byte t of row m: C[m, 8 t + e] > 0,
+    lpg_fc_bf16_mask), which a later ``mask`` = (bits, scale) takes in place of Y (1/16 of its bytes)."""
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -363,6 +365,25 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0) | _lib.fc_kernel(kernel)
+    if mask is not None and mask[0].dtype == torch.uint8:  # the previous layer's ReLU as bits
+        bits, scale = mask
+        if relu or bias is not None or dropout_p > 0:
+            raise RuntimeError("lpgnn bf16 FC: the folded ReLU backward takes no bias / ReLU / dropout")
+        if (bits.shape != (M, N // 8) or bits.device != A1.device or bits.stride(1) != 1 or N % 8
+                or C.stride(0) % 8 or C.data_ptr() % 16):  # the same bits through the Y form
+            y = ((bits[:, :, None] >> torch.arange(8, device=bits.device, dtype=torch.uint8)) & 1).reshape(M, -1)
+            return fc_forward_bf16(A1, W1, A2, W2, None, False, out=out, accumulate=accumulate, key=key,
+                                   mask=(y[:, :N].to(torch.bfloat16), scale), kernel=kernel)
+        with torch.cuda.device(A1.device):
+            tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, key or "lin-bf16-relubwd"))
+            st = L.lpg_fc_bf16_relu_bwd_bits(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(),
+                                             W1.stride(0), K2, None if A2 is None else A2.data_ptr(),
+                                             A2.stride(0) if K2 else 0, None if W2 is None else W2.data_ptr(),
+                                             W2.stride(0) if K2 else 0, C.data_ptr(), C.stride(0), flags,
+                                             bits.data_ptr(), bits.stride(0), float(scale), _lib.stream_of(A1))
+            TIMER.stop(tok)
+        _lib.check(st, "lpg_fc_bf16_relu_bwd_bits")
+        return C
     if mask is not None:
         Y, scale = mask
         if relu or bias is not None or dropout_p > 0:
@@ -383,6 +404,14 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
         _lib.check(st, "lpg_fc_bf16_relu_bwd")
         return C
     entry = "lpg_fc_f16" if f16 else "lpg_fc_bf16"
+    margs = ()
+    if mask_out is not None:
+        if (f16 or not relu or N % 8 or C.stride(0) % 8 or C.data_ptr() % 16 or mask_out.dtype != torch.uint8
+                or mask_out.shape != (M, N // 8) or mask_out.stride(1) != 1 or mask_out.device != A1.device):
+            raise RuntimeError("lpgnn bf16 FC: mask_out needs a bf16 ReLU call, N and ldc multiples of 8, an aligned "
+                               "C and a uint8 [M, N / 8] row-major mask on the same device")
+        entry = "lpg_fc_bf16_mask"
+        margs = (mask_out.data_ptr(), mask_out.stride(0))
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2,
                            key or (("relu-" if relu else "lin-") + ("f16" if f16 else "bf16"))))
@@ -391,7 +420,7 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
                            None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
                            None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags,
                            float(dropout_p), int(seed) & (2**64 - 1), int(row_offset), _lib.ptr(row_keys),
-                           _lib.stream_of(A1))
+                           *margs, _lib.stream_of(A1))
         TIMER.stop(tok)
     _lib.check(st, entry)
     return C

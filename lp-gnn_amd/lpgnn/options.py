@@ -14,6 +14,8 @@ import, so a whole run can be switched from the shell:
   LPGNN_FOLD_CONV1_WGRAD=0   fp32: conv1's weight gradient as its own pass (not in the next layer's
                              input-gradient GEMM)
   LPGNN_OVERLAP=1            independent SpMMs on a second stream beside the FC
+  LPGNN_RELU_BITS=0          bf16: the folded ReLU backward re-reads the layer output instead of the
+                             1-bit mask its forward wrote beside it
 """
 from __future__ import annotations
 
@@ -34,6 +36,7 @@ class PathOptions:
     fold_relu_bwd: bool = True
     fold_conv1_wgrad: bool = True
     overlap: bool = False
+    relu_bits: bool = False
 
     def __post_init__(self):
         if self.arith not in ("x3", "fp32"):
@@ -47,7 +50,8 @@ class PathOptions:
                    fuse_head_fwd=_env("LPGNN_FUSE_HEAD_FWD", "1") == "1",
                    fold_relu_bwd=_env("LPGNN_FOLD_RELU_BWD", "1") == "1",
                    fold_conv1_wgrad=_env("LPGNN_FOLD_CONV1_WGRAD", "1") == "1",
-                   overlap=_env("LPGNN_OVERLAP", "0") == "1")
+                   overlap=_env("LPGNN_OVERLAP", "0") == "1",
+                   relu_bits=_env("LPGNN_RELU_BITS", "0") == "1")
 
     def replace(self, **kw) -> "PathOptions":
         return dataclasses.replace(self, **kw)

@@ -437,3 +437,84 @@ def test_colsum_bf16_bitwise_masked_pass(M, N):
     out, db = relu_bwd_colsum_bf16(g, y, 1.0, True)
     assert torch.equal(out, g)
     assert torch.equal(colsum_bf16(g), db)
+
+
+def _packbits(y):
+    """uint8 [M, N / 8]: bit e of byte t of row m = (y[m, 8 t + e] > 0) -- the lpg_fc_bf16_mask layout."""
+    pos = (y.float() > 0).to(torch.uint8).reshape(y.shape[0], -1, 8)
+    w = (2 ** torch.arange(8, device=y.device, dtype=torch.int32)).to(torch.uint8)
+    return (pos * w).sum(-1, dtype=torch.int32).to(torch.uint8)
+
+
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("M,N,K1,K2,acc,p", [
+    (5000, 512, 128, 128, False, 0.2),   # two k phases, dropout
+    (700, 256, 64, 0, True, 0.0),        # small M (128 x 128 kernel), accumulate
+    (3000, 256, 8, 8, False, 0.1),       # conv1: the narrow-input kernel (nibbles paired across lanes)
+    (61000, 256, 64, 0, True, 0.1),      # a partial last round (the tail launch of choice 0)
+])
+def test_fc_bf16_mask_out_is_the_relu_mask(kernel, M, N, K1, K2, acc, p):
+    """lpg_fc_bf16_mask: C bit for bit lpg_fc_bf16's, and the mask is exactly (C > 0) packed 8 per byte."""
+    from lpgnn.fc import fc_forward_bf16
+
+    g = torch.Generator(device=DEV).manual_seed(M + N + kernel)
+    r = lambda *s: (torch.randn(*s, device=DEV, generator=g) * 0.2).to(BF)  # noqa: E731
+    A1, W1 = r(M, K1), r(N, K1)
+    A2, W2 = (r(M, K2), r(N, K2)) if K2 else (None, None)
+    b = torch.randn(N, device=DEV, generator=g) * 0.1
+    P = r(M, N) if acc else None
+    ref = fc_forward_bf16(A1, W1, A2, W2, b, True, p, 11, out=None if P is None else P.clone(), accumulate=acc,
+                          kernel=kernel)
+    bits = torch.full((M, N // 8), 0xA5, dtype=torch.uint8, device=DEV)
+    got = fc_forward_bf16(A1, W1, A2, W2, b, True, p, 11, out=None if P is None else P.clone(), accumulate=acc,
+                          kernel=kernel, mask_out=bits)
+    assert torch.equal(got, ref)
+    assert torch.equal(bits, _packbits(ref))
+
+
+@pytest.mark.parametrize("two,acc", [(True, False), (False, True)])
+def test_relu_bwd_bits_equal_relu_bwd_from_y(two, acc):
+    """lpg_fc_bf16_relu_bwd_bits: the folded ReLU backward from the 1-bit mask gives the bits of the
+    Y form (same product, same rounding per pair)."""
+    from lpgnn.fc import input_grad_bf16
+
+    M, N, K = 6000, 1024, 512
+    g = torch.Generator(device=DEV).manual_seed(3)
+    r = lambda *s: (torch.randn(*s, device=DEV, generator=g) * 0.2).to(BF)  # noqa: E731
+    G1, W1 = r(M, K), r(K, N)
+    G2, W2 = (r(M, K), r(K, N)) if two else (None, None)
+    Y = torch.relu(r(M, N))
+    Y[::7, ::5] = 0
+    P = r(M, N) if acc else None
+    want = input_grad_bf16(G1, W1, G2, W2, out=None if P is None else P.clone(), accumulate=acc, mask=(Y, 1.25))
+    got = input_grad_bf16(G1, W1, G2, W2, out=None if P is None else P.clone(), accumulate=acc,
+                          mask=(_packbits(Y), 1.25))
+    assert torch.equal(got, want)
+
+
+def test_gcn_fc_bf16_relu_bits_identical():
+    """options.relu_bits: every bf16 ReLU layer writes its 1-bit mask and the next layer's folded ReLU
+    backward reads it instead of the layer output -- the same loss and the same gradient bits."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.train import balanced
+
+    g = synth.uniform_lp(1500, 5200, 30000, seed=5)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    batch = BipartiteBatch(x_s=torch.from_numpy(g.x_s).to(DEV), x_t=torch.from_numpy(g.x_t).to(DEV),
+                           y_s=torch.from_numpy(g.y_s).to(DEV), y_t=torch.from_numpy(g.y_t).to(DEV),
+                           edge_index=adj, s_bs=g.m, t_bs=g.n)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=256, depth=5, dp=0.1, compute_dtype="bf16").to(DEV).train()
+    base = model.options
+    out = {}
+    for bits in (True, False):
+        model.options = base.replace(relu_bits=bits)
+        model.zero_grad()
+        torch.manual_seed(321)
+        lc, lv = model(batch)
+        loss = balanced(lc, lv, batch.y_s, batch.y_t)
+        loss.backward()
+        out[bits] = (loss.item(), {k: p.grad.clone() for k, p in model.named_parameters()})
+    assert out[True][0] == out[False][0]
+    for k, v in out[True][1].items():
+        assert torch.equal(v, out[False][1][k]), k
