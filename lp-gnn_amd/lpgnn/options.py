@@ -36,7 +36,7 @@ class PathOptions:
     fold_relu_bwd: bool = True
     fold_conv1_wgrad: bool = True
     overlap: bool = False
-    relu_bits: bool = False
+    relu_bits: bool = True
 
     def __post_init__(self):
         if self.arith not in ("x3", "fp32"):
@@ -51,7 +51,7 @@ class PathOptions:
                    fold_relu_bwd=_env("LPGNN_FOLD_RELU_BWD", "1") == "1",
                    fold_conv1_wgrad=_env("LPGNN_FOLD_CONV1_WGRAD", "1") == "1",
                    overlap=_env("LPGNN_OVERLAP", "0") == "1",
-                   relu_bits=_env("LPGNN_RELU_BITS", "0") == "1")
+                   relu_bits=_env("LPGNN_RELU_BITS", "1") == "1")
 
     def replace(self, **kw) -> "PathOptions":
         return dataclasses.replace(self, **kw)
