@@ -142,6 +142,30 @@ __device__ __forceinline__ uint32_t relu_bwd_pk_bits(uint32_t g, uint32_t b2, fl
   const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(gf * lpg_f32x2{scale, scale}, lpg_bf16x2));
   return ((b2 & 1u) ? (pk & 0xffffu) : 0u) | ((b2 & 2u) ? (pk & 0xffff0000u) : 0u);
 }
+// The ReLU mask bytes of one row's 8 consecutive 16-B chunks, one byte per lane on 8 consecutive lanes
+// (lane % 8 = the chunk: every store loop here has 8 chunks per row), gathered into the group's first
+// lane by three DPP steps (pair swap, quad swap, half-row mirror) and stored as one 8-byte word; a group
+// that crosses N (or an unaligned mask row) stores byte by byte.  Every lane of the wave must call it.
+template <class A>
+__device__ __forceinline__ void store_mask8(const A &a, int lane, uint32_t b, bool ok, int64_t row, int64_t col) {
+  const int sh = 8 * (lane & 3);
+  uint32_t lo = ok && !(lane & 4) ? (b << sh) : 0u, hi = ok && (lane & 4) ? (b << sh) : 0u;
+  lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+  hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false);
+  lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+  hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x4E, 0xF, 0xF, false);
+  lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x141, 0xF, 0xF, false);
+  const int64_t col0 = col - (int64_t)(lane & 7) * 8;
+  uint8_t *const p0 = a.mo + row * a.ldmo + col0 / 8;
+  const bool whole = row < a.M && col0 + 64 <= a.N && (reinterpret_cast<uintptr_t>(p0) & 7) == 0;
+  if (whole) {
+    if ((lane & 7) == 0) *reinterpret_cast<uint2 *>(p0) = make_uint2(lo, hi);
+  } else if (ok) {
+    a.mo[row * a.ldmo + col / 8] = (uint8_t)b;
+  }
+}
+
 __device__ __forceinline__ uint4 relu_bwd8_bits(uint4 g, uint32_t b, float scale) {
   return make_uint4(relu_bwd_pk_bits(g.x, b, scale), relu_bwd_pk_bits(g.y, b >> 2, scale),
                     relu_bwd_pk_bits(g.z, b >> 4, scale), relu_bwd_pk_bits(g.w, b >> 6, scale));
@@ -181,6 +205,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
     // global_store_dwordx4 per 8 outputs instead of one 2-byte store each.
     unsigned char *img = smem + wave * (FM * 16 * EP_PITCH);
     constexpr int CPR = FN * 16 / 8;  // 16-B chunks per row
+    static_assert(CPR == 8, "store_mask8: a row's 8 chunks on 8 consecutive lanes");
     if (a.accum) {  // the addend tile, coalesced 16-B loads into the same image
 #pragma unroll
       for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
@@ -254,14 +279,15 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
       const int lr = q / CPR, ch = q % CPR;
       const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
       uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
-      if (row < a.M && col < a.N) {
+      const bool ok = row < a.M && col < a.N;
+      if (ok) {
         if constexpr (E::kBf16) {  // (the folded ReLU backward: bf16 training only)
           if (a.mi) v = relu_bwd8_bits(v, yv[it].x, a.mscale);
           else if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
-          if (a.mo) a.mo[row * a.ldmo + col / 8] = (uint8_t)pos_bits8(v);
         }
         *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
       }
+      if (E::kBf16 && a.mo) store_mask8(a, lane, pos_bits8(v), ok, row, col);  // the layer's ReLU mask
     }
     return;
   }
@@ -398,6 +424,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
   }
   unsigned char *img = smem + wave * (FM * 16 * EP_PITCH);
   constexpr int CPR = FN * 16 / 8;  // 16-B chunks per row
+  static_assert(CPR == 8, "store_mask8: a row's 8 chunks on 8 consecutive lanes");
   if (a.accum) {  // the addend tile, coalesced 16-B loads into the image
 #pragma unroll
     for (int it = 0; it < FM * 16 * CPR / 64; ++it) {
@@ -507,10 +534,9 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
     const int lr = q / CPR, ch = q % CPR;
     const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
     const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
-    if (row < a.M && col < a.N) {
-      *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
-      if (E::kBf16 && a.mo) a.mo[row * a.ldmo + col / 8] = (uint8_t)pos_bits8(v);  // the layer's ReLU mask
-    }
+    const bool ok = row < a.M && col < a.N;
+    if (ok) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+    if (E::kBf16 && a.mo) store_mask8(a, lane, pos_bits8(v), ok, row, col);  // the layer's ReLU mask
   }
 }
 

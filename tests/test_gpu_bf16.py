@@ -452,6 +452,7 @@ def _packbits(y):
     (700, 256, 64, 0, True, 0.0),        # small M (128 x 128 kernel), accumulate
     (3000, 256, 8, 8, False, 0.1),       # conv1: the narrow-input kernel (nibbles paired across lanes)
     (19384, 2048, 64, 0, True, 0.1),     # two full rounds + 3000 rows (the tail launch of choice 0)
+    (3000, 200, 64, 0, False, 0.1),      # N % 64 != 0: 25 mask bytes a row (byte stores at the edge, unaligned rows)
 ])
 def test_fc_bf16_mask_out_is_the_relu_mask(kernel, M, N, K1, K2, acc, p):
     """lpg_fc_bf16_mask: C bit for bit lpg_fc_bf16's, and the mask is exactly (C > 0) packed 8 per byte."""
