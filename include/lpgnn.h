@@ -391,6 +391,22 @@ lpg_status lpg_fc_bf16_relu_bwd_bits(int64_t M, int64_t N, int64_t K1, const uin
                                      const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc, int32_t flags,
                                      const uint8_t *mask, int64_t ldm, float scale, void *stream);
 
+/* lpg_fc_bf16_relu_bwd / lpg_fc_bf16_relu_bwd_bits that also return the bias gradient of the layer
+ * whose ReLU they fold, db[n] = sum_m C[m, n] (fp32): bitwise lpg_colsum_bf16 on the stored C (its
+ * 64-row chunks, in-chunk order and fold), the chunk sums taken in the pipelined kernel's store loop
+ * -- no second pass over C where that kernel runs (c5: the 819 MB re-read of a 200 K x 2048 dZ).
+ * workspace: lpg_relu_bwd_colsum_workspace_bytes(M, N), 16-byte aligned; M = 0 zeroes db. */
+lpg_status lpg_fc_bf16_relu_bwd_db(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                   const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2, int64_t lda2,
+                                   const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc, int32_t flags,
+                                   const uint16_t *Y, int64_t ldy, float scale, float *db, void *workspace,
+                                   void *stream);
+lpg_status lpg_fc_bf16_relu_bwd_bits_db(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                        const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
+                                        int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
+                                        int32_t flags, const uint8_t *mask, int64_t ldm, float scale, float *db,
+                                        void *workspace, void *stream);
+
 /* bf16 weight gradient (c5 backward, reference train.py:128 loss.backward()
  * through GraphConv's lin_rel / lin_root): dW[n, k] = sum_r G[r, n] X[r, k],
  * G = dZ [R, N] and X = the layer input [R, K] as bf16 bit patterns

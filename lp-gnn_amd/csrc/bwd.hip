@@ -826,6 +826,30 @@ lpg_status smallk_fold(int64_t nblk, int64_t N, int K1, int K, const float *part
   return LPG_OK;
 }
 
+// db of a bf16 dZ [M, N] whose partial image [ceil(M / 64)][N] (lpg_colsum_bf16's, in `part`, the
+// workspace of lpg_relu_bwd_colsum_workspace_bytes) a producer already filled for rows [0, r0) --
+// the folded ReLU backward of fc_bf16_p (fc_bf16.hip) -- rows [r0, M) summed here from g by
+// relu_bwd_colsum_bf16_p1 (r0 a multiple of the 64-row chunk), then lpg_colsum_bf16's fold: db is
+// bitwise what lpg_colsum_bf16 returns for the same dZ.
+lpg_status colsum_bf16_from(int64_t M, int64_t N, const uint16_t *g, int64_t ldg, int64_t r0, float *part, float *db,
+                            hipStream_t s) {
+  LPG_REQUIRE(r0 >= 0 && r0 <= M && (r0 % kRowsColsum == 0 || r0 == M), "colsum_bf16_from: bad r0 %lld",
+              (long long)r0);
+  const int64_t nblk = (M + kRowsColsum - 1) / kRowsColsum;
+  if (r0 < M) {
+    const int64_t b0 = r0 / kRowsColsum;
+    hipLaunchKernelGGL(relu_bwd_colsum_bf16_p1<false>, dim3((unsigned)(nblk - b0)), dim3(kT), 0, s, M - r0, N,
+                       g + r0 * ldg, ldg, (const uint16_t *)nullptr, (int64_t)0, 1.f, (uint16_t *)nullptr, (int64_t)0,
+                       part + b0 * N);
+    LPG_HIP(hipGetLastError());
+  }
+  const float *img;
+  const int64_t nrow = fold(nblk, N, part, part + nblk * N, &img, s);
+  hipLaunchKernelGGL(sum_partials, dim3((unsigned)((N + kT - 1) / kT)), dim3(kT), 0, s, nrow, N, img, db);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
 namespace {
 int64_t heads_bwd_floats(int64_t M, int64_t K, int64_t N) {
   const int64_t nblk = (M + kRowsLinear - 1) / kRowsLinear, nchunk = (M + kRowsColsum - 1) / kRowsColsum;

@@ -67,6 +67,9 @@ struct FcB16Args {
   int64_t ldmo;
   const uint8_t *mi;
   int64_t ldmi;
+  // the folded ReLU backward's bias column sums (lpg_fc_bf16_relu_bwd*_db; fc_bf16_p only): the stored
+  // dZ's sums per 64-row chunk of the launch's rows into lpg_colsum_bf16's partial image [ceil(M / 64)][N]
+  float *cs;
 };
 
 
@@ -409,6 +412,35 @@ __device__ __forceinline__ void epilogue_bf16_t(const FcB16Args &a, f32x4 (&acc)
   }
 }
 
+// ... then summed down the wave's two 64-row chunks: lanes 0-31 take chunk 0, 32-63 chunk 1, a
+// column pair each, rows in order from 0.f -- relu_bwd_colsum_bf16_p1's blocks, order and fp32 sums
+// (bwd.hip), so lpg_colsum_bf16's fold of the image gives its bits.  Rows past M hold +0 (their mask
+// is 0) and are not read.
+template <int FM, int FN>
+__device__ __forceinline__ void colsum_chunks(const FcB16Args &a, const unsigned char *img, int lane, int64_t wrow0,
+                                              int64_t wcol0) {
+  constexpr int EP_PITCH = FN * 16 * 2 + 16;
+  static_assert(FM * 16 == 128 && FN * 16 == 64, "two 64-row chunks of 32 column pairs per wave");
+  const int h = lane >> 5, cp = lane & 31;
+  const int64_t r0 = wrow0 + 64 * h, col = wcol0 + 2 * cp;
+  if (r0 >= a.M || col >= a.N) return;
+  const int64_t nr = a.M - r0 < 64 ? a.M - r0 : 64;
+  const unsigned char *ip = img + 64 * h * EP_PITCH + cp * 4;
+  float s0 = 0.f, s1 = 0.f;
+  auto add = [&](int r) {
+    const uint32_t w = *reinterpret_cast<const uint32_t *>(ip + r * EP_PITCH);
+    s0 = s0 + __uint_as_float(w << 16);
+    s1 = s1 + __uint_as_float(w & 0xffff0000u);
+  };
+  if (nr == 64) {
+#pragma unroll 16
+    for (int r = 0; r < 64; ++r) add(r);
+  } else {
+    for (int r = 0; r < (int)nr; ++r) add(r);
+  }
+  *reinterpret_cast<float2 *>(a.cs + (r0 / 64) * a.N + col) = make_float2(s0, s1);
+}
+
 // Transposed fragments through the LDS image (fc_bf16_p with TRO = 2): the lane's four
 // consecutive columns go to the image as one ds_write_b64 (ds_read_b64 for the addend) instead
 // of four 2-byte accesses, then the rows leave as 16-byte stores as in epilogue_bf16.  Image
@@ -525,6 +557,16 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
       const int lr = q / CPR, ch = q % CPR;
       const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
       if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v[it];
+    }
+    if (a.cs) {  // the bias column sums of the stored dZ: each lane's own image chunks overwritten by dZ, ...
+#pragma unroll
+      for (int it = 0; it < SIT; ++it) {
+        const int q = it * 64 + lane;
+        *reinterpret_cast<uint4 *>(img + (q / CPR) * EP_PITCH + (q % CPR) * 16) = v[it];
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      colsum_chunks<FM, FN>(a, img, lane, wrow0, wcol0);
     }
     return;
   }
@@ -1150,7 +1192,7 @@ int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
 namespace lpg {
 namespace {
 template <class E>
-lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant);
+lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant, int64_t *cs_rows = nullptr);
 
 // dst[c, r] = src[r, c] for bf16 through a 64 x 64 LDS tile, 16-byte global accesses both ways
 // (the input gradients' W^T; torch's strided copy ran these at ~0.5 TB/s).  R, C multiples of 8.
@@ -1421,8 +1463,12 @@ static lpg_status relu_bwd_entry(const char *name, int64_t M, int64_t N, int64_t
                                  int64_t lda1, const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
                                  int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
                                  int32_t flags, const uint16_t *Y, int64_t ldy, const uint8_t *mask, int64_t ldm,
-                                 float scale, void *stream) {
+                                 float scale, void *stream, float *db = nullptr, void *workspace = nullptr) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "%s: negative size", name);
+  if (db) {
+    LPG_REQUIRE(workspace && aligned16(workspace), "%s: db needs a 16-byte aligned workspace", name);
+    if (M == 0 && N > 0) LPG_HIP(hipMemsetAsync(db, 0, sizeof(float) * N, as_stream(stream)));
+  }
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(C != nullptr && ldc >= N && (Y ? ldy >= N : (mask != nullptr && ldm >= N / 8)),
               "%s: bad C/ldc or Y/ldy (mask/ldm)", name);
@@ -1443,7 +1489,12 @@ static lpg_status relu_bwd_entry(const char *name, int64_t M, int64_t N, int64_t
     a.mi = mask;
     a.ldmi = ldm;
   }
-  return fc_bf16_dispatch<EBf16>(a, false, as_stream(stream), kernel);  // (every kernel's epilogue takes the fold)
+  hipStream_t s = as_stream(stream);
+  a.cs = db ? static_cast<float *>(workspace) : nullptr;
+  int64_t cs_rows = 0;
+  const lpg_status st = fc_bf16_dispatch<EBf16>(a, false, s, kernel, &cs_rows);  // (every kernel's epilogue takes the fold)
+  if (st != LPG_OK || !db) return st;
+  return colsum_bf16_from(M, N, C, ldc, cs_rows, static_cast<float *>(workspace), db, s);
 }
 
 extern "C" lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
@@ -1467,6 +1518,30 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd_bits(int64_t M, int64_t N, int64_t K1
                         flags, nullptr, 0, mask, ldm, scale, stream);
 }
 
+// ... and the bias column sums of the stored dZ, db [N] fp32 (the bits of lpg_colsum_bf16 on C): from the
+// store loop's registers where the pipelined kernel runs (no second read of C), else by the colsum pass.
+// workspace: lpg_relu_bwd_colsum_workspace_bytes(M, N)
+extern "C" lpg_status lpg_fc_bf16_relu_bwd_db(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
+                                              const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
+                                              int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
+                                              int32_t flags, const uint16_t *Y, int64_t ldy, float scale, float *db,
+                                              void *workspace, void *stream) {
+  LPG_REQUIRE(Y != nullptr && db != nullptr, "lpg_fc_bf16_relu_bwd_db: NULL Y or db");
+  return relu_bwd_entry("lpg_fc_bf16_relu_bwd_db", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, C, ldc,
+                        flags, Y, ldy, nullptr, 0, scale, stream, db, workspace);
+}
+
+extern "C" lpg_status lpg_fc_bf16_relu_bwd_bits_db(int64_t M, int64_t N, int64_t K1, const uint16_t *A1,
+                                                   int64_t lda1, const uint16_t *W1, int64_t ldw1, int64_t K2,
+                                                   const uint16_t *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
+                                                   uint16_t *C, int64_t ldc, int32_t flags, const uint8_t *mask,
+                                                   int64_t ldm, float scale, float *db, void *workspace,
+                                                   void *stream) {
+  LPG_REQUIRE(mask != nullptr && db != nullptr, "lpg_fc_bf16_relu_bwd_bits_db: NULL mask or db");
+  return relu_bwd_entry("lpg_fc_bf16_relu_bwd_bits_db", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, C, ldc,
+                        flags, nullptr, 0, mask, ldm, scale, stream, db, workspace);
+}
+
 namespace lpg {
 namespace {
 // rows [r, M) of a as their own call: operands, output, mask rows and dropout keys offset by r
@@ -1481,11 +1556,17 @@ FcB16Args rows_from(const FcB16Args &a, int64_t r) {
   t.mi = a.mi ? a.mi + r * a.ldmi : nullptr;
   t.row_off = a.row_off + r;
   t.row_keys = a.row_keys ? a.row_keys + r : nullptr;
+  t.cs = nullptr;
   return t;
 }
 
 template <class E>
-lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
+// cs_rows: the leading rows whose column-sum partials the launches wrote (a.cs: fc_bf16_p's epilogue
+// only; the other kernels never see a.cs)
+lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel, int64_t *cs_rows) {
+  if (cs_rows) *cs_rows = 0;
+  float *const cs = a.cs;
+  a.cs = nullptr;
   if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<E, 2, 2, 4, 4>(a, relu, s);  // 128 x 128
   if ((kernel == 0 || kernel >= 3) && p_ok(a)) {
     a.order = kernel == 0 ? 1 : kernel == 5 ? 2 : 0;  // the default in the n-split order (1-2 % at the c5 shapes)
@@ -1501,12 +1582,16 @@ lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel) {
         if (full > 0 && tail > 0 && 2 * tail <= per_round) {
           FcB16Args h = a;
           h.M = full;
+          h.cs = cs;
           const lpg_status st = launch_bf16_p<E, 2, 4, 8, 4>(h, relu, s);
           if (st != LPG_OK) return st;
+          if (cs_rows && cs) *cs_rows = full;
           return launch_bf16<E, 2, 2, 4, 4>(rows_from(a, full), relu, s);
         }
       }
     }
+    a.cs = cs;
+    if (cs_rows && cs) *cs_rows = a.M;
     return launch_bf16_p<E, 2, 4, 8, 4>(a, relu, s);
   }
   return launch_bf16<E, 2, 4, 8, 4>(a, relu, s);  // 256 x 256, BK 64, 2 buffers

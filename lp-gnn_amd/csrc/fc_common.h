@@ -87,6 +87,12 @@ int64_t smallk_fold_floats(int64_t nblk, int64_t KR, int64_t N);
 lpg_status smallk_fold(int64_t nblk, int64_t N, int K1, int K, const float *part, float *seg, float *dW1, float *dW2,
                        float *db, hipStream_t s);
 
+// bwd.hip: db [N] of a bf16 dZ [M, N] from lpg_colsum_bf16's partial image `part` (its workspace), the
+// chunks of rows [0, r0) already written by a producer (fc_bf16_p's folded ReLU backward), the rest
+// summed from g; the bits of lpg_colsum_bf16
+lpg_status colsum_bf16_from(int64_t M, int64_t N, const uint16_t *g, int64_t ldg, int64_t r0, float *part, float *db,
+                            hipStream_t s);
+
 // Host-side dropout threshold / scale shared by the FC entry points.
 inline void dropout_params(float p, uint32_t *thresh, float *scale) {
   *thresh = 0u;

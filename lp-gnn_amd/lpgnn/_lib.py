@@ -39,6 +39,8 @@ HEADER_SYMBOLS = (
     "lpg_fc_bf16_relu_bwd",
     "lpg_fc_bf16_mask",
     "lpg_fc_bf16_relu_bwd_bits",
+    "lpg_fc_bf16_relu_bwd_db",
+    "lpg_fc_bf16_relu_bwd_bits_db",
     "lpg_colsum_bf16",
     "lpg_transpose_bf16",
     "lpg_wgrad_bf16_workspace_bytes",
@@ -147,6 +149,10 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_bf16_mask.restype = c_i32
     L.lpg_fc_bf16_relu_bwd_bits.argtypes = L.lpg_fc_bf16_relu_bwd.argtypes
     L.lpg_fc_bf16_relu_bwd_bits.restype = c_i32
+    L.lpg_fc_bf16_relu_bwd_db.argtypes = L.lpg_fc_bf16_relu_bwd.argtypes[:-1] + [c_p, c_p, c_p]
+    L.lpg_fc_bf16_relu_bwd_db.restype = c_i32
+    L.lpg_fc_bf16_relu_bwd_bits_db.argtypes = L.lpg_fc_bf16_relu_bwd_db.argtypes
+    L.lpg_fc_bf16_relu_bwd_bits_db.restype = c_i32
     L.lpg_colsum_bf16.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p]
     L.lpg_colsum_bf16.restype = c_i32
     L.lpg_class_counts_workspace_bytes.argtypes = [c_i64]

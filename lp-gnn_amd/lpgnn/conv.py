@@ -145,8 +145,9 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
     # conv1's shape (narrow LP-feature inputs, kept aggregates, ReLU without dropout, fp32): its weight
     # gradients can be folded into the next layer's input-gradient GEMM (lpg_fc_x3_relu_wgrad_f32)
-    ctx.small_relu = (not bf16 and relu and dropout == 0 and agg_l is not None and agg_r is not None
-                      and agg_l.shape[1] + left.shape[1] <= 16 and agg_r.shape[1] + right.shape[1] <= 16)
+    ctx.narrow = (agg_l is not None and agg_r is not None and agg_l.shape[1] + left.shape[1] <= 16
+                  and agg_r.shape[1] + right.shape[1] <= 16)
+    ctx.small_relu = not bf16 and relu and dropout == 0 and ctx.narrow
     logits = None if heads is None or bf16 else (logit_l, logit_r)
     return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, *ws), logits
 
@@ -174,13 +175,16 @@ class _TwoDirection(torch.autograd.Function):
 
 
 def _link_prev(ctx, prev):
-    ctx.in_scale, ctx.wgk_prev, ctx.in_bits = None, None, None
+    ctx.in_scale, ctx.wgk_prev, ctx.in_bits, ctx.db_prev = None, None, None, None
     if prev is None:
         return
     if prev.bf16:
         ctx.in_scale = prev.scale
         ctx.in_bits = getattr(prev, "out_bits", None)  # (bits of left, bits of right) or None
         prev.out_folded = True
+        # a hidden layer (not conv1, whose backward sums dZ with its small-K weight gradients): its bias
+        # gradients come out of this layer's folded input-gradient stores (lpg_fc_bf16_relu_bwd*_db)
+        ctx.db_prev = None if getattr(prev, "narrow", True) else prev
     else:
         ctx.wgk_prev = prev
         prev.wgk_folded = True
@@ -211,7 +215,8 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
             g = g.to(dt).contiguous()
             if not want_db:
                 return g, None
-            # the bf16 heads' backward already summed these columns (fc.heads_bwd_bf16: the bits of colsum_bf16)
+            # the bf16 heads' backward (fc.heads_bwd_bf16) or the next layer's folded input-gradient store
+            # (lpg_fc_bf16_relu_bwd*_db) already summed these columns: the bits of colsum_bf16
             pre = (getattr(ctx, "folded_colsum", None) or {}).pop(y.data_ptr(), None)
             return g, (pre[1] if pre is not None and pre[0] is g else _fc.colsum_bf16(g))
         if not ctx.relu:
@@ -299,18 +304,20 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
 
     in_scale = getattr(ctx, "in_scale", None) if bf16 else None
     in_bits = getattr(ctx, "in_bits", None) if bf16 else None
-    ctx.in_bits = None
+    db_prev = getattr(ctx, "db_prev", None) if bf16 else None
+    ctx.in_bits = ctx.db_prev = None
     # fp32: conv1 produced (left, right) and feeds only this layer -- its weight gradients come out of
     # this layer's input-gradient GEMMs (prev = conv1's node; its saved inputs, aggregates and outputs)
     prev = getattr(ctx, "wgk_prev", None)
     ctx.wgk_prev = None
     p_saved = prev.saved_tensors if prev is not None and (need[0] or need[1]) else None
 
-    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in, conv1=None, bits=None):
+    def src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in, conv1=None, bits=None, has_b=False):
         """S^T (dZ W_rel) in the cheaper association + dZ_root W_root (the input's two gradients);
-        with a folded previous layer, through its ReLU/dropout backward (x_in = its output).  conv1 =
-        (Y, X1, X2) of the conv1 direction whose output x_in is: returns that direction's weight
-        gradients (dW_rel, dW_root, db) instead, the gradient itself never stored."""
+        with a folded previous layer, through its ReLU/dropout backward (x_in = its output) -- and,
+        has_b, that layer's bias gradient from the same stores, handed to its node (folded_colsum).
+        conv1 = (Y, X1, X2) of the conv1 direction whose output x_in is: returns that direction's
+        weight gradients (dW_rel, dW_root, db) instead, the gradient itself never stored."""
         if conv1 is not None:
             y, x1, x2 = conv1
             if t_src:
@@ -323,9 +330,18 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
             g = src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in)  # the two-pass route
             return _fc.relu_wgrad_smallk(g, y, 1.0, x1, x2, True)
         kw = {} if in_scale is None else {"mask": (x_in if bits is None else bits, in_scale)}
+        db = None
+        if kw and db_prev is not None and has_b:
+            db = kw["db_out"] = torch.empty(x_in.shape[1], dtype=torch.float32, device=x_in.device)
         if t_src:  # both terms over the same rows: one two-part GEMM
-            return ig(T, w_rel, dz_root, w_root, **kw)
-        return ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True, **kw)
+            g = ig(T, w_rel, dz_root, w_root, **kw)
+        else:
+            g = ig(dz_root, w_root, out=spmm_forward(St, ig(dz, w_rel)), accumulate=True, **kw)
+        if db is not None:  # keyed by the layer output's storage, checked by identity (`pre[0] is g`)
+            if getattr(db_prev, "folded_colsum", None) is None:
+                db_prev.folded_colsum = {}
+            db_prev.folded_colsum[x_in.data_ptr()] = (g, db)
+        return g
 
     g_l = g_r = None
     if p_saved is not None:
@@ -343,10 +359,12 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
     else:
         if need[1]:  # right = src of right2left (S = A), dst of left2right
             g_r = src_root_grad(AT, dz_l, w_rel_r2l, t_l, tsrc_l, dz_r, w_root_l2r, right,
-                                bits=None if in_bits is None else in_bits[1])
+                                bits=None if in_bits is None else in_bits[1],
+                                has_b=db_prev is not None and db_prev.has_b[0])
         if need[0]:  # left = src of left2right (S = A^T), dst of right2left
             g_l = src_root_grad(A, dz_r, w_rel_l2r, t_r, tsrc_r, dz_l, w_root_r2l, left,
-                                bits=None if in_bits is None else in_bits[0])
+                                bits=None if in_bits is None else in_bits[0],
+                                has_b=db_prev is not None and db_prev.has_b[1])
     return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 

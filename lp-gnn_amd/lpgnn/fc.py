@@ -319,7 +319,8 @@ def _prep_bf16(t: Tensor | None, dt=torch.bfloat16) -> Tensor | None:
 def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bias: Tensor | None,
                     relu: bool, dropout_p: float = 0.0, seed: int = 0, out: Tensor | None = None,
                     accumulate: bool = False, key: str | None = None, mask=None, kernel: int = 0,
-                    row_offset: int = 0, row_keys: Tensor | None = None, mask_out: Tensor | None = None) -> Tensor:
+                    row_offset: int = 0, row_keys: Tensor | None = None, mask_out: Tensor | None = None,
+                    db_out: Tensor | None = None) -> Tensor:
     """The c5 bf16 path: bf16 A/W, fp32 accumulate + fp32 bias, bf16 out (lpg_fc_bf16); with fp16
     operands (the --fp16 inference mode, val.py:269) the same kernels on the fp16 MFMA (lpg_fc_f16);
     ``accumulate`` adds the bf16 addend held in ``out`` (overwritten).
@@ -330,7 +331,10 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
     include/lpgnn.h; 0 = by shape, 1 = 128 x 128, 2 = 256 x 256, 3 = pipelined; the same bits).
     ``row_offset`` / ``row_keys``: the dropout row keys, as fc_forward.  ``mask_out`` (uint8 [M, N / 8],
     bf16 ReLU calls): filled with the output's 1-bit ReLU mask (bit e of byte t of row m: C[m, 8 t + e] > 0,
-    lpg_fc_bf16_mask), which a later ``mask`` = (bits, scale) takes in place of Y (1/16 of its bytes)."""
+    lpg_fc_bf16_mask), which a later ``mask`` = (bits, scale) takes in place of Y (1/16 of its bytes).
+    ``db_out`` (fp32 [N], with ``mask``): filled with the column sums of the returned dZ, the bias
+    gradient of the layer whose ReLU is folded -- bitwise colsum_bf16(dZ), taken in the FC's store loop
+    (lpg_fc_bf16_relu_bwd*_db) instead of a second pass over dZ."""
     if A1.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
     M, N = A1.shape[0], W1.shape[0]
@@ -341,6 +345,9 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
     f16 = dt == torch.float16
     if f16 and mask is not None:
         raise RuntimeError("lpgnn fp16 FC: the folded ReLU backward is a bf16 training path")
+    if db_out is not None and (mask is None or db_out.dtype != torch.float32 or db_out.shape != (N,)
+                               or not db_out.is_contiguous() or db_out.device != A1.device):
+        raise RuntimeError("lpgnn bf16 FC: db_out needs `mask` and an fp32 [N] contiguous tensor on the same device")
     k1, k2 = A1.shape[1], (0 if A2 is None else A2.shape[1])
     # conv1 (narrow LP features): the streaming small-K kernel takes the operands unpadded
     small = (mask is None and 4 <= k1 and k1 + k2 <= 16 and k1 % 4 == 0 and k2 % 4 == 0 and N % 4 == 0
@@ -373,16 +380,18 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
                 or C.stride(0) % 8 or C.data_ptr() % 16):  # the same bits through the Y form
             y = ((bits[:, :, None] >> torch.arange(8, device=bits.device, dtype=torch.uint8)) & 1).reshape(M, -1)
             return fc_forward_bf16(A1, W1, A2, W2, None, False, out=out, accumulate=accumulate, key=key,
-                                   mask=(y[:, :N].to(torch.bfloat16), scale), kernel=kernel)
+                                   mask=(y[:, :N].to(torch.bfloat16), scale), kernel=kernel, db_out=db_out)
+        entry = "lpg_fc_bf16_relu_bwd_bits" + ("_db" if db_out is not None else "")
+        dargs = _db_args(L, M, N, db_out, A1.device)
         with torch.cuda.device(A1.device):
             tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, key or "lin-bf16-relubwd"))
-            st = L.lpg_fc_bf16_relu_bwd_bits(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(),
-                                             W1.stride(0), K2, None if A2 is None else A2.data_ptr(),
-                                             A2.stride(0) if K2 else 0, None if W2 is None else W2.data_ptr(),
-                                             W2.stride(0) if K2 else 0, C.data_ptr(), C.stride(0), flags,
-                                             bits.data_ptr(), bits.stride(0), float(scale), _lib.stream_of(A1))
+            st = getattr(L, entry)(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(),
+                                   W1.stride(0), K2, None if A2 is None else A2.data_ptr(),
+                                   A2.stride(0) if K2 else 0, None if W2 is None else W2.data_ptr(),
+                                   W2.stride(0) if K2 else 0, C.data_ptr(), C.stride(0), flags,
+                                   bits.data_ptr(), bits.stride(0), float(scale), *dargs, _lib.stream_of(A1))
             TIMER.stop(tok)
-        _lib.check(st, "lpg_fc_bf16_relu_bwd_bits")
+        _lib.check(st, entry)
         return C
     if mask is not None:
         Y, scale = mask
@@ -392,16 +401,21 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
                 or Y.stride(0) % 8 or Y.data_ptr() % 16 or N % 8 or C.stride(0) % 8 or C.data_ptr() % 16):
             # layouts the folded store does not take: the same bits in two passes
             C = fc_forward_bf16(A1, W1, A2, W2, None, False, out=out, accumulate=accumulate, key=key, kernel=kernel)
-            return relu_bwd_colsum_bf16(C, Y, scale, False)[0]
+            dz = relu_bwd_colsum_bf16(C, Y, scale, False)[0]
+            if db_out is not None:
+                db_out.copy_(colsum_bf16(dz))
+            return dz
+        entry = "lpg_fc_bf16_relu_bwd" + ("_db" if db_out is not None else "")
+        dargs = _db_args(L, M, N, db_out, A1.device)
         with torch.cuda.device(A1.device):
             tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, key or "lin-bf16-relubwd"))
-            st = L.lpg_fc_bf16_relu_bwd(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
-                                        K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
-                                        None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
-                                        C.data_ptr(), C.stride(0), flags, Y.data_ptr(), Y.stride(0), float(scale),
-                                        _lib.stream_of(A1))
+            st = getattr(L, entry)(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
+                                   K2, None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
+                                   None if W2 is None else W2.data_ptr(), W2.stride(0) if K2 else 0,
+                                   C.data_ptr(), C.stride(0), flags, Y.data_ptr(), Y.stride(0), float(scale),
+                                   *dargs, _lib.stream_of(A1))
             TIMER.stop(tok)
-        _lib.check(st, "lpg_fc_bf16_relu_bwd")
+        _lib.check(st, entry)
         return C
     entry = "lpg_fc_f16" if f16 else "lpg_fc_bf16"
     margs = ()
@@ -424,6 +438,14 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
         TIMER.stop(tok)
     _lib.check(st, entry)
     return C
+
+
+def _db_args(L, M: int, N: int, db_out: Tensor | None, device) -> tuple:
+    """(db, workspace) pointers of the lpg_fc_bf16_relu_bwd*_db entries, () without db_out."""
+    if db_out is None:
+        return ()
+    ws = _workspace(L.lpg_relu_bwd_colsum_workspace_bytes(M, N), device)
+    return db_out.data_ptr(), ws.data_ptr()
 
 
 def wgrad_bf16(G: Tensor, X: Tensor) -> Tensor:
@@ -454,17 +476,18 @@ def wgrad_bf16(G: Tensor, X: Tensor) -> Tensor:
 
 
 def input_grad_bf16(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | None = None,
-                    out: Tensor | None = None, accumulate: bool = False, mask=None, kernel: int = 0) -> Tensor:
+                    out: Tensor | None = None, accumulate: bool = False, mask=None, kernel: int = 0,
+                    db_out: Tensor | None = None) -> Tensor:
     """G1 W1 [+ G2 W2] [+ out] in bf16 for Linear weights W [out, in]: the
     c5 input gradient of lin_rel / lin_root on the bf16 FC kernel (lpg_fc_bf16
     with the weights transposed; fp32 accumulation, one bf16 rounding).
     ``mask`` = (Y, scale): the previous layer's ReLU/dropout backward folded into the store
-    (fc_forward_bf16)."""
+    (fc_forward_bf16); ``db_out``: that layer's bias gradient, the column sums of the result."""
     t = lambda W: None if W is None else transpose_bf16(W.detach().to(torch.bfloat16))
     G1 = G1.to(torch.bfloat16)
     G2 = None if G2 is None else G2.to(torch.bfloat16)
     return fc_forward_bf16(G1, t(W1), G2, t(W2), None, False, out=out, accumulate=accumulate, key="igrad-bf16",
-                           mask=mask, kernel=kernel)
+                           mask=mask, kernel=kernel, db_out=db_out)
 
 
 def relu_dropout_bwd(g: Tensor, y: Tensor, scale: float) -> Tensor:

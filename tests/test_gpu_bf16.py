@@ -493,6 +493,41 @@ def test_relu_bwd_bits_equal_relu_bwd_from_y(two, acc):
     assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("M,N,bits,acc", [(19384, 2048, True, True),   # c5's two-part launch (tail: colsum pass)
+                                          (4099, 1032, False, False),  # ragged last 64-row chunk, N tail tile
+                                          (5000, 200, True, False),    # one partial n-tile
+                                          (64, 256, False, True)])     # one chunk (the small-tile kernel)
+def test_relu_bwd_db_equals_colsum(kernel, M, N, bits, acc):
+    """lpg_fc_bf16_relu_bwd*_db: the bias column sums the pipelined kernel takes in its store loop (the
+    colsum pass for rows and kernels it does not cover) are bitwise colsum_bf16 of the dZ it stores, and
+    dZ is the plain folded call's."""
+    from lpgnn.fc import colsum_bf16, input_grad_bf16
+
+    K = 256
+    g = torch.Generator(device=DEV).manual_seed(M + N + kernel)
+    r = lambda *s: (torch.randn(*s, device=DEV, generator=g) * 0.2).to(BF)  # noqa: E731
+    G1, W1 = r(M, K), r(K, N)
+    Y = torch.relu(r(M, N))
+    P = r(M, N) if acc else None
+    mask = (_packbits(Y) if bits else Y, 1.25)
+    want = input_grad_bf16(G1, W1, out=None if P is None else P.clone(), accumulate=acc, mask=mask, kernel=kernel)
+    db = torch.full((N,), float("nan"), device=DEV)
+    got = input_grad_bf16(G1, W1, out=None if P is None else P.clone(), accumulate=acc, mask=mask, kernel=kernel,
+                          db_out=db)
+    assert torch.equal(got, want)
+    assert torch.equal(db, colsum_bf16(want))
+
+
+def test_relu_bwd_db_empty_rows():
+    from lpgnn.fc import input_grad_bf16
+
+    G1, W1 = torch.zeros(0, 64, device=DEV, dtype=BF), torch.ones(64, 16, device=DEV, dtype=BF)
+    db = torch.full((16,), 7.0, device=DEV)
+    out = input_grad_bf16(G1, W1, mask=(torch.zeros(0, 16, device=DEV, dtype=BF), 1.0), db_out=db)
+    assert out.shape == (0, 16) and bool((db == 0).all())
+
+
 def test_gcn_fc_bf16_relu_bits_identical():
     """options.relu_bits: every bf16 ReLU layer writes its 1-bit mask and the next layer's folded ReLU
     backward reads it instead of the layer output -- the same loss and the same gradient bits."""
