@@ -1501,7 +1501,7 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd(int64_t M, int64_t N, int64_t K1, con
                                            const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
                                            int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
                                            int32_t flags, const uint16_t *Y, int64_t ldy, float scale, void *stream) {
-  LPG_REQUIRE(Y != nullptr, "lpg_fc_bf16_relu_bwd: NULL Y");
+  LPG_REQUIRE(Y != nullptr || M == 0 || N == 0, "lpg_fc_bf16_relu_bwd: NULL Y");
   return relu_bwd_entry("lpg_fc_bf16_relu_bwd", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, C, ldc, flags,
                         Y, ldy, nullptr, 0, scale, stream);
 }
@@ -1513,7 +1513,7 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd_bits(int64_t M, int64_t N, int64_t K1
                                                 int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C,
                                                 int64_t ldc, int32_t flags, const uint8_t *mask, int64_t ldm,
                                                 float scale, void *stream) {
-  LPG_REQUIRE(mask != nullptr, "lpg_fc_bf16_relu_bwd_bits: NULL mask");
+  LPG_REQUIRE(mask != nullptr || M == 0 || N == 0, "lpg_fc_bf16_relu_bwd_bits: NULL mask");
   return relu_bwd_entry("lpg_fc_bf16_relu_bwd_bits", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, C, ldc,
                         flags, nullptr, 0, mask, ldm, scale, stream);
 }
@@ -1526,7 +1526,7 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd_db(int64_t M, int64_t N, int64_t K1, 
                                               int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
                                               int32_t flags, const uint16_t *Y, int64_t ldy, float scale, float *db,
                                               void *workspace, void *stream) {
-  LPG_REQUIRE(Y != nullptr && db != nullptr, "lpg_fc_bf16_relu_bwd_db: NULL Y or db");
+  LPG_REQUIRE((Y != nullptr || M == 0 || N == 0) && db != nullptr, "lpg_fc_bf16_relu_bwd_db: NULL Y or db");
   return relu_bwd_entry("lpg_fc_bf16_relu_bwd_db", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, C, ldc,
                         flags, Y, ldy, nullptr, 0, scale, stream, db, workspace);
 }
@@ -1537,7 +1537,7 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd_bits_db(int64_t M, int64_t N, int64_t
                                                    uint16_t *C, int64_t ldc, int32_t flags, const uint8_t *mask,
                                                    int64_t ldm, float scale, float *db, void *workspace,
                                                    void *stream) {
-  LPG_REQUIRE(mask != nullptr && db != nullptr, "lpg_fc_bf16_relu_bwd_bits_db: NULL mask or db");
+  LPG_REQUIRE((mask != nullptr || M == 0 || N == 0) && db != nullptr, "lpg_fc_bf16_relu_bwd_bits_db: NULL mask or db");
   return relu_bwd_entry("lpg_fc_bf16_relu_bwd_bits_db", M, N, K1, A1, lda1, W1, ldw1, K2, A2, lda2, W2, ldw2, C, ldc,
                         flags, nullptr, 0, mask, ldm, scale, stream, db, workspace);
 }
