@@ -184,7 +184,7 @@ def _link_prev(ctx, prev):
         prev.out_folded = True
         # a hidden layer (not conv1, whose backward sums dZ with its small-K weight gradients): its bias
         # gradients come out of this layer's folded input-gradient stores (lpg_fc_bf16_relu_bwd*_db)
-        ctx.db_prev = None if getattr(prev, "narrow", True) else prev
+        ctx.db_prev = None if getattr(prev, "narrow", True) or not ctx.opts.fold_bias_sums else prev
     else:
         ctx.wgk_prev = prev
         prev.wgk_folded = True

@@ -16,6 +16,8 @@ import, so a whole run can be switched from the shell:
   LPGNN_OVERLAP=1            independent SpMMs on a second stream beside the FC
   LPGNN_RELU_BITS=0          bf16: the folded ReLU backward re-reads the layer output instead of the
                              1-bit mask its forward wrote beside it
+  LPGNN_FOLD_BIAS_SUMS=0     bf16: a hidden layer's bias gradient as its own column-sum pass over dZ (not
+                             summed in the next layer's folded input-gradient store)
 """
 from __future__ import annotations
 
@@ -37,6 +39,7 @@ class PathOptions:
     fold_conv1_wgrad: bool = True
     overlap: bool = False
     relu_bits: bool = True
+    fold_bias_sums: bool = True
 
     def __post_init__(self):
         if self.arith not in ("x3", "fp32"):
@@ -51,7 +54,8 @@ class PathOptions:
                    fold_relu_bwd=_env("LPGNN_FOLD_RELU_BWD", "1") == "1",
                    fold_conv1_wgrad=_env("LPGNN_FOLD_CONV1_WGRAD", "1") == "1",
                    overlap=_env("LPGNN_OVERLAP", "0") == "1",
-                   relu_bits=_env("LPGNN_RELU_BITS", "1") == "1")
+                   relu_bits=_env("LPGNN_RELU_BITS", "1") == "1",
+                   fold_bias_sums=_env("LPGNN_FOLD_BIAS_SUMS", "1") == "1")
 
     def replace(self, **kw) -> "PathOptions":
         return dataclasses.replace(self, **kw)

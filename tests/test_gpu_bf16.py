@@ -401,17 +401,19 @@ def test_gcn_fc_bf16_folded_relu_bwd_identical(monkeypatch):
     model = GCN_FC(8, 8, hids=256, depth=5, dp=0.1, compute_dtype="bf16").to(DEV).train()
     out = {}
     base = model.options
-    for fold in (True, False):
-        model.options = base.replace(fold_relu_bwd=fold)
+    for fold in (True, False, "bias"):
+        # "bias": the folded ReLU backward with the bias gradients as their own column-sum passes
+        model.options = base.replace(fold_relu_bwd=bool(fold), fold_bias_sums=fold is True)
         model.zero_grad()
         torch.manual_seed(321)  # same dropout seeds
         lc, lv = model(batch)
         loss = balanced(lc, lv, batch.y_s, batch.y_t)
         loss.backward()
         out[fold] = (loss.item(), {k: p.grad.clone() for k, p in model.named_parameters()})
-    assert out[True][0] == out[False][0]
-    for k, v in out[True][1].items():
-        assert torch.equal(v, out[False][1][k]), k
+    for alt in (False, "bias"):
+        assert out[True][0] == out[alt][0]
+        for k, v in out[True][1].items():
+            assert torch.equal(v, out[alt][1][k]), (alt, k)
 
 
 @pytest.mark.parametrize("R,C", [(8, 8), (2048, 2048), (72, 136), (1000, 8), (2048, 24)])
@@ -551,6 +553,7 @@ def test_gcn_fc_bf16_relu_bits_identical():
         loss = balanced(lc, lv, batch.y_s, batch.y_t)
         loss.backward()
         out[bits] = (loss.item(), {k: p.grad.clone() for k, p in model.named_parameters()})
-    assert out[True][0] == out[False][0]
-    for k, v in out[True][1].items():
-        assert torch.equal(v, out[False][1][k]), k
+    for alt in (False, "bias"):
+        assert out[True][0] == out[alt][0]
+        for k, v in out[True][1].items():
+            assert torch.equal(v, out[alt][1][k]), (alt, k)

@@ -51,6 +51,7 @@ for s in $STAGES; do
       ;;
     bench_part) step bench_part 600 python bench.py --partitioned --sub "" --cpu-steps 0 ;;  # N = 1 through the N > 1 path
     bench_c5_nobits) LPGNN_RELU_BITS=0 step bench_c5_nobits 900 python bench.py --config c5 --steps 10 --warmup 3 ;;
+    bench_c5_nodb) LPGNN_FOLD_BIAS_SUMS=0 step bench_c5_nodb 900 python bench.py --config c5 --steps 10 --warmup 3 ;;
     bench_c5) step bench_c5 900 python bench.py --config c5 --steps 10 --warmup 3 ;;
     bench_inf) step bench_inf 600 python bench.py --inference ;;
     bench_c4) step bench_c4 900 python bench.py --config c4 --steps 5 --warmup 2 --cpu-steps 0 ;;
