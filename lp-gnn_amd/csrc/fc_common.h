@@ -12,7 +12,8 @@ namespace lpg {
 // Counter-based dropout mask over (seed, row, column pair): one round of the 32-bit "lowbias32"
 // integer hash per row and one per (row, column pair); the pair's hash carries 16 bits for each of
 // its two columns (low half: the even column, high half: the odd one), kept iff those bits >=
-// the 16-bit threshold round(p * 2^16) (dropout_params; the drop rate is within 2^-17 of p).
+// the 16-bit threshold round(p * 2^16) (dropout_params; the drop rate is within 2^-17 of p, and the
+// kept values are scaled by the reciprocal of the kept rate, 2^16 / (2^16 - threshold)).
 // Stateless, so the backward pass never needs the mask (the kept set is exactly where the stored
 // output is > 0).  One hash per two outputs: the hash's two quarter-rate v_mul_lo_u32 were most of
 // a dropout epilogue's VALU (round 3: 1.56 VALU per MFMA in the bf16 FC with dropout, 0.37
@@ -100,7 +101,9 @@ inline void dropout_params(float p, uint32_t *thresh, float *scale) {
   if (p > 0.f) {
     const double th = (double)p * 65536.0 + 0.5;  // round(p * 2^16), in [1, 65535]
     *thresh = th >= 65535.0 ? 65535u : (uint32_t)(th < 1.0 ? 1.0 : th);
-    *scale = 1.f / (1.f - p);
+    // kept values x 2^16 / (2^16 - thresh): the reciprocal of the rate actually kept, so E[out]
+    // is exact whatever rounding the 16-bit threshold took (lpgnn.fc.dropout_scale mirrors it)
+    *scale = 65536.f / (float)(65536u - *thresh);
   }
 }
 

@@ -1248,9 +1248,11 @@ extern "C" lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1,
   }
   LPG_REQUIRE(workspace && aligned16(workspace), "%s: workspace missing or not 16-byte aligned", name);
   X3Args a;
-  // (C is only read -- the addend -- and never written here; without the flag Y stands in for it)
+  // (C is only read -- the addend -- and never written here; without the flag Y, whose alignment was
+  // checked above, stands in for it whatever C the caller passed)
+  const bool acc = (flags & LPG_FC_ACCUMULATE) != 0;
   const lpg_status st = x3_args(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, nullptr,
-                                const_cast<float *>(C ? C : Y), C ? ldc : ldy, flags, 0.f, 0, 0, nullptr, &a);
+                                const_cast<float *>(acc ? C : Y), acc ? ldc : ldy, flags, 0.f, 0, 0, nullptr, &a);
   if (st != LPG_OK) return st;
   a.store = 0;
   LPG_REQUIRE(wide_ok(a, 128, 128), "%s: operands the wide kernel does not take (lda1 == lda2, ldw1 == ldw2, "

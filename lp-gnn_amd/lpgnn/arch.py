@@ -111,7 +111,8 @@ class GraphConvTwoDirection(nn.Module):
         self.right2left = GraphConv((right_dim, left_dim), out_dim)
 
     def forward(self, left_feas, right_feas, edge_index: BipartiteCSR, edge_weight=None, relu: bool = False,
-                dropout: float = 0.0, fold_in: bool = False, opts: PathOptions | None = None):
+                dropout: float = 0.0, fold_in: bool = False, opts: PathOptions | None = None,
+                feeds_conv: bool = False):
         # edge_index is A (m x n, rows = cons).  arch.py:71-74: l2r = A^T, r2l = A.
         opts = opts or _DEFAULT_OPTIONS
         if edge_weight is None and isinstance(edge_index, BipartiteCSR) and \
@@ -119,7 +120,7 @@ class GraphConvTwoDirection(nn.Module):
             # one autograd node for both directions (lpgnn.conv): same forward,
             # fused gradient sums and the cheaper association in backward
             return _conv.two_direction(left_feas, right_feas, edge_index, self.left2right, self.right2left,
-                                       relu, dropout, fold_in, opts)
+                                       relu, dropout, fold_in, opts, feeds_conv)
         tdc = getattr(edge_index, "two_direction_conv", None)  # row-partitioned multi-GPU adjacency
         if tdc is not None and edge_weight is None:
             out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout, opts)
@@ -200,20 +201,24 @@ class GCN_FC(GCNBase):
             cd = torch.float16
         # conv -> ReLU (arch.py:181-182): the ReLU is the FC kernel's epilogue.
         opts = self.options
-        left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True, opts=opts)
         dp = self.dp if self.training else 0.0
         layers = list(self.layers)
         single = isinstance(edge_index, BipartiteCSR) and getattr(edge_index, "partitioned_conv", None) is None
         part_heads = getattr(edge_index, "two_direction_heads", None)  # row-partitioned multi-GPU adjacency
         fuse_heads = opts.fuse_heads and len(layers) > 0 and cd == torch.float32 and (single or part_heads is not None)
-        for conv in (layers[:-1] if fuse_heads else layers):
+        # feeds_conv: the layer's outputs go to another GraphConvTwoDirection (not to the heads)
+        left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True, opts=opts,
+                                 feeds_conv=len(layers) > 0)
+        chain = layers[:-1] if fuse_heads else layers
+        for i, conv in enumerate(chain):
             # conv -> dropout -> ReLU (arch.py:185-188).  ReLU commutes with
             # dropout (x * mask / (1-p), a non-negative scale), so the ReLU is
             # fused into the FC and dropout follows it (inside the conv, so a
             # partitioned run drops each variable once, at its owner).
             # fold_in: the previous layer's outputs feed only this layer (bf16: its ReLU/dropout
             # backward runs in this layer's input-gradient stores)
-            left, right = conv(left, right, edge_index, relu=True, dropout=dp, fold_in=True, opts=opts)
+            left, right = conv(left, right, edge_index, relu=True, dropout=dp, fold_in=True, opts=opts,
+                               feeds_conv=fuse_heads or i < len(chain) - 1)
         out = None
         if fuse_heads:  # last layer + heads (arch.py:184-190) as one node: one backward pass over its output
             last = layers[-1]

@@ -75,7 +75,7 @@ def _src_first(S: CSR, f_out: int, f_in: int, esz: int) -> bool:
 
 
 def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                  heads=None, heads_only=False, opts: PathOptions = DEFAULT):
+                  heads=None, heads_only=False, opts: PathOptions = DEFAULT, bits_out: bool = False):
     """The layer's forward (both directions); records on ctx what the backward
     needs and returns (left_new, right_new, tensors to save, logits).  With
     heads = ((Wh_l, bh_l), (Wh_r, bh_r)) the heads run in the FC epilogues
@@ -102,8 +102,10 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     ho = heads is not None and heads_only
 
     # bf16 ReLU layers also write their output's 1-bit ReLU mask (options.relu_bits): the next layer's
-    # folded ReLU backward reads it instead of the output (lpg_fc_bf16_relu_bwd_bits, 1/16 of the bytes)
-    want_bits = bf16 and relu and opts.relu_bits and f_out % 8 == 0 and left.dtype == torch.bfloat16
+    # folded ReLU backward reads it instead of the output (lpg_fc_bf16_relu_bwd_bits, 1/16 of the bytes).
+    # bits_out (decided by the caller, outside the autograd.Function): a GraphConvTwoDirection layer
+    # consumes this output and a backward will run -- the heads read Y, an eval forward reads nothing
+    want_bits = bits_out and bf16 and relu and opts.relu_bits and f_out % 8 == 0 and left.dtype == torch.bfloat16
 
     def direction(S, x_src, x_dst, w_rel, b, w_root, seed, ra, agg=None, head=None):
         """(output, aggregate kept for the backward, logits of `head` or None, ReLU mask bits or None)."""
@@ -141,7 +143,7 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     ctx.adj, ctx.relu, ctx.bf16, ctx.opts = adj, relu, bf16, opts
     ctx.out_bits = (bits_l, bits_r) if want_bits else None
     ctx.f16 = left.dtype == torch.float16
-    ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
+    ctx.scale = _fc.dropout_scale(dropout)
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
     # conv1's shape (narrow LP-feature inputs, kept aggregates, ReLU without dropout, fp32): its weight
     # gradients can be folded into the next layer's input-gradient GEMM (lpg_fc_x3_relu_wgrad_f32)
@@ -155,14 +157,15 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
 class _TwoDirection(torch.autograd.Function):
     @staticmethod
     def forward(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                prev=None, opts=DEFAULT):
+                prev=None, opts=DEFAULT, bits_out=False):
         """``prev``: the backward node of the layer that produced (left, right) and feeds only this
         layer (foldable_producer): bf16 -- its ReLU/dropout backward is folded into this layer's
         input-gradient stores (lpg_fc_bf16_relu_bwd) and it takes dZ as given (column sums only);
         fp32 conv1 -- its weight gradients are folded into this layer's input-gradient GEMMs
         (lpg_fc_x3_relu_wgrad_f32) and handed to it (``folded_wgk``)."""
         left_new, right_new, saved, _ = _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r,
-                                                      w_rel_r2l, b_r2l, w_root_r2l, relu, dropout, opts=opts)
+                                                      w_rel_r2l, b_r2l, w_root_r2l, relu, dropout, opts=opts,
+                                                      bits_out=bits_out)
         _link_prev(ctx, prev)
         ctx.save_for_backward(*saved)
         return left_new, right_new
@@ -171,7 +174,7 @@ class _TwoDirection(torch.autograd.Function):
     def backward(ctx, g_left, g_right):
         if ctx.f16:
             raise RuntimeError("lpgnn: fp16 is the reference's inference mode (val.py:269); train in fp32 or bf16")
-        return _backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None, None)
+        return _backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None, None, None)
 
 
 def _link_prev(ctx, prev):
@@ -433,8 +436,12 @@ def foldable_producer(x: Tensor, opts: PathOptions = DEFAULT):
         return None
     if getattr(g, "bf16", False):
         return g if opts.fold_relu_bwd and x.dtype == torch.bfloat16 else None
+    # conv1's folded backward returns no input gradients and hands its outputs zero-stride gradients:
+    # only when nothing differentiates through its inputs (features without requires_grad) or
+    # observes its outputs' gradients (a hook / retain_grad on them) -- else the two-pass route
     if opts.fold_conv1_wgrad and opts.arith == "x3" and getattr(g, "small_relu", False) and \
-            x.dtype == torch.float32 and g.opts.arith == "x3":
+            x.dtype == torch.float32 and g.opts.arith == "x3" and not any(g.needs_input_grad[:2]) and \
+            not x.retains_grad and not x._backward_hooks:
         return g
     return None
 
@@ -447,13 +454,15 @@ def _fold_prev(left: Tensor, right: Tensor, fold_in: bool, opts: PathOptions):
 
 
 def two_direction(left: Tensor, right: Tensor, adj: BipartiteCSR, left2right, right2left, relu: bool = False,
-                  dropout: float = 0.0, fold_in: bool = False, opts: PathOptions = DEFAULT):
+                  dropout: float = 0.0, fold_in: bool = False, opts: PathOptions = DEFAULT, feeds_conv: bool = False):
     """GraphConvTwoDirection.forward (arch.py:65-81) through one autograd node.  ``fold_in``: the
     caller guarantees (left, right) feed nothing but this layer (GCN_FC's layer chain) -- if they
     are a bf16 ReLU layer's outputs, that layer's ReLU/dropout backward is folded into this one's
     input-gradient stores; if they are fp32 conv1's, conv1's weight gradients come out of this
-    layer's input-gradient GEMMs."""
+    layer's input-gradient GEMMs.  ``feeds_conv``: the outputs feed the next GraphConvTwoDirection
+    layer (so a bf16 ReLU layer writes the 1-bit masks that layer's folded backward reads)."""
     prev = _fold_prev(left, right, fold_in, opts)
     return _TwoDirection.apply(left, right, adj, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                left2right.lin_root.weight, right2left.lin_rel.weight, right2left.lin_rel.bias,
-                               right2left.lin_root.weight, bool(relu), float(dropout), prev, opts)
+                               right2left.lin_root.weight, bool(relu), float(dropout), prev, opts,
+                               bool(feeds_conv and torch.is_grad_enabled()))

@@ -696,6 +696,19 @@ def heads_bwd_bf16(G: Tensor, W: Tensor, Y: Tensor, scale: float | None, want_db
     return dH, dW, db, dbY
 
 
+def dropout_scale(p: float) -> float:
+    """The scale the FC kernels give kept values under dropout p (fc_common.h dropout_params):
+    2^16 / (2^16 - round(p * 2^16)) as float32, the reciprocal of the rate actually kept -- F.dropout's
+    1 / (1 - p) for the 16-bit threshold.  The backward passes use the same value.  p below 2^-17
+    (which the 16-bit threshold cannot draw) is refused rather than silently drawn at 2^-16."""
+    if p <= 0:
+        return 1.0
+    if p >= 1.0 or p * 65536.0 < 0.5:
+        raise ValueError(f"lpgnn dropout: p = {p} outside [2^-17, 1) (16-bit keep threshold)")
+    th = int(min(max(float(torch.tensor(p, dtype=torch.float32)) * 65536.0 + 0.5, 1.0), 65535.0))
+    return float(torch.tensor(65536.0, dtype=torch.float32) / torch.tensor(65536 - th, dtype=torch.float32))
+
+
 def _new_seed() -> int:
     """A dropout seed from torch's default generator (torch.manual_seed reproducible)."""
     return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
@@ -716,7 +729,7 @@ class _FC(torch.autograd.Function):
         else:
             C = fc_forward(A1, W1, A2, W2, b, relu, dropout_p, seed, arith=arith, **kw)
         ctx.relu, ctx.has_a2, ctx.has_b = relu, A2 is not None, b is not None
-        ctx.scale = 1.0 / (1.0 - dropout_p) if dropout_p > 0 else 1.0
+        ctx.scale = dropout_scale(dropout_p)
         ctx.save_for_backward(A1, A2 if A2 is not None else A1, W1, W2 if W2 is not None else W1,
                               C if relu else A1)
         return C

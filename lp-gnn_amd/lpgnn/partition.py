@@ -548,7 +548,7 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
         ex.start_broadcast_(logit_r).finish()
         logits = (logit_l, logit_r)
     ctx.padj, ctx.relu, ctx.opts = padj, relu, opts
-    ctx.scale = 1.0 / (1.0 - dropout) if dropout > 0 else 1.0
+    ctx.scale = _fc.dropout_scale(dropout)
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
     return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r,
                                  w_rel_r2l, w_root_r2l), logits

@@ -6,8 +6,9 @@ threshold of ``dropout_params``).  The reference applies ``F.dropout(x, p, train
 each hidden layer's ReLU (arch.py:186-188 in vbdai/lp-gnn); torch draws that mask from its own
 Philox stream, which no other implementation reproduces, so what parity means here is (1) every
 kernel draws exactly this function's mask (checked bit for bit by tests/test_gpu_dropout_mask.py)
-and (2) the mask is a Bernoulli(1 - p) keep with kept values scaled by 1 / (1 - p), as F.dropout's
-(statistical checks in the same test; the drop rate is round(p * 2^16) / 2^16, within 2^-17 of p).
+and (2) the mask is a Bernoulli(1 - q) keep, q = round(p * 2^16) / 2^16 (within 2^-17 of p), with
+kept values scaled by 1 / (1 - q) -- F.dropout's 1 / (1 - p) at the rate actually drawn, so the
+expectation is exact (statistical checks in the same test).
 Nothing in ``lp-gnn_amd/`` imports this module.
 """
 from __future__ import annotations
@@ -37,6 +38,12 @@ def threshold(p: float) -> int:
         return 0
     th = float(np.float32(p)) * 65536.0 + 0.5
     return 65535 if th >= 65535.0 else int(max(th, 1.0))
+
+
+def scale(p: float) -> float:
+    """dropout_params: the kept values' scale 2^16 / (2^16 - threshold(p)) as float32 (1 at p = 0)."""
+    th = threshold(p)
+    return float(np.float32(65536.0) / np.float32(65536 - th)) if th else 1.0
 
 
 def keep_mask(seed: int, row_keys: np.ndarray, n_cols: int, p: float) -> np.ndarray:

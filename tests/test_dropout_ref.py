@@ -37,3 +37,24 @@ def test_mask_statistics(p):
     # a different seed gives a different mask; the same seed the same one
     assert not np.array_equal(keep, keep_mask(0xDEADBEEF12346, np.arange(M) + 77, N, p))
     assert np.array_equal(keep, keep_mask(0xDEADBEEF12345, np.arange(M) + 77, N, p))
+
+
+@pytest.mark.parametrize("p", [0.1, 0.2, 0.5, 0.9, 1e-3, 2.0 ** -16, 0.99999])
+def test_product_scale_is_the_kept_rate_reciprocal(p):
+    """lpgnn.fc.dropout_scale (what the backward passes use) equals the oracle's restatement of
+    dropout_params' scale: 2^16 / (2^16 - threshold), so E[kept * scale] = 1 exactly."""
+    from lpgnn.fc import dropout_scale
+    from oracle.dropout_ref import scale
+
+    s = dropout_scale(p)
+    assert s == scale(p)
+    q = threshold(p) / 65536.0
+    assert abs(s * (1 - q) - 1.0) < 2e-7
+
+
+@pytest.mark.parametrize("p", [1e-6, 2.0 ** -18, 1.0, 1.5])
+def test_product_scale_refuses_undrawable_rates(p):
+    from lpgnn.fc import dropout_scale
+
+    with pytest.raises(ValueError):
+        dropout_scale(p)

@@ -1,13 +1,13 @@
 """The fused dropout mask of every FC kernel family against its restatement (oracle/dropout_ref.py):
 the kept set of ``fc(..., relu=True, dropout_p=p, seed=s)`` is exactly ``keep_mask(s, keys, N, p)``,
-bit for bit, and kept values are the no-dropout output times 1 / (1 - p) (the reference's
+bit for bit, and kept values are the no-dropout output times 1 / (1 - q), q the drawn rate (the reference's
 F.dropout after the ReLU, arch.py:186-188).  Every output of these cases is positive before the
 dropout (bias +4, small operands), so "kept" is "stored output > 0"."""
 import numpy as np
 import pytest
 import torch
 
-from oracle.dropout_ref import keep_mask, threshold
+from oracle.dropout_ref import keep_mask, scale as keep_scale, threshold
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -28,7 +28,7 @@ def _check(y, base, seed, keys, p):
     got = (y != 0).cpu().numpy()
     assert np.array_equal(got, want), f"{int((got != want).sum())} of {got.size} mask bits differ"
     kept = torch.from_numpy(want).to(DEV)
-    scale = torch.tensor(1.0 / (1.0 - p), dtype=torch.float32)
+    scale = torch.tensor(keep_scale(p), dtype=torch.float32)
     if y.dtype == torch.float32:
         assert torch.equal(y[kept], base[kept] * scale.to(DEV))
     else:  # one RNE of the fp32 value: kept = 16-bit(fp32 result * scale)

@@ -209,6 +209,7 @@ def test_fused_dropout_epilogue_and_backward():
     the drop rate is p, the mask is reproducible from the seed, and the
     backward equals torch autograd through the realised mask."""
     from lpgnn.fc import fc_forward, graph_conv_fc
+    from oracle.dropout_ref import scale as keep_scale
 
     torch.manual_seed(3)
     M, N, K = 4000, 256, 64
@@ -227,7 +228,7 @@ def test_fused_dropout_epilogue_and_backward():
     assert bool((kept <= pos).all())
     rate = 1.0 - kept[pos].float().mean().item()
     assert abs(rate - p) < 0.01, rate
-    scale = torch.tensor(1.0 / (1.0 - p), dtype=torch.float32)
+    scale = torch.tensor(keep_scale(p), dtype=torch.float32)
     assert torch.equal(y[kept], base[kept] * scale.to(DEV))
     # backward through the fused op == torch through the realised mask
     A1r, A2r = A1.clone().requires_grad_(True), A2.clone().requires_grad_(True)
@@ -236,7 +237,7 @@ def test_fused_dropout_epilogue_and_backward():
     out = graph_conv_fc(A1r, A2r, W1r, br, W2r, True, dropout=p)
     g = torch.randn_like(out)
     out.backward(g)
-    mask = (out > 0).float() * (1.0 / (1.0 - p))
+    mask = (out > 0).float() * keep_scale(p)
     A1t, A2t = A1.clone().requires_grad_(True), A2.clone().requires_grad_(True)
     W1t, W2t, bt = (t.clone().requires_grad_(True) for t in (W1, W2, b))
     ref = torch.relu(torch.nn.functional.linear(A1t, W1t, bt) + torch.nn.functional.linear(A2t, W2t)) * mask

@@ -273,6 +273,8 @@ def _logits_close(got, want, h_got, h_want, what):
     d = (got - want).abs().max(-1).values
     bound = 10 * 2 * (h_got - h_want).norm(dim=-1) / h_want.norm(dim=-1) * (1 + 1e-6) + 4e-6
     over = d > 1e-4
+    print(f"[partition {what}] max|dh| {float(dh.max()):.3e}, max|dlogit| {float(d.max()):.3e}, "
+          f"nodes > 1e-4: {int(over.sum())} of {got.shape[0]}", flush=True)
     assert bool((~over | (d <= bound)).all()), (what, "a logit difference not explained by add_knowledge")
     assert int(over.sum()) <= max(2, got.shape[0] // 5000), (what, int(over.sum()))
 

@@ -370,3 +370,32 @@ def test_conv1_wgrad_fold_equals_separate_pass(hids, depth):
             torch.testing.assert_close(v, w, rtol=1e-4, atol=1e-4 * w.abs().max().item(), msg=k)
         else:
             assert torch.equal(v, w), k
+
+
+def test_conv1_wgrad_fold_keeps_feature_gradients():
+    """with x_s / x_t requiring grad (saliency use) the fold must not apply -- conv1's
+    folded backward returns no input gradients.  The feature gradients and every parameter gradient
+    equal the run with options.fold_conv1_wgrad off, bitwise."""
+    from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
+    from lpgnn.train import balanced
+
+    g = synth.uniform_lp(700, 1400, 9000, seed=5)
+    adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=256, depth=3, dp=0.0).to(DEV).train()
+    base = model.options.replace(arith="x3")
+    out = {}
+    for fold in (True, False):
+        model.options = base.replace(fold_conv1_wgrad=fold)
+        model.zero_grad()
+        x_s = torch.from_numpy(g.x_s).to(DEV).requires_grad_(True)
+        x_t = torch.from_numpy(g.x_t).to(DEV).requires_grad_(True)
+        batch = BipartiteBatch(x_s=x_s, x_t=x_t, y_s=torch.from_numpy(g.y_s).to(DEV),
+                               y_t=torch.from_numpy(g.y_t).to(DEV), edge_index=adj, s_bs=g.m, t_bs=g.n)
+        lc, lv = model(batch)
+        balanced(lc, lv, batch.y_s, batch.y_t).backward()
+        assert x_s.grad is not None and x_t.grad is not None and x_s.grad.abs().sum() > 0
+        out[fold] = (x_s.grad.clone(), x_t.grad.clone(), {k: p.grad.clone() for k, p in model.named_parameters()})
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
+    for k, v in out[True][2].items():
+        assert torch.equal(v, out[False][2][k]), k

@@ -36,6 +36,9 @@ for s in $STAGES; do
     tests_files)  # PYTEST_FILES (space-separated), every failure reported (maxfail PYTEST_MAXFAIL, default 30)
       step pytest_files 700 python -u -m pytest ${PYTEST_FILES} -m gpu --maxfail ${PYTEST_MAXFAIL:-30} -v \
         -p no:cacheprovider -rf --timeout 120 --timeout-method thread ;;
+    tests_s)  # the whole -m gpu suite with -s (the parity tests print their measured counts), every failure reported
+      step pytest_s 900 python -u -m pytest tests -m gpu -s --maxfail ${PYTEST_MAXFAIL:-30} -v -p no:cacheprovider -rf \
+        --timeout 300 --timeout-method thread ;;
     tests_all)  # the whole -m gpu suite, every failure reported
       step pytest_all 800 python -u -m pytest tests -m gpu --maxfail ${PYTEST_MAXFAIL:-30} -v -p no:cacheprovider -rf \
         --timeout 300 --timeout-method thread ;;
