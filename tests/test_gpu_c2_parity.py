@@ -43,6 +43,7 @@ from oracle import model_ref as O
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 DEV = "cuda:0"
 LOGIT_ATOL = 1e-4
+C2_OVER_MAX = 20  # nodes whose normalised logits are beyond 1e-4 (add_knowledge amplification): measured 13 / 9
 
 _CACHE = {}
 
@@ -158,8 +159,9 @@ def test_c2_eval_logits_labels_vs_reference_arithmetic(arith, monkeypatch):
           f"max|HIP - fp64| = {(got - r64['logits']).abs().max():.3e}")
     assert dh.max() <= LOGIT_ATOL
     assert bool((~over | (d <= bound)).all()), "a logit difference not explained by add_knowledge's amplification"
-    # round 2: 13 (x3) / 9 (exact fp32) of 300 000 nodes, all with |h| < 1e-2
-    assert int(over.sum()) <= n_nodes // 5000, "more than 0.02 % of nodes beyond 1e-4 of the reference arithmetic"
+    # measured (profiles/r05_parity_head.log, as in round 2): 13 (x3) / 9 (exact fp32) of 300 000 nodes, all
+    # with |h| < 1e-2 -- the bar is that count plus a margin, not a fraction of the graph
+    assert int(over.sum()) <= C2_OVER_MAX, "more nodes beyond 1e-4 of the reference arithmetic than measured"
     # (3) argmax == MKL's outside near-ties at the observed difference
     emax = float(d.max())
     top2 = ref.topk(2, dim=-1).values
@@ -172,6 +174,9 @@ def test_c2_eval_logits_labels_vs_reference_arithmetic(arith, monkeypatch):
     print(f"[{arith}] c2: inference_gnn labels differing from MKL's: {int(diff.sum())} "
           f"(near-tie nodes at eps={emax:.2e}: {int(tie.sum())})")
     assert bool((~diff | tie).all()), "a basis label differs from the reference arithmetic outside a near-tie"
+    # the north star's bit-identical basis labels: measured 0 differences in both arithmetics at the seed-0
+    # graph (rounds 2 and 5), so any difference -- even at a near-tie -- fails
+    assert int(diff.sum()) == 0, f"{int(diff.sum())} inference_gnn labels differ from the reference arithmetic's"
     # (5) against fp64: at least as close as the reference's fp32 arithmetic
     t = r64["logits"]
     e_got, e_ref = (got - t).abs(), (ref - t).abs()
@@ -217,7 +222,7 @@ def test_c2_training_step_grads_vs_oracle_autograd(arith, monkeypatch):
 # move its logits by more than a top-2 gap of 1 -- and only there.
 C5_MEAN, C5_P99, C5_ARGMAX = 0.05, 0.25, 0.995
 C5_HEAD_REL = 0.02        # relative Frobenius error of the heads h (before add_knowledge)
-C5_CLEAR_FLIPS_MAX = 30   # argmax flips where MKL's top-2 gap > 1 (round 2: ~3 of 300 000)
+C5_CLEAR_FLIPS_MAX = 8    # argmax flips where MKL's top-2 gap > 1 (measured 3 of 277 486 in rounds 2 and 5)
 
 
 def test_c5_bf16_logits_and_step_vs_fp32_oracle(monkeypatch):
@@ -282,13 +287,13 @@ def test_c5_bf16_logits_and_step_vs_fp32_oracle(monkeypatch):
 # tensor rounded to fp16, fp32 accumulation inside each op (MKL for the FC).  The HIP fp16 kernels
 # agree with it up to where an fp32 summation-order difference moves a value across an fp16 rounding
 # midpoint (one fp16 ulp, 2^-11 relative), propagated through the layers.  Bounds (round-4 measurement
-# printed by the test): heads within C2F16_HEAD_REL relative (Frobenius), logits' p99 within 4 fp16 ulps
+# printed by the test, profiles/r05_parity_head.log): heads within C2F16_HEAD_REL relative (Frobenius), logits' p99 within 4 fp16 ulps
 # of 16, every node beyond that explained by add_knowledge's amplification 10 * 2 |dh| / |h| (+ 2 ulps
 # of the output's rounding); inference_gnn labels equal except where such a node or an fp16 tie at the
 # top-m boundary decides.
 C2F16_HEAD_REL = 2e-3
 C2F16_LOGIT_P99 = 4 * 2.0 ** -7
-C2F16_LABEL_DIFF_MAX = 300
+C2F16_LABEL_DIFF_MAX = 20  # measured 9 of 300 000, none where the logits agree exactly (r05_parity_head.log)
 
 
 def test_c2_fp16_eval_vs_fp16_oracle(monkeypatch):

@@ -233,6 +233,11 @@ def test_fused_heads_node_equals_separate_heads(monkeypatch):
         out[fuse] = (loss.item(), {k: p.grad.clone() for k, p in model.named_parameters()})
     assert abs(out[True][0] - out[False][0]) < 1e-6
     for k, v in out[True][1].items():
+        w = out[False][1][k]
+        d = (v - w).abs()
+        print(f"{k}: max|fused - separate| {d.max():.3e} (max|g| {w.abs().max():.3e}, rel. Frobenius "
+              f"{((v - w).norm() / w.norm()).item():.2e})")
+    for k, v in out[True][1].items():
         torch.testing.assert_close(v, out[False][1][k], rtol=1e-4, atol=1e-6, msg=k)
 
 

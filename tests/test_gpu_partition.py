@@ -267,7 +267,8 @@ def _logits_close(got, want, h_got, h_want, what):
     """The north-star bar at the normalised logits (the c2 parity test's form): the heads' outputs h
     (before add_knowledge) within 1e-4 everywhere; the logits within 1e-4, or -- where add_knowledge's
     10 h / |h| amplifies the node's own head difference -- within its Lipschitz bound 10 * 2 |dh| / |h|,
-    on at most 0.02 % of the nodes (and at least 2)."""
+    on at most 2 nodes (measured at HEAD: 0 or 1 per side, profiles/r05_parity_head.log -- a boundary
+    variable's sum is split across ranks, so its fp32 order differs from one GPU's)."""
     dh = (h_got - h_want).abs()
     assert float(dh.max()) <= 1e-4, (what, float(dh.max()))
     d = (got - want).abs().max(-1).values
@@ -276,7 +277,7 @@ def _logits_close(got, want, h_got, h_want, what):
     print(f"[partition {what}] max|dh| {float(dh.max()):.3e}, max|dlogit| {float(d.max()):.3e}, "
           f"nodes > 1e-4: {int(over.sum())} of {got.shape[0]}", flush=True)
     assert bool((~over | (d <= bound)).all()), (what, "a logit difference not explained by add_knowledge")
-    assert int(over.sum()) <= max(2, got.shape[0] // 5000), (what, int(over.sum()))
+    assert int(over.sum()) <= 2, (what, int(over.sum()))
 
 
 def _worker_c4(rank, world, port, out_dir, mode, scale=50, hids=256):

@@ -379,7 +379,7 @@ def test_conv1_wgrad_fold_keeps_feature_gradients():
     from lpgnn import BipartiteBatch, BipartiteCSR, GCN_FC, synth
     from lpgnn.train import balanced
 
-    g = synth.uniform_lp(700, 1400, 9000, seed=5)
+    g = synth.uniform_lp(700, 1400, 9100, seed=5)
     adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV)
     torch.manual_seed(0)
     model = GCN_FC(8, 8, hids=256, depth=3, dp=0.0).to(DEV).train()
