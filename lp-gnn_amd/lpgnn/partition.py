@@ -156,6 +156,69 @@ def plan_partition(row, col, val, m: int, n: int, world: int, rank: int, bounds=
                          int((ntouch >= 2).sum()))
 
 
+def plan_partition_local(row, col, val, m: int, n: int, world: int, rank: int, group=None, bounds=None,
+                         local: bool = False) -> PartitionPlan:
+    """plan_partition's plan of `rank`, built from the rank's OWN constraint rows (the general planner of
+    a loaded LP: lpgnn.run --partition).  Equal to plan_partition field for field
+    (tests/test_partition.py), without any rank holding the partition's global structures:
+
+    * row blocks: nnz-balanced split points from the global row degrees (``bounds``, or row_blocks of
+      the global host `row`);
+    * owners: each rank counts its edges per variable; one MAX all-reduce of (count, lowest rank)
+      keys picks, per variable, the rank holding most of its edges (ties: lowest rank), untouched
+      variables going to the rank of their id block -- plan_partition's rule;
+    * receive lists: the owners learn who touches their variables from one all_to_all of the halo id
+      lists (plan_partition_blocks' exchange); the boundary count from one SUM all-reduce.
+
+    ``local``: (row, col, val) already hold only this rank's rows [bounds[rank], bounds[rank+1]) (global
+    row ids) -- then ``bounds`` is required.  Host numpy throughout; nothing goes to the device here."""
+    row = np.asarray(row, np.int64)
+    col = np.asarray(col, np.int64)
+    val = np.asarray(val, np.float32)
+    if bounds is None:
+        if local:
+            raise ValueError("plan_partition_local(local=True) needs the row block bounds")
+        bounds = row_blocks(row, m, world)
+    bounds = np.asarray(bounds, np.int64)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    if not local:
+        sel = (row >= lo) & (row < hi)
+        row, col, val = row[sel], col[sel], val[sel]
+    cnt = np.bincount(col, minlength=n).astype(np.int64)  # this rank's edges per variable
+    touch = (cnt > 0).astype(np.int64)
+    if world > 1:
+        # key: count * world + (world - 1 - rank) -- the MAX is the most edges, then the lowest rank
+        key = torch.from_numpy(np.where(cnt > 0, cnt * world + (world - 1 - rank), -1))
+        ntouch = torch.from_numpy(touch)
+        gpu = dist.get_backend(group) != "gloo"
+        if gpu:
+            key, ntouch = key.cuda(), ntouch.cuda()
+        dist.all_reduce(key, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(ntouch, group=group)
+        key, ntouch = key.cpu().numpy(), ntouch.cpu().numpy()
+    else:
+        key, ntouch = np.where(cnt > 0, cnt * world + (world - 1 - rank), -1), touch
+    owner = (np.arange(n, dtype=np.int64) * world) // max(n, 1)
+    hit = key >= 0
+    owner[hit] = world - 1 - key[hit] % world
+    owned = np.nonzero(owner == rank)[0].astype(np.int64)
+    touched = np.nonzero(cnt)[0].astype(np.int64)
+    halo = touched[owner[touched] != rank]  # ascending
+    o = owner[halo]
+    srt = np.argsort(o, kind="stable")       # grouped by owner rank, ascending variable within a group
+    send_counts = np.bincount(o, minlength=world).tolist()
+    send_idx = owned.shape[0] + srt.astype(np.int64)
+    if world > 1:
+        got, recv_counts = _a2a_ids(halo[srt], send_counts, group)
+        recv_idx = np.searchsorted(owned, got).astype(np.int64)
+    else:
+        recv_idx, recv_counts = np.empty(0, np.int64), [0]
+    is_own = owner[col] == rank
+    e_col = np.where(is_own, np.searchsorted(owned, col), owned.shape[0] + np.searchsorted(halo, col))
+    return PartitionPlan(rank, world, m, n, lo, hi, owned, halo, row - lo, col, e_col.astype(np.int64), val,
+                         send_idx, send_counts, recv_idx, recv_counts, int((ntouch >= 2).sum()))
+
+
 def _block_owner_ranges(blocks: int, world: int):
     if blocks % world:
         raise ValueError(f"{blocks} row blocks do not split evenly over {world} ranks")
@@ -782,6 +845,60 @@ def make_block_batch(spec, plan: PartitionPlan, device, group=None, cons=None):
         cons = (np.concatenate([c[0] for c in cons]), np.concatenate([c[1] for c in cons]))
     x_t, y_t = spec.var_rows(plan.local_vars)
     return local_batch(plan, cons[0], x_t, cons[1], y_t, device, group)
+
+
+def lp_partition_batch(record, world: int, rank: int, device, group=None):
+    """This rank's batch of a processed LP record ([row, col, A_data, c_feas, v_feas, y_s, y_t,
+    nnodes], dataset.py:213-217 -- what lpio.msgpack_load returns for a .pk file): the rank-local plan
+    (plan_partition_local over the host edge list), its constraint block and [owned | halo] variable
+    rows, the local dual CSR and boundary exchange on `device`.  The checks of LPDataset.get
+    (dataset.py:235-238) apply to the whole record, as there."""
+    row, col, A_data, c_feas, v_feas, y_s, y_t, nnodes = record
+    A_data = np.asarray(A_data)
+    c_feas, v_feas = np.asarray(c_feas, np.float32), np.asarray(v_feas, np.float32)
+    assert A_data.max() <= 1 and A_data.min() >= -1  # dataset.py:235-236
+    assert c_feas.max() <= 1 and c_feas.min() >= -1  # dataset.py:237-238
+    m, n = c_feas.shape[0], v_feas.shape[0]
+    assert int(nnodes) == m + n
+    plan = plan_partition_local(row, col, A_data.astype(np.float32), m, n, world, rank, group)
+    lv = plan.local_vars
+    y_s, y_t = np.asarray(y_s, np.int64), np.asarray(y_t, np.int64)
+    rows = slice(plan.row_lo, plan.row_hi)
+    return local_batch(plan, c_feas[rows], v_feas[lv], y_s[rows], y_t[lv], device, group)
+
+
+def gather_logits(lc: torch.Tensor, lv: torch.Tensor, batch, group=None):
+    """The whole graph's (cons [m, C], vars [n, C]) logits on every rank from the ranks' partitioned
+    outputs: each rank contributes its constraint block and its OWNED variables (a halo row is a copy
+    of its owner's); one padded all_gather.  For the metrics of lpgnn.run (accuracy, validation)."""
+    plan = batch.plan
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    own = torch.cat((lc.detach().float(), lv.detach().float()[:plan.n_own]))
+    if world == 1:
+        return own[:plan.m_local].clone(), own[plan.m_local:].clone()
+    gloo = dist.get_backend(group) == "gloo"
+    cnt = torch.tensor([own.shape[0]], dtype=torch.int64, device="cpu" if gloo else own.device)
+    cnts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    cnts = [int(c.item()) for c in cnts]
+    big = max(cnts)
+    pad = own.new_zeros((big, own.shape[1]))
+    pad[:own.shape[0]] = own
+    if gloo:
+        pad = pad.cpu()
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    # every rank's block bounds and owned ids (host metadata, once per call)
+    meta = [None] * world
+    dist.all_gather_object(meta, (plan.row_lo, plan.row_hi, plan.owned), group=group)
+    C = own.shape[1]
+    cons = own.new_empty((plan.m, C))
+    var = own.new_empty((plan.n, C))
+    for q, (lo, hi, owned) in enumerate(meta):
+        p = parts[q].to(own.device)
+        cons[lo:hi] = p[:hi - lo]
+        var[torch.from_numpy(np.asarray(owned)).to(own.device)] = p[hi - lo:cnts[q]]
+    return cons, var
 
 
 def local_batch(plan: PartitionPlan, x_s, x_t, y_s, y_t, device, group=None):

@@ -33,7 +33,21 @@ What is different, and why:
   parameter gradients are averaged with one bucketed all-reduce per round
   (a round = one graph per rank, all of that graph's mini-batches
   accumulated), so one optimizer step sees `world` graphs where the
-  reference's sees one -- a larger effective batch, reported as such.
+  reference's sees one -- a larger effective batch, reported as such;
+* ``--partition 1`` (torch.distributed initialised, or one process): the
+  graphs above ``--edge_num_thresh`` -- which the reference cuts into
+  NeighborLoader mini-batches on one device (train.py:103-116, val.py:19-27,
+  utils.py:808) -- are trained and evaluated WHOLE, row-partitioned over the
+  ranks (lpgnn.partition): every rank reads the .pk on the
+  host, plans only its own constraint rows (partition.plan_partition_local),
+  and one optimizer step per graph sees the full-graph gradient (the
+  per-rank balanced-loss shares and parameter gradients are all-reduced), so
+  the result is the one-GPU full-graph step's up to fp32 summation order.
+  Graphs at or below the threshold run whole on every rank (identical
+  replicated steps, no communication).  ``--partition 2``: every graph is
+  row-partitioned.  Training uses the balanced loss (the published one); the
+  logged accuracy and ``validation`` gather the owned rows' logits
+  (partition.gather_logits) and apply the reference's rules to the whole graph.
 """
 from __future__ import annotations
 
@@ -110,6 +124,15 @@ class LPDataset:
         if f not in self._nnz:
             self._nnz[f] = int(np.asarray(lpio.msgpack_load(self.path(i))[0]).shape[0])
         return self._nnz[f]
+
+    def record(self, i: int):
+        """Graph i's processed record [row, col, A_data, c_feas, v_feas, y_s, y_t, nnodes] (host arrays:
+        the row-partitioned path plans and slices it per rank)."""
+        from . import lpio
+
+        rec = lpio.msgpack_load(self.path(i))
+        self._nnz[self._indices[i]] = int(np.asarray(rec[0]).shape[0])
+        return rec
 
     def __getitem__(self, idx):
         if isinstance(idx, (list, tuple, np.ndarray)):
@@ -198,6 +221,9 @@ def parser():
     ap.add_argument("--prefetch_factor", type=int, default=2)
     ap.add_argument("--replicas", type=int, default=0,
                     help="data parallel over graphs when torch.distributed is initialised (world > 1)")
+    ap.add_argument("--partition", type=int, default=0, choices=(0, 1, 2),
+                    help="1: graphs above --edge_num_thresh are trained / evaluated whole, row-partitioned over "
+                         "the ranks (instead of NeighborLoader mini-batches); 2: every graph is")
     return ap
 
 
@@ -258,6 +284,19 @@ def _average_grads(model, world):
         p.grad.div_(world)
 
 
+def _partitioned(args, ds, i) -> bool:
+    """--partition: graph i of ds takes the row-partitioned path."""
+    p = int(getattr(args, "partition", 0))
+    return p == 2 or (p == 1 and ds.nnz(i) > args.edge_num_thresh)
+
+
+def _partition_batch(args, ds, i):
+    from .partition import lp_partition_batch
+
+    rank, world = _dist_world()
+    return lp_partition_batch(ds.record(i), world, rank, args.dev)
+
+
 # ------------------------------------------------------------------ run_exp
 def run_exp(args, model=None, ds=None):
     """train.py:55-157.  Returns a dict with the per-epoch mean losses, the
@@ -268,6 +307,10 @@ def run_exp(args, model=None, ds=None):
     os.makedirs(args.log_dir, exist_ok=True)
     rank, world = _dist_world()
     replicas = bool(args.replicas) and world > 1
+    if replicas and int(getattr(args, "partition", 0)):
+        raise ValueError("--replicas and --partition are exclusive (graphs over ranks vs one graph over ranks)")
+    if int(getattr(args, "partition", 0)) and args.loss != "balanced":
+        raise ValueError("--partition trains with the balanced loss (train.py:39-46, the published experiment)")
     if rank == 0:
         with open(os.path.join(args.log_dir, "args.json"), "w") as fp:
             json.dump({k: v for k, v in vars(args).items() if isinstance(v, (int, float, str, type(None)))}, fp,
@@ -292,6 +335,16 @@ def run_exp(args, model=None, ds=None):
             order = order[: len(order) // world * world][rank::world]
         ep_losses = []
         for idx_graphs, gi in enumerate(order):
+            if _partitioned(args, train_ds, gi):
+                loss, acc = _partition_train_step(args, model, opt, train_ds, gi)
+                glstep += 1
+                loss_meter.update(loss)
+                ep_losses.append(loss)
+                acc_meter.update(acc)
+                if glstep % 9 == 1:
+                    log.info(f"{epoch} {idx_graphs}/{len(order)} {glstep} {loss_meter.avg:.5f} {acc_meter.avg:.4f} "
+                             f"(row-partitioned over {world})")
+                continue
             graph = train_ds[gi]
             batches = epoch_batches(graph, args.arch, args.batch_size, dev=args.dev,
                                     seed=args.seed + 1000 * epoch + gi)
@@ -331,6 +384,31 @@ def run_exp(args, model=None, ds=None):
     return hist
 
 
+def _partition_train_step(args, model, opt, ds, gi):
+    """One full-graph step of graph gi row-partitioned over the ranks (train.py:117-129 on the whole
+    graph): forward on every rank's rows, the balanced loss's per-rank shares, backward, one
+    all-reduce of the parameter gradients, the optimizer step.  Returns the global (loss, accuracy)."""
+    from .partition import _all_reduce_, balanced_distributed, all_reduce_grads, gather_logits
+    from .val import accuracy_device
+
+    batch = _partition_batch(args, ds, gi)
+    lc, lv = model(batch)
+    loss = balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.n_own)
+    opt.zero_grad()
+    loss.backward()
+    all_reduce_grads(model)
+    opt.step()
+    tot = _all_reduce_(loss.detach().clone().reshape(1))
+    assert not torch.isnan(tot).item()  # train.py:126 (on the whole graph's loss)
+    cons, var = gather_logits(lc, lv, batch)
+    p = batch.plan
+    y = torch.empty(p.m + p.n, dtype=torch.int64, device=cons.device)
+    yc, yv = gather_logits(batch.y_s[:, None].float(), batch.y_t[:, None].float(), batch)
+    y[:p.m], y[p.m:] = yc[:, 0].long(), yv[:, 0].long()
+    acc = accuracy_device(torch.cat((cons, var)), y, p.m)[0]
+    return float(tot.item()), float(acc.item())
+
+
 # --------------------------------------------------------------- validation
 @torch.no_grad()
 def validation(model, ds, args):
@@ -343,11 +421,24 @@ def validation(model, ds, args):
     was_training = model.training
     model.eval()
     avg_acc, rows = 0., []
+    fp16 = next(model.parameters()).dtype == torch.float16
     for i in range(len(ds)):
-        graph = ds[i]
-        lc, lv = model_inference_with_batch(model, graph, args.arch, dev=args.dev, batch_size=args.batch_size,
-                                            fp16=next(model.parameters()).dtype == torch.float16)
-        y = graph.y if not hasattr(graph, "x_s") else torch.cat((graph.y_s, graph.y_t))
+        if _partitioned(args, ds, i):  # the whole graph, row-partitioned over the ranks (every rank: all rows)
+            from .partition import gather_logits
+
+            if fp16:
+                raise NotImplementedError("--fp16 evaluation of a row-partitioned graph (the partitioned layers "
+                                          "run fp32 / bf16); evaluate it with --partition 0")
+            batch = _partition_batch(args, ds, i)
+            yl = gather_logits(batch.y_s[:, None].float(), batch.y_t[:, None].float(), batch)
+            y = torch.cat(yl)[:, 0].long().cpu()
+            lc, lv = gather_logits(*model(batch), batch)
+            lc, lv = lc.cpu(), lv.cpu()
+        else:
+            graph = ds[i]
+            lc, lv = model_inference_with_batch(model, graph, args.arch, dev=args.dev, batch_size=args.batch_size,
+                                                fp16=fp16)
+            y = graph.y if not hasattr(graph, "x_s") else torch.cat((graph.y_s, graph.y_t))
         acc, prec, recl = accuracy(torch.cat((lc, lv), 0), y.cpu(), lc.shape[0], return_pr=True,
                                    dataset_name=args.dataset)
         avg_acc += acc / len(ds)
@@ -362,12 +453,12 @@ def main(argv=None):
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(message)s")
     args = parse_args(argv)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env > 1 and not args.replicas:
-        # under a launcher without --replicas every rank would train the full schedule and write
-        # args.json / mdl.pth into the same directory: refuse instead
-        raise SystemExit(f"WORLD_SIZE={world_env}: pass --replicas 1 for data-parallel training over graphs "
-                         "(or run one process)")
-    if args.replicas:
+    if world_env > 1 and not (args.replicas or args.partition):
+        # under a launcher without --replicas / --partition every rank would train the full schedule on
+        # its own and write args.json / mdl.pth into the same directory: refuse instead
+        raise SystemExit(f"WORLD_SIZE={world_env}: pass --replicas 1 for data-parallel training over graphs, "
+                         "--partition 1 to row-partition the large graphs over the ranks (or run one process)")
+    if args.replicas or args.partition:
         import torch.distributed as dist
 
         if world_env > 1 and not dist.is_initialized():

@@ -80,3 +80,70 @@ def test_half_model_trains_refused_eval_runs():
     assert lc.dtype == torch.float16 and torch.isfinite(lc).all() and torch.isfinite(lv).all()
     with pytest.raises(RuntimeError, match="inference mode"):
         model.train()(b)
+
+
+def _partition_worker(rank, world, port, tmp, epochs):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # ranks share the box's one GPU
+    try:
+        from lpgnn import GCN_FC, run
+
+        args = run.parse_args(["train", "--arch", "GCN_FC(8,8,hids=64,depth=3)", "--dataset", "synth",
+                               "--data_prefix", os.path.join(tmp, "data"), "--log_prefix", os.path.join(tmp, "runs"),
+                               "--epochs", str(epochs), "--edge_num_thresh", "700", "--partition", "1"])
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=64, depth=3).to(args.dev)  # dp 0.1: masks keyed on global node ids
+        torch.manual_seed(1)
+        hist = run.run_exp(args, model=model)
+        ds = run.LPDataset(args.dataset_processed_prefix, thresh_num=args.edge_num_thresh, device=args.dev)
+        _, acc, _ = run.validation(model, ds, args)
+        torch.save({"loss": hist["epoch_loss"], "acc": float(acc),
+                    "sd": {k: v.cpu() for k, v in model.state_dict().items()}}, os.path.join(tmp, f"part{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_run_partition_two_hip_ranks_match_one_gpu(tmp_path):
+    """``run.py train --partition 1`` with 2 HIP ranks (gloo, sharing the GPU) on .pk LPs above
+    --edge_num_thresh (800 and 1800 edges vs 700): every epoch's loss and the final parameters equal the
+    one-GPU full-graph training of the same model and seeds (dropout 0.1 -- the masks are keyed on
+    global node ids) within fp32 summation-order tolerance; both ranks end bitwise identical;
+    validation over every graph (partitioned above the threshold) gives the one-GPU accuracy."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from lpgnn import GCN_FC, run
+
+    write_dataset(str(tmp_path / "data" / "synth" / "highs-inp_tgt"), k=4,
+                  sizes=((60, 120, 600), (50, 90, 500), (80, 100, 800), (90, 200, 1800)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_partition_worker, args=(2, port, str(tmp_path), 3), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "part0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "part1.pt", weights_only=True)
+    for k in r0["sd"]:
+        assert torch.equal(r0["sd"][k], r1["sd"][k]), k
+    # one GPU, whole graphs (no threshold: every graph one full-graph step)
+    args = run.parse_args(["train", "--arch", "GCN_FC(8,8,hids=64,depth=3)", "--dataset", "synth", "--data_prefix",
+                           str(tmp_path / "data"), "--log_prefix", str(tmp_path / "runs1"), "--epochs", "3",
+                           "--edge_num_thresh", "1e12"])
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=64, depth=3).to(args.dev)
+    torch.manual_seed(1)
+    hist = run.run_exp(args, model=model)
+    print("partitioned epoch losses", r0["loss"], "one GPU", hist["epoch_loss"])
+    np.testing.assert_allclose(r0["loss"], hist["epoch_loss"], rtol=1e-5)
+    worst = 0.0
+    for k, v in model.state_dict().items():
+        d = (r0["sd"][k] - v.cpu()).abs().max().item()
+        worst = max(worst, d)
+        np.testing.assert_allclose(r0["sd"][k].numpy(), v.cpu().numpy(), rtol=1e-4, atol=2e-6, err_msg=k)
+    ds = run.LPDataset(args.dataset_processed_prefix, device=args.dev)
+    _, acc, _ = run.validation(model, ds, args)
+    print(f"max |param_partitioned - param_one_gpu| {worst:.2e}; accuracy {r0['acc']:.6f} vs {acc:.6f}")
+    assert abs(r0["acc"] - acc) < 1e-9 and abs(r1["acc"] - acc) < 1e-9

@@ -283,3 +283,48 @@ def test_exchange_dropout_keys_are_global_ids():
     p = plan_partition(g.row, g.col, g.val, g.m, g.n, 2, 1, bounds=[0, 120, 240],
                        owner=(np.arange(g.n) * 2) // g.n)
     assert Exchange(p, "cpu").var_keys is None
+
+
+# ------------------------------------------- the rank-local general planner (lpgnn.run --partition)
+def _plan_fields_equal(a, b):
+    for f in ("rank", "world", "m", "n", "row_lo", "row_hi", "send_counts", "recv_counts", "n_boundary_global"):
+        assert getattr(a, f) == getattr(b, f), f
+    for f in ("owned", "halo", "e_row", "e_gcol", "e_col", "e_val", "send_idx", "recv_idx"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+
+
+def _local_plan_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lpgnn import partition as part, synth
+
+        for g in (_graph(), synth.skewed_lp(300, 700, 3000, a=1.5, seed=4), synth.uniform_lp(200, 900, 1000, seed=1)):
+            want = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
+            _plan_fields_equal(part.plan_partition_local(g.row, g.col, g.val, g.m, g.n, world, rank), want)
+            # from the rank's own rows only
+            b = part.row_blocks(np.asarray(g.row, np.int64), g.m, world)
+            sel = (g.row >= b[rank]) & (g.row < b[rank + 1])
+            _plan_fields_equal(part.plan_partition_local(g.row[sel], g.col[sel], g.val[sel], g.m, g.n, world, rank,
+                                                         bounds=b, local=True), want)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_plan_partition_local_equals_global_planner(tmp_path, world):
+    """The rank-local planner (one MAX all-reduce of owner keys, one all_to_all of halo ids) builds
+    exactly plan_partition's plan from the global edge list, field for field -- including the
+    skewed-degree graph whose dense rows tie owners, and a graph with untouched variables."""
+    mp.spawn(_local_plan_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").exists()
+
+
+def test_plan_partition_local_world_one():
+    from lpgnn import partition as part
+
+    g = _graph()
+    _plan_fields_equal(part.plan_partition_local(g.row, g.col, g.val, g.m, g.n, 1, 0),
+                       part.plan_partition(g.row, g.col, g.val, g.m, g.n, 1, 0))

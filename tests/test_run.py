@@ -219,3 +219,133 @@ def test_world_size_without_replicas_is_refused(tmp_path, monkeypatch):
     with pytest.raises(SystemExit, match="--replicas"):
         run.main(["train", "--dataset", "synth", "--data_prefix", str(tmp_path / "d"), "--log_prefix",
                   str(tmp_path / "r")])
+
+
+# ---------------------------------------- --partition: large graphs row-partitioned over the ranks
+def _oracle_swaps():
+    """The product's HIP local compute -> the oracle (tests/test_partition.py's doubles)."""
+    import torch.nn.functional as F
+
+    import lpgnn.fc as fc
+    import lpgnn.partition as part
+    from oracle import model_ref as O
+
+    def spmm(adj, x):
+        fwd = (adj.fwd.rowptr.numpy(), adj.fwd.col.numpy(), adj.fwd.val.numpy())
+        bwd = (adj.bwd.rowptr.numpy(), adj.bwd.col.numpy(), adj.bwd.val.numpy())
+        return O.spmm_t(fwd, bwd, x)
+
+    def conv_fc(agg, x_dst, w_rel, b_rel, w_root, relu, dropout=0.0, row_offset=0, row_keys=None, arith=None):
+        out = F.linear(agg, w_rel, b_rel) + F.linear(x_dst, w_root)
+        return torch.relu(out) if relu else out
+
+    def knowledge(logit, feas, bound=10):
+        return O.add_knowledge(logit, logit[:1], feas, feas[:1], bound)[0]
+
+    part._local_spmm = spmm
+    fc.graph_conv_fc = conv_fc
+    fc.linear = lambda x, w, b, fold_in=False, opts=None: F.linear(x, w, b)
+    fc.knowledge = knowledge
+
+
+PART_SIZES = ((120, 260, 1800), (90, 200, 1350))
+
+
+def _partition_worker(rank, world, port, tmp, thresh):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    try:
+        from lpgnn import GCN_FC, run
+
+        _oracle_swaps()
+        args = run.parse_args(["train", "--dataset", "synth", "--data_prefix", os.path.join(tmp, "data"),
+                               "--log_prefix", os.path.join(tmp, "runs"), "--epochs", "3", "--partition", "1",
+                               "--edge_num_thresh", str(thresh), "--arch", "GCN_FC(8,8,hids=16,depth=3)"])
+        args.dev = "cpu"
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=16, depth=3, dp=0.0)
+        hist = run.run_exp(args, model=model)
+        ds = run.LPDataset(args.dataset_processed_prefix, thresh_num=args.edge_num_thresh, device="cpu")
+        _, va = run.split_train_val(ds)
+        _, acc, rows = run.validation(model, va, args)
+        torch.save({"loss": hist["epoch_loss"], "acc": float(acc), "sd": model.state_dict()},
+                   os.path.join(tmp, f"part{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_run_partition_gloo_matches_one_process(tmp_path):
+    """``run.py train --partition 1`` under 2 gloo ranks on a dataset whose graphs are above
+    --edge_num_thresh (oracle local compute): every epoch's loss and the final parameters equal a
+    one-process full-graph training of the same model (the oracle's forward, balanced loss, Adam +
+    StepLR, train.py:85-157) within fp32 summation-order tolerance, both ranks end bitwise
+    identical, rank 0's mdl.pth is that model, and ``validation`` (gathered logits, the reference's
+    accuracy) gives the one-process accuracy."""
+    from lpgnn import GCN_FC, run
+    from lpgnn.val import accuracy
+    from oracle import model_ref as O
+
+    write_dataset(str(tmp_path / "data" / "synth" / "highs-inp_tgt"), k=2, sizes=PART_SIZES)
+    mp.spawn(_partition_worker, args=(2, _free_port(), str(tmp_path), 1000), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "part0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "part1.pt", weights_only=True)
+    for k in r0["sd"]:
+        assert torch.equal(r0["sd"][k], r1["sd"][k]), k
+    ck = torch.load(tmp_path / "runs" / "tmp" / "mdl.pth", weights_only=True)
+    for k in ck:
+        assert torch.equal(ck[k], r0["sd"][k]), k
+
+    # one process, whole graph: the oracle's GCN_FC (MKL fp32), the same optimizer and schedule
+    args = _args(tmp_path, "--epochs", "3")
+    ds = run.LPDataset(args.dataset_processed_prefix, device="cpu")
+    tr, va = run.split_train_val(ds)
+    torch.manual_seed(0)
+    params = {k: v.detach().clone().requires_grad_(True)
+              for k, v in GCN_FC(8, 8, hids=16, depth=3, dp=0.0).state_dict().items()}
+    opt = torch.optim.Adam(list(params.values()), lr=1e-3, weight_decay=5e-4)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=max(3 // 4, 1), gamma=0.1)
+
+    def fwd(rec):
+        row, col, val, xs, xt, ys, yt, _ = rec
+        m, n = len(xs), len(xt)
+        A = O.csr_from_coo(np.asarray(row), np.asarray(col), np.asarray(val, np.float32), m, n)
+        AT = O.csr_transpose(*A, m, n)
+        lc, lv = O.gcn_fc_forward(params, torch.as_tensor(np.asarray(xs)), torch.as_tensor(np.asarray(xt)), A, AT, 3)
+        return lc, lv, torch.as_tensor(np.asarray(ys)), torch.as_tensor(np.asarray(yt))
+
+    losses = []
+    for _ in range(3):
+        lc, lv, ys, yt = fwd(tr.record(0))  # one train graph (70 / 30 of 2)
+        loss = O.balanced(lc, lv, ys, yt)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        sched.step()
+        losses.append(loss.item())
+    print("partitioned epoch losses", r0["loss"], "one process", losses)
+    np.testing.assert_allclose(r0["loss"], losses, rtol=1e-5)
+    for k, v in params.items():
+        np.testing.assert_allclose(r0["sd"][k].numpy(), v.detach().numpy(), rtol=1e-4, atol=2e-6, err_msg=k)
+    with torch.no_grad():
+        lc, lv, ys, yt = fwd(va.record(0))
+    acc = accuracy(torch.cat((lc, lv)), torch.cat((ys, yt)), lc.shape[0])
+    assert abs(r0["acc"] - acc) < 1e-9 and abs(r1["acc"] - acc) < 1e-9, (r0["acc"], r1["acc"], acc)
+
+
+def test_partition_flag_rules(tmp_path, monkeypatch):
+    from lpgnn import run
+
+    write_dataset(str(tmp_path / "data" / "synth" / "highs-inp_tgt"), k=2, sizes=PART_SIZES)
+    a = _args(tmp_path, "--partition", "1", "--edge_num_thresh", "1500")
+    ds = run.LPDataset(a.dataset_processed_prefix, device="cpu")
+    assert [run._partitioned(a, ds, i) for i in range(2)] == [True, False]  # 1800 > 1500 >= 1350
+    a.partition = 2
+    assert all(run._partitioned(a, ds, i) for i in range(2))
+    a.partition = 0
+    assert not any(run._partitioned(a, ds, i) for i in range(2))
+    b = _args(tmp_path, "--partition", "1", "--replicas", "1")
+    b.dev = "cpu"
+    monkeypatch.setattr(run, "_dist_world", lambda: (0, 2))  # replicas only engage at world > 1
+    with pytest.raises(ValueError, match="exclusive"):
+        run.run_exp(b, model=TinyModel())
