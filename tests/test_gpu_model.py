@@ -237,8 +237,13 @@ def test_fused_heads_node_equals_separate_heads(monkeypatch):
         d = (v - w).abs()
         print(f"{k}: max|fused - separate| {d.max():.3e} (max|g| {w.abs().max():.3e}, rel. Frobenius "
               f"{((v - w).norm() / w.norm()).item():.2e})")
+    # the two routes sum the heads' dZ in different fp32 orders (one fused pass vs Linear backward + ReLU
+    # backward): measured relative Frobenius distance <= 1.2e-6 per tensor, max elementwise 1.8e-6 at
+    # |g| <= 1.5 -- the elementwise floor is relative to the tensor's scale
     for k, v in out[True][1].items():
-        torch.testing.assert_close(v, out[False][1][k], rtol=1e-4, atol=1e-6, msg=k)
+        w = out[False][1][k]
+        assert ((v - w).norm() / w.norm()).item() <= 1e-5, k
+        torch.testing.assert_close(v, w, rtol=1e-4, atol=1e-5 * w.abs().max().item(), msg=k)
 
 
 @pytest.mark.parametrize("m,n", [(900, 1700), (5000, 2300)])
