@@ -20,6 +20,12 @@ One workload family at every N (the line the driver turns into a scaling curve):
 * sub-record ``inference`` (N=1) -- the reference's own timed path (scripts/pred_basis.py:157-176):
   eval-mode model(batch) + inference_gnn on c2, ms/graph, with the oracle's CPU inference beside it;
   ``inference_fp16`` the same after model.half() + batch_to(half=True) (its --fp16 mode, val.py:269).
+* sub-record ``c5`` (N=1) -- BASELINE.json configs[4]: the c2 graph, GCN_FC(8,8,hids=2048,depth=6)
+  in bf16, training steps, with its SpMM and MFMA rooflines and one oracle CPU training step (fp32,
+  the reference's arithmetic) beside it.
+* sub-record ``skewed`` (N=1) -- SURVEY.md §8d's skewed-degree workload: Zipf(1.5) constraint-row
+  degrees (synth.skewed_lp, 100K x 200K, ~2M edges), the c2 model's training step, per-direction
+  SpMM rooflines (the heavy-row units live).
 
 With --gpus N > 1 and no RANK / WORLD_SIZE in the environment, bench.py launches the N ranks
 itself (one child process per GPU, started before this process touches the GPU; rank 0 prints
@@ -57,7 +63,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense (MI355X_MICROARCH.md; the 5 PF figure is
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=("c2", "c4", "c5"), default="c2",
+    ap.add_argument("--config", choices=("c2", "c4", "c5", "skewed"), default="c2",
                     help="c2 = headline fp32 hid 1024 depth 3, weak scaling over N (default); c4 = 2M x 4M nnz 40M "
                          "(whole graph at N=1, row-partitioned at N>1: strong scaling); c5 = bf16 hid 2048 depth 6")
     ap.add_argument("--steps", type=int, default=20)
@@ -81,10 +87,14 @@ def parse(argv=None):
                     help="time eval-mode forward + inference_gnn (the reference's timed path) instead of training")
     ap.add_argument("--fp16", action="store_true",
                     help="with --inference: the reference's --fp16 mode (model.half(), batch_to(half=True))")
-    ap.add_argument("--sub", default="c4,inference,inference_fp16",
+    ap.add_argument("--sub", default="c4,inference,inference_fp16,c5,skewed",
                     help="sub-records after the headline ('' = none): c4 (configs[3] at the same N), "
                          "inference (N=1: the reference's timed eval path on c2), inference_fp16 (the same in "
-                         "the reference's --fp16 mode)")
+                         "the reference's --fp16 mode), c5 (N=1: configs[4], bf16 hid 2048 depth 6), skewed "
+                         "(N=1: Zipf(1.5) row degrees, the c2 model)")
+    ap.add_argument("--c5-steps", type=int, default=10)
+    ap.add_argument("--c5-warmup", type=int, default=3)
+    ap.add_argument("--c5-cpu-steps", type=int, default=1, help="oracle CPU training steps of c5 (0 = skip)")
     ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--c4-warmup", type=int, default=2)
     ap.add_argument("--c4-scale", type=int, default=1, help="c4 sub-record at 1/scale size (rehearsals)")
@@ -139,9 +149,11 @@ def _threads():
     return min(threads, len(os.sched_getaffinity(0)))
 
 
-def cpu_baseline(g, hids, depth, steps):
+def cpu_baseline(g, hids, depth, steps, warmup=True):
     """The oracle (C restatement of torch_sparse spmm_cpu + torch CPU GEMMs)
-    timed on this host for `steps` full fwd+bwd steps of the same workload."""
+    timed on this host for `steps` full fwd+bwd steps of the same workload (after one untimed
+    warm-up step unless ``warmup`` is False -- c5, whose CPU step is long, runs after the c2 leg
+    has already started the MKL / OpenMP threads)."""
     from oracle import model_ref as O
 
     threads = _threads()
@@ -161,7 +173,8 @@ def cpu_baseline(g, hids, depth, steps):
         loss.backward()
         opt.step()
 
-    step()  # untimed warm-up: first-touch allocations, MKL / OpenMP thread start-up
+    if warmup:
+        step()  # untimed warm-up: first-touch allocations, MKL / OpenMP thread start-up
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -236,7 +249,8 @@ def cpu_spmm(g, F, reps=3):
 def workload_name(args) -> str:
     """The one-GPU workload string (also the PMC key of the N=1 line)."""
     dt = ", bf16" if args.bf16 else (", fp16" if getattr(args, "fp16", False) else "")
-    kind = "synthetic block LP (8 row blocks, rho=%g)" % args.rho if args.config == "c4" else "synthetic LP"
+    kind = ("synthetic block LP (8 row blocks, rho=%g)" % args.rho if args.config == "c4" else
+            "synthetic Zipf(1.5) row-degree LP" if args.config == "skewed" else "synthetic LP")
     what = "eval forward + inference_gnn" if getattr(args, "inference", False) else "fwd+bwd+Adam"
     return (f"{args.config}: {kind} {args.m}x{args.n} nnz={args.nnz}, "
             f"GCN_FC(8,8,hids={args.hids},depth={args.depth}{dt}) {what}")
@@ -440,6 +454,8 @@ def one_gpu_job(args, dev, inference=False, fp16=False):
         from lpgnn.partition import bench_spec
 
         g = bench_spec(args, 1).full()
+    elif args.config == "skewed":
+        g = synth.skewed_lp(args.m, args.n, args.nnz, a=1.5, seed=0)
     else:
         g = synth.uniform_lp(args.m, args.n, args.nnz, seed=0)
     adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
@@ -479,6 +495,14 @@ def c4_args(args):
     if args.c4_scale > 1:
         a.m, a.n, a.nnz = a.m // args.c4_scale, a.n // args.c4_scale, a.nnz // args.c4_scale
     return a
+
+
+def sub_args(args, config):
+    """args for a one-GPU sub-record of BASELINE config `config` (c5, skewed) at its own sizes."""
+    a = copy.copy(args)
+    a.config, a.m, a.n, a.nnz, a.hids, a.depth = config, None, None, None, None, None
+    a.inference, a.fp16 = False, False
+    return fill(a)
 
 
 def run_config(ctx, a, steps, warmup, family):
@@ -681,6 +705,32 @@ def main():
         a_inf.inference, a_inf.fp16 = True, True
         rec, _ = run_inference(ctx, a_inf, args.inf_steps, 3, True, with_cpu=rank == 0)
         out["inference_fp16"] = rec
+    if "c5" in subs and not args.inference and world == 1 and not args.partitioned and args.config == "c2":
+        a5 = sub_args(args, "c5")
+        rec, g5 = run_config(ctx, a5, args.c5_steps, args.c5_warmup, "c5")
+        rec["steps"], rec["warmup"] = args.c5_steps, args.c5_warmup
+        rec["dtype"] = "bf16"
+        rec["note"] = ("BASELINE.json configs[4]: the c2 graph, GCN_FC(8,8,hids=2048,depth=6), bf16 activations / "
+                       "SpMM storage / MFMA FC (fp32 accumulation, fp32 master weights), fwd+bwd+Adam on one GPU")
+        if rank == 0 and args.c5_cpu_steps > 0:
+            cdt, threads = cpu_baseline(g5, a5.hids, a5.depth, args.c5_cpu_steps, warmup=False)
+            edges_step = rec["value"] * rec["ms_per_step"] / 1e3
+            rec["cpu_baseline"] = {"value": edges_step / cdt, "unit": "edges/s", "cores": threads, "kind": "port",
+                                   "sample": f"{args.c5_cpu_steps} full fwd+bwd+Adam step(s) of the same c5 workload "
+                                             f"in fp32 (the reference's CPU arithmetic), no separate warm-up step "
+                                             f"(the c2 leg started the MKL / OpenMP threads): oracle C spmm_cpu loop "
+                                             f"(OpenMP) + torch CPU GEMMs, {cdt:.2f} s/step",
+                                   "s_per_step": cdt}
+        del g5
+        out["c5"] = rec
+    if "skewed" in subs and not args.inference and world == 1 and not args.partitioned and args.config == "c2":
+        ask = sub_args(args, "skewed")
+        rec, _ = run_config(ctx, ask, args.steps, args.warmup, "skewed")
+        rec["steps"], rec["warmup"] = args.steps, args.warmup
+        rec["note"] = ("SURVEY.md 8d skewed-degree workload: Zipf(1.5) constraint-row degrees (synth.skewed_lp, "
+                       "capped at n, rescaled to ~2M edges), uniform variables, GCN_FC(8,8,hids=1024,depth=3) "
+                       "fwd+bwd+Adam; spmm_directions = per-direction roofline (cons<-vars carries the heavy rows)")
+        out["skewed"] = rec
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

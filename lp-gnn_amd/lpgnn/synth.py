@@ -248,4 +248,6 @@ CONFIGS = {
     "c4": dict(m=2_000_000, n=4_000_000, nnz=40_000_000, hids=1024, depth=3),
     # configs[4]: c2 graph, hid 2048, depth 6, bf16
     "c5": dict(m=100_000, n=200_000, nnz=2_000_000, hids=2048, depth=6),
+    # SURVEY.md 8d skewed-degree workload: Zipf(1.5) row degrees (skewed_lp) at the c2 sizes and model
+    "skewed": dict(m=100_000, n=200_000, nnz=2_000_000, hids=1024, depth=3),
 }
