@@ -42,7 +42,7 @@ from torch import Tensor
 
 from . import fc as _fc
 from .options import DEFAULT, PathOptions
-from .sparse import BipartiteCSR, CSR, spmm_forward
+from .sparse import BipartiteCSR, CSR, spmm_forward as _spmm_forward
 
 _GEMM_FLOPS = 160e12  # in-step rates used only to pick the cheaper association
 _SPMM_BYTES = 7e12
@@ -94,6 +94,7 @@ def _forward_core(ctx, left, right, adj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l
     ra_r = reassociate(AT.n_cols, AT.n_rows, left.shape[1], f_out, opts.reassociate)
     ra_l = reassociate(A.n_cols, A.n_rows, right.shape[1], f_out, opts.reassociate)
     fwd32 = functools.partial(_fc.fc_forward, arith=opts.arith)
+    spmm_forward = functools.partial(_spmm_forward, heavy=opts.spmm_heavy)  # noqa: F811 (the model's options)
 
     hd = heads if heads is not None and not bf16 else (None, None)
     # no-grad (eval) forward of the heads layer: its output feeds only the heads, so the fused kernels
@@ -202,6 +203,7 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
     bf16 = ctx.bf16
     dt = torch.bfloat16 if bf16 else torch.float32
     opts = ctx.opts
+    spmm_forward = functools.partial(_spmm_forward, heavy=opts.spmm_heavy)  # noqa: F811 (the model's options)
     pre = getattr(ctx, "folded_wgk", None)
     if getattr(ctx, "wgk_folded", False) and pre is not None:
         # conv1 whose weight gradients the next layer computed in its input-gradient GEMMs

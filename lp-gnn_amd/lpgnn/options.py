@@ -18,6 +18,8 @@ import, so a whole run can be switched from the shell:
                              1-bit mask its forward wrote beside it
   LPGNN_FOLD_BIAS_SUMS=0     bf16: a hidden layer's bias gradient as its own column-sum pass over dZ (not
                              summed in the next layer's folded input-gradient store)
+  LPGNN_SPMM_HEAVY=<deg>     SpMM rows with more edges than this run as (heavy row, slice) wave units
+                             (lpg_spmm_*_tuned's heavy list); 0 = off (default 1024)
 """
 from __future__ import annotations
 
@@ -40,10 +42,13 @@ class PathOptions:
     overlap: bool = False
     relu_bits: bool = True
     fold_bias_sums: bool = True
+    spmm_heavy: int = 1024  # sparse.DEFAULT_HEAVY
 
     def __post_init__(self):
         if self.arith not in ("x3", "fp32"):
             raise ValueError(f"PathOptions.arith must be 'x3' or 'fp32', got {self.arith!r}")
+        if int(self.spmm_heavy) < 0:
+            raise ValueError(f"PathOptions.spmm_heavy must be >= 0, got {self.spmm_heavy}")
 
     @classmethod
     def from_env(cls) -> "PathOptions":
@@ -55,7 +60,8 @@ class PathOptions:
                    fold_conv1_wgrad=_env("LPGNN_FOLD_CONV1_WGRAD", "1") == "1",
                    overlap=_env("LPGNN_OVERLAP", "0") == "1",
                    relu_bits=_env("LPGNN_RELU_BITS", "1") == "1",
-                   fold_bias_sums=_env("LPGNN_FOLD_BIAS_SUMS", "1") == "1")
+                   fold_bias_sums=_env("LPGNN_FOLD_BIAS_SUMS", "1") == "1",
+                   spmm_heavy=int(_env("LPGNN_SPMM_HEAVY", "1024")))
 
     def replace(self, **kw) -> "PathOptions":
         return dataclasses.replace(self, **kw)

@@ -564,10 +564,11 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
     from . import fc as _fc
     from .conv import reassociate
     from .options import DEFAULT
-    from .sparse import spmm_forward
+    from .sparse import spmm_forward as _spmm_forward
 
     opts = DEFAULT if opts is None else opts
     fcf = functools.partial(_fc.fc_forward, arith=opts.arith)
+    spmm_forward = functools.partial(_spmm_forward, heavy=opts.spmm_heavy)
 
     if dropout > 0 and not relu:
         raise RuntimeError("lpgnn FC: fused dropout requires the ReLU epilogue")
@@ -625,10 +626,11 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
 
     from . import fc as _fc
     from .conv import _src_first
-    from .sparse import spmm_forward
+    from .sparse import spmm_forward as _spmm_forward
 
     igf = functools.partial(_fc.input_grad, arith=ctx.opts.arith)
     wgf = functools.partial(_fc.wgrad, arith=ctx.opts.arith)
+    spmm_forward = functools.partial(_spmm_forward, heavy=ctx.opts.spmm_heavy)
 
     left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
     ex = ctx.padj.ex

@@ -18,7 +18,6 @@ There is no CPU path: a CPU tensor raises.
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -180,13 +179,17 @@ class BipartiteCSR:
         return cls(CSR(a_rp, a_c, a_v, m, n), CSR(at_rp, at_c, at_v, n, m))
 
 
-# rows with more edges than this run as (row, 64-column) wave units (lpg_spmm_f32_heavy); 0 = off
-HEAVY_THRESH = int(os.environ.get("LPGNN_SPMM_HEAVY", "1024"))
+DEFAULT_HEAVY = 1024  # PathOptions.spmm_heavy's default (rows above it: heavy wave units)
 
 
-def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0) -> torch.Tensor:
+def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0, heavy: int | None = None) -> torch.Tensor:
     """Y = adj @ x on the GPU (no autograd).  fp32, bf16 or fp16 storage.  ``slice_cols`` / ``depth``: the
-    per-call tuning of lpg_spmm_*_tuned (0 = auto; every choice gives the same bits)."""
+    per-call tuning of lpg_spmm_*_tuned (0 = auto; every choice gives the same bits).  ``heavy``: rows with
+    more edges than this run as (heavy row, slice) wave units, 0 = off (PathOptions.spmm_heavy; None = the
+    default options')."""
+    from .options import DEFAULT
+
+    heavy_thresh = DEFAULT.spmm_heavy if heavy is None else int(heavy)
     if x.device.type != "cuda" or adj.device != x.device:
         raise RuntimeError(f"lpgnn.spmm: x ({x.device}) and adj ({adj.device}) must be on the same HIP device; "
                            "there is no CPU path")
@@ -206,8 +209,8 @@ def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0)
     else:
         raise RuntimeError(f"lpgnn.spmm: unsupported dtype {x.dtype}")
     heavy = None
-    if Fd >= 256 and HEAVY_THRESH > 0:  # degree-aware: rows above the threshold on narrow wave units
-        heavy = adj.heavy_rows(HEAVY_THRESH)
+    if Fd >= 256 and heavy_thresh > 0:  # degree-aware: rows above the threshold on narrow wave units
+        heavy = adj.heavy_rows(heavy_thresh)
         if heavy[1] == 0:
             heavy = None
     with torch.cuda.device(x.device):
@@ -215,7 +218,7 @@ def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0)
         tok = TIMER.start(("spmm", adj.n_rows, adj.n_cols, Fd, str(x.dtype)))
         st = getattr(L, name)(ctypes.byref(adj.cstruct()), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), Fd,
                               None if heavy is None else heavy[0].data_ptr(), 0 if heavy is None else heavy[1],
-                              HEAVY_THRESH if heavy is not None else 0, int(slice_cols), int(depth), stream)
+                              heavy_thresh if heavy is not None else 0, int(slice_cols), int(depth), stream)
         TIMER.stop(tok)
     _lib.check(st, name)
     return y

@@ -54,7 +54,7 @@ def test_spmm_f16_skewed_heavy_rows_bitwise():
     m, n = 3000, 4000
     deg = np.minimum(rng.zipf(1.5, m), 200)
     deg[[5, 1500, 2999]] = [3000, 1500, 1100]
-    assert int(deg.max()) > S.HEAVY_THRESH  # heavy rows take the split path
+    assert int(deg.max()) > S.DEFAULT_HEAVY  # heavy rows take the split path
     row = np.repeat(np.arange(m), deg)
     col = np.concatenate([rng.choice(n, d, replace=False) for d in deg]).astype(np.int64)
     val = rng.uniform(-1, 1, len(row)).astype(np.float32)

@@ -250,7 +250,6 @@ def test_degree_aware_heavy_rows_bitwise(thresh, Fd, slice_cols, monkeypatch):
     from lpgnn import _lib, sparse, synth
     from lpgnn.sparse import spmm_forward
 
-    monkeypatch.setattr(sparse, "HEAVY_THRESH", thresh)
     g = synth.skewed_lp(3000, 5000, 60000, seed=11)
     row = np.concatenate([g.row, np.full(4000, 7, np.int64)])  # row 7: a dense constraint (4000 extra edges)
     col = np.concatenate([g.col, np.arange(1000, 5000, dtype=np.int64)])
@@ -263,7 +262,7 @@ def test_degree_aware_heavy_rows_bitwise(thresh, Fd, slice_cols, monkeypatch):
     rng = np.random.default_rng(Fd)
     for csr, ref, n_src in ((adj.fwd, A, g.n), (adj.bwd, AT, g.m)):
         X = rng.standard_normal((n_src, Fd)).astype(np.float32)
-        got = spmm_forward(csr, torch.from_numpy(X).to(DEV), slice_cols=slice_cols).cpu().numpy()
+        got = spmm_forward(csr, torch.from_numpy(X).to(DEV), slice_cols=slice_cols, heavy=thresh).cpu().numpy()
         assert np.array_equal(got, O.spmm_f32(*ref, X))
         if thresh < csr.degrees().max().item():  # the heavy path actually ran in this direction
             assert csr.heavy_rows(thresh)[1] > 0
@@ -333,6 +332,5 @@ def test_bf16_heavy_rows_bitwise(thresh, Fd, monkeypatch):
     A, _ = _oracle_pair(row, col, val, m, n)
     X = torch.randn(n, Fd).to(torch.bfloat16)
     Xbits = X.view(torch.int16).numpy().view(np.uint16)
-    monkeypatch.setattr(S, "HEAVY_THRESH", thresh)
-    y = spmm_forward(adj.fwd, X.to(DEV)).cpu().view(torch.int16).numpy().view(np.uint16)
+    y = spmm_forward(adj.fwd, X.to(DEV), heavy=thresh).cpu().view(torch.int16).numpy().view(np.uint16)
     assert np.array_equal(y, O.spmm_bf16(*A, Xbits))

@@ -14,6 +14,7 @@ SWITCHES = {  # env name -> (field, value the switch selects)
     "LPGNN_OVERLAP": ("overlap", True),
     "LPGNN_RELU_BITS": ("relu_bits", False),
     "LPGNN_FOLD_BIAS_SUMS": ("fold_bias_sums", False),
+    "LPGNN_SPMM_HEAVY": ("spmm_heavy", 256),
 }
 
 
@@ -27,14 +28,15 @@ def test_defaults_are_the_fused_x3_path(monkeypatch):
     o = PathOptions.from_env()
     assert o == PathOptions()
     assert (o.arith, o.reassociate, o.fuse_heads, o.fuse_head_fwd, o.fold_relu_bwd, o.fold_conv1_wgrad,
-            o.overlap, o.relu_bits, o.fold_bias_sums) == ("x3", True, True, True, True, True, False, True, True)
+            o.overlap, o.relu_bits, o.fold_bias_sums, o.spmm_heavy) == ("x3", True, True, True, True, True, False, True,
+                                                                        True, 1024)
 
 
 @pytest.mark.parametrize("name", sorted(SWITCHES))
 def test_each_switch_sets_one_field(monkeypatch, name):
     _clear(monkeypatch)
     field, value = SWITCHES[name]
-    raw = value if isinstance(value, str) else ("1" if value else "0")
+    raw = value if isinstance(value, str) else str(value) if type(value) is int else ("1" if value else "0")
     monkeypatch.setenv(name, raw)
     o = PathOptions.from_env()
     assert getattr(o, field) == value
@@ -49,3 +51,11 @@ def test_replace_is_a_copy_and_arith_is_checked():
         PathOptions(arith="fp64")
     with pytest.raises(Exception):
         base.relu_bits = False  # frozen: no module or object state a caller mutates
+
+
+def test_spmm_heavy_default_matches_the_sparse_module():
+    from lpgnn import sparse
+
+    assert PathOptions().spmm_heavy == sparse.DEFAULT_HEAVY
+    with pytest.raises(ValueError):
+        PathOptions(spmm_heavy=-1)

@@ -103,16 +103,14 @@ def _spmm_graph(out, L, gname, g, spmm_forward, BipartiteCSR):
         fns = {}
         ref = spmm_forward(csr, X)
         from lpgnn import sparse as S
-        h0 = S.HEAVY_THRESH
+        h0 = S.DEFAULT_HEAVY
         for sl, u, h in ((0, 0, h0), (128, 8, h0), (128, 16, h0), (256, 8, h0), (256, 16, h0), (256, 32, h0),
                          (512, 8, h0), (256, 8, 0), (256, 8, 256)):
-            def f(sl=sl, u=u, h=h):
-                S.HEAVY_THRESH = h  # degree-aware split: rows above h on (row, 64-column) waves; 0 = off
-                return spmm_forward(csr, X, slice_cols=sl, depth=u)
+            def f(sl=sl, u=u, h=h):  # degree-aware split: rows above h on (row, slice) waves; 0 = off
+                return spmm_forward(csr, X, slice_cols=sl, depth=u, heavy=h)
             assert torch.equal(f(), ref)
             fns[f"slice{sl} depth{u} heavy>{h}"] = f
         t = timeit(fns)
-        S.HEAVY_THRESH = h0
         B = g.nnz * 1024 * 4 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 1024 * 4
         for k, v in t.items():
             out[f"spmm {gname} {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000,
@@ -161,21 +159,16 @@ def bench_spmm16(out):
         adj = BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device="cuda")
         for name, csr, K in (("cons<-vars", adj.fwd, g.n), ("vars<-cons", adj.bwd, g.m)):
             X = torch.randn(K, 2048, device="cuda").to(torch.bfloat16)
-            from lpgnn import sparse as S0
-            hh, S0.HEAVY_THRESH = S0.HEAVY_THRESH, 0
-            ref = spmm_forward(csr, X, slice_cols=1024)  # the whole-row (round-1) form as the reference
-            S0.HEAVY_THRESH = hh
+            ref = spmm_forward(csr, X, slice_cols=1024, heavy=0)  # the whole-row (round-1) form as the reference
             fns = {}
             from lpgnn import sparse as S
-            h0 = S.HEAVY_THRESH
+            h0 = S.DEFAULT_HEAVY
             for sl, h in ((256, h0), (256, 0), (512, 0), (1024, 0)):
                 def f(sl=sl, h=h):
-                    S.HEAVY_THRESH = h
-                    return spmm_forward(csr, X, slice_cols=sl)
+                    return spmm_forward(csr, X, slice_cols=sl, heavy=h)
                 assert torch.equal(f(), ref)
                 fns[f"slice{sl} heavy>{h}"] = f
             t = timeit(fns)
-            S.HEAVY_THRESH = h0
             B = g.nnz * 2048 * 2 + g.nnz * 8 + (csr.n_rows + 1) * 8 + csr.n_rows * 2048 * 2
             for k, v in t.items():
                 out[f"spmm bf16 {gname} {name} {k}"] = dict(ms=v, gbs=B / v / 1e6, frac=B / v / 1e6 / 8000)
