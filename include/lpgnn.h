@@ -407,6 +407,44 @@ lpg_status lpg_fc_bf16_relu_bwd_bits_db(int64_t M, int64_t N, int64_t K1, const 
                                         int32_t flags, const uint8_t *mask, int64_t ldm, float scale, float *db,
                                         void *workspace, void *stream);
 
+/* Every 16-bit FC form above in one call, with the workspace of the persistent stream-K kernel
+ * (fc_bf16_sk): G = (CUs rounded down to a multiple of 8) resident blocks split the call's
+ * (tile, k-tile) iterations into G nearly equal ranges, a tile cut by a range boundary carrying its
+ * fp32 accumulators from one block to the next through `workspace` -- no partial last round of
+ * 256 x 256 tiles and no chip-wide burst of epilogue stores, the same bits as the per-call entries
+ * (the same MFMA chain per output).  It applies when the call has at least G tiles and the
+ * pipelined kernel takes its operands; otherwise the call runs exactly as the per-call entry would.
+ * Which entry the call stands for:
+ *   dtype 0 (bf16) / 1 (fp16);  Y or mask_in set: lpg_fc_bf16_relu_bwd[_bits] (flags: accumulate +
+ *   kernel only; bias / dropout unused; scale), with db: ..._db (db_workspace as there);  else
+ *   lpg_fc_bf16 / lpg_fc_f16, with mask_out: lpg_fc_bf16_mask.
+ * workspace: lpg_fc16_workspace_bytes() bytes, 16-byte aligned (NULL = the per-call entry's path);
+ * LPG_FC_KERNEL(6) asks for the stream-K form explicitly (the default choice 0 takes it too). */
+typedef struct lpg_fc16_call {
+  int32_t dtype, flags;
+  int64_t M, N, K1, K2;
+  const uint16_t *A1, *W1, *A2, *W2;
+  int64_t lda1, ldw1, lda2, ldw2;
+  const float *bias;
+  uint16_t *C;
+  int64_t ldc;
+  float dropout_p;
+  uint64_t seed;
+  int64_t row_offset;
+  const int64_t *row_keys;
+  uint8_t *mask_out;
+  int64_t ldmo;
+  const uint16_t *Y;
+  int64_t ldy;
+  const uint8_t *mask_in;
+  int64_t ldmi;
+  float scale;
+  float *db;
+  void *db_workspace;
+} lpg_fc16_call;
+int64_t lpg_fc16_workspace_bytes(void);
+lpg_status lpg_fc16(const lpg_fc16_call *call, void *workspace, int64_t workspace_bytes, void *stream);
+
 /* bf16 weight gradient (c5 backward, reference train.py:128 loss.backward()
  * through GraphConv's lin_rel / lin_root): dW[n, k] = sum_r G[r, n] X[r, k],
  * G = dZ [R, N] and X = the layer input [R, K] as bf16 bit patterns

@@ -898,6 +898,283 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
 #endif
 }
 
+// ---- fc_bf16_sk: the pipelined kernel, persistent and stream-K -----------------
+//
+// One resident block per CU (G blocks) walks a contiguous range of the launch's (tile, k-tile)
+// iterations -- W = tiles x nk split into G nearly equal ranges -- instead of one tile per block.
+// Two costs of the one-tile-per-block grid go: (1) the partial last round (c5's 200 K rows are 24.4
+// rounds of 256 x 256 tiles, 100 K rows 12.2; fp16 inference at N = 1024 6.1) -- every block now does
+// W / G iterations; (2) the blocks' epilogues no longer start together, so their output stores
+// (HBM-bound when 256 CUs store at once) spread over other blocks' k loops.
+// A range boundary inside a tile splits its k loop: the block whose range ENDS in tile t computes
+// t's first k-tiles FIRST (before its whole tiles), writes the fp32 accumulators to a partial slot
+// and publishes a flag; the block whose range STARTS in t continues from those accumulators LAST,
+// then runs the epilogue.  The accumulation order of every output is the one-block kernel's (the
+// same MFMA chain, carried exactly through memory), so every kernel choice keeps giving the same
+// bits.  Hand-off: plain partial stores, every wave drains, barrier, one lane's agent-scope release
+// and relaxed agent-scope flag store; the consumer's one lane polls relaxed (bounded, s_sleep),
+// fences acquire at agent scope, then the block reads.  A consumer whose flag never comes (its
+// producer not resident) computes the whole tile itself -- the same bits, never a hang.
+struct SkArgs {
+  int64_t T;       // tiles (mt * nt)
+  int32_t G;       // persistent blocks (a multiple of 8)
+  int32_t spin;    // poll budget of a consumer before it computes the whole tile
+  uint32_t *flags; // [G + 1], zeroed before the launch: flags[v] = 1 once slot v holds a partial
+  float *part;     // [G + 1] slots of NW x FM x FN x 64 float4
+};
+
+// EPI: the epilogue flavours compiled into an instance (the others' fields are nulled at compile time,
+// so their code and registers go): 0 = plain / addend / dropout, 1 = the folded ReLU backward (Y or its
+// bits, with the bias column sums), 2 = the ReLU mask output
+//
+// Register budget: fc_bf16_p's body takes 255 VGPRs and ~60 SGPRs; inside a loop every argument it
+// reads would stay live across the epilogue (SGPR spills into VGPRs).  So each piece re-reads the
+// arguments from the kernarg segment through a laundered pointer (s_load per piece, nothing
+// loop-invariant to hoist), and every lane-dependent address derives from a laundered lane id.
+template <class E, int WM, int WN, int FM, int FN, bool RELU, int EPI>
+__global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_sk(FcB16Args a_arg, SkArgs sk_arg) {
+  typedef typename E::v8 v8;
+  typedef __attribute__((address_space(4))) const char kchar;
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  constexpr int A_BYTES = BM * BK * 2, TILE_BYTES = A_BYTES + BN * BK * 2;
+  constexpr int PA = BM / 8, PT = PA + BN / 8, PPW = PT / NW;
+  static_assert(PA % NW == 0 && PT % NW == 0, "whole pieces per wave");
+  static_assert(sizeof(FcB16Args) % 8 == 0, "SkArgs follows FcB16Args in the kernarg segment");
+  constexpr int EP_BYTES = NW * FM * 16 * (FN * 16 * 2 + 16);
+  constexpr int SMEM = 2 * TILE_BYTES > EP_BYTES ? 2 * TILE_BYTES : EP_BYTES;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+  (void)a_arg;
+  (void)sk_arg;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the arguments through a laundered kernarg pointer: re-read where used (before the k loop, again
+  // before the epilogue), so no field is live across the other phase
+  auto args = [&]() {
+    kchar *kp = (kchar *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    FcB16Args a = *(__attribute__((address_space(4))) const FcB16Args *)kp;
+    if constexpr (EPI != 1) a.my = nullptr, a.mi = nullptr, a.cs = nullptr;
+    if constexpr (EPI != 2) a.mo = nullptr;
+    return a;
+  };
+  auto skargs = [&]() {
+    kchar *kp = (kchar *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *(__attribute__((address_space(4))) const SkArgs *)(kp + sizeof(FcB16Args));
+  };
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  volatile uint32_t *word = reinterpret_cast<volatile uint32_t *>(smem);
+  f32x4 acc[FM][FN];
+
+  // The range's pieces in one loop (one copy of the k loop and of the epilogue): piece 0 -- if the
+  // range ends inside a tile -- is that tile's first k-tiles, a partial for block v + 1; then the
+  // whole tiles; last -- if the range starts inside a tile -- that tile's remaining k-tiles, from
+  // block v - 1's partial.
+  for (int q = 0;; ++q) {
+    const FcB16Args a = args();
+    const SkArgs sk = skargs();
+    int ln = tid & 63;
+    asm volatile("" : "+v"(ln));
+    const int fr = ln & 15, fq = ln >> 4;
+
+    // 32-bit index math (the host checks the iteration count); XCD-contiguous ranges: the blocks of
+    // one XCD (blockIdx % 8) take neighbouring ranges
+    const int nk1 = (int)(a.K1 / BK), nk = nk1 + (int)(a.K2 / BK);
+    const int G = sk.G, W = (int)sk.T * nk;
+    const int bid = (int)blockIdx.x, v = (bid % 8) * (G / 8) + bid / 8;
+    const int s = (int)((int64_t)W * v / G), e = (int)((int64_t)W * (v + 1) / G);  // e - s >= nk
+    const bool producer = e % nk != 0, consumer = s % nk != 0;
+    const int t_first = (s + nk - 1) / nk, t_end = e / nk;  // whole tiles [t_first, t_end)
+    const int npieces = (producer ? 1 : 0) + (t_end - t_first) + (consumer ? 1 : 0);
+    if (q >= npieces) break;
+    const bool is_prod = producer && q == 0, is_cons = consumer && q == npieces - 1;
+    const int t = is_prod ? t_end : is_cons ? s / nk : t_first + q - (producer ? 1 : 0);
+
+    // tile t -> (m0, n0) in fc_bf16_p's n-split order (t = its wgid; the host sets order 1)
+    const int mt = (int)a.mt, nt = (int)a.nt;
+    int mi = t / nt, ni = t % nt;
+    if (nt >= 2) {
+      const int nh = nt / 2, t0 = mt * nh;
+      if (t < t0) {
+        mi = t / nh;
+        ni = t % nh;
+      } else {
+        mi = (t - t0) / (nt - nh);
+        ni = nh + (t - t0) % (nt - nh);
+      }
+    }
+    const int64_t m0 = (int64_t)mi * BM, n0 = (int64_t)ni * BN;
+    const int ke = is_prod ? e % nk : nk;
+    auto slot = [&](int sl) {
+      return reinterpret_cast<f32x4 *>(sk.part) + ((int64_t)(sl * NW + wave) * (FM * FN)) * 64 + ln;
+    };
+
+    // the carried accumulators, or zeros
+    int kb = 0;
+    bool have = false;
+    if (is_cons) {
+      __syncthreads();  // smem free (the last epilogue's image reads are done)
+      if (tid == 0) {
+        uint32_t got = 0u;
+        for (int i = 0; i < sk.spin; ++i) {
+          if (__hip_atomic_load(sk.flags + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+            got = 1u;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(8);
+        }
+        if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        *word = got;
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      have = *word != 0u;  // (a producer that never published: the whole tile here, the same bits)
+      kb = have ? s % nk : 0;
+    }
+    if (have) {
+      const f32x4 *P = slot(v);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = P[(i * FN + j) * 64];
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    // k-tiles [kb, ke) (fc_bf16_p's pipeline: barrier mid-tile, reads one 32-k step ahead, DMA pieces
+    // and reads placed one per MFMA)
+    {
+      uint32_t vo[PPW];
+#pragma unroll
+      for (int p = 0; p < PPW; ++p) {
+        const int qq = wave + NW * p;
+        const int row = (qq < PA ? qq : qq - PA) * 8 + (ln >> 3);
+        vo[p] = (uint32_t)((row * (qq < PA ? a.lda1 : a.ldw1) + swz(row, ln & 7) * 8) * 2);
+      }
+      const int64_t kp1 = a.K1 > 0 ? a.K1 : BK, kp2 = a.K2 > 0 ? a.K2 : BK;
+      const int64_t mrows = a.M - m0 < BM ? a.M - m0 : BM;
+      const int64_t ncols = a.N - n0 < BN ? a.N - n0 : BN;
+      const uint64_t pa1 = (uint64_t)(a.A1 + m0 * a.lda1), pw1 = (uint64_t)(a.W1 + n0 * a.ldw1);
+      const uint64_t pa2 = a.A2 ? (uint64_t)(a.A2 + m0 * a.lda1) : pa1;
+      const uint64_t pw2 = a.W2 ? (uint64_t)(a.W2 + n0 * a.ldw1) : pw1;
+      const uint32_t na1 = (uint32_t)(((mrows - 1) * a.lda1 + kp1) * 2), na2 = (uint32_t)(((mrows - 1) * a.lda1 + kp2) * 2);
+      const uint32_t nw1 = (uint32_t)(((ncols - 1) * a.ldw1 + kp1) * 2), nw2 = (uint32_t)(((ncols - 1) * a.ldw1 + kp2) * 2);
+      auto stage = [&](int b, int tk) {
+        const bool ok = tk < ke;
+        tk = ok ? tk : ke - 1;
+        const bool p2 = tk >= nk1;
+        const int kk = p2 ? tk - nk1 : tk;
+        unsigned char *base = smem + b * TILE_BYTES;
+        const uint32_t na = ok ? (p2 ? na2 : na1) : 0u, nw = ok ? (p2 ? nw2 : nw1) : 0u;
+#pragma unroll
+        for (int p = 0; p < PPW; ++p) {
+          const int qq = wave + NW * p;
+          if (p < PA / NW)
+            dma16(p2 ? pa2 : pa1, na, base + qq * 1024, vo[p], kk * (BK * 2));
+          else
+            dma16(p2 ? pw2 : pw1, nw, base + qq * 1024, vo[p], kk * (BK * 2));
+        }
+      };
+      auto rd = [&](int b, int st, v8(&av)[FM], v8(&bv)[FN]) {
+        const unsigned char *As = smem + b * TILE_BYTES;
+        const unsigned char *Bs = As + A_BYTES;
+        const int chunk = st * 4 + fq;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = wm * FM * 16 + i * 16 + fr;
+          av[i] = *reinterpret_cast<const v8 *>(As + row * 128 + swz(row, chunk) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * FN * 16 + j * 16 + fr;
+          bv[j] = *reinterpret_cast<const v8 *>(Bs + row * 128 + swz(row, chunk) * 16);
+        }
+      };
+      auto mma = [&](const v8(&av)[FM], const v8(&bv)[FN]) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i) acc[i][j] = E::mma(bv[j], av[i], acc[i][j]);
+      };
+      auto barrier = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      constexpr int NR = FM + FN, NM = FM * FN;
+      const int n = ke - kb;
+      v8 a0[FM], b0[FN], a1[FM], b1[FN];
+      __syncthreads();  // the previous piece's epilogue / partial reads of smem are done everywhere
+      stage(0, kb);
+      barrier();
+      if (n > 1) stage(1, kb + 1);
+      rd(0, 0, a0, b0);
+      for (int j = 0; j + 1 < n; ++j) {
+        const int b = j & 1;
+        rd(b, 1, a1, b1);
+        mma(a0, b0);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+        barrier();
+        stage(b, kb + j + 2);
+        rd(b ^ 1, 0, a0, b0);
+        mma(a1, b1);
+#pragma unroll
+        for (int k = 0; k < PPW; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        if constexpr (NM > PPW + NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - PPW - NR, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      rd((n - 1) & 1, 1, a1, b1);
+      mma(a0, b0);
+      mma(a1, b1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+
+    if (is_prod) {  // the partial for block v + 1: stores drained by every wave, then one release + flag
+      const SkArgs sk2 = skargs();
+      f32x4 *P = reinterpret_cast<f32x4 *>(sk2.part) + ((int64_t)((v + 1) * NW + wave) * (FM * FN)) * 64 + (tid & 63);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) P[(i * FN + j) * 64] = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(sk2.flags + v + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      int ln2 = tid & 63;
+      asm volatile("" : "+v"(ln2));
+      epilogue_bf16_ti<E, FM, FN, RELU>(args(), acc, smem, wave, ln2, m0 + wm * FM * 16, n0 + wn * FN * 16);
+    }
+  }
+#endif
+}
+
 // ---- weight gradient dW = G^T X in bf16 (fp32 out) ---------------------------
 //
 // dW[n, k] = sum_r G[r, n] X[r, k] (G = dZ [R, N], X = the layer input [R, K],
@@ -1154,6 +1431,44 @@ lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
   return LPG_OK;
 }
 
+// fc_bf16_sk's workspace: the flags ([G + 1] words at the start, padded to 16 B, zeroed per launch), then
+// G + 1 partial slots of one 256 x 256 fp32 tile each
+constexpr int64_t kSkSlotBytes = 256 * 256 * 4;
+inline int sk_blocks() { return device_cus() / 8 * 8; }
+inline int64_t sk_flag_bytes(int G) { return ((int64_t)(G + 1) * 4 + 255) / 256 * 256; }
+inline int64_t sk_workspace_bytes() { return sk_flag_bytes(sk_blocks()) + (int64_t)(sk_blocks() + 1) * kSkSlotBytes; }
+
+// whether fc_bf16_sk can take the call: a large enough 16-byte aligned workspace and at least one
+// 256 x 256 tile per persistent block (so every range covers a whole tile: no chain of partials)
+bool sk_ok(const FcB16Args &a, const void *ws, int64_t ws_bytes) {
+  // (the mask flavours -- the folded ReLU backward, the ReLU mask output -- do not fit the register
+  // budget of the persistent form yet: they run the one-tile-per-block kernel)
+  if (a.my || a.mi || a.cs || a.mo) return false;
+  const int G = sk_blocks();
+  const int64_t T = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  return ws && aligned16(ws) && G >= 8 && T >= G && (a.K1 + a.K2) / BK >= 1 && ws_bytes >= sk_workspace_bytes() &&
+         T * ((a.K1 + a.K2) / BK) < ((int64_t)1 << 31) / 1024;  // 32-bit iteration index math in the kernel
+}
+
+template <class E, int WM, int WN, int FM, int FN>
+lpg_status launch_bf16_sk(FcB16Args a, bool relu, hipStream_t s, void *ws) {
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  static_assert(BM * BN * 4 == kSkSlotBytes, "one slot per 256 x 256 tile");
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int G = sk_blocks();
+  SkArgs sk{a.mt * a.nt, G, 1 << 16, static_cast<uint32_t *>(ws),
+            reinterpret_cast<float *>(static_cast<unsigned char *>(ws) + sk_flag_bytes(G))};
+  LPG_HIP(hipMemsetAsync(ws, 0, sk_flag_bytes(G), s));
+  const dim3 grid((unsigned)G), block(64 * WM * WN);
+  if (relu)
+    hipLaunchKernelGGL((fc_bf16_sk<E, WM, WN, FM, FN, true, 0>), grid, block, 0, s, a, sk);
+  else
+    hipLaunchKernelGGL((fc_bf16_sk<E, WM, WN, FM, FN, false, 0>), grid, block, 0, s, a, sk);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
 // whether fc_bf16_p can take these operands: one offset set for both k phases, 32-bit offsets
 bool p_ok(const FcB16Args &a) {
   if (a.K1 == 0) return false;
@@ -1170,7 +1485,9 @@ bool p_ok(const FcB16Args &a) {
 // Every choice computes the same bits.  Measured at the c5 shapes
 // (profiles/r02_kbench_bf16.log, r02_kbench_fck10.log): fc_bf16_p 1212-1300 TF/s vs hipBLASLt
 // 1248-1268, fc_fwd_bf16 256^2 1033; wgrad_bf16 1172-1222 vs hipBLASLt's bf16-output GEMM 924-1004.
-constexpr int kKernels = 5;
+// 6 = the persistent stream-K form (fc_bf16_sk) when the call carries its workspace (lpg_fc16), else
+// choice 0; choice 0 takes it too whenever a workspace is given.
+constexpr int kKernels = 6;
 
 int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
   const int64_t tiles = ((N + 255) / 256) * ((K + 255) / 256);
@@ -1192,7 +1509,8 @@ int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
 namespace lpg {
 namespace {
 template <class E>
-lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant, int64_t *cs_rows = nullptr);
+lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int variant, int64_t *cs_rows = nullptr,
+                             void *skws = nullptr, int64_t skws_bytes = 0);
 
 // dst[c, r] = src[r, c] for bf16 through a 64 x 64 LDS tile, 16-byte global accesses both ways
 // (the input gradients' W^T; torch's strided copy ran these at ~0.5 TB/s).  R, C multiples of 8.
@@ -1391,7 +1709,7 @@ static lpg_status fc16_entry(const char *name, int64_t M, int64_t N, int64_t K1,
                                   const uint16_t *W2, int64_t ldw2, const float *bias, uint16_t *C, int64_t ldc,
                                   int32_t flags, float dropout_p, uint64_t seed, int64_t row_offset,
                                   const int64_t *row_keys, void *stream, uint8_t *mask = nullptr,
-                                  int64_t ldm = 0) {
+                                  int64_t ldm = 0, void *skws = nullptr, int64_t skws_bytes = 0) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "%s: negative size", name);
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(C != nullptr && ldc >= N, "%s: bad C/ldc", name);
@@ -1418,7 +1736,7 @@ static lpg_status fc16_entry(const char *name, int64_t M, int64_t N, int64_t K1,
   LPG_REQUIRE(lda1 % 8 == 0 && ldw1 % 8 == 0 && (K2 == 0 || (lda2 % 8 == 0 && ldw2 % 8 == 0)) &&
                   (K1 == 0 || (aligned16(A1) && aligned16(W1))) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
               "%s: A/W must be 16-byte aligned with leading dimensions multiple of 8", name);
-  return fc_bf16_dispatch<E>(a, flags & 1, as_stream(stream), kernel);
+  return fc_bf16_dispatch<E>(a, flags & 1, as_stream(stream), kernel, nullptr, skws, skws_bytes);
 }
 
 extern "C" lpg_status lpg_fc_bf16(int64_t M, int64_t N, int64_t K1, const uint16_t *A1, int64_t lda1,
@@ -1463,7 +1781,8 @@ static lpg_status relu_bwd_entry(const char *name, int64_t M, int64_t N, int64_t
                                  int64_t lda1, const uint16_t *W1, int64_t ldw1, int64_t K2, const uint16_t *A2,
                                  int64_t lda2, const uint16_t *W2, int64_t ldw2, uint16_t *C, int64_t ldc,
                                  int32_t flags, const uint16_t *Y, int64_t ldy, const uint8_t *mask, int64_t ldm,
-                                 float scale, void *stream, float *db = nullptr, void *workspace = nullptr) {
+                                 float scale, void *stream, float *db = nullptr, void *workspace = nullptr,
+                                 void *skws = nullptr, int64_t skws_bytes = 0) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "%s: negative size", name);
   if (db) {
     LPG_REQUIRE(workspace && aligned16(workspace), "%s: db needs a 16-byte aligned workspace", name);
@@ -1492,7 +1811,7 @@ static lpg_status relu_bwd_entry(const char *name, int64_t M, int64_t N, int64_t
   hipStream_t s = as_stream(stream);
   a.cs = db ? static_cast<float *>(workspace) : nullptr;
   int64_t cs_rows = 0;
-  const lpg_status st = fc_bf16_dispatch<EBf16>(a, false, s, kernel, &cs_rows);  // (every kernel's epilogue takes the fold)
+  const lpg_status st = fc_bf16_dispatch<EBf16>(a, false, s, kernel, &cs_rows, skws, skws_bytes);  // (every kernel's epilogue takes the fold)
   if (st != LPG_OK || !db) return st;
   return colsum_bf16_from(M, N, C, ldc, cs_rows, static_cast<float *>(workspace), db, s);
 }
@@ -1542,6 +1861,34 @@ extern "C" lpg_status lpg_fc_bf16_relu_bwd_bits_db(int64_t M, int64_t N, int64_t
                         flags, nullptr, 0, mask, ldm, scale, stream, db, workspace);
 }
 
+extern "C" int64_t lpg_fc16_workspace_bytes(void) { return sk_workspace_bytes(); }
+
+extern "C" lpg_status lpg_fc16(const lpg_fc16_call *c, void *workspace, int64_t workspace_bytes, void *stream) {
+  LPG_REQUIRE(c != nullptr, "lpg_fc16: NULL call");
+  LPG_REQUIRE(c->dtype == 0 || c->dtype == 1, "lpg_fc16: dtype %d (0 = bf16, 1 = fp16)", c->dtype);
+  LPG_REQUIRE(!workspace || workspace_bytes >= sk_workspace_bytes(), "lpg_fc16: workspace of %lld bytes, need %lld",
+              (long long)workspace_bytes, (long long)sk_workspace_bytes());
+  if (c->Y || c->mask_in) {
+    LPG_REQUIRE(c->dtype == 0, "lpg_fc16: the folded ReLU backward is a bf16 training path");
+    LPG_REQUIRE(!(c->Y && c->mask_in), "lpg_fc16: Y or mask_in, not both");
+    return relu_bwd_entry(c->db ? (c->Y ? "lpg_fc_bf16_relu_bwd_db" : "lpg_fc_bf16_relu_bwd_bits_db")
+                                : (c->Y ? "lpg_fc_bf16_relu_bwd" : "lpg_fc_bf16_relu_bwd_bits"),
+                          c->M, c->N, c->K1, c->A1, c->lda1, c->W1, c->ldw1, c->K2, c->A2, c->lda2, c->W2, c->ldw2,
+                          c->C, c->ldc, c->flags, c->Y, c->ldy, c->mask_in, c->ldmi, c->scale, stream, c->db,
+                          c->db_workspace, workspace, workspace_bytes);
+  }
+  if (c->dtype == 1) {
+    LPG_REQUIRE(!c->mask_out, "lpg_fc16: the ReLU mask output is a bf16 training path");
+    return fc16_entry<EF16>("lpg_fc_f16", c->M, c->N, c->K1, c->A1, c->lda1, c->W1, c->ldw1, c->K2, c->A2, c->lda2,
+                            c->W2, c->ldw2, c->bias, c->C, c->ldc, c->flags, c->dropout_p, c->seed, c->row_offset,
+                            c->row_keys, stream, nullptr, 0, workspace, workspace_bytes);
+  }
+  return fc16_entry<EBf16>(c->mask_out ? "lpg_fc_bf16_mask" : "lpg_fc_bf16", c->M, c->N, c->K1, c->A1, c->lda1, c->W1,
+                           c->ldw1, c->K2, c->A2, c->lda2, c->W2, c->ldw2, c->bias, c->C, c->ldc, c->flags,
+                           c->dropout_p, c->seed, c->row_offset, c->row_keys, stream, c->mask_out, c->ldmo, workspace,
+                           workspace_bytes);
+}
+
 namespace lpg {
 namespace {
 // rows [r, M) of a as their own call: operands, output, mask rows and dropout keys offset by r
@@ -1563,14 +1910,22 @@ FcB16Args rows_from(const FcB16Args &a, int64_t r) {
 template <class E>
 // cs_rows: the leading rows whose column-sum partials the launches wrote (a.cs: fc_bf16_p's epilogue
 // only; the other kernels never see a.cs)
-lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel, int64_t *cs_rows) {
+lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel, int64_t *cs_rows, void *skws,
+                             int64_t skws_bytes) {
   if (cs_rows) *cs_rows = 0;
   float *const cs = a.cs;
   a.cs = nullptr;
   if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<E, 2, 2, 4, 4>(a, relu, s);  // 128 x 128
+  if ((kernel == 0 || kernel == 6) && p_ok(a) && sk_ok(a, skws, skws_bytes)) {
+    // the persistent stream-K form of the pipelined kernel (with a workspace), n-split tile order
+    a.order = 1;
+    a.cs = cs;
+    if (cs_rows && cs) *cs_rows = a.M;
+    return launch_bf16_sk<E, 2, 4, 8, 4>(a, relu, s, skws);
+  }
   if ((kernel == 0 || kernel >= 3) && p_ok(a)) {
-    a.order = kernel == 0 ? 1 : kernel == 5 ? 2 : 0;  // the default in the n-split order (1-2 % at the c5 shapes)
-    if (kernel == 0 || kernel == 4 || kernel == 5) {
+    a.order = kernel == 0 || kernel == 6 ? 1 : kernel == 5 ? 2 : 0;  // the default in the n-split order (1-2 % at the c5 shapes)
+    if (kernel == 0 || kernel == 4 || kernel == 5 || kernel == 6) {
       // The last round of 256 x 256 tiles (one block per CU) is usually partial: c5's 200 K rows are 24
       // rounds + 41 % of one, 100 K rows 12 + 21 %, and the CUs without a tile idle for a whole block
       // time.  Those rows run as a second launch on 128 x 128 tiles (4 x the blocks, 2 per CU) -- the

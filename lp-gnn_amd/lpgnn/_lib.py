@@ -41,6 +41,8 @@ HEADER_SYMBOLS = (
     "lpg_fc_bf16_relu_bwd_bits",
     "lpg_fc_bf16_relu_bwd_db",
     "lpg_fc_bf16_relu_bwd_bits_db",
+    "lpg_fc16_workspace_bytes",
+    "lpg_fc16",
     "lpg_colsum_bf16",
     "lpg_transpose_bf16",
     "lpg_wgrad_bf16_workspace_bytes",
@@ -100,6 +102,16 @@ class LpgCsr(ctypes.Structure):
                 ("rowptr", c_p), ("col", c_p), ("val", c_p)]
 
 
+class LpgFc16Call(ctypes.Structure):
+    """include/lpgnn.h lpg_fc16_call: every 16-bit FC form in one call (lpg_fc16)."""
+    _fields_ = [("dtype", c_i32), ("flags", c_i32), ("M", c_i64), ("N", c_i64), ("K1", c_i64), ("K2", c_i64),
+                ("A1", c_p), ("W1", c_p), ("A2", c_p), ("W2", c_p), ("lda1", c_i64), ("ldw1", c_i64),
+                ("lda2", c_i64), ("ldw2", c_i64), ("bias", c_p), ("C", c_p), ("ldc", c_i64),
+                ("dropout_p", ctypes.c_float), ("seed", ctypes.c_uint64), ("row_offset", c_i64), ("row_keys", c_p),
+                ("mask_out", c_p), ("ldmo", c_i64), ("Y", c_p), ("ldy", c_i64), ("mask_in", c_p), ("ldmi", c_i64),
+                ("scale", ctypes.c_float), ("db", c_p), ("db_workspace", c_p)]
+
+
 _lib = None
 
 
@@ -142,6 +154,10 @@ def lib() -> ctypes.CDLL:
     L.lpg_fc_bf16.argtypes = L.lpg_fc_f32.argtypes
     L.lpg_fc_f16.argtypes = L.lpg_fc_f32.argtypes
     L.lpg_fc_f16.restype = c_i32
+    L.lpg_fc16_workspace_bytes.argtypes = []
+    L.lpg_fc16_workspace_bytes.restype = c_i64
+    L.lpg_fc16.argtypes = [ctypes.POINTER(LpgFc16Call), c_p, c_i64, c_p]
+    L.lpg_fc16.restype = c_i32
     L.lpg_fc_bf16_relu_bwd.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
                                        c_p, c_i64, c_i32, c_p, c_i64, ctypes.c_float, c_p]
     L.lpg_fc_bf16_relu_bwd.restype = c_i32

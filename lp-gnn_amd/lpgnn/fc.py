@@ -21,6 +21,8 @@ runs in lpg_linear_small_bwd_f32.  Tolerance-level parity for gradients.
 """
 from __future__ import annotations
 
+import ctypes
+
 
 import torch
 import torch.nn.functional as F
@@ -418,6 +420,24 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
         _lib.check(st, entry)
         return C
     entry = "lpg_fc_f16" if f16 else "lpg_fc_bf16"
+    if mask_out is None and not small and kernel in (0, 6):
+        # the persistent stream-K form with its workspace (lpg_fc16): the same bits, no partial last
+        # round, spread epilogues (fc_bf16.hip fc_bf16_sk); the call falls back where it does not apply
+        call = _lib.LpgFc16Call(
+            dtype=1 if f16 else 0, flags=flags, M=M, N=N, K1=A1.shape[1], K2=K2, A1=A1.data_ptr(), W1=W1.data_ptr(),
+            A2=None if A2 is None else A2.data_ptr(), W2=None if W2 is None else W2.data_ptr(), lda1=A1.stride(0),
+            ldw1=W1.stride(0), lda2=A2.stride(0) if K2 else 0, ldw2=W2.stride(0) if K2 else 0,
+            bias=None if bias is None else bias.data_ptr(), C=C.data_ptr(), ldc=C.stride(0),
+            dropout_p=float(dropout_p), seed=int(seed) & (2**64 - 1), row_offset=int(row_offset),
+            row_keys=_lib.ptr(row_keys), scale=1.0)
+        ws = _workspace(L.lpg_fc16_workspace_bytes(), A1.device)
+        with torch.cuda.device(A1.device):
+            tok = TIMER.start(("fc", M, N, A1.shape[1] + K2,
+                               key or (("relu-" if relu else "lin-") + ("f16" if f16 else "bf16"))))
+            st = L.lpg_fc16(ctypes.byref(call), ws.data_ptr(), ws.numel() * 4, _lib.stream_of(A1))
+            TIMER.stop(tok)
+        _lib.check(st, "lpg_fc16")
+        return C
     margs = ()
     if mask_out is not None:
         if (f16 or not relu or N % 8 or C.stride(0) % 8 or C.data_ptr() % 16 or mask_out.dtype != torch.uint8

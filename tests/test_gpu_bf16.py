@@ -45,7 +45,7 @@ def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
 
 # per-call kernel choices of lpg_fc_bf16 (LPG_FC_KERNEL, include/lpgnn.h): 1 = 128 x 128,
 # 2 = 256 x 256, 3 = the pipelined transposed-fragment kernel (the default from 4096 rows)
-KERNELS = (1, 2, 3, 4, 5)
+KERNELS = (1, 2, 3, 4, 5, 6)
 
 
 def _f64_ulp_check(out, A, W, P, b, relu, A2=None, W2=None):
@@ -556,3 +556,37 @@ def test_gcn_fc_bf16_relu_bits_identical():
     assert out[True][0] == out[False][0]
     for k, v in out[True][1].items():
         assert torch.equal(v, out[False][1][k]), k
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K1,K2,relu,drop,acc", [
+    (16384 + 77, 1024, 1024, 0, False, 0.0, False),   # fp16-inference shape family, ragged rows
+    (20000, 1024, 512, 512, True, 0.2, False),         # two k phases, ReLU + dropout
+    (30011, 2048, 256, 0, True, 0.0, True),            # accumulate addend, many boundaries
+    (8192, 2048, 64, 64, False, 0.0, False),           # nk = 2: ranges of a few k-tiles, most tiles split
+])
+def test_fc16_stream_k_identical(dt, M, N, K1, K2, relu, drop, acc):
+    """lpg_fc16's persistent stream-K form (fc_bf16_sk: the (tile, k-tile) iterations split into one
+    range per CU, a tile cut by a range boundary carrying its fp32 accumulators from block to block
+    through the workspace) gives exactly the bits of the one-tile-per-block pipelined kernel (choice 3)
+    -- the same MFMA chain per output -- with dropout keyed the same, an addend, two k phases, ragged
+    rows; and within one 16-bit ulp of fp64 of the same operands."""
+    from lpgnn.fc import fc_forward_bf16
+
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert ((M + 255) // 256) * ((N + 255) // 256) >= cus // 8 * 8  # the stream-K form applies
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    r = lambda *s: torch.randn(*s, device=DEV, generator=g)  # noqa: E731
+    A1, W1 = r(M, K1).to(dt), (r(N, K1) * 0.05).to(dt)
+    A2, W2 = (r(M, K2).to(dt), (r(N, K2) * 0.05).to(dt)) if K2 else (None, None)
+    b = r(N) * 0.1
+    P = r(M, N).to(dt) if acc else None
+    outs = []
+    for k in (6, 3, 0):
+        out = P.clone() if acc else None
+        outs.append(fc_forward_bf16(A1, W1, A2, W2, b, relu, drop, seed=77, out=out, accumulate=acc, kernel=k))
+    assert torch.equal(outs[0], outs[1]), int((outs[0] != outs[1]).sum())
+    assert torch.equal(outs[2], outs[1])
+    if dt == torch.bfloat16 and drop == 0.0:
+        _f64_ulp_check(outs[0].cpu(), A1.cpu(), W1.cpu(), None if P is None else P.cpu(), b.cpu(), relu,
+                       None if A2 is None else A2.cpu(), None if W2 is None else W2.cpu())
