@@ -123,7 +123,7 @@ class GraphConvTwoDirection(nn.Module):
                                        relu, dropout, fold_in, opts, feeds_conv)
         tdc = getattr(edge_index, "two_direction_conv", None)  # row-partitioned multi-GPU adjacency
         if tdc is not None and edge_weight is None:
-            out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout, opts)
+            out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout, opts, fold_in)
             if out is not None:
                 return out
         l2r, r2l = edge_index.t(), edge_index
@@ -227,7 +227,7 @@ class GCN_FC(GCNBase):
                                                 self.lin_left, self.lin_right, dp, fold_in=True, opts=opts)
             else:
                 out = part_heads(left, right, last.left2right, last.right2left, self.lin_left, self.lin_right, dp,
-                                 opts)
+                                 opts, fold_in=True)
                 if out is None:  # not applicable on this adjacency: the separate path
                     left, right = last(left, right, edge_index, relu=True, dropout=dp, opts=opts)
         if out is not None:

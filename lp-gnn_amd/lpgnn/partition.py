@@ -543,15 +543,37 @@ class _PartTwoDirection(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                opts=None):
+                opts=None, prev=None):
         left_new, right_new, saved, _ = _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r,
                                                            w_rel_r2l, b_r2l, w_root_r2l, relu, dropout, opts=opts)
+        _link_prev(ctx, prev)
         ctx.save_for_backward(*saved)
         return left_new, right_new
 
     @staticmethod
     def backward(ctx, g_left, g_right):
-        return _part_backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None,)
+        return _part_backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None, None)
+
+
+def _link_prev(ctx, prev):
+    """prev: conv1's node whose weight gradients this layer's input-gradient GEMMs compute (the
+    partitioned conv1 fold, _part_backward_core)."""
+    ctx.wgk_prev = prev
+    if prev is not None:
+        prev.wgk_folded = True
+
+
+def foldable_producer(left, right, opts):
+    """conv1's partitioned node (fp32, ReLU, no dropout, narrow LP-feature inputs that need no
+    gradient) when it produced (left, right) and the options fold its weight gradients into the next
+    layer's x3 input-gradient GEMMs (options.fold_conv1_wgrad, lpg_fc_x3_relu_wgrad_f32); else None."""
+    g = left.grad_fn
+    if (g is None or g is not right.grad_fn or not isinstance(g, _PartTwoDirection._backward_cls)
+            or not torch.is_grad_enabled() or not getattr(g, "small_relu", False)):
+        return None
+    if not (opts.fold_conv1_wgrad and opts.arith == "x3" and g.opts.arith == "x3") or any(g.needs_input_grad[:2]):
+        return None
+    return g
 
 
 def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu,
@@ -613,6 +635,10 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
         logits = (logit_l, logit_r)
     ctx.padj, ctx.relu, ctx.opts = padj, relu, opts
     ctx.scale = _fc.dropout_scale(dropout)
+    # conv1's shape (narrow LP features, aggregates kept, ReLU without dropout): its weight gradients
+    # can come out of the next layer's input-gradient GEMMs (foldable_producer)
+    ctx.small_relu = (relu and dropout == 0 and agg_l is not None and agg_r is not None
+                      and agg_l.shape[1] + left.shape[1] <= 16 and agg_r.shape[1] + right.shape[1] <= 16)
     ctx.has_b = (b_l2r is not None, b_r2l is not None)
     return left_new, right_new, (left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r,
                                  w_rel_r2l, w_root_r2l), logits
@@ -636,6 +662,19 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     ex = ctx.padj.ex
     A, AT = ctx.padj.local.fwd, ctx.padj.local.bwd
     n_own = ex.n_own
+    pre = getattr(ctx, "folded_wgk", None)
+    if getattr(ctx, "wgk_folded", False) and pre is not None:
+        # conv1 whose weight gradients the next layer computed in its input-gradient GEMMs: no pass over
+        # its output gradients and no exchange (every rank takes this path alike)
+        ctx.folded_wgk = None
+        (dw_rel_l2r, dw_root_l2r, db_l2r), (dw_rel_r2l, dw_root_r2l, db_r2l) = pre
+        keep = lambda t, i, has=True: t if (need[i] and has) else None  # noqa: E731
+        return (None, None, None, keep(dw_rel_l2r, 3), keep(db_l2r, 4, ctx.has_b[0]), keep(dw_root_l2r, 5),
+                keep(dw_rel_r2l, 6), keep(db_r2l, 7, ctx.has_b[1]), keep(dw_root_r2l, 8), None, None)
+    prev = getattr(ctx, "wgk_prev", None)
+    ctx.wgk_prev = None
+    if prev is not None and dz is not None and need[0] and need[1]:
+        return _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward)
     if dz is None:
         if g_right is None:
             g_right = torch.zeros_like(right_new)
@@ -724,6 +763,76 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
 
 
+def _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward):
+    """_part_backward_core of the layer after conv1 (gradients through its ReLU/dropout given, dz) with
+    conv1's weight gradients folded into this layer's input-gradient GEMMs (lpg_fc_x3_relu_wgrad_f32:
+    the masked tile times conv1's 8 + 8 inputs, never storing conv1's output gradient).
+
+    Variables: conv1's output gradient on an owned variable is the source-side term of right2left summed
+    over every rank that touches it, plus the root term of left2right.  The source-side term is
+    re-associated, (A^T dZ_l) W_rel: T = A^T dZ_l over the local variables, its halo rows REDUCED to
+    their owners first (sum over ranks, the exchange conv1's own backward would have done on the
+    product), then one fused GEMM over the owned rows.  Constraints are local: conv.py's fold as is.
+    conv1's node receives zero-stride gradients and returns the handed weight gradients."""
+    from . import fc as _fc
+
+    left, right, agg_l, agg_r, left_new, right_new, w_rel_l2r, w_root_l2r, w_rel_r2l, w_root_r2l = saved
+    ex = ctx.padj.ex
+    A, AT = ctx.padj.local.fwd, ctx.padj.local.bwd
+    n_own = ex.n_own
+    dz_l, db_r2l, dz_r, db_l2r = dz
+    p_left, p_right, p_agg_l, p_agg_r, p_left_new, p_right_new = prev.saved_tensors[:6]
+    dw_rel_r2l, dw_root_r2l = (wgf(dz_l, agg_l) if need[6] else None), (wgf(dz_l, left) if need[8] else None)
+
+    # conv1's left2right (owned variables): T's halo partials to the owners, then the fused GEMM
+    T = spmm_forward(AT, dz_l)
+    T_own = ex.start_reduce(T, inplace=True).finish()
+
+    def fused(G1, W1, G2, W2, addend, y, x1, x2, two_pass):
+        r = _fc.input_grad_relu_wgrad(G1, W1, G2, W2, addend, y, x1, x2)
+        if r is None:  # operands the fused kernel does not take: the stored gradient, then conv1's pass
+            r = _fc.relu_wgrad_smallk(two_pass(), y, 1.0, x1, x2, True)
+        return r
+
+    def g_right_own():
+        g = igf(T_own, w_rel_r2l)
+        return igf(dz_r, w_root_l2r, out=g, accumulate=True)
+    wk_r = fused(T_own, w_rel_r2l, dz_r, w_root_l2r, None, p_right_new[:n_own], p_agg_r[:n_own], p_right[:n_own],
+                 g_right_own)
+
+    # this layer's left2right weight gradients and conv1's right2left (constraints, local)
+    f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
+    from .conv import _src_first
+
+    use_t = _src_first(AT, f_out, f_in, 4) or agg_r is None
+    rel_from_t = need[3] and (agg_r is None or (use_t and A.n_rows < n_own))
+    dw_rel_l2r = wgf(dz_r, agg_r[:n_own]) if need[3] and not rel_from_t else None
+    dw_root_l2r = wgf(dz_r, right[:n_own]) if need[5] else None
+    full = torch.empty((right.shape[0], f_out if use_t else f_in), dtype=torch.float32, device=left.device)
+    if use_t:
+        full[:n_own] = dz_r
+    else:
+        igf(dz_r, w_rel_l2r, out=full[:n_own])
+    ex.start_broadcast_(full).finish()
+    t = spmm_forward(A, full)
+    if use_t:
+        if rel_from_t:
+            dw_rel_l2r = wgf(t, left)
+
+        def g_left():
+            g = igf(dz_l, w_root_r2l)
+            return igf(t, w_rel_l2r, out=g, accumulate=True)
+        wk_l = fused(t, w_rel_l2r, dz_l, w_root_r2l, None, p_left_new, p_agg_l, p_left, g_left)
+    else:
+        def g_left():
+            return igf(dz_l, w_root_r2l, out=t.clone(), accumulate=True)
+        wk_l = fused(dz_l, w_root_r2l, None, None, t, p_left_new, p_agg_l, p_left, g_left)
+    prev.folded_wgk = (wk_r, wk_l)
+    g_l = torch.zeros((), dtype=left.dtype, device=left.device).expand(left.shape)
+    g_r = torch.zeros((), dtype=right.dtype, device=right.device).expand(right.shape)
+    return (g_l, g_r, None, dw_rel_l2r, db_l2r, dw_root_l2r, dw_rel_r2l, db_r2l, dw_root_r2l, None, None)
+
+
 class _PartTwoDirectionHeads(torch.autograd.Function):
     """The last hidden layer + heads on a partition (conv._TwoDirectionHeads'
     twin).  Backward: the halo rows' LOGIT gradients (3 wide) are reduced to
@@ -734,13 +843,14 @@ class _PartTwoDirectionHeads(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                wh_l, bh_l, wh_r, bh_r, opts=None):
+                wh_l, bh_l, wh_r, bh_r, opts=None, prev=None):
         import functools
 
         from . import fc as _fc
         from .options import DEFAULT
 
         opts = DEFAULT if opts is None else opts
+        _link_prev(ctx, prev)
         fcf = functools.partial(_fc.fc_forward, arith=opts.arith)
         left_new, right_new, saved, logits = _part_forward_core(
             ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
@@ -771,7 +881,7 @@ class _PartTwoDirectionHeads(torch.autograd.Function):
         core = _part_backward_core(ctx, saved, need, None, None, dz=(dz_l, db_r2l, dz_r, db_l2r))
         keep = lambda t, i, has=True: t if (need[i] and has) else None
         return (*core, keep(dwh_l, 11), keep(dbh_l, 12, ctx.heads_b[0]), keep(dwh_r, 13),
-                keep(dbh_r, 14, ctx.heads_b[1]), None)
+                keep(dbh_r, 14, ctx.heads_b[1]), None, None)
 
 
 class PartitionedCSR:
@@ -797,24 +907,34 @@ class PartitionedCSR:
     def device(self):
         return self.local.device
 
-    def two_direction_conv(self, left, right, left2right, right2left, relu=False, dropout=0.0, opts=None):
-        """GraphConvTwoDirection.forward on this partition (one autograd node)."""
+    def two_direction_conv(self, left, right, left2right, right2left, relu=False, dropout=0.0, opts=None,
+                           fold_in=False):
+        """GraphConvTwoDirection.forward on this partition (one autograd node).  ``fold_in``: (left,
+        right) feed nothing but this layer (GCN_FC's chain): if conv1 produced them, its weight
+        gradients come out of this layer's input-gradient GEMMs."""
         if self.orient != "cons" or left.dtype != torch.float32 or _local_spmm is not _product_spmm:
             return None  # generic per-direction path (oracle tests, bf16)
+        from .options import DEFAULT
+
+        prev = foldable_producer(left, right, opts or DEFAULT) if fold_in else None
         return _PartTwoDirection.apply(left, right, self, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                        left2right.lin_root.weight, right2left.lin_rel.weight,
                                        right2left.lin_rel.bias, right2left.lin_root.weight, bool(relu),
-                                       float(dropout), opts)
+                                       float(dropout), opts, prev)
 
-    def two_direction_heads(self, left, right, left2right, right2left, lin_left, lin_right, dropout=0.0, opts=None):
+    def two_direction_heads(self, left, right, left2right, right2left, lin_left, lin_right, dropout=0.0, opts=None,
+                            fold_in=False):
         """The last layer + heads (arch.py:184-190) on this partition, one autograd node (None: not applicable)."""
         if self.orient != "cons" or left.dtype != torch.float32 or _local_spmm is not _product_spmm:
             return None
+        from .options import DEFAULT
+
+        prev = foldable_producer(left, right, opts or DEFAULT) if fold_in else None
         return _PartTwoDirectionHeads.apply(left, right, self, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                             left2right.lin_root.weight, right2left.lin_rel.weight,
                                             right2left.lin_rel.bias, right2left.lin_root.weight, True,
                                             float(dropout), lin_left.weight, lin_left.bias, lin_right.weight,
-                                            lin_right.bias, opts)
+                                            lin_right.bias, opts, prev)
 
     def partitioned_conv(self, x, fc):
         """One GraphConv direction: fc(agg, x_dst) is lin_rel + lin_root (+ReLU, +dropout)."""

@@ -368,6 +368,53 @@ def _worker_c4(rank, world, port, out_dir, mode, scale=50, hids=256):
         dist.destroy_process_group()
 
 
+def _worker_fold(rank, world, port, out_dir):
+    """The partitioned conv1 weight-gradient fold (partition._part_backward_folded) against the
+    separate pass (options.fold_conv1_wgrad off) on 2 HIP ranks: the same loss; conv1's gradients
+    within fp32 summation-order tolerance (the variable side's sum over ranks is re-associated), every
+    other gradient bitwise."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lpgnn import GCN_FC, partition as part
+
+        spec = _c4_small(100)
+        plan = part.plan_partition_blocks(spec, world, rank)
+        batch = part.make_block_batch(spec, plan, device="cuda:0")
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=256, depth=4, dp=0.1).to("cuda:0").train()
+        base = model.options.replace(arith="x3")
+        out = {}
+        for fold in (True, False):
+            model.options = base.replace(fold_conv1_wgrad=fold)
+            model.zero_grad()
+            torch.manual_seed(5)
+            lc, lv = model(batch)
+            loss = part.balanced_distributed(lc, lv, batch.y_s, batch.y_t, batch.n_own)
+            loss.backward()
+            part.all_reduce_grads(model)
+            out[fold] = (loss.item(), {k: p.grad.detach().clone() for k, p in model.named_parameters()})
+        assert out[True][0] == out[False][0]
+        for k, v in out[True][1].items():
+            w = out[False][1][k]
+            if k.startswith("conv1."):
+                rel = ((v - w).norm() / w.norm()).item()
+                assert rel <= 1e-5, (k, rel)
+                torch.testing.assert_close(v, w, rtol=1e-4, atol=1e-5 * w.abs().max().item(), msg=k)
+            else:
+                assert torch.equal(v, w), k
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_partitioned_conv1_wgrad_fold_equals_separate_pass(tmp_path):
+    mp.spawn(_worker_fold, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+
+
 @pytest.mark.timeout(600)
 def test_c4_reduced_two_ranks_hip_vs_oracle(tmp_path):
     """c4 at 1/50 size through the HIP partitioned path (2 ranks): owned and halo logits, the
