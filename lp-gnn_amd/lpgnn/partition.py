@@ -644,6 +644,16 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
                                  w_rel_r2l, w_root_r2l), logits
 
 
+def _relu_bwd(ctx, g, y, want_db):
+    """(dZ, bias gradient) of a layer output gradient through the layer's ReLU/dropout."""
+    from . import fc as _fc
+
+    if not ctx.relu:
+        g = g.contiguous()
+        return g, (g.sum(0) if want_db else None)
+    return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
+
+
 def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     """_PartTwoDirection's backward from the output gradients, or -- dz =
     (dz_l, db_r2l, dz_r_own, db_l2r) -- from gradients that already went
@@ -673,7 +683,14 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
                 keep(dw_rel_r2l, 6), keep(db_r2l, 7, ctx.has_b[1]), keep(dw_root_r2l, 8), None, None)
     prev = getattr(ctx, "wgk_prev", None)
     ctx.wgk_prev = None
-    if prev is not None and dz is not None and need[0] and need[1]:
+    if prev is not None and need[0] and need[1]:
+        if dz is None:  # through this layer's ReLU/dropout first (halo gradients reduced to the owners)
+            g_right = torch.zeros_like(right_new) if g_right is None else g_right
+            g_left = torch.zeros_like(left_new) if g_left is None else g_left
+            red = ex.start_reduce(g_right.contiguous(), inplace=False)
+            dz_l, db_r2l = _relu_bwd(ctx, g_left, left_new, ctx.has_b[1] and need[7])
+            dz_r, db_l2r = _relu_bwd(ctx, red.finish(), right_new[:n_own], ctx.has_b[0] and need[4])
+            dz = (dz_l, db_r2l, dz_r, db_l2r)
         return _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward)
     if dz is None:
         if g_right is None:
@@ -683,10 +700,7 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
         red = ex.start_reduce(g_right.contiguous(), inplace=False)  # halo grads -> owners, in flight ...
 
     def mask(g, y, want_db):
-        if not ctx.relu:
-            g = g.contiguous()
-            return g, (g.sum(0) if want_db else None)
-        return _fc.relu_bwd_colsum(g.contiguous(), y, ctx.scale, want_db)
+        return _relu_bwd(ctx, g, y, want_db)
 
     def wgrads(dz, agg, x_dst, need_rel, need_root):
         if not (need_rel or need_root):
