@@ -1051,13 +1051,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_sk(FcB16Args a_arg, S
     // k-tiles [kb, ke) (fc_bf16_p's pipeline: barrier mid-tile, reads one 32-k step ahead, DMA pieces
     // and reads placed one per MFMA)
     {
-      uint32_t vo[PPW];
-#pragma unroll
-      for (int p = 0; p < PPW; ++p) {
-        const int qq = wave + NW * p;
-        const int row = (qq < PA ? qq : qq - PA) * 8 + (ln >> 3);
-        vo[p] = (uint32_t)((row * (qq < PA ? a.lda1 : a.ldw1) + swz(row, ln & 7) * 8) * 2);
-      }
+      // the lane's DMA offsets: piece p of an operand is 8 NW rows past piece p - 1, so one offset per
+      // operand plus a scalar step per piece (two VGPRs instead of PPW; laundered per stage so they are
+      // not hoisted back into PPW registers)
+      const int rowA = wave * 8 + (ln >> 3);
+      const uint32_t voA = (uint32_t)((rowA * a.lda1 + swz(rowA, ln & 7) * 8) * 2);
+      const uint32_t voW = (uint32_t)((rowA * a.ldw1 + swz(rowA, ln & 7) * 8) * 2);
+      const uint32_t stepA = (uint32_t)(NW * 8 * a.lda1 * 2), stepW = (uint32_t)(NW * 8 * a.ldw1 * 2);
       const int64_t kp1 = a.K1 > 0 ? a.K1 : BK, kp2 = a.K2 > 0 ? a.K2 : BK;
       const int64_t mrows = a.M - m0 < BM ? a.M - m0 : BM;
       const int64_t ncols = a.N - n0 < BN ? a.N - n0 : BN;
@@ -1073,13 +1073,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_sk(FcB16Args a_arg, S
         const int kk = p2 ? tk - nk1 : tk;
         unsigned char *base = smem + b * TILE_BYTES;
         const uint32_t na = ok ? (p2 ? na2 : na1) : 0u, nw = ok ? (p2 ? nw2 : nw1) : 0u;
+        uint32_t oa = voA, ow = voW;
+        asm volatile("" : "+v"(oa), "+v"(ow));
 #pragma unroll
         for (int p = 0; p < PPW; ++p) {
           const int qq = wave + NW * p;
           if (p < PA / NW)
-            dma16(p2 ? pa2 : pa1, na, base + qq * 1024, vo[p], kk * (BK * 2));
+            dma16(p2 ? pa2 : pa1, na, base + qq * 1024, oa + (uint32_t)p * stepA, kk * (BK * 2));
           else
-            dma16(p2 ? pw2 : pw1, nw, base + qq * 1024, vo[p], kk * (BK * 2));
+            dma16(p2 ? pw2 : pw1, nw, base + qq * 1024, ow + (uint32_t)(p - PA / NW) * stepW, kk * (BK * 2));
         }
       };
       auto rd = [&](int b, int st, v8(&av)[FM], v8(&bv)[FN]) {
