@@ -955,6 +955,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_sk(FcB16Args a_arg, S
     FcB16Args a = *(__attribute__((address_space(4))) const FcB16Args *)kp;
     if constexpr (EPI != 1) a.my = nullptr, a.mi = nullptr, a.cs = nullptr;
     if constexpr (EPI != 2) a.mo = nullptr;
+    if constexpr (EPI == 1) a.bias = nullptr, a.drop_thresh = 0u;  // (the folded backward has neither)
     return a;
   };
   auto skargs = [&]() {
@@ -1150,8 +1151,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_sk(FcB16Args a_arg, S
       rd((n - 1) & 1, 1, a1, b1);
       mma(a0, b0);
       mma(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);  // nothing of the epilogue moves up beside the last MFMAs
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
     }
 
     if (is_prod) {  // the partial for block v + 1: stores drained by every wave, then one release + flag
