@@ -419,7 +419,9 @@ lpg_status lpg_fc_bf16_relu_bwd_bits_db(int64_t M, int64_t N, int64_t K1, const 
  *   kernel only; bias / dropout unused; scale), with db: ..._db (db_workspace as there);  else
  *   lpg_fc_bf16 / lpg_fc_f16, with mask_out: lpg_fc_bf16_mask.
  * workspace: lpg_fc16_workspace_bytes() bytes, 16-byte aligned (NULL = the per-call entry's path);
- * LPG_FC_KERNEL(6) asks for the stream-K form explicitly (the default choice 0 takes it too). */
+ * LPG_FC_KERNEL(6) selects the stream-K form; every other choice runs as the per-call entry.  The
+ * form is a measured alternative, not the default: 15-25 % slower than choice 0 at the c5 and
+ * fp16-inference shapes (profiles/r05_sk_ab.log). */
 typedef struct lpg_fc16_call {
   int32_t dtype, flags;
   int64_t M, N, K1, K2;

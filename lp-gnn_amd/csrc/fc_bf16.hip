@@ -1491,7 +1491,9 @@ bool p_ok(const FcB16Args &a) {
 // (profiles/r02_kbench_bf16.log, r02_kbench_fck10.log): fc_bf16_p 1212-1300 TF/s vs hipBLASLt
 // 1248-1268, fc_fwd_bf16 256^2 1033; wgrad_bf16 1172-1222 vs hipBLASLt's bf16-output GEMM 924-1004.
 // 6 = the persistent stream-K form (fc_bf16_sk) when the call carries its workspace (lpg_fc16), else
-// choice 0; choice 0 takes it too whenever a workspace is given.
+// choice 0.  (Not the default: 15-25 % slower than choice 0 at the c5 / fp16-inference shapes,
+// profiles/r05_sk_ab.log -- each XCD's 32 resident blocks walk ranges 24 tiles apart, so the A panels
+// the one-tile grid's concurrent blocks share in L2 are fetched once per block.)
 constexpr int kKernels = 6;
 
 int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
@@ -1921,8 +1923,10 @@ lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel, i
   float *const cs = a.cs;
   a.cs = nullptr;
   if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<E, 2, 2, 4, 4>(a, relu, s);  // 128 x 128
-  if ((kernel == 0 || kernel == 6) && p_ok(a) && sk_ok(a, skws, skws_bytes)) {
-    // the persistent stream-K form of the pipelined kernel (with a workspace), n-split tile order
+  if (kernel == 6 && p_ok(a) && sk_ok(a, skws, skws_bytes)) {
+    // the persistent stream-K form of the pipelined kernel (with a workspace), n-split tile order --
+    // measured 15-25 % slower than the default at the c5 and fp16-inference shapes
+    // (profiles/r05_sk_ab.log): a per-call choice, not the default
     a.order = 1;
     a.cs = cs;
     if (cs_rows && cs) *cs_rows = a.M;

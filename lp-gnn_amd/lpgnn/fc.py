@@ -420,9 +420,9 @@ def fc_forward_bf16(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None
         _lib.check(st, entry)
         return C
     entry = "lpg_fc_f16" if f16 else "lpg_fc_bf16"
-    if mask_out is None and not small and kernel in (0, 6):
-        # the persistent stream-K form with its workspace (lpg_fc16): the same bits, no partial last
-        # round, spread epilogues (fc_bf16.hip fc_bf16_sk); the call falls back where it does not apply
+    if mask_out is None and not small and kernel == 6:
+        # the persistent stream-K form with its workspace (lpg_fc16, choice 6): the same bits, no partial
+        # last round -- measured slower than the default (profiles/r05_sk_ab.log), kept as a choice
         call = _lib.LpgFc16Call(
             dtype=1 if f16 else 0, flags=flags, M=M, N=N, K1=A1.shape[1], K2=K2, A1=A1.data_ptr(), W1=W1.data_ptr(),
             A2=None if A2 is None else A2.data_ptr(), W2=None if W2 is None else W2.data_ptr(), lda1=A1.stride(0),

@@ -582,7 +582,7 @@ def test_fc16_stream_k_identical(dt, M, N, K1, K2, relu, drop, acc):
     b = r(N) * 0.1
     P = r(M, N).to(dt) if acc else None
     outs = []
-    for k in (6, 3, 0):
+    for k in (6, 3, 0):  # (6 = the stream-K form, 3 = the one-tile pipelined kernel, 0 = default)
         out = P.clone() if acc else None
         outs.append(fc_forward_bf16(A1, W1, A2, W2, b, relu, drop, seed=77, out=out, accumulate=acc, kernel=k))
     assert torch.equal(outs[0], outs[1]), int((outs[0] != outs[1]).sum())
