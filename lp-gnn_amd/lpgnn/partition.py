@@ -783,10 +783,11 @@ def _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward):
     the masked tile times conv1's 8 + 8 inputs, never storing conv1's output gradient).
 
     Variables: conv1's output gradient on an owned variable is the source-side term of right2left summed
-    over every rank that touches it, plus the root term of left2right.  The source-side term is
-    re-associated, (A^T dZ_l) W_rel: T = A^T dZ_l over the local variables, its halo rows REDUCED to
-    their owners first (sum over ranks, the exchange conv1's own backward would have done on the
-    product), then one fused GEMM over the owned rows.  Constraints are local: conv.py's fold as is.
+    over every rank that touches it, plus the root term of left2right.  The source-side term's halo
+    rows are REDUCED to their owners before the fused GEMM (the exchange conv1's own backward would
+    have done on the product): T = A^T dZ_l (then (T W_rel + dZ_r W_root) in one two-part GEMM) or
+    P = A^T (dZ_l W_rel) (then dZ_r W_root + P), whichever association the one-GPU path takes.
+    Constraints are local: conv.py's fold as is.
     conv1's node receives zero-stride gradients and returns the handed weight gradients."""
     from . import fc as _fc
 
@@ -798,26 +799,36 @@ def _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward):
     p_left, p_right, p_agg_l, p_agg_r, p_left_new, p_right_new = prev.saved_tensors[:6]
     dw_rel_r2l, dw_root_r2l = (wgf(dz_l, agg_l) if need[6] else None), (wgf(dz_l, left) if need[8] else None)
 
-    # conv1's left2right (owned variables): T's halo partials to the owners, then the fused GEMM
-    T = spmm_forward(AT, dz_l)
-    T_own = ex.start_reduce(T, inplace=True).finish()
-
     def fused(G1, W1, G2, W2, addend, y, x1, x2, two_pass):
         r = _fc.input_grad_relu_wgrad(G1, W1, G2, W2, addend, y, x1, x2)
         if r is None:  # operands the fused kernel does not take: the stored gradient, then conv1's pass
             r = _fc.relu_wgrad_smallk(two_pass(), y, 1.0, x1, x2, True)
         return r
 
-    def g_right_own():
-        g = igf(T_own, w_rel_r2l)
-        return igf(dz_r, w_root_l2r, out=g, accumulate=True)
-    wk_r = fused(T_own, w_rel_r2l, dz_r, w_root_l2r, None, p_right_new[:n_own], p_agg_r[:n_own], p_right[:n_own],
-                 g_right_own)
+    # conv1's left2right (owned variables): the source-side term's halo partials to the owners, then the
+    # fused GEMM -- in the association the one-GPU path picks (conv._src_first): (A^T dZ_l) W_rel over
+    # the variables, or A^T (dZ_l W_rel) with the GEMM over the constraints and the reduced SpMM output
+    # as the fused kernel's addend
+    from .conv import _src_first
+
+    if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
+        T_own = ex.start_reduce(spmm_forward(AT, dz_l), inplace=True).finish()
+
+        def g_right_own():
+            g = igf(T_own, w_rel_r2l)
+            return igf(dz_r, w_root_l2r, out=g, accumulate=True)
+        wk_r = fused(T_own, w_rel_r2l, dz_r, w_root_l2r, None, p_right_new[:n_own], p_agg_r[:n_own],
+                     p_right[:n_own], g_right_own)
+    else:
+        P_own = ex.start_reduce(spmm_forward(AT, igf(dz_l, w_rel_r2l)), inplace=True).finish()
+
+        def g_right_own():
+            return igf(dz_r, w_root_l2r, out=P_own.clone(), accumulate=True)
+        wk_r = fused(dz_r, w_root_l2r, None, None, P_own, p_right_new[:n_own], p_agg_r[:n_own], p_right[:n_own],
+                     g_right_own)
 
     # this layer's left2right weight gradients and conv1's right2left (constraints, local)
     f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
-    from .conv import _src_first
-
     use_t = _src_first(AT, f_out, f_in, 4) or agg_r is None
     rel_from_t = need[3] and (agg_r is None or (use_t and A.n_rows < n_own))
     dw_rel_l2r = wgf(dz_r, agg_r[:n_own]) if need[3] and not rel_from_t else None
