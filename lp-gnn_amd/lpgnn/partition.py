@@ -758,11 +758,14 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     g_l = None
     if need[0] or use_t:  # left: source of left2right through reduce(AT @ left)[:n_own]
         f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
-        full = torch.empty((right.shape[0], f_out if use_t else f_in), dtype=torch.float32, device=left.device)
-        if use_t:
-            full[:n_own] = dz_r
+        if use_t and right.shape[0] == n_own and dz_r.is_contiguous():
+            full = dz_r  # no halo rows (one rank): dZ_r is the whole source table, no copy
         else:
-            igf(dz_r, w_rel_l2r, out=full[:n_own])
+            full = torch.empty((right.shape[0], f_out if use_t else f_in), dtype=torch.float32, device=left.device)
+            if use_t:
+                full[:n_own] = dz_r
+            else:
+                igf(dz_r, w_rel_l2r, out=full[:n_own])
         bc = ex.start_broadcast_(full)           # owners' aggregate gradient -> halo rows, in flight ...
         root = igf(dz_l, w_root_r2l) if need[0] else None  # ... under the root-path gradient
         bc.finish()
@@ -833,11 +836,14 @@ def _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward):
     rel_from_t = need[3] and (agg_r is None or (use_t and A.n_rows < n_own))
     dw_rel_l2r = wgf(dz_r, agg_r[:n_own]) if need[3] and not rel_from_t else None
     dw_root_l2r = wgf(dz_r, right[:n_own]) if need[5] else None
-    full = torch.empty((right.shape[0], f_out if use_t else f_in), dtype=torch.float32, device=left.device)
-    if use_t:
-        full[:n_own] = dz_r
+    if use_t and right.shape[0] == n_own and dz_r.is_contiguous():
+        full = dz_r  # no halo rows (one rank): dZ_r is the whole source table, no copy
     else:
-        igf(dz_r, w_rel_l2r, out=full[:n_own])
+        full = torch.empty((right.shape[0], f_out if use_t else f_in), dtype=torch.float32, device=left.device)
+        if use_t:
+            full[:n_own] = dz_r
+        else:
+            igf(dz_r, w_rel_l2r, out=full[:n_own])
     ex.start_broadcast_(full).finish()
     t = spmm_forward(A, full)
     if use_t:
