@@ -161,7 +161,9 @@ lpg_status lpg_spmm_f16_tuned(const lpg_csr *A, const uint16_t *X, int64_t ldx, 
  *   lpg_fc_bf16 / _relu_bwd: 1 = 128 x 128 tiles, 2 = 256 x 256 tiles,
  *     3 = the pipelined 256 x 256 kernel (the default from 4096 rows, there in the n-split tile
  *     order), 4 / 5 = the default choice with the pipelined kernel in the m-major / n-quarter
- *     tile order. */
+ *     tile order, 6 = the persistent stream-K form (lpg_fc16 with a workspace only), 7 = two 4-wave
+ *     blocks per CU on 128 x 256 tiles with one LDS stage (fc_bf16_q; measured 3-10 % slower than
+ *     the default, profiles/r05_q_ab.log). */
 #define LPG_FC_RELU 1
 #define LPG_FC_ACCUMULATE 2
 #define LPG_FC_HEADS_ONLY 4 /* lpg_fc_x3_heads_f32 only: C is not written (the logits are the only output;

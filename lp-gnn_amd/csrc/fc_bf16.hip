@@ -898,6 +898,132 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
 #endif
 }
 
+// ---- fc_bf16_q: two blocks per CU, 128 x 256 tiles, one LDS stage ---------------
+//
+// fc_bf16_p's single 8-wave block per CU runs its epilogue (the addend read and the output stores,
+// HBM-bound when every CU stores at once) with the MFMA pipe idle.  Here a block is 4 waves side by
+// side in n (each wave the same 128 x 64 fragment set: the same MFMA chain per output, so the same bits
+// as every other choice), the tile 128 x 256, and ONE 48 KiB LDS stage: with the epilogue image
+// (4 x 128 x 144 B) the block takes 74 KiB, so two blocks share a CU and one block's epilogue and DMA
+// waits run beside the other's MFMAs.  Per 64-k tile: the tile landed (wait + barrier) -> both 32-k
+// fragment sets read into registers -> barrier -> the next tile's DMA into the same buffer -> the 2 x 32
+// MFMAs (the DMA lands under them).  1.5 x the staged bytes per MFMA of the 256 x 256 tile.
+template <class E, int WM, int WN, int FM, int FN, bool RELU>
+__global__ __launch_bounds__(64 * WM * WN, 2) void fc_bf16_q(FcB16Args a) {
+  typedef typename E::v8 v8;
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  constexpr int A_BYTES = BM * BK * 2, TILE_BYTES = A_BYTES + BN * BK * 2;
+  constexpr int PA = BM / 8, PT = PA + BN / 8, PPW = PT / NW;
+  static_assert(PA % NW == 0 && PT % NW == 0, "whole pieces per wave");
+  constexpr int EP_BYTES = NW * FM * 16 * (FN * 16 * 2 + 16);
+  constexpr int SMEM = TILE_BYTES > EP_BYTES ? TILE_BYTES : EP_BYTES;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int64_t nwg = a.mt * a.nt;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
+  int64_t mi = wgid / a.nt, ni = wgid % a.nt;
+  if (a.order == 1 && a.nt >= 2) {  // n-split, as fc_bf16_p
+    const int64_t nh = a.nt / 2, t0 = a.mt * nh;
+    if (wgid < t0) {
+      mi = wgid / nh;
+      ni = wgid % nh;
+    } else {
+      mi = (wgid - t0) / (a.nt - nh);
+      ni = nh + (wgid - t0) % (a.nt - nh);
+    }
+  }
+  const int64_t m0 = mi * BM, n0 = ni * BN;
+  const int64_t mrows = a.M - m0 < BM ? a.M - m0 : BM;
+  const int64_t ncols = a.N - n0 < BN ? a.N - n0 : BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int nk1 = (int)(a.K1 / BK);
+  const int nk = nk1 + (int)(a.K2 / BK);
+
+  const int64_t kp1 = a.K1 > 0 ? a.K1 : BK, kp2 = a.K2 > 0 ? a.K2 : BK;
+  const uint64_t pa1 = (uint64_t)(a.A1 + m0 * a.lda1), pw1 = (uint64_t)(a.W1 + n0 * a.ldw1);
+  const uint64_t pa2 = a.A2 ? (uint64_t)(a.A2 + m0 * a.lda1) : pa1, pw2 = a.W2 ? (uint64_t)(a.W2 + n0 * a.ldw1) : pw1;
+  const uint32_t na1 = (uint32_t)(((mrows - 1) * a.lda1 + kp1) * 2), na2 = (uint32_t)(((mrows - 1) * a.lda1 + kp2) * 2);
+  const uint32_t nw1 = (uint32_t)(((ncols - 1) * a.ldw1 + kp1) * 2), nw2 = (uint32_t)(((ncols - 1) * a.ldw1 + kp2) * 2);
+  // piece p of a wave covers rows (wave + NW p) * 8 + lane / 8 of its operand: the swizzle depends on
+  // the row only through (row / 2) & 7, the same for every p (NW even), so one voffset per operand and
+  // the piece's row step in the (scalar) base address and record count -- 2 VGPRs, not PPW.
+  static_assert(NW % 2 == 0, "piece swizzle independent of p");
+  const int rowa = wave * 8 + (lane >> 3);
+  const uint32_t voa = (uint32_t)((rowa * a.lda1 + swz(rowa, lane & 7) * 8) * 2);
+  const uint32_t vow = (uint32_t)((rowa * a.ldw1 + swz(rowa, lane & 7) * 8) * 2);
+  auto stage = [&](int t) {
+    const bool p2 = t >= nk1;
+    const int kk = p2 ? t - nk1 : t;
+    const uint64_t ba = p2 ? pa2 : pa1, bw = p2 ? pw2 : pw1;
+    const int64_t ra = p2 ? na2 : na1, rw = p2 ? nw2 : nw1;
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) {
+      const int q = wave + NW * p;
+      const bool isa = p < PA / NW;
+      const int64_t step = (int64_t)NW * 8 * 2 * (isa ? p : p - PA / NW) * (isa ? a.lda1 : a.ldw1);
+      const int64_t left = (isa ? ra : rw) - step;
+      dma16((isa ? ba : bw) + step, left > 0 ? (uint32_t)left : 0u, smem + q * 1024, isa ? voa : vow, kk * (BK * 2));
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  auto rd = [&](int st, v8(&av)[FM], v8(&bv)[FN]) {
+    const unsigned char *As = smem;
+    const unsigned char *Bs = As + A_BYTES;
+    const int chunk = st * 4 + fq;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * FM * 16 + i * 16 + fr;
+      av[i] = *reinterpret_cast<const v8 *>(As + row * 128 + swz(row, chunk) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * FN * 16 + j * 16 + fr;
+      bv[j] = *reinterpret_cast<const v8 *>(Bs + row * 128 + swz(row, chunk) * 16);
+    }
+  };
+  auto mma = [&](const v8(&av)[FM], const v8(&bv)[FN]) {  // W x A^T (transposed fragments), as fc_bf16_p
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) acc[i][j] = E::mma(bv[j], av[i], acc[i][j]);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  v8 a0[FM], b0[FN], a1[FM], b1[FN];
+  if (nk > 0) stage(0);
+  for (int t = 0; t < nk; ++t) {
+    barrier();  // tile t landed everywhere
+    rd(0, a0, b0);
+    rd(1, a1, b1);
+    barrier();  // every wave holds its fragments: the buffer is free
+    if (t + 1 < nk) stage(t + 1);
+    mma(a0, b0);
+    mma(a1, b1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int elane = lane;  // opaque: keeps the epilogue's lane-derived addresses from living across the loop
+  asm volatile("" : "+v"(elane));
+  epilogue_bf16_ti<E, FM, FN, RELU>(a, acc, smem, wave, elane, m0 + wm * FM * 16, n0 + wn * FN * 16);
+}
+
 // ---- fc_bf16_sk: the pipelined kernel, persistent and stream-K -----------------
 //
 // One resident block per CU (G blocks) walks a contiguous range of the launch's (tile, k-tile)
@@ -1474,6 +1600,21 @@ lpg_status launch_bf16_sk(FcB16Args a, bool relu, hipStream_t s, void *ws) {
   return LPG_OK;
 }
 
+template <class E, int WM, int WN, int FM, int FN>
+lpg_status launch_bf16_q(FcB16Args a, bool relu, hipStream_t s) {
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  a.mt = (a.M + BM - 1) / BM;
+  a.nt = (a.N + BN - 1) / BN;
+  const int64_t nwg = a.mt * a.nt;
+  LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_bf16: grid too large");
+  if (relu)
+    hipLaunchKernelGGL((fc_bf16_q<E, WM, WN, FM, FN, true>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
+  else
+    hipLaunchKernelGGL((fc_bf16_q<E, WM, WN, FM, FN, false>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
 // whether fc_bf16_p can take these operands: one offset set for both k phases, 32-bit offsets
 bool p_ok(const FcB16Args &a) {
   if (a.K1 == 0) return false;
@@ -1494,7 +1635,8 @@ bool p_ok(const FcB16Args &a) {
 // choice 0.  (Not the default: 15-25 % slower than choice 0 at the c5 / fp16-inference shapes,
 // profiles/r05_sk_ab.log -- each XCD's 32 resident blocks walk ranges 24 tiles apart, so the A panels
 // the one-tile grid's concurrent blocks share in L2 are fetched once per block.)
-constexpr int kKernels = 6;
+// 7 = fc_bf16_q (two 4-wave blocks per CU on 128 x 256 tiles, one LDS stage) when p_ok, else choice 0.
+constexpr int kKernels = 7;
 
 int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
   const int64_t tiles = ((N + 255) / 256) * ((K + 255) / 256);
@@ -1923,6 +2065,12 @@ lpg_status fc_bf16_dispatch(FcB16Args a, bool relu, hipStream_t s, int kernel, i
   float *const cs = a.cs;
   a.cs = nullptr;
   if (kernel == 1 || (kernel == 0 && a.M < 4096)) return launch_bf16<E, 2, 2, 4, 4>(a, relu, s);  // 128 x 128
+  if (kernel == 7 && p_ok(a)) {  // two 4-wave blocks per CU, 128 x 256 tiles, n-split order
+    a.order = 1;
+    a.cs = cs;
+    if (cs_rows && cs) *cs_rows = a.M;
+    return launch_bf16_q<E, 1, 4, 8, 4>(a, relu, s);
+  }
   if (kernel == 6 && p_ok(a) && sk_ok(a, skws, skws_bytes)) {
     // the persistent stream-K form of the pipelined kernel (with a workspace), n-split tile order --
     // measured 15-25 % slower than the default at the c5 and fp16-inference shapes

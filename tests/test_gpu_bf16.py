@@ -45,7 +45,7 @@ def test_fc_bf16_matches_fp32_gemm(M, N, K1, K2, relu, bias):
 
 # per-call kernel choices of lpg_fc_bf16 (LPG_FC_KERNEL, include/lpgnn.h): 1 = 128 x 128,
 # 2 = 256 x 256, 3 = the pipelined transposed-fragment kernel (the default from 4096 rows)
-KERNELS = (1, 2, 3, 4, 5, 6)
+KERNELS = (1, 2, 3, 4, 5, 6, 7)
 
 
 def _f64_ulp_check(out, A, W, P, b, relu, A2=None, W2=None):
