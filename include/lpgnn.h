@@ -121,6 +121,51 @@ lpg_status lpg_spmm_f32_heavy(const lpg_csr *A, const float *X, int64_t ldx,
                               const int32_t *heavy_rows, int64_t n_heavy, int64_t thresh,
                               void *stream);
 
+/* ---- multi-GPU: the row-partitioned SpMM (SURVEY.md §8b "Multi-GPU", §8e) ---------------------
+ *
+ * One rank per GPU holds a block of constraint rows and the variables they touch (boundary
+ * variables: touched by >= 2 ranks).  vars<-cons over the local edges gives full sums for the
+ * variables only this rank touches and partial sums for the boundary ones; these entries sum the
+ * boundary rows over the ranks with one RCCL all-reduce of a dense [n_boundary, F] buffer, so every
+ * rank ends with the full sums of the boundary rows it holds (the same bits on every rank).  The
+ * communicator is RCCL's (rccl.h's ncclComm_t), made here from a unique id that rank 0 draws and the
+ * caller distributes (any side channel: torch.distributed, MPI, a file).  RCCL is resolved at run
+ * time (the copy the process already loaded first), so only these entries need it.
+ * Replaces nothing in the reference (no distributed code: train.py:81-82); lpgnn.partition's
+ * Python exchange is the sparse owner form of the same sum. */
+typedef struct ncclComm *ncclComm_t; /* as rccl.h */
+#define LPG_COMM_ID_BYTES 128        /* NCCL_UNIQUE_ID_BYTES */
+/* a fresh unique id into id[LPG_COMM_ID_BYTES] (host memory), on ONE rank */
+lpg_status lpg_comm_unique_id(void *id);
+/* this rank's communicator over nranks ranks on the current device (collective: every rank calls it
+ * with the same id) */
+lpg_status lpg_comm_init(ncclComm_t *comm, int32_t nranks, const void *id, int32_t rank);
+lpg_status lpg_comm_destroy(ncclComm_t comm);
+lpg_status lpg_comm_info(ncclComm_t comm, int32_t *nranks, int32_t *rank);
+
+/* Its two halves, for a caller that runs the collective itself (MPI, another RCCL wrapper): pack
+ * copies the mapped rows of Y into boundary_buf in boundary order (zero rows for -1); unpack copies
+ * boundary_buf's rows back into the mapped rows.  Stream-ordered, no collective. */
+lpg_status lpg_boundary_pack_f32(const float *Y, int64_t ldy, int64_t rows, int64_t F, int64_t n_boundary,
+                                 const int32_t *boundary_map, float *boundary_buf, void *stream);
+lpg_status lpg_boundary_unpack_f32(float *Y, int64_t ldy, int64_t rows, int64_t F, int64_t n_boundary,
+                                   const int32_t *boundary_map, const float *boundary_buf, void *stream);
+/* The boundary exchange alone: boundary_map (device int32 [n_boundary], the same global boundary
+ * order on every rank) gives the row of Y holding boundary variable b on this rank, or -1 when this
+ * rank does not touch it; boundary_buf: device fp32 [n_boundary, F] workspace.  Packs those rows
+ * (zero rows for -1), all-reduces (sum) the buffer over comm on `stream`, and writes the sums back
+ * into the mapped rows; other rows of Y are untouched.  Collective: every rank calls it with the same
+ * n_boundary and F.  Entries of boundary_map outside [0, rows) count as -1. */
+lpg_status lpg_boundary_allreduce_f32(float *Y, int64_t ldy, int64_t rows, int64_t F, int64_t n_boundary,
+                                      const int32_t *boundary_map, float *boundary_buf, ncclComm_t comm,
+                                      void *stream);
+/* lpg_spmm_f32(A, X) on this rank's local CSR (rows = local variables for vars<-cons), then
+ * lpg_boundary_allreduce_f32 on its rows.  The backward w.r.t. X of a partitioned cons<-vars product
+ * is this entry on A^T; cons<-vars itself needs no exchange (lpg_spmm_f32). */
+lpg_status lpg_spmm_partitioned_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                                    int64_t n_boundary, const int32_t *boundary_map, float *boundary_buf,
+                                    ncclComm_t comm, void *stream);
+
 /* Same, bf16 storage (uint16 bit patterns) with fp32 accumulation; the
  * accumulated row is rounded to bf16 once (round-to-nearest-even). */
 lpg_status lpg_spmm_bf16(const lpg_csr *A, const uint16_t *X, int64_t ldx,

@@ -92,6 +92,14 @@ HEADER_SYMBOLS = (
     "lpg_induced_count",
     "lpg_induced_fill",
     "lpg_sample_reset",
+    "lpg_comm_unique_id",
+    "lpg_comm_init",
+    "lpg_comm_destroy",
+    "lpg_comm_info",
+    "lpg_boundary_pack_f32",
+    "lpg_boundary_unpack_f32",
+    "lpg_boundary_allreduce_f32",
+    "lpg_spmm_partitioned_f32",
 )
 
 c_i64, c_i32, c_p = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
@@ -133,6 +141,18 @@ def lib() -> ctypes.CDLL:
     L.lpg_csr_pack_f32.restype = c_i32
     L.lpg_spmm_f32.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p]
     L.lpg_spmm_f32.restype = c_i32
+    L.lpg_comm_unique_id.argtypes = [c_p]
+    L.lpg_comm_init.argtypes = [ctypes.POINTER(c_p), c_i32, c_p, c_i32]
+    L.lpg_comm_destroy.argtypes = [c_p]
+    L.lpg_comm_info.argtypes = [c_p, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]
+    L.lpg_boundary_pack_f32.argtypes = [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p]
+    L.lpg_boundary_unpack_f32.argtypes = L.lpg_boundary_pack_f32.argtypes
+    L.lpg_boundary_allreduce_f32.argtypes = [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]
+    L.lpg_spmm_partitioned_f32.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p,
+                                           c_p]
+    for _n in ("lpg_comm_unique_id", "lpg_comm_init", "lpg_comm_destroy", "lpg_comm_info", "lpg_boundary_pack_f32",
+               "lpg_boundary_unpack_f32", "lpg_boundary_allreduce_f32", "lpg_spmm_partitioned_f32"):
+        getattr(L, _n).restype = c_i32
     L.lpg_spmm_f32_heavy.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p]
     L.lpg_spmm_f32_heavy.restype = c_i32
     L.lpg_spmm_bf16.argtypes = [ctypes.POINTER(LpgCsr), c_p, c_i64, c_p, c_i64, c_i64, c_p]
