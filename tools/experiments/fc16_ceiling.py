@@ -56,6 +56,16 @@ def main():
                 return F.fc_forward_bf16(A1, W1, A2, W2, b, relu, drop, 5, out=out, accumulate=acc)
             ms = bench(run)
             print(f"{name:26s} {fill:7s} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TF/s", flush=True)
+            if fill == "random" and not acc:
+                # the vendor GEMM (hipBLASLt through torch) on the same operands: A [M, K] @ W^T, bias, no
+                # ReLU / dropout epilogue, the two K parts as one concatenated operand
+                Ac = A1 if A2 is None else torch.cat([A1, A2], 1)
+                Wc = W1 if W2 is None else torch.cat([W1, W2], 1)
+                bb = b.to(dt)
+                ms_v = bench(lambda: torch.nn.functional.linear(Ac, Wc, bb))
+                print(f"{name:26s} {'vendor':7s} {ms_v:8.3f} ms  {flops / ms_v / 1e9:7.1f} TF/s  (torch linear)",
+                      flush=True)
+                del Ac, Wc
             del A1, W1, A2, W2, out
             torch.cuda.empty_cache()
 
