@@ -123,7 +123,7 @@ class GraphConvTwoDirection(nn.Module):
                                        relu, dropout, fold_in, opts, feeds_conv)
         tdc = getattr(edge_index, "two_direction_conv", None)  # row-partitioned multi-GPU adjacency
         if tdc is not None and edge_weight is None:
-            out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout, opts, fold_in)
+            out = tdc(left_feas, right_feas, self.left2right, self.right2left, relu, dropout, opts, fold_in, feeds_conv)
             if out is not None:
                 return out
         l2r, r2l = edge_index.t(), edge_index

@@ -402,6 +402,30 @@ class Exchange:
                 tot = tot.to(device)
             dist.all_reduce(tot, group=group)
         self.active = bool(tot.item() > 0)
+        self._deferred = []  # (data_ptr, pending broadcast) of layer outputs whose halo rows are in flight
+
+    def defer(self, full: torch.Tensor, pending: _Pending) -> None:
+        """Leave a broadcast of `full`'s halo rows in flight: the consumer settles it (settle) right
+        before it first reads those rows, so the exchange runs under the compute in between."""
+        self._deferred.append((full.data_ptr(), pending))
+
+    def settle(self, full: torch.Tensor) -> torch.Tensor:
+        """Finish the deferred broadcast into `full`, if any (its halo rows are then current)."""
+        if self._deferred:
+            ptr = full.data_ptr()
+            keep = []
+            for q, p in self._deferred:
+                if q == ptr:
+                    p.finish()
+                else:
+                    keep.append((q, p))
+            self._deferred = keep
+        return full
+
+    def settle_all(self) -> None:
+        for _, p in self._deferred:
+            p.finish()
+        self._deferred = []
 
     @property
     def var_key_args(self) -> dict:
@@ -432,11 +456,16 @@ class Exchange:
         p.then = then
         return p
 
-    def start_broadcast_(self, full: torch.Tensor) -> _Pending:
-        """Asynchronous broadcast_rows_: finish() fills the halo rows and returns `full`."""
+    def start_broadcast_(self, full: torch.Tensor, quiet: bool = False) -> _Pending:
+        """Asynchronous broadcast_rows_: finish() fills the halo rows and returns `full`.  quiet: the
+        rows are written through a storage alias that leaves `full`'s autograd version alone -- for a
+        layer output whose halo rows land after the node that made it returned (Exchange.defer; that
+        node's backward reads only its owned rows)."""
+        dst = full.data if quiet else full
+
         def then(recv):
             if self.send_idx.numel():
-                full.index_copy_(0, self.send_idx, recv)
+                dst.index_copy_(0, self.send_idx, recv)
             return full
         if not self.active:
             return _Pending(None, then=lambda _: full)
@@ -543,16 +572,18 @@ class _PartTwoDirection(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu, dropout,
-                opts=None, prev=None):
+                opts=None, prev=None, defer=False):
         left_new, right_new, saved, _ = _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r,
-                                                           w_rel_r2l, b_r2l, w_root_r2l, relu, dropout, opts=opts)
+                                                           w_rel_r2l, b_r2l, w_root_r2l, relu, dropout, opts=opts,
+                                                           defer=defer)
         _link_prev(ctx, prev)
         ctx.save_for_backward(*saved)
         return left_new, right_new
 
     @staticmethod
     def backward(ctx, g_left, g_right):
-        return _part_backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None, None)
+        return _part_backward_core(ctx, ctx.saved_tensors, ctx.needs_input_grad, g_left, g_right) + (None, None,
+                                                                                                      None)
 
 
 def _link_prev(ctx, prev):
@@ -577,10 +608,14 @@ def foldable_producer(left, right, opts):
 
 
 def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_rel_r2l, b_r2l, w_root_r2l, relu,
-                       dropout, heads=None, opts=None):
+                       dropout, heads=None, opts=None, defer=False):
     """_PartTwoDirection's forward; returns (left_new, right_new, tensors to save, logits).
     heads = ((Wh_l, bh_l), (Wh_r, bh_r)): the heads in the FC epilogues (conv._forward_core's
-    rule) for the rows the FCs compute, a separate Linear for the halo rows; logits None without."""
+    rule) for the rows the FCs compute, a separate Linear for the halo rows; logits None without --
+    and then right_new's halo rows are never read (the halo logits are the owners', broadcast), so
+    they are not broadcast.  defer: the broadcast of right_new's halo rows stays in flight for the
+    next partitioned layer to settle (Exchange.defer) -- it runs under that layer's first GEMM and
+    SpMM, which read no halo row of it."""
     import functools
 
     from . import fc as _fc
@@ -609,6 +644,7 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
     else:
         agg_r = spmm_forward(AT, left)          # partials for [owned | halo]
     red = ex.start_reduce(agg_r, inplace=True)  # halo partials -> owners, in flight ...
+    ex.settle(right)                            # (the previous layer's deferred halo rows)
     agg_l = spmm_forward(A, right)              # ... under the purely local constraint side
     hl, hr = heads if heads is not None else (None, None)
     left_new = fcf(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu, dropout, seed_l, heads=hl,
@@ -624,7 +660,12 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
         right_new = torch.empty((right.shape[0], w_rel_l2r.shape[0]), dtype=torch.float32, device=left.device)
         own = fcf(agg_r[:n_own], w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, dropout, seed_r,
                              out=right_new[:n_own], heads=hr, **ex.var_key_args)
-    ex.start_broadcast_(right_new).finish()
+    if heads is None:
+        bc = ex.start_broadcast_(right_new, quiet=defer)
+        if defer:
+            ex.defer(right_new, bc)
+        else:
+            bc.finish()
     logits = None
     if heads is not None:
         # halo rows are copies of other ranks' variables: their logits are the OWNERS' logits, broadcast
@@ -750,12 +791,7 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
     first = need[0] and _src_first(AT, dz_r.shape[1], w_rel_l2r.shape[1], 4)
     rel_from_t = need[3] and (agg_r is None or (first and A.n_rows < ex.n_own))
     use_t = first or rel_from_t
-    dw_rel_l2r, dw_root_l2r = wgrads(dz_r, None if agg_r is None else agg_r[:n_own], right[:n_own],
-                                     need[3] and not rel_from_t, need[5])
-    if need[1]:  # ... and as the destination of left2right (owned rows)
-        igf(dz_r, w_root_l2r, out=g_r[:n_own], accumulate=True)
-
-    g_l = None
+    bc = full = None
     if need[0] or use_t:  # left: source of left2right through reduce(AT @ left)[:n_own]
         f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
         if use_t and right.shape[0] == n_own and dz_r.is_contiguous():
@@ -767,7 +803,15 @@ def _part_backward_core(ctx, saved, need, g_left, g_right, dz=None):
             else:
                 igf(dz_r, w_rel_l2r, out=full[:n_own])
         bc = ex.start_broadcast_(full)           # owners' aggregate gradient -> halo rows, in flight ...
-        root = igf(dz_l, w_root_r2l) if need[0] else None  # ... under the root-path gradient
+    # ... under the weight gradients and the variables' root-path and the constraints' root-path gradients
+    dw_rel_l2r, dw_root_l2r = wgrads(dz_r, None if agg_r is None else agg_r[:n_own], right[:n_own],
+                                     need[3] and not rel_from_t, need[5])
+    if need[1]:  # ... and as the destination of left2right (owned rows)
+        igf(dz_r, w_root_l2r, out=g_r[:n_own], accumulate=True)
+
+    g_l = None
+    if bc is not None:
+        root = igf(dz_l, w_root_r2l) if need[0] else None
         bc.finish()
         if use_t:
             t = spmm_forward(A, full)
@@ -800,42 +844,16 @@ def _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward):
     n_own = ex.n_own
     dz_l, db_r2l, dz_r, db_l2r = dz
     p_left, p_right, p_agg_l, p_agg_r, p_left_new, p_right_new = prev.saved_tensors[:6]
-    dw_rel_r2l, dw_root_r2l = (wgf(dz_l, agg_l) if need[6] else None), (wgf(dz_l, left) if need[8] else None)
-
-    def fused(G1, W1, G2, W2, addend, y, x1, x2, two_pass):
-        r = _fc.input_grad_relu_wgrad(G1, W1, G2, W2, addend, y, x1, x2)
-        if r is None:  # operands the fused kernel does not take: the stored gradient, then conv1's pass
-            r = _fc.relu_wgrad_smallk(two_pass(), y, 1.0, x1, x2, True)
-        return r
-
-    # conv1's left2right (owned variables): the source-side term's halo partials to the owners, then the
-    # fused GEMM -- in the association the one-GPU path picks (conv._src_first): (A^T dZ_l) W_rel over
-    # the variables, or A^T (dZ_l W_rel) with the GEMM over the constraints and the reduced SpMM output
-    # as the fused kernel's addend
     from .conv import _src_first
 
-    if _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4):
-        T_own = ex.start_reduce(spmm_forward(AT, dz_l), inplace=True).finish()
-
-        def g_right_own():
-            g = igf(T_own, w_rel_r2l)
-            return igf(dz_r, w_root_l2r, out=g, accumulate=True)
-        wk_r = fused(T_own, w_rel_r2l, dz_r, w_root_l2r, None, p_right_new[:n_own], p_agg_r[:n_own],
-                     p_right[:n_own], g_right_own)
-    else:
-        P_own = ex.start_reduce(spmm_forward(AT, igf(dz_l, w_rel_r2l)), inplace=True).finish()
-
-        def g_right_own():
-            return igf(dz_r, w_root_l2r, out=P_own.clone(), accumulate=True)
-        wk_r = fused(dz_r, w_root_l2r, None, None, P_own, p_right_new[:n_own], p_agg_r[:n_own], p_right[:n_own],
-                     g_right_own)
-
-    # this layer's left2right weight gradients and conv1's right2left (constraints, local)
+    # Both exchanges are issued first and finished where their rows are consumed, so they run under the
+    # four weight-gradient GEMMs (which need neither): the source-side term of conv1's left2right
+    # (below) to the owners, and the owners' aggregate gradient to the halo rows.
+    src_first = _src_first(A, dz_l.shape[1], w_rel_r2l.shape[1], 4)
+    red = ex.start_reduce(spmm_forward(AT, dz_l if src_first else igf(dz_l, w_rel_r2l)), inplace=True)
     f_out, f_in = dz_r.shape[1], w_rel_l2r.shape[1]
     use_t = _src_first(AT, f_out, f_in, 4) or agg_r is None
     rel_from_t = need[3] and (agg_r is None or (use_t and A.n_rows < n_own))
-    dw_rel_l2r = wgf(dz_r, agg_r[:n_own]) if need[3] and not rel_from_t else None
-    dw_root_l2r = wgf(dz_r, right[:n_own]) if need[5] else None
     if use_t and right.shape[0] == n_own and dz_r.is_contiguous():
         full = dz_r  # no halo rows (one rank): dZ_r is the whole source table, no copy
     else:
@@ -844,7 +862,40 @@ def _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward):
             full[:n_own] = dz_r
         else:
             igf(dz_r, w_rel_l2r, out=full[:n_own])
-    ex.start_broadcast_(full).finish()
+    bc = ex.start_broadcast_(full)
+    # ... under: this layer's weight gradients, both directions
+    dw_rel_r2l, dw_root_r2l = (wgf(dz_l, agg_l) if need[6] else None), (wgf(dz_l, left) if need[8] else None)
+    dw_rel_l2r = wgf(dz_r, agg_r[:n_own]) if need[3] and not rel_from_t else None
+    dw_root_l2r = wgf(dz_r, right[:n_own]) if need[5] else None
+
+    def fused(G1, W1, G2, W2, addend, y, x1, x2, two_pass):
+        r = _fc.input_grad_relu_wgrad(G1, W1, G2, W2, addend, y, x1, x2)
+        if r is None:  # operands the fused kernel does not take: the stored gradient, then conv1's pass
+            r = _fc.relu_wgrad_smallk(two_pass(), y, 1.0, x1, x2, True)
+        return r
+
+    # conv1's left2right (owned variables): the source-side term's halo partials reduced to the owners,
+    # then the fused GEMM -- in the association the one-GPU path picks (conv._src_first): (A^T dZ_l) W_rel
+    # over the variables, or A^T (dZ_l W_rel) with the GEMM over the constraints and the reduced SpMM
+    # output as the fused kernel's addend
+    if src_first:
+        T_own = red.finish()
+
+        def g_right_own():
+            g = igf(T_own, w_rel_r2l)
+            return igf(dz_r, w_root_l2r, out=g, accumulate=True)
+        wk_r = fused(T_own, w_rel_r2l, dz_r, w_root_l2r, None, p_right_new[:n_own], p_agg_r[:n_own],
+                     p_right[:n_own], g_right_own)
+    else:
+        P_own = red.finish()
+
+        def g_right_own():
+            return igf(dz_r, w_root_l2r, out=P_own.clone(), accumulate=True)
+        wk_r = fused(dz_r, w_root_l2r, None, None, P_own, p_right_new[:n_own], p_agg_r[:n_own], p_right[:n_own],
+                     g_right_own)
+
+    # conv1's right2left (constraints, local) from the broadcast aggregate gradient
+    bc.finish()
     t = spmm_forward(A, full)
     if use_t:
         if rel_from_t:
@@ -939,10 +990,12 @@ class PartitionedCSR:
         return self.local.device
 
     def two_direction_conv(self, left, right, left2right, right2left, relu=False, dropout=0.0, opts=None,
-                           fold_in=False):
+                           fold_in=False, feeds_conv=False):
         """GraphConvTwoDirection.forward on this partition (one autograd node).  ``fold_in``: (left,
         right) feed nothing but this layer (GCN_FC's chain): if conv1 produced them, its weight
-        gradients come out of this layer's input-gradient GEMMs."""
+        gradients come out of this layer's input-gradient GEMMs.  ``feeds_conv``: the outputs go only
+        to another partitioned layer (GCN_FC's chain), which settles the broadcast of their halo rows
+        itself -- it stays in flight under that layer's first GEMM and SpMM (Exchange.defer)."""
         if self.orient != "cons" or left.dtype != torch.float32 or _local_spmm is not _product_spmm:
             return None  # generic per-direction path (oracle tests, bf16)
         from .options import DEFAULT
@@ -951,7 +1004,7 @@ class PartitionedCSR:
         return _PartTwoDirection.apply(left, right, self, left2right.lin_rel.weight, left2right.lin_rel.bias,
                                        left2right.lin_root.weight, right2left.lin_rel.weight,
                                        right2left.lin_rel.bias, right2left.lin_root.weight, bool(relu),
-                                       float(dropout), opts, prev)
+                                       float(dropout), opts, prev, bool(feeds_conv))
 
     def two_direction_heads(self, left, right, left2right, right2left, lin_left, lin_right, dropout=0.0, opts=None,
                             fold_in=False):

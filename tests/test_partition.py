@@ -328,3 +328,48 @@ def test_plan_partition_local_world_one():
     g = _graph()
     _plan_fields_equal(part.plan_partition_local(g.row, g.col, g.val, g.m, g.n, 1, 0),
                        part.plan_partition(g.row, g.col, g.val, g.m, g.n, 1, 0))
+
+
+def _defer_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lpgnn import partition as part
+
+        g = _graph()
+        plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
+        ex = part.Exchange(plan, "cpu")
+        assert ex.active and plan.halo.shape[0] > 0
+        # every local row holds its global id: after the broadcast the halo rows hold their owners' ids
+        full = torch.full((plan.n_local, 3), -1.0)
+        full[:plan.n_own] = torch.from_numpy(plan.owned.astype(np.float32))[:, None]
+        other = torch.zeros(plan.n_local, 3)
+        ex.defer(full, ex.start_broadcast_(full, quiet=True))
+        ex.defer(other, ex.start_broadcast_(other))
+        v0 = full._version
+        # in flight: the halo rows are not written until the consumer settles them
+        assert bool((full[plan.n_own:] == -1).all())
+        ex.settle(other)
+        assert len(ex._deferred) == 1 and bool((full[plan.n_own:] == -1).all())
+        ex.settle(full)
+        assert ex._deferred == []
+        assert torch.equal(full[:, 0], torch.from_numpy(plan.local_vars.astype(np.float32)))
+        assert full._version == v0  # quiet: written past autograd's version counter
+        ex.settle(full)  # nothing pending: a no-op
+        # a later exchange on the same group still pairs up after deferred ones (issue order)
+        ex.defer(full, ex.start_broadcast_(full))
+        red = ex.reduce_rows(torch.ones(plan.n_local, 2), inplace=False)
+        ex.settle_all()
+        assert ex._deferred == [] and red.shape == (plan.n_own, 2)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_deferred_broadcast_settles_on_demand(tmp_path):
+    """Exchange.defer / settle (the partitioned forward leaves a layer output's halo broadcast in
+    flight for the next layer): the halo rows stay untouched until settled, settling one target leaves
+    the others pending, and every deferred broadcast lands its owners' rows exactly."""
+    mp.spawn(_defer_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert (tmp_path / f"ok{r}").exists()
