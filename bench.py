@@ -77,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-steps", type=int, default=1, help="oracle CPU steps for cpu_baseline (0 = skip)")
     ap.add_argument("--profile-only", action="store_true", help="no CPU baseline, no sub-records (rocprof runs)")
     ap.add_argument("--print-workload", action="store_true", help="print the workload string and exit")
+    ap.add_argument("--vendor", type=int, default=1,
+                    help="1: time rocSPARSE's SpMM (torch.sparse.mm) beside ours on the c2 graph at N=1 (vendor_spmm)")
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned RCCL path even at N=1 (the N>1 code path)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -209,6 +211,40 @@ def cpu_inference(g, hids, depth, steps, fp16=False):
     for _ in range(steps):
         infer()
     return (time.perf_counter() - t0) / steps, threads
+
+
+def vendor_spmm(g, F, dev, reps=5):
+    """The vendor sparse library on the headline SpMM, on the GPU beside ours: rocSPARSE through
+    torch.sparse.mm on a CSR tensor (fp32, F = hid) against lpg_spmm_f32, per direction, median of
+    `reps` after one warm-up (HIP events on the current stream).  Not a baseline the metric uses."""
+    import lpgnn
+    from lpgnn.sparse import spmm_forward
+
+    adj = lpgnn.BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(5)
+    out = {}
+    for d, csr in (("cons<-vars", adj.fwd), ("vars<-cons", adj.bwd)):
+        x = torch.randn(csr.n_cols, F, device=dev, generator=gen)
+        sp = torch.sparse_csr_tensor(csr.rowptr, csr.col.long(), csr.val, size=(csr.n_rows, csr.n_cols))
+
+        def med(fn):
+            fn()
+            ts = []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                torch.cuda.synchronize(dev)
+                ts.append(e0.elapsed_time(e1))
+            return float(np.median(ts))
+        t_v = med(lambda: torch.sparse.mm(sp, x))
+        t_o = med(lambda: spmm_forward(csr, x))
+        diff = float((torch.sparse.mm(sp, x) - spmm_forward(csr, x)).abs().max())
+        out[d] = {"rocsparse_ms": t_v, "rocsparse_edges_per_s": csr.nnz / (t_v / 1e3), "ours_ms": t_o,
+                  "ours_edges_per_s": csr.nnz / (t_o / 1e3), "speedup": t_v / t_o, "max_abs_diff": diff}
+        del x, sp
+    return out
 
 
 def cpu_spmm(g, F, reps=3):
@@ -679,6 +715,15 @@ def main():
                                "s_per_step": cdt}
         out["cpu_spmm"] = dict(cpu_spmm(g, args.hids), threads=threads,
                                note="F=hid SpMM alone on the host, median of 3 (SURVEY.md 8d CPU numbers)")
+    if rank == 0 and world == 1 and not args.inference and not args.partitioned and args.config == "c2" and \
+            g is not None and not args.profile_only and args.vendor:
+        import warnings
+
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")  # torch's "sparse CSR support is in beta" notice
+            out["vendor_spmm"] = dict(vendor_spmm(g, args.hids, dev),
+                                      note="rocSPARSE (torch.sparse.mm, CSR, fp32) on the same graph and GPU, "
+                                           "beside lpg_spmm_f32; not part of value")
     del g
     if args.inference:
         out["mode"] = head.get("mode")
