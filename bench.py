@@ -400,9 +400,13 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
     # gradients; K >= hid): MFMA utilisation.  x3 = fp32 through the exact three-way bf16 split,
     # 6 bf16 MFMA products per fp32 product, so its MFMA-bound peak is the dense bf16 peak / 6.
     fc_keys = [k for k in kern if k[0] in ("fc", "wgrad") and k[3] >= hids and k[2] >= 64]
-    x3 = any(str(k[4]).endswith("x3") for k in fc_keys)
+    # matrix-core products per fp32 product: x3 six bf16, f16x2 three fp16 (LPGNN_FC_ARITH=f16x2)
+    prods = lambda k: 6 if str(k[4]).endswith("x3") else 3 if str(k[4]).endswith("f16x2") else 1  # noqa: E731
+    x3 = any(prods(k) > 1 for k in fc_keys)
+    f16x2 = any(prods(k) == 3 for k in fc_keys)
     half = esz == 2
     fc_flops = sum(kern[k][0] * 2.0 * k[1] * k[2] * k[3] for k in fc_keys)
+    fc_work = sum(kern[k][0] * 2.0 * k[1] * k[2] * k[3] * prods(k) for k in fc_keys)
     fc_ms = sum(kern[k][1] for k in fc_keys)
     fc_launches = sum(kern[k][0] for k in fc_keys)
     # RCCL exchanges (lpgnn.partition._Pending): issue -> consumption span and the compute stream's
@@ -411,7 +415,7 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
     ex_exposed = sum(v[1] for k, v in kern.items() if k[0] == "exchange" and k[4] == "exposed")
     ex_n = sum(v[0] for k, v in kern.items() if k[0] == "exchange" and k[4] == "span")
     mine = dict(dt=dt, edges=launches * local_nnz, bytes=bytes_total, spmm_ms=spmm_ms, launches=launches,
-                fc_flops=fc_flops, fc_ms=fc_ms, ex_span=ex_span, ex_exposed=ex_exposed, ex_n=ex_n)
+                fc_flops=fc_flops, fc_work=fc_work, fc_ms=fc_ms, ex_span=ex_span, ex_exposed=ex_exposed, ex_n=ex_n)
     every = ctx.gather(mine)
     dt_max = max(r["dt"] for r in every)
     world = len(every)
@@ -438,18 +442,25 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
     fc_tf_all = sum(r["fc_flops"] for r in every) / (max(r["fc_ms"] for r in every) * world / 1e3) / 1e12 \
         if any(r["fc_ms"] for r in every) else 0.0
     fc_peak = BF16_MFMA_PEAK_TFLOPS if half else (BF16_MFMA_PEAK_TFLOPS / 6 if x3 else FP32_MFMA_PEAK_TFLOPS)
+    work_tf = sum(r["fc_work"] for r in every) / (max(r["fc_ms"] for r in every) * world / 1e3) / 1e12 \
+        if any(r["fc_ms"] for r in every) else 0.0
+    if f16x2 and not half:  # mixed products per fp32 product: the peak the launches' matrix-core work implies
+        fc_peak = fc_tf_all * BF16_MFMA_PEAK_TFLOPS / work_tf if work_tf > 0 else BF16_MFMA_PEAK_TFLOPS / 6
     fc = {"bound": "mfma", "achieved": fc_tf_all, "peak": fc_peak, "unit": "TFLOP/s", "frac": fc_tf_all / fc_peak,
           "launches": fc_launches,
           "kernel": ("lpg fc_f16 (hidden-width FC forward on v_mfma_f32_16x16x32_f16)" if fp16 else
                      "lpg fc_bf16 + wgrad_bf16 (hidden-width GEMMs, fwd + bwd: FC forward, input "
                      "gradients on the FC kernel, weight gradients)" if half else
+                     "lpg fc_x3_wide f16x2 + wgrad_x3 (hidden-width GEMMs, fwd + bwd; fp32 via two "
+                     "row-scaled fp16 terms (3 products) and the exact 3-way bf16 split (6); peak = dense "
+                     "bf16 over the launches' products)" if f16x2 and not half else
                      "lpg fc_fwd_x3 + wgrad_x3 (hidden-width GEMMs, fwd + bwd; fp32 via exact "
                      "3-way bf16 split, peak = dense bf16 / 6)" if x3 else
                      "lpg fc_fwd_f32 (hidden GraphConv FC, fwd)"),
           "fp32_mfma_peak_frac": None if half else fc_tf_all / FP32_MFMA_PEAK_TFLOPS,
           # the bf16 MFMA work these launches issue (x3: 6 bf16 products per fp32 product),
           # comparable with a plain bf16 GEMM's rate on this chip
-          "bf16_mfma_equiv_tflops": fc_tf_all * (6 if x3 and not half else 1)}
+          "bf16_mfma_equiv_tflops": work_tf if not half else fc_tf_all}
     dirs = {}
     for k, v in per_launch.items():
         if k[0] != "spmm" or k[3] != hids:

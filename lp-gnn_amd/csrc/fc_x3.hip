@@ -91,6 +91,9 @@ struct X3Args {
   // reads at 200 K x (1024 + 1024) -> 1024: 10.1 GB -> 6.7 GB per launch, 1-2 % faster
   // (profiles/r04_pmc_fc_x3_k2048_probe.json, r04_x3_order_ab.log)
   int32_t order;
+  // "f16x2" operands (fc_x3_wide<..., F16 = true>): sa[m] = the power-of-2 scale of A row m (over both
+  // k phases), sw[n] = that of W row n (both phases; W then holds two fp16 planes h, l of W * sw)
+  const float *sa, *sw;
 };
 
 // dst plane p [rows, cols] (ldd) = term p of src (transposed: src is [cols, rows]).
@@ -114,6 +117,80 @@ __global__ __launch_bounds__(256) void split3_planes(int64_t rows, int64_t cols,
       d[ps + 1] = (uint16_t)(m >> 16);
       d[2 * ps + 1] = (uint16_t)(l >> 16);
     }
+  }
+}
+
+// ---- f16x2 operand preparation ---------------------------------------------------
+// The power-of-2 scale that puts a row's largest |x| in [2^14, 2^15): 2^(15 - e) for max = f 2^e,
+// f in [0.5, 1); 1 for an all-zero or non-finite row (NaN / Inf propagate through the split as in
+// fp32).  e is clamped to [-100, 120] so the scale and its inverse stay normal fp32 numbers.
+__device__ __forceinline__ float f16x2_scale(float mx) {
+  if (!(mx > 0.f) || !(mx <= 3.4e38f)) return 1.f;
+  int e;
+  frexpf(mx, &e);
+  e = e < -100 ? -100 : (e > 120 ? 120 : e);
+  return ldexpf(1.f, 15 - e);
+}
+
+// sa[m] for the rows of [A1 | A2] (16-byte aligned rows, K1, K2 multiples of 4): one wave a row
+__global__ __launch_bounds__(256) void rowscale_f32(int64_t M, int64_t K1, const float *__restrict__ A1, int64_t lda1,
+                                                    int64_t K2, const float *__restrict__ A2, int64_t lda2,
+                                                    float *__restrict__ sa) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += (int64_t)gridDim.x * 4) {
+    float mx = 0.f;
+    for (int ph = 0; ph < 2; ++ph) {
+      const float *a = ph ? A2 : A1;
+      const int64_t K = ph ? K2 : K1;
+      if (!a || K == 0) continue;
+      a += row * (ph ? lda2 : lda1);
+      for (int64_t k = 4 * lane; k < K; k += 256) {
+        const f32x4 v = *reinterpret_cast<const f32x4 *>(a + k);
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (lane == 0) sa[row] = f16x2_scale(mx);
+  }
+}
+
+// W for the f16x2 kernels: row r of [src1 | src2] (or column r of each with transpose) times its scale
+// sw[r], as two fp16 planes h = RNE_f16(x s), l = RNE_f16(x s - h) at dst + p * ps; one block a row
+__global__ __launch_bounds__(256) void split_f16x2_rows(int64_t rows, int64_t cols1, const float *__restrict__ src1,
+                                                        int64_t lds1, int64_t cols2, const float *__restrict__ src2,
+                                                        int64_t lds2, int32_t transpose, uint16_t *__restrict__ dst1,
+                                                        int64_t ldd1, uint16_t *__restrict__ dst2, int64_t ldd2,
+                                                        int64_t ps, float *__restrict__ sw) {
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    auto at = [&](int ph, int64_t c) {
+      const float *src = ph ? src2 : src1;
+      const int64_t ld = ph ? lds2 : lds1;
+      return transpose ? src[c * ld + r] : src[r * ld + c];
+    };
+    float mx = 0.f;
+    for (int ph = 0; ph < 2; ++ph)
+      for (int64_t c = tid; c < (ph ? cols2 : cols1); c += 256) mx = fmaxf(mx, fabsf(at(ph, c)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (lane == 0) red[wave] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    const float sc = f16x2_scale(mx);
+    for (int ph = 0; ph < 2; ++ph) {
+      uint16_t *d = (ph ? dst2 : dst1) + r * (ph ? ldd2 : ldd1);
+      for (int64_t c = tid; c < (ph ? cols2 : cols1); c += 256) {
+        const float v = at(ph, c) * sc;
+        const _Float16 h = (_Float16)v;
+        const _Float16 l = (_Float16)sub_f32(v, (float)h);
+        d[c] = __builtin_bit_cast(uint16_t, h);
+        d[ps + c] = __builtin_bit_cast(uint16_t, l);
+      }
+    }
+    if (tid == 0) sw[r] = sc;
   }
 }
 
@@ -394,19 +471,27 @@ lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
 // k order and product sequence per output as fc_fwd_x3_16: the same C, bit for bit.
 // Requires lda1 == lda2, ldw1 == ldw2, ps1 == ps2 (one offset set for both k phases; the host
 // falls back to fc_fwd_x3_16 otherwise).
-template <int WM, int TM, int TN, int MINW, bool RELU, bool HEADS, bool WGK = false>
+//
+// F16 ("f16x2", round 5): A split in registers into two fp16 terms of (A row * sa[row]) and W given as
+// two fp16 planes of (W row * sw[col]); per (i, j) three v_mfma_f32_16x16x32_f16 -- hh into accH, hl
+// and lh into accL -- instead of six bf16 ones, and the sum rescaled by 1 / (sa sw) (powers of 2:
+// exact) before the epilogue.  Representation error <= ~3 * 2^-22 of sum |a b| (a quarter of an fp32
+// SGEMM's own; tools/experiments/split_error.py), half the matrix-core work.
+template <int WM, int TM, int TN, int MINW, bool RELU, bool HEADS, bool WGK = false, bool F16 = false>
 __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   constexpr int NW = WM;
+  constexpr int NP = F16 ? 2 : 3;  // W planes
   constexpr int BM = WM * TM * 16, BN = TN * 16;
   constexpr int A_BYTES = BM * BK * 4, WP_BYTES = BN * BK * 2;
-  constexpr int TILE_BYTES = A_BYTES + 3 * WP_BYTES;
+  constexpr int TILE_BYTES = A_BYTES + NP * WP_BYTES;
+  constexpr int SM_BYTES = 2 * (A_BYTES + 3 * WP_BYTES);  // both arithmetics: the epilogue images fit
   // DMA pieces of 1 KiB (one wave instruction): A pieces (8 rows x 128 B) first, then the W
   // pieces (16 rows x 64 B, plane by plane) -- piece q lands at q * 1 KiB of the tile image;
   // wave w moves pieces w, w + NW, ... (the last round partial when NW does not divide PT)
-  constexpr int PA_T = BM / 8, PT = PA_T + 3 * (BN / 16), PPW = (PT + NW - 1) / NW;
+  constexpr int PA_T = BM / 8, PT = PA_T + NP * (BN / 16), PPW = (PT + NW - 1) / NW;
   static_assert(BM % 8 == 0 && BN % 16 == 0, "whole pieces");
   static_assert(TN % 2 == 0, "W fragments are consumed in pairs");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TILE_BYTES];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SM_BYTES];
 
   const int64_t nwg = a.mt * a.nt;
   const int64_t bid = blockIdx.x;
@@ -451,8 +536,8 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   const uint64_t pa1 = (uint64_t)(a.A1 + m0 * a.lda1), pw1 = (uint64_t)(a.W1 + n0 * a.ldw1);
   const uint64_t pa2 = a.A2 ? (uint64_t)(a.A2 + m0 * a.lda1) : pa1, pw2 = a.W2 ? (uint64_t)(a.W2 + n0 * a.ldw1) : pw1;
   const uint32_t na1 = (uint32_t)(((mrows - 1) * a.lda1 + kp1) * 4), na2 = (uint32_t)(((mrows - 1) * a.lda1 + kp2) * 4);
-  const uint32_t nw1 = (uint32_t)((2 * a.ps1 + (ncols - 1) * a.ldw1 + kp1) * 2);
-  const uint32_t nw2 = (uint32_t)((2 * a.ps1 + (ncols - 1) * a.ldw1 + kp2) * 2);
+  const uint32_t nw1 = (uint32_t)(((NP - 1) * a.ps1 + (ncols - 1) * a.ldw1 + kp1) * 2);
+  const uint32_t nw2 = (uint32_t)(((NP - 1) * a.ps1 + (ncols - 1) * a.ldw1 + kp2) * 2);
   uint32_t vo[PPW];
 #pragma unroll
   for (int p = 0; p < PPW; ++p) {
@@ -495,12 +580,68 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
 
   const int fr = lane & 15, fg = lane >> 4;
   const int rA0 = wave * TM * 16 + fr;
+  float sA[F16 ? TM : 1];  // F16: the scales of the A rows this lane splits
+  if constexpr (F16) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int64_t row = m0 + rA0 + i * 16;
+      sA[i] = a.sa[row < a.M ? row : a.M - 1];
+    }
+  }
 
   if (nk > 0) stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   int b = 0;
+  if constexpr (F16) {
+    for (int t = 0; t < nk; ++t) {
+      if (t + 1 < nk) stage(b ^ 1, t + 1);
+      const unsigned char *T = smem + b * TILE_BYTES;
+      Split2 av[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const unsigned char *ra = T + (rA0 + i * 16) * (BK * 4);
+        av[i] = split2f16(*reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg) * 16),
+                          *reinterpret_cast<const f32x4 *>(ra + swzA(rA0 + i * 16, 2 * fg + 1) * 16), sA[i]);
+      }
+      auto ldb = [&](int j, f16x8(&bj)[2]) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          bj[p] = *reinterpret_cast<const f16x8 *>(T + A_BYTES + p * WP_BYTES + (j * 16 + fr) * (BK * 2) +
+                                                   swzW(j * 16 + fr, fg) * 16);
+      };
+      auto mfma3 = [&](int i, int j, const f16x8(&bj)[2]) {
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i].l, bj[0], accL[i][j], 0, 0, 0);
+        accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i].h, bj[1], accL[i][j], 0, 0, 0);
+        accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i].h, bj[0], accH[i][j], 0, 0, 0);
+      };
+      f16x8 c0[2], c1[2];
+      ldb(0, c0);
+      ldb(1, c1);
+#pragma unroll
+      for (int j = 0; j < TN; j += 2) {
+        f16x8 n0_[2], n1_[2];
+        if (j + 2 < TN) {
+          ldb(j + 2, n0_);
+          ldb(j + 3, n1_);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          mfma3(i, j, c0);
+          mfma3(i, j + 1, c1);
+        }
+        if (j + 2 < TN) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p) c0[p] = n0_[p], c1[p] = n1_[p];
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // tile t+1 landed; every wave done with tile t
+      asm volatile("" ::: "memory");
+      b ^= 1;
+    }
+  } else
   for (int t = 0; t < nk; ++t) {
     if (t + 1 < nk) stage(b ^ 1, t + 1);
     const unsigned char *T = smem + b * TILE_BYTES;
@@ -558,6 +699,27 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = accH[i][j] + accL[i][j];
+  if constexpr (F16) {  // undo the scales: output (row, col) times 1 / sa[row] times 1 / sw[col] (exact)
+    float ia[TM][4], iw[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = mw + i * 16 + 4 * fg + r;
+        ia[i][r] = 1.f / a.sa[row < a.M ? row : a.M - 1];
+      }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = nw + j * 16 + fr;
+      iw[j] = 1.f / a.sw[col < a.N ? col : a.N - 1];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] * ia[i][r] * iw[j];
+  }
   // fused heads (hn <= 3 here; the host routes hn = 4 to fc_fwd_x3_16): the store loops also put
   // each output into a per-wave LDS image (the tile buffers are free: every wave passed the last
   // k-tile's barrier), and a second pass reads them back column block by column block into this
@@ -575,7 +737,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
     // is never stored.  (The first form loaded Y and C per accumulator register before the images,
     // one dependent 4-byte load after another: 2.94 ms against 1.76 for the plain launch at 200 K rows.)
     constexpr int KP = 20, U = 4;
-    static_assert((NW * TM * 16 * HP + BM * KP) * 4 <= 2 * TILE_BYTES, "images fit the tile buffers");
+    static_assert((NW * TM * 16 * HP + BM * KP) * 4 <= SM_BYTES, "images fit the tile buffers");
     float *const wimg = reinterpret_cast<float *>(smem);
     float *const xs = wimg + NW * TM * 16 * HP;
     const int ks = a.wk1 + a.wk2;
@@ -665,7 +827,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
     }
     return;
   }
-  static_assert(!HEADS || NW * TM * 16 * HP * 4 <= 2 * TILE_BYTES, "heads image fits the tile buffers");
+  static_assert(!HEADS || NW * TM * 16 * HP * 4 <= SM_BYTES, "heads image fits the tile buffers");
   float *const himg = reinterpret_cast<float *>(smem) + wave * (TM * 16 * HP) + 4 * fg * HP + fr;
   auto hput = [&](int i, int r, int j, float v) {
     if constexpr (HEADS) himg[(i * 16 + r) * HP + j * 16] = v;
@@ -829,22 +991,25 @@ bool wide_ok(const X3Args &a, int64_t BM, int64_t BN) {
   return (BM * a.lda1 + K) * 4 < ((int64_t)1 << 31) && (2 * a.ps1 + BN * a.ldw1 + K) * 2 < ((int64_t)1 << 31);
 }
 
-template <int WM, int TM, int TN, int MINW, bool HEADS = false, bool WGK = false>
+template <int WM, int TM, int TN, int MINW, bool HEADS = false, bool WGK = false, bool F16 = false>
 lpg_status launch_x3_wide(X3Args a, bool relu, hipStream_t s) {
   constexpr int BM = WM * TM * 16, BN = TN * 16, NT = 64 * WM;
   a.mt = (a.M + BM - 1) / BM;
   a.nt = (a.N + BN - 1) / BN;
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
+  LPG_REQUIRE(!F16 || (a.sa && a.sw), "lpg_fc_f16x2: the row scales are missing");
   if constexpr (WGK) {
-    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, false, false, true>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, false, false, true, F16>), dim3((unsigned)nwg), dim3(NT), 0, s,
+                       a);
     LPG_HIP(hipGetLastError());
     return LPG_OK;
   }
   if (relu)
-    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, true, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, true, HEADS, false, F16>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
   else
-    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, false, HEADS>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, false, HEADS, false, F16>), dim3((unsigned)nwg), dim3(NT), 0, s,
+                       a);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }
@@ -1069,6 +1234,39 @@ constexpr int kX3Kernels = 3;
 
 using namespace lpg;
 
+extern "C" lpg_status lpg_rowscale_f32(int64_t M, int64_t K1, const float *A1, int64_t lda1, int64_t K2,
+                                       const float *A2, int64_t lda2, float *scale, void *stream) {
+  LPG_REQUIRE(M >= 0 && K1 >= 0 && K2 >= 0, "lpg_rowscale_f32: negative size");
+  if (M == 0) return LPG_OK;
+  LPG_REQUIRE(scale && (K1 == 0 || A1) && (K2 == 0 || A2), "lpg_rowscale_f32: NULL pointer");
+  LPG_REQUIRE(K1 % 4 == 0 && K2 % 4 == 0 && (K1 == 0 || (lda1 >= K1 && lda1 % 4 == 0 && aligned16(A1))) &&
+                  (K2 == 0 || (lda2 >= K2 && lda2 % 4 == 0 && aligned16(A2))),
+              "lpg_rowscale_f32: K and leading dimensions multiples of 4 floats, rows 16-byte aligned");
+  int64_t blocks = (M + 3) / 4;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(rowscale_f32, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), M, K1,
+                     K1 ? A1 : nullptr, lda1, K2, K2 ? A2 : nullptr, lda2, scale);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_split_f16x2(int64_t rows, int64_t cols1, const float *src1, int64_t lds1, int64_t cols2,
+                                      const float *src2, int64_t lds2, int32_t transpose, uint16_t *dst1,
+                                      int64_t ldd1, uint16_t *dst2, int64_t ldd2, int64_t plane_stride, float *scale,
+                                      void *stream) {
+  LPG_REQUIRE(rows >= 0 && cols1 >= 0 && cols2 >= 0, "lpg_split_f16x2: negative size");
+  if (rows == 0) return LPG_OK;
+  LPG_REQUIRE(scale && (cols1 == 0 || (src1 && dst1)) && (cols2 == 0 || (src2 && dst2)), "lpg_split_f16x2: NULL pointer");
+  LPG_REQUIRE((cols1 == 0 || (lds1 >= (transpose ? rows : cols1) && ldd1 >= cols1 && plane_stride >= rows * ldd1)) &&
+                  (cols2 == 0 || (lds2 >= (transpose ? rows : cols2) && ldd2 >= cols2 && plane_stride >= rows * ldd2)),
+              "lpg_split_f16x2: bad leading dimension / plane stride");
+  int64_t blocks = rows < 16384 ? rows : 16384;
+  hipLaunchKernelGGL(split_f16x2_rows, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), rows, cols1, src1,
+                     lds1, cols2, src2, lds2, transpose, dst1, ldd1, dst2, ldd2, plane_stride, scale);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
 extern "C" lpg_status lpg_split3_f32(int64_t rows, int64_t cols, const float *src, int64_t lds, int32_t transpose,
                                      uint16_t *dst, int64_t ldd, int64_t plane_stride, void *stream) {
   LPG_REQUIRE(rows >= 0 && cols >= 0, "lpg_split3_f32: negative size");
@@ -1110,11 +1308,12 @@ static lpg_status x3_args(int64_t M, int64_t N, int64_t K1, const float *A1, int
   return LPG_OK;
 }
 
-extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
-                                    const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
-                                    int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
-                                    float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
-                                    int64_t row_offset, const int64_t *row_keys, void *stream) {
+// the plain FC of both arithmetics: x3 (sa == nullptr) or f16x2 (sa, sw: the row scales; W two fp16 planes)
+static lpg_status fc_x3_plain(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1, const uint16_t *W1,
+                              int64_t ldw1, int64_t ps1, int64_t K2, const float *A2, int64_t lda2,
+                              const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *sa, const float *sw,
+                              const float *bias, float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                              int64_t row_offset, const int64_t *row_keys, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_f32: negative size");
   if (M == 0 || N == 0) return LPG_OK;
   LPG_REQUIRE(!(flags & LPG_FC_HEADS_ONLY), "lpg_fc_x3_f32: LPG_FC_HEADS_ONLY needs the heads entry");
@@ -1126,8 +1325,38 @@ extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const floa
   const bool relu = flags & 1;
   const int kern = (flags >> 8) & 15;
   a.order = kern == 2 ? 0 : kern == 3 ? 2 : 1;
+  if (sa) {
+    LPG_REQUIRE(sw, "lpg_fc_f16x2_f32: sw is NULL");
+    if (!wide_ok(a, 128, 128)) {
+      set_error("lpg_fc_f16x2_f32: operands the wide kernel does not take (lda1 == lda2, ldw1 == ldw2, ps1 == ps2)");
+      return LPG_ERR_UNSUPPORTED;
+    }
+    a.sa = sa;
+    a.sw = sw;
+    return launch_x3_wide<4, 2, 8, 2, false, false, true>(a, relu, s);
+  }
   if (kern != 1 && wide_ok(a, 128, 128)) return launch_x3_wide<4, 2, 8, 2>(a, relu, s);
   return launch_x3_16<4, 1, 2, 8>(a, relu, s);
+}
+
+extern "C" lpg_status lpg_fc_x3_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                    const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                    int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *bias,
+                                    float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                                    int64_t row_offset, const int64_t *row_keys, void *stream) {
+  return fc_x3_plain(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, nullptr, nullptr, bias, C, ldc,
+                     flags, dropout_p, seed, row_offset, row_keys, stream);
+}
+
+extern "C" lpg_status lpg_fc_f16x2_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                       const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                       int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *sa,
+                                       const float *sw, const float *bias, float *C, int64_t ldc, int32_t flags,
+                                       float dropout_p, uint64_t seed, int64_t row_offset, const int64_t *row_keys,
+                                       void *stream) {
+  LPG_REQUIRE(sa && sw, "lpg_fc_f16x2_f32: NULL row scales");
+  return fc_x3_plain(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, sa, sw, bias, C, ldc, flags,
+                     dropout_p, seed, row_offset, row_keys, stream);
 }
 
 extern "C" int64_t lpg_fc_x3_heads_workspace_bytes(int64_t M, int64_t N) {
@@ -1135,14 +1364,12 @@ extern "C" int64_t lpg_fc_x3_heads_workspace_bytes(int64_t M, int64_t N) {
   return ((N + 127) / 128) * M * 4 * (int64_t)sizeof(float);
 }
 
-extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
-                                          const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
-                                          int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2,
-                                          const float *bias, float *C, int64_t ldc, int32_t flags, float dropout_p,
-                                          uint64_t seed, int64_t row_offset, const int64_t *row_keys,
-                                          int32_t hn, const float *hw,
-                                          int64_t ldhw, const float *hb,
-                                          float *logits, int64_t ldl, void *workspace, void *stream) {
+static lpg_status fc_x3_heads(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1, const uint16_t *W1,
+                              int64_t ldw1, int64_t ps1, int64_t K2, const float *A2, int64_t lda2,
+                              const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *sa, const float *sw,
+                              const float *bias, float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                              int64_t row_offset, const int64_t *row_keys, int32_t hn, const float *hw, int64_t ldhw,
+                              const float *hb, float *logits, int64_t ldl, void *workspace, void *stream) {
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_x3_heads_f32: negative size");
   if (M == 0) return LPG_OK;
   LPG_REQUIRE(N > 0, "lpg_fc_x3_heads_f32: N must be positive");
@@ -1162,7 +1389,16 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
   // per-call alternative) takes fc_fwd_x3_16 -- the same C, bit for bit
   lpg_status r;
   a.order = ((flags >> 8) & 15) == 2 ? 0 : ((flags >> 8) & 15) == 3 ? 2 : 1;
-  if (hn <= 3 && ((flags >> 8) & 15) != 1 && wide_ok(a, 128, 128))
+  if (sa) {
+    LPG_REQUIRE(sw, "lpg_fc_f16x2_heads_f32: sw is NULL");
+    if (!(hn <= 3 && wide_ok(a, 128, 128))) {
+      set_error("lpg_fc_f16x2_heads_f32: operands the wide kernel does not take (hn <= 3, one offset set)");
+      return LPG_ERR_UNSUPPORTED;
+    }
+    a.sa = sa;
+    a.sw = sw;
+    r = launch_x3_wide<4, 2, 8, 2, true, false, true>(a, flags & 1, s);
+  } else if (hn <= 3 && ((flags >> 8) & 15) != 1 && wide_ok(a, 128, 128))
     r = launch_x3_wide<4, 2, 8, 2, true>(a, flags & 1, s);
   else
     r = launch_x3_16<4, 1, 2, 8, true>(a, flags & 1, s);
@@ -1172,6 +1408,31 @@ extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, cons
                      a.hpart, hb, logits, ldl);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
+}
+
+extern "C" lpg_status lpg_fc_x3_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                          const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                          int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2,
+                                          const float *bias, float *C, int64_t ldc, int32_t flags, float dropout_p,
+                                          uint64_t seed, int64_t row_offset, const int64_t *row_keys,
+                                          int32_t hn, const float *hw,
+                                          int64_t ldhw, const float *hb,
+                                          float *logits, int64_t ldl, void *workspace, void *stream) {
+  return fc_x3_heads(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, nullptr, nullptr, bias, C, ldc,
+                     flags, dropout_p, seed, row_offset, row_keys, hn, hw, ldhw, hb, logits, ldl, workspace, stream);
+}
+
+extern "C" lpg_status lpg_fc_f16x2_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                             const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2,
+                                             const float *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
+                                             int64_t ps2, const float *sa, const float *sw, const float *bias,
+                                             float *C, int64_t ldc, int32_t flags, float dropout_p, uint64_t seed,
+                                             int64_t row_offset, const int64_t *row_keys, int32_t hn, const float *hw,
+                                             int64_t ldhw, const float *hb, float *logits, int64_t ldl,
+                                             void *workspace, void *stream) {
+  LPG_REQUIRE(sa && sw, "lpg_fc_f16x2_heads_f32: NULL row scales");
+  return fc_x3_heads(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, sa, sw, bias, C, ldc, flags,
+                     dropout_p, seed, row_offset, row_keys, hn, hw, ldhw, hb, logits, ldl, workspace, stream);
 }
 
 extern "C" int64_t lpg_wgrad_x3_workspace_bytes(int64_t R, int64_t N, int64_t K) {
@@ -1221,14 +1482,14 @@ extern "C" int64_t lpg_fc_x3_relu_wgrad_workspace_bytes(int64_t M, int64_t N, in
   return smallk_fold_floats((M + 127) / 128, K + 1, N) * (int64_t)sizeof(float);
 }
 
-extern "C" lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
-                                               const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2,
-                                               const float *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
-                                               int64_t ps2, const float *C, int64_t ldc, int32_t flags, const float *Y,
-                                               int64_t ldy, int64_t ks1, const float *X1, int64_t ldx1, int64_t ks2,
-                                               const float *X2, int64_t ldx2, float *dW1, float *dW2, float *db,
-                                               void *workspace, void *stream) {
-  const char *name = "lpg_fc_x3_relu_wgrad_f32";
+static lpg_status fc_x3_relu_wgrad(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                   const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                   int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *sa,
+                                   const float *sw, const float *C, int64_t ldc, int32_t flags, const float *Y,
+                                   int64_t ldy, int64_t ks1, const float *X1, int64_t ldx1, int64_t ks2,
+                                   const float *X2, int64_t ldx2, float *dW1, float *dW2, float *db, void *workspace,
+                                   void *stream) {
+  const char *name = sa ? "lpg_fc_f16x2_relu_wgrad_f32" : "lpg_fc_x3_relu_wgrad_f32";
   LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "%s: negative size", name);
   LPG_REQUIRE((flags & ~LPG_FC_ACCUMULATE) == 0, "%s: only the accumulate flag is accepted, got 0x%x", name, flags);
   LPG_REQUIRE(ks1 >= 0 && ks2 >= 0 && ks1 + ks2 >= 1 && ks1 + ks2 <= 16, "%s: need 1 <= ks1 + ks2 <= 16", name);
@@ -1268,8 +1529,40 @@ extern "C" lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1,
   float *part = static_cast<float *>(workspace);
   a.wpart = part;
   a.order = 1;
-  lpg_status r = launch_x3_wide<4, 2, 8, 2, false, true>(a, false, s);
+  lpg_status r;
+  if (sa) {
+    LPG_REQUIRE(sw, "%s: sw is NULL", name);
+    a.sa = sa;
+    a.sw = sw;
+    r = launch_x3_wide<4, 2, 8, 2, false, true, true>(a, false, s);
+  } else {
+    r = launch_x3_wide<4, 2, 8, 2, false, true>(a, false, s);
+  }
   if (r != LPG_OK) return r;
   const int64_t mt = (M + 127) / 128;
   return smallk_fold(mt, N, (int)ks1, (int)ks, part, part + mt * (ks + 1) * N, dW1, dW2, db, s);
+}
+
+extern "C" lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                               const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2,
+                                               const float *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
+                                               int64_t ps2, const float *C, int64_t ldc, int32_t flags, const float *Y,
+                                               int64_t ldy, int64_t ks1, const float *X1, int64_t ldx1, int64_t ks2,
+                                               const float *X2, int64_t ldx2, float *dW1, float *dW2, float *db,
+                                               void *workspace, void *stream) {
+  return fc_x3_relu_wgrad(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, nullptr, nullptr, C, ldc,
+                          flags, Y, ldy, ks1, X1, ldx1, ks2, X2, ldx2, dW1, dW2, db, workspace, stream);
+}
+
+extern "C" lpg_status lpg_fc_f16x2_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                                  const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2,
+                                                  const float *A2, int64_t lda2, const uint16_t *W2, int64_t ldw2,
+                                                  int64_t ps2, const float *sa, const float *sw, const float *C,
+                                                  int64_t ldc, int32_t flags, const float *Y, int64_t ldy, int64_t ks1,
+                                                  const float *X1, int64_t ldx1, int64_t ks2, const float *X2,
+                                                  int64_t ldx2, float *dW1, float *dW2, float *db, void *workspace,
+                                                  void *stream) {
+  LPG_REQUIRE(sa && sw, "lpg_fc_f16x2_relu_wgrad_f32: NULL row scales");
+  return fc_x3_relu_wgrad(M, N, K1, A1, lda1, W1, ldw1, ps1, K2, A2, lda2, W2, ldw2, ps2, sa, sw, C, ldc, flags, Y,
+                          ldy, ks1, X1, ldx1, ks2, X2, ldx2, dW1, dW2, db, workspace, stream);
 }

@@ -52,6 +52,29 @@ __device__ __forceinline__ Split3 split3(f32x4 lo, f32x4 hi) {
   return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, Mi), __builtin_bit_cast(bf16x8, L)};
 }
 
+// ---- "f16x2": two fp16 planes per operand after a power-of-2 row scale (fc_x3.hip, F16 kernels) ----
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+struct Split2 {
+  f16x8 h, l;
+};
+
+// 8 consecutive k of one row, times the row's scale s (a power of 2: exact), as h = RNE_f16(x s) and
+// l = RNE_f16(x s - h) (the residual exact in fp32): |x s - h - l| <= 2^-22 |x s| while |x s| >= 2^-3,
+// and <= 2^-25 below (fp16 subnormals); the scale puts the row's largest |x| in [2^14, 2^15)
+__device__ __forceinline__ Split2 split2f16(f32x4 lo, f32x4 hi, float s) {
+  Split2 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float v = (i < 4 ? lo[i] : hi[i - 4]) * s;
+    const _Float16 h = (_Float16)v;
+    r.h[i] = h;
+    r.l[i] = (_Float16)sub_f32(v, (float)h);
+  }
+  return r;
+}
+
 // 4-B raw buffer load (v# in SGPRs: base and size wave-uniform): offsets at or past `nbytes` return
 // zeros, with no branch and no compare in the kernel
 __device__ __forceinline__ float buf_load1(const float *base, uint32_t nbytes, int voff, int soff) {

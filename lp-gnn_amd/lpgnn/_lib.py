@@ -100,6 +100,11 @@ HEADER_SYMBOLS = (
     "lpg_boundary_unpack_f32",
     "lpg_boundary_allreduce_f32",
     "lpg_spmm_partitioned_f32",
+    "lpg_rowscale_f32",
+    "lpg_split_f16x2",
+    "lpg_fc_f16x2_f32",
+    "lpg_fc_f16x2_heads_f32",
+    "lpg_fc_f16x2_relu_wgrad_f32",
 )
 
 c_i64, c_i32, c_p = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
@@ -220,6 +225,17 @@ def lib() -> ctypes.CDLL:
                                            c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p,
                                            c_i64, c_p, c_p, c_p, c_p, c_p]
     L.lpg_fc_x3_relu_wgrad_f32.restype = c_i32
+    # the f16x2 entries: the x3 signatures with the row scales (sa, sw) after ps2
+    for _x3, _f16 in (("lpg_fc_x3_f32", "lpg_fc_f16x2_f32"), ("lpg_fc_x3_heads_f32", "lpg_fc_f16x2_heads_f32"),
+                      ("lpg_fc_x3_relu_wgrad_f32", "lpg_fc_f16x2_relu_wgrad_f32")):
+        _t = getattr(L, _x3).argtypes
+        getattr(L, _f16).argtypes = _t[:14] + [c_p, c_p] + _t[14:]
+        getattr(L, _f16).restype = c_i32
+    L.lpg_rowscale_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p]
+    L.lpg_rowscale_f32.restype = c_i32
+    L.lpg_split_f16x2.argtypes = [c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_i64, c_i64,
+                                  c_p, c_p]
+    L.lpg_split_f16x2.restype = c_i32
     L.lpg_wgrad_x3_workspace_bytes.argtypes = [c_i64, c_i64, c_i64]
     L.lpg_wgrad_x3_workspace_bytes.restype = c_i64
     L.lpg_wgrad_x3_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p]

@@ -326,10 +326,10 @@ def _backward_core(ctx, saved, need, g_left, g_right, dz=None):
         if conv1 is not None:
             y, x1, x2 = conv1
             if t_src:
-                r = _fc.input_grad_relu_wgrad(T, w_rel, dz_root, w_root, None, y, x1, x2)
+                r = _fc.input_grad_relu_wgrad(T, w_rel, dz_root, w_root, None, y, x1, x2, arith=opts.arith)
             else:
                 r = _fc.input_grad_relu_wgrad(dz_root, w_root, None, None, spmm_forward(St, ig(dz, w_rel)), y, x1,
-                                              x2)
+                                              x2, arith=opts.arith)
             if r is not None:
                 return r
             g = src_root_grad(St, dz, w_rel, T, t_src, dz_root, w_root, x_in)  # the two-pass route
@@ -441,8 +441,8 @@ def foldable_producer(x: Tensor, opts: PathOptions = DEFAULT):
     # conv1's folded backward returns no input gradients and hands its outputs zero-stride gradients:
     # only when nothing differentiates through its inputs (features without requires_grad) or
     # observes its outputs' gradients (a hook / retain_grad on them) -- else the two-pass route
-    if opts.fold_conv1_wgrad and opts.arith == "x3" and getattr(g, "small_relu", False) and \
-            x.dtype == torch.float32 and g.opts.arith == "x3" and not any(g.needs_input_grad[:2]) and \
+    if opts.fold_conv1_wgrad and opts.arith in _fc.X3LIKE and getattr(g, "small_relu", False) and \
+            x.dtype == torch.float32 and g.opts.arith in _fc.X3LIKE and not any(g.needs_input_grad[:2]) and \
             not x.retains_grad and not x._backward_hooks:
         return g
     return None

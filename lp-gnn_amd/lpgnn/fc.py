@@ -54,6 +54,10 @@ def _pad_k(t: Tensor, mult: int = 4) -> Tensor:
 # "x3" = fp32 on the bf16 matrix cores through the exact three-way bf16 split (lpg_fc_x3_f32, lpg_wgrad_x3_f32).
 # The default of calls that pass no ``arith``; a model passes its own (GCN_FC(options=...), lpgnn.options).
 ARITH = _DEFAULT_OPTIONS.arith
+# "f16x2" = the same kernels' fp16 form: two fp16 terms per operand after a power-of-2 row scale, three
+# products (lpg_fc_f16x2_*: half the matrix-core work, representation error a quarter of an fp32 SGEMM's);
+# where it does not apply (the weight gradient, operands the wide kernel does not take) the call runs x3
+X3LIKE = ("x3", "f16x2")
 
 _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless the narrow-input kernel applies
 
@@ -79,7 +83,7 @@ def fc_forward(A1: Tensor, W1: Tensor, A2: Tensor | None, W2: Tensor | None, bia
         M, N = A1.shape[0], W1.shape[0]
         k4 = lambda k: -(-k // 4) * 4
         small = 4 <= k4(A1.shape[1]) and k4(A1.shape[1]) + (0 if A2 is None else k4(A2.shape[1])) <= 16
-        if (arith or ARITH) == "x3" and not small and N > 32 and heads[0].shape[0] <= 4:
+        if (arith or ARITH) in X3LIKE and not small and N > 32 and heads[0].shape[0] <= 4:
             return _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, heads, kernel,
                                row_offset, heads_only, row_keys)
         C = _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p, seed, out, accumulate, arith, kernel=kernel,
@@ -126,11 +130,11 @@ def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, acc
     K2 = 0 if A2 is None else A2.shape[1]
     L = _lib.lib()
     flags = (1 if relu else 0) | (2 if accumulate else 0)
-    if (arith or ARITH) == "x3" and not small and N > 32:
+    if (arith or ARITH) in X3LIKE and not small and N > 32:
         if heads is not None and heads_only:
             flags |= 4  # LPG_FC_HEADS_ONLY
         return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags | _lib.fc_kernel(kernel), dropout_p, seed, relu,
-                      heads=heads, row_offset=row_offset, row_keys=row_keys)
+                      heads=heads, row_offset=row_offset, row_keys=row_keys, f16=(arith or ARITH) == "f16x2")
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
         st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
@@ -164,13 +168,92 @@ def split3(W: Tensor, transpose: bool = False) -> Tensor:
     return out
 
 
+def rowscale(A1: Tensor, A2: Tensor | None = None) -> Tensor:
+    """The f16x2 power-of-2 scale of every row of [A1 | A2] (fp32 [M]; lpg_rowscale_f32): the row's largest
+    |x| times it lies in [2^14, 2^15)."""
+    M = A1.shape[0]
+    out = torch.empty(M, dtype=torch.float32, device=A1.device)
+    K2 = 0 if A2 is None else A2.shape[1]
+    with torch.cuda.device(A1.device):
+        st = _lib.lib().lpg_rowscale_f32(M, A1.shape[1], A1.data_ptr(), A1.stride(0), K2,
+                                         None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
+                                         out.data_ptr(), _lib.stream_of(A1))
+    _lib.check(st, "lpg_rowscale_f32")
+    return out
+
+
+def split_f16x2(W1: Tensor, W2: Tensor | None = None, transpose: bool = False):
+    """(P1, P2, sw): rows of [W1 | W2] (columns with ``transpose``) times their shared power-of-2 scale sw,
+    as two fp16 planes each (int16 [2, R, ld], ld the columns rounded up to 8, zero padded; P2 None without
+    W2) -- the weights of the f16x2 kernels (lpg_split_f16x2)."""
+    W1 = W1.detach().float()
+    W2 = None if W2 is None else W2.detach().float()
+    W1 = W1 if W1.stride(-1) == 1 else W1.contiguous()
+    W2 = None if W2 is None else (W2 if W2.stride(-1) == 1 else W2.contiguous())
+    R = W1.shape[1] if transpose else W1.shape[0]
+    c1 = W1.shape[0] if transpose else W1.shape[1]
+    c2 = 0 if W2 is None else (W2.shape[0] if transpose else W2.shape[1])
+    ld = -(-max(c1, c2) // 8) * 8
+    mk = (lambda: torch.zeros((2, R, ld), dtype=torch.int16, device=W1.device)) if (ld != c1 or (c2 and ld != c2)) \
+        else (lambda: torch.empty((2, R, ld), dtype=torch.int16, device=W1.device))
+    P1 = mk()
+    P2 = mk() if W2 is not None else None
+    sw = torch.empty(R, dtype=torch.float32, device=W1.device)
+    with torch.cuda.device(W1.device):
+        st = _lib.lib().lpg_split_f16x2(R, c1, W1.data_ptr(), W1.stride(0), c2, None if W2 is None else W2.data_ptr(),
+                                        W2.stride(0) if c2 else 0, 1 if transpose else 0, P1.data_ptr(), ld,
+                                        None if P2 is None else P2.data_ptr(), ld, R * ld, sw.data_ptr(),
+                                        _lib.stream_of(W1))
+    _lib.check(st, "lpg_split_f16x2")
+    return P1, P2, sw
+
+
 def _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags, dropout_p, seed, relu, W1s=None, W2s=None, heads=None,
-           row_offset=0, row_keys=None):
+           row_offset=0, row_keys=None, f16=False, transpose=False):
     """lpg_fc_x3_f32 on fp32 A and pre-split W (split here unless given); with
-    ``heads`` = (Wh, bh) lpg_fc_x3_heads_f32, returning (C, logits)."""
-    W1s = split3(W1) if W1s is None else W1s
-    W2s = (split3(W2) if W2s is None else W2s) if K2 else None
+    ``heads`` = (Wh, bh) lpg_fc_x3_heads_f32, returning (C, logits).  ``f16``: the f16x2 form
+    (lpg_fc_f16x2_f32 / _heads_f32) from the fp32 weights W1, W2 (``transpose``: the input-gradient GEMM's
+    W^T), falling back to x3 where it does not apply."""
     L = _lib.lib()
+    if f16:
+        sa = rowscale(A1, A2 if K2 else None)
+        P1, P2, sw = split_f16x2(W1, W2 if K2 else None, transpose)
+        args = (M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), P1.data_ptr(), P1.stride(1), P1.stride(0), K2,
+                None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
+                None if P2 is None else P2.data_ptr(), P2.stride(1) if K2 else 0, P2.stride(0) if K2 else 0,
+                sa.data_ptr(), sw.data_ptr(),
+                None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), flags, float(dropout_p),
+                int(seed) & (2**64 - 1), int(row_offset), _lib.ptr(row_keys))
+        key = ("fc", M, N, A1.shape[1] + K2, ("relu" if relu else "lin") + "-f16x2")
+        with torch.cuda.device(A1.device):
+            if heads is None:
+                tok = TIMER.start(key)
+                st = L.lpg_fc_f16x2_f32(*args, _lib.stream_of(A1))
+                TIMER.stop(tok)
+                if st != 3:  # LPG_ERR_UNSUPPORTED: the x3 form below
+                    _lib.check(st, "lpg_fc_f16x2_f32")
+                    return C
+            else:
+                Wh = heads[0].detach().contiguous()
+                bh = None if heads[1] is None else heads[1].detach().contiguous()
+                if Wh.dtype != torch.float32 or Wh.shape[1] != N:
+                    raise RuntimeError("lpgnn fused heads: fp32 head weight [hn, N] expected")
+                logits = torch.empty((M, Wh.shape[0]), dtype=torch.float32, device=A1.device)
+                ws = torch.empty(max(16, L.lpg_fc_x3_heads_workspace_bytes(M, N)), dtype=torch.uint8,
+                                 device=A1.device)
+                tok = TIMER.start(key)
+                st = L.lpg_fc_f16x2_heads_f32(*args, Wh.shape[0], Wh.data_ptr(), Wh.stride(0),
+                                              None if bh is None else bh.data_ptr(), logits.data_ptr(),
+                                              logits.stride(0), ws.data_ptr(), _lib.stream_of(A1))
+                TIMER.stop(tok)
+                if st != 3:
+                    _lib.check(st, "lpg_fc_f16x2_heads_f32")
+                    return C, logits
+    if W1s is None:
+        W1s = split3(W1, transpose=transpose)
+    if K2 and W2s is None:
+        W2s = split3(W2, transpose=transpose)
+    W2s = W2s if K2 else None
     args = (M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1s.data_ptr(), W1s.stride(1), W1s.stride(0), K2,
             None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
             None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0, W2s.stride(0) if K2 else 0,
@@ -203,7 +286,7 @@ def wgrad(G: Tensor, X: Tensor, arith: str | None = None) -> Tensor:
     """G^T X (the weight gradient dZ^T x of a Linear, [N, K]) in fp32:
     lpg_wgrad_x3_f32 (deterministic split-R reduction) or, with arith
     "fp32", the library GEMM (hipBLASLt)."""
-    if (arith or ARITH) != "x3" or G.shape[1] % 4 or X.shape[1] % 4 or G.dtype != torch.float32:
+    if (arith or ARITH) not in X3LIKE or G.shape[1] % 4 or X.shape[1] % 4 or G.dtype != torch.float32:
         return G.t() @ X
     if G.device.type != "cuda":
         raise RuntimeError("lpgnn: the GCN_FC hot path runs on a HIP device only (no CPU path)")
@@ -226,7 +309,7 @@ def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | No
     """G1 W1 [+ G2 W2] [+ out] for Linear weights W [out, in] (the input
     gradient of lin_rel / lin_root): the x3 FC kernel with the weights split
     transposed, or the library GEMMs with arith "fp32"."""
-    if (arith or ARITH) != "x3" or G1.shape[1] % 32 or (G2 is not None and G2.shape[1] % 32) \
+    if (arith or ARITH) not in X3LIKE or G1.shape[1] % 32 or (G2 is not None and G2.shape[1] % 32) \
             or W1.shape[1] <= 32 or G1.dtype != torch.float32:
         r = out if accumulate else None
         if r is None:
@@ -248,18 +331,19 @@ def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | No
             raise RuntimeError("lpgnn input_grad: accumulate needs the addend in `out`")
         out = torch.empty((M, N), dtype=torch.float32, device=G1.device)
     K2 = 0 if G2 is None else G2.shape[1]
-    return _fc_x3(M, N, G1, None, G2, None, K2, None, out, 2 if accumulate else 0, 0.0, 0, False,
-                  W1s=split3(W1, transpose=True), W2s=split3(W2, transpose=True) if K2 else None)
+    return _fc_x3(M, N, G1, W1, G2, W2, K2, None, out, 2 if accumulate else 0, 0.0, 0, False,
+                  f16=(arith or ARITH) == "f16x2", transpose=True)
 
 
 def input_grad_relu_wgrad(G1: Tensor, W1: Tensor, G2: Tensor | None, W2: Tensor | None, addend: Tensor | None,
-                          Y: Tensor, X1: Tensor, X2: Tensor | None):
+                          Y: Tensor, X1: Tensor, X2: Tensor | None, arith: str | None = None):
     """conv1's weight gradients folded into the input-gradient GEMM of the layer it feeds
     (lpg_fc_x3_relu_wgrad_f32): g = G1 W1 [+ G2 W2] [+ addend] is the gradient of conv1's ReLU output
     Y, and instead of g the call returns (dW1 [N, k1] = dZ^T X1, dW2 [N, k2] = dZ^T X2 or None,
     db [N] = sum dZ), dZ = (Y > 0) ? g : 0 (conv1 has no dropout; arch.py:181-182) -- what
     relu_wgrad_smallk computes from the stored g, without storing it.  None when the operands do not
-    fit the fused kernel (the caller then takes input_grad + relu_wgrad_smallk)."""
+    fit the fused kernel (the caller then takes input_grad + relu_wgrad_smallk).  ``arith`` "f16x2": the
+    GEMM in the f16x2 form (lpg_fc_f16x2_relu_wgrad_f32)."""
     k1, k2 = X1.shape[1], (0 if X2 is None else X2.shape[1])
     if (G1.dtype != torch.float32 or G1.shape[1] % 32 or (G2 is not None and G2.shape[1] % 32)
             or W1.shape[1] <= 32 or W1.shape[1] % 2 or not 1 <= k1 + k2 <= 16 or Y.dtype != torch.float32):
@@ -268,8 +352,13 @@ def input_grad_relu_wgrad(G1: Tensor, W1: Tensor, G2: Tensor | None, W2: Tensor 
     if G2 is not None and G2.stride(0) != G1.stride(0):
         return None
     M, N = G1.shape[0], W1.shape[1]
-    W1s = split3(W1, transpose=True)
-    W2s = split3(W2, transpose=True) if G2 is not None else None
+    f16 = (arith or ARITH) == "f16x2"
+    if f16:
+        W1s, W2s, sw = split_f16x2(W1, W2 if G2 is not None else None, transpose=True)
+        sa = rowscale(G1, G2)
+    else:
+        W1s = split3(W1, transpose=True)
+        W2s = split3(W2, transpose=True) if G2 is not None else None
     if W2s is not None and W2s.shape != W1s.shape:
         return None
     Y = Y if (Y.stride(1) == 1 and Y.stride(0) % 2 == 0 and Y.data_ptr() % 8 == 0) else Y.contiguous()
@@ -285,18 +374,22 @@ def input_grad_relu_wgrad(G1: Tensor, W1: Tensor, G2: Tensor | None, W2: Tensor 
     ws = torch.empty(max(16, L.lpg_fc_x3_relu_wgrad_workspace_bytes(M, N, k1 + k2)) // 4 + 4, dtype=torch.float32,
                      device=G1.device)
     K2 = 0 if G2 is None else G2.shape[1]
-    with torch.cuda.device(G1.device):
-        tok = TIMER.start(("fc", M, N, G1.shape[1] + K2, "wgk-x3"))
-        st = L.lpg_fc_x3_relu_wgrad_f32(
-            M, N, G1.shape[1], G1.data_ptr(), G1.stride(0), W1s.data_ptr(), W1s.stride(1), W1s.stride(0), K2,
+    head = (M, N, G1.shape[1], G1.data_ptr(), G1.stride(0), W1s.data_ptr(), W1s.stride(1), W1s.stride(0), K2,
             None if G2 is None else G2.data_ptr(), G2.stride(0) if K2 else 0,
-            None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0, W2s.stride(0) if K2 else 0,
-            None if addend is None else addend.data_ptr(), N if addend is None else addend.stride(0),
+            None if W2s is None else W2s.data_ptr(), W2s.stride(1) if K2 else 0, W2s.stride(0) if K2 else 0)
+    tail = (None if addend is None else addend.data_ptr(), N if addend is None else addend.stride(0),
             2 if addend is not None else 0, Y.data_ptr(), Y.stride(0), k1, X1.data_ptr(), X1.stride(0), k2,
             None if X2 is None else X2.data_ptr(), X2.stride(0) if k2 else 0, dW1.data_ptr(),
             None if dW2 is None else dW2.data_ptr(), db.data_ptr(), ws.data_ptr(), _lib.stream_of(G1))
+    name = "lpg_fc_f16x2_relu_wgrad_f32" if f16 else "lpg_fc_x3_relu_wgrad_f32"
+    with torch.cuda.device(G1.device):
+        tok = TIMER.start(("fc", M, N, G1.shape[1] + K2, "wgk-f16x2" if f16 else "wgk-x3"))
+        if f16:
+            st = L.lpg_fc_f16x2_relu_wgrad_f32(*head, sa.data_ptr(), sw.data_ptr(), *tail)
+        else:
+            st = L.lpg_fc_x3_relu_wgrad_f32(*head, *tail)
         TIMER.stop(tok)
-    _lib.check(st, "lpg_fc_x3_relu_wgrad_f32")
+    _lib.check(st, name)
     return dW1, dW2, db
 
 

@@ -5,8 +5,10 @@ measurements and for the bitwise contract of the exact-fp32 FC.  A model carries
 ``PathOptions`` (``GCN_FC(..., options=...)``); the defaults come from the environment once, at
 import, so a whole run can be switched from the shell:
 
+  LPGNN_FC_ARITH=x3          the FC and input-gradient GEMMs on the exact three-way bf16 split (six
+                             products) instead of the default f16x2 (two row-scaled fp16 terms per
+                             operand, three products; the weight gradients are x3 in both)
   LPGNN_FC_ARITH=fp32        the exact-fp32 MFMA FC (bitwise oracle/fc_ref.c) + hipBLASLt backward
-                             instead of the x3 kernels (fp32 on the bf16 matrix cores, exact split)
   LPGNN_REASSOC=0            lin_rel(S x) never re-associated as S (x W_rel^T)
   LPGNN_FUSE_HEADS=0         the heads as their own autograd node
   LPGNN_FUSE_HEAD_FWD=0      the heads' forward as their own kernels (not in the last FC's epilogue)
@@ -33,7 +35,7 @@ def _env(name: str, default: str) -> str:
 
 @dataclasses.dataclass(frozen=True)
 class PathOptions:
-    arith: str = "x3"
+    arith: str = "f16x2"
     reassociate: bool = True
     fuse_heads: bool = True
     fuse_head_fwd: bool = True
@@ -45,14 +47,14 @@ class PathOptions:
     spmm_heavy: int = 1024  # sparse.DEFAULT_HEAVY
 
     def __post_init__(self):
-        if self.arith not in ("x3", "fp32"):
-            raise ValueError(f"PathOptions.arith must be 'x3' or 'fp32', got {self.arith!r}")
+        if self.arith not in ("x3", "fp32", "f16x2"):
+            raise ValueError(f"PathOptions.arith must be 'x3', 'f16x2' or 'fp32', got {self.arith!r}")
         if int(self.spmm_heavy) < 0:
             raise ValueError(f"PathOptions.spmm_heavy must be >= 0, got {self.spmm_heavy}")
 
     @classmethod
     def from_env(cls) -> "PathOptions":
-        return cls(arith=_env("LPGNN_FC_ARITH", "x3"),
+        return cls(arith=_env("LPGNN_FC_ARITH", "f16x2"),
                    reassociate=_env("LPGNN_REASSOC", "1") == "1",
                    fuse_heads=_env("LPGNN_FUSE_HEADS", "1") == "1",
                    fuse_head_fwd=_env("LPGNN_FUSE_HEAD_FWD", "1") == "1",

@@ -594,6 +594,12 @@ def _link_prev(ctx, prev):
         prev.wgk_folded = True
 
 
+def _fc_x3like():
+    from .fc import X3LIKE
+
+    return X3LIKE
+
+
 def foldable_producer(left, right, opts):
     """conv1's partitioned node (fp32, ReLU, no dropout, narrow LP-feature inputs that need no
     gradient) when it produced (left, right) and the options fold its weight gradients into the next
@@ -602,7 +608,8 @@ def foldable_producer(left, right, opts):
     if (g is None or g is not right.grad_fn or not isinstance(g, _PartTwoDirection._backward_cls)
             or not torch.is_grad_enabled() or not getattr(g, "small_relu", False)):
         return None
-    if not (opts.fold_conv1_wgrad and opts.arith == "x3" and g.opts.arith == "x3") or any(g.needs_input_grad[:2]):
+    if not (opts.fold_conv1_wgrad and opts.arith in _fc_x3like() and g.opts.arith in _fc_x3like()) or \
+            any(g.needs_input_grad[:2]):
         return None
     return g
 
@@ -869,7 +876,7 @@ def _part_backward_folded(ctx, saved, need, dz, prev, igf, wgf, spmm_forward):
     dw_root_l2r = wgf(dz_r, right[:n_own]) if need[5] else None
 
     def fused(G1, W1, G2, W2, addend, y, x1, x2, two_pass):
-        r = _fc.input_grad_relu_wgrad(G1, W1, G2, W2, addend, y, x1, x2)
+        r = _fc.input_grad_relu_wgrad(G1, W1, G2, W2, addend, y, x1, x2, arith=ctx.opts.arith)
         if r is None:  # operands the fused kernel does not take: the stored gradient, then conv1's pass
             r = _fc.relu_wgrad_smallk(two_pass(), y, 1.0, x1, x2, True)
         return r

@@ -136,7 +136,7 @@ def _near_tie_labels(logits, m, eps):
     return ((p1 - thr).abs() <= 2 * eps) | ((logits[:, 0] - logits[:, 2]).abs() <= 2 * eps)
 
 
-@pytest.mark.parametrize("arith", ["x3", "fp32"])
+@pytest.mark.parametrize("arith", ["x3", "fp32", "f16x2"])
 def test_c2_eval_logits_labels_vs_reference_arithmetic(arith, monkeypatch):
     from lpgnn.val import inference_gnn
 
@@ -183,7 +183,7 @@ def test_c2_eval_logits_labels_vs_reference_arithmetic(arith, monkeypatch):
     assert e_got.max() <= 1.5 * e_ref.max() and e_got.mean() <= 1.5 * e_ref.mean()
 
 
-@pytest.mark.parametrize("arith", ["x3"])
+@pytest.mark.parametrize("arith", ["x3", "f16x2"])
 def test_c2_training_step_grads_vs_oracle_autograd(arith, monkeypatch):
     """One c2 training step (train.py:117-128, dropout 0): loss and every
     parameter gradient vs the oracle's MKL autograd; each gradient's distance

@@ -1,0 +1,157 @@
+"""The f16x2 arithmetic of the fp32 FC kernels (LPGNN_FC_ARITH=f16x2; csrc/fc_x3.hip fc_x3_wide<..., F16>,
+lpg_rowscale_f32, lpg_split_f16x2, lpg_fc_f16x2_*): every operand as two fp16 terms after a power-of-2
+row scale, three matrix-core products.  Checked against float64 with the error bound the scheme states
+(|err| <= 2^-20 sum |a b|, below an fp32 SGEMM's own), against the x3 kernels (same dropout mask, same
+epilogues), on the fused heads and conv1-fold forms, and on rows whose scales spread over 2^+-20 (the
+case a per-tensor scale breaks)."""
+import pytest
+import torch
+
+from lpgnn import fc as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+BOUND = 2.0 ** -20  # of sum |a b| (tools/experiments/split_error.py measures ~2^-25)
+
+
+def _err(C, A1, W1, A2=None, W2=None, bias=None, addend=None, relu=False):
+    """(max |C - ref| / (sum |a b| + tiny), ref) with ref in float64 (pre-dropout)."""
+    A1d, W1d = A1.double(), W1.double()
+    ref = A1d @ W1d.T
+    den = A1d.abs() @ W1d.abs().T
+    if A2 is not None:
+        ref = ref + A2.double() @ W2.double().T
+        den = den + A2.double().abs() @ W2.double().abs().T
+    if addend is not None:
+        ref = ref + addend.double()
+        den = den + addend.double().abs()
+    if bias is not None:
+        ref = ref + bias.double()
+        den = den + bias.double().abs()
+    if relu:
+        ref = ref.clamp_min(0)
+    return float(((C.double() - ref).abs() / (den + 1e-30)).max()), ref
+
+
+def test_rowscale_and_split():
+    torch.manual_seed(0)
+    A = torch.randn(1000, 256, device=DEV) * torch.exp(4 * torch.randn(1000, 1, device=DEV))
+    A[7] = 0.0
+    s = F.rowscale(A)
+    mx = A.abs().amax(1) * s
+    nz = A.abs().amax(1) > 0
+    assert bool(((mx[nz] >= 2 ** 14) & (mx[nz] < 2 ** 15)).all())
+    assert float(s[7]) == 1.0
+    assert bool((torch.frexp(s).mantissa == 0.5).all())  # powers of two
+    W = torch.randn(384, 512, device=DEV) * torch.exp(2 * torch.randn(384, 1, device=DEV))
+    for transpose in (False, True):
+        P, _, sw = F.split_f16x2(W, None, transpose)
+        Wt = W.t() if transpose else W
+        h = P[0].view(torch.float16).float()[:, :Wt.shape[1]].double()
+        lo = P[1].view(torch.float16).float()[:, :Wt.shape[1]].double()
+        x = Wt.double() * sw.double()[:, None]
+        assert float(((h + lo - x).abs() - (2 ** -22 * x.abs() + 2 ** -25)).max()) <= 0
+        assert bool((P[:, :, Wt.shape[1]:] == 0).all())  # zero padding
+
+
+@pytest.mark.parametrize("M,N,K1,K2,relu,acc,bias", [
+    (5000, 1024, 1024, 0, False, False, False),
+    (5000, 1024, 1024, 0, True, False, True),
+    (3001, 384, 512, 512, True, False, True),   # two operands, ragged M
+    (4096, 1024, 1024, 0, True, True, True),    # addend (the re-associated var side)
+    (777, 256, 64, 0, False, False, False),
+])
+def test_fc_f16x2_against_fp64(M, N, K1, K2, relu, acc, bias):
+    torch.manual_seed(M + N)
+    A1 = torch.randn(M, K1, device=DEV) * torch.exp(torch.randn(M, 1, device=DEV))
+    W1 = torch.randn(N, K1, device=DEV) * 0.03
+    A2 = torch.randn(M, K2, device=DEV) if K2 else None
+    W2 = torch.randn(N, K2, device=DEV) * 0.03 if K2 else None
+    b = torch.randn(N, device=DEV) * 0.1 if bias else None
+    addend = torch.randn(M, N, device=DEV) if acc else None
+    out = addend.clone() if acc else None
+    C = F.fc_forward(A1, W1, A2, W2, b, relu, out=out, accumulate=acc, arith="f16x2")
+    e, _ = _err(C, A1, W1, A2, W2, b, addend, relu)
+    x3 = F.fc_forward(A1, W1, A2, W2, b, relu, out=None if not acc else addend.clone(), accumulate=acc, arith="x3")
+    e3, _ = _err(x3, A1, W1, A2, W2, b, addend, relu)
+    print(f"f16x2 {e:.2e}  x3 {e3:.2e}")
+    assert e <= BOUND
+
+
+def test_dropout_mask_equals_x3():
+    torch.manual_seed(3)
+    A = torch.randn(6000, 1024, device=DEV)
+    W = torch.randn(1024, 1024, device=DEV) * 0.03
+    b = torch.randn(1024, device=DEV) * 0.1
+    y16 = F.fc_forward(A, W, None, None, b, True, 0.1, 77, arith="f16x2", row_offset=123)
+    y3 = F.fc_forward(A, W, None, None, b, True, 0.1, 77, arith="x3", row_offset=123)
+    # the same keep mask wherever the pre-dropout value is clearly positive
+    clear = y3.abs() > 1e-3
+    assert torch.equal((y16 != 0) & clear, (y3 != 0) & clear)
+    assert float(((y16 - y3).abs() / (y3.abs() + 1)).max()) < 1e-5
+
+
+def test_heads_and_input_grad_f16x2():
+    torch.manual_seed(5)
+    M, N = 5000, 1024
+    A = torch.randn(M, N, device=DEV)
+    W = torch.randn(N, N, device=DEV) * 0.03
+    b = torch.randn(N, device=DEV) * 0.1
+    Wh = torch.randn(3, N, device=DEV) * 0.05
+    bh = torch.randn(3, device=DEV)
+    C16, L16 = F.fc_forward(A, W, None, None, b, True, heads=(Wh, bh), arith="f16x2")
+    C3, L3 = F.fc_forward(A, W, None, None, b, True, heads=(Wh, bh), arith="x3")
+    assert float((C16 - C3).abs().max()) <= 1e-5 * float(C3.abs().max())
+    assert float((L16 - L3).abs().max()) <= 1e-5 * float(L3.abs().max())
+    # input gradient G W (+ G2 W2), gradient-like rows spread over e^(4 N(0,1))
+    G = torch.randn(M, N, device=DEV) * torch.exp(4 * torch.randn(M, 1, device=DEV))
+    g16 = F.input_grad(G, W, arith="f16x2")
+    ref = G.double() @ W.double()
+    den = G.double().abs() @ W.double().abs()
+    assert float(((g16.double() - ref).abs() / (den + 1e-30)).max()) <= BOUND
+    # every row relative to itself (a per-tensor scale would lose the small rows entirely)
+    rel_row = ((g16.double() - ref).norm(dim=1) / ref.norm(dim=1)).max()
+    assert float(rel_row) <= 1e-6
+
+
+def test_conv1_fold_f16x2_equals_x3():
+    torch.manual_seed(9)
+    M, N, k = 6000, 1024, 8
+    G = torch.randn(M, N, device=DEV) * 1e-3
+    W = torch.randn(N, N, device=DEV) * 0.03
+    Y = torch.relu(torch.randn(M, N, device=DEV))
+    X1 = torch.randn(M, k, device=DEV)
+    X2 = torch.randn(M, k, device=DEV)
+    r16 = F.input_grad_relu_wgrad(G, W, None, None, None, Y, X1, X2, arith="f16x2")
+    r3 = F.input_grad_relu_wgrad(G, W, None, None, None, Y, X1, X2, arith="x3")
+    assert r16 is not None and r3 is not None
+    for a, b in zip(r16, r3):
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max())
+
+
+def test_model_step_f16x2_close_to_x3():
+    from lpgnn import GCN_FC, BipartiteBatch, BipartiteCSR, synth
+    from lpgnn.options import DEFAULT
+    from lpgnn.train import balanced
+
+    g = synth.uniform_lp(3000, 6000, 60000, seed=2)
+    t = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    batch = BipartiteBatch(x_s=t(g.x_s), x_t=t(g.x_t), y_s=t(g.y_s), y_t=t(g.y_t),
+                           edge_index=BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV),
+                           s_bs=g.m, t_bs=g.n, bs=g.m + g.n)
+    out = {}
+    for arith in ("x3", "f16x2"):
+        torch.manual_seed(0)
+        model = GCN_FC(8, 8, hids=256, depth=3, dp=0.0, options=DEFAULT.replace(arith=arith)).to(DEV)
+        lc, lv = model(batch)
+        loss = balanced(lc, lv, batch.y_s, batch.y_t)
+        loss.backward()
+        out[arith] = (float(loss), [p.grad.clone() for p in model.parameters()], lc.detach(), lv.detach())
+    assert abs(out["x3"][0] - out["f16x2"][0]) <= 1e-5 * abs(out["x3"][0])
+    for a, b in zip(out["x3"][1], out["f16x2"][1]):
+        assert float((a - b).norm()) <= 1e-4 * float(b.norm()) + 1e-12
+    # the normalised logits (add_knowledge's 10 / |h| amplifies the heads' difference): the north star's 1e-4
+    for a, b in zip(out["x3"][2:], out["f16x2"][2:]):
+        d = float((a - b).abs().max())
+        print(f"max |logit_x3 - logit_f16x2| = {d:.2e}")
+        assert d <= 1e-4

@@ -127,8 +127,15 @@ def _worker_dropout(rank, world, port, out_dir):
         # separate Linear (equal to fp32 rounding, test_x3_fused_heads_match_separate_linear), and
         # normalize()'s 10/|h| amplifies that where |h| is small -- the north star's 1e-4 bar
         torch.testing.assert_close(out[True][1], out[False][1], rtol=0, atol=1e-4)
+        # the gradients: the one-GPU test's criterion (test_fused_heads_node_equals_separate_heads) --
+        # relative Frobenius distance, elementwise against the tensor's scale
         for k, v in out[True][2].items():
-            torch.testing.assert_close(v, out[False][2][k], rtol=1e-4, atol=1e-6, msg=k)
+            w = out[False][2][k]
+            rel = ((v - w).norm() / w.norm()).item()
+            print(f"[rank {rank}] {k}: rel. Frobenius {rel:.2e}, max|d| {(v - w).abs().max().item():.2e} "
+                  f"(max|g| {w.abs().max().item():.2e})")
+            assert rel <= 1e-5, k
+            torch.testing.assert_close(v, w, rtol=1e-4, atol=1e-5 * w.abs().max().item(), msg=k)
         open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
     finally:
         dist.destroy_process_group()
@@ -267,8 +274,10 @@ def _logits_close(got, want, h_got, h_want, what):
     """The north-star bar at the normalised logits (the c2 parity test's form): the heads' outputs h
     (before add_knowledge) within 1e-4 everywhere; the logits within 1e-4, or -- where add_knowledge's
     10 h / |h| amplifies the node's own head difference -- within its Lipschitz bound 10 * 2 |dh| / |h|,
-    on at most 2 nodes (measured at HEAD: 0 or 1 per side, profiles/r05_parity_head.log -- a boundary
-    variable's sum is split across ranks, so its fp32 order differs from one GPU's)."""
+    on at most 5 nodes (measured: x3 0 or 1 per side, profiles/r05_parity_head.log; the default f16x2
+    arithmetic 1 and 3, profiles/r05_pytest_gpu_f16x2.log -- a boundary variable's sum is split across ranks,
+    so its fp32 order differs from one GPU's, and f16x2's per-row operand scale re-rounds a row whose
+    largest element lands on the other side of a power of 2)."""
     dh = (h_got - h_want).abs()
     assert float(dh.max()) <= 1e-4, (what, float(dh.max()))
     d = (got - want).abs().max(-1).values
@@ -277,7 +286,7 @@ def _logits_close(got, want, h_got, h_want, what):
     print(f"[partition {what}] max|dh| {float(dh.max()):.3e}, max|dlogit| {float(d.max()):.3e}, "
           f"nodes > 1e-4: {int(over.sum())} of {got.shape[0]}", flush=True)
     assert bool((~over | (d <= bound)).all()), (what, "a logit difference not explained by add_knowledge")
-    assert int(over.sum()) <= 2, (what, int(over.sum()))
+    assert int(over.sum()) <= 5, (what, int(over.sum()))
 
 
 def _worker_c4(rank, world, port, out_dir, mode, scale=50, hids=256):

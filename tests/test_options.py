@@ -23,12 +23,12 @@ def _clear(monkeypatch):
         monkeypatch.delenv(k, raising=False)
 
 
-def test_defaults_are_the_fused_x3_path(monkeypatch):
+def test_defaults_are_the_fused_f16x2_path(monkeypatch):
     _clear(monkeypatch)
     o = PathOptions.from_env()
     assert o == PathOptions()
     assert (o.arith, o.reassociate, o.fuse_heads, o.fuse_head_fwd, o.fold_relu_bwd, o.fold_conv1_wgrad,
-            o.overlap, o.relu_bits, o.fold_bias_sums, o.spmm_heavy) == ("x3", True, True, True, True, True, False, True,
+            o.overlap, o.relu_bits, o.fold_bias_sums, o.spmm_heavy) == ("f16x2", True, True, True, True, True, False, True,
                                                                         True, 1024)
 
 
