@@ -321,6 +321,43 @@ lpg_status lpg_fc_x3_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1, const floa
                                     const float *X1, int64_t ldx1, int64_t ks2, const float *X2, int64_t ldx2,
                                     float *dW1, float *dW2, float *db, void *workspace, void *stream);
 
+/* ---- f16x2: the same three entries on two fp16 terms per operand (the default arithmetic, round 5) ----
+ * Each row of [A1 | A2] is multiplied by a power of two sa[m] (lpg_rowscale_f32: its largest |x| lands
+ * in [2^14, 2^15)) and split in registers into h = RNE_f16(x sa), l = RNE_f16(x sa - h); W is given as
+ * two fp16 planes of [W1 | W2] rows times their own power of two sw[n] (lpg_split_f16x2: plane 0 = h,
+ * plane 1 = l, at W + p * ps).  Per (m, n): hh + (hl + lh) in fp32 (three v_mfma_f32_16x16x32_f16,
+ * half x3's six), then times 1 / (sa[m] sw[n]) (exact) and the same epilogue.  Representation error
+ * <= ~3 * 2^-22 of sum |a b| -- a quarter of an fp32 SGEMM's own error (tools/experiments/
+ * split_error.py); per-row scales keep every row's relative accuracy whatever the spread between rows.
+ * The other arguments and rules are the x3 entries'; operands the wide kernel does not take (lda1 !=
+ * lda2, ldw1 != ldw2, ps1 != ps2; heads hn = 4) return LPG_ERR_UNSUPPORTED and the caller runs x3. */
+lpg_status lpg_rowscale_f32(int64_t M, int64_t K1, const float *A1, int64_t lda1, int64_t K2, const float *A2,
+                            int64_t lda2, float *scale, void *stream);
+/* rows of [src1 | src2] (columns with transpose != 0) times their shared scale, as two fp16 planes each:
+ * dst1 / dst2 [rows, ldd] with plane 1 at + plane_stride, zero columns past cols left to the caller. */
+lpg_status lpg_split_f16x2(int64_t rows, int64_t cols1, const float *src1, int64_t lds1, int64_t cols2,
+                           const float *src2, int64_t lds2, int32_t transpose, uint16_t *dst1, int64_t ldd1,
+                           uint16_t *dst2, int64_t ldd2, int64_t plane_stride, float *scale, void *stream);
+lpg_status lpg_fc_f16x2_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1, const uint16_t *W1,
+                            int64_t ldw1, int64_t ps1, int64_t K2, const float *A2, int64_t lda2, const uint16_t *W2,
+                            int64_t ldw2, int64_t ps2, const float *sa, const float *sw, const float *bias, float *C,
+                            int64_t ldc, int32_t flags, float dropout_p, uint64_t seed, int64_t row_offset,
+                            const int64_t *row_keys, void *stream);
+lpg_status lpg_fc_f16x2_heads_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                  const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                  int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *sa,
+                                  const float *sw, const float *bias, float *C, int64_t ldc, int32_t flags,
+                                  float dropout_p, uint64_t seed, int64_t row_offset, const int64_t *row_keys,
+                                  int32_t hn, const float *hw, int64_t ldhw, const float *hb, float *logits,
+                                  int64_t ldl, void *workspace, void *stream);
+lpg_status lpg_fc_f16x2_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                       const uint16_t *W1, int64_t ldw1, int64_t ps1, int64_t K2, const float *A2,
+                                       int64_t lda2, const uint16_t *W2, int64_t ldw2, int64_t ps2, const float *sa,
+                                       const float *sw, const float *C, int64_t ldc, int32_t flags, const float *Y,
+                                       int64_t ldy, int64_t ks1, const float *X1, int64_t ldx1, int64_t ks2,
+                                       const float *X2, int64_t ldx2, float *dW1, float *dW2, float *db,
+                                       void *workspace, void *stream);
+
 /* Weight gradient on the same arithmetic: dW[n, k] = sum_r G[r, n] X[r, k]
  * (G = dZ [R, N], ldg; X = the layer input [R, K], ldx; dW [N, K], lddw, the
  * torch Linear weight layout) -- the lin_rel / lin_root weight gradients of
