@@ -368,6 +368,15 @@ lpg_status lpg_fc_f16x2_relu_wgrad_f32(int64_t M, int64_t N, int64_t K1, const f
 int64_t lpg_wgrad_x3_workspace_bytes(int64_t R, int64_t N, int64_t K);
 lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
                             int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream);
+/* The weight gradient in f16x2: G column n and X column k times their power-of-2 column scales sG[n],
+ * sX[k] (lpg_colscale_f32: each column's largest |x| over the R rows in [2^14, 2^15)), two fp16 terms
+ * each, three products; otherwise lpg_wgrad_x3_f32 (same workspace, deterministic fold). */
+lpg_status lpg_wgrad_f16x2_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
+                               int64_t ldx, const float *sG, const float *sX, float *dW, int64_t lddw,
+                               void *workspace, void *stream);
+int64_t lpg_colscale_workspace_bytes(int64_t R, int64_t N);
+lpg_status lpg_colscale_f32(int64_t R, int64_t N, const float *G, int64_t ldg, float *scale, void *workspace,
+                            void *stream);
 
 /* Backward of ReLU (+ fused dropout): out[i] = y[i] > 0 ? g[i] * scale : 0,
  * y = the stored lpg_fc_f32 output, scale = 1/(1-p) (1 without dropout).

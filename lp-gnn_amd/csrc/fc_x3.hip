@@ -1048,13 +1048,20 @@ constexpr int WG_T = 128;  // output tile (n and k)
 // 0-3 G and waves 4-7 X with 6-7 repeating 4-5's work, 1.83 per MFMA on every SIMD, and issued a
 // chunk's loads one fragment row before their use: 189 / 211 TF/s at R = 100 / 200 K against 197 /
 // 218 for the balanced tasks, profiles/r03_wgrad_bal.log.)
+//
+// F16 (f16x2, round 5): G column n and X column k times their power-of-2 column scales sG[n], sX[k]
+// (lpg_colscale_f32), split into two fp16 terms; three v_mfma_f32_16x16x32_f16 per fragment pair
+// (hh into accH, hl + lh into accL) and the partial tile times 1 / (sG sX) (exact) at the store.
+template <bool F16 = false>
 __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_t K, const float *__restrict__ G,
                                                     int64_t ldg, const float *__restrict__ X, int64_t ldx,
                                                     float *__restrict__ part, int64_t nt, int64_t kt,
-                                                    int64_t chunks_per_split) {
+                                                    int64_t chunks_per_split, const float *__restrict__ sG,
+                                                    const float *__restrict__ sX) {
   constexpr int GC = 256, XC = 128;               // tile columns of G (n) and X (k)
   constexpr int GP = GC * 32 * 2, XP = XC * 32 * 2;  // one plane image: columns x 32 rows x bf16
-  constexpr int BUFB = 3 * GP + 3 * XP;           // one buffer: G planes, then X planes (72 KiB)
+  constexpr int NPL = F16 ? 2 : 3;                // planes per operand
+  constexpr int BUFB = NPL * GP + NPL * XP;       // one buffer: G planes, then X planes (72 / 48 KiB)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB];
 
   const int64_t nwg = (int64_t)gridDim.x, xcd = (int64_t)blockIdx.x % 8, q8 = nwg / 8, rr = nwg % 8;
@@ -1097,14 +1104,26 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
 #pragma unroll
     for (int u = 0; u < 3; ++u) load_unit(u, c);
   };
-  auto split_col = [&](unsigned char *buf, int u) {  // unit u's 8 rows -> three bf16x8
-    const Split3 t = split3(f32x4{raw[u][0], raw[u][1], raw[u][2], raw[u][3]},
-                            f32x4{raw[u][4], raw[u][5], raw[u][6], raw[u][7]});
+  float su[F16 ? 3 : 1];  // F16: the scales of this thread's three columns
+  if constexpr (F16) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) su[u] = u < 2 ? sG[col_u[u]] : sX[col_u[u]];
+  }
+  auto split_col = [&](unsigned char *buf, int u) {  // unit u's 8 rows -> three bf16x8 (F16: two f16x8)
     const int col = u == 1 ? 128 + gc : gc, pl = u < 2 ? GP : XP;
-    unsigned char *dst = buf + (u < 2 ? 0 : 3 * GP) + col * 64 + swzW(col, rg) * 16;
-    *reinterpret_cast<bf16x8 *>(dst) = t.h;
-    *reinterpret_cast<bf16x8 *>(dst + pl) = t.m;
-    *reinterpret_cast<bf16x8 *>(dst + 2 * pl) = t.l;
+    unsigned char *dst = buf + (u < 2 ? 0 : NPL * GP) + col * 64 + swzW(col, rg) * 16;
+    if constexpr (F16) {
+      const Split2 t = split2f16(f32x4{raw[u][0], raw[u][1], raw[u][2], raw[u][3]},
+                                 f32x4{raw[u][4], raw[u][5], raw[u][6], raw[u][7]}, su[u]);
+      *reinterpret_cast<f16x8 *>(dst) = t.h;
+      *reinterpret_cast<f16x8 *>(dst + pl) = t.l;
+    } else {
+      const Split3 t = split3(f32x4{raw[u][0], raw[u][1], raw[u][2], raw[u][3]},
+                              f32x4{raw[u][4], raw[u][5], raw[u][6], raw[u][7]});
+      *reinterpret_cast<bf16x8 *>(dst) = t.h;
+      *reinterpret_cast<bf16x8 *>(dst + pl) = t.m;
+      *reinterpret_cast<bf16x8 *>(dst + 2 * pl) = t.l;
+    }
   };
 
   const int wm = wave >> 1, wn = wave & 1;  // 4 (n) x 2 (k) waves of 64 x 64
@@ -1119,6 +1138,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
 #pragma unroll
     for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8 *>(im + p * plane + col * 64 + swzW(col, fg) * 16);
   };
+  auto frag16 = [&](const unsigned char *im, int plane, int col, f16x8(&f)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) f[p] = *reinterpret_cast<const f16x8 *>(im + p * plane + col * 64 + swzW(col, fg) * 16);
+  };
   // multiply the chunk in buf; with `next`, split unit i - 1 of the next chunk (raw) into it after
   // fragment row i - 1's 24 MFMAs and issue that unit's loads of chunk `cload` (in source order, so
   // the VALU lands between MFMA groups)
@@ -1126,6 +1149,28 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
   // pointer non-null -- put a branch around every split, and at each join the waitcnt pass assumed
   // the path without the other units' loads and waited for all of them)
   auto multiply = [&](const unsigned char *buf, unsigned char *next, int64_t cload, auto split) {
+    if constexpr (F16) {
+      f16x8 bv[4][2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) frag16(buf + 2 * GP, XP, wn * 64 + j * 16 + fr, bv[j]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (decltype(split)::value && i > 0) {
+          split_col(next, i - 1);
+          __builtin_amdgcn_sched_barrier(0);
+          load_unit(i - 1, cload);
+        }
+        f16x8 av[2];
+        frag16(buf, GP, wm * 64 + i * 16 + fr, av);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[1], bv[j][0], accL[i][j], 0, 0, 0);
+          accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[0], bv[j][1], accL[i][j], 0, 0, 0);
+          accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[0], bv[j][0], accH[i][j], 0, 0, 0);
+        }
+      }
+      return;
+    } else {
     bf16x8 bv[4][3];
 #pragma unroll
     for (int j = 0; j < 4; ++j) frag(buf + 3 * GP, XP, wn * 64 + j * 16 + fr, bv[j]);
@@ -1149,6 +1194,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
         accL[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][1], accL[i][j], 0, 0, 0);
         accH[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[j][0], accH[i][j], 0, 0, 0);
       }
+    }
     }
   };
   auto sync = [&]() {
@@ -1181,14 +1227,54 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
   for (int j = 0; j < 4; ++j) {
     const int64_t col = k0 + wn * 64 + j * 16 + fr;
     if (col >= K) continue;
+    const float ix = F16 ? 1.f / sX[col] : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t row = n0 + wm * 64 + i * 16 + 4 * fg + r;
-        if (row < N) P[row * K + col] = accH[i][j][r] + accL[i][j][r];
+        if (row < N) {
+          float v = accH[i][j][r] + accL[i][j][r];
+          if constexpr (F16) v = v * (1.f / sG[row]) * ix;
+          P[row * K + col] = v;
+        }
       }
   }
+}
+
+// per-column maxima of |G| (N, ldg multiples of 4, 16-byte aligned rows): block (column block of 1024,
+// row chunk of rc) -- a thread's 4 columns as float4 over the chunk, eight rows in flight -- then one
+// integer atomicMax per column on the bits (|x| >= 0: the uint order is the float order, NaN above
+// every number): the same maxima whatever the order, so deterministic
+__global__ __launch_bounds__(256) void colmax_f32(int64_t R, int64_t N, const float *__restrict__ G, int64_t ldg,
+                                                  int64_t rc, unsigned *__restrict__ mbits) {
+  const int64_t c4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4, chunk = blockIdx.y;
+  if (c4 >= N) return;
+  const int64_t r0 = chunk * rc, r1 = r0 + rc < R ? r0 + rc : R;
+  f32x4 m = {0.f, 0.f, 0.f, 0.f};
+  int64_t r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4 *>(G + (r + u) * ldg + c4);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[u][e]));
+  }
+  for (; r < r1; ++r) {
+    const f32x4 v = *reinterpret_cast<const f32x4 *>(G + r * ldg + c4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[e]));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) atomicMax(mbits + c4 + e, __float_as_uint(m[e]));
+}
+
+__global__ __launch_bounds__(256) void colscale_f32(int64_t N, const unsigned *__restrict__ mbits,
+                                                    float *__restrict__ scale) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col < N) scale[col] = f16x2_scale(__uint_as_float(mbits[col]));
 }
 
 // dW[n, k] = sum_s part[s][n, k], s ascending (fixed order), float4 per thread
@@ -1440,9 +1526,11 @@ extern "C" int64_t lpg_wgrad_x3_workspace_bytes(int64_t R, int64_t N, int64_t K)
   return wgrad_splits(R, N, K) * N * K * (int64_t)sizeof(float) + 512;  // + the zero row
 }
 
-extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
-                                       int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream) {
+static lpg_status wgrad_x3_impl(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
+                                int64_t ldx, const float *sG, const float *sX, float *dW, int64_t lddw,
+                                void *workspace, void *stream) {
   LPG_REQUIRE(R >= 0 && N >= 0 && K >= 0, "lpg_wgrad_x3_f32: negative size");
+  LPG_REQUIRE(!sG == !sX, "lpg_wgrad_f16x2_f32: both column scales or neither");
   if (N == 0 || K == 0) return LPG_OK;
   LPG_REQUIRE(dW && lddw >= K && lddw % 4 == 0 && aligned16(dW), "lpg_wgrad_x3_f32: bad dW/lddw");
   if (R == 0) {
@@ -1467,11 +1555,56 @@ extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const fl
   const int64_t ntw = (N + 255) / 256, ktw = (K + 127) / 128;  // 256 x 128 tiles
   const int64_t nbw = S_used * ntw * ktw;
   LPG_REQUIRE(nbw < (int64_t)1 << 31, "lpg_wgrad_x3_f32: grid too large");
-  hipLaunchKernelGGL(wgrad_x3w, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw, ktw,
-                     cps);
+  if (sG)
+    hipLaunchKernelGGL(wgrad_x3w<true>, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw,
+                       ktw, cps, sG, sX);
+  else
+    hipLaunchKernelGGL(wgrad_x3w<false>, dim3((unsigned)nbw), dim3(512), 0, st, R, N, K, G, ldg, X, ldx, part, ntw,
+                       ktw, cps, nullptr, nullptr);
   LPG_HIP(hipGetLastError());
   const int64_t n4 = N * (K / 4);
   hipLaunchKernelGGL(wgrad_fold, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, N, K, S_used, part, dW, lddw);
+  LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+extern "C" lpg_status lpg_wgrad_x3_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg, const float *X,
+                                       int64_t ldx, float *dW, int64_t lddw, void *workspace, void *stream) {
+  return wgrad_x3_impl(R, N, K, G, ldg, X, ldx, nullptr, nullptr, dW, lddw, workspace, stream);
+}
+
+extern "C" lpg_status lpg_wgrad_f16x2_f32(int64_t R, int64_t N, int64_t K, const float *G, int64_t ldg,
+                                          const float *X, int64_t ldx, const float *sG, const float *sX, float *dW,
+                                          int64_t lddw, void *workspace, void *stream) {
+  LPG_REQUIRE(sG && sX, "lpg_wgrad_f16x2_f32: NULL column scales");
+  return wgrad_x3_impl(R, N, K, G, ldg, X, ldx, sG, sX, dW, lddw, workspace, stream);
+}
+
+constexpr int64_t kColChunk = 256;  // rows per column-max block
+
+extern "C" int64_t lpg_colscale_workspace_bytes(int64_t R, int64_t N) {
+  if (R <= 0 || N <= 0) return 0;
+  return N * (int64_t)sizeof(unsigned);
+}
+
+extern "C" lpg_status lpg_colscale_f32(int64_t R, int64_t N, const float *G, int64_t ldg, float *scale,
+                                       void *workspace, void *stream) {
+  LPG_REQUIRE(R >= 0 && N >= 0, "lpg_colscale_f32: negative size");
+  if (N == 0) return LPG_OK;
+  LPG_REQUIRE(scale && workspace, "lpg_colscale_f32: NULL pointer");
+  LPG_REQUIRE(R == 0 || (G && ldg >= N && N % 4 == 0 && ldg % 4 == 0 && aligned16(G)),
+              "lpg_colscale_f32: N and ldg multiples of 4 floats, G 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  unsigned *mbits = static_cast<unsigned *>(workspace);
+  LPG_HIP(hipMemsetAsync(mbits, 0, N * sizeof(unsigned), st));
+  const int64_t chunks = (R + kColChunk - 1) / kColChunk;
+  LPG_REQUIRE(chunks < 65536, "lpg_colscale_f32: too many rows");
+  if (chunks > 0) {
+    hipLaunchKernelGGL(colmax_f32, dim3((unsigned)((N + 1023) / 1024), (unsigned)chunks), dim3(256), 0, st, R, N, G,
+                       ldg, kColChunk, mbits);
+    LPG_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(colscale_f32, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, N, mbits, scale);
   LPG_HIP(hipGetLastError());
   return LPG_OK;
 }

@@ -105,6 +105,9 @@ HEADER_SYMBOLS = (
     "lpg_fc_f16x2_f32",
     "lpg_fc_f16x2_heads_f32",
     "lpg_fc_f16x2_relu_wgrad_f32",
+    "lpg_wgrad_f16x2_f32",
+    "lpg_colscale_workspace_bytes",
+    "lpg_colscale_f32",
 )
 
 c_i64, c_i32, c_p = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
@@ -231,6 +234,12 @@ def lib() -> ctypes.CDLL:
         _t = getattr(L, _x3).argtypes
         getattr(L, _f16).argtypes = _t[:14] + [c_p, c_p] + _t[14:]
         getattr(L, _f16).restype = c_i32
+    L.lpg_wgrad_f16x2_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p]
+    L.lpg_wgrad_f16x2_f32.restype = c_i32
+    L.lpg_colscale_workspace_bytes.argtypes = [c_i64, c_i64]
+    L.lpg_colscale_workspace_bytes.restype = c_i64
+    L.lpg_colscale_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p]
+    L.lpg_colscale_f32.restype = c_i32
     L.lpg_rowscale_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p]
     L.lpg_rowscale_f32.restype = c_i32
     L.lpg_split_f16x2.argtypes = [c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_i64, c_i64,

@@ -295,13 +295,33 @@ def wgrad(G: Tensor, X: Tensor, arith: str | None = None) -> Tensor:
     L = _lib.lib()
     dW = torch.empty((N, K), dtype=torch.float32, device=G.device)
     ws = torch.empty(max(1, L.lpg_wgrad_x3_workspace_bytes(R, N, K)), dtype=torch.uint8, device=G.device)
+    f16 = (arith or ARITH) == "f16x2"
     with torch.cuda.device(G.device):
-        tok = TIMER.start(("wgrad", R, N, K, "x3"))
-        st = L.lpg_wgrad_x3_f32(R, N, K, G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), dW.data_ptr(),
-                                dW.stride(0), ws.data_ptr(), _lib.stream_of(G))
+        if f16:
+            sG, sX = colscale(G), colscale(X)
+            tok = TIMER.start(("wgrad", R, N, K, "f16x2"))
+            st = L.lpg_wgrad_f16x2_f32(R, N, K, G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), sG.data_ptr(),
+                                       sX.data_ptr(), dW.data_ptr(), dW.stride(0), ws.data_ptr(), _lib.stream_of(G))
+        else:
+            tok = TIMER.start(("wgrad", R, N, K, "x3"))
+            st = L.lpg_wgrad_x3_f32(R, N, K, G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), dW.data_ptr(),
+                                    dW.stride(0), ws.data_ptr(), _lib.stream_of(G))
         TIMER.stop(tok)
-    _lib.check(st, "lpg_wgrad_x3_f32")
+    _lib.check(st, "lpg_wgrad_f16x2_f32" if f16 else "lpg_wgrad_x3_f32")
     return dW
+
+
+def colscale(G: Tensor) -> Tensor:
+    """The f16x2 power-of-2 scale of every column of G [R, N] (fp32 [N]; lpg_colscale_f32): the column's
+    largest |x| over the rows times it lies in [2^14, 2^15)."""
+    R, N = G.shape
+    L = _lib.lib()
+    out = torch.empty(N, dtype=torch.float32, device=G.device)
+    ws = torch.empty(max(4, L.lpg_colscale_workspace_bytes(R, N)) // 4, dtype=torch.float32, device=G.device)
+    with torch.cuda.device(G.device):
+        st = L.lpg_colscale_f32(R, N, G.data_ptr(), G.stride(0), out.data_ptr(), ws.data_ptr(), _lib.stream_of(G))
+    _lib.check(st, "lpg_colscale_f32")
+    return out
 
 
 def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | None = None,

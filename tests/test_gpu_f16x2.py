@@ -155,3 +155,23 @@ def test_model_step_f16x2_close_to_x3():
         d = float((a - b).abs().max())
         print(f"max |logit_x3 - logit_f16x2| = {d:.2e}")
         assert d <= 1e-4
+
+
+@pytest.mark.parametrize("R,N,K", [(100_000, 1024, 1024), (20_000, 256, 384), (1000, 64, 16 * 8)])
+def test_wgrad_f16x2_against_fp64(R, N, K):
+    torch.manual_seed(R)
+    G = torch.randn(R, N, device=DEV) * torch.exp(4 * torch.randn(1, N, device=DEV))  # column scales spread
+    X = torch.relu(torch.randn(R, K, device=DEV)) * torch.exp(torch.randn(1, K, device=DEV))
+    sG = F.colscale(G)
+    mx = G.abs().amax(0) * sG
+    assert bool(((mx >= 2 ** 14) & (mx < 2 ** 15)).all())
+    dW = F.wgrad(G, X, arith="f16x2")
+    ref = G.double().t() @ X.double()
+    den = G.double().abs().t() @ X.double().abs()
+    e = float(((dW.double() - ref).abs() / (den + 1e-30)).max())
+    e3 = float(((F.wgrad(G, X, arith="x3").double() - ref).abs() / (den + 1e-30)).max())
+    print(f"wgrad f16x2 {e:.2e}  x3 {e3:.2e}")
+    assert e <= BOUND
+    # every output row (a column of G) relative to itself
+    rel = ((dW.double() - ref).norm(dim=1) / ref.norm(dim=1)).max()
+    assert float(rel) <= 1e-6
