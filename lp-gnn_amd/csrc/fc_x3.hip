@@ -122,9 +122,12 @@ __global__ __launch_bounds__(256) void split3_planes(int64_t rows, int64_t cols,
 
 // ---- f16x2 operand preparation ---------------------------------------------------
 // The power-of-2 scale that puts a row's largest |x| in [2^14, 2^15): 2^(15 - e) for max = f 2^e,
-// f in [0.5, 1); 1 for an all-zero or non-finite row (NaN / Inf propagate through the split as in
-// fp32).  e is clamped to [-100, 120] so the scale and its inverse stay normal fp32 numbers.
+// f in [0.5, 1); 1 for a non-finite row (NaN / Inf propagate through the split as in fp32); for an
+// all-zero row the largest scale, 2^115, so the scale of two operands' rows side by side is the
+// smaller of their own (the host combines cached per-operand scales that way).  e is clamped to
+// [-100, 120] so the scale and its inverse stay normal fp32 numbers.
 __device__ __forceinline__ float f16x2_scale(float mx) {
+  if (mx == 0.f) return ldexpf(1.f, 115);
   if (!(mx > 0.f) || !(mx <= 3.4e38f)) return 1.f;
   int e;
   frexpf(mx, &e);

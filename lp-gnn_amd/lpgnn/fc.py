@@ -22,6 +22,7 @@ runs in lpg_linear_small_bwd_f32.  Tolerance-level parity for gradients.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 
 import torch
@@ -168,18 +169,49 @@ def split3(W: Tensor, transpose: bool = False) -> Tensor:
     return out
 
 
-def rowscale(A1: Tensor, A2: Tensor | None = None) -> Tensor:
-    """The f16x2 power-of-2 scale of every row of [A1 | A2] (fp32 [M]; lpg_rowscale_f32): the row's largest
-    |x| times it lies in [2^14, 2^15)."""
-    M = A1.shape[0]
-    out = torch.empty(M, dtype=torch.float32, device=A1.device)
-    K2 = 0 if A2 is None else A2.shape[1]
-    with torch.cuda.device(A1.device):
-        st = _lib.lib().lpg_rowscale_f32(M, A1.shape[1], A1.data_ptr(), A1.stride(0), K2,
-                                         None if A2 is None else A2.data_ptr(), A2.stride(0) if K2 else 0,
-                                         out.data_ptr(), _lib.stream_of(A1))
+class _ScaleCache:
+    """The f16x2 row / column scales of live operands, by object identity and autograd version (an entry
+    holds only a weak reference): an operand several GEMMs of one step use -- a layer input in the forward
+    lin and the constraint-side FC, dZ or a layer input in two weight gradients -- is swept once.  A freed
+    tensor's entry is dropped, and an in-place change bumps the version, so an entry never outlives the
+    values it describes."""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, kind: str, t: Tensor, make):
+        key = (kind, id(t))
+        e = self._d.get(key)
+        if e is not None and e[0]() is t and e[1] == t._version and e[2] == (t.data_ptr(), tuple(t.shape)):
+            return e[3]
+        v = make(t)
+        if len(self._d) > 64:
+            self._d = {k: x for k, x in self._d.items() if x[0]() is not None}
+        self._d[key] = (weakref.ref(t), t._version, (t.data_ptr(), tuple(t.shape)), v)
+        return v
+
+
+_SCALES = _ScaleCache()
+
+
+def _rowscale1(A: Tensor) -> Tensor:
+    M = A.shape[0]
+    out = torch.empty(M, dtype=torch.float32, device=A.device)
+    with torch.cuda.device(A.device):
+        st = _lib.lib().lpg_rowscale_f32(M, A.shape[1], A.data_ptr(), A.stride(0), 0, None, 0, out.data_ptr(),
+                                         _lib.stream_of(A))
     _lib.check(st, "lpg_rowscale_f32")
     return out
+
+
+def rowscale(A1: Tensor, A2: Tensor | None = None) -> Tensor:
+    """The f16x2 power-of-2 scale of every row of [A1 | A2] (fp32 [M]; lpg_rowscale_f32): the row's largest
+    |x| times it lies in [2^14, 2^15) (an all-zero row: 2^115).  Per operand, cached (_ScaleCache); the
+    scale of the two side by side is the smaller of theirs (a power of 2 decreasing in the maximum)."""
+    s1 = _SCALES.get("row", A1, _rowscale1)
+    if A2 is None or A2.shape[1] == 0:
+        return s1
+    return torch.minimum(s1, _SCALES.get("row", A2, _rowscale1))
 
 
 def split_f16x2(W1: Tensor, W2: Tensor | None = None, transpose: bool = False):
@@ -313,7 +345,11 @@ def wgrad(G: Tensor, X: Tensor, arith: str | None = None) -> Tensor:
 
 def colscale(G: Tensor) -> Tensor:
     """The f16x2 power-of-2 scale of every column of G [R, N] (fp32 [N]; lpg_colscale_f32): the column's
-    largest |x| over the rows times it lies in [2^14, 2^15)."""
+    largest |x| over the rows times it lies in [2^14, 2^15) (cached per operand, _ScaleCache)."""
+    return _SCALES.get("col", G, _colscale1)
+
+
+def _colscale1(G: Tensor) -> Tensor:
     R, N = G.shape
     L = _lib.lib()
     out = torch.empty(N, dtype=torch.float32, device=G.device)

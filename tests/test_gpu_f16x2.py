@@ -41,7 +41,12 @@ def test_rowscale_and_split():
     mx = A.abs().amax(1) * s
     nz = A.abs().amax(1) > 0
     assert bool(((mx[nz] >= 2 ** 14) & (mx[nz] < 2 ** 15)).all())
-    assert float(s[7]) == 1.0
+    assert float(s[7]) == 2.0 ** 115  # an all-zero row: the largest scale (combines by min)
+    s2 = F.rowscale(A, A * 4)
+    assert torch.equal(s2, F.rowscale(A * 4))  # side by side: the smaller scale
+    assert F.rowscale(A) is s  # cached for the live, unchanged operand
+    A.mul_(2)
+    assert F.rowscale(A) is not s and torch.equal((F.rowscale(A) * 2)[nz], s[nz])  # an in-place change re-sweeps
     assert bool((torch.frexp(s).mantissa == 0.5).all())  # powers of two
     W = torch.randn(384, 512, device=DEV) * torch.exp(2 * torch.randn(384, 1, device=DEV))
     for transpose in (False, True):
