@@ -377,6 +377,11 @@ lpg_status lpg_wgrad_f16x2_f32(int64_t R, int64_t N, int64_t K, const float *G, 
 int64_t lpg_colscale_workspace_bytes(int64_t R, int64_t N);
 lpg_status lpg_colscale_f32(int64_t R, int64_t N, const float *G, int64_t ldg, float *scale, void *workspace,
                             void *stream);
+/* Both scales of one operand in one read (the same values as lpg_rowscale_f32 on G alone and
+ * lpg_colscale_f32): rscale [R], cscale [N]; workspace lpg_rowcolscale_workspace_bytes(R, N) bytes. */
+int64_t lpg_rowcolscale_workspace_bytes(int64_t R, int64_t N);
+lpg_status lpg_rowcolscale_f32(int64_t R, int64_t N, const float *G, int64_t ldg, float *rscale, float *cscale,
+                               void *workspace, void *stream);
 
 /* Backward of ReLU (+ fused dropout): out[i] = y[i] > 0 ? g[i] * scale : 0,
  * y = the stored lpg_fc_f32 output, scale = 1/(1-p) (1 without dropout).

@@ -1277,7 +1277,71 @@ __global__ __launch_bounds__(256) void colmax_f32(int64_t R, int64_t N, const fl
 __global__ __launch_bounds__(256) void colscale_f32(int64_t N, const unsigned *__restrict__ mbits,
                                                     float *__restrict__ scale) {
   const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (col < N) scale[col] = f16x2_scale(__uint_as_float(mbits[col]));
+  if (col < N) scale[col] = f16x2_scale(mbits ? __uint_as_float(mbits[col]) : 0.f);
+}
+
+// Row AND column maxima of |G| in one read (an operand that is both a row-scaled GEMM A operand and a
+// column-scaled weight-gradient operand: the layer inputs, dZ, S^T dZ).  colmax_f32's blocks (column
+// block of 1024, row chunk of rc <= 256, eight rows in flight); a thread's four |x| of each of the
+// eight rows reduce to one value per row, the eight rows over the wave's 64 lanes in a halving
+// butterfly (each exchange halves the values a lane carries: 4 + 2 + 1 + 1 + 1 + 1 shuffles for
+// eight rows, not 48), the four waves through LDS.  One column block (N <= 1024): the row's scale
+// stored directly; else an integer atomicMax per (row, column block) into rbits.
+__global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const float *__restrict__ G, int64_t ldg,
+                                                     int64_t rc, unsigned *__restrict__ cbits,
+                                                     unsigned *__restrict__ rbits, float *__restrict__ rscale) {
+  __shared__ float red[4][256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t c4 = ((int64_t)blockIdx.x * 256 + tid) * 4, r0 = (int64_t)blockIdx.y * rc;
+  const int64_t r1 = r0 + rc < R ? r0 + rc : R;
+  const bool col_ok = c4 < N;
+  const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0, b3 = (lane & 8) != 0;
+  const int slot = (b5 ? 4 : 0) + (b4 ? 2 : 0) + (b3 ? 1 : 0);
+  f32x4 m = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0; r < r1; r += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = (col_ok && r + u < r1) ? *reinterpret_cast<const f32x4 *>(G + (r + u) * ldg + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float a0 = fabsf(v[u][0]), a1 = fabsf(v[u][1]), a2 = fabsf(v[u][2]), a3 = fabsf(v[u][3]);
+      m[0] = fmaxf(m[0], a0);
+      m[1] = fmaxf(m[1], a1);
+      m[2] = fmaxf(m[2], a2);
+      m[3] = fmaxf(m[3], a3);
+      x[u] = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
+    }
+    float y[4], z[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // lanes 0-31 keep rows 0-3, lanes 32-63 rows 4-7
+      const float send = b5 ? x[i] : x[i + 4], keep = b5 ? x[i + 4] : x[i];
+      y[i] = fmaxf(keep, __shfl_xor(send, 32));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float send = b4 ? y[i] : y[i + 2], keep = b4 ? y[i + 2] : y[i];
+      z[i] = fmaxf(keep, __shfl_xor(send, 16));
+    }
+    float w = fmaxf(b3 ? z[1] : z[0], __shfl_xor(b3 ? z[0] : z[1], 8));
+    w = fmaxf(w, __shfl_xor(w, 4));
+    w = fmaxf(w, __shfl_xor(w, 2));
+    w = fmaxf(w, __shfl_xor(w, 1));
+    if ((lane & 7) == 0) red[wave][r - r0 + slot] = w;  // (rows past r1 write zeros into unused slots)
+  }
+  if (col_ok) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicMax(cbits + c4 + e, __float_as_uint(m[e]));
+  }
+  __syncthreads();
+  if (tid < r1 - r0) {
+    const float mx = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
+    if (rscale)
+      rscale[r0 + tid] = f16x2_scale(mx);
+    else
+      atomicMax(rbits + r0 + tid, __float_as_uint(mx));
+  }
 }
 
 // dW[n, k] = sum_s part[s][n, k], s ascending (fixed order), float4 per thread
@@ -1609,6 +1673,44 @@ extern "C" lpg_status lpg_colscale_f32(int64_t R, int64_t N, const float *G, int
   }
   hipLaunchKernelGGL(colscale_f32, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, N, mbits, scale);
   LPG_HIP(hipGetLastError());
+  return LPG_OK;
+}
+
+extern "C" int64_t lpg_rowcolscale_workspace_bytes(int64_t R, int64_t N) {
+  if (R <= 0 || N <= 0) return 0;
+  return (N + (N > 1024 ? R : 0)) * (int64_t)sizeof(unsigned);
+}
+
+extern "C" lpg_status lpg_rowcolscale_f32(int64_t R, int64_t N, const float *G, int64_t ldg, float *rscale,
+                                          float *cscale, void *workspace, void *stream) {
+  LPG_REQUIRE(R >= 0 && N >= 0, "lpg_rowcolscale_f32: negative size");
+  if (R == 0 || N == 0) {  // no maxima: every scale is the all-zero one (colscale_f32 on no bits)
+    hipStream_t st = as_stream(stream);
+    if (N > 0 && cscale)
+      hipLaunchKernelGGL(colscale_f32, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, N, nullptr, cscale);
+    if (R > 0 && rscale)
+      hipLaunchKernelGGL(colscale_f32, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, R, nullptr, rscale);
+    LPG_HIP(hipGetLastError());
+    return LPG_OK;
+  }
+  LPG_REQUIRE(rscale && cscale && workspace && G, "lpg_rowcolscale_f32: NULL pointer");
+  LPG_REQUIRE(ldg >= N && N % 4 == 0 && ldg % 4 == 0 && aligned16(G),
+              "lpg_rowcolscale_f32: N and ldg multiples of 4 floats, G 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  unsigned *cbits = static_cast<unsigned *>(workspace);
+  unsigned *rbits = N > 1024 ? cbits + N : nullptr;
+  const int64_t chunks = (R + kColChunk - 1) / kColChunk;
+  LPG_REQUIRE(chunks < 65536, "lpg_rowcolscale_f32: too many rows");
+  LPG_HIP(hipMemsetAsync(cbits, 0, (N + (rbits ? R : 0)) * sizeof(unsigned), st));
+  hipLaunchKernelGGL(rowcolmax_f32, dim3((unsigned)((N + 1023) / 1024), (unsigned)chunks), dim3(256), 0, st, R, N, G,
+                     ldg, kColChunk, cbits, rbits, rbits ? nullptr : rscale);
+  LPG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(colscale_f32, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, N, cbits, cscale);
+  LPG_HIP(hipGetLastError());
+  if (rbits) {
+    hipLaunchKernelGGL(colscale_f32, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, R, rbits, rscale);
+    LPG_HIP(hipGetLastError());
+  }
   return LPG_OK;
 }
 

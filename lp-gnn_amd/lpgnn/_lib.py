@@ -108,6 +108,8 @@ HEADER_SYMBOLS = (
     "lpg_wgrad_f16x2_f32",
     "lpg_colscale_workspace_bytes",
     "lpg_colscale_f32",
+    "lpg_rowcolscale_workspace_bytes",
+    "lpg_rowcolscale_f32",
 )
 
 c_i64, c_i32, c_p = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
@@ -240,6 +242,10 @@ def lib() -> ctypes.CDLL:
     L.lpg_colscale_workspace_bytes.restype = c_i64
     L.lpg_colscale_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p]
     L.lpg_colscale_f32.restype = c_i32
+    L.lpg_rowcolscale_workspace_bytes.argtypes = [c_i64, c_i64]
+    L.lpg_rowcolscale_workspace_bytes.restype = c_i64
+    L.lpg_rowcolscale_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p]
+    L.lpg_rowcolscale_f32.restype = c_i32
     L.lpg_rowscale_f32.argtypes = [c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p]
     L.lpg_rowscale_f32.restype = c_i32
     L.lpg_split_f16x2.argtypes = [c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_i64, c_i64,

@@ -179,19 +179,56 @@ class _ScaleCache:
     def __init__(self):
         self._d = {}
 
-    def get(self, kind: str, t: Tensor, make):
-        key = (kind, id(t))
-        e = self._d.get(key)
+    def lookup(self, kind: str, t: Tensor):
+        e = self._d.get((kind, id(t)))
         if e is not None and e[0]() is t and e[1] == t._version and e[2] == (t.data_ptr(), tuple(t.shape)):
             return e[3]
-        v = make(t)
+        return None
+
+    def put(self, kind: str, t: Tensor, v):
         if len(self._d) > 64:
             self._d = {k: x for k, x in self._d.items() if x[0]() is not None}
-        self._d[key] = (weakref.ref(t), t._version, (t.data_ptr(), tuple(t.shape)), v)
+        self._d[(kind, id(t))] = (weakref.ref(t), t._version, (t.data_ptr(), tuple(t.shape)), v)
+
+    def get(self, kind: str, t: Tensor, make):
+        v = self.lookup(kind, t)
+        if v is None:
+            v = make(t)
+            self.put(kind, t, v)
         return v
 
 
 _SCALES = _ScaleCache()
+
+
+def _both_ok(t: Tensor) -> bool:
+    return (t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and t.shape[1] % 4 == 0
+            and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 and t.shape[1] > 0)
+
+
+def _scale(kind: str, t: Tensor) -> Tensor:
+    """The cached ``kind`` ("row" / "col") scales of t; a miss on an operand lpg_rowcolscale_f32 accepts
+    sweeps it once for both (every f16x2 operand of a training step -- layer inputs, dZ, S^T dZ -- is a
+    row-scaled GEMM operand and a column-scaled weight-gradient operand)."""
+    v = _SCALES.lookup(kind, t)
+    if v is not None:
+        return v
+    if not _both_ok(t):
+        v = (_rowscale1 if kind == "row" else _colscale1)(t)
+        _SCALES.put(kind, t, v)
+        return v
+    R, N = t.shape
+    L = _lib.lib()
+    rs = torch.empty(R, dtype=torch.float32, device=t.device)
+    cs = torch.empty(N, dtype=torch.float32, device=t.device)
+    ws = torch.empty(max(4, L.lpg_rowcolscale_workspace_bytes(R, N)) // 4, dtype=torch.float32, device=t.device)
+    with torch.cuda.device(t.device):
+        st = L.lpg_rowcolscale_f32(R, N, t.data_ptr(), t.stride(0), rs.data_ptr(), cs.data_ptr(), ws.data_ptr(),
+                                   _lib.stream_of(t))
+    _lib.check(st, "lpg_rowcolscale_f32")
+    _SCALES.put("row", t, rs)
+    _SCALES.put("col", t, cs)
+    return rs if kind == "row" else cs
 
 
 def _rowscale1(A: Tensor) -> Tensor:
@@ -206,12 +243,13 @@ def _rowscale1(A: Tensor) -> Tensor:
 
 def rowscale(A1: Tensor, A2: Tensor | None = None) -> Tensor:
     """The f16x2 power-of-2 scale of every row of [A1 | A2] (fp32 [M]; lpg_rowscale_f32): the row's largest
-    |x| times it lies in [2^14, 2^15) (an all-zero row: 2^115).  Per operand, cached (_ScaleCache); the
-    scale of the two side by side is the smaller of theirs (a power of 2 decreasing in the maximum)."""
-    s1 = _SCALES.get("row", A1, _rowscale1)
+    |x| times it lies in [2^14, 2^15) (an all-zero row: 2^115).  Per operand, cached (_ScaleCache, both
+    scales of an operand from one sweep: _scale); the scale of the two side by side is the smaller of
+    theirs (a power of 2 decreasing in the maximum)."""
+    s1 = _scale("row", A1)
     if A2 is None or A2.shape[1] == 0:
         return s1
-    return torch.minimum(s1, _SCALES.get("row", A2, _rowscale1))
+    return torch.minimum(s1, _scale("row", A2))
 
 
 def split_f16x2(W1: Tensor, W2: Tensor | None = None, transpose: bool = False):
@@ -345,8 +383,8 @@ def wgrad(G: Tensor, X: Tensor, arith: str | None = None) -> Tensor:
 
 def colscale(G: Tensor) -> Tensor:
     """The f16x2 power-of-2 scale of every column of G [R, N] (fp32 [N]; lpg_colscale_f32): the column's
-    largest |x| over the rows times it lies in [2^14, 2^15) (cached per operand, _ScaleCache)."""
-    return _SCALES.get("col", G, _colscale1)
+    largest |x| over the rows times it lies in [2^14, 2^15) (cached per operand with its row scales, _scale)."""
+    return _scale("col", G)
 
 
 def _colscale1(G: Tensor) -> Tensor:

@@ -59,6 +59,41 @@ def test_rowscale_and_split():
         assert bool((P[:, :, Wt.shape[1]:] == 0).all())  # zero padding
 
 
+@pytest.mark.parametrize("R,N", [(1000, 256), (100_000, 1024), (3001, 2048), (257, 1028), (5, 4), (0, 64), (64, 0)])
+def test_rowcolscale_equals_separate_sweeps(R, N):
+    """lpg_rowcolscale_f32 (one read, both scales) gives exactly the row sweep's and the column sweep's scales
+    (ragged rows and columns, N above one column block, zero rows, empty operands)."""
+    from lpgnn import _lib
+    torch.manual_seed(R + N)
+    G = torch.randn(R, N, device=DEV) * torch.exp(3 * torch.randn(R, 1, device=DEV)) \
+        * torch.exp(3 * torch.randn(1, N, device=DEV))
+    if R > 10:
+        G[3] = 0.0
+    L = _lib.lib()
+    rs = torch.full((R,), -1.0, device=DEV)
+    cs = torch.full((N,), -1.0, device=DEV)
+    ws = torch.empty(max(16, L.lpg_rowcolscale_workspace_bytes(R, N)), dtype=torch.uint8, device=DEV)
+    _lib.check(L.lpg_rowcolscale_f32(R, N, G.data_ptr(), max(N, 4), rs.data_ptr(), cs.data_ptr(), ws.data_ptr(),
+                                     _lib.stream_of(G)), "lpg_rowcolscale_f32")
+    zero = 2.0 ** 115
+    ref_r = F._rowscale1(G) if N else torch.full((R,), zero, device=DEV)
+    ref_c = F._colscale1(G) if R else torch.full((N,), zero, device=DEV)
+    assert torch.equal(rs, ref_r)
+    assert torch.equal(cs, ref_c)
+
+
+def test_scale_cache_one_sweep_for_both():
+    """A row-scale request fills the column entry too (and the other way round)."""
+    G = torch.randn(5000, 512, device=DEV)
+    r = F.rowscale(G)
+    c = F._SCALES.lookup("col", G)
+    assert c is not None and torch.equal(c, F._colscale1(G)) and F.colscale(G) is c
+    H = torch.randn(700, 96, device=DEV)
+    c = F.colscale(H)
+    assert torch.equal(F._SCALES.lookup("row", H), F._rowscale1(H)) and torch.equal(c, F._colscale1(H))
+    del r
+
+
 @pytest.mark.parametrize("M,N,K1,K2,relu,acc,bias", [
     (5000, 1024, 1024, 0, False, False, False),
     (5000, 1024, 1024, 0, True, False, True),
