@@ -63,6 +63,20 @@ __device__ __forceinline__ void dma16(uint64_t p, uint32_t n, unsigned char *lds
 #endif
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// dma16 split in two: the descriptor once (outside a k loop: wave-uniform SGPRs, no v_readfirstlane
+// per piece), the piece with it
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dma_rsrc(uint64_t p, uint32_t n) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
+}
+__device__ __forceinline__ void dma16r(__amdgpu_buffer_rsrc_t rs, unsigned char *lds, uint32_t voff, int soff) {
+  typedef __attribute__((address_space(3))) void lds_v;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_v *)lds, 16, voff, soff, 0, 0);
+}
+#endif
+
 // The ReLU/dropout backward of two packed bf16 values (element 0 in the low half):
 // (y > 0) ? RNE_bf16(g * scale) : 0 per element, on the packed datapath -- one v_pk_mul_f32 and one
 // v_cvt_pk_bf16_f32 per pair.  Shared by lpg_relu_bwd_colsum_bf16 (bwd.hip) and the folded form in

@@ -556,22 +556,30 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
       vo[p] = (uint32_t)((plane * a.ps1 + rc * a.ldw1 + swzW(row, lane & 3) * 8) * 2);
     }
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the four descriptors (operand x k phase) once, in SGPRs: a stage selects, it does not rebuild
+  const __amdgpu_buffer_rsrc_t rsa1 = dma_rsrc(pa1, na1), rsa2 = dma_rsrc(pa2, na2);
+  const __amdgpu_buffer_rsrc_t rsw1 = dma_rsrc(pw1, nw1), rsw2 = dma_rsrc(pw2, nw2);
+#endif
   auto stage = [&](int b, int t) {
+#if defined(__HIP_DEVICE_COMPILE__)
     const bool p2 = t >= nk1;
     const int kk = p2 ? t - nk1 : t;
-    const uint64_t pa = p2 ? pa2 : pa1, pw = p2 ? pw2 : pw1;
-    const uint32_t na = p2 ? na2 : na1, nw = p2 ? nw2 : nw1;
+    const __amdgpu_buffer_rsrc_t ra = p2 ? rsa2 : rsa1, rw = p2 ? rsw2 : rsw1;
     unsigned char *base = smem + b * TILE_BYTES;
 #pragma unroll
     for (int p = 0; p < PPW; ++p) {
       const int q = wave + NW * p;  // wave-uniform
       if (PT % NW == 0 || q < PT) {
         if (q < PA_T)
-          dma16(pa, na, base + q * 1024, vo[p], kk * (BK * 4));
+          dma16r(ra, base + q * 1024, vo[p], kk * (BK * 4));
         else
-          dma16(pw, nw, base + q * 1024, vo[p], kk * (BK * 2));
+          dma16r(rw, base + q * 1024, vo[p], kk * (BK * 2));
       }
     }
+#else
+    (void)b, (void)t;
+#endif
   };
 
   f32x4 accH[TM][TN], accL[TM][TN];
@@ -1282,13 +1290,15 @@ __global__ __launch_bounds__(256) void colscale_f32(int64_t N, const unsigned *_
 
 // Row AND column maxima of |G| in one read (an operand that is both a row-scaled GEMM A operand and a
 // column-scaled weight-gradient operand: the layer inputs, dZ, S^T dZ).  colmax_f32's blocks (column
-// block of 1024, row chunk of rc <= 256, eight rows in flight); a thread's four |x| of each of the
+// block of 1024, row chunk of rc <= 256, sixteen rows in flight); a thread's four |x| of each of
 // eight rows reduce to one value per row, the eight rows over the wave's 64 lanes in a halving
 // butterfly (each exchange halves the values a lane carries: 4 + 2 + 1 + 1 + 1 + 1 shuffles for
 // eight rows, not 48), the four waves through LDS.  One column block (N <= 1024): the row's scale
-// stored directly; else an integer atomicMax per (row, column block) into rbits.
+// stored directly; else an integer atomicMax per (row, column block) into rbits.  The chunk's column
+// maxima go to cpart[chunk][N] with plain stores (an atomicMax per column and chunk cost a third of
+// the sweep: hundreds of chunks hit each column's address) and colfold_f32 folds them.
 __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const float *__restrict__ G, int64_t ldg,
-                                                     int64_t rc, unsigned *__restrict__ cbits,
+                                                     int64_t rc, float *__restrict__ cpart,
                                                      unsigned *__restrict__ rbits, float *__restrict__ rscale) {
   __shared__ float red[4][256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1298,11 +1308,16 @@ __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const
   const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0, b3 = (lane & 8) != 0;
   const int slot = (b5 ? 4 : 0) + (b4 ? 2 : 0) + (b3 ? 1 : 0);
   f32x4 m = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t r = r0; r < r1; r += 8) {
-    f32x4 v[8];
+  auto load8 = [&](int64_t r, f32x4(&v)[8]) {
 #pragma unroll
     for (int u = 0; u < 8; ++u)
       v[u] = (col_ok && r + u < r1) ? *reinterpret_cast<const f32x4 *>(G + (r + u) * ldg + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  // the next eight rows' loads issued before this eight's reduction: sixteen rows in flight
+  f32x4 v[8], nv[8];
+  load8(r0, v);
+  for (int64_t r = r0; r < r1; r += 8) {
+    if (r + 8 < r1) load8(r + 8, nv);
     float x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -1329,11 +1344,10 @@ __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const
     w = fmaxf(w, __shfl_xor(w, 2));
     w = fmaxf(w, __shfl_xor(w, 1));
     if ((lane & 7) == 0) red[wave][r - r0 + slot] = w;  // (rows past r1 write zeros into unused slots)
-  }
-  if (col_ok) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) atomicMax(cbits + c4 + e, __float_as_uint(m[e]));
+    for (int u = 0; u < 8; ++u) v[u] = nv[u];
   }
+  if (col_ok) *reinterpret_cast<f32x4 *>(cpart + (int64_t)blockIdx.y * N + c4) = m;
   __syncthreads();
   if (tid < r1 - r0) {
     const float mx = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
@@ -1341,6 +1355,34 @@ __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const
       rscale[r0 + tid] = f16x2_scale(mx);
     else
       atomicMax(rbits + r0 + tid, __float_as_uint(mx));
+  }
+}
+
+// scale[n] from the chunks' column maxima part[c][n]: a block per 64 columns, its 256 threads 16
+// float4 column groups x 16 chunk strides (loads independent, unrolled), then the 16 folded in LDS
+__global__ __launch_bounds__(256) void colfold_f32(int64_t chunks, int64_t N, const float *__restrict__ part,
+                                                   float *__restrict__ scale) {
+  __shared__ f32x4 red[16][16];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int64_t c4 = (int64_t)blockIdx.x * 64 + tx * 4;
+  f32x4 m = {0.f, 0.f, 0.f, 0.f};
+  if (c4 < N) {
+#pragma unroll 8
+    for (int64_t c = ty; c < chunks; c += 16) {
+      const f32x4 v = *reinterpret_cast<const f32x4 *>(part + c * N + c4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], v[e]);
+    }
+  }
+  red[ty][tx] = m;
+  __syncthreads();
+  if (ty == 0 && c4 < N) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], red[k][tx][e]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) scale[c4 + e] = f16x2_scale(m[e]);
   }
 }
 
@@ -1676,9 +1718,16 @@ extern "C" lpg_status lpg_colscale_f32(int64_t R, int64_t N, const float *G, int
   return LPG_OK;
 }
 
+#ifndef LPG_ROWCOL_CHUNK
+#define LPG_ROWCOL_CHUNK 256
+#endif
+constexpr int64_t kRowColChunk = LPG_ROWCOL_CHUNK;  // rows per block of the combined sweep (<= 256)
+static_assert(kRowColChunk % 8 == 0 && kRowColChunk <= 256, "rowcolmax_f32's LDS holds 256 rows");
+
 extern "C" int64_t lpg_rowcolscale_workspace_bytes(int64_t R, int64_t N) {
   if (R <= 0 || N <= 0) return 0;
-  return (N + (N > 1024 ? R : 0)) * (int64_t)sizeof(unsigned);
+  const int64_t chunks = (R + kRowColChunk - 1) / kRowColChunk;
+  return (chunks * N + (N > 1024 ? R : 0)) * (int64_t)sizeof(float);
 }
 
 extern "C" lpg_status lpg_rowcolscale_f32(int64_t R, int64_t N, const float *G, int64_t ldg, float *rscale,
@@ -1694,18 +1743,18 @@ extern "C" lpg_status lpg_rowcolscale_f32(int64_t R, int64_t N, const float *G, 
     return LPG_OK;
   }
   LPG_REQUIRE(rscale && cscale && workspace && G, "lpg_rowcolscale_f32: NULL pointer");
-  LPG_REQUIRE(ldg >= N && N % 4 == 0 && ldg % 4 == 0 && aligned16(G),
-              "lpg_rowcolscale_f32: N and ldg multiples of 4 floats, G 16-byte aligned");
+  LPG_REQUIRE(ldg >= N && N % 4 == 0 && ldg % 4 == 0 && aligned16(G) && aligned16(workspace),
+              "lpg_rowcolscale_f32: N and ldg multiples of 4 floats, G and the workspace 16-byte aligned");
   hipStream_t st = as_stream(stream);
-  unsigned *cbits = static_cast<unsigned *>(workspace);
-  unsigned *rbits = N > 1024 ? cbits + N : nullptr;
-  const int64_t chunks = (R + kColChunk - 1) / kColChunk;
+  const int64_t chunks = (R + kRowColChunk - 1) / kRowColChunk;
   LPG_REQUIRE(chunks < 65536, "lpg_rowcolscale_f32: too many rows");
-  LPG_HIP(hipMemsetAsync(cbits, 0, (N + (rbits ? R : 0)) * sizeof(unsigned), st));
+  float *cpart = static_cast<float *>(workspace);
+  unsigned *rbits = N > 1024 ? reinterpret_cast<unsigned *>(cpart + chunks * N) : nullptr;
+  if (rbits) LPG_HIP(hipMemsetAsync(rbits, 0, R * sizeof(unsigned), st));
   hipLaunchKernelGGL(rowcolmax_f32, dim3((unsigned)((N + 1023) / 1024), (unsigned)chunks), dim3(256), 0, st, R, N, G,
-                     ldg, kColChunk, cbits, rbits, rbits ? nullptr : rscale);
+                     ldg, kRowColChunk, cpart, rbits, rbits ? nullptr : rscale);
   LPG_HIP(hipGetLastError());
-  hipLaunchKernelGGL(colscale_f32, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, N, cbits, cscale);
+  hipLaunchKernelGGL(colfold_f32, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, chunks, N, cpart, cscale);
   LPG_HIP(hipGetLastError());
   if (rbits) {
     hipLaunchKernelGGL(colscale_f32, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, R, rbits, rscale);

@@ -63,16 +63,32 @@ struct Split2 {
 // 8 consecutive k of one row, times the row's scale s (a power of 2: exact), as h = RNE_f16(x s) and
 // l = RNE_f16(x s - h) (the residual exact in fp32): |x s - h - l| <= 2^-22 |x s| while |x s| >= 2^-3,
 // and <= 2^-25 below (fp16 subnormals); the scale puts the row's largest |x| in [2^14, 2^15)
+//
+// Per pair of k, four mixed-precision FMAs and nothing else: h = fma_mix(x, s, 0) rounded to fp16 (lo
+// half, then the next x into the hi half), l = fma_mix(x, s, -h) with h read as fp16 from its half --
+// x s - h computed exactly inside the FMA and rounded once, the same RNE_f16 of the exact residual
+// the f32 multiply / convert / subtract / convert chain gave (x s is exact: s a power of 2; x s - h
+// is exact in fp32), in 2 instructions per element instead of 5.
+__device__ __forceinline__ void split_pair_f16(float x0, float x1, float s, uint32_t &h, uint32_t &l) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h), "=&v"(l)
+      : "v"(x0), "v"(x1), "v"(s));
+}
+
 __device__ __forceinline__ Split2 split2f16(f32x4 lo, f32x4 hi, float s) {
-  Split2 r;
+  u32x4 H, L;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const float v = (i < 4 ? lo[i] : hi[i - 4]) * s;
-    const _Float16 h = (_Float16)v;
-    r.h[i] = h;
-    r.l[i] = (_Float16)sub_f32(v, (float)h);
+  for (int i = 0; i < 4; ++i) {
+    const float x0 = i < 2 ? lo[2 * i] : hi[2 * i - 4], x1 = i < 2 ? lo[2 * i + 1] : hi[2 * i - 3];
+    uint32_t h, l;
+    split_pair_f16(x0, x1, s, h, l);
+    H[i] = h;
+    L[i] = l;
   }
-  return r;
+  return Split2{__builtin_bit_cast(f16x8, H), __builtin_bit_cast(f16x8, L)};
 }
 
 // 4-B raw buffer load (v# in SGPRs: base and size wave-uniform): offsets at or past `nbytes` return
