@@ -256,6 +256,15 @@ lpg_status lpg_fc_f32(int64_t M, int64_t N,
                       int64_t K2, const float *A2, int64_t lda2, const float *W2, int64_t ldw2,
                       const float *bias, float *C, int64_t ldc, int32_t flags,
                       float dropout_p, uint64_t seed, int64_t row_offset, const int64_t *row_keys, void *stream);
+/* lpg_fc_f32's small-K form (conv1: 4 <= K1, K1 + K2 <= 16) that also returns C's f16x2 scales from
+ * its own stores (rscale [M], cscale [N]: the values lpg_rowcolscale_f32 gives on C); flags: the ReLU
+ * bit only (no addend, no dropout), N <= 1024; scale_ws lpg_fc_smallk_scales_workspace_bytes(M, N)
+ * bytes, 16-byte aligned.  LPG_ERR_UNSUPPORTED when the small-K kernel does not take the operands. */
+int64_t lpg_fc_smallk_scales_workspace_bytes(int64_t M, int64_t N);
+lpg_status lpg_fc_smallk_scales_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1, const float *W1,
+                                    int64_t ldw1, int64_t K2, const float *A2, int64_t lda2, const float *W2,
+                                    int64_t ldw2, const float *bias, float *C, int64_t ldc, int32_t flags,
+                                    float *rscale, float *cscale, void *scale_ws, void *stream);
 
 /* fp32 FC on the bf16 matrix cores (same operation and epilogue as
  * lpg_fc_f32; also the input-gradient GEMMs dZ W of its backward, with W
@@ -580,6 +589,15 @@ lpg_status lpg_linear_small_bwd_f32(int64_t M, int64_t K, int64_t N, const float
 lpg_status lpg_heads_relu_bwd_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W,
                                   const float *Y, int64_t ldy, float scale, float *dZ, int64_t lddz, float *dW,
                                   float *db, float *dbY, void *workspace, void *stream);
+/* The same, also returning dZ's f16x2 scales from its own stores (rscale [M], cscale [K]: the values
+ * lpg_rowcolscale_f32 gives on dZ, without reading it again when K is a multiple of 1024; other K: the
+ * pass, then that sweep); K a multiple of 4, scale_ws
+ * lpg_heads_scales_workspace_bytes(M, K) bytes, 16-byte aligned. */
+int64_t lpg_heads_scales_workspace_bytes(int64_t M, int64_t K);
+lpg_status lpg_heads_relu_bwd_scales_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
+                                         const float *W, const float *Y, int64_t ldy, float scale, float *dZ,
+                                         int64_t lddz, float *dW, float *db, float *dbY, float *rscale,
+                                         float *cscale, void *scale_ws, void *workspace, void *stream);
 
 /* bf16 twin of lpg_relu_wgrad_smallk_f32 (c5 conv1, arch.py:170 through
  * train.py:128): g, y, A1, A2 bf16 bit patterns; dW1, dW2, db fp32.  y == NULL:

@@ -393,11 +393,18 @@ __global__ __launch_bounds__(kT) void wgrad_smallk_p2(int64_t nrow, int64_t N, i
 // group's arithmetic.
 template <bool BF> using H16 = typename std::conditional<BF, uint4, float4>::type;
 
-template <int N, bool MASK, bool BF, bool STORE>
+//
+// SC (fp32, K a multiple of 1024 so every lane takes part in each k pass; f16x2 consumers of dZ): also
+// the f16x2 scale of every stored dH row (rsc[m]; a block holds
+// whole rows, so the row maximum is the block's: per group of eight rows a halving butterfly over the
+// wave (rowmax8), the four waves through LDS) and the block's column maxima of |dH| (cpart[block][K],
+// folded by colfold_f32) -- the scales lpg_rowcolscale_f32 would take from a second read of dZ.
+template <int N, bool MASK, bool BF, bool STORE, bool SC = false>
 __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const float *__restrict__ G, int64_t ldg,
                                                    const float *__restrict__ W, const void *__restrict__ Hv,
                                                    int64_t ldh, void *__restrict__ dHv, int64_t lddh, float scale,
-                                                   float *__restrict__ part, float *__restrict__ party) {
+                                                   float *__restrict__ part, float *__restrict__ party,
+                                                   float *__restrict__ rsc = nullptr, float *__restrict__ cpart = nullptr) {
   using E = typename std::conditional<BF, uint16_t, float>::type;
   constexpr int EPT = BF ? 8 : 4;  // columns per thread
   constexpr int P = EPT / 2;       // column pairs
@@ -406,6 +413,12 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
   constexpr int CH = kRowsColsum;  // column-sum chunk
   static_assert(RB % CH == 0 && CH % (2 * U) == 0, "block shape");
   __shared__ float4 sg4[RB];
+  __shared__ float rmx[SC ? kT / 64 : 1][SC ? RB : 1];  // SC: per wave, the rows' maxima of |dH|
+  static_assert(!SC || (!BF && U == 8), "the f16x2 scales: fp32, groups of eight rows");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if constexpr (SC) {
+    for (int i = threadIdx.x; i < (kT / 64) * RB; i += kT) rmx[i / RB][i % RB] = 0.f;
+  }
   const E *H = static_cast<const E *>(Hv);
   E *dH = static_cast<E *>(dHv);
   const int64_t r0 = (int64_t)blockIdx.x * RB;
@@ -446,7 +459,10 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
         hb[u] = *reinterpret_cast<const H16<BF> *>(H + m * ldh + k);
       }
     };
-    auto row = [&](H16<BF> hv, int64_t m) {
+    lpg_f32x2 cmx[P];  // SC: the thread's column maxima of |dH| over the block's rows
+#pragma unroll
+    for (int q = 0; q < P; ++q) cmx[q] = lpg_f32x2{0.f, 0.f};
+    auto row = [&](H16<BF> hv, int64_t m) -> float {
       lpg_f32x2 h[P];
       uint32_t hw[4] = {0u, 0u, 0u, 0u};
       if constexpr (BF) {
@@ -490,6 +506,21 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
         cs[0] = cs[0] + lpg_f32x2{o[0], o[1]};
         cs[1] = cs[1] + lpg_f32x2{o[2], o[3]};
         if (STORE) *reinterpret_cast<float4 *>(dH + m * lddh + k) = make_float4(o[0], o[1], o[2], o[3]);
+        if constexpr (SC) {
+          const float a0 = fabsf(o[0]), a1 = fabsf(o[1]), a2 = fabsf(o[2]), a3 = fabsf(o[3]);
+          cmx[0] = lpg_f32x2{fmaxf(cmx[0][0], a0), fmaxf(cmx[0][1], a1)};
+          cmx[1] = lpg_f32x2{fmaxf(cmx[1][0], a2), fmaxf(cmx[1][1], a3)};
+          return fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
+        }
+      }
+      return 0.f;
+    };
+    // SC: eight rows' lane maxima -> the rows' wave maxima (rows m0 .. m0 + 7 of the block) into rmx
+    auto rows8 = [&](const float (&x)[8], int64_t m0) {
+      if constexpr (SC) {
+        const float w = rowmax8(x, lane);
+        const int r = (int)(m0 - r0) + rowmax8_slot(lane);
+        if ((lane & 7) == 0 && r < RB) rmx[wv][r] = fmaxf(rmx[wv][r], w);
       }
     };
     auto flush = [&](int ch) {  // the chunk's column sums into relu_bwd_colsum's partial image
@@ -508,12 +539,26 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
       for (int j = 0; j < CH / (2 * U); ++j) {
         issue(hB, cb + (2 * j + 1) * U);
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SC) {
+          float xm[8];
 #pragma unroll
-        for (int u = 0; u < U; ++u) row(hA[u], cb + 2 * j * U + u);
+          for (int u = 0; u < U; ++u) xm[u % 8] = row(hA[u], cb + 2 * j * U + u);
+          rows8(xm, cb + 2 * j * U);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) row(hA[u], cb + 2 * j * U + u);
+        }
         issue(hA, cb + (2 * j + 2) * U);
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SC) {
+          float xm[8];
 #pragma unroll
-        for (int u = 0; u < U; ++u) row(hB[u], cb + (2 * j + 1) * U + u);
+          for (int u = 0; u < U; ++u) xm[u % 8] = row(hB[u], cb + (2 * j + 1) * U + u);
+          rows8(xm, cb + (2 * j + 1) * U);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) row(hB[u], cb + (2 * j + 1) * U + u);
+        }
       }
       flush(ch);
     }
@@ -521,9 +566,16 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
       const int64_t cb = r0 + (int64_t)nfull * CH;
       for (int64_t m0 = cb; m0 < r1; m0 += U) {
         if (m0 != cb) issue(hA, m0);
+        if constexpr (SC) {
+          float xm[8];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (m0 + u < r1) row(hA[u], m0 + u);
+          for (int u = 0; u < U; ++u) xm[u % 8] = m0 + u < r1 ? row(hA[u], m0 + u) : 0.f;
+          rows8(xm, m0);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (m0 + u < r1) row(hA[u], m0 + u);
+        }
       }
       flush(nfull);
     }
@@ -533,6 +585,17 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
       for (int q = 0; q < P; q += 2)
         *reinterpret_cast<float4 *>(pw + c * K + k + 2 * q) =
             make_float4(acc[c][q][0], acc[c][q][1], acc[c][q + 1][0], acc[c][q + 1][1]);
+    if constexpr (SC)
+      *reinterpret_cast<float4 *>(cpart + (int64_t)blockIdx.x * K + k) = make_float4(cmx[0][0], cmx[0][1], cmx[1][0], cmx[1][1]);
+  }
+  if constexpr (SC) {  // the rows' maxima over the four waves (and every k pass): the row scales
+    __syncthreads();
+    if (threadIdx.x < RB && r0 + threadIdx.x < r1) {
+      float mx = rmx[0][threadIdx.x];
+#pragma unroll
+      for (int w = 1; w < kT / 64; ++w) mx = fmaxf(mx, rmx[w][threadIdx.x]);
+      rsc[r0 + threadIdx.x] = f16x2_scale(mx);
+    }
   }
   if (threadIdx.x == 0) {  // db = sum_m G[m, c] in row order
     float sg[4] = {0.f, 0.f, 0.f, 0.f};
@@ -861,7 +924,8 @@ int64_t heads_bwd_floats(int64_t M, int64_t K, int64_t N) {
 template <bool BF>
 lpg_status heads_bwd(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg, const float *W, const void *H,
                      int64_t ldh, void *dH, int64_t lddh, float scale, float *dW, float *db, float *dbY, bool mask,
-                     void *workspace, void *stream, const char *what) {
+                     void *workspace, void *stream, const char *what, float *rscale = nullptr,
+                     float *cscale = nullptr, float *cpart = nullptr) {
   constexpr int EPT = BF ? 8 : 4;
   LPG_REQUIRE(M >= 0 && K >= 0 && N >= 1 && N <= kSmallNMax, "%s: need 1 <= N <= %d", what, kSmallNMax);
   LPG_REQUIRE(K % EPT == 0 && ldh % EPT == 0 && (dH == nullptr || lddh % EPT == 0) && ldg >= N,
@@ -885,8 +949,16 @@ lpg_status heads_bwd(int64_t M, int64_t K, int64_t N, const float *G, int64_t ld
   float *party = part + fold_floats(nblk, tot);
   float *py = dbY ? party : nullptr;
   const dim3 grid((unsigned)nblk), block(kT);
+  const bool sc = rscale != nullptr;
+  if (sc) {
+    LPG_REQUIRE(!BF && mask && cscale && cpart && aligned16(cpart) && K % 4 == 0,
+                "%s: the f16x2 scales need the fp32 masked form, cscale and a 16-byte aligned partial buffer", what);
+  }
 #define LPG_HB(NN)                                                                                                \
-  if (mask)                                                                                                       \
+  if (sc && !BF)                                                                                                  \
+    hipLaunchKernelGGL((heads_bwd_p1<NN, true, false, true, true>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH,  \
+                       lddh, scale, part, py, rscale, cpart);                                                     \
+  else if (mask)                                                                                                  \
     hipLaunchKernelGGL((heads_bwd_p1<NN, true, BF, true>), grid, block, 0, s, M, K, G, ldg, W, H, ldh, dH, lddh,   \
                        scale, part, py);                                                                          \
   else if (dH)                                                                                                    \
@@ -903,6 +975,10 @@ lpg_status heads_bwd(int64_t M, int64_t K, int64_t N, const float *G, int64_t ld
   }
 #undef LPG_HB
   LPG_HIP(hipGetLastError());
+  if (sc) {
+    hipLaunchKernelGGL(colfold_f32, dim3((unsigned)((K + 63) / 64)), dim3(256), 0, s, nblk, K, cpart, cscale);
+    LPG_HIP(hipGetLastError());
+  }
   const float *img;
   const int64_t nrow = fold(nblk, tot, part, part + nblk * tot, &img, s);
   hipLaunchKernelGGL(linear_small_bwd_p2, dim3((unsigned)((tot + kT - 1) / kT)), dim3(kT), 0, s, nrow, K, (int)N, tot,
@@ -973,6 +1049,37 @@ extern "C" lpg_status lpg_heads_relu_bwd_f32(int64_t M, int64_t K, int64_t N, co
   LPG_REQUIRE(dZ != nullptr, "lpg_heads_relu_bwd_f32: NULL dZ");
   return heads_bwd<false>(M, K, N, G, ldg, W, Y, ldy, dZ, lddz, scale, dW, db, dbY, true, workspace, stream,
                           "lpg_heads_relu_bwd_f32");
+}
+
+// lpg_heads_relu_bwd_f32 that also returns dZ's f16x2 scales (rscale [M], cscale [K]: the values
+// lpg_rowcolscale_f32 gives on dZ) from the stores themselves; cpart: lpg_heads_scales_workspace_bytes.
+extern "C" int64_t lpg_heads_scales_workspace_bytes(int64_t M, int64_t K) {
+  if (M <= 0 || K <= 0) return 0;
+  const int64_t own = ((M + kRowsLinear - 1) / kRowsLinear) * K * (int64_t)sizeof(float);
+  const int64_t sweep = lpg_rowcolscale_workspace_bytes(M, K);  // (the K % 1024 != 0 route)
+  return own > sweep ? own : sweep;
+}
+
+extern "C" lpg_status lpg_heads_relu_bwd_scales_f32(int64_t M, int64_t K, int64_t N, const float *G, int64_t ldg,
+                                                    const float *W, const float *Y, int64_t ldy, float scale,
+                                                    float *dZ, int64_t lddz, float *dW, float *db, float *dbY,
+                                                    float *rscale, float *cscale, void *scale_ws, void *workspace,
+                                                    void *stream) {
+  LPG_REQUIRE(dZ != nullptr && rscale != nullptr, "lpg_heads_relu_bwd_scales_f32: NULL dZ / rscale");
+  if (M == 0 || K == 0) {  // no rows: lpg_rowcolscale_f32's empty-operand scales
+    const lpg_status st = heads_bwd<false>(M, K, N, G, ldg, W, Y, ldy, dZ, lddz, scale, dW, db, dbY, true, workspace,
+                                           stream, "lpg_heads_relu_bwd_scales_f32");
+    if (st != LPG_OK) return st;
+    return lpg_rowcolscale_f32(M, K, nullptr, K, rscale, cscale, nullptr, stream);
+  }
+  if (K % (kT * 4) != 0) {  // a k pass with idle lanes cannot run the rows' butterfly: the pass, then a sweep
+    const lpg_status st = heads_bwd<false>(M, K, N, G, ldg, W, Y, ldy, dZ, lddz, scale, dW, db, dbY, true, workspace,
+                                           stream, "lpg_heads_relu_bwd_scales_f32");
+    if (st != LPG_OK) return st;
+    return lpg_rowcolscale_f32(M, K, dZ, lddz, rscale, cscale, scale_ws, stream);
+  }
+  return heads_bwd<false>(M, K, N, G, ldg, W, Y, ldy, dZ, lddz, scale, dW, db, dbY, true, workspace, stream,
+                          "lpg_heads_relu_bwd_scales_f32", rscale, cscale, static_cast<float *>(scale_ws));
 }
 
 extern "C" int64_t lpg_heads_bwd_bf16_workspace_bytes(int64_t M, int64_t K, int64_t N) {

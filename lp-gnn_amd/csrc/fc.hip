@@ -69,6 +69,10 @@ struct FcArgs {
   // a slice of the rows; drop_row, fc_common.h)
   int64_t row_off;
   const int64_t *row_keys;
+  // fc_smallk_f32<..., SC>: the f16x2 row scales of C (rsc[m], N <= 1024) and the blocks' column maxima
+  // of |C| (cpart[row split][N], folded by colfold_f32) from the stores themselves
+  float *rsc;
+  float *cpart;
 };
 
 __device__ __forceinline__ float epilogue(const FcArgs &a, float v, float b, int64_t row, int64_t col, bool relu) {
@@ -389,7 +393,7 @@ __device__ __forceinline__ void load_row_k(float (&x)[K > 0 ? K : 1], const floa
   }
 }
 
-template <int K1, int K2, bool RELU>
+template <int K1, int K2, bool RELU, bool SC = false>
 __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
   static_assert(K1 % 4 == 0 && K2 % 4 == 0 && K1 >= 4, "small-K kernel: K1, K2 multiples of 4");
   constexpr int KT = K1 + K2;
@@ -400,6 +404,9 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
   // every load of a chunk in flight together -- one at a time the staging cost a memory latency
   // per value); every lane then reads the same row values (LDS broadcast)
   __shared__ __attribute__((aligned(16))) float sx[2][kSmallKRows * KT];
+  __shared__ float rmx[SC ? 2 : 1][SC ? 4 : 1][SC ? kSmallKRows : 1];  // SC: per chunk parity and wave
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float cmx[4] = {0.f, 0.f, 0.f, 0.f};  // SC: the thread's column maxima of |C|
   const int64_t sb = blockIdx.y;
   const int64_t rb = sb * a.M / S, re = (sb + 1) * a.M / S;
   if (re <= rb) return;  // (block-uniform)
@@ -453,8 +460,8 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
       const int64_t r0 = rb + (int64_t)ch * kSmallKRows;
       const int64_t r1 = r0 + kSmallKRows < re ? r0 + kSmallKRows : re;
       const float *xb = sx[ch & 1];
-      if (col_ok) {
-        for (int64_t m = r0; m < r1; ++m) {
+      // one row: its outputs computed and stored; returns the lane's max |output| (SC)
+      auto one_row = [&](int64_t m) -> float {
           const float *xr = xb + (m - r0) * KT;
           const uint32_t rk = DROP ? drop_row_key(a.seed, drop_row(a.row_keys, a.row_off, m, a.M)) : 0u;
           float o[4];
@@ -491,7 +498,30 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
             }
           }
           *reinterpret_cast<float4 *>(a.C + m * a.ldc + c) = make_float4(o[0], o[1], o[2], o[3]);
+          if constexpr (SC) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cmx[e] = fmaxf(cmx[e], fabsf(o[e]));
+            return fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+          }
+          return 0.f;
+      };
+      if constexpr (SC) {
+        // groups of eight rows, every lane taking part in the butterfly (lanes past N contribute 0)
+        for (int64_t m8 = r0; m8 < r1; m8 += 8) {
+          float xm[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) xm[u] = (col_ok && m8 + u < r1) ? one_row(m8 + u) : 0.f;
+          const float w = rowmax8(xm, lane);
+          if ((lane & 7) == 0) rmx[ch & 1][wv][(int)(m8 - r0) + rowmax8_slot(lane)] = w;
         }
+        lds_barrier();
+        if (threadIdx.x < r1 - r0) {  // the chunk's row scales (one column group: whole rows here)
+          const float mx = fmaxf(fmaxf(rmx[ch & 1][0][threadIdx.x], rmx[ch & 1][1][threadIdx.x]),
+                                 fmaxf(rmx[ch & 1][2][threadIdx.x], rmx[ch & 1][3][threadIdx.x]));
+          a.rsc[r0 + threadIdx.x] = f16x2_scale(mx);
+        }
+      } else if (col_ok) {
+        for (int64_t m = r0; m < r1; ++m) one_row(m);
       }
       if (ch + 1 < nch) {  // the next chunk's rows (loaded a chunk ago) into the other buffer
         store_x((ch + 1) & 1);
@@ -503,6 +533,11 @@ __global__ __launch_bounds__(256) void fc_smallk_f32(FcArgs a, int64_t S) {
   using T_ = std::true_type;
   using F_ = std::false_type;
   const bool acc = a.accum, bias = a.bias != nullptr, drop = a.drop_thresh != 0;
+  if constexpr (SC) {  // (conv1's forms: bias, no addend, no dropout)
+    if (bias) rows(F_{}, T_{}, F_{}); else rows(F_{}, F_{}, F_{});
+    if (col_ok) *reinterpret_cast<float4 *>(a.cpart + sb * a.N + c) = make_float4(cmx[0], cmx[1], cmx[2], cmx[3]);
+    return;
+  }
   if (acc) {
     if (bias) { if (drop) rows(T_{}, T_{}, T_{}); else rows(T_{}, T_{}, F_{}); }
     else { if (drop) rows(T_{}, F_{}, T_{}); else rows(T_{}, F_{}, F_{}); }
@@ -522,8 +557,17 @@ inline int64_t smallk_splits(int64_t M, int64_t ncg, int64_t resident) {
 }
 
 template <int K1, int K2>
-lpg_status launch_smallk(const FcArgs &a, bool relu, hipStream_t s) {
+lpg_status launch_smallk(const FcArgs &a, bool relu, hipStream_t s, float *cscale = nullptr) {
   const int64_t ncg = (a.N + 1023) / 1024;
+  if (a.rsc) {  // the f16x2 scales of C from the stores (one column group), then the column fold
+    auto kern = relu ? fc_smallk_f32<K1, K2, true, true> : fc_smallk_f32<K1, K2, false, true>;
+    const int64_t S = smallk_splits(a.M, ncg, resident_blocks(kern, 256));
+    hipLaunchKernelGGL(kern, dim3(1u, (unsigned)S), dim3(256), 0, s, a, S);
+    LPG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(colfold_f32, dim3((unsigned)((a.N + 63) / 64)), dim3(256), 0, s, S, a.N, a.cpart, cscale);
+    LPG_HIP(hipGetLastError());
+    return LPG_OK;
+  }
   auto kern = relu ? fc_smallk_f32<K1, K2, true> : fc_smallk_f32<K1, K2, false>;
   const int64_t S = smallk_splits(a.M, ncg, resident_blocks(kern, 256));
   const dim3 grid((unsigned)ncg, (unsigned)S);
@@ -533,11 +577,12 @@ lpg_status launch_smallk(const FcArgs &a, bool relu, hipStream_t s) {
 }
 
 // K1, K2 multiples of 4, 4 <= K1, K1 + K2 <= 16; returns false if not covered
-bool try_smallk(const FcArgs &a, bool relu, hipStream_t s, lpg_status *st) {
+bool try_smallk(const FcArgs &a, bool relu, hipStream_t s, lpg_status *st, float *cscale = nullptr) {
   if (a.K1 < 4 || a.K1 + a.K2 > 16 || a.N % 4 || a.ldc % 4 || !aligned16(a.C)) return false;
   if ((a.N + 1023) / 1024 >= 65536) return false;
+  if (a.rsc && (a.N > 1024 || a.accum || a.drop_thresh != 0)) return false;
   switch (a.K1 * 100 + a.K2) {
-#define LPG_SK(X, Y) case X * 100 + Y: *st = launch_smallk<X, Y>(a, relu, s); return true;
+#define LPG_SK(X, Y) case X * 100 + Y: *st = launch_smallk<X, Y>(a, relu, s, cscale); return true;
     LPG_SK(4, 0) LPG_SK(4, 4) LPG_SK(4, 8) LPG_SK(4, 12) LPG_SK(8, 0) LPG_SK(8, 4) LPG_SK(8, 8)
     LPG_SK(12, 0) LPG_SK(12, 4) LPG_SK(16, 0)
 #undef LPG_SK
@@ -579,6 +624,41 @@ extern "C" lpg_status lpg_fc_f32(int64_t M, int64_t N, int64_t K1, const float *
   // 128 x 128, 64 KiB: 2 blocks / CU.  (A 3-stage ring, BK = 64, 128 x 256 and 256 x 128 tiles of
   // the same kernel gave the same bits and ran 4-20 % slower; they are not shipped.)
   return launch_fc<2, 2, 2, 2, 32, 2>(a, relu, s);
+}
+
+// conv1's narrow FC (the small-K kernel) that also returns C's f16x2 scales from its own stores (the
+// next layer's f16x2 GEMMs take C as a row-scaled A operand and a column-scaled weight-gradient
+// operand): rscale [M], cscale [N], the values lpg_rowcolscale_f32 gives on C.  LPG_ERR_UNSUPPORTED
+// unless the small-K kernel applies with N <= 1024, no addend and no dropout.
+extern "C" int64_t lpg_fc_smallk_scales_workspace_bytes(int64_t M, int64_t N) {
+  if (M <= 0 || N <= 0) return 0;
+  return ((M + kSmallKRows - 1) / kSmallKRows) * N * (int64_t)sizeof(float);
+}
+
+extern "C" lpg_status lpg_fc_smallk_scales_f32(int64_t M, int64_t N, int64_t K1, const float *A1, int64_t lda1,
+                                               const float *W1, int64_t ldw1, int64_t K2, const float *A2,
+                                               int64_t lda2, const float *W2, int64_t ldw2, const float *bias,
+                                               float *C, int64_t ldc, int32_t flags, float *rscale, float *cscale,
+                                               void *scale_ws, void *stream) {
+  LPG_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "lpg_fc_smallk_scales_f32: negative size");
+  if (M == 0 || N == 0) return LPG_OK;
+  LPG_REQUIRE(C != nullptr && ldc >= N && rscale && cscale && scale_ws && aligned16(scale_ws),
+              "lpg_fc_smallk_scales_f32: bad C / scale buffers");
+  LPG_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1 && ldw1 >= K1), "lpg_fc_smallk_scales_f32: bad A1/W1");
+  LPG_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2 && ldw2 >= K2), "lpg_fc_smallk_scales_f32: bad A2/W2");
+  LPG_REQUIRE(K1 % 4 == 0 && K2 % 4 == 0 && lda1 % 4 == 0 && ldw1 % 4 == 0 && (K2 == 0 || (lda2 % 4 == 0 && ldw2 % 4 == 0)),
+              "lpg_fc_smallk_scales_f32: K and leading dimensions must be multiples of 4 floats");
+  LPG_REQUIRE(aligned16(A1) && aligned16(W1) && (K2 == 0 || (aligned16(A2) && aligned16(W2))),
+              "lpg_fc_smallk_scales_f32: A/W must be 16-byte aligned");
+  LPG_REQUIRE((flags & ~1) == 0, "lpg_fc_smallk_scales_f32: only the ReLU flag (no addend) 0x%x", flags);
+  FcArgs a{M, N, K1, K2, A1, A2, W1, W2, bias, lda1, lda2, ldw1, ldw2, C, ldc, 0, 0, 0u, 0u, 1.f, 0, 0, nullptr};
+  a.rsc = rscale;
+  a.cpart = static_cast<float *>(scale_ws);
+  lpg_status st;
+  if (try_smallk(a, flags & 1, as_stream(stream), &st, cscale)) return st;
+  set_error("lpg_fc_smallk_scales_f32: the small-K kernel does not take these operands (K1 >= 4, K1 + K2 <= 16, "
+            "N <= 1024, N and ldc multiples of 4, C 16-byte aligned)");
+  return LPG_ERR_UNSUPPORTED;
 }
 
 extern "C" lpg_status lpg_relu_dropout_bwd_f32(int64_t n, const float *g, const float *y, float scale, float *out,

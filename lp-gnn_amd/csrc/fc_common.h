@@ -121,4 +121,77 @@ inline void dropout_params(float p, uint32_t *thresh, float *scale) {
   }
 }
 
+// ---- f16x2 operand scales (fc_x3.hip's f16x2 kernels; the maxima come from lpg_rowcolscale_f32 or from
+// the producing kernel's own stores: fc_smallk_f32, heads_bwd_p1) ----
+// ---- f16x2 operand preparation ---------------------------------------------------
+// The power-of-2 scale that puts a row's largest |x| in [2^14, 2^15): 2^(15 - e) for max = f 2^e,
+// f in [0.5, 1); 1 for a non-finite row (NaN / Inf propagate through the split as in fp32); for an
+// all-zero row the largest scale, 2^115, so the scale of two operands' rows side by side is the
+// smaller of their own (the host combines cached per-operand scales that way).  e is clamped to
+// [-100, 120] so the scale and its inverse stay normal fp32 numbers.
+__device__ __forceinline__ float f16x2_scale(float mx) {
+  if (mx == 0.f) return ldexpf(1.f, 115);
+  if (!(mx > 0.f) || !(mx <= 3.4e38f)) return 1.f;
+  int e;
+  frexpf(mx, &e);
+  e = e < -100 ? -100 : (e > 120 ? 120 : e);
+  return ldexpf(1.f, 15 - e);
+}
+
+// Eight rows' values x[0..7] (one per row, this lane's part) -> their maxima over the wave's 64 lanes in
+// a halving butterfly: each exchange halves what a lane carries (4 + 2 + 1 + 1 + 1 + 1 shuffles, not 48);
+// lane l ends with row ((l >> 5) & 1) * 4 + ((l >> 4) & 1) * 2 + ((l >> 3) & 1)'s maximum.
+__device__ __forceinline__ float rowmax8(const float (&x)[8], int lane) {
+  const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0, b3 = (lane & 8) != 0;
+  float y[4], z[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // lanes 0-31 keep rows 0-3, lanes 32-63 rows 4-7
+    const float send = b5 ? x[i] : x[i + 4], keep = b5 ? x[i + 4] : x[i];
+    y[i] = fmaxf(keep, __shfl_xor(send, 32));
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float send = b4 ? y[i] : y[i + 2], keep = b4 ? y[i + 2] : y[i];
+    z[i] = fmaxf(keep, __shfl_xor(send, 16));
+  }
+  float w = fmaxf(b3 ? z[1] : z[0], __shfl_xor(b3 ? z[0] : z[1], 8));
+  w = fmaxf(w, __shfl_xor(w, 4));
+  w = fmaxf(w, __shfl_xor(w, 2));
+  return fmaxf(w, __shfl_xor(w, 1));
+}
+__device__ __forceinline__ int rowmax8_slot(int lane) {
+  return ((lane & 32) ? 4 : 0) + ((lane & 16) ? 2 : 0) + ((lane & 8) ? 1 : 0);
+}
+
+namespace {
+typedef float lpg_cf32x4 __attribute__((ext_vector_type(4)));
+// scale[n] from the chunks' column maxima part[c][n]: a block per 64 columns, its 256 threads 16
+// float4 column groups x 16 chunk strides (loads independent, unrolled), then the 16 folded in LDS
+__global__ __launch_bounds__(256) void colfold_f32(int64_t chunks, int64_t N, const float *__restrict__ part,
+                                                   float *__restrict__ scale) {
+  __shared__ lpg_cf32x4 red[16][16];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int64_t c4 = (int64_t)blockIdx.x * 64 + tx * 4;
+  lpg_cf32x4 m = {0.f, 0.f, 0.f, 0.f};
+  if (c4 < N) {
+#pragma unroll 8
+    for (int64_t c = ty; c < chunks; c += 16) {
+      const lpg_cf32x4 v = *reinterpret_cast<const lpg_cf32x4 *>(part + c * N + c4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], v[e]);
+    }
+  }
+  red[ty][tx] = m;
+  __syncthreads();
+  if (ty == 0 && c4 < N) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], red[k][tx][e]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) scale[c4 + e] = f16x2_scale(m[e]);
+  }
+}
+}  // namespace
+
 }  // namespace lpg

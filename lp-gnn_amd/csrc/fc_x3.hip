@@ -120,21 +120,7 @@ __global__ __launch_bounds__(256) void split3_planes(int64_t rows, int64_t cols,
   }
 }
 
-// ---- f16x2 operand preparation ---------------------------------------------------
-// The power-of-2 scale that puts a row's largest |x| in [2^14, 2^15): 2^(15 - e) for max = f 2^e,
-// f in [0.5, 1); 1 for a non-finite row (NaN / Inf propagate through the split as in fp32); for an
-// all-zero row the largest scale, 2^115, so the scale of two operands' rows side by side is the
-// smaller of their own (the host combines cached per-operand scales that way).  e is clamped to
-// [-100, 120] so the scale and its inverse stay normal fp32 numbers.
-__device__ __forceinline__ float f16x2_scale(float mx) {
-  if (mx == 0.f) return ldexpf(1.f, 115);
-  if (!(mx > 0.f) || !(mx <= 3.4e38f)) return 1.f;
-  int e;
-  frexpf(mx, &e);
-  e = e < -100 ? -100 : (e > 120 ? 120 : e);
-  return ldexpf(1.f, 15 - e);
-}
-
+// ---- f16x2 operand preparation (f16x2_scale, rowmax8, colfold_f32: fc_common.h) ---------------------
 // sa[m] for the rows of [A1 | A2] (16-byte aligned rows, K1, K2 multiples of 4): one wave a row
 __global__ __launch_bounds__(256) void rowscale_f32(int64_t M, int64_t K1, const float *__restrict__ A1, int64_t lda1,
                                                     int64_t K2, const float *__restrict__ A2, int64_t lda2,
@@ -568,6 +554,8 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   // the four descriptors (operand x k phase) once, in SGPRs: a stage selects, it does not rebuild
   const __amdgpu_buffer_rsrc_t rsa1 = dma_rsrc(pa1, na1), rsa2 = dma_rsrc(pa2, na2);
   const __amdgpu_buffer_rsrc_t rsw1 = dma_rsrc(pw1, nw1), rsw2 = dma_rsrc(pw2, nw2);
+#else
+  (void)pa2, (void)pw2, (void)na1, (void)na2, (void)nw1, (void)nw2;
 #endif
   auto stage = [&](int b, int t) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1313,8 +1301,7 @@ __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const
   const int64_t c4 = ((int64_t)blockIdx.x * 256 + tid) * 4, r0 = (int64_t)blockIdx.y * rc;
   const int64_t r1 = r0 + rc < R ? r0 + rc : R;
   const bool col_ok = c4 < N;
-  const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0, b3 = (lane & 8) != 0;
-  const int slot = (b5 ? 4 : 0) + (b4 ? 2 : 0) + (b3 ? 1 : 0);
+  const int slot = rowmax8_slot(lane);
   f32x4 m = {0.f, 0.f, 0.f, 0.f};
   auto load8 = [&](int64_t r, f32x4(&v)[8]) {
 #pragma unroll
@@ -1336,21 +1323,7 @@ __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const
       m[3] = fmaxf(m[3], a3);
       x[u] = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
     }
-    float y[4], z[2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // lanes 0-31 keep rows 0-3, lanes 32-63 rows 4-7
-      const float send = b5 ? x[i] : x[i + 4], keep = b5 ? x[i + 4] : x[i];
-      y[i] = fmaxf(keep, __shfl_xor(send, 32));
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float send = b4 ? y[i] : y[i + 2], keep = b4 ? y[i + 2] : y[i];
-      z[i] = fmaxf(keep, __shfl_xor(send, 16));
-    }
-    float w = fmaxf(b3 ? z[1] : z[0], __shfl_xor(b3 ? z[0] : z[1], 8));
-    w = fmaxf(w, __shfl_xor(w, 4));
-    w = fmaxf(w, __shfl_xor(w, 2));
-    w = fmaxf(w, __shfl_xor(w, 1));
+    const float w = rowmax8(x, lane);
     if ((lane & 7) == 0) red[wave][r - r0 + slot] = w;  // (rows past r1 write zeros into unused slots)
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = nv[u];
@@ -1363,34 +1336,6 @@ __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const
       rscale[r0 + tid] = f16x2_scale(mx);
     else
       atomicMax(rbits + r0 + tid, __float_as_uint(mx));
-  }
-}
-
-// scale[n] from the chunks' column maxima part[c][n]: a block per 64 columns, its 256 threads 16
-// float4 column groups x 16 chunk strides (loads independent, unrolled), then the 16 folded in LDS
-__global__ __launch_bounds__(256) void colfold_f32(int64_t chunks, int64_t N, const float *__restrict__ part,
-                                                   float *__restrict__ scale) {
-  __shared__ f32x4 red[16][16];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int64_t c4 = (int64_t)blockIdx.x * 64 + tx * 4;
-  f32x4 m = {0.f, 0.f, 0.f, 0.f};
-  if (c4 < N) {
-#pragma unroll 8
-    for (int64_t c = ty; c < chunks; c += 16) {
-      const f32x4 v = *reinterpret_cast<const f32x4 *>(part + c * N + c4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], v[e]);
-    }
-  }
-  red[ty][tx] = m;
-  __syncthreads();
-  if (ty == 0 && c4 < N) {
-#pragma unroll
-    for (int k = 1; k < 16; ++k)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], red[k][tx][e]);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) scale[c4 + e] = f16x2_scale(m[e]);
   }
 }
 

@@ -74,6 +74,10 @@ HEADER_SYMBOLS = (
     "lpg_linear_small_bwd_workspace_bytes",
     "lpg_linear_small_bwd_f32",
     "lpg_heads_relu_bwd_f32",
+    "lpg_heads_scales_workspace_bytes",
+    "lpg_fc_smallk_scales_workspace_bytes",
+    "lpg_fc_smallk_scales_f32",
+    "lpg_heads_relu_bwd_scales_f32",
     "lpg_relu_wgrad_smallk_bf16",
     "lpg_linear_small_fwd_bf16",
     "lpg_linear_small_fwd_f16",
@@ -292,6 +296,16 @@ def lib() -> ctypes.CDLL:
     L.lpg_heads_relu_bwd_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, ctypes.c_float, c_p, c_i64,
                                          c_p, c_p, c_p, c_p, c_p]
     L.lpg_heads_relu_bwd_f32.restype = c_i32
+    L.lpg_fc_smallk_scales_workspace_bytes.argtypes = [c_i64, c_i64]
+    L.lpg_fc_smallk_scales_workspace_bytes.restype = c_i64
+    L.lpg_fc_smallk_scales_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64,
+                                           c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]
+    L.lpg_fc_smallk_scales_f32.restype = c_i32
+    L.lpg_heads_scales_workspace_bytes.argtypes = [c_i64, c_i64]
+    L.lpg_heads_scales_workspace_bytes.restype = c_i64
+    L.lpg_heads_relu_bwd_scales_f32.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, ctypes.c_float, c_p,
+                                                c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]
+    L.lpg_heads_relu_bwd_scales_f32.restype = c_i32
     L.lpg_relu_wgrad_smallk_bf16.argtypes = L.lpg_relu_wgrad_smallk_f32.argtypes
     L.lpg_relu_wgrad_smallk_bf16.restype = c_i32
     L.lpg_linear_small_fwd_bf16.argtypes = [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64, c_p]

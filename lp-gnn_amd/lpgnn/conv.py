@@ -403,8 +403,11 @@ class _TwoDirectionHeads(torch.autograd.Function):
         left_new, right_new = saved[4], saved[5]
         g_ll = torch.zeros(left_new.shape[0], wh_l.shape[0], device=left_new.device) if g_ll is None else g_ll
         g_lr = torch.zeros(right_new.shape[0], wh_r.shape[0], device=right_new.device) if g_lr is None else g_lr
-        dz_l, dwh_l, dbh_l, db_r2l = _fc.heads_relu_bwd(g_ll, wh_l, left_new, ctx.scale, ctx.has_b[1] and need[7])
-        dz_r, dwh_r, dbh_r, db_l2r = _fc.heads_relu_bwd(g_lr, wh_r, right_new, ctx.scale, ctx.has_b[0] and need[4])
+        ar = ctx.opts.arith  # dZ is only read below: its f16x2 scales come out of the same pass
+        dz_l, dwh_l, dbh_l, db_r2l = _fc.heads_relu_bwd(g_ll, wh_l, left_new, ctx.scale, ctx.has_b[1] and need[7],
+                                                        arith=ar)
+        dz_r, dwh_r, dbh_r, db_l2r = _fc.heads_relu_bwd(g_lr, wh_r, right_new, ctx.scale, ctx.has_b[0] and need[4],
+                                                        arith=ar)
         core = _backward_core(ctx, saved, need, None, None, dz=(dz_l, db_r2l, dz_r, db_l2r))
         keep = lambda t, i, has=True: t if (need[i] and has) else None
         return (*core, keep(dwh_l, 11), keep(dbh_l, 12, ctx.heads_b[0]), keep(dwh_r, 13),

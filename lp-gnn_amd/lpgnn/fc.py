@@ -136,6 +136,28 @@ def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, acc
             flags |= 4  # LPG_FC_HEADS_ONLY
         return _fc_x3(M, N, A1, W1, A2, W2, K2, bias, C, flags | _lib.fc_kernel(kernel), dropout_p, seed, relu,
                       heads=heads, row_offset=row_offset, row_keys=row_keys, f16=(arith or ARITH) == "f16x2")
+    if (small and (arith or ARITH) == "f16x2" and out is None and not accumulate and dropout_p == 0
+            and row_keys is None and 0 < N <= 1024 and M > 0):
+        # conv1 (narrow LP features) feeding f16x2 GEMMs: C's row / column scales from its own stores
+        # (lpg_fc_smallk_scales_f32), cached for it -- C is fresh, so nothing rewrites it behind autograd
+        rs = torch.empty(M, dtype=torch.float32, device=A1.device)
+        cs = torch.empty(N, dtype=torch.float32, device=A1.device)
+        sws = torch.empty(max(16, L.lpg_fc_smallk_scales_workspace_bytes(M, N)) // 4, dtype=torch.float32,
+                          device=A1.device)
+        with torch.cuda.device(A1.device):
+            tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
+            st = L.lpg_fc_smallk_scales_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(),
+                                            W1.stride(0), K2, None if A2 is None else A2.data_ptr(),
+                                            A2.stride(0) if K2 else 0, None if W2 is None else W2.data_ptr(),
+                                            W2.stride(0) if K2 else 0, None if bias is None else bias.data_ptr(),
+                                            C.data_ptr(), C.stride(0), 1 if relu else 0, rs.data_ptr(),
+                                            cs.data_ptr(), sws.data_ptr(), _lib.stream_of(A1))
+            TIMER.stop(tok)
+        if st != 3:  # (LPG_ERR_UNSUPPORTED: the plain entry below)
+            _lib.check(st, "lpg_fc_smallk_scales_f32")
+            _SCALES.put("row", C, rs)
+            _SCALES.put("col", C, cs)
+            return C
     with torch.cuda.device(A1.device):
         tok = TIMER.start(("fc", M, N, A1.shape[1] + K2, "relu" if relu else "lin"))
         st = L.lpg_fc_f32(M, N, A1.shape[1], A1.data_ptr(), A1.stride(0), W1.data_ptr(), W1.stride(0),
@@ -1000,9 +1022,11 @@ def linear_small_bwd(G: Tensor, W: Tensor, H: Tensor, need_dh: bool):
     return dH, dW, db
 
 
-def heads_relu_bwd(G: Tensor, W: Tensor, Y: Tensor, scale: float, want_dby: bool):
+def heads_relu_bwd(G: Tensor, W: Tensor, Y: Tensor, scale: float, want_dby: bool, arith: str | None = None):
     """(dZ, dW, db, dbY): the heads' backward through the producing layer's
-    ReLU/dropout in one pass over Y (lpg_heads_relu_bwd_f32)."""
+    ReLU/dropout in one pass over Y (lpg_heads_relu_bwd_f32).  ``arith`` "f16x2" (explicit, not the
+    process default: the caller vouches that dZ is only read afterwards): dZ feeds f16x2 GEMMs, so the same
+    pass also returns its row / column scales (lpg_heads_relu_bwd_scales_f32), cached for it."""
     M, K = Y.shape
     N = W.shape[0]
     G, W = G.contiguous(), W.contiguous()
@@ -1014,13 +1038,27 @@ def heads_relu_bwd(G: Tensor, W: Tensor, Y: Tensor, scale: float, want_dby: bool
     dW = torch.empty_like(W)
     db = torch.empty(N, dtype=torch.float32, device=Y.device)
     dbY = torch.empty(K, dtype=torch.float32, device=Y.device) if want_dby else None
+    sc = arith == "f16x2" and K % 4 == 0 and M > 0  # (opt-in: the caller knows dZ is not rewritten later)
     with torch.cuda.device(Y.device):
         tok = TIMER.start(("heads_relu_bwd", M, N, K, "f32"))
-        st = L.lpg_heads_relu_bwd_f32(M, K, N, G.data_ptr(), G.stride(0), W.data_ptr(), Y.data_ptr(), Y.stride(0),
-                                      float(scale), dZ.data_ptr(), K, dW.data_ptr(), db.data_ptr(),
-                                      None if dbY is None else dbY.data_ptr(), ws.data_ptr(), _lib.stream_of(Y))
+        if sc:
+            rs = torch.empty(M, dtype=torch.float32, device=Y.device)
+            cs = torch.empty(K, dtype=torch.float32, device=Y.device)
+            sws = torch.empty(max(16, L.lpg_heads_scales_workspace_bytes(M, K)) // 4, dtype=torch.float32,
+                              device=Y.device)
+            st = L.lpg_heads_relu_bwd_scales_f32(M, K, N, G.data_ptr(), G.stride(0), W.data_ptr(), Y.data_ptr(),
+                                                 Y.stride(0), float(scale), dZ.data_ptr(), K, dW.data_ptr(),
+                                                 db.data_ptr(), None if dbY is None else dbY.data_ptr(), rs.data_ptr(),
+                                                 cs.data_ptr(), sws.data_ptr(), ws.data_ptr(), _lib.stream_of(Y))
+        else:
+            st = L.lpg_heads_relu_bwd_f32(M, K, N, G.data_ptr(), G.stride(0), W.data_ptr(), Y.data_ptr(),
+                                          Y.stride(0), float(scale), dZ.data_ptr(), K, dW.data_ptr(), db.data_ptr(),
+                                          None if dbY is None else dbY.data_ptr(), ws.data_ptr(), _lib.stream_of(Y))
         TIMER.stop(tok)
-    _lib.check(st, "lpg_heads_relu_bwd_f32")
+    _lib.check(st, "lpg_heads_relu_bwd_scales_f32" if sc else "lpg_heads_relu_bwd_f32")
+    if sc:
+        _SCALES.put("row", dZ, rs)
+        _SCALES.put("col", dZ, cs)
     return dZ, dW, db, dbY
 
 

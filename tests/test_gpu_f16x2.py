@@ -215,3 +215,42 @@ def test_wgrad_f16x2_against_fp64(R, N, K):
     # every output row (a column of G) relative to itself
     rel = ((dW.double() - ref).norm(dim=1) / ref.norm(dim=1)).max()
     assert float(rel) <= 1e-6
+
+
+@pytest.mark.parametrize("M,N,relu,bias", [(100_000, 1024, True, True), (777, 256, True, False), (5, 1000, False, True),
+                                           (3001, 1024, False, False)])
+def test_smallk_scales_from_the_stores(M, N, relu, bias):
+    """conv1's narrow FC with arith f16x2 (lpg_fc_smallk_scales_f32): C bitwise the plain small-K kernel's,
+    and the row / column scales it caches for C exactly the sweep's."""
+    torch.manual_seed(M + N)
+    A1 = torch.randn(M, 8, device=DEV) * torch.exp(2 * torch.randn(M, 1, device=DEV))
+    A2 = torch.randn(M, 8, device=DEV)
+    W1 = torch.randn(N, 8, device=DEV)
+    W2 = torch.randn(N, 8, device=DEV)
+    b = torch.randn(N, device=DEV) if bias else None
+    C = F.fc_forward(A1, W1, A2, W2, b, relu, arith="f16x2")
+    C0 = F.fc_forward(A1, W1, A2, W2, b, relu, arith="fp32")
+    assert torch.equal(C, C0)
+    rs, cs = F._SCALES.lookup("row", C), F._SCALES.lookup("col", C)
+    assert rs is not None and cs is not None
+    assert torch.equal(rs, F._rowscale1(C))
+    assert torch.equal(cs, F._colscale1(C))
+
+
+@pytest.mark.parametrize("M,K", [(100_000, 1024), (5000, 2048), (130, 64), (1, 1024)])
+def test_heads_scales_from_the_stores(M, K):
+    """The heads' backward with arith f16x2 (lpg_heads_relu_bwd_scales_f32): dZ, dW, db, dbY bitwise the
+    plain entry's, and dZ's cached row / column scales exactly the sweep's."""
+    torch.manual_seed(M + K)
+    Y = torch.relu(torch.randn(M, K, device=DEV))
+    G = torch.randn(M, 3, device=DEV) * torch.exp(3 * torch.randn(M, 1, device=DEV))
+    W = torch.randn(3, K, device=DEV)
+    r16 = F.heads_relu_bwd(G, W, Y, 1.25, True, arith="f16x2")
+    r0 = F.heads_relu_bwd(G, W, Y, 1.25, True)
+    for a, b in zip(r16, r0):
+        assert torch.equal(a, b)
+    dZ = r16[0]
+    rs, cs = F._SCALES.lookup("row", dZ), F._SCALES.lookup("col", dZ)
+    assert rs is not None and cs is not None
+    assert torch.equal(rs, F._rowscale1(dZ))
+    assert torch.equal(cs, F._colscale1(dZ))
