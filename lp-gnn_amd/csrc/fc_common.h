@@ -139,25 +139,34 @@ __device__ __forceinline__ float f16x2_scale(float mx) {
 }
 
 // Eight rows' values x[0..7] (one per row, this lane's part) -> their maxima over the wave's 64 lanes in
-// a halving butterfly: each exchange halves what a lane carries (4 + 2 + 1 + 1 + 1 + 1 shuffles, not 48);
-// lane l ends with row ((l >> 5) & 1) * 4 + ((l >> 4) & 1) * 2 + ((l >> 3) & 1)'s maximum.
+// a halving butterfly: each exchange halves what a lane carries (4 + 2 + 1 exchanges, then a 3-step
+// all-reduce inside eight lanes); lane l ends with row ((l >> 5) & 1) * 4 + ((l >> 4) & 1) * 2 +
+// ((l >> 3) & 1)'s maximum.  No LDS traffic: the 32- and 16-lane exchanges are gfx950's
+// v_permlane32_swap / v_permlane16_swap (a swap of rows 0-3 of the upper half with rows 4-7 of the lower
+// half leaves every lane its own value and its partner's in the two results: one swap + one max per
+// pair), the 8-lane one a DPP row rotation, the rest DPP (half-mirror, quad permutations).  (As
+// __shfl_xor these were ten ds_bpermute per eight rows.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float rowmax8(const float (&x)[8], int lane) {
-  const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0, b3 = (lane & 8) != 0;
   float y[4], z[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {  // lanes 0-31 keep rows 0-3, lanes 32-63 rows 4-7
-    const float send = b5 ? x[i] : x[i + 4], keep = b5 ? x[i + 4] : x[i];
-    y[i] = fmaxf(keep, __shfl_xor(send, 32));
+  for (int i = 0; i < 4; ++i) {  // lanes 0-31 end with rows 0-3, lanes 32-63 with rows 4-7
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[i]), __float_as_uint(x[i + 4]), false, false);
+    y[i] = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const float send = b4 ? y[i] : y[i + 2], keep = b4 ? y[i + 2] : y[i];
-    z[i] = fmaxf(keep, __shfl_xor(send, 16));
+  for (int i = 0; i < 2; ++i) {  // odd 16-lane rows end with the odd pair
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(y[i]), __float_as_uint(y[i + 2]), false, false);
+    z[i] = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
   }
-  float w = fmaxf(b3 ? z[1] : z[0], __shfl_xor(b3 ? z[0] : z[1], 8));
-  w = fmaxf(w, __shfl_xor(w, 4));
-  w = fmaxf(w, __shfl_xor(w, 2));
-  return fmaxf(w, __shfl_xor(w, 1));
+  const bool b3 = (lane & 8) != 0;  // lanes 8-15 of each 16 keep z[1], and take the other half's z[1]
+  float w = fmaxf(b3 ? z[1] : z[0], dpp_f32<0x128>(b3 ? z[0] : z[1]));  // row_ror:8 = lane ^ 8 in a row
+  w = fmaxf(w, dpp_f32<0x141>(w));                                      // row_half_mirror: i <-> 7 - i
+  w = fmaxf(w, dpp_f32<0xB1>(w));                                       // quad_perm [1,0,3,2]
+  return fmaxf(w, dpp_f32<0x4E>(w));                                    // quad_perm [2,3,0,1]
 }
 __device__ __forceinline__ int rowmax8_slot(int lane) {
   return ((lane & 32) ? 4 : 0) + ((lane & 16) ? 2 : 0) + ((lane & 8) ? 1 : 0);
