@@ -192,25 +192,34 @@ def split3(W: Tensor, transpose: bool = False) -> Tensor:
 
 
 class _ScaleCache:
-    """The f16x2 row / column scales of live operands, by object identity and autograd version (an entry
-    holds only a weak reference): an operand several GEMMs of one step use -- a layer input in the forward
-    lin and the constraint-side FC, dZ or a layer input in two weight gradients -- is swept once.  A freed
-    tensor's entry is dropped, and an in-place change bumps the version, so an entry never outlives the
-    values it describes."""
+    """The f16x2 row / column scales of live operands, by storage region and autograd version: the key
+    is the tensor's base (a view's ``_base``, held only by a weak reference) with the view's offset,
+    shape and strides, so an operand several GEMMs of one step use -- a layer input in the forward lin
+    and the constraint-side FC, dZ or a layer input in two weight gradients, a partition's owned rows
+    sliced afresh at each use -- is swept once.  A freed base drops its entries, and an in-place change
+    bumps the version (shared by a base and its views), so an entry never outlives the values it
+    describes."""
 
     def __init__(self):
         self._d = {}
 
+    @staticmethod
+    def _key(kind: str, t: Tensor):
+        base = t._base if t._base is not None else t
+        return base, (kind, id(base), t.storage_offset(), tuple(t.shape), tuple(t.stride()))
+
     def lookup(self, kind: str, t: Tensor):
-        e = self._d.get((kind, id(t)))
-        if e is not None and e[0]() is t and e[1] == t._version and e[2] == (t.data_ptr(), tuple(t.shape)):
+        base, key = self._key(kind, t)
+        e = self._d.get(key)
+        if e is not None and e[0]() is base and e[1] == t._version and e[2] == base.data_ptr():
             return e[3]
         return None
 
     def put(self, kind: str, t: Tensor, v):
         if len(self._d) > 64:
             self._d = {k: x for k, x in self._d.items() if x[0]() is not None}
-        self._d[(kind, id(t))] = (weakref.ref(t), t._version, (t.data_ptr(), tuple(t.shape)), v)
+        base, key = self._key(kind, t)
+        self._d[key] = (weakref.ref(base), t._version, base.data_ptr(), v)
 
     def get(self, kind: str, t: Tensor, make):
         v = self.lookup(kind, t)

@@ -963,10 +963,14 @@ class _PartTwoDirectionHeads(torch.autograd.Function):
         g_ll = torch.zeros(left_new.shape[0], wh_l.shape[0], device=left_new.device) if g_ll is None else g_ll
         g_lr = torch.zeros(right_new.shape[0], wh_r.shape[0], device=right_new.device) if g_lr is None else g_lr
         red = ex.start_reduce(g_lr.contiguous(), inplace=False)  # halo logit grads -> owners, in flight ...
-        dz_l, dwh_l, dbh_l, db_r2l = _fc.heads_relu_bwd(g_ll, wh_l, left_new, ctx.scale, ctx.has_b[1] and need[7])
+        # dZ is only read below (copied into a [owned | halo] buffer where halo rows exist): its f16x2 scales
+        # come out of the same pass (heads_relu_bwd with the model's arithmetic)
+        ar = ctx.opts.arith
+        dz_l, dwh_l, dbh_l, db_r2l = _fc.heads_relu_bwd(g_ll, wh_l, left_new, ctx.scale, ctx.has_b[1] and need[7],
+                                                        arith=ar)
         g_own = red.finish()
         dz_r, dwh_r, dbh_r, db_l2r = _fc.heads_relu_bwd(g_own, wh_r, right_new[:ex.n_own], ctx.scale,
-                                                        ctx.has_b[0] and need[4])
+                                                        ctx.has_b[0] and need[4], arith=ar)
         core = _part_backward_core(ctx, saved, need, None, None, dz=(dz_l, db_r2l, dz_r, db_l2r))
         keep = lambda t, i, has=True: t if (need[i] and has) else None
         return (*core, keep(dwh_l, 11), keep(dbh_l, 12, ctx.heads_b[0]), keep(dwh_r, 13),
