@@ -124,6 +124,7 @@ def _fc_forward(A1, W1, A2, W2, bias, relu, dropout_p=0.0, seed=0, out=None, acc
         if out.shape != (M, N) or out.dtype != torch.float32 or out.stride(1) != 1 or out.device != A1.device:
             raise RuntimeError("lpgnn FC: `out` must be a float32 [M, N] row-major view on the same device")
         C = out
+        _SCALES.forget(out)  # (rewritten through its pointer below: no version bump)
     elif accumulate:
         raise RuntimeError("lpgnn FC: accumulate needs the addend in `out`")
     else:
@@ -227,6 +228,13 @@ class _ScaleCache:
             v = make(t)
             self.put(kind, t, v)
         return v
+
+    def forget(self, t: Tensor) -> None:
+        """Drop every entry on t's base: its storage was written by a path the autograd version does not
+        see (our kernels writing a caller's ``out`` through its pointer, a quiet halo broadcast)."""
+        base = t._base if t._base is not None else t
+        b = id(base)
+        self._d = {k: x for k, x in self._d.items() if k[1] != b}
 
 
 _SCALES = _ScaleCache()
@@ -455,6 +463,8 @@ def input_grad(G1: Tensor, W1: Tensor, G2: Tensor | None = None, W2: Tensor | No
         if accumulate:
             raise RuntimeError("lpgnn input_grad: accumulate needs the addend in `out`")
         out = torch.empty((M, N), dtype=torch.float32, device=G1.device)
+    else:
+        _SCALES.forget(out)  # (rewritten through its pointer: no version bump)
     K2 = 0 if G2 is None else G2.shape[1]
     return _fc_x3(M, N, G1, W1, G2, W2, K2, None, out, 2 if accumulate else 0, 0.0, 0, False,
                   f16=(arith or ARITH) == "f16x2", transpose=True)

@@ -466,6 +466,9 @@ class Exchange:
         def then(recv):
             if self.send_idx.numel():
                 dst.index_copy_(0, self.send_idx, recv)
+                if quiet:  # (no version bump: drop the f16x2 scales cached on full's storage)
+                    from .fc import _SCALES
+                    _SCALES.forget(full)
             return full
         if not self.active:
             return _Pending(None, then=lambda _: full)

@@ -52,3 +52,15 @@ def test_get_computes_once():
     mk = lambda x: calls.append(1) or "v"  # noqa: E731
     assert c.get("col", t, mk) == "v" and c.get("col", t, mk) == "v"
     assert len(calls) == 1
+
+
+def test_forget_drops_every_view_of_the_base():
+    c = _ScaleCache()
+    base = torch.randn(10, 8)
+    other = torch.randn(10, 8)
+    c.put("row", base[:6], "a")
+    c.put("col", base, "b")
+    c.put("row", other, "c")
+    c.forget(base[6:])                                # any view names the whole base
+    assert c.lookup("row", base[:6]) is None and c.lookup("col", base) is None
+    assert c.lookup("row", other) == "c"
