@@ -10,6 +10,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "lp-gnn_a
 from lpgnn import fc as F  # noqa: E402
 
 DEV = "cuda:0"
+KERNELS = [int(k) for k in os.environ.get("F16_FC_KERNELS", "").split(",") if k]  # LPG_FC_KERNEL choices (tile order)
 
 
 def timed(fn, reps=20):
@@ -33,6 +34,10 @@ def main():
         W1 = torch.randn(1024, K1, device=DEV) * 0.03
         W2 = torch.randn(1024, K2, device=DEV) * 0.03 if K2 else None
         C = torch.empty(M, 1024, device=DEV)
+        for kern in KERNELS:
+            run = lambda: F.fc_forward(A1, W1, A2, W2, None, False, out=C, arith="f16x2", kernel=kern)  # noqa: E731
+            t = timed(run)
+            print(f"M={M} K={K1 + K2} kernel {kern}: {t:8.1f} us", flush=True)
         run = lambda: F.fc_forward(A1, W1, A2, W2, None, False, out=C, arith="f16x2")  # noqa: E731
         t = timed(run)
         run()
