@@ -30,7 +30,10 @@ constexpr int kRowsColsum = 64;
 #ifndef LPG_HEADS_U_BF16
 #define LPG_HEADS_U_BF16 8
 #endif
-constexpr int kRowsLinear = 128;  // heads_bwd_p1 rows per block (two 64-row column-sum chunks)
+#ifndef LPG_HEADS_RB
+#define LPG_HEADS_RB 128
+#endif
+constexpr int kRowsLinear = LPG_HEADS_RB;  // heads_bwd_p1 rows per block (64-row column-sum chunks)
 constexpr int kMaxSmallK = 16;
 constexpr int kSmallNMax = 4;
 constexpr int64_t kFold = 64;
