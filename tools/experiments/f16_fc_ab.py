@@ -31,6 +31,10 @@ def main():
     for M, K1, K2 in [(100_000, 1024, 0), (200_000, 1024, 0), (100_000, 1024, 1024)]:
         A1 = torch.randn(M, K1, device=DEV)
         A2 = torch.randn(M, K2, device=DEV) if K2 else None
+        if os.environ.get("F16_FC_ZEROS"):  # power probe: zero activations (the same instructions, no toggling)
+            A1.zero_()
+            if A2 is not None:
+                A2.zero_()
         W1 = torch.randn(1024, K1, device=DEV) * 0.03
         W2 = torch.randn(1024, K2, device=DEV) * 0.03 if K2 else None
         C = torch.empty(M, 1024, device=DEV)
