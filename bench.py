@@ -141,9 +141,30 @@ def load_pmc_traffic(key: str):
     return None, None
 
 
+def load_pmc_dir_traffic(key: str):
+    """Per-direction HBM bytes per launch of the F=hid SpMM ({"cons<-vars": B, "vars<-cons": B}) from the
+    committed per-direction PMC summary (profiles/*pmc_dirs*.json, tools/pmc_spmm_dirs.py), or None."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_dirs*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("workload") == key and d.get("directions"):
+            return d["directions"]
+    return None
+
+
 def rank_share_key(family: str, world: int, rank: int = 0) -> str:
     """The PMC key of one rank's share of a partitioned workload (tools/pmc_rank_share.py)."""
     return f"{family} rank share: rank {rank} of {world}, F=1024 SpMM both directions"
+
+
+def _arith() -> str:
+    from lpgnn.options import DEFAULT
+
+    return DEFAULT.arith
 
 
 def _threads():
@@ -267,8 +288,12 @@ def cpu_spmm(g, F, reps=3):
             t0 = time.perf_counter()
             O.spmm_f32(rp, col, val, x)
             ts.append(time.perf_counter() - t0)
-        sp = torch.sparse_csr_tensor(torch.from_numpy(rp), torch.from_numpy(col.astype(np.int64)),
-                                     torch.from_numpy(val), size=(len(rp) - 1, x.shape[0]))
+        import warnings
+
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")  # torch's "sparse CSR support is in beta" notice (keeps stderr short)
+            sp = torch.sparse_csr_tensor(torch.from_numpy(rp), torch.from_numpy(col.astype(np.int64)),
+                                         torch.from_numpy(val), size=(len(rp) - 1, x.shape[0]))
         xt = torch.from_numpy(x)
         tm = []
         for _ in range(reps):
@@ -384,7 +409,7 @@ def timed(ctx, step, steps, warmup):
 
 
 def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_key, single_dirs=None, fp16=False,
-           training=True):
+           training=True, touched=None):
     """value, ms_per_step, the SpMM roofline and the hidden-width GEMM roofline of one timed run,
     aggregated over the ranks (collective: every rank calls it).
 
@@ -451,7 +476,7 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
           "kernel": ("lpg fc_f16 (hidden-width FC forward on v_mfma_f32_16x16x32_f16)" if fp16 else
                      "lpg fc_bf16 + wgrad_bf16 (hidden-width GEMMs, fwd + bwd: FC forward, input "
                      "gradients on the FC kernel, weight gradients)" if half else
-                     "lpg fc_x3_wide f16x2 + wgrad_x3 (hidden-width GEMMs, fwd + bwd; fp32 via two "
+                     "lpg fc_x3_wide f16x2 + wgrad_x3w f16x2 (hidden-width GEMMs, fwd + bwd; fp32 via two "
                      "row-scaled fp16 terms (3 products) and the exact 3-way bf16 split (6); peak = dense "
                      "bf16 over the launches' products)" if f16x2 and not half else
                      "lpg fc_fwd_x3 + wgrad_x3 (hidden-width GEMMs, fwd + bwd; fp32 via exact "
@@ -461,14 +486,27 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
           # the bf16 MFMA work these launches issue (x3: 6 bf16 products per fp32 product),
           # comparable with a plain bf16 GEMM's rate on this chip
           "bf16_mfma_equiv_tflops": work_tf if not half else fc_tf_all}
-    dirs = {}
+    dirs, narrow = {}, {}
+    dir_traffic = load_pmc_dir_traffic(traffic_key)
     for k, v in per_launch.items():
-        if k[0] != "spmm" or k[3] != hids:
+        if k[0] != "spmm":
             continue
         name = (single_dirs or {}).get((k[1], k[2]), f"{k[1]}x{k[2]}")
         med = float(np.median(v))
-        dirs[name] = {"median_ms": med, "launches": len(v), "edges_per_s": local_nnz / (med / 1e3),
-                      "roofline_frac": spmm_bytes(k[1], local_nnz, k[3], esz) / (med / 1e3) / 1e9 / HBM_PEAK_GBS}
+        if k[3] <= 64:  # conv1's input (F = 8): the narrow kernel, latency-bound, its time per launch
+            narrow[name] = med
+            continue
+        if k[3] != hids:
+            continue
+        d = {"median_ms": med, "launches": len(v), "edges_per_s": local_nnz / (med / 1e3),
+             "roofline_frac": spmm_bytes(k[1], local_nnz, k[3], esz) / (med / 1e3) / 1e9 / HBM_PEAK_GBS}
+        if touched and (k[1], k[2]) in touched:  # SURVEY 8d compulsory model: each touched source row once
+            d["compulsory_frac"] = (spmm_bytes(k[1], local_nnz, k[3], esz) - (local_nnz - touched[(k[1], k[2])])
+                                    * k[3] * esz) / (med / 1e3) / 1e9 / HBM_PEAK_GBS
+        if dir_traffic and name in dir_traffic:  # counter bytes (PMC) over the measured launch time
+            d["traffic_bytes"] = dir_traffic[name]
+            d["traffic_frac"] = dir_traffic[name] / (med / 1e3) / 1e9 / HBM_PEAK_GBS
+        dirs[name] = d
     out = {"value": value, "ms_per_step": dt_max / max(1, steps) * 1e3, "roofline": roof, "fc_roofline": fc}
     if any(r["ex_n"] for r in every):
         st = max(1, steps)
@@ -481,6 +519,8 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
                           "hidden_frac": (1.0 - r["ex_exposed"] / r["ex_span"]) if r["ex_span"] > 0 else None}
                          for r in every],
             "max_exposed_ms_per_step": max(r["ex_exposed"] for r in every) / st}
+    if narrow:
+        out["narrow_ms"] = narrow
     out.update({"spmm_directions": dirs,
             "spmm_edges_per_s_kernel": launches * local_nnz / (spmm_ms / 1e3) if spmm_ms > 0 else None,
             "spmm_ms_per_step": spmm_ms / max(1, steps),
@@ -488,6 +528,98 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
                         for k, v in sorted(kern.items(), key=lambda kv: tuple(map(str, kv[0])))
                         if k[0] != "exchange"}})
     return out
+
+
+# --------------------------------------------------------------------- output
+HEADLINE_MAX_BYTES = 6144  # the driver keeps the last ~8 KB of stdout+stderr; the line must fit whole
+SUB_NAMES = ("c4", "inference", "inference_fp16", "c5", "skewed")
+BULKY = ("kernels", "cpu_spmm", "vendor_spmm", "exchange", "library") + SUB_NAMES
+
+
+def _r(x, nd=4):
+    return None if x is None else float(f"{x:.{nd}g}")
+
+
+def _compact_roof(roof):
+    keep = ("bound", "achieved", "peak", "unit", "frac", "traffic", "bytes_per_launch", "avg_launch_ms", "launches",
+            "kernel", "traffic_source")
+    out = {k: (_r(roof[k], 6) if isinstance(roof[k], float) else roof[k]) for k in keep if k in roof}
+    if roof.get("traffic") and roof.get("avg_launch_ms"):  # PMC bytes over the measured launch time
+        out["traffic_frac"] = _r(roof["traffic"] / (roof["avg_launch_ms"] / 1e3) / 1e9 / roof["peak"])
+    if "per_rank" in roof:
+        out["per_rank_frac"] = [_r(r["frac"]) for r in roof["per_rank"]]
+    return out
+
+
+def sub_summary(name, rec):
+    """One sub-record's figures for the headline: step time, value and both rooflines (the full record with
+    its kernel table goes to the detail file)."""
+    s = {"value": _r(rec.get("value"), 6), "ms_per_step": _r(rec.get("ms_per_step"), 5),
+         "spmm_frac": _r(rec.get("roofline", {}).get("frac")), "fc_frac": _r(rec.get("fc_roofline", {}).get("frac"))}
+    if rec.get("roofline", {}).get("traffic_frac") is not None:
+        s["spmm_traffic_frac"] = rec["roofline"]["traffic_frac"]
+    cb = rec.get("cpu_baseline")
+    if cb:
+        s["cpu_s"] = _r(cb.get("s_per_step", cb.get("s_per_graph")))
+    if name == "skewed":  # SURVEY 8d: the edge-gather, compulsory and counter-bytes fractions per direction
+        s["dirs"] = {d: {k: _r(v.get(k)) for k in ("median_ms", "roofline_frac", "compulsory_frac", "traffic_frac",
+                                                      "bound") if v.get(k) is not None}
+                     for d, v in rec.get("spmm_directions", {}).items()}
+        s["narrow_F8_ms"] = {d: _r(v) for d, v in rec.get("narrow_ms", {}).items()}
+    if "exchange_overlap" in rec:
+        s["max_exposed_ms"] = _r(rec["exchange_overlap"]["max_exposed_ms_per_step"])
+    return s
+
+
+def compact_headline(out, detail_path=None):
+    """The one JSON line the driver parses: the contract's keys, both rooflines, the CPU baseline, the rank
+    devices and one short summary per sub-record -- never the per-kernel tables (those stay in the detail
+    file).  Asserted below HEADLINE_MAX_BYTES by tests/test_bench_report.py."""
+    head = {k: v for k, v in out.items() if k not in BULKY}
+    head["roofline"] = _compact_roof(out["roofline"])
+    fc = out.get("fc_roofline")
+    if fc:
+        head["fc_roofline"] = {k: (_r(fc[k], 6) if isinstance(fc[k], float) else fc[k])
+                               for k in ("bound", "achieved", "peak", "unit", "frac", "launches",
+                                         "bf16_mfma_equiv_tflops") if k in fc}
+        head["fc_roofline"]["kernel"] = fc.get("kernel", "")[:90]
+    if "spmm_directions" in out:
+        head["spmm_directions"] = {d: {"median_ms": _r(v["median_ms"]), "frac": _r(v["roofline_frac"])}
+                                   for d, v in out["spmm_directions"].items()}
+    d = out.get("dist", {})
+    head["dist"] = {"backend": d.get("backend"), "world_size": d.get("world_size"),
+                    "pci": [r.get("pci") for r in d.get("ranks", [])], "launcher": d.get("launcher")}
+    if "exchange_overlap" in out:
+        head["exchange_overlap"] = {"max_exposed_ms_per_step": _r(out["exchange_overlap"]["max_exposed_ms_per_step"]),
+                                    "hidden_frac": [_r(r["hidden_frac"]) for r in
+                                                    out["exchange_overlap"]["per_rank"]]}
+    subs = {n: sub_summary(n, out[n]) for n in SUB_NAMES if n in out}
+    if subs:
+        head["subs"] = subs
+    if detail_path:
+        head["detail"] = detail_path
+    for k in ("value", "ms_per_step", "ms_per_graph", "max_hbm_allocated_gb"):
+        if isinstance(head.get(k), float):
+            head[k] = _r(head[k], 7)
+    return head
+
+
+def emit(out, args):
+    """Write the full record (every sub-record with its kernel table) to the detail file, then print the
+    compact headline as the LAST line of stdout."""
+    path = os.environ.get("LPGNN_BENCH_DETAIL", os.path.join("gpurun_out", "bench_detail.json"))
+    try:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    except OSError as e:  # a read-only tree: the headline still prints
+        print(f"bench: detail file {path} not written ({e})", file=sys.stderr)
+        path = None
+    line = json.dumps(compact_headline(out, path))
+    if len(line) > HEADLINE_MAX_BYTES:
+        print(f"bench: headline {len(line)} bytes > {HEADLINE_MAX_BYTES}", file=sys.stderr)
+    sys.stderr.flush()
+    print(line, flush=True)
 
 
 # ------------------------------------------------------------------------ jobs
@@ -562,15 +694,17 @@ def run_config(ctx, a, steps, warmup, family):
         step, g, local_nnz = one_gpu_job(a, ctx.dev)
         workload = workload_name(a)
         dirs = {(a.m, a.n): "cons<-vars", (a.n, a.m): "vars<-cons"}
+        touched = {(g.m, g.n): int(np.count_nonzero(np.bincount(g.col, minlength=g.n))),
+                   (g.n, g.m): int(np.count_nonzero(np.bincount(g.row, minlength=g.m)))}
         key = workload
     else:
         job = partition.build_bench_job(a, ctx.rank, ctx.world, ctx.dev)
         step, g, local_nnz, workload = job.step, None, job.local_nnz, job.workload
-        dirs = None
+        dirs, touched = None, None
         key = rank_share_key(family, ctx.world) if ctx.world > 1 else workload
     dt, kern, per_launch = timed(ctx, step, steps, warmup)
     rec = report(ctx, dt, kern, per_launch, steps=steps, hids=a.hids, local_nnz=local_nnz,
-                 esz=2 if a.bf16 else 4, traffic_key=key, single_dirs=dirs)
+                 esz=2 if a.bf16 else 4, traffic_key=key, single_dirs=dirs, touched=touched)
     rec["workload"] = workload
     rec["config"] = {"workload": workload, "n_cons": a.m * (ctx.world if part and a.config != "c4" else 1),
                      "n_vars": a.n * (ctx.world if part and a.config != "c4" else 1),
@@ -697,6 +831,9 @@ def main():
         "scaling": "strong" if args.config == "c4" else "weak",
         "vs_baseline": None,
         "dtype": "bf16" if args.bf16 else ("fp16" if args.fp16 else "fp32"),
+        # the matrix-core arithmetic of the fp32 GEMMs: f16x2 = two row/column-scaled fp16 terms per operand,
+        # three products (22-bit scaled operands, fp32-class by a tested error bound)
+        "arith": "bf16" if args.bf16 else ("fp16" if args.fp16 else _arith()),
         "data": "synthetic (seeded uniform / block LP graphs, LP feature layout; random-init GCN_FC weights)",
         "config": cfg,
         "dist": {"backend": ctx.backend, "world_size": world, "ranks": ranks,
@@ -788,7 +925,7 @@ def main():
                        "fwd+bwd+Adam; spmm_directions = per-direction roofline (cons<-vars carries the heavy rows)")
         out["skewed"] = rec
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out, args)
     if distributed:
         torch.distributed.destroy_process_group()
 

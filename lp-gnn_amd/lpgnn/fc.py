@@ -210,6 +210,8 @@ class _ScaleCache:
         return base, (kind, id(base), t.storage_offset(), tuple(t.shape), tuple(t.stride()))
 
     def lookup(self, kind: str, t: Tensor):
+        if t.is_inference():  # an inference-mode tensor has no version counter: never cached
+            return None
         base, key = self._key(kind, t)
         e = self._d.get(key)
         if e is not None and e[0]() is base and e[1] == t._version and e[2] == base.data_ptr():
@@ -217,6 +219,8 @@ class _ScaleCache:
         return None
 
     def put(self, kind: str, t: Tensor, v):
+        if t.is_inference():  # no version counter to key on (torch.inference_mode): computed per use
+            return
         if len(self._d) > 64:
             self._d = {k: x for k, x in self._d.items() if x[0]() is not None}
         base, key = self._key(kind, t)

@@ -5,9 +5,9 @@ measurements and for the bitwise contract of the exact-fp32 FC.  A model carries
 ``PathOptions`` (``GCN_FC(..., options=...)``); the defaults come from the environment once, at
 import, so a whole run can be switched from the shell:
 
-  LPGNN_FC_ARITH=x3          the FC and input-gradient GEMMs on the exact three-way bf16 split (six
-                             products) instead of the default f16x2 (two row-scaled fp16 terms per
-                             operand, three products; the weight gradients are x3 in both)
+  LPGNN_FC_ARITH=x3          every fp32 GEMM (FC, input and weight gradients) on the exact three-way
+                             bf16 split (six products) instead of the default f16x2 (two row- or
+                             column-scaled fp16 terms per operand, three products)
   LPGNN_FC_ARITH=fp32        the exact-fp32 MFMA FC (bitwise oracle/fc_ref.c) + hipBLASLt backward
   LPGNN_REASSOC=0            lin_rel(S x) never re-associated as S (x W_rel^T)
   LPGNN_FUSE_HEADS=0         the heads as their own autograd node

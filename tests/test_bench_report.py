@@ -72,3 +72,89 @@ def test_report_aggregates_over_ranks(tmp_path):
 
 if __name__ == "__main__":
     sys.exit(pytest.main([__file__, "-q"]))
+
+
+# ---------------------------------------------------------------- the driver-parsed headline line
+def _full_record(world=1):
+    """A full bench record as main() builds it: round 5's final default line (every sub-record with its
+    kernel table, 20.9 KB), widened to `world` ranks for the N > 1 shape."""
+    import copy
+    import json
+
+    path = os.path.join(ROOT, "profiles", "r05_bench_default_final.log")
+    line = [ln for ln in open(path).read().splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    out["arith"] = "f16x2"
+    if world > 1:
+        out = copy.deepcopy(out)
+        out["n_gpus"] = world
+        r0 = out["dist"]["ranks"][0]
+        out["dist"]["ranks"] = [dict(r0, rank=r, local_rank=r, device=f"cuda:{r}", pci="0000:%02x:00" % (0x10 + r))
+                                for r in range(world)]
+        out["roofline"]["per_rank"] = [{"frac": 0.95, "avg_launch_ms": 1.1, "launches": 80, "bytes_per_launch": 8.8e9}
+                                       for _ in range(world)]
+        out["exchange_overlap"] = {"what": "x" * 200, "max_exposed_ms_per_step": 0.31,
+                                   "per_rank": [{"exchanges_per_step": 12, "span_ms_per_step": 3.0,
+                                                 "exposed_ms_per_step": 0.3, "hidden_frac": 0.9}] * world}
+        out["exchange"] = {"per_rank": [{"k": "v" * 300}] * world}
+        for s in ("inference", "inference_fp16", "c5", "skewed"):
+            out.pop(s, None)
+    return out
+
+
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "arith", "data", "config", "dist", "roofline", "fc_roofline")
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_headline_is_compact_and_parses(world):
+    """The line the driver parses: under 8 KB whole (the driver keeps the last ~8 KB of stdout+stderr and
+    returned parsed:null for round 5's 20.9 KB line), valid JSON, the contract's keys, the roofline with
+    its PMC traffic, the CPU baseline at N=1, one summary per sub-record, and no kernel tables."""
+    import json
+
+    import bench
+
+    out = _full_record(world)
+    assert len(json.dumps(out)) > 8192 or world > 1  # the full record alone would not fit
+    line = json.dumps(bench.compact_headline(out, "gpurun_out/bench_detail.json"))
+    assert len(line.encode()) < bench.HEADLINE_MAX_BYTES <= 8192, len(line)
+    head = json.loads(line)
+    for k in REQUIRED:
+        assert k in head, k
+    assert head["value"] == pytest.approx(out["value"], rel=1e-6)
+    assert head["ms_per_step"] == pytest.approx(out["ms_per_step"], rel=1e-6)
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in head["roofline"], k
+    assert head["roofline"]["frac"] == pytest.approx(out["roofline"]["frac"], rel=1e-5)
+    assert "kernels" not in head and "kernels" not in json.dumps(head["subs"] if "subs" in head else {})
+    assert len(head["dist"]["pci"]) == world
+    if world == 1:
+        cb = head["cpu_baseline"]
+        for k in ("value", "unit", "cores", "kind", "sample"):
+            assert k in cb, k
+        assert set(head["subs"]) == {"c4", "inference", "inference_fp16", "c5", "skewed"}
+        assert head["subs"]["c5"]["ms_per_step"] == pytest.approx(out["c5"]["ms_per_step"], rel=1e-4)
+        assert "cpu_s" in head["subs"]["c5"]
+    else:
+        assert head["exchange_overlap"]["max_exposed_ms_per_step"] == pytest.approx(0.31)
+        assert len(head["roofline"]["per_rank_frac"]) == world
+
+
+def test_emit_prints_headline_last_and_writes_detail(tmp_path, capsys, monkeypatch):
+    """emit(): the full record goes to the detail file (every sub-record and kernel table), the compact line
+    is the LAST line of stdout and names the file."""
+    import json
+
+    import bench
+
+    out = _full_record(1)
+    detail = tmp_path / "d" / "bench_detail.json"
+    monkeypatch.setenv("LPGNN_BENCH_DETAIL", str(detail))
+    print("some earlier output")
+    bench.emit(out, None)
+    lines = capsys.readouterr().out.strip().splitlines()
+    head = json.loads(lines[-1])
+    assert head["detail"] == str(detail)
+    full = json.load(open(detail))
+    assert full["c5"]["kernels"] and full["skewed"]["kernels"]

@@ -197,6 +197,37 @@ def test_model_step_f16x2_close_to_x3():
         assert d <= 1e-4
 
 
+def test_forward_under_inference_mode_equals_no_grad():
+    """A GCN_FC forward under torch.inference_mode() with the f16x2 default: its tensors carry no autograd
+    version counter, so the scale cache computes their scales per use instead of keying on the version
+     -- the same logits, bit for bit, as under torch.no_grad(), in eval and in train mode
+    (dropout keyed the same way)."""
+    from lpgnn import GCN_FC, BipartiteBatch, BipartiteCSR, synth
+    from lpgnn.options import DEFAULT
+
+    g = synth.uniform_lp(3000, 6000, 60000, seed=4)
+    t = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    batch = BipartiteBatch(x_s=t(g.x_s), x_t=t(g.x_t), y_s=t(g.y_s), y_t=t(g.y_t),
+                           edge_index=BipartiteCSR.from_coo(g.row, g.col, g.val, g.m, g.n, device=DEV),
+                           s_bs=g.m, t_bs=g.n, bs=g.m + g.n)
+    torch.manual_seed(0)
+    model = GCN_FC(8, 8, hids=256, depth=3, options=DEFAULT.replace(arith="f16x2")).to(DEV)
+    for train in (False, True):
+        model.train(train)
+        with torch.no_grad():
+            torch.manual_seed(1)
+            ref = model(batch)
+        with torch.inference_mode():
+            torch.manual_seed(1)
+            got = model(batch)
+            assert got[0].is_inference()
+            got2 = model(batch) if not train else got  # twice: nothing stale was cached
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b)
+        for a, b in zip(ref, got2):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("R,N,K", [(100_000, 1024, 1024), (20_000, 256, 384), (1000, 64, 16 * 8)])
 def test_wgrad_f16x2_against_fp64(R, N, K):
     torch.manual_seed(R)
