@@ -290,22 +290,129 @@ __global__ __launch_bounds__(kBlock) void spmm_f32_rowslim(int64_t n_rows, const
   if (ok) *reinterpret_cast<V *>(Y + row * ldy + c0 + lane * CW) = acc;
 }
 
-// -------------------------------------------------------------- fp32 narrow
-// F <= FW <= 64: FW lanes per row, 256/FW rows per block (conv1, F = 8).
-template <int FW, int U>
-__global__ __launch_bounds__(kBlock) void spmm_f32_narrow(
+// ------------------------------------------------------------------- narrow
+// F <= FW <= 64 (conv1's input, F = 8): FW lanes per row, 256/FW rows per block, one output element
+// per lane, its sum over the row's edges in CSR order (acc = acc + v*x, product rounded first), one
+// rounding to the storage type at the end.  L: the storage -- NF32 (fp32) or N16<E> (bf16 / fp16).
+//
+// HEAVY: the launch's first hv.blocks blocks are heavy-row units, one block per row with more than
+// hv.thresh edges (a skewed LP's dense constraints, up to thousands of edges; longest first).  One FW-lane
+// group walking such a row is one long dependent chain of memory round trips (round 5: 1.05 ms for the
+// skewed conv1 launch against 0.03 ms on the uniform graph).  The unit splits the row into chunks of
+// CH = 192 * kNarrowPer / FW edges.  Waves 1-3 (192 loader lanes, kNarrowPer products each) gather a
+// chunk -- X[col, f] and the rounded product v*x, with the NEXT chunk's (col, val) already in flight --
+// into one of two LDS buffers, column-major (lane f's products contiguous, rows padded by 4 floats so the
+// 16-B reads of the FW summing lanes fall in distinct banks), while lane f < F of wave 0 adds the
+// previous chunk's products into its accumulator in CSR order (four per 16-B LDS read).  One barrier
+// per chunk.  The same products in the same order: the same bits as the FW-lane loop.
+constexpr int kNarrowPer = 16;      // products per loader lane per chunk
+constexpr int kNarrowLoaders = 192;  // waves 1..3
+
+struct NF32 {
+  typedef float T;
+  __device__ static __forceinline__ float get(float x) { return x; }
+  __device__ static __forceinline__ float put(float a) { return a; }
+};
+template <class E> struct N16 {
+  typedef uint16_t T;
+  __device__ static __forceinline__ float get(uint16_t h) { return E::lo(h); }
+  __device__ static __forceinline__ uint16_t put(float a) { return E::rne(a); }
+};
+
+template <class L, int FW>
+__device__ __forceinline__ void narrow_heavy_row(int64_t row, const int64_t *__restrict__ rowptr,
+                                                 const int32_t *__restrict__ col, const float *__restrict__ val,
+                                                 const typename L::T *__restrict__ X, int64_t ldx,
+                                                 typename L::T *__restrict__ Y, int64_t ldy, int64_t F) {
+  constexpr int EPI = kNarrowLoaders / FW;  // edges per loader step
+  constexpr int CH = EPI * kNarrowPer;       // edges per chunk
+  constexpr int LD = CH + 4;                 // a column's stride in the LDS image
+  __shared__ __attribute__((aligned(16))) float prod[2][FW * LD];
+  const int t = threadIdx.x;
+  const int64_t e0 = rowptr[row];
+  const int64_t end = rowptr[row + 1];
+  const int nch = (int)((end - e0 + CH - 1) / CH);
+  if (t >= 64) {  // loaders
+    const int l = t - 64;
+    const int f = l % FW;    // this lane's column (192 is a multiple of FW)
+    const int le0 = l / FW;  // this lane's first edge of a chunk; then every EPI-th
+    const bool act = f < F;
+    int c[kNarrowPer];
+    float v[kNarrowPer];
+    auto fetch = [&](int64_t cb) {  // chunk base cb: its (col, val)
+#pragma unroll
+      for (int i = 0; i < kNarrowPer; ++i) {
+        const int64_t e = cb + le0 + i * EPI;
+        c[i] = e < end ? col[e] : 0;
+        v[i] = e < end ? val[e] : 0.f;
+      }
+    };
+    fetch(e0);
+    for (int k = 0; k <= nch; ++k) {
+      if (k < nch) {
+        const int64_t cb = e0 + (int64_t)k * CH;
+        float x[kNarrowPer];
+#pragma unroll
+        for (int i = 0; i < kNarrowPer; ++i)
+          x[i] = (act && cb + le0 + i * EPI < end) ? L::get(X[(int64_t)c[i] * ldx + f]) : 0.f;
+        float p[kNarrowPer];
+#pragma unroll
+        for (int i = 0; i < kNarrowPer; ++i) p[i] = v[i] * x[i];
+        if (k + 1 < nch) fetch(cb + CH);  // the next chunk's indices in flight under this chunk's stores
+        float *buf = prod[k & 1] + f * LD;
+#pragma unroll
+        for (int i = 0; i < kNarrowPer; ++i)
+          if (act && cb + le0 + i * EPI < end) buf[le0 + i * EPI] = p[i];
+      }
+      __syncthreads();
+    }
+  } else {  // wave 0: lane t < F sums the previous chunk while the loaders fill the next
+    const bool act = t < FW && t < F;
+    float acc = 0.f;
+    for (int k = 0; k <= nch; ++k) {
+      if (k > 0 && act) {
+        const int n = (int)(end - (e0 + (int64_t)(k - 1) * CH) < CH ? end - (e0 + (int64_t)(k - 1) * CH) : CH);
+        const float *buf = prod[(k - 1) & 1] + t * LD;
+        int j = 0;
+#pragma unroll 4
+        for (; j + 4 <= n; j += 4) {
+          const float4 q = *reinterpret_cast<const float4 *>(buf + j);
+          acc = acc + q.x;
+          acc = acc + q.y;
+          acc = acc + q.z;
+          acc = acc + q.w;
+        }
+        for (; j < n; ++j) acc = acc + buf[j];
+      }
+      __syncthreads();
+    }
+    if (act) Y[row * ldy + t] = L::put(acc);
+  }
+}
+
+template <class L, int FW, int U, bool HEAVY>
+__global__ __launch_bounds__(kBlock) void spmm_narrow(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-    const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
-    float *__restrict__ Y, int64_t ldy, int64_t F) {
+    const float *__restrict__ val, const typename L::T *__restrict__ X, int64_t ldx,
+    typename L::T *__restrict__ Y, int64_t ldy, int64_t F, HeavyRows hv) {
   constexpr int RPB = kBlock / FW;
+  int64_t blk = blockIdx.x;
+  if constexpr (HEAVY) {
+    if (blk < hv.blocks) {
+      narrow_heavy_row<L, FW>(hv.rows[blk], rowptr, col, val, X, ldx, Y, ldy, F);
+      return;
+    }
+    blk -= hv.blocks;
+  }
   const int sub = threadIdx.x % FW;
-  const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / FW;
+  const int64_t row = blk * RPB + threadIdx.x / FW;
   if (row >= n_rows) return;
-  const bool active = sub < F;
-  const float *Xs = X + sub;
-  float acc = 0.f;
   int64_t e = rowptr[row];
   const int64_t end = rowptr[row + 1];
+  if (HEAVY && end - e > hv.thresh) return;  // a heavy row: done by its unit above
+  const bool active = sub < F;
+  const typename L::T *Xs = X + sub;
+  float acc = 0.f;
   for (; e + U <= end; e += U) {
     int c[U];
     float v[U], x[U];
@@ -315,15 +422,15 @@ __global__ __launch_bounds__(kBlock) void spmm_f32_narrow(
       v[k] = val[e + k];
     }
 #pragma unroll
-    for (int k = 0; k < U; ++k) x[k] = active ? Xs[(int64_t)c[k] * ldx] : 0.f;
+    for (int k = 0; k < U; ++k) x[k] = active ? L::get(Xs[(int64_t)c[k] * ldx]) : 0.f;
 #pragma unroll
     for (int k = 0; k < U; ++k) acc = acc + v[k] * x[k];
   }
   for (; e < end; ++e) {
-    const float x = active ? Xs[(int64_t)col[e] * ldx] : 0.f;
+    const float x = active ? L::get(Xs[(int64_t)col[e] * ldx]) : 0.f;
     acc = acc + val[e] * x;
   }
-  if (active) Y[row * ldy + sub] = acc;
+  if (active) Y[row * ldy + sub] = L::put(acc);
 }
 
 // ------------------------------------------------------------- fp32 generic
@@ -601,42 +708,6 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, cons
   }
 }
 
-// F <= FW <= 64, bf16: FW lanes per row, 256/FW rows per block (the c5 conv1 input, F = 8); the
-// same per-element sequence as spmm_bf16_generic (fp32 sum in edge order, one RNE at the end).
-template <class E, int FW, int U>
-__global__ __launch_bounds__(kBlock) void spmm_bf16_narrow(
-    int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-    const float *__restrict__ val, const uint16_t *__restrict__ X, int64_t ldx,
-    uint16_t *__restrict__ Y, int64_t ldy, int64_t F) {
-  constexpr int RPB = kBlock / FW;
-  const int sub = threadIdx.x % FW;
-  const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / FW;
-  if (row >= n_rows) return;
-  const bool active = sub < F;
-  const uint16_t *Xs = X + sub;
-  float acc = 0.f;
-  int64_t e = rowptr[row];
-  const int64_t end = rowptr[row + 1];
-  for (; e + U <= end; e += U) {
-    int c[U];
-    float v[U], x[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      c[k] = col[e + k];
-      v[k] = val[e + k];
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) x[k] = active ? E::lo(Xs[(int64_t)c[k] * ldx]) : 0.f;
-#pragma unroll
-    for (int k = 0; k < U; ++k) acc = acc + v[k] * x[k];
-  }
-  for (; e < end; ++e) {
-    const float x = active ? E::lo(Xs[(int64_t)col[e] * ldx]) : 0.f;
-    acc = acc + val[e] * x;
-  }
-  if (active) Y[row * ldy + sub] = E::rne(acc);
-}
-
 template <class E>
 __global__ __launch_bounds__(kBlock) void spmm_bf16_generic(
     int64_t n_rows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
@@ -698,12 +769,29 @@ lpg_status launch_wide_f32(const lpg_csr *A, const float *X, int64_t ldx, float 
                 ldy, F, hv);
 }
 
-template <int FW>
-lpg_status launch_narrow_f32(const lpg_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
-                             int64_t F, hipStream_t s) {
+template <class L, int FW>
+lpg_status launch_narrow_fw(const lpg_csr *A, const typename L::T *X, int64_t ldx, typename L::T *Y, int64_t ldy,
+                            int64_t F, HeavyRows hv, hipStream_t s) {
   constexpr int RPB = kBlock / FW;
-  dim3 grid((unsigned)((A->n_rows + RPB - 1) / RPB));
-  return launch(spmm_f32_narrow<FW, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
+  const int64_t nblk = (A->n_rows + RPB - 1) / RPB + hv.blocks;
+  LPG_REQUIRE(nblk < ((int64_t)1 << 31), "lpg_spmm: grid too large");
+  dim3 grid((unsigned)nblk);
+  if (hv.blocks > 0)
+    return launch(spmm_narrow<L, FW, 4, true>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
+  return launch(spmm_narrow<L, FW, 4, false>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F, hv);
+}
+
+// F <= 64: FW = the next power of 2 >= F lanes per row
+template <class L>
+lpg_status launch_narrow(const lpg_csr *A, const typename L::T *X, int64_t ldx, typename L::T *Y, int64_t ldy,
+                         int64_t F, HeavyRows hv, hipStream_t s) {
+  if (F <= 1) return launch_narrow_fw<L, 1>(A, X, ldx, Y, ldy, F, hv, s);
+  if (F <= 2) return launch_narrow_fw<L, 2>(A, X, ldx, Y, ldy, F, hv, s);
+  if (F <= 4) return launch_narrow_fw<L, 4>(A, X, ldx, Y, ldy, F, hv, s);
+  if (F <= 8) return launch_narrow_fw<L, 8>(A, X, ldx, Y, ldy, F, hv, s);
+  if (F <= 16) return launch_narrow_fw<L, 16>(A, X, ldx, Y, ldy, F, hv, s);
+  if (F <= 32) return launch_narrow_fw<L, 32>(A, X, ldx, Y, ldy, F, hv, s);
+  return launch_narrow_fw<L, 64>(A, X, ldx, Y, ldy, F, hv, s);
 }
 
 template <class E, int NV, int U>
@@ -753,15 +841,7 @@ static lpg_status spmm_f32_impl(const lpg_csr *A, const float *X, int64_t ldx, f
   LPG_REQUIRE(A->nnz == 0 || X != nullptr, "lpg_spmm_f32: X is NULL");
   hipStream_t s = as_stream(stream);
 
-  if (F <= 64) {
-    if (F <= 1) return launch_narrow_f32<1>(A, X, ldx, Y, ldy, F, s);
-    if (F <= 2) return launch_narrow_f32<2>(A, X, ldx, Y, ldy, F, s);
-    if (F <= 4) return launch_narrow_f32<4>(A, X, ldx, Y, ldy, F, s);
-    if (F <= 8) return launch_narrow_f32<8>(A, X, ldx, Y, ldy, F, s);
-    if (F <= 16) return launch_narrow_f32<16>(A, X, ldx, Y, ldy, F, s);
-    if (F <= 32) return launch_narrow_f32<32>(A, X, ldx, Y, ldy, F, s);
-    return launch_narrow_f32<64>(A, X, ldx, Y, ldy, F, s);
-  }
+  if (F <= 64) return launch_narrow<NF32>(A, X, ldx, Y, ldy, F, hv, s);
   const bool vec = (F % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && aligned16(X) && aligned16(Y);
   if (!vec) {
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
@@ -840,14 +920,7 @@ static lpg_status spmm_bf16_impl(const lpg_csr *A, const uint16_t *X, int64_t ld
   LPG_REQUIRE(A->nnz == 0 || X != nullptr, "lpg_spmm_bf16: X is NULL");
   hipStream_t s = as_stream(stream);
   const bool vec = (F % 8 == 0) && (ldx % 8 == 0) && (ldy % 8 == 0) && aligned16(X) && aligned16(Y);
-  if (F <= 64) {  // narrow: FW lanes per row (any alignment)
-    const int FW = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
-    dim3 grid((unsigned)((A->n_rows + kBlock / FW - 1) / (kBlock / FW)));
-    if (FW == 8) return launch(spmm_bf16_narrow<E, 8, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
-    if (FW == 16) return launch(spmm_bf16_narrow<E, 16, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
-    if (FW == 32) return launch(spmm_bf16_narrow<E, 32, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
-    return launch(spmm_bf16_narrow<E, 64, 4>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);
-  }
+  if (F <= 64) return launch_narrow<N16<E>>(A, X, ldx, Y, ldy, F, hv, s);  // any alignment
   if (!vec || F < 256) {
     dim3 grid((unsigned)((A->n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
     return launch(spmm_bf16_generic<E>, grid, s, A->n_rows, A->rowptr, A->col, A->val, X, ldx, Y, ldy, F);

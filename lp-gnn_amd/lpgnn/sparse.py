@@ -180,6 +180,10 @@ class BipartiteCSR:
 
 
 DEFAULT_HEAVY = 1024  # PathOptions.spmm_heavy's default (rows above it: heavy wave units)
+# F <= 64 (conv1's input): rows above this many edges (or above spmm_heavy, if lower) run as one
+# 256-lane LDS-staged block each instead of one FW-lane chain of dependent loads (spmm.hip
+# narrow_heavy_row): a 6 000-edge Zipf row took the whole 1 ms launch in the FW-lane form
+NARROW_HEAVY = 64
 
 
 def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0, heavy: int | None = None) -> torch.Tensor:
@@ -209,7 +213,9 @@ def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0,
     else:
         raise RuntimeError(f"lpgnn.spmm: unsupported dtype {x.dtype}")
     heavy = None
-    if Fd >= 256 and heavy_thresh > 0:  # degree-aware: rows above the threshold on narrow wave units
+    if Fd <= 64 and heavy_thresh > 0:  # narrow F: rows above NARROW_HEAVY on one block each (LDS-staged)
+        heavy_thresh = min(heavy_thresh, NARROW_HEAVY)
+    if (Fd >= 256 or Fd <= 64) and heavy_thresh > 0:  # degree-aware: rows above the threshold on their own units
         heavy = adj.heavy_rows(heavy_thresh)
         if heavy[1] == 0:
             heavy = None

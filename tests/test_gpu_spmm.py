@@ -334,3 +334,91 @@ def test_bf16_heavy_rows_bitwise(thresh, Fd, monkeypatch):
     Xbits = X.view(torch.int16).numpy().view(np.uint16)
     y = spmm_forward(adj.fwd, X.to(DEV), heavy=thresh).cpu().view(torch.int16).numpy().view(np.uint16)
     assert np.array_equal(y, O.spmm_bf16(*A, Xbits))
+
+
+def _long_row_graph(rng, m, n, long_deg):
+    """Rows of degree 0..70 (so the 64-edge narrow threshold falls inside the range) plus a row of
+    `long_deg` edges (crosses many LDS chunks) and one of exactly 64 and 65 edges."""
+    deg = rng.integers(0, 71, m)
+    deg[[1, 5, 9]] = [long_deg, 64, 65]
+    row = np.repeat(np.arange(m), deg)
+    col = np.concatenate([np.sort(rng.choice(n, d, replace=False)) for d in deg]).astype(np.int64)
+    val = rng.uniform(-1, 1, len(row)).astype(np.float32)
+    return row, col, val
+
+
+@pytest.mark.parametrize("thresh", [0, 3, 64, 1024])
+@pytest.mark.parametrize("Fd", [1, 3, 8, 16, 33, 64])
+def test_narrow_heavy_rows_bitwise(thresh, Fd):
+    """F <= 64 with the heavy-row unit (spmm.hip narrow_heavy_row: one 256-lane block per row above
+    min(thresh, NARROW_HEAVY) edges, products staged in LDS, each column's chain summed in CSR order):
+    bitwise the oracle's spmm_cpu loop, in fp32 and in bf16 / fp16 storage, on a graph with a
+    50 000-edge row (12+ LDS chunks at F = 8) and rows on both sides of the threshold."""
+    from lpgnn import sparse as S
+    from lpgnn.sparse import spmm_forward
+
+    rng = np.random.default_rng(Fd * 7 + thresh)
+    m, n = 400, 60000
+    row, col, val = _long_row_graph(rng, m, n, 50000)
+    adj = _adj(row, col, val, m, n)
+    A, _ = _oracle_pair(row, col, val, m, n)
+    eff = min(thresh, S.NARROW_HEAVY) if thresh > 0 else 0
+    if eff > 0:
+        assert adj.fwd.heavy_rows(eff)[1] > 0  # the heavy units really run
+    X = rng.standard_normal((n, Fd)).astype(np.float32)
+    got = spmm_forward(adj.fwd, torch.from_numpy(X).to(DEV), heavy=thresh).cpu().numpy()
+    assert np.array_equal(got, O.spmm_f32(*A, X))
+    Xb = torch.from_numpy(X).to(torch.bfloat16)
+    yb = spmm_forward(adj.fwd, Xb.to(DEV), heavy=thresh).cpu().view(torch.int16).numpy().view(np.uint16)
+    assert np.array_equal(yb, O.spmm_bf16(*A, Xb.view(torch.int16).numpy().view(np.uint16)))
+    Xh = torch.from_numpy(X).half()  # fp16 mode: the edge values rounded to fp16 too (batch_to(half=True))
+    yh = spmm_forward(adj.half().fwd, Xh.to(DEV), heavy=thresh).cpu()
+    assert torch.equal(yh.float(), O.spmm_f16(*A, Xh))
+
+
+def test_narrow_heavy_strided_output_and_empty():
+    """The heavy unit honours ldx / ldy (an F = 8 slice of wider buffers) and leaves other columns alone;
+    a graph whose only edges are in one heavy row, and a heavy list on a graph with no edges."""
+    from lpgnn.sparse import spmm_forward
+    from lpgnn import _lib
+    import ctypes
+
+    rng = np.random.default_rng(5)
+    m, n = 3, 5000
+    row = np.full(5000, 1, np.int64)
+    col = np.arange(5000, dtype=np.int64)
+    val = rng.uniform(-1, 1, 5000).astype(np.float32)
+    adj = _adj(row, col, val, m, n)
+    A, _ = _oracle_pair(row, col, val, m, n)
+    X = rng.standard_normal((n, 8)).astype(np.float32)
+    y = spmm_forward(adj.fwd, torch.from_numpy(X).to(DEV), heavy=64).cpu().numpy()
+    assert np.array_equal(y, O.spmm_f32(*A, X))
+    # strided: X is [n, 8] inside [n, 12], Y is [m, 8] inside [m, 20] (sentinel elsewhere)
+    Xbig = torch.zeros(n, 12, device=DEV)
+    Xbig[:, 2:10] = torch.from_numpy(X).to(DEV)
+    Ybig = torch.full((m, 20), 7.0, device=DEV)
+    idx, cnt = adj.fwd.heavy_rows(64)
+    L = _lib.lib()
+    with torch.cuda.device(DEV):
+        st = L.lpg_spmm_f32_heavy(ctypes.byref(adj.fwd.cstruct()), Xbig[:, 2:].data_ptr(), 12, Ybig[:, 4:].data_ptr(),
+                                  20, 8, idx.data_ptr(), cnt, 64, _lib.stream_of(Xbig))
+    _lib.check(st, "lpg_spmm_f32_heavy")
+    Yb = Ybig.cpu().numpy()
+    assert np.array_equal(Yb[:, 4:12], O.spmm_f32(*A, X))
+    assert (Yb[:, :4] == 7).all() and (Yb[:, 12:] == 7).all()
+
+
+def test_narrow_heavy_skewed_lp_full_size():
+    """The skewed sub-record's conv1 input SpMM (synth.skewed_lp at the c2 sizes, Zipf(1.5) rows up to
+    6 025 edges, F = 8) bitwise the oracle loop in both directions, with the default options."""
+    from lpgnn import synth
+    from lpgnn.sparse import spmm_forward
+
+    g = synth.skewed_lp(100_000, 200_000, 2_000_000, a=1.5, seed=0)
+    adj = _adj(g.row, g.col, g.val, g.m, g.n)
+    A, AT = _oracle_pair(g.row, g.col, g.val, g.m, g.n)
+    rng = np.random.default_rng(0)
+    Xv = rng.standard_normal((g.n, 8)).astype(np.float32)
+    Xc = rng.standard_normal((g.m, 8)).astype(np.float32)
+    assert np.array_equal(spmm_forward(adj.fwd, torch.from_numpy(Xv).to(DEV)).cpu().numpy(), O.spmm_f32(*A, Xv))
+    assert np.array_equal(spmm_forward(adj.bwd, torch.from_numpy(Xc).to(DEV)).cpu().numpy(), O.spmm_f32(*AT, Xc))
