@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
 // every number): the same maxima whatever the order, so deterministic
 __global__ __launch_bounds__(256) void colmax_f32(int64_t R, int64_t N, const float *__restrict__ G, int64_t ldg,
                                                   int64_t rc, unsigned *__restrict__ mbits) {
-  const int64_t c4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4, chunk = blockIdx.y;
+  const int64_t c4 = ((int64_t)blockIdx.y * 256 + threadIdx.x) * 4, chunk = blockIdx.x;  // x: row chunks (any R)
   if (c4 >= N) return;
   const int64_t r0 = chunk * rc, r1 = r0 + rc < R ? r0 + rc : R;
   f32x4 m = {0.f, 0.f, 0.f, 0.f};
@@ -1298,7 +1298,8 @@ __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const
                                                      unsigned *__restrict__ rbits, float *__restrict__ rscale) {
   __shared__ float red[4][256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t c4 = ((int64_t)blockIdx.x * 256 + tid) * 4, r0 = (int64_t)blockIdx.y * rc;
+  // blockIdx.x: the row chunk (the x dimension takes any R), blockIdx.y: the 1024-column block
+  const int64_t c4 = ((int64_t)blockIdx.y * 256 + tid) * 4, r0 = (int64_t)blockIdx.x * rc;
   const int64_t r1 = r0 + rc < R ? r0 + rc : R;
   const bool col_ok = c4 < N;
   const int slot = rowmax8_slot(lane);
@@ -1328,7 +1329,7 @@ __global__ __launch_bounds__(256) void rowcolmax_f32(int64_t R, int64_t N, const
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = nv[u];
   }
-  if (col_ok) *reinterpret_cast<f32x4 *>(cpart + (int64_t)blockIdx.y * N + c4) = m;
+  if (col_ok) *reinterpret_cast<f32x4 *>(cpart + (int64_t)blockIdx.x * N + c4) = m;
   __syncthreads();
   if (tid < r1 - r0) {
     const float mx = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
@@ -1660,9 +1661,9 @@ extern "C" lpg_status lpg_colscale_f32(int64_t R, int64_t N, const float *G, int
   unsigned *mbits = static_cast<unsigned *>(workspace);
   LPG_HIP(hipMemsetAsync(mbits, 0, N * sizeof(unsigned), st));
   const int64_t chunks = (R + kColChunk - 1) / kColChunk;
-  LPG_REQUIRE(chunks < 65536, "lpg_colscale_f32: too many rows");
+  LPG_REQUIRE(chunks < ((int64_t)1 << 31), "lpg_colscale_f32: too many rows");
   if (chunks > 0) {
-    hipLaunchKernelGGL(colmax_f32, dim3((unsigned)((N + 1023) / 1024), (unsigned)chunks), dim3(256), 0, st, R, N, G,
+    hipLaunchKernelGGL(colmax_f32, dim3((unsigned)chunks, (unsigned)((N + 1023) / 1024)), dim3(256), 0, st, R, N, G,
                        ldg, kColChunk, mbits);
     LPG_HIP(hipGetLastError());
   }
@@ -1700,11 +1701,11 @@ extern "C" lpg_status lpg_rowcolscale_f32(int64_t R, int64_t N, const float *G, 
               "lpg_rowcolscale_f32: N and ldg multiples of 4 floats, G and the workspace 16-byte aligned");
   hipStream_t st = as_stream(stream);
   const int64_t chunks = (R + kRowColChunk - 1) / kRowColChunk;
-  LPG_REQUIRE(chunks < 65536, "lpg_rowcolscale_f32: too many rows");
+  LPG_REQUIRE(chunks < ((int64_t)1 << 31), "lpg_rowcolscale_f32: too many rows");
   float *cpart = static_cast<float *>(workspace);
   unsigned *rbits = N > 1024 ? reinterpret_cast<unsigned *>(cpart + chunks * N) : nullptr;
   if (rbits) LPG_HIP(hipMemsetAsync(rbits, 0, R * sizeof(unsigned), st));
-  hipLaunchKernelGGL(rowcolmax_f32, dim3((unsigned)((N + 1023) / 1024), (unsigned)chunks), dim3(256), 0, st, R, N, G,
+  hipLaunchKernelGGL(rowcolmax_f32, dim3((unsigned)chunks, (unsigned)((N + 1023) / 1024)), dim3(256), 0, st, R, N, G,
                      ldg, kRowColChunk, cpart, rbits, rbits ? nullptr : rscale);
   LPG_HIP(hipGetLastError());
   hipLaunchKernelGGL(colfold_f32, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, chunks, N, cpart, cscale);

@@ -206,6 +206,9 @@ class GCN_FC(GCNBase):
         single = isinstance(edge_index, BipartiteCSR) and getattr(edge_index, "partitioned_conv", None) is None
         part_heads = getattr(edge_index, "two_direction_heads", None)  # row-partitioned multi-GPU adjacency
         fuse_heads = opts.fuse_heads and len(layers) > 0 and cd == torch.float32 and (single or part_heads is not None)
+        ex = getattr(edge_index, "ex", None)  # a partition's boundary exchange (lpgnn.partition.Exchange)
+        if ex is not None:  # no halo broadcast of an earlier (e.g. aborted) forward may still be in flight
+            ex.settle_all()
         # feeds_conv: the layer's outputs go to another GraphConvTwoDirection (not to the heads)
         left, right = self.conv1(x_left.to(cd), x_right.to(cd), edge_index, relu=True, opts=opts,
                                  feeds_conv=len(layers) > 0)
@@ -230,6 +233,8 @@ class GCN_FC(GCNBase):
                                  opts, fold_in=True)
                 if out is None:  # not applicable on this adjacency: the separate path
                     left, right = last(left, right, edge_index, relu=True, dropout=dp, opts=opts)
+        if ex is not None:  # every deferred broadcast was settled by its consumer; make sure of it
+            ex.settle_all()
         if out is not None:
             left, right = out
         else:

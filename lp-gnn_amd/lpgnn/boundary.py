@@ -135,6 +135,14 @@ def boundary_pack(y: torch.Tensor, bmap: torch.Tensor, buf: torch.Tensor | None 
     return buf
 
 
+def _forget_scales(y: torch.Tensor) -> None:
+    """y was rewritten through its pointer (a write autograd's version counter does not see): drop any f16x2
+    row / column scales cached on its storage (lpgnn.fc._ScaleCache), as the FC's ``out=`` paths do."""
+    from .fc import _SCALES
+
+    _SCALES.forget(y)
+
+
 def boundary_unpack_(y: torch.Tensor, bmap: torch.Tensor, buf: torch.Tensor) -> torch.Tensor:
     """y[bmap[b]] = buf[b] where bmap[b] >= 0, in place: lpg_boundary_unpack_f32."""
     nb, F = _check_rows(y, bmap, buf)
@@ -142,6 +150,7 @@ def boundary_unpack_(y: torch.Tensor, bmap: torch.Tensor, buf: torch.Tensor) -> 
         st = _lib.lib().lpg_boundary_unpack_f32(y.data_ptr(), y.stride(0), y.shape[0], F, nb, bmap.data_ptr(),
                                                 buf.data_ptr(), _lib.stream_of(y))
     _lib.check(st, "lpg_boundary_unpack_f32")
+    _forget_scales(y)
     return y
 
 
@@ -155,6 +164,7 @@ def boundary_allreduce_(y: torch.Tensor, bmap: torch.Tensor, comm: LibComm,
         st = _lib.lib().lpg_boundary_allreduce_f32(y.data_ptr(), y.stride(0), y.shape[0], F, nb, bmap.data_ptr(),
                                                    buf.data_ptr(), comm.handle, _lib.stream_of(y))
     _lib.check(st, "lpg_boundary_allreduce_f32")
+    _forget_scales(y)
     return y
 
 

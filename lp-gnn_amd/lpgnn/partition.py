@@ -614,6 +614,10 @@ def foldable_producer(left, right, opts):
     if not (opts.fold_conv1_wgrad and opts.arith in _fc_x3like() and g.opts.arith in _fc_x3like()) or \
             any(g.needs_input_grad[:2]):
         return None
+    # the fold hands conv1's outputs zero-stride gradients: not when something observes them (a hook or
+    # retain_grad on left / right) -- then the two-pass route, as conv.foldable_producer
+    if any(x.retains_grad or x._backward_hooks for x in (left, right)):
+        return None
     return g
 
 
