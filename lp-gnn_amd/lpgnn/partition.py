@@ -699,6 +699,55 @@ def _part_forward_core(ctx, left, right, padj, w_rel_l2r, b_l2r, w_root_l2r, w_r
                                  w_rel_r2l, w_root_r2l), logits
 
 
+def _part_forward_f16(left, right, padj, l2r, r2l, relu, opts, defer):
+    """One GraphConvTwoDirection layer of the reference's --fp16 evaluation (val.py:269 model.half(),
+    utils.py:909-915 batch_to(half=True)) on a row partition: fp16 storage, the one-GPU path's fp16
+    kernels and association rule (lpgnn.conv._forward_core), forward only (the reference trains in fp32).
+    The vars<-cons aggregate's partial sums are formed and reduced to the owners in fp32 and rounded to
+    fp16 once -- as the one-GPU fp16 SpMM sums a row in fp32 and rounds once -- so the partition changes
+    only the order of that fp32 sum.  The constraint side is local (bitwise the one-GPU rows).  Returns
+    (left_new, right_new) with right_new's halo rows broadcast (deferred with ``defer``, as the fp32 node)."""
+    import functools
+
+    from . import fc as _fc
+    from .conv import reassociate
+    from .sparse import spmm_forward as _spmm_forward
+
+    if torch.is_grad_enabled() and any(p.requires_grad for p in (left, right)):
+        raise RuntimeError("the fp16 row-partitioned path is the reference's inference mode: no gradients")
+    spmm = functools.partial(_spmm_forward, heavy=opts.spmm_heavy)
+    f16 = torch.float16
+    w16 = lambda t: t.detach().to(f16)  # noqa: E731 (model.half(): already fp16)
+    b32 = lambda t: None if t is None else t.detach()  # noqa: E731 (fc_forward_bf16 adds the bias in fp32)
+    w_rel_l2r, b_l2r, w_root_l2r = w16(l2r.lin_rel.weight), b32(l2r.lin_rel.bias), w16(l2r.lin_root.weight)
+    w_rel_r2l, b_r2l, w_root_r2l = w16(r2l.lin_rel.weight), b32(r2l.lin_rel.bias), w16(r2l.lin_root.weight)
+    fc16 = _fc.fc_forward_bf16  # dispatches the fp16 kernels on fp16 operands (lpg_fc_f16)
+    ex = padj.ex
+    A, AT = padj.local.fwd, padj.local.bwd
+    n_own = ex.n_own
+    f_out = w_rel_l2r.shape[0]
+    with torch.no_grad():
+        ra = reassociate(ex.m, ex.n, left.shape[1], f_out, opts.reassociate)
+        src = fc16(left, w_rel_l2r, None, None, None, False) if ra else left
+        red = ex.start_reduce(spmm(AT, src.float()), inplace=True)  # fp32 partials -> owners, in flight ...
+        ex.settle(right)
+        agg_l = spmm(A, right)  # ... under the purely local constraint side (fp16 storage)
+        left_new = fc16(agg_l, w_rel_r2l, left, w_root_r2l, b_r2l, relu)
+        agg_own = red.finish().to(f16)  # the owners' fp32 sums, rounded once
+        right_new = torch.empty((right.shape[0], f_out), dtype=f16, device=left.device)
+        if ra:  # lin_root + bias + ReLU accumulated onto the aggregated product
+            right_new[:n_own] = agg_own
+            fc16(right[:n_own], w_root_l2r, None, None, b_l2r, relu, out=right_new[:n_own], accumulate=True)
+        else:
+            fc16(agg_own, w_rel_l2r, right[:n_own], w_root_l2r, b_l2r, relu, out=right_new[:n_own])
+        bc = ex.start_broadcast_(right_new, quiet=defer)
+        if defer:
+            ex.defer(right_new, bc)
+        else:
+            bc.finish()
+    return left_new, right_new
+
+
 def _relu_bwd(ctx, g, y, want_db):
     """(dZ, bias gradient) of a layer output gradient through the layer's ReLU/dropout."""
     from . import fc as _fc
@@ -997,6 +1046,18 @@ class PartitionedCSR:
     def t(self) -> "PartitionedCSR":
         return PartitionedCSR(self.local.t(), self.ex, "vars" if self.orient == "cons" else "cons")
 
+    def to(self, device, non_blocking: bool = False) -> "PartitionedCSR":
+        """batch_to (utils.py:909-915): a partition lives on its rank's device already."""
+        if torch.device(device) != self.device and not (torch.device(device).index is None
+                                                         and torch.device(device).type == self.device.type):
+            raise RuntimeError(f"a row partition stays on its rank's device {self.device}, not {device}")
+        return self
+
+    def half(self) -> "PartitionedCSR":
+        """SparseTensor.half() (batch_to(half=True), the reference's --fp16 mode): the local edge values
+        rounded to fp16 (kept in fp32 storage), as BipartiteCSR.half()."""
+        return PartitionedCSR(self.local.half(), self.ex, self.orient)
+
     def sparse_sizes(self):
         return self.local.sparse_sizes()
 
@@ -1014,6 +1075,11 @@ class PartitionedCSR:
         gradients come out of this layer's input-gradient GEMMs.  ``feeds_conv``: the outputs go only
         to another partitioned layer (GCN_FC's chain), which settles the broadcast of their halo rows
         itself -- it stays in flight under that layer's first GEMM and SpMM (Exchange.defer)."""
+        if self.orient == "cons" and left.dtype == torch.float16 and _local_spmm is _product_spmm:
+            from .options import DEFAULT
+
+            return _part_forward_f16(left, right, self, left2right, right2left, bool(relu), opts or DEFAULT,
+                                     bool(feeds_conv))
         if self.orient != "cons" or left.dtype != torch.float32 or _local_spmm is not _product_spmm:
             return None  # generic per-direction path (oracle tests, bf16)
         from .options import DEFAULT

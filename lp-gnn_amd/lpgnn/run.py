@@ -426,10 +426,11 @@ def validation(model, ds, args):
         if _partitioned(args, ds, i):  # the whole graph, row-partitioned over the ranks (every rank: all rows)
             from .partition import gather_logits
 
-            if fp16:
-                raise NotImplementedError("--fp16 evaluation of a row-partitioned graph (the partitioned layers "
-                                          "run fp32 / bf16); evaluate it with --partition 0")
             batch = _partition_batch(args, ds, i)
+            if fp16:  # val.py:269 / utils.py:909-915: fp16 features and edge values, the fp16 partitioned layers
+                from .data import batch_to
+
+                batch = batch_to(batch, batch.x_s.device, half=True)
             yl = gather_logits(batch.y_s[:, None].float(), batch.y_t[:, None].float(), batch)
             y = torch.cat(yl)[:, 0].long().cpu()
             lc, lv = gather_logits(*model(batch), batch)

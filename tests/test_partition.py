@@ -373,3 +373,45 @@ def test_deferred_broadcast_settles_on_demand(tmp_path):
     mp.spawn(_defer_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     for r in range(2):
         assert (tmp_path / f"ok{r}").exists()
+
+
+def _gather16_worker(rank, world, port, out_dir):
+    """--fp16 evaluation of a row-partitioned graph (run.validation with --partition): batch_to(half=True)
+    on a partitioned batch (fp16 features, fp16-rounded local edge values, the same exchange), then the
+    ranks' fp16 logits gathered into global order by gather_logits."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import lpgnn.partition as part
+        from lpgnn.data import batch_to
+
+        g = _graph()
+        plan = part.plan_partition(g.row, g.col, g.val, g.m, g.n, world, rank)
+        batch = part.make_local_batch(plan, g.x_s, g.x_t, g.y_s, g.y_t, device="cpu")
+        ex0 = batch.edge_index.ex
+        val0 = batch.edge_index.local.fwd.val.clone()
+        b16 = batch_to(batch, "cpu", half=True)
+        assert b16.x_s.dtype == torch.float16 and b16.x_t.dtype == torch.float16 and b16.y_s.dtype == torch.int64
+        adj = b16.edge_index
+        assert isinstance(adj, part.PartitionedCSR) and adj.ex is ex0 and adj.orient == "cons"
+        assert torch.equal(adj.local.fwd.val, val0.half().float())
+        # logits = the global node id (exact in fp16 below 2048) in column 0, its negation in column 1
+        gid_c = torch.arange(plan.row_lo, plan.row_hi, dtype=torch.float32) % 2048
+        gid_v = torch.from_numpy(plan.local_vars).float() % 2048
+        lc = torch.stack((gid_c, -gid_c), 1).half()
+        lv = torch.stack((gid_v, -gid_v), 1).half()
+        cons, var = part.gather_logits(lc, lv, b16)
+        want_c = torch.arange(g.m, dtype=torch.float32) % 2048
+        want_v = torch.arange(g.n, dtype=torch.float32) % 2048
+        assert cons.dtype == torch.float32 and torch.equal(cons[:, 0], want_c) and torch.equal(cons[:, 1], -want_c)
+        assert torch.equal(var[:, 0], want_v) and torch.equal(var[:, 1], -want_v)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fp16_partitioned_batch_and_gather_order(tmp_path, world):
+    mp.spawn(_gather16_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").exists()
