@@ -74,6 +74,31 @@ class CSR:
             cache[thresh] = (idx, int(idx.numel()))
         return cache[thresh]
 
+    def hot_source_fraction(self, rows: int) -> float:
+        """The fraction of the edges whose source (column) is among the `rows` most-referenced sources --
+        how much of an SpMM's gather traffic a cache holding that many source rows serves.  Once per CSR
+        and row budget (one host sync at the graph's first SpMM)."""
+        cache = self.__dict__.setdefault("_hot", {})
+        if rows not in cache:
+            if self.nnz == 0 or rows <= 0:
+                cache[rows] = 0.0
+            else:
+                cnt = torch.bincount(self.col.long(), minlength=self.n_cols)
+                top = torch.topk(cnt, min(rows, self.n_cols)).values
+                cache[rows] = float(top.sum().item()) / self.nnz
+        return cache[rows]
+
+
+# Gather locality (SURVEY.md 8d, the skewed workload): when most of an F-wide SpMM's edge gathers hit a
+# small set of hot source rows (a skewed LP's dense constraints, gathered by every variable that touches
+# them), those rows stay in L2 / MALL whatever the slice width, and full-width rows (one wave per
+# (row, 1024 columns), the edge list read once instead of once per 128-column slice) win: the skewed
+# vars<-cons launch 0.95 -> 0.57 ms (profiles/r06_spmm_skewed_sweep.log).  On a graph without such a hot
+# set the 128-column slices keep the gathered table slice MALL-resident (uniform c2: 1.11 vs 1.15+ ms).
+HOT_CACHE_BYTES = 64 << 20   # the source rows a launch may count on finding in cache
+HOT_FRACTION = 0.6           # ... serving at least this fraction of its edges -> full-width rows
+WIDE_SLICE = 1024
+
 
 class BipartiteCSR:
     """Drop-in for the reference batch's ``edge_index`` SparseTensor(m x n).
@@ -219,6 +244,9 @@ def spmm_forward(adj: CSR, x: torch.Tensor, slice_cols: int = 0, depth: int = 0,
         heavy = adj.heavy_rows(heavy_thresh)
         if heavy[1] == 0:
             heavy = None
+    if (slice_cols == 0 and x.dtype == torch.float32 and Fd >= WIDE_SLICE and heavy_thresh > 0
+            and adj.hot_source_fraction(HOT_CACHE_BYTES // (Fd * 4)) >= HOT_FRACTION):
+        slice_cols = WIDE_SLICE  # a hot, cache-resident source set: full-width rows (degree-aware, as heavy rows)
     with torch.cuda.device(x.device):
         stream = _lib.stream_of(x)
         tok = TIMER.start(("spmm", adj.n_rows, adj.n_cols, Fd, str(x.dtype)))
