@@ -1,7 +1,6 @@
 // Internal helpers shared by the liblpgnn_hip translation units.
 #pragma once
 #include <hip/hip_runtime.h>
-#include <cstdlib>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -46,15 +45,6 @@ inline int device_cus() {
     cus[dev] = n;
   }
   return cus[dev];
-}
-
-// First-round stagger of the one-tile GEMM grids (fc_bf16_p, fc_x3_wide): *sleeps = the s_sleep(127)
-// count of the odd-XCD blocks of the first round, *blocks = that round's size (blocks_per_cu x CUs).
-// The environment variable (an A/B knob, read per call) overrides the default of 0 (off).
-inline void stagger_params(int32_t *sleeps, int32_t *blocks, const char *env, int blocks_per_cu) {
-  const char *v = getenv(env);
-  *sleeps = v ? atoi(v) : 0;
-  *blocks = blocks_per_cu * device_cus();
 }
 
 // Workgroups of `kernel` (block of `threads`) that stay resident on the whole device at once:

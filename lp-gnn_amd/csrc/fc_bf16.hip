@@ -70,10 +70,6 @@ struct FcB16Args {
   // the folded ReLU backward's bias column sums (lpg_fc_bf16_relu_bwd*_db; fc_bf16_p only): the stored
   // dZ's sums per 64-row chunk of the launch's rows into lpg_colsum_bf16's partial image [ceil(M / 64)][N]
   float *cs;
-  // fc_bf16_p: the first-round blocks (block id < stagger_blocks) of the odd XCDs sleep stagger x 127 x 64
-  // clocks before their first tile, so half the chip runs its epilogues (HBM-bound when every CU stores at
-  // once) while the other half is in its k loop (0: off)
-  int32_t stagger, stagger_blocks;
 };
 
 
@@ -768,9 +764,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void fc_bf16_p(FcB16Args a) {
   const int wm = wave / WN, wn = wave % WN;
   const int nk1 = (int)(a.K1 / BK);
   const int nk = nk1 + (int)(a.K2 / BK);
-  if (a.stagger > 0 && bid < a.stagger_blocks && (bid & 1)) {
-    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   LPG_PROBE(0);
 
   // descriptors from row m0 of A / row n0 of W; a range ends after the block's last row, so the
@@ -1560,7 +1553,6 @@ lpg_status launch_bf16_p(FcB16Args a, bool relu, hipStream_t s) {
   a.mt = (a.M + BM - 1) / BM;
   a.nt = (a.N + BN - 1) / BN;
   const int64_t nwg = a.mt * a.nt;
-  stagger_params(&a.stagger, &a.stagger_blocks, "LPGNN_FC16_STAGGER", 1);
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_bf16: grid too large");
   if (relu)
     hipLaunchKernelGGL((fc_bf16_p<E, WM, WN, FM, FN, true>), dim3((unsigned)nwg), dim3(64 * WM * WN), 0, s, a);

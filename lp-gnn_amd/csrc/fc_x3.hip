@@ -94,8 +94,6 @@ struct X3Args {
   // "f16x2" operands (fc_x3_wide<..., F16 = true>): sa[m] = the power-of-2 scale of A row m (over both
   // k phases), sw[n] = that of W row n (both phases; W then holds two fp16 planes h, l of W * sw)
   const float *sa, *sw;
-  // fc_x3_wide: first-round blocks of the odd XCDs sleep stagger x 127 x 64 clocks first (fc_bf16.hip)
-  int32_t stagger, stagger_blocks;
 };
 
 // dst plane p [rows, cols] (ldd) = term p of src (transposed: src is [cols, rows]).
@@ -528,9 +526,6 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nk1 = (int)(a.K1 / BK);
   const int nk = nk1 + (int)(a.K2 / BK);
-  if (a.stagger > 0 && bid < a.stagger_blocks && (bid & 1)) {
-    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
 
   // descriptors: A from row m0, W from column n0 (plane p at + p * ps); ranges cover exactly the
   // bytes the block reads, so a stray offset reads zeros instead of faulting (dma16)
@@ -1011,7 +1006,6 @@ lpg_status launch_x3_wide(X3Args a, bool relu, hipStream_t s) {
   const int64_t nwg = a.mt * a.nt;
   LPG_REQUIRE(nwg < (int64_t)1 << 31, "lpg_fc_x3_f32: grid too large");
   LPG_REQUIRE(!F16 || (a.sa && a.sw), "lpg_fc_f16x2: the row scales are missing");
-  stagger_params(&a.stagger, &a.stagger_blocks, "LPGNN_FCX3_STAGGER", MINW);
   if constexpr (WGK) {
     hipLaunchKernelGGL((fc_x3_wide<WM, TM, TN, MINW, false, false, true, F16>), dim3((unsigned)nwg), dim3(NT), 0, s,
                        a);
