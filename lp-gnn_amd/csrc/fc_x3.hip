@@ -596,6 +596,16 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
     }
   }
 
+  // the bias of this lane's output columns, loaded before the k loop (its latency hidden there instead of
+  // exposed at the start of the epilogue, where it cost 2.5 % of a 200K-row launch: profiles/r06_epi_cost.log)
+  float bpre[!WGK ? TN : 1];
+  if constexpr (!WGK) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = n0 + j * 16 + (lane & 15);
+      bpre[j] = a.bias ? a.bias[col < a.N ? col : a.N - 1] : 0.f;
+    }
+  }
   if (nk > 0) stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -870,7 +880,8 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int64_t col = nw + j * 16 + fr;
-        const float bb = BIAS ? a.bias[col] : 0.f;
+        float bb = 0.f;
+        if constexpr (BIAS) bb = !WGK ? bpre[j] : a.bias[col];
         const uint32_t ck = drop_col_key(col);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
