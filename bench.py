@@ -506,6 +506,12 @@ def report(ctx, dt, kern, per_launch, *, steps, hids, local_nnz, esz, traffic_ke
         if dir_traffic and name in dir_traffic:  # counter bytes (PMC) over the measured launch time
             d["traffic_bytes"] = dir_traffic[name]
             d["traffic_frac"] = dir_traffic[name] / (med / 1e3) / 1e9 / HBM_PEAK_GBS
+        # what bounds the direction, from the three models: HBM when the counter bytes run near the peak;
+        # the cache hierarchy when the edge gathers exceed what HBM could deliver (hot source rows re-read
+        # from L2 / MALL: the compulsory bytes are the HBM floor, the gathers the cache's work)
+        tf = d.get("traffic_frac")
+        d["bound"] = ("hbm" if (tf if tf is not None else d["roofline_frac"]) >= 0.75 else
+                      "cache (gathers of hot sources from L2/MALL)" if d["roofline_frac"] > 1.0 else "latency")
         dirs[name] = d
     out = {"value": value, "ms_per_step": dt_max / max(1, steps) * 1e3, "roofline": roof, "fc_roofline": fc}
     if any(r["ex_n"] for r in every):
