@@ -55,9 +55,10 @@ def _pad_k(t: Tensor, mult: int = 4) -> Tensor:
 # "x3" = fp32 on the bf16 matrix cores through the exact three-way bf16 split (lpg_fc_x3_f32, lpg_wgrad_x3_f32).
 # The default of calls that pass no ``arith``; a model passes its own (GCN_FC(options=...), lpgnn.options).
 ARITH = _DEFAULT_OPTIONS.arith
-# "f16x2" = the same kernels' fp16 form: two fp16 terms per operand after a power-of-2 row scale, three
-# products (lpg_fc_f16x2_*: half the matrix-core work, representation error a quarter of an fp32 SGEMM's);
-# where it does not apply (the weight gradient, operands the wide kernel does not take) the call runs x3
+# "f16x2" (the default) = the same kernels' fp16 form: two fp16 terms per operand after a power-of-2 row
+# (weight gradient: column) scale, three products (lpg_fc_f16x2_*, lpg_wgrad_f16x2_f32: half the
+# matrix-core work, representation error a quarter of an fp32 SGEMM's); where it does not apply (operands
+# the wide kernel does not take) the call runs x3
 X3LIKE = ("x3", "f16x2")
 
 _FC_BK = 32  # lpg_fc_f32's tiled k-tile: K1, K2 are zero-padded to it unless the narrow-input kernel applies
