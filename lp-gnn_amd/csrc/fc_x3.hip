@@ -1372,9 +1372,14 @@ __global__ __launch_bounds__(256) void wgrad_fold(int64_t N, int64_t K, int64_t 
 // The R split of the x3 weight gradient: a function of the shape only (no environment or global
 // state), so a given (R, N, K) always folds its partials in the same order -- the same dW bits.
 int64_t wgrad_splits(int64_t R, int64_t N, int64_t K) {
-  const int64_t tiles = ((N + WG_T - 1) / WG_T) * ((K + WG_T - 1) / WG_T);
+  // one block per CU, one round: the kernel's 256 x 128 tiles times S row ranges = the CU count.  Round 6
+  // (tools/experiments/wgrad_split_ab.py, profiles/r06_wgrad_split_ab.log): at N = K = 1024 S = 8 (256
+  // blocks) runs R = 100 K / 200 K in 0.69 / 1.25 ms against 0.74 / 1.30 for the former 1024 blocks (four
+  // rounds, 4x the partial tiles to fold) and 0.80 / 1.52 for a round and a half
+  const int64_t tiles = ((N + 255) / 256) * ((K + 127) / 128);
   const int64_t nchunks = (R + 31) / 32;
-  int64_t S = (2048 + tiles - 1) / tiles;  // aim at >= 2048 blocks (8 per CU)
+  const int64_t cus = device_cus();
+  int64_t S = (cus + tiles - 1) / tiles;
   const int64_t maxS = nchunks / 8 > 1 ? nchunks / 8 : 1;  // >= 8 chunks (256 rows) per split
   if (S > maxS) S = maxS;
   if (S > 64) S = 64;

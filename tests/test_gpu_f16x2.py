@@ -241,11 +241,14 @@ def test_wgrad_f16x2_against_fp64(R, N, K):
     den = G.double().abs().t() @ X.double().abs()
     e = float(((dW.double() - ref).abs() / (den + 1e-30)).max())
     e3 = float(((F.wgrad(G, X, arith="x3").double() - ref).abs() / (den + 1e-30)).max())
-    print(f"wgrad f16x2 {e:.2e}  x3 {e3:.2e}")
+    # every output row (a column of G) relative to itself, beside an fp32 GEMM's (hipBLASLt through torch.mm)
+    rowrel = lambda d: float(((d.double() - ref).norm(dim=1) / ref.norm(dim=1)).max())  # noqa: E731
+    rel, rel32 = rowrel(dW), rowrel(G.t() @ X)
+    print(f"wgrad f16x2 {e:.2e}  x3 {e3:.2e}; worst row relative: f16x2 {rel:.2e}  fp32 GEMM {rel32:.2e}")
     assert e <= BOUND
-    # every output row (a column of G) relative to itself
-    rel = ((dW.double() - ref).norm(dim=1) / ref.norm(dim=1)).max()
-    assert float(rel) <= 1e-6
+    # one R range per CU (wgrad_splits) makes each fp32 accumulation chain R / (S * 32) chunks long: measured
+    # 1.3e-6 at R = 100 K, a third of the fp32 GEMM's 4.1e-6 (profiles/r06_wgrad_split_ab.log)
+    assert rel <= 2e-6 and rel <= rel32
 
 
 @pytest.mark.parametrize("M,N,relu,bias", [(100_000, 1024, True, True), (777, 256, True, False), (5, 1000, False, True),

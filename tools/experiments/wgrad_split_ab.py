@@ -1,7 +1,7 @@
-"""The f16x2 / x3 weight gradient's R-split (wgrad_splits' block target, LPGNN_WGRAD_TARGET, read once per
-process) at the c2 shapes: run once per target value, e.g.
-
-  for t in 1024 2048 4096; do LPGNN_WGRAD_TARGET=$t python tools/experiments/wgrad_split_ab.py; done
+"""The f16x2 / x3 weight gradient's R-split at the c2 shapes (N = K = 1024, R = 100 K / 200 K).  The round-6
+A/B (profiles/r06_wgrad_split_ab.log) ran it once per block target with a temporary LPGNN_WGRAD_TARGET read in
+csrc/fc_x3.hip wgrad_splits; that hook is gone (the split is a function of the shape and the CU count only),
+so the script now times the shipped rule.
 """
 import os
 import sys
@@ -33,4 +33,4 @@ for R in (100_000, 200_000):
         ts.append(e0.elapsed_time(e1) / 4)
     t = float(np.median(ts))
     res.append(f"R={R}: {t:.4f} ms ({3 * 2 * R * 1024 * 1024 / t / 1e9 / 2500:.3f} of 2.5 PF)")
-print(f"target {os.environ.get('LPGNN_WGRAD_TARGET', '2048')}: " + "  ".join(res), flush=True)
+print("  ".join(res), flush=True)
