@@ -138,6 +138,11 @@ __device__ __forceinline__ float f16x2_scale(float mx) {
   return ldexpf(1.f, 15 - e);
 }
 
+// 1 / s for a scale of f16x2_scale (a power of two in [2^-105, 2^115], so 1 / s is a normal power of
+// two): the exponent reflected about 0 by one integer subtract -- the bits of the IEEE division, which
+// costs ~10 VALU (v_div_scale / v_rcp / v_div_fmas / v_div_fixup) per call
+__device__ __forceinline__ float inv_pow2(float s) { return __uint_as_float(0x7f000000u - __float_as_uint(s)); }
+
 // Eight rows' values x[0..7] (one per row, this lane's part) -> their maxima over the wave's 64 lanes in
 // a halving butterfly: each exchange halves what a lane carries (4 + 2 + 1 exchanges, then a 3-step
 // all-reduce inside eight lanes); lane l ends with row ((l >> 5) & 1) * 4 + ((l >> 4) & 1) * 2 +

@@ -588,11 +588,22 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   const int fr = lane & 15, fg = lane >> 4;
   const int rA0 = wave * TM * 16 + fr;
   float sA[F16 ? TM : 1];  // F16: the scales of the A rows this lane splits
+  // F16: the block's BM row scales and BN column scales in the last KiB of LDS (no tile, epilogue image or
+  // WGK image reaches it), written here and read by the epilogue -- their load latency hidden under the
+  // first tile's DMA instead of exposed after the last k-tile
+  constexpr int SC_OFF = SM_BYTES - (BM + BN) * 4;
+  static_assert(!F16 || (2 * TILE_BYTES <= SC_OFF && NW * TM * 16 * (BN + 4) * 4 + BM * 20 * 4 <= SC_OFF),
+                "the scale slots clear the tile buffers and the epilogue images");
+  float *const ssc = reinterpret_cast<float *>(smem + SC_OFF);  // [BM] row scales, then [BN] column scales
   if constexpr (F16) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int64_t row = m0 + rA0 + i * 16;
       sA[i] = a.sa[row < a.M ? row : a.M - 1];
+    }
+    for (int q = tid; q < BM + BN; q += NW * 64) {
+      const int64_t row = m0 + q, col = n0 + (q - BM);
+      ssc[q] = q < BM ? a.sa[row < a.M ? row : a.M - 1] : a.sw[col < a.N ? col : a.N - 1];
     }
   }
 
@@ -717,25 +728,21 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = accH[i][j] + accL[i][j];
   if constexpr (F16) {  // undo the scales: output (row, col) times 1 / sa[row] times 1 / sw[col] (exact)
-    float ia[TM][4], iw[TN];
+    // (as 4-vectors: packed multiplies, the same two roundings per element)
+    f32x4 ia[TM];
+    float iw[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      const f32x4 s4 = *reinterpret_cast<const f32x4 *>(ssc + wave * TM * 16 + i * 16 + 4 * fg);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = mw + i * 16 + 4 * fg + r;
-        ia[i][r] = 1.f / a.sa[row < a.M ? row : a.M - 1];
-      }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t col = nw + j * 16 + fr;
-      iw[j] = 1.f / a.sw[col < a.N ? col : a.N - 1];
+      for (int r = 0; r < 4; ++r) ia[i][r] = inv_pow2(s4[r]);
     }
 #pragma unroll
+    for (int j = 0; j < TN; ++j) iw[j] = inv_pow2(ssc[BM + j * 16 + fr]);
+#pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] * ia[i][r] * iw[j];
+      for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] * ia[i] * f32x4{iw[j], iw[j], iw[j], iw[j]};
   }
   // fused heads (hn <= 3 here; the host routes hn = 4 to fc_fwd_x3_16): the store loops also put
   // each output into a per-wave LDS image (the tile buffers are free: every wave passed the last
@@ -1245,7 +1252,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
   for (int j = 0; j < 4; ++j) {
     const int64_t col = k0 + wn * 64 + j * 16 + fr;
     if (col >= K) continue;
-    const float ix = F16 ? 1.f / sX[col] : 1.f;
+    const float ix = F16 ? inv_pow2(sX[col]) : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1253,7 +1260,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3w(int64_t R, int64_t N, int64_
         const int64_t row = n0 + wm * 64 + i * 16 + 4 * fg + r;
         if (row < N) {
           float v = accH[i][j][r] + accL[i][j][r];
-          if constexpr (F16) v = v * (1.f / sG[row]) * ix;
+          if constexpr (F16) v = v * inv_pow2(sG[row]) * ix;
           P[row * K + col] = v;
         }
       }
