@@ -543,7 +543,10 @@ BULKY = ("kernels", "cpu_spmm", "vendor_spmm", "exchange", "library") + SUB_NAME
 
 
 def _r(x, nd=4):
-    return None if x is None else float(f"{x:.{nd}g}")
+    """x to nd significant digits; anything that is not a real number (None, a label) as it is."""
+    if isinstance(x, bool) or not isinstance(x, (int, float)):
+        return x
+    return float(f"{x:.{nd}g}")
 
 
 def _compact_roof(roof):
@@ -621,7 +624,14 @@ def emit(out, args):
     except OSError as e:  # a read-only tree: the headline still prints
         print(f"bench: detail file {path} not written ({e})", file=sys.stderr)
         path = None
-    line = json.dumps(compact_headline(out, path))
+    try:
+        line = json.dumps(compact_headline(out, path))
+    except Exception as e:  # never lose the headline to a summary bug: the contract's keys, as measured
+        print(f"bench: compact headline failed ({type(e).__name__}: {e}); minimal line", file=sys.stderr)
+        line = json.dumps({k: out.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup",
+                                                   "ms_per_step", "higher_is_better", "scaling", "vs_baseline",
+                                                   "dtype", "arith", "data", "config", "roofline", "fc_roofline",
+                                                   "cpu_baseline")} | {"detail": path}, default=str)
     if len(line) > HEADLINE_MAX_BYTES:
         print(f"bench: headline {len(line)} bytes > {HEADLINE_MAX_BYTES}", file=sys.stderr)
     sys.stderr.flush()

@@ -75,16 +75,21 @@ if __name__ == "__main__":
 
 
 # ---------------------------------------------------------------- the driver-parsed headline line
-def _full_record(world=1):
-    """A full bench record as main() builds it: round 5's final default line (every sub-record with its
-    kernel table, 20.9 KB), widened to `world` ranks for the N > 1 shape."""
+def _full_record(world=1, src="r05"):
+    """A full bench record as main() builds it, widened to `world` ranks for the N > 1 shape: round 5's final
+    default line (every sub-record with its kernel table, 20.9 KB), or ("r06") the detail file of a round-6
+    default run (tests/data/bench_detail_r06.json: per-direction compulsory / counter-bytes fractions and
+    their `bound` labels, which the first round-6 summary choked on)."""
     import copy
     import json
 
-    path = os.path.join(ROOT, "profiles", "r05_bench_default_final.log")
-    line = [ln for ln in open(path).read().splitlines() if ln.startswith("{")][-1]
-    out = json.loads(line)
-    out["arith"] = "f16x2"
+    if src == "r06":
+        out = json.load(open(os.path.join(ROOT, "tests", "data", "bench_detail_r06.json")))
+    else:
+        path = os.path.join(ROOT, "profiles", "r05_bench_default_final.log")
+        line = [ln for ln in open(path).read().splitlines() if ln.startswith("{")][-1]
+        out = json.loads(line)
+        out["arith"] = "f16x2"
     if world > 1:
         out = copy.deepcopy(out)
         out["n_gpus"] = world
@@ -106,8 +111,8 @@ REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
             "vs_baseline", "dtype", "arith", "data", "config", "dist", "roofline", "fc_roofline")
 
 
-@pytest.mark.parametrize("world", [1, 8])
-def test_headline_is_compact_and_parses(world):
+@pytest.mark.parametrize("world,src", [(1, "r05"), (8, "r05"), (1, "r06"), (8, "r06")])
+def test_headline_is_compact_and_parses(world, src):
     """The line the driver parses: under 8 KB whole (the driver keeps the last ~8 KB of stdout+stderr and
     returned parsed:null for round 5's 20.9 KB line), valid JSON, the contract's keys, the roofline with
     its PMC traffic, the CPU baseline at N=1, one summary per sub-record, and no kernel tables."""
@@ -115,7 +120,7 @@ def test_headline_is_compact_and_parses(world):
 
     import bench
 
-    out = _full_record(world)
+    out = _full_record(world, src)
     assert len(json.dumps(out)) > 8192 or world > 1  # the full record alone would not fit
     line = json.dumps(bench.compact_headline(out, "gpurun_out/bench_detail.json"))
     assert len(line.encode()) < bench.HEADLINE_MAX_BYTES <= 8192, len(line)
@@ -136,6 +141,10 @@ def test_headline_is_compact_and_parses(world):
         assert set(head["subs"]) == {"c4", "inference", "inference_fp16", "c5", "skewed"}
         assert head["subs"]["c5"]["ms_per_step"] == pytest.approx(out["c5"]["ms_per_step"], rel=1e-4)
         assert "cpu_s" in head["subs"]["c5"]
+        if src == "r06":  # the skewed directions' three fractions and their bound labels
+            for dd in head["subs"]["skewed"]["dirs"].values():
+                assert {"roofline_frac", "compulsory_frac", "traffic_frac", "bound"} <= set(dd), dd
+                assert isinstance(dd["bound"], str)
     else:
         assert head["exchange_overlap"]["max_exposed_ms_per_step"] == pytest.approx(0.31)
         assert len(head["roofline"]["per_rank_frac"]) == world
@@ -148,7 +157,7 @@ def test_emit_prints_headline_last_and_writes_detail(tmp_path, capsys, monkeypat
 
     import bench
 
-    out = _full_record(1)
+    out = _full_record(1, "r06")
     detail = tmp_path / "d" / "bench_detail.json"
     monkeypatch.setenv("LPGNN_BENCH_DETAIL", str(detail))
     print("some earlier output")
@@ -158,3 +167,17 @@ def test_emit_prints_headline_last_and_writes_detail(tmp_path, capsys, monkeypat
     assert head["detail"] == str(detail)
     full = json.load(open(detail))
     assert full["c5"]["kernels"] and full["skewed"]["kernels"]
+
+
+def test_emit_survives_a_summary_failure(tmp_path, capsys, monkeypatch):
+    """A bug in the compact summary still leaves a parseable last line with the contract's keys."""
+    import json
+
+    import bench
+
+    out = _full_record(1, "r06")
+    monkeypatch.setenv("LPGNN_BENCH_DETAIL", str(tmp_path / "bench_detail.json"))
+    monkeypatch.setattr(bench, "compact_headline", lambda *a: 1 / 0)
+    bench.emit(out, None)
+    head = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert head["value"] == out["value"] and head["roofline"]["frac"] == out["roofline"]["frac"]

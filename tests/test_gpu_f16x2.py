@@ -186,7 +186,7 @@ def test_model_step_f16x2_close_to_x3():
         lc, lv = model(batch)
         loss = balanced(lc, lv, batch.y_s, batch.y_t)
         loss.backward()
-        out[arith] = (float(loss), [p.grad.clone() for p in model.parameters()], lc.detach(), lv.detach())
+        out[arith] = (float(loss.detach()), [p.grad.clone() for p in model.parameters()], lc.detach(), lv.detach())
     assert abs(out["x3"][0] - out["f16x2"][0]) <= 1e-5 * abs(out["x3"][0])
     for a, b in zip(out["x3"][1], out["f16x2"][1]):
         assert float((a - b).norm()) <= 1e-4 * float(b.norm()) + 1e-12
