@@ -4,6 +4,8 @@ pipelined form) and 9 (that form for the whole call).  Interleaved rounds, media
 fraction of 2.5 PF, and whether every choice wrote the same bits.
 
   python tools/experiments/bf16_tail_ab.py
+
+Choices 8 and 9 existed only in the A/B build (profiles/r06_bf16_tail_ab.log); the library rejects them now.
 """
 import os
 import sys

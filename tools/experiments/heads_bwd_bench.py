@@ -35,4 +35,19 @@ for M in (100_000, 200_000):
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) / 5)
         t = float(np.median(ts))
-        print(f"M={M} {'scales' if arith else 'plain '}: {t:.4f} ms  {2 * M * 1024 * 4 / t / 1e9:.0f} GB/s", flush=True)
+        print(f"M={M} {'scales' if arith else 'plain '}: {t:.4f} ms  {2 * M * 1024 * 4 / t / 1e9:.2f} TB/s", flush=True)
+    # the same bytes through torch's elementwise kernel (read Y, write Z): what a plain stream reaches here
+    Z = torch.empty_like(Y)
+    torch.mul(Y, 1.1, out=Z)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(7):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            torch.mul(Y, 1.1, out=Z)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / 5)
+    t = float(np.median(ts))
+    print(f"M={M} torch mul (read + write): {t:.4f} ms  {2 * M * 1024 * 4 / t / 1e9:.2f} TB/s", flush=True)
