@@ -21,6 +21,6 @@ void clear_error() { g_err[0] = '\0'; }
 extern "C" const char *lpg_last_error(void) { return lpg::g_err; }
 
 extern "C" const char *lpg_build_info(void) {
-  return "liblpgnn_hip: gfx950 (CDNA4), wave64, fp32/bf16/fp16 CSR SpMM + MFMA FC (x3 fp32, bf16, fp16), "
-         "no-atomic deterministic, -ffp-contract=off";
+  return "liblpgnn_hip: gfx950 (CDNA4), wave64, fp32/bf16/fp16 CSR SpMM + MFMA FC (fp32 as f16x2 or x3 on the "
+         "16-bit matrix cores, exact fp32, bf16, fp16), deterministic (no float atomics), -ffp-contract=off";
 }
