@@ -1640,7 +1640,10 @@ constexpr int kKernels = 7;
 
 int64_t wgrad_bf16_rows(int64_t R, int64_t N, int64_t K, int64_t *S_out) {
   const int64_t tiles = ((N + 255) / 256) * ((K + 255) / 256);
-  int64_t S = (512 + tiles / 2) / tiles;
+  // one block per CU, one round (round 6: the c5 step 64.3-65.0 -> 63.9-64.1 ms against two rounds,
+  // profiles/r06_wgrad_bf16_split_ab.log -- half the partial tiles to fold, no second-round ramp)
+  const int64_t cus = device_cus();
+  int64_t S = (cus + tiles / 2) / tiles;
   const int64_t smax = (R + 511) / 512;
   S = S < smax ? S : smax;
   S = S < 1 ? 1 : S;
