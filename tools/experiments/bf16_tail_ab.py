@@ -5,6 +5,8 @@ and the folded ReLU backward (mask bits in, bias column sums out).  Interleaved 
 the fraction of 2.5 PF, and whether both wrote the same bits.
 
   python tools/experiments/bf16_tail_ab.py
+
+Choice 8 existed only in the A/B builds (profiles/r06_bf16_tail_ab.log); the shipped library rejects it.
 """
 import os
 import sys
