@@ -30,6 +30,9 @@ constexpr int kRowsColsum = 64;
 #ifndef LPG_HEADS_U_BF16
 #define LPG_HEADS_U_BF16 8
 #endif
+#ifndef LPG_HEADS_U_SC
+#define LPG_HEADS_U_SC 4
+#endif
 #ifndef LPG_HEADS_RB
 #define LPG_HEADS_RB 128
 #endif
@@ -411,13 +414,15 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
   using E = typename std::conditional<BF, uint16_t, float>::type;
   constexpr int EPT = BF ? 8 : 4;  // columns per thread
   constexpr int P = EPT / 2;       // column pairs
-  constexpr int U = BF ? LPG_HEADS_U_BF16 : LPG_HEADS_U_F32;  // rows per group (8: 128 B per lane in flight)
+  // rows per group (8: 128 B per lane in flight); the f16x2-scales form LPG_HEADS_U_SC (4: two groups per
+  // eight-row maximum)
+  constexpr int U = SC ? LPG_HEADS_U_SC : BF ? LPG_HEADS_U_BF16 : LPG_HEADS_U_F32;
   constexpr int RB = kRowsLinear;  // rows per block
   constexpr int CH = kRowsColsum;  // column-sum chunk
   static_assert(RB % CH == 0 && CH % (2 * U) == 0, "block shape");
   __shared__ float4 sg4[RB];
   __shared__ float rmx[SC ? kT / 64 : 1][SC ? RB : 1];  // SC: per wave, the rows' maxima of |dH|
-  static_assert(!SC || (!BF && U == 8), "the f16x2 scales: fp32, groups of eight rows");
+  static_assert(!SC || (!BF && (U == 8 || U == 4)), "the f16x2 scales: fp32, groups of eight or four rows");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if constexpr (SC) {
     for (int i = threadIdx.x; i < (kT / 64) * RB; i += kT) rmx[i / RB][i % RB] = 0.f;
@@ -542,11 +547,11 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
       for (int j = 0; j < CH / (2 * U); ++j) {
         issue(hB, cb + (2 * j + 1) * U);
         __builtin_amdgcn_sched_barrier(0);
+        float xm[8];  // (SC) the eight rows' lane maxima: one group of eight, or the two groups of four
         if constexpr (SC) {
-          float xm[8];
 #pragma unroll
-          for (int u = 0; u < U; ++u) xm[u % 8] = row(hA[u], cb + 2 * j * U + u);
-          rows8(xm, cb + 2 * j * U);
+          for (int u = 0; u < U; ++u) xm[u] = row(hA[u], cb + 2 * j * U + u);
+          if constexpr (U == 8) rows8(xm, cb + 2 * j * U);
         } else {
 #pragma unroll
           for (int u = 0; u < U; ++u) row(hA[u], cb + 2 * j * U + u);
@@ -554,10 +559,9 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
         issue(hA, cb + (2 * j + 2) * U);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (SC) {
-          float xm[8];
 #pragma unroll
-          for (int u = 0; u < U; ++u) xm[u % 8] = row(hB[u], cb + (2 * j + 1) * U + u);
-          rows8(xm, cb + (2 * j + 1) * U);
+          for (int u = 0; u < U; ++u) xm[(U == 4 ? 4 : 0) + u] = row(hB[u], cb + (2 * j + 1) * U + u);
+          rows8(xm, cb + (U == 4 ? 2 * j : 2 * j + 1) * U);
         } else {
 #pragma unroll
           for (int u = 0; u < U; ++u) row(hB[u], cb + (2 * j + 1) * U + u);
@@ -567,12 +571,17 @@ __global__ __launch_bounds__(kT) void heads_bwd_p1(int64_t M, int64_t K, const f
     }
     if (nfull < nch) {  // the partial last chunk, row by row (hA holds its first group)
       const int64_t cb = r0 + (int64_t)nfull * CH;
-      for (int64_t m0 = cb; m0 < r1; m0 += U) {
+      for (int64_t m0 = cb; m0 < r1; m0 += (SC ? 8 : U)) {
         if (m0 != cb) issue(hA, m0);
         if constexpr (SC) {
           float xm[8];
 #pragma unroll
-          for (int u = 0; u < U; ++u) xm[u % 8] = m0 + u < r1 ? row(hA[u], m0 + u) : 0.f;
+          for (int u = 0; u < U; ++u) xm[u] = m0 + u < r1 ? row(hA[u], m0 + u) : 0.f;
+          if constexpr (U == 4) {  // the second group of four
+            issue(hB, m0 + 4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) xm[4 + u] = m0 + 4 + u < r1 ? row(hB[u], m0 + 4 + u) : 0.f;
+          }
           rows8(xm, m0);
         } else {
 #pragma unroll
