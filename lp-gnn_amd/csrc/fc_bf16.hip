@@ -82,6 +82,25 @@ __device__ __forceinline__ uint16_t to_bf16_rne(float f) {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+#ifndef LPG_EPI_NT
+#define LPG_EPI_NT 1
+#endif
+// The epilogue's streamed tiles -- the addend in, the output out -- as non-temporal accesses (round 6): they
+// are touched once, and as ordinary accesses they displaced the A / W panels the concurrent blocks share
+// in L2.  c5 step 64.2 -> 63.2 ms, fc_roofline 0.470 -> 0.482 (profiles/r06_epi_nt_ab.log); the same bits.
+typedef unsigned int epi_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 epi_ld(const uint16_t *p) {
+  if constexpr (LPG_EPI_NT) {
+    const epi_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const epi_u32x4 *>(p));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  return *reinterpret_cast<const uint4 *>(p);
+}
+__device__ __forceinline__ void epi_st(uint16_t *p, uint4 v) {
+  if constexpr (LPG_EPI_NT) __builtin_nontemporal_store(epi_u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<epi_u32x4 *>(p));
+  else *reinterpret_cast<uint4 *>(p) = v;
+}
+
 // The 16-bit storage type of a kernel instance: bf16 (the c5 path) or fp16 (the reference's --fp16
 // inference mode, val.py:269: model.half()).  Same layouts, tiles and epilogues; only the MFMA
 // (v_mfma_f32_16x16x32_bf16 / _f16, the same operand layout and rate on gfx950) and the conversions
@@ -464,8 +483,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
       const int lr = q / CPR, ch = q % CPR;
       const int64_t row = wrow0 + lr < a.M ? wrow0 + lr : a.M - 1, col = wcol0 + ch * 8;
       if (col < a.N)
-        *reinterpret_cast<uint4 *>(img + lr * EP_PITCH + ch * 16) =
-            *reinterpret_cast<const uint4 *>(a.C + row * a.ldc + col);
+        *reinterpret_cast<uint4 *>(img + lr * EP_PITCH + ch * 16) = epi_ld(a.C + row * a.ldc + col);
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -556,7 +574,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
       const int q = it * 64 + lane;
       const int lr = q / CPR, ch = q % CPR;
       const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
-      if (row < a.M && col < a.N) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v[it];
+      if (row < a.M && col < a.N) epi_st(a.C + row * a.ldc + col, v[it]);
     }
     if (a.cs) {  // the bias column sums of the stored dZ: each lane's own image chunks overwritten by dZ, ...
 #pragma unroll
@@ -577,7 +595,7 @@ __device__ __forceinline__ void epilogue_bf16_ti(const FcB16Args &a, f32x4 (&acc
     const int64_t row = wrow0 + lr, col = wcol0 + ch * 8;
     const uint4 v = *reinterpret_cast<const uint4 *>(img + lr * EP_PITCH + ch * 16);
     const bool ok = row < a.M && col < a.N;
-    if (ok) *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+    if (ok) epi_st(a.C + row * a.ldc + col, v);
     if (E::kBf16 && a.mo) store_mask8(a, lane, pos_bits8(v), ok, row, col);  // the layer's ReLU mask
   }
 }

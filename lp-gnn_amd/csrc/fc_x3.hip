@@ -474,6 +474,23 @@ lpg_status launch_x3_16(X3Args a, bool relu, hipStream_t s) {
 // and lh into accL -- instead of six bf16 ones, and the sum rescaled by 1 / (sa sw) (powers of 2:
 // exact) before the epilogue.  Representation error <= ~3 * 2^-22 of sum |a b| (a quarter of an fp32
 // SGEMM's own; tools/experiments/split_error.py), half the matrix-core work.
+#ifndef LPG_X3_EPI_NT
+#define LPG_X3_EPI_NT 0
+#endif
+// the epilogue's streamed operands (the addend, the stored output, the conv1 fold's Y / C rows) as
+// non-temporal accesses when LPG_X3_EPI_NT, as the bf16 kernels' epi_ld / epi_st (fc_bf16.hip).  Off: unlike
+// there, the c2 step did not gain (fc_roofline 0.390 -> 0.385, profiles/r06_epi_nt_ab.log)
+template <class T>
+__device__ __forceinline__ T x3_ld(const T *p) {
+  if constexpr (LPG_X3_EPI_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <class T>
+__device__ __forceinline__ void x3_st(T *p, T v) {
+  if constexpr (LPG_X3_EPI_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 template <int WM, int TM, int TN, int MINW, bool RELU, bool HEADS, bool WGK = false, bool F16 = false>
 __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
   constexpr int NW = WM;
@@ -801,8 +818,8 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
         const int64_t row = m0 + r0 + u;
         const bool ok = cok0 && row < a.M;
         const int64_t rr = row < a.M ? row : a.M - 1;
-        const f32x2 y = *reinterpret_cast<const f32x2 *>(a.wy + rr * a.ldwy + cc);
-        const f32x2 cval = *reinterpret_cast<const f32x2 *>(a.C + rr * a.ldc + cc);
+        const f32x2 y = x3_ld(reinterpret_cast<const f32x2 *>(a.wy + rr * a.ldwy + cc));
+        const f32x2 cval = x3_ld(reinterpret_cast<const f32x2 *>(a.C + rr * a.ldc + cc));
         yv[u] = ok ? y : f32x2{0.f, 0.f};
         cv[u] = (ok && acc_c) ? cval : f32x2{0.f, 0.f};
       }
@@ -868,7 +885,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + rp(i, r)[j * 16];
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + x3_ld(rp(i, r) + j * 16);
     }
     auto body = [&](auto bias_c, auto drop_c) {
       constexpr bool BIAS = decltype(bias_c)::value, DROP = decltype(drop_c)::value;
@@ -908,7 +925,7 @@ __global__ __launch_bounds__(64 * WM, MINW) void fc_x3_wide(X3Args a) {
             if constexpr (BIAS) v = v + bb;
             if (RELU) v = (v < 0.f) ? 0.f : v;
             if constexpr (DROP) v = drop_half(hr[r], fr) >= a.drop_thresh ? v * a.drop_scale : 0.f;
-            if (!HEADS || a.store) rp(i, r)[j * 16] = v;
+            if (!HEADS || a.store) x3_st(rp(i, r) + j * 16, v);
             hput(i, r, j, v);
           }
         }

@@ -225,6 +225,26 @@ __global__ __launch_bounds__(kBlock) void spmm_f32_rowwave(
 // 256-column slice still 4 GB): one wave per (row, 64*CW-column slice), lane l holding columns
 // c0 + CW*l .. +CW-1 (CW = 2: 512 B per gather, CW = 1: 256 B), so a slice of the table is 2-4x
 // smaller than at 256 columns.  Same edge order, the chunk remainder gathered together: the same bits.
+#ifndef LPG_SPMM_NT
+#define LPG_SPMM_NT 1
+#endif
+// The wide kernels' output rows (written once) as non-temporal stores (round 6), so they do not displace
+// the gathered source slice the launch keeps in L2 / MALL: c2 step 15.67 -> 15.60 ms, c5 62.15 -> 61.96 on
+// one box (profiles/r06_epi_nt_ab.log); the same bits.
+typedef float spmm_f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int spmm_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_out(float *p, float v) {
+  if constexpr (LPG_SPMM_NT) __builtin_nontemporal_store(v, p); else *p = v;
+}
+__device__ __forceinline__ void st_out(float *p, float2 v) {
+  if constexpr (LPG_SPMM_NT) __builtin_nontemporal_store(spmm_f32x2{v.x, v.y}, reinterpret_cast<spmm_f32x2 *>(p));
+  else *reinterpret_cast<float2 *>(p) = v;
+}
+__device__ __forceinline__ void st_out(void *p, uint2 v) {
+  if constexpr (LPG_SPMM_NT) __builtin_nontemporal_store(spmm_u32x2{v.x, v.y}, reinterpret_cast<spmm_u32x2 *>(p));
+  else *reinterpret_cast<uint2 *>(p) = v;
+}
+
 template <int CW> struct VecF;
 template <> struct VecF<1> { typedef float T; };
 template <> struct VecF<2> { typedef float2 T; };
@@ -287,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void spmm_f32_rowslim(int64_t n_rows, const
     }
     e += n;
   }
-  if (ok) *reinterpret_cast<V *>(Y + row * ldy + c0 + lane * CW) = acc;
+  if (ok) st_out(Y + row * ldy + c0 + lane * CW, acc);
 }
 
 // ------------------------------------------------------------------- narrow
@@ -704,7 +724,7 @@ __global__ __launch_bounds__(kBlock) void spmm_bf16_rowslim(int64_t n_rows, cons
     uint2 o;
     o.x = E::pack(acc[0], acc[1]);
     o.y = E::pack(acc[2], acc[3]);
-    *reinterpret_cast<uint2 *>(Y + row * ldy + c0 + lane * 4) = o;
+    st_out(Y + row * ldy + c0 + lane * 4, o);
   }
 }
 
