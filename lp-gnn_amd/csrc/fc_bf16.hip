@@ -234,9 +234,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
         const int q = it * 64 + lane;
         const int lr = q / CPR, ch = q % CPR;
         const int64_t row = wrow0 + lr < a.M ? wrow0 + lr : a.M - 1, col = wcol0 + ch * 8;
-        if (col < a.N)
-          *reinterpret_cast<uint4 *>(img + lr * EP_PITCH + ch * 16) =
-              *reinterpret_cast<const uint4 *>(a.C + row * a.ldc + col);
+        if (col < a.N) *reinterpret_cast<uint4 *>(img + lr * EP_PITCH + ch * 16) = epi_ld(a.C + row * a.ldc + col);
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -307,7 +305,7 @@ __device__ __forceinline__ void epilogue_bf16(const FcB16Args &a, f32x4 (&acc)[F
           if (a.mi) v = relu_bwd8_bits(v, yv[it].x, a.mscale);
           else if (a.my) v = relu_bwd8(v, yv[it], a.mscale);
         }
-        *reinterpret_cast<uint4 *>(a.C + row * a.ldc + col) = v;
+        epi_st(a.C + row * a.ldc + col, v);
       }
       if (E::kBf16 && a.mo) store_mask8(a, lane, pos_bits8(v), ok, row, col);  // the layer's ReLU mask
     }
